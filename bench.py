@@ -1,0 +1,166 @@
+#!/usr/bin/env python3
+"""Headline benchmark: VGG-11 training throughput (images/sec, whole job) on N MI355X.
+
+    python bench.py --gpus 1 --steps 40 --warmup 10
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Config = BASELINE.json: VGG-11 (reference architecture, random init), synthetic CIFAR-10-shaped
+data (3x32x32, 10 classes, on-device crop/flip/normalise), bf16 compute with fp32 master
+weights/grads, SGD(0.1, 0.9, 1e-4), part-3 strategy (bucketed backward-overlapped DDP on RCCL).
+Default protocol is the reference's: GLOBAL batch 256 split int(256/N) per GPU (strong scaling);
+``--per-gpu-batch B`` switches to weak scaling. Every timed step is a full training step
+(augment + forward + backward + gradient all-reduce + optimizer), captured in one hipGraph.
+W untimed warm-up steps, then EXACTLY K timed steps bracketed by barrier + synchronize; the
+elapsed time is the MAX over ranks; rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+BASELINE_IMG_S = 385.5  # reference part 3 (DDP), 4 CPU nodes, Table 1
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=40)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--model", default="vgg11")
+    p.add_argument("--global-batch", type=int, default=256)
+    p.add_argument("--per-gpu-batch", type=int, default=None, help="weak scaling")
+    p.add_argument("--strategy", default="ddp", choices=["ddp", "allreduce", "gather_scatter"])
+    p.add_argument("--bucket-mb", type=float, default=25.0)
+    p.add_argument("--first-bucket-mb", type=float, default=1.0)
+    p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--train-size", type=int, default=None)
+    p.add_argument("--json-out", default=None)
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import ddp_amd
+    from ddp_amd.data import SyntheticCIFAR10, SyntheticImageNet, DeviceLoader
+    from ddp_amd.engine import TrainStep, CrossEntropyLoss
+    from ddp_amd.models import build
+    from ddp_amd.optim import FusedSGD
+    from ddp_amd.parallel import (DistributedDataParallel, RcclCommunicator, STRATEGIES,
+                                  check_replicas)
+    from ddp_amd.utils import seed_everything
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)  # control plane (TCPStore)
+    comm = RcclCommunicator(rank, world, local_rank)
+
+    seed_everything(ddp_amd.SEED)
+    if args.per_gpu_batch:
+        B, scaling = args.per_gpu_batch, "weak"
+    else:
+        B, scaling = int(args.global_batch / world), "strong"
+    global_batch = B * world
+    resnet = args.model.startswith("resnet")
+    ds = (SyntheticImageNet(True, n=args.train_size) if resnet
+          else SyntheticCIFAR10(True, n=args.train_size))
+    loader = DeviceLoader(ds, B, device, world, rank, train=True, cpad=8)
+    model = build(args.model).to(device)
+    criterion = CrossEntropyLoss()
+    sync = None
+    if args.strategy == "ddp":
+        model = DistributedDataParallel(model, comm, bucket_cap_mb=args.bucket_mb,
+                                        first_bucket_cap_mb=args.first_bucket_mb)
+    else:
+        fn = STRATEGIES[args.strategy]
+        sync = lambda m: fn(m, comm)  # noqa: E731
+    opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    step = TrainStep(model, opt, criterion, loader, sync=sync, use_graph=not args.no_graph)
+
+    graph_ok = False
+    nwarm = max(args.warmup, 2)
+    step.warmup(min(nwarm, 2))
+    if not args.no_graph:
+        try:
+            step.capture()
+            graph_ok = True
+        except Exception as e:  # fall back to eager steps, loudly
+            print(f"[bench] hipGraph capture failed ({e!r}); timing eager steps", file=sys.stderr)
+            step.graph = None
+    for _ in range(nwarm - 2):
+        step.step()
+    torch.cuda.synchronize()
+    warm_loss = step.pop_loss()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step.step()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss = step.pop_loss() / max(args.steps, 1)
+    consistent = True
+    if world > 1:
+        arena = model.arena if hasattr(model, "arena") else opt.arena
+        consistent = check_replicas(arena, world)
+    ms = elapsed / args.steps * 1000.0
+    value = global_batch * args.steps / elapsed
+    out = {
+        "metric": "images/sec (whole node) VGG-11 CIFAR-10" if not resnet
+        else "images/sec (whole node) ResNet-50 synthetic ImageNet",
+        "value": round(value, 2),
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 4),
+        "higher_is_better": True,
+        "scaling": scaling,
+        "vs_baseline": round(value / BASELINE_IMG_S, 2) if not resnet else None,
+        "dtype": "bf16",
+        "data": "synthetic (CIFAR-10-shaped 3x32x32, 10 classes, on-device crop/flip/normalise; random-init weights)"
+        if not resnet else "synthetic (ImageNet-shaped 3x224x224, 1000 classes)",
+        "config": {"model": args.model, "global_batch": global_batch, "per_gpu_batch": B,
+                   "seq_len": None, "parallelism": f"dp{world}",
+                   "strategy": {"ddp": "part3 bucketed DDP", "allreduce": "part2b all_reduce",
+                                "gather_scatter": "part2a gather/scatter"}[args.strategy],
+                   "hipgraph": graph_ok, "bucket_mb": args.bucket_mb,
+                   "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4) fused"},
+        "train_loss_mean": round(loss, 4),
+        "warmup_loss_sum": round(warm_loss, 4),
+        "replicas_consistent": consistent,
+    }
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,108 @@
+"""Build the in-tree native extension ``_native`` for gfx950 with hipcc (no JIT cache).
+
+    python -m ddp_amd._build            # or: python distributed-data-parallel-ml-training_amd/_build.py
+
+* every ``csrc/kernels/*.hip`` is compiled for ``--offload-arch=gfx950`` (device code),
+* ``csrc/runtime/*.cpp`` (RCCL communicator + bucketed reducer) and ``csrc/bind.cpp`` (pybind11)
+  are host C++ compiled by the same hipcc,
+* the result is linked against HIP and RCCL into ``_native<EXT_SUFFIX>`` next to this file so it
+  travels with the repository snapshot to the GPU box. At run time torch's bundled
+  ``libamdhip64.so.7`` / ``librccl.so.1`` satisfy the DT_NEEDED entries (torch is imported first),
+  so the process has exactly one HIP runtime.
+Objects are cached in ``build/native`` and rebuilt when a source or any header changes.
+"""
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(PKG_DIR, "csrc")
+BUILD = os.path.join(REPO, "build", "native")
+ARCH = os.environ.get("DDP_AMD_ARCH", "gfx950")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+
+
+def _hipcc():
+    for c in (os.path.join(ROCM, "bin", "hipcc"), shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build ddp_amd)")
+
+
+def _includes():
+    import pybind11
+    return ["-I" + CSRC, "-I" + os.path.join(CSRC, "kernels"), "-I" + pybind11.get_include(),
+            "-I" + sysconfig.get_paths()["include"], "-I" + os.path.join(ROCM, "include")]
+
+
+def ext_path():
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return os.path.join(PKG_DIR, "_native" + suffix)
+
+
+def _newest_header():
+    hs = glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)
+    return max((os.path.getmtime(h) for h in hs), default=0.0)
+
+
+def _compile(cmd, src, obj, hdr_time, verbose):
+    if os.path.exists(obj):
+        t = os.path.getmtime(obj)
+        if t >= os.path.getmtime(src) and t >= hdr_time:
+            return obj, False
+    if verbose:
+        print("[ddp_amd build]", os.path.relpath(src, PKG_DIR), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {src}\n{r.stdout}\n{r.stderr}")
+    return obj, True
+
+
+def build(verbose=True, jobs=None):
+    hipcc = _hipcc()
+    os.makedirs(BUILD, exist_ok=True)
+    inc = _includes()
+    common = ["-O3", "-std=c++17", "-fPIC", "-Wno-unused-result"]
+    hdr_time = _newest_header()
+    tasks = []
+    for src in sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))):
+        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-x", "hip", *common, *inc, "-c", src, "-o", obj]
+        tasks.append((cmd, src, obj))
+    host_srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))) + [os.path.join(CSRC, "bind.cpp")]
+    for src in host_srcs:
+        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        cmd = [hipcc, "-x", "c++", "-D__HIP_PLATFORM_AMD__", *common, "-fvisibility=hidden", *inc,
+               "-c", src, "-o", obj]
+        tasks.append((cmd, src, obj))
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    changed = False
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        futs = [ex.submit(_compile, c, s, o, hdr_time, verbose) for c, s, o in tasks]
+        objs = []
+        for f in futs:
+            o, ch = f.result()
+            objs.append(o)
+            changed |= ch
+    out = ext_path()
+    if changed or not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(o) for o in objs):
+        tmp = out + ".tmp"
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp,
+               "-L" + os.path.join(ROCM, "lib"), "-lrccl", "-lamdhip64"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, out)
+        if verbose:
+            print("[ddp_amd build] linked", os.path.relpath(out, REPO), flush=True)
+    return out
+
+
+if __name__ == "__main__":
+    build(verbose=True)
+    sys.exit(0)

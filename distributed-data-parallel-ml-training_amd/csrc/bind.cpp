@@ -1,0 +1,220 @@
+// pybind11 bindings for the ddp_amd native extension.
+// Tensors cross the boundary as raw device addresses (uintptr_t) plus explicit shapes; the
+// Python wrappers in ops/ validate dtype / shape / contiguity / device before calling. Every
+// launcher takes the HIP stream explicitly so the calls can be captured into a hipGraph.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <stdexcept>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "runtime/comm.h"
+
+namespace py = pybind11;
+using ddp_amd::BucketSpec;
+using ddp_amd::RcclComm;
+using ddp_amd::Reducer;
+
+#include "kernels/api.h"
+
+template <typename T>
+static T* P(uintptr_t v) { return reinterpret_cast<T*>(v); }
+static hipStream_t S(uintptr_t v) { return reinterpret_cast<hipStream_t>(v); }
+static void check(int rc, const char* what) {
+  if (rc != 0) {
+    std::string msg = std::string(what) + " failed: ";
+    msg += (rc > 0) ? hipGetErrorString((hipError_t)rc) : "invalid arguments";
+    throw std::runtime_error(msg);
+  }
+}
+
+static ddp_amd::ConvGeom geom(py::tuple g) {
+  if (g.size() != 12) throw std::runtime_error("conv geometry needs 12 ints");
+  ddp_amd::ConvGeom c;
+  int* f = &c.N;
+  for (int i = 0; i < 12; ++i) f[i] = g[i].cast<int>();
+  return c;
+}
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "ddp_amd native extension: gfx950 HIP kernels + RCCL runtime";
+
+  // geometry tuple: (N,H,W,C,K,R,S,stride,pad,P,Q,Creal)
+  m.def("conv_fwd", [](py::tuple g, uintptr_t x, uintptr_t wc, uintptr_t bias, uintptr_t y,
+                       uintptr_t stats, uintptr_t ws, int splits, uintptr_t st) {
+    auto c = geom(g);
+    check(ddp_conv_fwd(&c, P<void>(x), P<void>(wc), P<float>(bias), P<void>(y), P<float>(stats),
+                       P<float>(ws), splits, S(st)), "conv_fwd");
+  });
+  m.def("conv_dgrad", [](py::tuple g, uintptr_t dy, uintptr_t wt, uintptr_t dx, uintptr_t ws,
+                         int splits, uintptr_t st) {
+    auto c = geom(g);
+    check(ddp_conv_dgrad(&c, P<void>(dy), P<void>(wt), P<void>(dx), P<float>(ws), splits, S(st)),
+          "conv_dgrad");
+  });
+  m.def("conv_wgrad", [](py::tuple g, uintptr_t dy, uintptr_t x, uintptr_t dw, int splits,
+                         uintptr_t st) {
+    auto c = geom(g);
+    check(ddp_conv_wgrad(&c, P<void>(dy), P<void>(x), P<float>(dw), splits, S(st)), "conv_wgrad");
+  });
+
+  m.def("bn_act_fwd", [](int N, int H, int W, int C, int pool, int relu, float eps, uintptr_t z,
+                         uintptr_t res, uintptr_t stats, uintptr_t gamma, uintptr_t beta,
+                         uintptr_t out, uintptr_t st) {
+    ddp_amd::BnArgs a{};
+    a.N = N; a.H = H; a.W = W; a.C = C; a.pool = pool; a.relu = relu; a.eps = eps;
+    a.z = P<unsigned short>(z); a.res = P<unsigned short>(res); a.stats = P<float>(stats);
+    a.gamma = P<float>(gamma); a.beta = P<float>(beta); a.out = P<unsigned short>(out);
+    check(ddp_bn_act_fwd(&a, S(st)), "bn_act_fwd");
+  });
+  m.def("bn_act_bwd", [](int N, int H, int W, int C, int pool, int relu, float eps, uintptr_t z,
+                         uintptr_t res, uintptr_t stats, uintptr_t gamma, uintptr_t beta,
+                         uintptr_t dout, uintptr_t sums, uintptr_t dz, uintptr_t dres,
+                         uintptr_t dgamma, uintptr_t dbeta, uintptr_t dbias, uintptr_t st) {
+    ddp_amd::BnArgs a{};
+    a.N = N; a.H = H; a.W = W; a.C = C; a.pool = pool; a.relu = relu; a.eps = eps;
+    a.z = P<unsigned short>(z); a.res = P<unsigned short>(res); a.stats = P<float>(stats);
+    a.gamma = P<float>(gamma); a.beta = P<float>(beta); a.dout = P<unsigned short>(dout);
+    a.sums = P<float>(sums); a.dz = P<unsigned short>(dz); a.dres = P<unsigned short>(dres);
+    a.dgamma = P<float>(dgamma); a.dbeta = P<float>(dbeta); a.dbias = P<float>(dbias);
+    check(ddp_bn_act_bwd(&a, S(st)), "bn_act_bwd");
+  });
+
+  m.def("linear_ce_fwd", [](uintptr_t x, uintptr_t W, uintptr_t b, uintptr_t labels, int B, int F,
+                            int J, uintptr_t logits, uintptr_t dlogits, uintptr_t loss_sum,
+                            uintptr_t correct, uintptr_t st) {
+    check(ddp_linear_ce_fwd(P<void>(x), P<float>(W), P<float>(b), P<long long>(labels), B, F, J,
+                            P<float>(logits), P<float>(dlogits), P<float>(loss_sum),
+                            P<int>(correct), S(st)), "linear_ce_fwd");
+  });
+  m.def("linear_bwd", [](uintptr_t dlogits, uintptr_t x, uintptr_t W, int B, int F, int J,
+                         uintptr_t gscale, uintptr_t dx, uintptr_t dW, uintptr_t db,
+                         uintptr_t st) {
+    check(ddp_linear_bwd(P<float>(dlogits), P<void>(x), P<float>(W), B, F, J, P<float>(gscale),
+                         P<void>(dx), P<float>(dW), P<float>(db), S(st)), "linear_bwd");
+  });
+  m.def("softmax_ce", [](uintptr_t logits, int bf16, uintptr_t labels, int B, int J,
+                         uintptr_t loss_sum, uintptr_t correct, uintptr_t dlogits,
+                         int dlogits_bf16, uintptr_t st) {
+    check(ddp_softmax_ce(P<void>(logits), bf16, P<long long>(labels), B, J, P<float>(loss_sum),
+                         P<int>(correct), P<void>(dlogits), dlogits_bf16, S(st)), "softmax_ce");
+  });
+
+  m.def("sgd", [](uintptr_t p, uintptr_t g, uintptr_t buf, size_t n, float lr, float momentum,
+                  float wd, float grad_scale, int nesterov, uintptr_t st) {
+    check(ddp_sgd(P<float>(p), P<float>(g), P<float>(buf), n, lr, momentum, wd, grad_scale,
+                  nesterov, S(st)), "sgd");
+  });
+  // descs: list of (p, wc, wt, K, Cr, C, R, S)
+  m.def("pack_conv_weights", [](std::vector<std::tuple<uintptr_t, uintptr_t, uintptr_t, int, int,
+                                                       int, int, int>> descs, uintptr_t st) {
+    std::vector<ddp_amd::PackDesc> d;
+    for (auto& t : descs) {
+      ddp_amd::PackDesc x;
+      x.p = P<float>(std::get<0>(t));
+      x.wc = P<unsigned short>(std::get<1>(t));
+      x.wt = P<unsigned short>(std::get<2>(t));
+      x.K = std::get<3>(t); x.Cr = std::get<4>(t); x.C = std::get<5>(t);
+      x.R = std::get<6>(t); x.S = std::get<7>(t);
+      d.push_back(x);
+    }
+    check(ddp_pack_conv_weights(d.data(), (int)d.size(), S(st)), "pack_conv_weights");
+  });
+  m.def("counter_add", [](uintptr_t c, int delta, uintptr_t st) {
+    check(ddp_counter_add(P<int>(c), delta, S(st)), "counter_add");
+  });
+
+  m.def("synth_generate", [](uintptr_t images, uintptr_t labels, int n, int pix_per_img,
+                             unsigned int seed, int classes, uintptr_t st) {
+    check(ddp_synth_generate(P<unsigned char>(images), P<int>(labels), n, pix_per_img, seed,
+                             classes, S(st)), "synth_generate");
+  });
+  m.def("augment", [](uintptr_t images, uintptr_t labels, uintptr_t indices, uintptr_t cursor,
+                      int L, int B, int H, int W, int Cp, int pad, int flip, unsigned int seed,
+                      unsigned int epoch, std::vector<float> mean, std::vector<float> std_,
+                      uintptr_t x, uintptr_t y, uintptr_t st) {
+    ddp_amd::AugArgs a{};
+    a.images = P<unsigned char>(images); a.labels = P<int>(labels); a.indices = P<int>(indices);
+    a.cursor = P<int>(cursor); a.L = L; a.B = B; a.H = H; a.W = W; a.Cp = Cp; a.pad = pad;
+    a.flip = flip; a.seed = seed; a.epoch = epoch;
+    for (int c = 0; c < 3; ++c) { a.mean[c] = mean.at(c); a.inv_std[c] = 1.f / std_.at(c); }
+    a.x = P<unsigned short>(x); a.y = P<long long>(y);
+    check(ddp_augment(&a, S(st)), "augment");
+  });
+  m.def("nchw_to_nhwc", [](uintptr_t x, int N, int C, int H, int W, int Cp, uintptr_t out,
+                           uintptr_t st) {
+    check(ddp_nchw_to_nhwc(P<float>(x), N, C, H, W, Cp, P<void>(out), S(st)), "nchw_to_nhwc");
+  });
+  m.def("mean_ws", [](uintptr_t in, size_t n, int ws, uintptr_t out, uintptr_t st) {
+    check(ddp_mean_ws(P<float>(in), n, ws, P<float>(out), S(st)), "mean_ws");
+  });
+  m.def("scale", [](uintptr_t x, size_t n, float s, uintptr_t st) {
+    check(ddp_scale(P<float>(x), n, s, S(st)), "scale");
+  });
+
+  // ---------------- communication runtime ----------------
+  m.def("plan_buckets", [](std::vector<size_t> offsets, std::vector<size_t> numels,
+                           size_t elem_bytes, size_t cap, size_t cap_first) {
+    auto b = ddp_amd::plan_buckets(offsets, numels, elem_bytes, cap, cap_first);
+    std::vector<std::tuple<int, int, size_t, size_t>> out;
+    for (auto& x : b) out.emplace_back(x.first_param, x.last_param, x.offset, x.count);
+    return out;
+  });
+  m.def("make_unique_id", []() { return py::bytes(RcclComm::make_unique_id()); });
+
+  py::class_<RcclComm>(m, "RcclComm")
+      .def(py::init([](int rank, int world, std::string uid, int device) {
+             // ncclCommInitRank blocks until every rank joins: release the GIL meanwhile
+             py::gil_scoped_release nogil;
+             return new RcclComm(rank, world, uid, device);
+           }),
+           py::arg("rank"), py::arg("world"), py::arg("uid"), py::arg("device"))
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("world", &RcclComm::world)
+      .def("all_reduce", [](RcclComm& c, uintptr_t buf, size_t n, int dt, int op, uintptr_t st) {
+        c.all_reduce(P<void>(buf), n, dt, op, S(st));
+      })
+      .def("broadcast", [](RcclComm& c, uintptr_t buf, size_t n, int dt, int root, uintptr_t st) {
+        c.broadcast(P<void>(buf), n, dt, root, S(st));
+      })
+      .def("all_gather", [](RcclComm& c, uintptr_t s, uintptr_t r, size_t n, int dt, uintptr_t st) {
+        c.all_gather(P<void>(s), P<void>(r), n, dt, S(st));
+      })
+      .def("reduce_scatter", [](RcclComm& c, uintptr_t s, uintptr_t r, size_t n, int dt, int op,
+                                uintptr_t st) { c.reduce_scatter(P<void>(s), P<void>(r), n, dt, op, S(st)); })
+      .def("gather", [](RcclComm& c, uintptr_t s, uintptr_t r, size_t n, int dt, int root,
+                        uintptr_t st) { c.gather(P<void>(s), P<void>(r), n, dt, root, S(st)); })
+      .def("scatter", [](RcclComm& c, uintptr_t s, uintptr_t r, size_t n, int dt, int root,
+                         uintptr_t st) { c.scatter(P<void>(s), P<void>(r), n, dt, root, S(st)); })
+      .def("scatter_replicated", [](RcclComm& c, uintptr_t b, size_t n, int dt, int root,
+                                    uintptr_t st) { c.scatter_replicated(P<void>(b), n, dt, root, S(st)); })
+      .def("send", [](RcclComm& c, uintptr_t b, size_t n, int dt, int peer, uintptr_t st) {
+        c.send(P<void>(b), n, dt, peer, S(st));
+      })
+      .def("recv", [](RcclComm& c, uintptr_t b, size_t n, int dt, int peer, uintptr_t st) {
+        c.recv(P<void>(b), n, dt, peer, S(st));
+      })
+      .def("async_error", &RcclComm::async_error)
+      .def("abort", &RcclComm::abort);
+
+  py::class_<Reducer>(m, "Reducer")
+      .def(py::init([](RcclComm* comm, uintptr_t arena, std::vector<size_t> offsets,
+                       std::vector<size_t> numels, size_t cap, size_t cap_first, bool avg) {
+             return new Reducer(comm, P<float>(arena), offsets, numels, cap, cap_first, avg);
+           }),
+           py::keep_alive<1, 2>())
+      .def("buckets", [](Reducer& r) {
+        std::vector<std::tuple<int, int, size_t, size_t>> out;
+        for (auto& x : r.buckets()) out.emplace_back(x.first_param, x.last_param, x.offset, x.count);
+        return out;
+      })
+      .def("prepare", &Reducer::prepare)
+      .def("mark_ready", [](Reducer& r, int p, uintptr_t st) { r.mark_ready(p, S(st)); })
+      .def("finalize", [](Reducer& r, uintptr_t st) { r.finalize(S(st)); })
+      .def("set_debug_sync", &Reducer::set_debug_sync)
+      .def("launched", &Reducer::launched)
+      .def("comm_stream", [](Reducer& r) { return reinterpret_cast<uintptr_t>(r.comm_stream()); });
+}

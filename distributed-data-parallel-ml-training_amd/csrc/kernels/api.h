@@ -1,0 +1,87 @@
+// C ABI of the gfx950 kernel library: argument structs + launcher declarations.
+// Shared by the .hip kernel translation units and the pybind11 binding (bind.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace ddp_amd {
+
+struct ConvGeom {
+  int N, H, W, C;     // input (NHWC, C % 8 == 0)
+  int K;              // output channels
+  int R, S, stride, pad;
+  int P, Q;           // output spatial
+  int Creal;          // real (unpadded) input channels — weight-gradient layout
+};
+
+struct BnArgs {
+  int N, H, W, C;               // z / pre-pool shape
+  int pool;                     // 0: none, 1: 2x2 stride-2 max-pool
+  int relu;                     // apply ReLU
+  float eps;
+  const unsigned short* z;      // conv output (bf16)
+  const unsigned short* res;    // optional residual added before ReLU (bf16, same shape as z)
+  const float* stats;           // [2C] sum, sumsq over N*H*W
+  const float* gamma;           // [C]
+  const float* beta;            // [C]
+  unsigned short* out;          // forward output (bf16, pooled shape)
+  const unsigned short* dout;   // backward: grad wrt block output (pooled shape)
+  float* sums;                  // backward scratch [2C]: S1 = sum dy_bn, S2 = sum dy_bn*xhat
+  unsigned short* dz;           // backward: grad wrt conv output
+  unsigned short* dres;         // backward: grad wrt residual (optional)
+  float* dgamma;                // grad arena slices (accumulated)
+  float* dbeta;
+  float* dbias;                 // conv bias grad (optional)
+};
+
+struct PackDesc {
+  const float* p;          // fp32 master [K][Cr][R][S]
+  unsigned short* wc;      // bf16 [K][R][S][C]   (may be null)
+  unsigned short* wt;      // bf16 [C][R][S][K]   (may be null)
+  int K, Cr, C, R, S;
+};
+
+struct AugArgs {
+  const unsigned char* images;  // [Nd][H][W][3] uint8
+  const int* labels;            // [Nd]
+  const int* indices;           // [L] sample order for this rank/epoch
+  const int* cursor;            // device batch counter (may be null -> 0)
+  int L, B, H, W, Cp, pad, flip;
+  uint32_t seed, epoch;
+  float mean[3], inv_std[3];
+  unsigned short* x;            // [B][H][W][Cp] bf16
+  long long* y;                 // [B]
+};
+
+}  // namespace ddp_amd
+
+extern "C" {
+int ddp_conv_fwd(const ddp_amd::ConvGeom* g, const void* x, const void* wc, const float* bias,
+                 void* y, float* stats, float* ws, int splits, hipStream_t st);
+int ddp_conv_dgrad(const ddp_amd::ConvGeom* g, const void* dy, const void* wt, void* dx,
+                   float* ws, int splits, hipStream_t st);
+int ddp_conv_wgrad(const ddp_amd::ConvGeom* g, const void* dy, const void* x, float* dw,
+                   int splits, hipStream_t st);
+int ddp_bn_act_fwd(const ddp_amd::BnArgs* a, hipStream_t st);
+int ddp_bn_act_bwd(const ddp_amd::BnArgs* a, hipStream_t st);
+int ddp_linear_ce_fwd(const void* x, const float* W, const float* b, const long long* labels,
+                      int B, int F, int J, float* logits, float* dlogits, float* loss_sum,
+                      int* correct, hipStream_t st);
+int ddp_linear_bwd(const float* dlogits, const void* x, const float* W, int B, int F, int J,
+                   const float* gscale, void* dx, float* dW, float* db, hipStream_t st);
+int ddp_softmax_ce(const void* logits, int logits_bf16, const long long* labels, int B, int J,
+                   float* loss_sum, int* correct, void* dlogits, int dlogits_bf16,
+                   hipStream_t st);
+int ddp_sgd(float* p, const float* g, float* buf, size_t n, float lr, float momentum, float wd,
+            float grad_scale, int nesterov, hipStream_t st);
+int ddp_pack_conv_weights(const ddp_amd::PackDesc* descs, int n, hipStream_t st);
+int ddp_counter_add(int* c, int delta, hipStream_t st);
+int ddp_synth_generate(unsigned char* images, int* labels, int n, int pix_per_img,
+                       unsigned int seed, int classes, hipStream_t st);
+int ddp_augment(const ddp_amd::AugArgs* a, hipStream_t st);
+int ddp_nchw_to_nhwc(const float* x, int N, int C, int H, int W, int Cp, void* out,
+                     hipStream_t st);
+int ddp_mean_ws(const float* in, size_t n, int ws, float* out, hipStream_t st);
+int ddp_scale(float* x, size_t n, float s, hipStream_t st);
+}

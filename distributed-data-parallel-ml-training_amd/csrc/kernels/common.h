@@ -1,0 +1,67 @@
+// Shared device helpers for the gfx950 (CDNA4) kernel library.
+// Activations are NHWC bf16; master weights / gradients / optimizer state are fp32.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ddp_amd {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int kWave = 64;  // CDNA wavefront width (never 32)
+
+// bf16 <-> fp32 bit conversions. round-to-nearest-even; NaN kept NaN.
+__device__ __forceinline__ float bf2f(unsigned short h) {
+  return __uint_as_float(((unsigned int)h) << 16);
+}
+// A plain cast lowers to v_cvt_pk_bf16_f32 (RNE, NaN-preserving) on gfx950 -O3.
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(unsigned short, b);
+}
+__device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
+
+// 16-byte vector load/store of 8 bf16 values as raw u16 lanes.
+__device__ __forceinline__ u16x8 ld8(const unsigned short* p) {
+  return *reinterpret_cast<const u16x8*>(p);
+}
+__device__ __forceinline__ void st8(unsigned short* p, u16x8 v) {
+  *reinterpret_cast<u16x8*>(p) = v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
+// Bijective XCD-aware block remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
+// consecutive logical tiles land on the same XCD (shared L2) instead of round-robin.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int nx = 8;
+  if (nwg < nx) return orig;
+  const int q = nwg / nx, r = nwg % nx;
+  const int xcd = orig % nx, idx = orig / nx;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+// Counter-based RNG (splitmix-style 32-bit hash); identical formula in data/synthetic.py.
+__host__ __device__ __forceinline__ uint32_t hash_u32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du;
+  x ^= x >> 15; x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+__host__ __device__ __forceinline__ uint32_t hash3(uint32_t a, uint32_t b, uint32_t c) {
+  return hash_u32(a ^ hash_u32(b ^ hash_u32(c + 0x9e3779b9u)));
+}
+
+}  // namespace ddp_amd

@@ -1,0 +1,226 @@
+// Classifier head for gfx950: small-output Linear fused with softmax cross-entropy.
+//
+// Reference parity: fc1 = Linear(512, 10) (part1/model.py:40,45) + CrossEntropyLoss (mean)
+// (part1/main.py:75,119) and the eval metrics argmax/eq/sum (part1/main.py:105-106);
+// SURVEY.md §2.B N2d/N2f/N2i.
+//
+// fwd  : one wave per row; each lane owns F/64 features, 10 dot products reduced across the
+//        wave, softmax in registers, loss/accuracy accumulated with one atomic per row.
+//        dlogits = (softmax - onehot) / B is written for the backward (mean reduction).
+// bwd  : dx[b][:] = g * dlogits[b] @ W     (one wave per row, bf16 out)
+//        dW[j][f] += g * sum_b dlogits[b][j] x[b][f]; db[j] += g * sum_b dlogits[b][j]
+// The Linear weight is read straight from the fp32 master copy (20 KB).
+// A separate generic softmax-CE (any J, logits from the MFMA GEMM) serves ResNet-50's 1000-way head.
+#include "common.h"
+#include "api.h"
+
+namespace ddp_amd {
+
+constexpr int kMaxJ = 16;
+
+__global__ __launch_bounds__(256) void linear_ce_fwd_kernel(
+    const unsigned short* __restrict__ x, const float* __restrict__ W, const float* __restrict__ b,
+    const long long* __restrict__ labels, int B, int F, int J, float inv_b, float* logits_out,
+    float* dlogits, float* loss_sum, int* correct) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  float acc[kMaxJ];
+#pragma unroll
+  for (int j = 0; j < kMaxJ; ++j) acc[j] = 0.f;
+  for (int f0 = lane * 8; f0 < F; f0 += 64 * 8) {
+    const u16x8 xv = ld8(x + (size_t)row * F + f0);
+    float xf[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) xf[e] = bf2f(xv[e]);
+#pragma unroll
+    for (int j = 0; j < kMaxJ; ++j) {
+      if (j < J) {
+        const float4 w0 = *reinterpret_cast<const float4*>(W + (size_t)j * F + f0);
+        const float4 w1 = *reinterpret_cast<const float4*>(W + (size_t)j * F + f0 + 4);
+        acc[j] += xf[0] * w0.x + xf[1] * w0.y + xf[2] * w0.z + xf[3] * w0.w + xf[4] * w1.x +
+                  xf[5] * w1.y + xf[6] * w1.z + xf[7] * w1.w;
+      }
+    }
+  }
+  float mx = -INFINITY;
+  int arg = 0;
+#pragma unroll
+  for (int j = 0; j < kMaxJ; ++j) {
+    if (j < J) {
+      acc[j] = wave_sum(acc[j]) + (b ? b[j] : 0.f);
+      if (acc[j] > mx) { mx = acc[j]; arg = j; }
+    }
+  }
+  float se = 0.f;
+#pragma unroll
+  for (int j = 0; j < kMaxJ; ++j)
+    if (j < J) se += __expf(acc[j] - mx);
+  const float lse = mx + __logf(se);
+  const int y = labels ? (int)labels[row] : -1;
+  if (lane < J) {
+    float lj = 0.f;
+#pragma unroll
+    for (int j = 0; j < kMaxJ; ++j)
+      if (j == lane) lj = acc[j];
+    if (logits_out) logits_out[(size_t)row * J + lane] = lj;
+    if (dlogits && labels) {
+      const float p = __expf(lj - lse);
+      dlogits[(size_t)row * J + lane] = (p - (lane == y ? 1.f : 0.f)) * inv_b;
+    }
+  }
+  if (lane == 0 && labels) {
+    float ly = 0.f;
+#pragma unroll
+    for (int j = 0; j < kMaxJ; ++j)
+      if (j == y) ly = acc[j];
+    if (loss_sum) atomicAdd(loss_sum, (lse - ly) * inv_b);
+    if (correct && arg == y) atomicAdd(correct, 1);
+  }
+}
+
+// dx: one wave per row.
+__global__ __launch_bounds__(256) void linear_dx_kernel(const float* __restrict__ dlogits,
+                                                        const float* __restrict__ W, int B, int F,
+                                                        int J, const float* gscale,
+                                                        unsigned short* dx) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const float g = gscale ? *gscale : 1.f;
+  float dl[kMaxJ];
+#pragma unroll
+  for (int j = 0; j < kMaxJ; ++j) dl[j] = (j < J) ? dlogits[(size_t)row * J + j] * g : 0.f;
+  for (int f0 = lane * 8; f0 < F; f0 += 64 * 8) {
+    float o[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < kMaxJ; ++j) {
+      if (j < J) {
+        const float4 w0 = *reinterpret_cast<const float4*>(W + (size_t)j * F + f0);
+        const float4 w1 = *reinterpret_cast<const float4*>(W + (size_t)j * F + f0 + 4);
+        o[0] += dl[j] * w0.x; o[1] += dl[j] * w0.y; o[2] += dl[j] * w0.z; o[3] += dl[j] * w0.w;
+        o[4] += dl[j] * w1.x; o[5] += dl[j] * w1.y; o[6] += dl[j] * w1.z; o[7] += dl[j] * w1.w;
+      }
+    }
+    u16x8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = f2bf(o[e]);
+    st8(dx + (size_t)row * F + f0, v);
+  }
+}
+
+// dW / db: thread per feature column f (all J classes), loop over the batch.
+__global__ __launch_bounds__(256) void linear_dw_kernel(const float* __restrict__ dlogits,
+                                                        const unsigned short* __restrict__ x,
+                                                        int B, int F, int J, const float* gscale,
+                                                        float* dW, float* db) {
+  const int f = blockIdx.x * 256 + threadIdx.x;
+  const float g = gscale ? *gscale : 1.f;
+  if (f < F) {
+    float acc[kMaxJ];
+#pragma unroll
+    for (int j = 0; j < kMaxJ; ++j) acc[j] = 0.f;
+    for (int r = 0; r < B; ++r) {
+      const float xv = bf2f(x[(size_t)r * F + f]);
+#pragma unroll
+      for (int j = 0; j < kMaxJ; ++j)
+        if (j < J) acc[j] += dlogits[(size_t)r * J + j] * xv;
+    }
+#pragma unroll
+    for (int j = 0; j < kMaxJ; ++j)
+      if (j < J) dW[(size_t)j * F + f] += acc[j] * g;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < J && db) {
+    float s = 0.f;
+    for (int r = 0; r < B; ++r) s += dlogits[(size_t)r * J + threadIdx.x];
+    db[threadIdx.x] += s * g;
+  }
+}
+
+// Generic softmax cross-entropy on [B][J] logits (bf16 or fp32), one block per row.
+// Writes dlogits (bf16, scaled by 1/B * g) for the MFMA GEMM backward.
+__global__ __launch_bounds__(256) void softmax_ce_kernel(const void* logits, int logits_bf16,
+                                                         const long long* labels, int B, int J,
+                                                         float inv_b, float* loss_sum,
+                                                         int* correct, void* dlogits,
+                                                         int dlogits_bf16) {
+  __shared__ float red[2][4];
+  __shared__ int redi[4];
+  const int row = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  auto get = [&](int j) -> float {
+    return logits_bf16 ? bf2f(((const unsigned short*)logits)[(size_t)row * J + j])
+                       : ((const float*)logits)[(size_t)row * J + j];
+  };
+  float mx = -INFINITY;
+  int arg = 0x7fffffff;
+  for (int j = tid; j < J; j += 256) {
+    const float v = get(j);
+    if (v > mx) { mx = v; arg = j; }
+  }
+  // argmax with lowest-index tie-break
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(mx, o, kWave);
+    const int oa = __shfl_xor(arg, o, kWave);
+    if (om > mx || (om == mx && oa < arg)) { mx = om; arg = oa; }
+  }
+  if (lane == 0) { red[0][wid] = mx; redi[wid] = arg; }
+  __syncthreads();
+  mx = red[0][0]; arg = redi[0];
+  for (int w = 1; w < 4; ++w)
+    if (red[0][w] > mx || (red[0][w] == mx && redi[w] < arg)) { mx = red[0][w]; arg = redi[w]; }
+  float se = 0.f;
+  for (int j = tid; j < J; j += 256) se += __expf(get(j) - mx);
+  se = wave_sum(se);
+  __syncthreads();
+  if (lane == 0) red[1][wid] = se;
+  __syncthreads();
+  se = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  const float lse = mx + __logf(se);
+  const int y = (int)labels[row];
+  if (dlogits)
+    for (int j = tid; j < J; j += 256) {
+      const float p = __expf(get(j) - lse);
+      const float d = (p - (j == y ? 1.f : 0.f)) * inv_b;
+      if (dlogits_bf16) ((unsigned short*)dlogits)[(size_t)row * J + j] = f2bf(d);
+      else ((float*)dlogits)[(size_t)row * J + j] = d;
+    }
+  if (tid == 0) {
+    if (loss_sum) atomicAdd(loss_sum, (lse - get(y)) * inv_b);
+    if (correct && arg == y) atomicAdd(correct, 1);
+  }
+}
+
+}  // namespace ddp_amd
+
+using namespace ddp_amd;
+
+extern "C" int ddp_linear_ce_fwd(const void* x, const float* W, const float* b,
+                                 const long long* labels, int B, int F, int J, float* logits,
+                                 float* dlogits, float* loss_sum, int* correct, hipStream_t st) {
+  if (J > kMaxJ || F % 8) return -1;
+  hipLaunchKernelGGL(linear_ce_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, st,
+                     (const unsigned short*)x, W, b, labels, B, F, J, 1.f / (float)B, logits,
+                     dlogits, loss_sum, correct);
+  return (int)hipGetLastError();
+}
+
+extern "C" int ddp_linear_bwd(const float* dlogits, const void* x, const float* W, int B, int F,
+                              int J, const float* gscale, void* dx, float* dW, float* db,
+                              hipStream_t st) {
+  if (J > kMaxJ || F % 8) return -1;
+  if (dx)
+    hipLaunchKernelGGL(linear_dx_kernel, dim3((B + 3) / 4), dim3(256), 0, st, dlogits, W, B, F, J,
+                       gscale, (unsigned short*)dx);
+  hipLaunchKernelGGL(linear_dw_kernel, dim3((F + 255) / 256), dim3(256), 0, st, dlogits,
+                     (const unsigned short*)x, B, F, J, gscale, dW, db);
+  return (int)hipGetLastError();
+}
+
+extern "C" int ddp_softmax_ce(const void* logits, int logits_bf16, const long long* labels, int B,
+                              int J, float* loss_sum, int* correct, void* dlogits,
+                              int dlogits_bf16, hipStream_t st) {
+  hipLaunchKernelGGL(softmax_ce_kernel, dim3(B), dim3(256), 0, st, logits, logits_bf16, labels, B,
+                     J, 1.f / (float)B, loss_sum, correct, dlogits, dlogits_bf16);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,282 @@
+// Native communication runtime — see comm.h.
+#include "comm.h"
+
+#include <cstring>
+#include <stdexcept>
+
+namespace ddp_amd {
+
+#define HIP_OK(x)                                                                        \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess)                                                                \
+      throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e_) +     \
+                               " at " __FILE__ ":" + std::to_string(__LINE__));          \
+  } while (0)
+
+#define NCCL_OK(x)                                                                       \
+  do {                                                                                   \
+    ncclResult_t r_ = (x);                                                               \
+    if (r_ != ncclSuccess)                                                               \
+      throw std::runtime_error(std::string("RCCL error: ") + ncclGetErrorString(r_) +   \
+                               " at " __FILE__ ":" + std::to_string(__LINE__));          \
+  } while (0)
+
+// dtype codes shared with parallel/comm.py
+static ncclDataType_t to_nccl(int dtype) {
+  switch (dtype) {
+    case 0: return ncclFloat32;
+    case 1: return ncclBfloat16;
+    case 2: return ncclFloat16;
+    case 3: return ncclInt32;
+    case 4: return ncclInt64;
+    case 5: return ncclUint8;
+    default: throw std::runtime_error("unsupported dtype code");
+  }
+}
+static size_t dtype_bytes(int dtype) {
+  switch (dtype) {
+    case 0: case 3: return 4;
+    case 1: case 2: return 2;
+    case 4: return 8;
+    case 5: return 1;
+    default: return 4;
+  }
+}
+// op codes: 0 sum, 1 prod, 2 max, 3 min, 4 avg
+static ncclRedOp_t to_op(int op) {
+  switch (op) {
+    case 0: return ncclSum;
+    case 1: return ncclProd;
+    case 2: return ncclMax;
+    case 3: return ncclMin;
+    case 4: return ncclAvg;
+    default: throw std::runtime_error("unsupported reduction op");
+  }
+}
+
+std::vector<BucketSpec> plan_buckets(const std::vector<size_t>& offsets,
+                                     const std::vector<size_t>& numels, size_t elem_bytes,
+                                     size_t cap_bytes, size_t cap_first_bytes) {
+  std::vector<BucketSpec> out;
+  const int n = (int)numels.size();
+  int end = n;  // exclusive
+  size_t bytes = 0;
+  int start = n;
+  auto flush = [&](int s, int e) {
+    if (s >= e) return;
+    BucketSpec b;
+    b.first_param = s;
+    b.last_param = e;
+    b.offset = offsets[s];
+    b.count = offsets[e - 1] + numels[e - 1] - offsets[s];
+    out.push_back(b);
+  };
+  for (int p = n - 1; p >= 0; --p) {
+    const size_t cap = out.empty() ? cap_first_bytes : cap_bytes;
+    const size_t pb = numels[p] * elem_bytes;
+    if (start < end && bytes + pb > cap) {
+      flush(start, end);
+      end = start;
+      bytes = 0;
+    }
+    start = p;
+    bytes += pb;
+  }
+  flush(start, end);
+  return out;
+}
+
+RcclComm::RcclComm(int rank, int world, const std::string& uid_bytes, int device)
+    : rank_(rank), world_(world), device_(device) {
+  HIP_OK(hipSetDevice(device));
+  if (world > 1) {
+    if (uid_bytes.size() != sizeof(ncclUniqueId))
+      throw std::runtime_error("bad ncclUniqueId size");
+    ncclUniqueId id;
+    std::memcpy(&id, uid_bytes.data(), sizeof(id));
+    NCCL_OK(ncclCommInitRank(&comm_, world, id, rank));
+  }
+}
+
+RcclComm::~RcclComm() {
+  if (comm_ && !aborted_) ncclCommDestroy(comm_);
+}
+
+std::string RcclComm::make_unique_id() {
+  ncclUniqueId id;
+  NCCL_OK(ncclGetUniqueId(&id));
+  return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
+}
+
+void RcclComm::all_reduce(void* buf, size_t count, int dtype, int op, hipStream_t st) {
+  if (world_ == 1 || count == 0) return;
+  NCCL_OK(ncclAllReduce(buf, buf, count, to_nccl(dtype), to_op(op), comm_, st));
+}
+
+void RcclComm::broadcast(void* buf, size_t count, int dtype, int root, hipStream_t st) {
+  if (world_ == 1 || count == 0) return;
+  NCCL_OK(ncclBroadcast(buf, buf, count, to_nccl(dtype), root, comm_, st));
+}
+
+void RcclComm::all_gather(const void* send, void* recv, size_t count, int dtype, hipStream_t st) {
+  if (world_ == 1) {
+    if (send != recv) HIP_OK(hipMemcpyAsync(recv, send, count * dtype_bytes(dtype), hipMemcpyDeviceToDevice, st));
+    return;
+  }
+  NCCL_OK(ncclAllGather(send, recv, count, to_nccl(dtype), comm_, st));
+}
+
+void RcclComm::reduce_scatter(const void* send, void* recv, size_t count, int dtype, int op,
+                              hipStream_t st) {
+  if (world_ == 1) {
+    if (send != recv) HIP_OK(hipMemcpyAsync(recv, send, count * dtype_bytes(dtype), hipMemcpyDeviceToDevice, st));
+    return;
+  }
+  NCCL_OK(ncclReduceScatter(send, recv, count, to_nccl(dtype), to_op(op), comm_, st));
+}
+
+void RcclComm::gather(const void* send, void* recv, size_t count, int dtype, int root,
+                      hipStream_t st) {
+  const size_t bytes = count * dtype_bytes(dtype);
+  if (rank_ == root)
+    HIP_OK(hipMemcpyAsync((char*)recv + (size_t)root * bytes, send, bytes, hipMemcpyDeviceToDevice, st));
+  if (world_ == 1) return;
+  const ncclDataType_t dt = to_nccl(dtype);
+  NCCL_OK(ncclGroupStart());
+  if (rank_ == root) {
+    for (int r = 0; r < world_; ++r)
+      if (r != root) NCCL_OK(ncclRecv((char*)recv + (size_t)r * bytes, count, dt, r, comm_, st));
+  } else {
+    NCCL_OK(ncclSend(send, count, dt, root, comm_, st));
+  }
+  NCCL_OK(ncclGroupEnd());
+}
+
+void RcclComm::scatter(const void* send, void* recv, size_t count, int dtype, int root,
+                       hipStream_t st) {
+  const size_t bytes = count * dtype_bytes(dtype);
+  if (rank_ == root && (const char*)send + (size_t)root * bytes != recv)
+    HIP_OK(hipMemcpyAsync(recv, (const char*)send + (size_t)root * bytes, bytes, hipMemcpyDeviceToDevice, st));
+  if (world_ == 1) return;
+  const ncclDataType_t dt = to_nccl(dtype);
+  NCCL_OK(ncclGroupStart());
+  if (rank_ == root) {
+    for (int r = 0; r < world_; ++r)
+      if (r != root) NCCL_OK(ncclSend((const char*)send + (size_t)r * bytes, count, dt, r, comm_, st));
+  } else {
+    NCCL_OK(ncclRecv(recv, count, dt, root, comm_, st));
+  }
+  NCCL_OK(ncclGroupEnd());
+}
+
+void RcclComm::scatter_replicated(void* buf, size_t count, int dtype, int root, hipStream_t st) {
+  if (world_ == 1 || count == 0) return;
+  const ncclDataType_t dt = to_nccl(dtype);
+  NCCL_OK(ncclGroupStart());
+  if (rank_ == root) {
+    for (int r = 0; r < world_; ++r)
+      if (r != root) NCCL_OK(ncclSend(buf, count, dt, r, comm_, st));
+  } else {
+    NCCL_OK(ncclRecv(buf, count, dt, root, comm_, st));
+  }
+  NCCL_OK(ncclGroupEnd());
+}
+
+void RcclComm::send(const void* buf, size_t count, int dtype, int peer, hipStream_t st) {
+  NCCL_OK(ncclSend(buf, count, to_nccl(dtype), peer, comm_, st));
+}
+
+void RcclComm::recv(void* buf, size_t count, int dtype, int peer, hipStream_t st) {
+  NCCL_OK(ncclRecv(buf, count, to_nccl(dtype), peer, comm_, st));
+}
+
+int RcclComm::async_error() {
+  if (!comm_) return 0;
+  ncclResult_t r = ncclSuccess;
+  ncclCommGetAsyncError(comm_, &r);
+  return (int)r;
+}
+
+void RcclComm::abort() {
+  if (comm_ && !aborted_) {
+    ncclCommAbort(comm_);
+    aborted_ = true;
+  }
+}
+
+// ------------------------------------------------------------------ Reducer
+Reducer::Reducer(RcclComm* comm, float* arena, std::vector<size_t> offsets,
+                 std::vector<size_t> numels, size_t cap_bytes, size_t cap_first_bytes,
+                 bool average)
+    : comm_(comm), arena_(arena), offsets_(std::move(offsets)), numels_(std::move(numels)),
+      average_(average) {
+  buckets_ = plan_buckets(offsets_, numels_, sizeof(float), cap_bytes, cap_first_bytes);
+  bucket_of_param_.assign(numels_.size(), -1);
+  for (size_t b = 0; b < buckets_.size(); ++b)
+    for (int p = buckets_[b].first_param; p < buckets_[b].last_param; ++p) bucket_of_param_[p] = (int)b;
+  pending_.assign(buckets_.size(), 0);
+  ready_.assign(buckets_.size(), 0);
+  ready_ev_.resize(buckets_.size());
+  done_ev_.resize(buckets_.size());
+  for (size_t b = 0; b < buckets_.size(); ++b) {
+    HIP_OK(hipEventCreateWithFlags(&ready_ev_[b], hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&done_ev_[b], hipEventDisableTiming));
+  }
+  int lo = 0, hi = 0;
+  HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  HIP_OK(hipStreamCreateWithPriority(&comm_stream_, hipStreamNonBlocking, hi));
+  prepare();
+}
+
+Reducer::~Reducer() {
+  for (auto e : ready_ev_) hipEventDestroy(e);
+  for (auto e : done_ev_) hipEventDestroy(e);
+  if (comm_stream_) hipStreamDestroy(comm_stream_);
+}
+
+void Reducer::prepare() {
+  for (size_t b = 0; b < buckets_.size(); ++b) {
+    pending_[b] = buckets_[b].last_param - buckets_[b].first_param;
+    ready_[b] = 0;
+  }
+  next_launch_ = 0;
+}
+
+void Reducer::mark_ready(int p, hipStream_t compute) {
+  if (p < 0 || p >= (int)bucket_of_param_.size()) throw std::runtime_error("bad param index");
+  const int b = bucket_of_param_[p];
+  if (pending_[b] <= 0) throw std::runtime_error("parameter marked ready twice in one backward");
+  if (--pending_[b] == 0) {
+    ready_[b] = 1;
+    launch_ready(compute);
+  }
+}
+
+// Launch buckets strictly in plan order so every rank issues collectives identically.
+void Reducer::launch_ready(hipStream_t compute) {
+  while (next_launch_ < (int)buckets_.size() && ready_[next_launch_]) {
+    const int b = next_launch_++;
+    const BucketSpec& bs = buckets_[b];
+    HIP_OK(hipEventRecord(ready_ev_[b], compute));
+    HIP_OK(hipStreamWaitEvent(comm_stream_, ready_ev_[b], 0));
+    comm_->all_reduce(arena_ + bs.offset, bs.count, /*fp32*/ 0, average_ ? 4 : 0, comm_stream_);
+    HIP_OK(hipEventRecord(done_ev_[b], comm_stream_));
+    if (debug_sync_) HIP_OK(hipStreamSynchronize(comm_stream_));
+  }
+}
+
+void Reducer::finalize(hipStream_t compute) {
+  for (size_t b = 0; b < buckets_.size(); ++b)
+    if (!ready_[b]) {
+      if (pending_[b] != 0)
+        throw std::runtime_error("Reducer::finalize: bucket " + std::to_string(b) +
+                                 " has parameters whose gradient was never produced "
+                                 "(unused parameters are not supported)");
+    }
+  launch_ready(compute);
+  for (int b = 0; b < next_launch_; ++b) HIP_OK(hipStreamWaitEvent(compute, done_ev_[b], 0));
+  prepare();
+}
+
+}  // namespace ddp_amd

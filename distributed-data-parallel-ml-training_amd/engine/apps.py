@@ -1,0 +1,80 @@
+"""Entry points behind part1/main.py, part2/part2a/main.py, part2/part2b/main.py, part3/main.py.
+
+Reference parity: ``main()`` of each reference script (part1/main.py:114-130,
+part2/part2a/main.py:181-207, part2/part2b/main.py:169-195, part3/main.py:159-186):
+parse -> [init process group + diagnostics] -> seed (89395) -> per-rank batch int(256/ws) ->
+CrossEntropyLoss -> loaders (sharded train, unsharded test) -> VGG11 -> [DDP] ->
+SGD(0.1, 0.9, 1e-4) -> 1 epoch of train_model + test_model -> [destroy_process_group].
+
+On a GPU the same program runs on the gfx950 kernels with the native RCCL communicator;
+on a CPU it runs on ATen + Gloo, exactly like the reference.
+"""
+import functools
+
+import torch
+
+from .. import SEED
+from ..data import SyntheticCIFAR10, make_loader
+from ..models import build
+from ..optim import FusedSGD
+from ..parallel import (DistributedDataParallel, STRATEGIES, destroy, init_distributed_setup,
+                        make_communicator, test_distributed_setup)
+from ..utils import MetricsSink, load_checkpoint, parse_all, pick_device, save_checkpoint, \
+    seed_everything
+from .trainer import CrossEntropyLoss, test_model, train_model
+
+PART_STRATEGY = {"part1": None, "part2a": "gather_scatter", "part2b": "allreduce", "part3": "ddp"}
+
+
+def main(part, argv=None):
+    strategy = PART_STRATEGY[part]
+    distributed = strategy is not None
+    args = parse_all(argv, distributed=distributed, description=f"ddp_amd {part}")
+    torch.set_num_threads(args.threads)
+    world, rank = 1, 0
+    if distributed:
+        world, rank = args.size, args.rank
+        device = pick_device(args.device)
+        init_distributed_setup(args.master_ip, args.master_port, rank, world, backend="gloo")
+        test_distributed_setup()
+    else:
+        device = pick_device(args.device)
+
+    seed_everything(SEED)
+    batch_size = int(args.global_batch / world)  # batch for one node
+
+    criterion = CrossEntropyLoss()
+    train_ds = SyntheticCIFAR10(train=True, seed=SEED, n=args.train_size)
+    test_ds = SyntheticCIFAR10(train=False, seed=SEED, n=args.test_size)
+    train_loader = make_loader(train_ds, batch_size, device, world, rank, train=True,
+                               shard=distributed, max_batches=args.max_batches)
+    test_loader = make_loader(test_ds, batch_size, device, train=False, shard=False)
+
+    model = build(args.model).to(device)
+    comm = make_communicator(device) if distributed else None
+    if strategy == "ddp":
+        model = DistributedDataParallel(model, comm, bucket_cap_mb=args.bucket_mb,
+                                        first_bucket_cap_mb=args.first_bucket_mb)
+    optimizer = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=0.0001)
+    if args.resume:
+        load_checkpoint(args.resume, model, optimizer)
+    sync = None
+    if strategy in STRATEGIES:
+        sync = functools.partial(_sync, STRATEGIES[strategy], comm)
+    metrics = MetricsSink(args.metrics, rank)
+
+    for epoch in range(args.epochs):
+        train_loader.set_epoch(epoch)
+        train_model(model, train_loader, optimizer, criterion, epoch, device, sync, metrics=metrics)
+        if not args.no_test:
+            test_model(model, test_loader, criterion, device)
+
+    if args.save and rank == 0:
+        save_checkpoint(args.save, model, optimizer)
+    if distributed:
+        destroy()
+    return model
+
+
+def _sync(fn, comm, model):
+    fn(model, comm)

@@ -1,0 +1,64 @@
+"""Whole-step hipGraph capture.
+
+A training step on MI355X at the reference's global batch (256, or 32 per GPU at 8 GPUs) is
+launch/latency bound: ~40 kernels forward+backward+optimizer at microsecond scale. Instead of a
+tracing compiler we capture the ENTIRE step — on-device augmentation of the next batch, forward,
+backward (whose fused kernels trigger the DDP bucket all-reduces on the comm stream through
+events), the gradient sync of 2A/2B, and the fused SGD + weight re-pack — into one hipGraph and
+replay it. Host cost per step becomes one graph launch.
+
+Capture protocol: a few eager warm-up steps on a side stream (lazy allocations, autograd
+structures), then ``torch.cuda.graph`` capture; replays are bit-identical to eager steps.
+"""
+import torch
+
+
+class TrainStep:
+    def __init__(self, model, optimizer, criterion, loader, sync=None, use_graph=True):
+        self.model, self.optimizer, self.criterion, self.loader = model, optimizer, criterion, loader
+        self.sync = sync
+        self.use_graph = use_graph
+        dev = loader.device
+        self.loss_sum = torch.zeros((), dtype=torch.float32, device=dev)
+        self.graph = None
+
+    def _body(self):
+        self.optimizer.zero_grad()
+        x, y = self.loader.fill()
+        out = self.model(x)
+        loss = self.criterion(out, y)
+        loss.backward()
+        if self.sync is not None:
+            self.sync(self.model)
+        self.optimizer.step()
+        self.loss_sum.add_(loss.detach())
+
+    def warmup(self, steps):
+        """Eager steps on a side stream (also the fallback execution path)."""
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(steps):
+                self._body()
+        torch.cuda.current_stream().wait_stream(s)
+
+    def capture(self):
+        if not self.use_graph:
+            return
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._body()
+        self.graph = g
+
+    def step(self):
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._body()
+
+    def pop_loss(self):
+        """Mean-free running loss sum since the last call (forces a device sync)."""
+        v = float(self.loss_sum.item())
+        self.loss_sum.zero_()
+        return v

@@ -1,0 +1,83 @@
+"""Training and evaluation loops with the reference's observable behaviour.
+
+Reference parity: ``train_model`` (part1/main.py:52-93; part2/part2a/main.py:118-160 with the
+sync call at :143) and ``test_model`` (part1/main.py:96-111):
+* per batch: timer start -> ``.to(device)`` -> zero_grad -> forward -> loss -> backward ->
+  [gradient sync] -> step -> ``loss.item()``;
+* ``[epoch, batch] loss: x.xxx`` every 20 batches (rank-local running mean, not all-reduced);
+* iteration 0 is warm-up; the wall time of iterations 1..39 is summed and printed at 39;
+* eval: model.eval(), no_grad, sum of per-batch mean CE divided by the NUMBER OF BATCHES,
+  argmax accuracy over the whole (unsharded) test set, reference print format.
+"""
+import time
+
+import torch
+import torch.nn as nn
+
+
+class CrossEntropyLoss(nn.Module):
+    """``nn.CrossEntropyLoss()`` (mean); GPU logits use the fused softmax-CE HIP kernel."""
+
+    def forward(self, logits, target):
+        if logits.is_cuda:
+            from ..ops.layers import cross_entropy
+            return cross_entropy(logits, target)
+        return nn.functional.cross_entropy(logits, target)
+
+
+def train_model(model, train_loader, optimizer, criterion, epoch, device="cpu", sync=None,
+                log=print, metrics=None, watchdog=None):
+    running_loss = 0.0
+    total_time = 0
+    stats = {"iter_ns": []}
+    for batch_idx, (data, target) in enumerate(train_loader):
+        start_time = time.perf_counter_ns()
+        data, target = data.to(device), target.to(device)
+
+        optimizer.zero_grad()
+        output = model(data)
+        loss = criterion(output, target)
+        loss.backward()
+        if sync is not None:
+            sync(model)
+        optimizer.step()
+
+        running_loss += loss.item()
+        if batch_idx % 20 == 19:
+            log(f'[{epoch + 1}, {batch_idx + 1:5d}] loss: {running_loss / 20:.3f}')
+            running_loss = 0.0
+
+        dt = time.perf_counter_ns() - start_time
+        stats["iter_ns"].append(dt)
+        if 0 < batch_idx < 40:
+            total_time += dt
+        if batch_idx == 39:
+            log(f'Total time for 1-39 iteration in ns: {total_time}')
+            log(f'Average time for 1-39 iteration in ns: {total_time / 39.0}')
+        if metrics is not None:
+            metrics.log(event="iter", epoch=epoch, batch=batch_idx, ns=dt)
+        if watchdog is not None:
+            watchdog.beat()
+    stats["total_1_39_ns"] = total_time
+    return stats
+
+
+def test_model(model, test_loader, criterion, device="cpu", log=print):
+    model.eval()
+    test_loss = 0
+    correct = 0
+    nb = 0
+    with torch.no_grad():
+        for data, target in test_loader:
+            data, target = data.to(device), target.to(device)
+            output = model(data)
+            test_loss += criterion(output, target)
+            pred = output.max(1, keepdim=True)[1]
+            correct += pred.eq(target.view_as(pred)).sum().item()
+            nb += 1
+    n = len(test_loader.dataset)
+    test_loss = float(test_loss) / max(nb, 1)
+    log('Test set: Average loss: {:.4f}, Accuracy: {}/{} ({:.0f}%)\n'.format(
+        test_loss, correct, n, 100. * correct / n))
+    model.train()
+    return test_loss, correct

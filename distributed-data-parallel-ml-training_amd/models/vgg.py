@@ -1,0 +1,110 @@
+"""VGG family (VGG-11/13/16/19) for 3x32x32 inputs and 10 classes.
+
+Reference parity: part1/model.py:3-50 (identical copies in part2/part2a, part2/part2b, part3).
+The module tree — ``layers`` (nn.Sequential of Conv2d(3x3,s1,p1,bias) / BatchNorm2d(
+track_running_stats=False) / ReLU(inplace) / MaxPool2d(2,2)) and ``fc1`` (Linear(512, 10)) —
+is kept exactly so that ``state_dict`` keys and shapes match the reference checkpoint layout
+(``layers.{0,4,8,...}.{weight,bias}``, BN without running buffers, ``fc1.{weight,bias}``).
+
+Execution:
+* CPU tensors run the ATen modules unchanged (the numerical oracle, and the part1 CPU path).
+* GPU tensors run the fused gfx950 path: each Conv->BN->ReLU(->MaxPool) group becomes one
+  ``ConvBNAct`` autograd Function (ops/layers.py), activations stay NHWC bf16, the head is a
+  fused small-Linear kernel. Inputs may be NCHW fp32 (converted on device) or the NHWC bf16
+  batches produced by the on-device data pipeline (data/loader.py).
+"""
+import torch
+import torch.nn as nn
+
+_cfg = {
+    'VGG11': [64, 'M', 128, 'M', 256, 256, 'M', 512, 512, 'M', 512, 512, 'M'],
+    'VGG13': [64, 64, 'M', 128, 128, 'M', 256, 256, 'M', 512, 512, 'M', 512, 512, 'M'],
+    'VGG16': [64, 64, 'M', 128, 128, 'M', 256, 256, 256, 'M', 512, 512, 512, 'M', 512, 512, 512, 'M'],
+    'VGG19': [64, 64, 'M', 128, 128, 'M', 256, 256, 256, 256, 'M', 512, 512, 512, 512, 'M',
+              512, 512, 512, 512, 'M'],
+}
+
+IN_CHANNELS_PADDED = 8  # first conv consumes 3 real + 5 zero channels on the MFMA path
+
+
+def _make_layers(cfg):
+    """Same module sequence (and therefore the same Sequential indices) as part1/model.py:11-27."""
+    mods = []
+    cin = 3
+    for v in cfg:
+        if v == 'M':
+            mods.append(nn.MaxPool2d(kernel_size=2, stride=2))
+            continue
+        mods += [nn.Conv2d(cin, v, kernel_size=3, stride=1, padding=1, bias=True),
+                 nn.BatchNorm2d(v, track_running_stats=False),
+                 nn.ReLU(inplace=True)]
+        cin = v
+    return nn.Sequential(*mods)
+
+
+class _VGG(nn.Module):
+    """VGG module for 3x32x32 input, 10 classes."""
+
+    def __init__(self, name, num_classes=10):
+        super().__init__()
+        self.name = name
+        self.layers = _make_layers(_cfg[name])
+        self.fc1 = nn.Linear(512, num_classes)
+        self._plan = None
+
+    # ------------------------------------------------------------ fused GPU plan
+    def fused_plan(self):
+        """Group the Sequential into ConvBNAct stages (built once per device)."""
+        from ..ops.layers import ConvBNActSpec
+        dev = self.fc1.weight.device
+        if self._plan is not None and self._plan[0] == dev:
+            return self._plan[1]
+        mods = list(self.layers)
+        stages, i, first = [], 0, True
+        while i < len(mods):
+            conv = mods[i]
+            if not isinstance(conv, nn.Conv2d):
+                raise RuntimeError(f"unexpected module {conv} at layers.{i}")
+            bn, relu = mods[i + 1], mods[i + 2]
+            assert isinstance(bn, nn.BatchNorm2d) and isinstance(relu, nn.ReLU)
+            pool = i + 3 < len(mods) and isinstance(mods[i + 3], nn.MaxPool2d)
+            spec = ConvBNActSpec(conv, bn, relu=True, pool=pool,
+                                 cin_pad=IN_CHANNELS_PADDED if first else None)
+            stages.append(spec)
+            first = False
+            i += 4 if pool else 3
+        self._plan = (dev, stages)
+        return stages
+
+    def packed_specs(self):
+        return self.fused_plan() if self.fc1.weight.is_cuda else []
+
+    def forward(self, x):
+        if not x.is_cuda:
+            y = self.layers(x)
+            y = y.view(y.size(0), -1)
+            return self.fc1(y)
+        from ..ops.layers import conv_bn_act, linear_small, to_nhwc_input
+        h = to_nhwc_input(x, IN_CHANNELS_PADDED)
+        for spec in self.fused_plan():
+            h = conv_bn_act(h, spec)
+        if h.shape[1] != 1 or h.shape[2] != 1:
+            raise RuntimeError("VGG head expects 1x1 spatial features (32x32 input)")
+        h = h.view(h.shape[0], -1)  # NHWC with H=W=1: identical to the NCHW flatten
+        return linear_small(h, self.fc1)
+
+
+def VGG11():
+    return _VGG('VGG11')
+
+
+def VGG13():
+    return _VGG('VGG13')
+
+
+def VGG16():
+    return _VGG('VGG16')
+
+
+def VGG19():
+    return _VGG('VGG19')

@@ -1,0 +1,78 @@
+"""Fused multi-tensor SGD.
+
+Reference parity: ``optim.SGD(params, lr=0.1, momentum=0.9, weight_decay=1e-4)``
+(part1/main.py:124-125, part3/main.py:176-177): no dampening, no nesterov, momentum buffer
+initialised to the first gradient. On the GPU one launch of ``sgd_kernel`` (csrc/kernels/optim.hip)
+updates the whole flat parameter arena, followed by one launch that re-packs every conv weight
+into the bf16 MFMA operand layouts the next forward consumes. On the CPU it is exactly
+``torch.optim.SGD`` (the oracle).
+"""
+import torch
+
+from .arena import arena_for
+
+
+class FusedSGD(torch.optim.SGD):
+    def __init__(self, params, lr=0.1, momentum=0.0, dampening=0.0, weight_decay=0.0,
+                 nesterov=False, grad_scale=1.0):
+        params = list(params)
+        super().__init__(params, lr=lr, momentum=momentum, dampening=dampening,
+                         weight_decay=weight_decay, nesterov=nesterov)
+        self._grad_scale_factor = grad_scale
+        self._fused = bool(params) and params[0].is_cuda
+        if self._fused:
+            if dampening != 0.0:
+                raise ValueError("fused SGD supports dampening=0 only")
+            if len(self.param_groups) != 1:
+                raise ValueError("fused SGD supports a single param group")
+            self.arena = arena_for(params)
+            self.momentum_buffer = torch.zeros_like(self.arena.data)
+
+    def _packs(self):
+        return [p._ddp_amd_pack() for p in self.arena.params if hasattr(p, "_ddp_amd_pack")]
+
+    def zero_grad(self, set_to_none=False):
+        if self._fused:
+            self.arena.zero_grad()  # kernels accumulate into the arena: always zero, never None
+        else:
+            super().zero_grad(set_to_none=set_to_none)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        if not self._fused:
+            return super().step(closure)
+        from ..ops.common import native, stream_handle
+        g = self.param_groups[0]
+        s = stream_handle()
+        a = self.arena
+        native().sgd(a.data.data_ptr(), a.grad.data_ptr(), self.momentum_buffer.data_ptr(), a.total,
+                     float(g["lr"]), float(g["momentum"]), float(g["weight_decay"]),
+                     float(self._grad_scale_factor), int(bool(g["nesterov"])), s)
+        packs = self._packs()
+        if packs:
+            native().pack_conv_weights(packs, s)
+        return None
+
+    def state_dict(self):
+        sd = super().state_dict()
+        if self._fused:
+            # expose the momentum buffers in torch.optim.SGD's per-parameter layout
+            a = self.arena
+            for i, p in enumerate(a.params):
+                o, n = a.offsets[i], a.numels[i]
+                sd["state"][i] = {"momentum_buffer": self.momentum_buffer[o:o + n].view(p.shape).clone()}
+        return sd
+
+    def load_state_dict(self, sd):
+        if not self._fused:
+            return super().load_state_dict(sd)
+        a = self.arena
+        st = sd.get("state", {})
+        for i, p in enumerate(a.params):
+            o, n = a.offsets[i], a.numels[i]
+            buf = st.get(i, st.get(str(i), {})).get("momentum_buffer")
+            if buf is not None:
+                self.momentum_buffer[o:o + n].copy_(buf.reshape(-1).to(self.momentum_buffer.device))
+        for k in ("lr", "momentum", "weight_decay", "nesterov"):
+            if sd.get("param_groups"):
+                self.param_groups[0][k] = sd["param_groups"][0].get(k, self.param_groups[0][k])

@@ -1,0 +1,173 @@
+"""Process-group bootstrap and communicators.
+
+Reference parity:
+* ``init_distributed_setup`` (part2/part2a/main.py:52-58): sets MASTER_ADDR/MASTER_PORT and
+  calls ``init_process_group``; ``test_distributed_setup`` (part2/part2a/main.py:42-49) prints
+  the four diagnostic lines; ``dist.destroy_process_group`` at the end (part3/main.py:186).
+* The reference's data plane is Gloo over TCP.
+
+MI355X design: one process per GPU. torch.distributed (Gloo, CPU) is the *control plane* —
+rendezvous through the TCPStore at --master-ip:--master-port, barriers, timing reductions,
+printing the setup. The *data plane* is our native RCCL communicator over xGMI
+(csrc/runtime/comm.cpp): rank 0 creates the ncclUniqueId and publishes it through the same
+TCPStore. On CPU-only runs (tests, part1 on CPU) a TorchCommunicator over Gloo implements the
+same interface so every strategy can be exercised without GPUs.
+"""
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+# dtype / op codes shared with csrc/runtime/comm.cpp
+_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.int32: 3, torch.int64: 4,
+       torch.uint8: 5}
+SUM, PROD, MAX, MIN, AVG = 0, 1, 2, 3, 4
+_TORCH_OP = {SUM: dist.ReduceOp.SUM, PROD: dist.ReduceOp.PRODUCT, MAX: dist.ReduceOp.MAX,
+             MIN: dist.ReduceOp.MIN}
+
+
+def init_distributed_setup(master_ip, master_port, rank, world_size, backend="gloo",
+                           timeout_s=1800):
+    """Reference-compatible bootstrap (part2/part2a/main.py:52-58)."""
+    os.environ["MASTER_ADDR"] = str(master_ip)
+    os.environ["MASTER_PORT"] = str(master_port)
+    dist.init_process_group(backend, rank=rank, world_size=world_size,
+                            timeout=datetime.timedelta(seconds=timeout_s))
+
+
+def test_distributed_setup():
+    """Reference-format diagnostics (part2/part2a/main.py:42-49)."""
+    print(f'Is initialized: {dist.is_initialized()}')
+    print(f'Backend: {dist.get_backend()}')
+    print(f'World size: {dist.get_world_size()}')
+    print(f'Rank: {dist.get_rank()}\n')
+
+
+def destroy():
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def _store():
+    # the default group's store is the TCPStore created by init_process_group (env://)
+    return dist.distributed_c10d._get_default_store()
+
+
+class TorchCommunicator:
+    """torch.distributed (Gloo on CPU) implementation of the communicator interface."""
+
+    kind = "torch"
+
+    def __init__(self, group=None):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+
+    def all_reduce(self, t, op=SUM):
+        if op == AVG:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            t /= self.world
+        else:
+            dist.all_reduce(t, op=_TORCH_OP[op], group=self.group)
+
+    def all_reduce_async(self, t):
+        return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+
+    def broadcast(self, t, src=0):
+        dist.broadcast(t, src, group=self.group)
+
+    def all_gather(self, t):
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t, group=self.group)
+        return out
+
+    def gather(self, t, dst=0):
+        """Reference 2A gather (part2/part2a/main.py:104-107,114): returns the list on dst."""
+        if self.rank == dst:
+            lst = [torch.zeros_like(t) for _ in range(self.world)]
+            dist.gather(t, lst, dst=dst, group=self.group)
+            return lst
+        dist.gather(t, dst=dst, group=self.group)
+        return None
+
+    def scatter_replicated(self, t, src=0):
+        """Reference 2A scatter of [mean]*ws (part2/part2a/main.py:110,115)."""
+        if self.rank == src:
+            dist.scatter(t, [t] * self.world, src=src, group=self.group)
+        else:
+            dist.scatter(t, src=src, group=self.group)
+
+    def barrier(self):
+        dist.barrier(group=self.group)
+
+    def synchronize(self):
+        pass
+
+
+class RcclCommunicator:
+    """Native RCCL communicator (one GPU per process, collectives over xGMI)."""
+
+    kind = "rccl"
+
+    def __init__(self, rank=None, world=None, device=None, key="ddp_amd/rccl_uid"):
+        from ..ops.common import native
+        self.rank = dist.get_rank() if rank is None else rank
+        self.world = dist.get_world_size() if world is None else world
+        self.device = torch.cuda.current_device() if device is None else device
+        n = native()
+        uid = b""
+        if self.world > 1:
+            store = _store()
+            if self.rank == 0:
+                uid = n.make_unique_id()
+                store.set(key, uid)
+            else:
+                store.wait([key])
+                uid = store.get(key)
+        self.comm = n.RcclComm(self.rank, self.world, uid, self.device)
+
+    @staticmethod
+    def _s():
+        return torch.cuda.current_stream().cuda_stream
+
+    def all_reduce(self, t, op=SUM):
+        self.comm.all_reduce(t.data_ptr(), t.numel(), _DT[t.dtype], op, self._s())
+
+    def broadcast(self, t, src=0):
+        self.comm.broadcast(t.data_ptr(), t.numel(), _DT[t.dtype], src, self._s())
+
+    def all_gather(self, t):
+        out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        self.comm.all_gather(t.data_ptr(), out.data_ptr(), t.numel(), _DT[t.dtype], self._s())
+        return list(out.unbind(0))
+
+    def gather_into(self, t, buf, dst=0):
+        """Grouped send/recv gather of t into buf[world, numel] on dst."""
+        self.comm.gather(t.data_ptr(), buf.data_ptr() if buf is not None else 0, t.numel(),
+                         _DT[t.dtype], dst, self._s())
+
+    def scatter_replicated(self, t, src=0):
+        self.comm.scatter_replicated(t.data_ptr(), t.numel(), _DT[t.dtype], src, self._s())
+
+    def barrier(self):
+        if dist.is_initialized():
+            dist.barrier()
+
+    def synchronize(self):
+        torch.cuda.synchronize()
+
+    def check_health(self):
+        err = self.comm.async_error()
+        if err != 0:
+            raise RuntimeError(f"RCCL async error {err}")
+
+    def abort(self):
+        self.comm.abort()
+
+
+def make_communicator(device):
+    """RCCL on GPU, torch.distributed (Gloo) on CPU."""
+    if torch.device(device).type == "cuda":
+        return RcclCommunicator()
+    return TorchCommunicator()

@@ -1,0 +1,4 @@
+"""CLI contract, seeding, device selection, metrics, checkpoints, watchdog."""
+from .cli import get_rank, parse_arguments, parse_all, build_parser  # noqa: F401
+from .misc import (seed_everything, pick_device, MetricsSink, save_checkpoint,  # noqa: F401
+                   load_checkpoint, Watchdog)

@@ -1,0 +1,115 @@
+"""Multi-process (Gloo, CPU) workers for the distributed tests."""
+import os
+import socket
+import sys
+
+import torch
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def run_workers(fn, world, *args, timeout=300):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=fn, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            r, payload = q.get(timeout=timeout)
+            out[r] = {k: (torch.from_numpy(v) if hasattr(v, "dtype") and hasattr(v, "shape") else v)
+                      for k, v in payload.items()}
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for p in procs:
+        assert p.exitcode == 0, f"worker exit code {p.exitcode}"
+    return out
+
+
+def _init(rank, world, port):
+    sys.path.insert(0, REPO)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def train_worker(rank, world, port, q, strategy, steps, per_rank_batch, bucket_mb):
+    try:
+        _init(rank, world, port)
+        import torch.distributed as dist
+        from ddp_amd.models import VGG11
+        from ddp_amd.optim import FusedSGD
+        from ddp_amd.parallel import (TorchCommunicator, DistributedDataParallel, STRATEGIES,
+                                      check_replicas)
+        from ddp_amd.engine import CrossEntropyLoss
+        from ddp_amd.data import SyntheticCIFAR10, CPULoader
+        torch.manual_seed(89395)
+        model = VGG11()
+        comm = TorchCommunicator()
+        if strategy == "ddp":
+            model = DistributedDataParallel(model, comm, bucket_cap_mb=bucket_mb,
+                                            first_bucket_cap_mb=min(bucket_mb, 1.0))
+        opt = FusedSGD(model.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
+        crit = CrossEntropyLoss()
+        loader = CPULoader(SyntheticCIFAR10(True, n=per_rank_batch * world * steps),
+                           per_rank_batch, num_replicas=world, rank=rank)
+        first_grads = None
+        for i, (x, y) in enumerate(loader):
+            if i >= steps:
+                break
+            opt.zero_grad()
+            loss = crit(model(x), y)
+            loss.backward()
+            if strategy in STRATEGIES:
+                STRATEGIES[strategy](model, comm)
+            if first_grads is None:
+                first_grads = torch.cat([p.grad.reshape(-1).clone() for p in model.parameters()])
+            opt.step()
+        params = torch.cat([p.detach().reshape(-1).clone() for p in model.parameters()])
+        consistent = None
+        if strategy == "ddp":
+            consistent = check_replicas(model.arena, world)
+            info = {"buckets": list(model.buckets)}
+        else:
+            info = {}
+        dist.destroy_process_group()
+        q.put((rank, {"params": params.numpy(), "grads0": first_grads.numpy(),
+                      "consistent": consistent, **info}))
+    except Exception as e:  # surface the error in the parent
+        import traceback
+        q.put((rank, {"error": traceback.format_exc()}))
+        raise
+
+
+def local_grad_worker(rank, world, port, q, per_rank_batch):
+    """Gradients of each rank WITHOUT synchronisation (to build the expected average)."""
+    _init(rank, world, port)
+    import torch.distributed as dist
+    from ddp_amd.models import VGG11
+    from ddp_amd.engine import CrossEntropyLoss
+    from ddp_amd.data import SyntheticCIFAR10, CPULoader
+    torch.manual_seed(89395)
+    model = VGG11()
+    loader = CPULoader(SyntheticCIFAR10(True, n=per_rank_batch * world), per_rank_batch,
+                       num_replicas=world, rank=rank)
+    x, y = next(iter(loader))
+    CrossEntropyLoss()(model(x), y).backward()
+    g = torch.cat([p.grad.reshape(-1).clone() for p in model.parameters()])
+    dist.destroy_process_group()
+    q.put((rank, {"grads0": g.numpy()}))

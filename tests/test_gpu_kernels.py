@@ -1,0 +1,248 @@
+"""Numerics of every gfx950 kernel against a plain PyTorch fp32 reference of the same op.
+
+Inputs are bf16-representable (the kernels consume bf16 activations/weights), references run in
+fp32 (or fp64) on the same values; tolerances are bf16-output level.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+def rel_err(a, b):
+    return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-12))
+
+
+CONV_CASES = [
+    # N, Cin, H, W, K, R, stride, pad
+    (4, 64, 16, 16, 128, 3, 1, 1),
+    (2, 8, 32, 32, 64, 3, 1, 1),     # VGG layer 0 (padded channels)
+    (8, 512, 2, 2, 512, 3, 1, 1),    # deep tiny-spatial layer (split-K)
+    (4, 64, 15, 15, 32, 3, 2, 1),    # stride 2, odd size
+    (2, 128, 14, 14, 256, 1, 1, 0),  # 1x1
+    (2, 64, 14, 14, 128, 1, 2, 0),   # 1x1 stride 2
+    (2, 8, 32, 32, 64, 7, 2, 3),     # 7x7 stem-like
+]
+
+
+def _conv_setup(N, Cin, H, W, K, R, stride, pad, Creal=None):
+    from ddp_amd.ops.layers import ConvBNActSpec
+    Creal = Creal or Cin
+    conv = torch.nn.Conv2d(Creal, K, R, stride, pad, bias=True).to(DEV)
+    with torch.no_grad():
+        conv.weight.copy_(bf(conv.weight))
+        conv.bias.copy_(torch.randn_like(conv.bias) * 0.1)
+    spec = ConvBNActSpec(conv, None, cin_pad=Cin)
+    spec.maybe_pack()
+    x = bf(torch.randn(N, Creal, H, W, device=DEV))
+    x_nhwc = torch.zeros(N, H, W, Cin, device=DEV, dtype=torch.bfloat16)
+    x_nhwc[..., :Creal] = x.permute(0, 2, 3, 1).to(torch.bfloat16)
+    return conv, spec, x, x_nhwc
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_stats(native_ext, case):
+    from ddp_amd.ops.layers import conv_forward
+    N, Cin, H, W, K, R, stride, pad = case
+    Creal = 3 if Cin == 8 else Cin
+    conv, spec, x, xn = _conv_setup(N, Cin, H, W, K, R, stride, pad, Creal)
+    stats = torch.zeros(2 * K, device=DEV)
+    z = conv_forward(spec, xn, conv.bias, stats)
+    ref = F.conv2d(x, conv.weight, conv.bias, stride, pad).permute(0, 2, 3, 1)
+    assert z.shape == ref.shape
+    assert rel_err(z, ref) < 1e-2
+    zf = z.float().reshape(-1, K)
+    assert torch.allclose(stats[:K], zf.sum(0), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(stats[K:], (zf * zf).sum(0), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("case", [c for c in CONV_CASES if c[1] != 8])
+def test_conv_dgrad(native_ext, case):
+    from ddp_amd.ops.layers import conv_backward
+    N, Cin, H, W, K, R, stride, pad = case
+    conv, spec, x, xn = _conv_setup(N, Cin, H, W, K, R, stride, pad)
+    P = (H + 2 * pad - R) // stride + 1
+    dz = bf(torch.randn(N, K, P, P, device=DEV))
+    dzn = dz.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    dw = torch.zeros_like(conv.weight)
+    dx = conv_backward(spec, xn, dzn, dw, True)
+    xr = x.clone().requires_grad_(True)
+    wr = conv.weight.detach().clone().requires_grad_(True)
+    out = F.conv2d(xr, wr, None, stride, pad)
+    out.backward(dz)
+    assert rel_err(dx.permute(0, 3, 1, 2), xr.grad) < 1e-2
+    assert rel_err(dw, wr.grad) < 1e-2
+
+
+def test_conv_wgrad_padded_layer0(native_ext):
+    from ddp_amd.ops.layers import conv_backward
+    conv, spec, x, xn = _conv_setup(4, 8, 32, 32, 64, 3, 1, 1, Creal=3)
+    dz = bf(torch.randn(4, 64, 32, 32, device=DEV))
+    dw = torch.zeros_like(conv.weight)
+    conv_backward(spec, xn, dz.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16), dw, False)
+    wr = conv.weight.detach().clone().requires_grad_(True)
+    F.conv2d(x, wr, None, 1, 1).backward(dz)
+    assert rel_err(dw, wr.grad) < 1e-2
+
+
+def _bn_ref(z, gamma, beta, eps, relu, pool, res=None):
+    # z: NCHW fp32 (bf16-valued)
+    y = F.batch_norm(z, None, None, gamma, beta, training=True, eps=eps)
+    if res is not None:
+        y = y + res
+    if relu:
+        y = F.relu(y)
+    if pool:
+        y = F.max_pool2d(y, 2, 2)
+    return y
+
+
+@pytest.mark.parametrize("C,H,pool,res", [(64, 8, True, False), (128, 4, False, False),
+                                          (512, 2, True, False), (256, 8, False, True),
+                                          (2048, 2, False, True)])
+def test_bn_act_fwd_bwd(native_ext, C, H, pool, res):
+    from ddp_amd.ops.common import ptr, stream_handle
+    nat = native_ext
+    N = 8
+    z = bf(torch.randn(N, C, H, H, device=DEV) * 2 + 0.5)
+    r = bf(torch.randn(N, C, H, H, device=DEV)) if res else None
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV) * 0.1
+    zn = z.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    rn = r.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16) if res else None
+    zf = zn.float().reshape(-1, C)
+    stats = torch.cat([zf.sum(0), (zf * zf).sum(0)])
+    Ho = H // 2 if pool else H
+    out = torch.empty(N, Ho, Ho, C, device=DEV, dtype=torch.bfloat16)
+    s = stream_handle()
+    nat.bn_act_fwd(N, H, H, C, int(pool), 1, 1e-5, ptr(zn), ptr(rn), ptr(stats), ptr(gamma),
+                   ptr(beta), ptr(out), s)
+    zr = z.clone().requires_grad_(True)
+    gr = gamma.clone().requires_grad_(True)
+    br = beta.clone().requires_grad_(True)
+    rr = r.clone().requires_grad_(True) if res else None
+    ref = _bn_ref(zr, gr, br, 1e-5, True, pool, rr)
+    assert rel_err(out.permute(0, 3, 1, 2), ref) < 1e-2
+    dout = bf(torch.randn_like(ref))
+    ref.backward(dout)
+    doutn = dout.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    sums = torch.empty(2 * C, device=DEV)
+    dz = torch.empty_like(zn)
+    dres = torch.empty_like(zn) if res else None
+    dg = torch.zeros(C, device=DEV)
+    db = torch.zeros(C, device=DEV)
+    dbias = torch.zeros(C, device=DEV)
+    nat.bn_act_bwd(N, H, H, C, int(pool), 1, 1e-5, ptr(zn), ptr(rn), ptr(stats), ptr(gamma),
+                   ptr(beta), ptr(doutn), ptr(sums), ptr(dz), ptr(dres), ptr(dg), ptr(db),
+                   ptr(dbias), s)
+    torch.cuda.synchronize()
+    assert rel_err(dz.permute(0, 3, 1, 2), zr.grad) < 2e-2
+    assert rel_err(dg, gr.grad) < 1e-2
+    assert rel_err(db, br.grad) < 1e-2
+    assert torch.allclose(dbias, zr.grad.sum((0, 2, 3)), atol=5e-2)
+    if res:
+        assert rel_err(dres.permute(0, 3, 1, 2), rr.grad) < 1e-2
+
+
+def test_linear_ce(native_ext):
+    from ddp_amd.ops.layers import linear_small, cross_entropy
+    B, Fi, J = 64, 512, 10
+    lin = torch.nn.Linear(Fi, J).to(DEV)
+    x = bf(torch.randn(B, Fi, device=DEV))
+    y = torch.randint(0, J, (B,), device=DEV)
+    lin.weight.grad = torch.zeros_like(lin.weight)
+    lin.bias.grad = torch.zeros_like(lin.bias)
+    xb = x.to(torch.bfloat16).requires_grad_(True)
+    logits = linear_small(xb, lin)
+    loss = cross_entropy(logits, y)
+    loss.backward()
+    xr = x.clone().requires_grad_(True)
+    wr = lin.weight.detach().clone().requires_grad_(True)
+    brr = lin.bias.detach().clone().requires_grad_(True)
+    lr_ = F.linear(xr, wr, brr)
+    lref = F.cross_entropy(lr_, y)
+    lref.backward()
+    assert rel_err(logits, lr_) < 1e-4
+    assert abs(float(loss) - float(lref)) < 1e-4
+    assert rel_err(xb.grad, xr.grad) < 1e-2
+    assert rel_err(lin.weight.grad, wr.grad) < 1e-4
+    assert rel_err(lin.bias.grad, brr.grad) < 1e-4
+
+
+def test_softmax_ce_bf16_1000(native_ext):
+    from ddp_amd.ops.common import ptr, stream_handle
+    B, J = 32, 1000
+    logits = bf(torch.randn(B, J, device=DEV) * 3)
+    y = torch.randint(0, J, (B,), device=DEV)
+    loss = torch.zeros((), device=DEV)
+    correct = torch.zeros((), dtype=torch.int32, device=DEV)
+    dl = torch.empty(B, J, device=DEV, dtype=torch.bfloat16)
+    native_ext.softmax_ce(ptr(logits.to(torch.bfloat16)), 1, ptr(y), B, J, ptr(loss), ptr(correct),
+                          ptr(dl), 1, stream_handle())
+    torch.cuda.synchronize()
+    lr_ = logits.clone().requires_grad_(True)
+    ref = F.cross_entropy(lr_, y)
+    ref.backward()
+    assert abs(float(loss) - float(ref)) < 1e-3
+    assert int(correct) == int((logits.argmax(1) == y).sum())
+    assert rel_err(dl, lr_.grad) < 1e-2
+
+
+def test_sgd_matches_torch(native_ext):
+    from ddp_amd.optim import FusedSGD
+    torch.manual_seed(0)
+    ps = [torch.nn.Parameter(torch.randn(s, device=DEV)) for s in [(17,), (64, 3, 3, 3), (5, 7)]]
+    ref = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    opt = FusedSGD(ps, lr=0.1, momentum=0.9, weight_decay=1e-4)
+    ropt = torch.optim.SGD(ref, lr=0.1, momentum=0.9, weight_decay=1e-4)
+    for it in range(3):
+        gs = [torch.randn_like(p) for p in ps]
+        opt.zero_grad()
+        for p, g in zip(ps, gs):
+            p.grad.copy_(g)
+        for p, g in zip(ref, gs):
+            p.grad = g.clone()
+        opt.step()
+        ropt.step()
+    for p, r in zip(ps, ref):
+        assert torch.allclose(p, r, rtol=1e-5, atol=1e-6)
+
+
+def test_pack_weights(native_ext):
+    from ddp_amd.ops.layers import ConvBNActSpec
+    conv = torch.nn.Conv2d(3, 64, 3, padding=1).to(DEV)
+    spec = ConvBNActSpec(conv, None, cin_pad=8)
+    spec.maybe_pack()
+    w = conv.weight.detach()
+    exp = torch.zeros(64, 3, 3, 8, device=DEV)
+    exp[..., :3] = w.permute(0, 2, 3, 1)
+    assert torch.equal(spec.wc.float(), exp.to(torch.bfloat16).float())
+    conv2 = torch.nn.Conv2d(64, 128, 3, padding=1).to(DEV)
+    s2 = ConvBNActSpec(conv2, None)
+    s2.maybe_pack()
+    assert torch.equal(s2.wt.float(), conv2.weight.detach().permute(1, 2, 3, 0).to(torch.bfloat16).float())
+
+
+def test_synthetic_and_augment_match_cpu(native_ext):
+    import numpy as np
+    from ddp_amd.data import SyntheticCIFAR10, DeviceLoader, augment_cpu
+    ds = SyntheticCIFAR10(True, n=300)
+    imgs_c, labels_c = ds.cpu_arrays()
+    imgs_g, labels_g = ds.device_arrays(DEV)
+    assert np.array_equal(imgs_g.cpu().numpy(), imgs_c)
+    assert np.array_equal(labels_g.cpu().numpy(), labels_c)
+    loader = DeviceLoader(ds, 50, DEV, num_replicas=2, rank=1, epoch=3)
+    x, y = loader.batch(10, 50)
+    idx = loader.idx[10:60].cpu().numpy()
+    ref = augment_cpu(imgs_c, idx, ds.seed, 3, train=True)
+    got = x[..., :3].permute(0, 3, 1, 2).float().cpu()
+    assert torch.equal(got, ref.to(torch.bfloat16).float())
+    assert torch.all(x[..., 3:] == 0)
+    assert torch.equal(y.cpu(), torch.from_numpy(labels_c[idx]))
