@@ -283,28 +283,53 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
 }
 
 // Split-K finish: fp32 workspace -> (+bias) bf16 output (+ per-channel stats for FWD).
-// One thread per 8 contiguous channels of one row.
+// Thread layout: cg_local = tid % Gb (8 channels each), rows strided; the per-channel sums are
+// reduced in registers, then across the block through LDS, then ONE atomic per channel per block.
+// Grid: x = row blocks, y = channel chunks of Gb groups.
 __global__ __launch_bounds__(256) void splitk_finish_kernel(const float* ws, unsigned short* out,
                                                             const float* bias, float* stats,
                                                             int Mg, int Ng) {
-  const int groups = Ng / 8;
-  const size_t total = (size_t)Mg * groups;
-  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total;
-       t += (size_t)gridDim.x * blockDim.x) {
-    const int row = (int)(t / groups), cg = (int)(t - (size_t)row * groups);
-    const float* src = ws + (size_t)row * Ng + cg * 8;
+  __shared__ float red[2][8][256];
+  const int G = Ng / 8;
+  const int Gb = G < 256 ? G : 256;
+  const int cgl = threadIdx.x % Gb, prow = threadIdx.x / Gb, prows = 256 / Gb;
+  const int cg = blockIdx.y * Gb + cgl;
+  float s[8], ss[8], bv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    s[e] = 0.f;
+    ss[e] = 0.f;
+    bv[e] = (bias && cg < G) ? bias[cg * 8 + e] : 0.f;
+  }
+  const bool active = prow < prows && cg < G;  // Gb need not divide 256 (e.g. 1000 classes)
+  for (int row = blockIdx.x * prows + prow; active && row < Mg; row += gridDim.x * prows) {
+    const float4* src = reinterpret_cast<const float4*>(ws + (size_t)row * Ng + cg * 8);
+    const float4 a = src[0], b = src[1];
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     u16x8 o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float v = src[e] + (bias ? bias[cg * 8 + e] : 0.f);
-      o[e] = f2bf(v);
-      if (stats) {
-        const float r = bf2f(o[e]);
-        atomicAdd(stats + cg * 8 + e, r);
-        atomicAdd(stats + Ng + cg * 8 + e, r * r);
-      }
+      o[e] = f2bf(v[e] + bv[e]);
+      const float r = bf2f(o[e]);
+      s[e] += r;
+      ss[e] += r * r;
     }
     st8(out + (size_t)row * Ng + cg * 8, o);
+  }
+  if (!stats) return;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[0][e][threadIdx.x] = s[e];
+    red[1][e][threadIdx.x] = ss[e];
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < Gb * 16; idx += 256) {
+    const int k = idx / (Gb * 8), rem = idx % (Gb * 8);
+    const int c = rem / 8, e = rem % 8;
+    if (blockIdx.y * Gb + c >= G) continue;
+    float t = 0.f;
+    for (int r = 0; r < prows; ++r) t += red[k][e][r * Gb + c];
+    atomicAdd(stats + k * Ng + (blockIdx.y * Gb + c) * 8 + e, t);
   }
 }
 
@@ -334,9 +359,14 @@ static void launch_cfg(ConvArgs& a, int target_blocks, hipStream_t st) {
   dim3 grid(tiles, 1, splits);
   hipLaunchKernelGGL((conv_igemm_kernel<MODE, BM, BN, BK>), grid, dim3(256), 0, st, a);
   if (MODE != MODE_WGRAD && splits > 1) {
-    const size_t work = (size_t)a.Mg * (a.Ng / 8);
-    const int blocks = (int)std::min<size_t>((work + 255) / 256, (size_t)4096);
-    hipLaunchKernelGGL(splitk_finish_kernel, dim3(blocks), dim3(256), 0, st, a.out_f32, a.out,
+    const int G = a.Ng / 8;
+    const int Gb = G < 256 ? G : 256;
+    const int chunks = (G + Gb - 1) / Gb;
+    const int rows_per_block = 256 / Gb;
+    // ~8 rows per thread keeps the per-block atomics cheap while filling the chip
+    int bx = (a.Mg + rows_per_block * 8 - 1) / (rows_per_block * 8);
+    bx = std::max(1, std::min(bx, 1024 / chunks + 1));
+    hipLaunchKernelGGL(splitk_finish_kernel, dim3(bx, chunks), dim3(256), 0, st, a.out_f32, a.out,
                        MODE == MODE_FWD ? a.bias : nullptr, MODE == MODE_FWD ? a.stats : nullptr,
                        a.Mg, a.Ng);
   }

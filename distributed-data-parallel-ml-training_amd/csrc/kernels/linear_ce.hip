@@ -109,31 +109,43 @@ __global__ __launch_bounds__(256) void linear_dx_kernel(const float* __restrict_
   }
 }
 
-// dW / db: thread per feature column f (all J classes), loop over the batch.
+// dW / db: block = 64 feature columns x one 64-row batch chunk (4 row groups of 16 rows);
+// partial sums reduced through LDS, one atomic per (j, f) per block.
+constexpr int kDwRows = 64;
 __global__ __launch_bounds__(256) void linear_dw_kernel(const float* __restrict__ dlogits,
                                                         const unsigned short* __restrict__ x,
                                                         int B, int F, int J, const float* gscale,
                                                         float* dW, float* db) {
-  const int f = blockIdx.x * 256 + threadIdx.x;
+  __shared__ float red[4][kMaxJ][64];
+  const int fl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int f = blockIdx.x * 64 + fl;
+  const int r0 = blockIdx.y * kDwRows;
+  const int r1 = min(B, r0 + kDwRows);
   const float g = gscale ? *gscale : 1.f;
-  if (f < F) {
-    float acc[kMaxJ];
+  float acc[kMaxJ];
 #pragma unroll
-    for (int j = 0; j < kMaxJ; ++j) acc[j] = 0.f;
-    for (int r = 0; r < B; ++r) {
+  for (int j = 0; j < kMaxJ; ++j) acc[j] = 0.f;
+  if (f < F)
+    for (int r = r0 + rg; r < r1; r += 4) {
       const float xv = bf2f(x[(size_t)r * F + f]);
 #pragma unroll
       for (int j = 0; j < kMaxJ; ++j)
         if (j < J) acc[j] += dlogits[(size_t)r * J + j] * xv;
     }
 #pragma unroll
+  for (int j = 0; j < kMaxJ; ++j) red[rg][j][fl] = acc[j];
+  __syncthreads();
+  if (rg == 0 && f < F) {
+#pragma unroll
     for (int j = 0; j < kMaxJ; ++j)
-      if (j < J) dW[(size_t)j * F + f] += acc[j] * g;
+      if (j < J)
+        atomicAdd(dW + (size_t)j * F + f,
+                  (red[0][j][fl] + red[1][j][fl] + red[2][j][fl] + red[3][j][fl]) * g);
   }
   if (blockIdx.x == 0 && threadIdx.x < J && db) {
     float s = 0.f;
-    for (int r = 0; r < B; ++r) s += dlogits[(size_t)r * J + threadIdx.x];
-    db[threadIdx.x] += s * g;
+    for (int r = r0; r < r1; ++r) s += dlogits[(size_t)r * J + threadIdx.x];
+    atomicAdd(db + threadIdx.x, s * g);
   }
 }
 
@@ -212,7 +224,8 @@ extern "C" int ddp_linear_bwd(const float* dlogits, const void* x, const float* 
   if (dx)
     hipLaunchKernelGGL(linear_dx_kernel, dim3((B + 3) / 4), dim3(256), 0, st, dlogits, W, B, F, J,
                        gscale, (unsigned short*)dx);
-  hipLaunchKernelGGL(linear_dw_kernel, dim3((F + 255) / 256), dim3(256), 0, st, dlogits,
+  hipLaunchKernelGGL(linear_dw_kernel, dim3((F + 63) / 64, (B + kDwRows - 1) / kDwRows), dim3(256),
+                     0, st, dlogits,
                      (const unsigned short*)x, B, F, J, gscale, dW, db);
   return (int)hipGetLastError();
 }

@@ -243,6 +243,7 @@ def test_synthetic_and_augment_match_cpu(native_ext):
     idx = loader.idx[10:60].cpu().numpy()
     ref = augment_cpu(imgs_c, idx, ds.seed, 3, train=True)
     got = x[..., :3].permute(0, 3, 1, 2).float().cpu()
-    assert torch.equal(got, ref.to(torch.bfloat16).float())
+    # fp32 op order differs from numpy: allow one bf16 ulp on rounding ties
+    assert torch.allclose(got, ref.to(torch.bfloat16).float(), rtol=8e-3, atol=1e-2)
     assert torch.all(x[..., 3:] == 0)
     assert torch.equal(y.cpu(), torch.from_numpy(labels_c[idx]))

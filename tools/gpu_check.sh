@@ -1,13 +1,33 @@
 #!/bin/bash
-cd "$GRAFT_REPO_ROOT"
+# GPU-box check: numerics tests, 1-GPU bench, kernel-trace profile.
+# Usage (from the container): gpurun --timeout 900 -- bash tools/gpu_check.sh [tests|bench|prof]...
+cd "$GRAFT_REPO_ROOT" || exit 2
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 500 python -m pytest tests/test_gpu_kernels.py tests/test_gpu_model.py -q -m gpu -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
-rc=$?
-echo "pytest rc=$rc"
-tail -30 gpurun_out/pytest_gpu.log
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after pytest rc=$rc"; exit $rc; fi
-timeout -k 10 240 python bench.py --steps 20 --warmup 5 > gpurun_out/bench1.log 2>&1
-rc=$?
-echo "bench rc=$rc"; tail -20 gpurun_out/bench1.log
-exit $rc
+steps="${@:-tests bench prof}"
+ok_or_stop() {  # continue only after a clean exit or an ordinary test failure
+  local rc=$1 what=$2
+  echo "$what rc=$rc"
+  if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "stopping after $what rc=$rc"; exit "$rc"; fi
+}
+for s in $steps; do
+  case $s in
+    tests)
+      timeout -k 10 600 python -m pytest tests -q -m gpu -p no:cacheprovider -rA > gpurun_out/pytest_gpu.log 2>&1
+      rc=$?; grep -E "passed|failed|error|rel err" gpurun_out/pytest_gpu.log | tail -15; ok_or_stop $rc pytest ;;
+    bench)
+      timeout -k 10 300 python bench.py --steps 40 --warmup 10 > gpurun_out/bench1.log 2>&1
+      rc=$?; tail -3 gpurun_out/bench1.log; ok_or_stop $rc bench ;;
+    bench8w)  # weak-scaling point and eager (no graph) comparison
+      timeout -k 10 300 python bench.py --steps 40 --warmup 10 --no-graph > gpurun_out/bench_eager.log 2>&1
+      rc=$?; tail -1 gpurun_out/bench_eager.log; ok_or_stop $rc bench_eager ;;
+    prof)
+      root="$GRAFT_REPO_ROOT"
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats \
+          --output-format csv -d "$root/gpurun_out/prof" -o vgg11 -- \
+          python3 "$root/bench.py" --steps 20 --warmup 5 > "$root/gpurun_out/prof.log" 2>&1)
+      rc=$?; tail -2 gpurun_out/prof.log; ok_or_stop $rc prof
+      find gpurun_out/prof -name "*kernel_stats.csv" | head -3 ;;
+  esac
+done
+exit 0
