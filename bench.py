@@ -8,8 +8,10 @@
 Config = BASELINE.json: VGG-11 (reference architecture, random init), synthetic CIFAR-10-shaped
 data (3x32x32, 10 classes, on-device crop/flip/normalise), bf16 compute with fp32 master
 weights/grads, SGD(0.1, 0.9, 1e-4), part-3 strategy (bucketed backward-overlapped DDP on RCCL).
-Default protocol is the reference's: GLOBAL batch 256 split int(256/N) per GPU (strong scaling);
-``--per-gpu-batch B`` switches to weak scaling. Every timed step is a full training step
+Default protocol: each GPU trains on the reference's batch of 256 images per step (weak scaling:
+per-GPU work is fixed as N grows; at N=1 this is exactly the reference's global batch 256).
+``--global-batch B`` instead splits a fixed global batch int(B/N) per GPU (strong scaling, the
+reference's Table-1 protocol at 4 nodes). Every timed step is a full training step
 (augment + forward + backward + gradient all-reduce + optimizer), captured in one hipGraph.
 W untimed warm-up steps, then EXACTLY K timed steps bracketed by barrier + synchronize; the
 elapsed time is the MAX over ranks; rank 0 prints one JSON line.
@@ -32,8 +34,9 @@ def parse():
     p.add_argument("--steps", type=int, default=40)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--model", default="vgg11")
-    p.add_argument("--global-batch", type=int, default=256)
-    p.add_argument("--per-gpu-batch", type=int, default=None, help="weak scaling")
+    p.add_argument("--global-batch", type=int, default=None, help="strong scaling")
+    p.add_argument("--per-gpu-batch", type=int, default=None,
+                   help="weak scaling (default 256 for VGG, 64 for ResNet-50)")
     p.add_argument("--strategy", default="ddp", choices=["ddp", "allreduce", "gather_scatter"])
     p.add_argument("--bucket-mb", type=float, default=25.0)
     p.add_argument("--first-bucket-mb", type=float, default=1.0)
@@ -68,10 +71,11 @@ def main():
     comm = RcclCommunicator(rank, world, local_rank)
 
     seed_everything(ddp_amd.SEED)
-    if args.per_gpu_batch:
-        B, scaling = args.per_gpu_batch, "weak"
-    else:
+    if args.global_batch:
         B, scaling = int(args.global_batch / world), "strong"
+    else:
+        B = args.per_gpu_batch or (64 if args.model.startswith("resnet") else 256)
+        scaling = "weak"
     global_batch = B * world
     resnet = args.model.startswith("resnet")
     ds = (SyntheticImageNet(True, n=args.train_size) if resnet

@@ -43,32 +43,59 @@ PYBIND11_MODULE(_native, m) {
   m.doc() = "ddp_amd native extension: gfx950 HIP kernels + RCCL runtime";
 
   // geometry tuple: (N,H,W,C,K,R,S,stride,pad,P,Q,Creal)
+  // ws / ws_elems: fp32 split-K slab workspace (0 disables split-K); splits 0 = automatic
   m.def("conv_fwd", [](py::tuple g, uintptr_t x, uintptr_t wc, uintptr_t bias, uintptr_t y,
-                       uintptr_t stats, uintptr_t ws, int splits, uintptr_t st) {
+                       uintptr_t stats, uintptr_t ws, size_t ws_elems, int splits, uintptr_t st) {
     auto c = geom(g);
     check(ddp_conv_fwd(&c, P<void>(x), P<void>(wc), P<float>(bias), P<void>(y), P<float>(stats),
-                       P<float>(ws), splits, S(st)), "conv_fwd");
+                       P<float>(ws), ws_elems, splits, S(st)), "conv_fwd");
   });
   m.def("conv_dgrad", [](py::tuple g, uintptr_t dy, uintptr_t wt, uintptr_t dx, uintptr_t ws,
-                         int splits, uintptr_t st) {
+                         size_t ws_elems, int splits, uintptr_t st) {
     auto c = geom(g);
-    check(ddp_conv_dgrad(&c, P<void>(dy), P<void>(wt), P<void>(dx), P<float>(ws), splits, S(st)),
-          "conv_dgrad");
+    check(ddp_conv_dgrad(&c, P<void>(dy), P<void>(wt), P<void>(dx), P<float>(ws), ws_elems,
+                         splits, S(st)), "conv_dgrad");
   });
-  m.def("conv_wgrad", [](py::tuple g, uintptr_t dy, uintptr_t x, uintptr_t dw, int splits,
-                         uintptr_t st) {
+  m.def("conv_wgrad", [](py::tuple g, uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws,
+                         size_t ws_elems, int splits, uintptr_t st) {
     auto c = geom(g);
-    check(ddp_conv_wgrad(&c, P<void>(dy), P<void>(x), P<float>(dw), splits, S(st)), "conv_wgrad");
+    check(ddp_conv_wgrad(&c, P<void>(dy), P<void>(x), P<float>(dw), P<float>(ws), ws_elems,
+                         splits, S(st)), "conv_wgrad");
   });
 
   m.def("bn_act_fwd", [](int N, int H, int W, int C, int pool, int relu, float eps, uintptr_t z,
                          uintptr_t res, uintptr_t stats, uintptr_t gamma, uintptr_t beta,
-                         uintptr_t out, uintptr_t st) {
+                         uintptr_t out, uintptr_t st, uintptr_t running_mean,
+                         uintptr_t running_var, float momentum, int use_running) {
     ddp_amd::BnArgs a{};
     a.N = N; a.H = H; a.W = W; a.C = C; a.pool = pool; a.relu = relu; a.eps = eps;
     a.z = P<unsigned short>(z); a.res = P<unsigned short>(res); a.stats = P<float>(stats);
     a.gamma = P<float>(gamma); a.beta = P<float>(beta); a.out = P<unsigned short>(out);
+    a.running_mean = P<float>(running_mean); a.running_var = P<float>(running_var);
+    a.momentum = momentum; a.use_running = use_running;
     check(ddp_bn_act_fwd(&a, S(st)), "bn_act_fwd");
+  }, py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("pool"), py::arg("relu"),
+     py::arg("eps"), py::arg("z"), py::arg("res"), py::arg("stats"), py::arg("gamma"),
+     py::arg("beta"), py::arg("out"), py::arg("stream"), py::arg("running_mean") = 0,
+     py::arg("running_var") = 0, py::arg("momentum") = 0.1f, py::arg("use_running") = 0);
+  m.def("maxpool_fwd", [](uintptr_t x, int N, int H, int W, int C, int KH, int KW, int stride,
+                          int pad, int Ho, int Wo, uintptr_t y, uintptr_t idx, uintptr_t st) {
+    check(ddp_maxpool_fwd(P<void>(x), N, H, W, C, KH, KW, stride, pad, Ho, Wo, P<void>(y),
+                          P<void>(idx), S(st)), "maxpool_fwd");
+  });
+  m.def("maxpool_bwd", [](uintptr_t dy, uintptr_t idx, int N, int H, int W, int C, int KH, int KW,
+                          int stride, int pad, int Ho, int Wo, uintptr_t dx, uintptr_t st) {
+    check(ddp_maxpool_bwd(P<void>(dy), P<void>(idx), N, H, W, C, KH, KW, stride, pad, Ho, Wo,
+                          P<void>(dx), S(st)), "maxpool_bwd");
+  });
+  m.def("avgpool_fwd", [](uintptr_t x, int N, int HW, int C, uintptr_t y, uintptr_t st) {
+    check(ddp_avgpool_fwd(P<void>(x), N, HW, C, P<void>(y), S(st)), "avgpool_fwd");
+  });
+  m.def("avgpool_bwd", [](uintptr_t dy, int N, int HW, int C, uintptr_t dx, uintptr_t st) {
+    check(ddp_avgpool_bwd(P<void>(dy), N, HW, C, P<void>(dx), S(st)), "avgpool_bwd");
+  });
+  m.def("colsum", [](uintptr_t dl, int B, int J, uintptr_t db, uintptr_t st) {
+    check(ddp_colsum(P<void>(dl), B, J, P<float>(db), S(st)), "colsum");
   });
   m.def("bn_act_bwd", [](int N, int H, int W, int C, int pool, int relu, float eps, uintptr_t z,
                          uintptr_t res, uintptr_t stats, uintptr_t gamma, uintptr_t beta,
@@ -122,6 +149,17 @@ PYBIND11_MODULE(_native, m) {
       d.push_back(x);
     }
     check(ddp_pack_conv_weights(d.data(), (int)d.size(), S(st)), "pack_conv_weights");
+  });
+  m.def("sgd_pack", [](uintptr_t items, int n_items, uintptr_t descs, uintptr_t p, uintptr_t g,
+                       uintptr_t buf, float lr, float momentum, float wd, float grad_scale,
+                       int nesterov, uintptr_t st) {
+    check(ddp_sgd_pack(P<void>(items), n_items, P<long long>(descs), P<float>(p), P<float>(g),
+                       P<float>(buf), lr, momentum, wd, grad_scale, nesterov, S(st)), "sgd_pack");
+  });
+  m.def("sgd_tile_dims", [](int RS) {
+    int tk, tc;
+    ddp_sgd_tile_dims(RS, &tk, &tc);
+    return std::make_pair(tk, tc);
   });
   m.def("counter_add", [](uintptr_t c, int delta, uintptr_t st) {
     check(ddp_counter_add(P<int>(c), delta, S(st)), "counter_add");

@@ -7,6 +7,10 @@
 
 namespace ddp_amd {
 
+// BatchNorm statistics are accumulated into kStatRep replicas [rep][2][C] (sum, sum of squares)
+// to spread float-atomic contention over many addresses; consumers sum the replicas.
+constexpr int kStatRep = 16;
+
 struct ConvGeom {
   int N, H, W, C;     // input (NHWC, C % 8 == 0)
   int K;              // output channels
@@ -33,6 +37,10 @@ struct BnArgs {
   float* dgamma;                // grad arena slices (accumulated)
   float* dbeta;
   float* dbias;                 // conv bias grad (optional)
+  float* running_mean;          // optional (track_running_stats=True): updated in training fwd
+  float* running_var;
+  float momentum;
+  int use_running;              // eval with running statistics instead of batch statistics
 };
 
 struct PackDesc {
@@ -58,11 +66,11 @@ struct AugArgs {
 
 extern "C" {
 int ddp_conv_fwd(const ddp_amd::ConvGeom* g, const void* x, const void* wc, const float* bias,
-                 void* y, float* stats, float* ws, int splits, hipStream_t st);
+                 void* y, float* stats, float* ws, size_t ws_elems, int splits, hipStream_t st);
 int ddp_conv_dgrad(const ddp_amd::ConvGeom* g, const void* dy, const void* wt, void* dx,
-                   float* ws, int splits, hipStream_t st);
+                   float* ws, size_t ws_elems, int splits, hipStream_t st);
 int ddp_conv_wgrad(const ddp_amd::ConvGeom* g, const void* dy, const void* x, float* dw,
-                   int splits, hipStream_t st);
+                   float* ws, size_t ws_elems, int splits, hipStream_t st);
 int ddp_bn_act_fwd(const ddp_amd::BnArgs* a, hipStream_t st);
 int ddp_bn_act_bwd(const ddp_amd::BnArgs* a, hipStream_t st);
 int ddp_linear_ce_fwd(const void* x, const float* W, const float* b, const long long* labels,
@@ -76,12 +84,23 @@ int ddp_softmax_ce(const void* logits, int logits_bf16, const long long* labels,
 int ddp_sgd(float* p, const float* g, float* buf, size_t n, float lr, float momentum, float wd,
             float grad_scale, int nesterov, hipStream_t st);
 int ddp_pack_conv_weights(const ddp_amd::PackDesc* descs, int n, hipStream_t st);
+int ddp_sgd_pack(const void* items, int n_items, const long long* descs, float* p, const float* g,
+                 float* buf, float lr, float momentum, float wd, float grad_scale, int nesterov,
+                 hipStream_t st);
+void ddp_sgd_tile_dims(int RS, int* TK, int* TC);
 int ddp_counter_add(int* c, int delta, hipStream_t st);
 int ddp_synth_generate(unsigned char* images, int* labels, int n, int pix_per_img,
                        unsigned int seed, int classes, hipStream_t st);
 int ddp_augment(const ddp_amd::AugArgs* a, hipStream_t st);
 int ddp_nchw_to_nhwc(const float* x, int N, int C, int H, int W, int Cp, void* out,
                      hipStream_t st);
+int ddp_maxpool_fwd(const void* x, int N, int H, int W, int C, int KH, int KW, int stride,
+                    int pad, int Ho, int Wo, void* y, void* idx, hipStream_t st);
+int ddp_maxpool_bwd(const void* dy, const void* idx, int N, int H, int W, int C, int KH, int KW,
+                    int stride, int pad, int Ho, int Wo, void* dx, hipStream_t st);
+int ddp_avgpool_fwd(const void* x, int N, int HW, int C, void* y, hipStream_t st);
+int ddp_avgpool_bwd(const void* dy, int N, int HW, int C, void* dx, hipStream_t st);
+int ddp_colsum(const void* dl, int B, int J, float* db, hipStream_t st);
 int ddp_mean_ws(const float* in, size_t n, int ws, float* out, hipStream_t st);
 int ddp_scale(float* x, size_t n, float s, hipStream_t st);
 }

@@ -20,12 +20,38 @@ namespace ddp_amd {
 
 __device__ __forceinline__ void bn_coeffs(const BnArgs& a, int c0, float* scale, float* shift,
                                           float* mean, float* invstd) {
+  if (a.use_running) {  // eval mode of track_running_stats=True BatchNorm
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = c0 + e;
+      const float mu = a.running_mean[c];
+      const float is = rsqrtf(a.running_var[c] + a.eps);
+      const float sc = a.gamma[c] * is;
+      scale[e] = sc;
+      shift[e] = a.beta[c] - mu * sc;
+      mean[e] = mu;
+      invstd[e] = is;
+    }
+    return;
+  }
   const float inv_m = 1.f / (float)(a.N * a.H * a.W);
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  for (int r = 0; r < kStatRep; ++r) {  // sum the contention-spreading replicas
+    const float4* p1 = reinterpret_cast<const float4*>(a.stats + r * 2 * a.C + c0);
+    const float4* p2 = reinterpret_cast<const float4*>(a.stats + r * 2 * a.C + a.C + c0);
+    const float4 x0 = p1[0], x1 = p1[1], y0 = p2[0], y1 = p2[1];
+    s1[0] += x0.x; s1[1] += x0.y; s1[2] += x0.z; s1[3] += x0.w;
+    s1[4] += x1.x; s1[5] += x1.y; s1[6] += x1.z; s1[7] += x1.w;
+    s2[0] += y0.x; s2[1] += y0.y; s2[2] += y0.z; s2[3] += y0.w;
+    s2[4] += y1.x; s2[5] += y1.y; s2[6] += y1.z; s2[7] += y1.w;
+  }
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int c = c0 + e;
-    const float mu = a.stats[c] * inv_m;
-    const float var = fmaxf(a.stats[a.C + c] * inv_m - mu * mu, 0.f);
+    const float mu = s1[e] * inv_m;
+    const float var = fmaxf(s2[e] * inv_m - mu * mu, 0.f);
     const float is = rsqrtf(var + a.eps);
     const float sc = a.gamma[c] * is;
     scale[e] = sc;
@@ -35,11 +61,60 @@ __device__ __forceinline__ void bn_coeffs(const BnArgs& a, int c0, float* scale,
   }
 }
 
+// Block-cooperative per-channel coefficients for channels [c_begin, c_begin + n): the 16
+// statistics replicas are summed ONCE per channel per block (not once per thread) into LDS.
+__device__ __forceinline__ void block_coeffs(const BnArgs& a, int c_begin, int n, float* l_sc,
+                                             float* l_sh, float* l_mu, float* l_is) {
+  const float inv_m = 1.f / (float)(a.N * a.H * a.W);
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int c = c_begin + i;
+    float mu, is;
+    if (a.use_running) {
+      mu = a.running_mean[c];
+      is = rsqrtf(a.running_var[c] + a.eps);
+    } else {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int r = 0; r < kStatRep; ++r) {
+        s1 += a.stats[r * 2 * a.C + c];
+        s2 += a.stats[r * 2 * a.C + a.C + c];
+      }
+      mu = s1 * inv_m;
+      is = rsqrtf(fmaxf(s2 * inv_m - mu * mu, 0.f) + a.eps);
+    }
+    const float sc = a.gamma[c] * is;
+    l_sc[i] = sc;
+    l_sh[i] = a.beta[c] - mu * sc;
+    if (l_mu) l_mu[i] = mu;
+    if (l_is) l_is[i] = is;
+  }
+  __syncthreads();
+}
+
 // ------------------------------- forward -------------------------------
 __global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnArgs a) {
   const int G = a.C / 8;
   const int Ho = a.pool ? a.H / 2 : a.H, Wo = a.pool ? a.W / 2 : a.W;
   const size_t total = (size_t)a.N * Ho * Wo * G;
+  // running statistics (track_running_stats=True, training): block 0 updates every channel
+  if (a.running_mean && !a.use_running && blockIdx.x == 0) {
+    const float M = (float)(a.N * a.H * a.W);
+    for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+      float s1 = 0.f, s2 = 0.f;
+      for (int r = 0; r < kStatRep; ++r) {
+        s1 += a.stats[r * 2 * a.C + c];
+        s2 += a.stats[r * 2 * a.C + a.C + c];
+      }
+      const float mu = s1 / M;
+      const float var = fmaxf(s2 / M - mu * mu, 0.f);
+      const float unbiased = M > 1.f ? var * M / (M - 1.f) : var;
+      a.running_mean[c] = (1.f - a.momentum) * a.running_mean[c] + a.momentum * mu;
+      a.running_var[c] = (1.f - a.momentum) * a.running_var[c] + a.momentum * unbiased;
+    }
+  }
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  block_coeffs(a, 0, a.C, lds, lds + a.C, nullptr, nullptr);
+  float sc[8], sh[8];
   for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total;
        t += (size_t)gridDim.x * blockDim.x) {
     const int cg = (int)(t % G);
@@ -47,8 +122,11 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnArgs a) {
     const int wo = (int)(pix % Wo);
     const int ho = (int)((pix / Wo) % Ho);
     const int n = (int)(pix / ((size_t)Wo * Ho));
-    float sc[8], sh[8], mu[8], is[8];
-    bn_coeffs(a, cg * 8, sc, sh, mu, is);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sc[e] = lds[cg * 8 + e];
+      sh[e] = lds[a.C + cg * 8 + e];
+    }
     u16x8 o;
     if (!a.pool) {
       const size_t off = (((size_t)n * a.H + ho) * a.W + wo) * a.C + cg * 8;
@@ -175,9 +253,22 @@ __device__ __forceinline__ void block_reduce_atomic(float (&v)[NV][8], int Gb, i
 }
 
 // Grid: x = blocks over pixels, y = channel chunks of (at most) 256 groups.
+// Per-thread copy of the block's LDS coefficient tables for its 8 channels.
+__device__ __forceinline__ void load_coeffs(const float* lds, int nch, int cl0, float* sc,
+                                            float* sh, float* mu, float* is) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = lds[cl0 + e];
+    sh[e] = lds[nch + cl0 + e];
+    mu[e] = lds[2 * nch + cl0 + e];
+    is[e] = lds[3 * nch + cl0 + e];
+  }
+}
+
 template <bool POOL>
 __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
   __shared__ float red[8 * 256];
+  extern __shared__ __attribute__((aligned(16))) float lds[];
   const int G = a.C / 8;
   const int Gb = G < 256 ? G : 256;
   const int Ho = POOL ? a.H / 2 : a.H, Wo = POOL ? a.W / 2 : a.W;
@@ -185,8 +276,10 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
   const int cg_base = blockIdx.y * Gb;
   const int cgl = threadIdx.x % Gb;
   const int prow = threadIdx.x / Gb, prows = 256 / Gb;
+  const int nch = Gb * 8;
+  block_coeffs(a, cg_base * 8, nch, lds, lds + nch, lds + 2 * nch, lds + 3 * nch);
   float sc[8], sh[8], mu[8], is[8];
-  bn_coeffs(a, (cg_base + cgl) * 8, sc, sh, mu, is);
+  load_coeffs(lds, nch, cgl * 8, sc, sh, mu, is);
   float acc[2][8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { acc[0][e] = 0.f; acc[1][e] = 0.f; }
@@ -211,6 +304,7 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
 template <bool POOL>
 __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(BnArgs a) {
   __shared__ float red[8 * 256];
+  extern __shared__ __attribute__((aligned(16))) float lds[];
   const int G = a.C / 8;
   const int Gb = G < 256 ? G : 256;
   const int Ho = POOL ? a.H / 2 : a.H, Wo = POOL ? a.W / 2 : a.W;
@@ -221,7 +315,9 @@ __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(BnArgs a) {
   const float inv_m = 1.f / (float)(a.N * a.H * a.W);
   float sc[8], sh[8], mu[8], is[8], k1[8], k2[8], gi[8];
   const int c0 = (cg_base + cgl) * 8;
-  bn_coeffs(a, c0, sc, sh, mu, is);
+  const int nch = Gb * 8;
+  block_coeffs(a, cg_base * 8, nch, lds, lds + nch, lds + 2 * nch, lds + 3 * nch);
+  load_coeffs(lds, nch, cgl * 8, sc, sh, mu, is);
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     k1[e] = a.sums[c0 + e] * inv_m;
@@ -280,7 +376,10 @@ extern "C" int ddp_bn_act_fwd(const BnArgs* args, hipStream_t st) {
   BnArgs a = *args;
   const int Ho = a.pool ? a.H / 2 : a.H, Wo = a.pool ? a.W / 2 : a.W;
   const size_t items = (size_t)a.N * Ho * Wo * (a.C / 8);
-  hipLaunchKernelGGL(bn_act_fwd_kernel, dim3(grid_for(items, 8192)), dim3(256), 0, st, a);
+  if (a.C % 8) return -1;
+  // each block builds the [scale|shift] table of all C channels in LDS, then streams items
+  hipLaunchKernelGGL(bn_act_fwd_kernel, dim3(grid_for(items / 4, 1024)), dim3(256),
+                     2 * a.C * sizeof(float), st, a);
   return (int)hipGetLastError();
 }
 
@@ -296,16 +395,17 @@ extern "C" int ddp_bn_act_bwd(const BnArgs* args, hipStream_t st) {
   const size_t rows_per_block = 256 / Gb;
   // enough blocks to fill the chip, but each thread still loops over several pixels
   size_t bx = (npix + rows_per_block * 4 - 1) / (rows_per_block * 4);
-  const size_t cap = (size_t)(2048 / chunks > 0 ? 2048 / chunks : 1);
+  const size_t cap = (size_t)(1024 / chunks > 0 ? 1024 / chunks : 1);
+  const size_t lds = 4 * (size_t)Gb * 8 * sizeof(float);
   if (bx > cap) bx = cap;
   if (bx < 1) bx = 1;
-  (void)hipMemsetAsync(a.sums, 0, sizeof(float) * 2 * a.C, st);
+  // a.sums must be zero on entry (the caller's per-step scratch is zeroed once per forward)
   if (a.pool) {
-    hipLaunchKernelGGL(bn_act_bwd_reduce_kernel<true>, dim3((unsigned)bx, chunks), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(bn_act_bwd_apply_kernel<true>, dim3((unsigned)bx, chunks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(bn_act_bwd_reduce_kernel<true>, dim3((unsigned)bx, chunks), dim3(256), lds, st, a);
+    hipLaunchKernelGGL(bn_act_bwd_apply_kernel<true>, dim3((unsigned)bx, chunks), dim3(256), lds, st, a);
   } else {
-    hipLaunchKernelGGL(bn_act_bwd_reduce_kernel<false>, dim3((unsigned)bx, chunks), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(bn_act_bwd_apply_kernel<false>, dim3((unsigned)bx, chunks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(bn_act_bwd_reduce_kernel<false>, dim3((unsigned)bx, chunks), dim3(256), lds, st, a);
+    hipLaunchKernelGGL(bn_act_bwd_apply_kernel<false>, dim3((unsigned)bx, chunks), dim3(256), lds, st, a);
   }
   return (int)hipGetLastError();
 }

@@ -1,22 +1,35 @@
 // Implicit-GEMM convolution for gfx950: forward, backward-data and backward-weight on bf16
-// MFMA (v_mfma_f32_16x16x32_bf16) with fp32 accumulation, LDS-tiled, register-staged
-// prefetch, optional split-K, XCD-aware tile order.
+// MFMA (v_mfma_f32_16x16x32_bf16) with fp32 accumulation.
 //
 // Reference parity: replaces the ATen/oneDNN Conv2d fwd/bwd the reference triggers from
-// part1/model.py:18-23 (3x3 s1 p1 + bias) — see SURVEY.md §2.B N1 and §2.D for shapes.
-// Also serves ResNet-50's 1x1 / 3x3 / 7x7, stride 1/2 convolutions.
+// part1/model.py:18-23 (3x3 s1 p1 + bias) — SURVEY.md §2.B N1, shapes in §2.D. Also serves
+// ResNet-50's 1x1 / 3x3 / 7x7, stride 1/2 convolutions and the 2048->1000 classifier (1x1 conv).
 //
-// Layouts (all NHWC, channels innermost, C % 8 == 0 — layer 0 is zero-padded 3 -> 8):
+// Layouts (NHWC, channels innermost, C % 8 == 0 — layer 0 is zero-padded 3 -> 8):
 //   x  [N][H][W][C]      bf16  activations
 //   y  [N][P][Q][K]      bf16  conv output (pre-BN)
 //   Wc [K][R][S][C]      bf16  forward weight copy   (GEMM B operand, k-contiguous)
 //   Wt [C][R][S][K]      bf16  dgrad weight copy     (GEMM B operand, k-contiguous)
-//   dW [K][Creal][R][S]  fp32  PyTorch-layout weight gradient (accumulated, atomics)
+//   dW [K][Creal][R][S]  fp32  PyTorch-layout weight gradient (accumulated)
 //
 // GEMM views (rows x cols, reduction):
-//   FWD   : M=N*P*Q, N=K,      red=R*S*C   A=im2col(x)  B=Wc
-//   DGRAD : M=N*H*W, N=C,      red=R*S*K   A=col2im-gather(dy) B=Wt
-//   WGRAD : M=K,     N=R*S*C,  red=N*P*Q   A=dy^T       B=im2col(x)^T  (transposed in LDS)
+//   FWD   : M=N*P*Q, N=K,      red=R*S*C   A=im2col(x)          B=Wc
+//   DGRAD : M=N*H*W, N=C,      red=R*S*K   A=col2im-gather(dy)  B=Wt
+//   WGRAD : M=K,     N=R*S*C,  red=N*P*Q   A=dy^T               B=im2col(x)^T
+//
+// Kernel structure (256 threads = 4 waves in 2x2, BK = 64):
+//   * operands are gathered global->registers (implicit im2col with zero fill), written to a
+//     double-buffered LDS tile AFTER the MFMA phase that overlaps their flight, one barrier per
+//     k-step (cdna_hip_programming.md §5.5 T14 / Guideline 15);
+//   * FWD/DGRAD tiles are [row][k] with the 16-B chunk index XOR-swizzled by (row>>1)&7, read
+//     by ds_read_b128 conflict-free (T2);
+//   * WGRAD tiles keep the global order [m][channel] (m = the reduction index) and the MFMA
+//     fragments are read with ds_read_b64_tr_b16 (gfx950 transposing LDS read, T10), chunk
+//     XOR-swizzled by m so both 16-lane groups of a half-wave hit disjoint banks;
+//   * XCD-aware bijective tile order (T1); split-K writes plain fp32 slabs [split][M][N] that a
+//     finish kernel reduces in a fixed order (no float atomics on the GEMM output);
+//   * FWD epilogue adds the bias, rounds to bf16 and accumulates the per-channel BatchNorm
+//     statistics of the rounded output (sum, sum of squares) — BN needs no separate stats pass.
 #include "common.h"
 #include "api.h"
 #include <algorithm>
@@ -25,95 +38,139 @@ namespace ddp_amd {
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
 
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef short short8_t __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
 struct ConvArgs {
   ConvGeom g;
   const unsigned short* a;   // FWD: x, DGRAD: dy, WGRAD: dy
   const unsigned short* b;   // FWD: Wc, DGRAD: Wt, WGRAD: x
-  unsigned short* out;       // FWD: y, DGRAD: dx (bf16), unused for WGRAD
-  float* out_f32;            // split-K workspace (FWD/DGRAD) or dW (WGRAD)
+  unsigned short* out;       // FWD: y, DGRAD: dx (bf16)
+  float* dw;                 // WGRAD output (PyTorch layout, accumulated)
+  float* ws;                 // split-K slabs [splits][Mg][Ng]
   const float* bias;         // FWD only (may be null)
-  float* stats;              // FWD only: [2*K] sum / sum-of-squares of the bf16 output (may be null)
+  float* stats;              // FWD only: [2*Ng] sum / sum-of-squares of the bf16 output
   int Mg, Ng, Kg;            // GEMM dims
-  int splits;                // split-K factor (gridDim.z)
+  int splits;
   int ksteps_per_split;
 };
 
-template <int MODE, int BM, int BN, int BK>
-struct TileLoader {
-  // chunks of 8 bf16 (16 B) per thread per operand tile
-  static constexpr int CA = BM * BK / 8 / 256;
-  static constexpr int CB = BN * BK / 8 / 256;
-  static_assert(CA >= 1 && CB >= 1, "tile too small for 256 threads");
+// ------------------------------------------------------------------ operand gathers
+// Index math is hoisted: the pixel decomposition of a GEMM row is computed once per kernel
+// (RowInfo), the (r, s, c) decomposition of the reduction index once per k-step, and runtime
+// divisions inside the k-loop use a float-reciprocal divmod (exact for x < 2^23).
+__device__ __forceinline__ int fdiv(int x, int d, float inv) {
+  int q = (int)((float)x * inv);
+  const int r = x - q * d;
+  q += (r < 0) ? -1 : (r >= d ? 1 : 0);
+  return q;
+}
+
+struct RowInfo {
+  int base;    // element offset of the row's image (FWD: n*H*W*C, DGRAD: n*P*Q*K)
+  int h0, w0;  // FWD: p*stride-pad, q*stride-pad ; DGRAD: h+pad, w+pad ; invalid row: h0 < -2^20
 };
 
-// Gather one 16-byte chunk of the A operand.
-//   FWD/DGRAD: row = GEMM row (pixel), kk = reduction index (multiple of 8)
-//   WGRAD    : row = output channel group start (multiple of 8), kk = pixel index m
 template <int MODE>
-__device__ __forceinline__ u16x8 load_a(const ConvArgs& A, int row, int kk) {
+__device__ __forceinline__ RowInfo row_info(const ConvArgs& A, int row) {
   const ConvGeom& g = A.g;
-  u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+  RowInfo ri{0, -(1 << 24), 0};
+  if (row >= A.Mg) return ri;
   if (MODE == MODE_FWD) {
-    if (row >= A.Mg || kk >= A.Kg) return z;
     const int pq = g.P * g.Q;
     const int n = row / pq, rem = row - n * pq;
     const int p = rem / g.Q, q = rem - p * g.Q;
-    const int rs = kk / g.C, c = kk - rs * g.C;
-    const int r = rs / g.S, s = rs - r * g.S;
-    const int h = p * g.stride - g.pad + r, w = q * g.stride - g.pad + s;
-    if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) return z;
-    return ld8(A.a + ((size_t)(n * g.H + h) * g.W + w) * g.C + c);
-  } else if (MODE == MODE_DGRAD) {
-    if (row >= A.Mg || kk >= A.Kg) return z;
+    ri.base = n * g.H * g.W * g.C;
+    ri.h0 = p * g.stride - g.pad;
+    ri.w0 = q * g.stride - g.pad;
+  } else {
     const int hw = g.H * g.W;
     const int n = row / hw, rem = row - n * hw;
     const int h = rem / g.W, w = rem - h * g.W;
-    const int rs = kk / g.K, ko = kk - rs * g.K;
-    const int r = rs / g.S, s = rs - r * g.S;
-    int ph = h + g.pad - r, pw = w + g.pad - s;
-    if (ph < 0 || pw < 0) return z;
-    if (g.stride != 1) {
-      if ((ph % g.stride) | (pw % g.stride)) return z;
-      ph /= g.stride; pw /= g.stride;
-    }
-    if (ph >= g.P || pw >= g.Q) return z;
-    return ld8(A.a + ((size_t)(n * g.P + ph) * g.Q + pw) * g.K + ko);
-  } else {  // WGRAD: A'[kout][m] = dy[m][kout]  (row = kout group start, kk = m)
-    if (row >= A.Mg || kk >= A.Kg) return z;
-    return ld8(A.a + (size_t)kk * g.K + row);
+    ri.base = n * g.P * g.Q * g.K;
+    ri.h0 = h + g.pad;
+    ri.w0 = w + g.pad;
   }
+  return ri;
+}
+
+struct KInfo {
+  int r, s, c;  // kernel tap and channel of the chunk's first reduction element
+  bool ok;
+};
+
+template <int MODE>
+__device__ __forceinline__ KInfo k_info(const ConvArgs& A, int kk, float invC, float invS) {
+  const ConvGeom& g = A.g;
+  KInfo k;
+  k.ok = kk < A.Kg;
+  const int cdim = MODE == MODE_FWD ? g.C : g.K;
+  const int rs = fdiv(kk, cdim, invC);
+  k.c = kk - rs * cdim;
+  k.r = fdiv(rs, g.S, invS);
+  k.s = rs - k.r * g.S;
+  return k;
 }
 
 template <int MODE>
-__device__ __forceinline__ u16x8 load_b(const ConvArgs& A, int col, int kk) {
+__device__ __forceinline__ u16x8 gather_a(const ConvArgs& A, const RowInfo& ri, const KInfo& k) {
   const ConvGeom& g = A.g;
   u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (MODE == MODE_FWD || MODE == MODE_DGRAD) {
-    if (col >= A.Ng || kk >= A.Kg) return z;
-    return ld8(A.b + (size_t)col * A.Kg + kk);
-  } else {  // WGRAD: B'[j=(r,s,c)][m] = x[n][p*st-pad+r][q*st-pad+s][c]  (col = j group start, kk = m)
-    if (col >= A.Ng || kk >= A.Kg) return z;
-    const int pq = g.P * g.Q;
-    const int n = kk / pq, rem = kk - n * pq;
-    const int p = rem / g.Q, q = rem - p * g.Q;
-    const int rs = col / g.C, c = col - rs * g.C;
-    const int r = rs / g.S, s = rs - r * g.S;
-    const int h = p * g.stride - g.pad + r, w = q * g.stride - g.pad + s;
+  if (!k.ok) return z;
+  if (MODE == MODE_FWD) {
+    const int h = ri.h0 + k.r, w = ri.w0 + k.s;
     if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) return z;
-    return ld8(A.b + ((size_t)(n * g.H + h) * g.W + w) * g.C + c);
+    return ld8(A.a + ri.base + (h * g.W + w) * g.C + k.c);
+  } else {
+    int ph = ri.h0 - k.r, pw = ri.w0 - k.s;
+    if (ph < 0 || pw < 0) return z;
+    if (g.stride != 1) {
+      if ((ph % g.stride) | (pw % g.stride)) return z;
+      ph /= g.stride;
+      pw /= g.stride;
+    }
+    if (ph >= g.P || pw >= g.Q) return z;
+    return ld8(A.a + ri.base + (ph * g.Q + pw) * g.K + k.c);
   }
 }
 
-template <int MODE, int BM, int BN, int BK>
+// WGRAD B' chunk: x at pixel-index m for the 8 consecutive (r,s,c) columns described by k.
+__device__ __forceinline__ u16x8 gather_x_wgrad(const ConvArgs& A, const KInfo& k, int m,
+                                                float invPQ, float invQ) {
+  const ConvGeom& g = A.g;
+  u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (!k.ok || m >= A.Kg) return z;
+  const int pq = g.P * g.Q;
+  const int n = fdiv(m, pq, invPQ), rem = m - n * pq;
+  const int p = fdiv(rem, g.Q, invQ), q = rem - p * g.Q;
+  const int h = p * g.stride - g.pad + k.r, w = q * g.stride - g.pad + k.s;
+  if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) return z;
+  return ld8(A.b + ((n * g.H + h) * g.W + w) * g.C + k.c);
+}
+
+// ------------------------------------------------------------------ LDS addressing
+// [row][k] tile, 64 bf16 per row = 8 chunks of 16 B; chunk XOR (row>>1)&7.
+__device__ __forceinline__ int rk_off(int row, int chunk) {
+  return row * 64 + ((chunk ^ ((row >> 1) & 7)) << 3);
+}
+// [m][col] tile with NCOL bf16 per row; chunk XOR (m mod chunks-per-row).
+template <int NCOL>
+__device__ __forceinline__ int mc_off(int m, int col) {
+  constexpr int NCH = NCOL / 8;
+  return m * NCOL + (((col >> 3) ^ (m & (NCH - 1))) << 3) + (col & 7);
+}
+
+template <int MODE, int BM, int BN>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
-  constexpr int LDK = BK + 8;            // padded LDS row (bf16 elements), 16-B aligned rows
+  constexpr int BK = 64;
   constexpr int WTM = BM / 2, WTN = BN / 2;
   constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr int CA = TileLoader<MODE, BM, BN, BK>::CA;
-  constexpr int CB = TileLoader<MODE, BM, BN, BK>::CB;
-  __shared__ __attribute__((aligned(16))) unsigned short smem[(BM + BN) * LDK];
-  unsigned short* As = smem;
-  unsigned short* Bs = smem + BM * LDK;
+  constexpr int CA = BM * BK / 8 / 256;  // 16-B chunks per thread per tile
+  constexpr int CB = BN * BK / 8 / 256;
+  constexpr int TILE_A = BM * BK, TILE_B = BN * BK;
+  static_assert(CA >= 1 && CB >= 1, "tile too small for 256 threads");
+  __shared__ __attribute__((aligned(16))) unsigned short smem[2 * (TILE_A + TILE_B)];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
@@ -128,7 +185,6 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
   const int ksteps = (args.Kg + BK - 1) / BK;
   const int ks_begin = blockIdx.z * args.ksteps_per_split;
   const int ks_end = min(ksteps, ks_begin + args.ksteps_per_split);
-  if (ks_begin >= ks_end) return;
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -138,87 +194,117 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
 
   u16x8 ra[CA], rb[CB];
 
+  // Per-thread constants of the gathers. FWD/DGRAD: chunk c = tid + 256 i covers GEMM row
+  // (tid>>3) + 32 i and reduction chunk tid&7 (same for every i). WGRAD: chunk c covers
+  // reduction row c / (BX/8) and channel group tid % (BX/8) (same for every i).
+  const ConvGeom& gg = args.g;
+  const float invC = 1.f / (float)(MODE == MODE_FWD ? gg.C : gg.K);
+  const float invS = 1.f / (float)gg.S;
+  const float invPQ = 1.f / (float)(gg.P * gg.Q), invQ = 1.f / (float)gg.Q;
+  RowInfo rinfo[MODE != MODE_WGRAD ? CA : 1];
+  KInfo xk;  // WGRAD: (r,s,c) of this thread's B' column group
+  if (MODE != MODE_WGRAD) {
+#pragma unroll
+    for (int i = 0; i < CA; ++i) rinfo[i] = row_info<MODE>(args, row0 + (tid >> 3) + 32 * i);
+  } else {
+    const int j = col0 + (tid % (BN / 8)) * 8;
+    const int rs = j / gg.C;
+    xk.c = j - rs * gg.C;
+    xk.r = rs / gg.S;
+    xk.s = rs - xk.r * gg.S;
+    xk.ok = j < args.Ng;
+  }
+
   auto gload = [&](int ks) {
     const int k0 = ks * BK;
+    if (MODE != MODE_WGRAD) {
+      const int kk = k0 + (tid & 7) * 8;
+      const KInfo k = k_info<MODE>(args, kk, invC, invS);
+#pragma unroll
+      for (int i = 0; i < CA; ++i) ra[i] = gather_a<MODE>(args, rinfo[i], k);
+#pragma unroll
+      for (int i = 0; i < CB; ++i) {
+        const int col = col0 + (tid >> 3) + 32 * i;
+        u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+        rb[i] = (col < args.Ng && kk < args.Kg) ? ld8(args.b + (size_t)col * args.Kg + kk) : z;
+      }
+    } else {
+      const int kc = row0 + (tid % (BM / 8)) * 8;
+#pragma unroll
+      for (int i = 0; i < CA; ++i) {  // dy[m][kout]: row of BM channels per m
+        const int m = k0 + (tid + i * 256) / (BM / 8);
+        u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+        ra[i] = (m < args.Kg && kc < args.Mg) ? ld8(args.a + (size_t)m * gg.K + kc) : z;
+      }
+#pragma unroll
+      for (int i = 0; i < CB; ++i)
+        rb[i] = gather_x_wgrad(args, xk, k0 + (tid + i * 256) / (BN / 8), invPQ, invQ);
+    }
+  };
+
+  auto lstore = [&](int buf) {
+    unsigned short* As = smem + buf * (TILE_A + TILE_B);
+    unsigned short* Bs = As + TILE_A;
     if (MODE != MODE_WGRAD) {
 #pragma unroll
       for (int i = 0; i < CA; ++i) {
         const int c = tid + i * 256;
-        const int r = c / (BK / 8), kc = c - r * (BK / 8);
-        ra[i] = load_a<MODE>(args, row0 + r, k0 + kc * 8);
+        st8(As + rk_off(c >> 3, c & 7), ra[i]);
       }
 #pragma unroll
       for (int i = 0; i < CB; ++i) {
         const int c = tid + i * 256;
-        const int r = c / (BK / 8), kc = c - r * (BK / 8);
-        rb[i] = load_b<MODE>(args, col0 + r, k0 + kc * 8);
+        st8(Bs + rk_off(c >> 3, c & 7), rb[i]);
       }
     } else {
 #pragma unroll
       for (int i = 0; i < CA; ++i) {
         const int c = tid + i * 256;
-        const int m = c / (BM / 8), grp = c - m * (BM / 8);
-        ra[i] = load_a<MODE>(args, row0 + grp * 8, k0 + m);
+        st8(As + mc_off<BM>(c / (BM / 8), (c % (BM / 8)) * 8), ra[i]);
       }
 #pragma unroll
       for (int i = 0; i < CB; ++i) {
         const int c = tid + i * 256;
-        const int m = c / (BN / 8), grp = c - m * (BN / 8);
-        rb[i] = load_b<MODE>(args, col0 + grp * 8, k0 + m);
+        st8(Bs + mc_off<BN>(c / (BN / 8), (c % (BN / 8)) * 8), rb[i]);
       }
     }
   };
 
-  auto lstore = [&]() {
-    if (MODE != MODE_WGRAD) {
-#pragma unroll
-      for (int i = 0; i < CA; ++i) {
-        const int c = tid + i * 256;
-        const int r = c / (BK / 8), kc = c - r * (BK / 8);
-        st8(As + r * LDK + kc * 8, ra[i]);
-      }
-#pragma unroll
-      for (int i = 0; i < CB; ++i) {
-        const int c = tid + i * 256;
-        const int r = c / (BK / 8), kc = c - r * (BK / 8);
-        st8(Bs + r * LDK + kc * 8, rb[i]);
-      }
-    } else {  // transpose into [row][k] while writing LDS
-#pragma unroll
-      for (int i = 0; i < CA; ++i) {
-        const int c = tid + i * 256;
-        const int m = c / (BM / 8), grp = c - m * (BM / 8);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) As[(grp * 8 + e) * LDK + m] = ra[i][e];
-      }
-#pragma unroll
-      for (int i = 0; i < CB; ++i) {
-        const int c = tid + i * 256;
-        const int m = c / (BN / 8), grp = c - m * (BN / 8);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) Bs[(grp * 8 + e) * LDK + m] = rb[i][e];
-      }
-    }
-  };
-
-  gload(ks_begin);
-  for (int ks = ks_begin; ks < ks_end; ++ks) {
-    __syncthreads();
-    lstore();
-    __syncthreads();
-    if (ks + 1 < ks_end) gload(ks + 1);
+  auto compute = [&](int buf) {
+    const unsigned short* As = smem + buf * (TILE_A + TILE_B);
+    const unsigned short* Bs = As + TILE_A;
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 32) {
       bf16x8 fa[TM], fb[TN];
+      if (MODE != MODE_WGRAD) {
+        const int ch = (kk >> 3) + (lane >> 4);
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const unsigned short* p = As + (wm * WTM + i * 16 + (lane & 15)) * LDK + kk + 8 * (lane >> 4);
-        fa[i] = *reinterpret_cast<const bf16x8*>(p);
-      }
+        for (int i = 0; i < TM; ++i)
+          fa[i] = *reinterpret_cast<const bf16x8*>(As + rk_off(wm * WTM + i * 16 + (lane & 15), ch));
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const unsigned short* p = Bs + (wn * WTN + j * 16 + (lane & 15)) * LDK + kk + 8 * (lane >> 4);
-        fb[j] = *reinterpret_cast<const bf16x8*>(p);
+        for (int j = 0; j < TN; ++j)
+          fb[j] = *reinterpret_cast<const bf16x8*>(Bs + rk_off(wn * WTN + j * 16 + (lane & 15), ch));
+      } else {
+        // ds_read_b64_tr_b16: lane 4q+p of each 16-lane group supplies row q, columns 4p..4p+3;
+        // lane i receives column i of the 4 rows. Two reads give the 8 k-values of a fragment.
+        const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+        const int m0 = kk + 8 * g + q;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int col = wm * WTM + i * 16 + 4 * p;
+          v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(As + mc_off<BM>(m0, col)));
+          v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(As + mc_off<BM>(m0 + 4, col)));
+          const short8_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          fa[i] = __builtin_bit_cast(bf16x8, v);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = wn * WTN + j * 16 + 4 * p;
+          v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(Bs + mc_off<BN>(m0, col)));
+          v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(Bs + mc_off<BN>(m0 + 4, col)));
+          const short8_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          fb[j] = __builtin_bit_cast(bf16x8, v);
+        }
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -226,11 +312,27 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
+  };
+
+  if (ks_begin < ks_end) {
+    gload(ks_begin);
+    lstore(0);
+    __syncthreads();
+    int buf = 0;
+    for (int ks = ks_begin; ks < ks_end; ++ks) {
+      const bool more = ks + 1 < ks_end;
+      if (more) gload(ks + 1);  // in flight during the MFMA phase
+      compute(buf);
+      if (more) lstore(buf ^ 1);  // the other buffer was last read before the previous barrier
+      __syncthreads();
+      buf ^= 1;
+    }
   }
 
   // ---------------- epilogue ----------------
   const ConvGeom& g = args.g;
   const bool split = args.splits > 1;
+  float* slab = split ? args.ws + (size_t)blockIdx.z * args.Mg * args.Ng : nullptr;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = col0 + wn * WTN + j * 16 + (lane & 15);
@@ -238,7 +340,6 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
     float bias = 0.f;
     if (MODE == MODE_FWD && !split && args.bias && cok) bias = args.bias[col];
     float s = 0.f, ss = 0.f;
-    // WGRAD output decomposition of col = (r, s, c)
     int wr = 0, wsx = 0, wc = 0;
     if (MODE == MODE_WGRAD) {
       const int rs = col / g.C;
@@ -253,11 +354,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
         const int row = row0 + wm * WTM + i * 16 + 4 * (lane >> 4) + v;
         if (!cok || row >= args.Mg) continue;
         const float val = acc[i][j][v];
-        if (MODE == MODE_WGRAD) {
-          if (wc < g.Creal)
-            atomicAdd(args.out_f32 + (((size_t)row * g.Creal + wc) * g.R + wr) * g.S + wsx, val);
-        } else if (split) {
-          atomicAdd(args.out_f32 + (size_t)row * args.Ng + col, val);
+        if (split) {
+          slab[(size_t)row * args.Ng + col] = val;
+        } else if (MODE == MODE_WGRAD) {
+          if (wc < g.Creal) args.dw[(((size_t)row * g.Creal + wc) * g.R + wr) * g.S + wsx] += val;
         } else {
           const unsigned short h = f2bf(val + bias);
           args.out[(size_t)row * args.Ng + col] = h;
@@ -275,18 +375,20 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
       ss += __shfl_xor(ss, 16, kWave);
       ss += __shfl_xor(ss, 32, kWave);
       if ((lane >> 4) == 0 && cok) {
-        atomicAdd(args.stats + col, s);
-        atomicAdd(args.stats + args.Ng + col, ss);
+        float* st = args.stats + (blockIdx.x % kStatRep) * 2 * args.Ng;  // spread contention
+        atomicAdd(st + col, s);
+        atomicAdd(st + args.Ng + col, ss);
       }
     }
   }
 }
 
-// Split-K finish: fp32 workspace -> (+bias) bf16 output (+ per-channel stats for FWD).
-// Thread layout: cg_local = tid % Gb (8 channels each), rows strided; the per-channel sums are
-// reduced in registers, then across the block through LDS, then ONE atomic per channel per block.
-// Grid: x = row blocks, y = channel chunks of Gb groups.
-__global__ __launch_bounds__(256) void splitk_finish_kernel(const float* ws, unsigned short* out,
+// Split-K finish for FWD/DGRAD: sum the slabs in split order -> (+bias) bf16 output
+// (+ per-channel stats of the rounded output for FWD).
+// Thread layout: cg_local = tid % Gb (8 channels each), rows strided; stats reduced in
+// registers, then through LDS, then ONE atomic per channel per block.
+__global__ __launch_bounds__(256) void splitk_finish_kernel(const float* ws, int splits,
+                                                            unsigned short* out,
                                                             const float* bias, float* stats,
                                                             int Mg, int Ng) {
   __shared__ float red[2][8][256];
@@ -294,6 +396,8 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(const float* ws, uns
   const int Gb = G < 256 ? G : 256;
   const int cgl = threadIdx.x % Gb, prow = threadIdx.x / Gb, prows = 256 / Gb;
   const int cg = blockIdx.y * Gb + cgl;
+  const bool active = prow < prows && cg < G;  // Gb need not divide 256 (e.g. 1000 classes)
+  const size_t slab = (size_t)Mg * Ng;
   float s[8], ss[8], bv[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -301,15 +405,20 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(const float* ws, uns
     ss[e] = 0.f;
     bv[e] = (bias && cg < G) ? bias[cg * 8 + e] : 0.f;
   }
-  const bool active = prow < prows && cg < G;  // Gb need not divide 256 (e.g. 1000 classes)
   for (int row = blockIdx.x * prows + prow; active && row < Mg; row += gridDim.x * prows) {
-    const float4* src = reinterpret_cast<const float4*>(ws + (size_t)row * Ng + cg * 8);
-    const float4 a = src[0], b = src[1];
-    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = bv[e];
+    for (int z = 0; z < splits; ++z) {
+      const float4* src = reinterpret_cast<const float4*>(ws + z * slab + (size_t)row * Ng + cg * 8);
+      const float4 a = src[0], b = src[1];
+      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+      v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+    }
     u16x8 o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      o[e] = f2bf(v[e] + bv[e]);
+      o[e] = f2bf(v[e]);
       const float r = bf2f(o[e]);
       s[e] += r;
       ss[e] += r * r;
@@ -329,7 +438,41 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(const float* ws, uns
     if (blockIdx.y * Gb + c >= G) continue;
     float t = 0.f;
     for (int r = 0; r < prows; ++r) t += red[k][e][r * Gb + c];
-    atomicAdd(stats + k * Ng + (blockIdx.y * Gb + c) * 8 + e, t);
+    float* st = stats + ((blockIdx.x + blockIdx.y) % kStatRep) * 2 * Ng;
+    atomicAdd(st + k * Ng + (blockIdx.y * Gb + c) * 8 + e, t);
+  }
+}
+
+// Split-K finish for WGRAD: dW[k][c][r][s] += sum_z slab[z][k][(r,s,c)].
+// Block (k, split-group): sums its group of slabs for GEMM row k with coalesced reads
+// (reduction order fixed inside a group), transposes (r,s,c) -> (c,r,s) through LDS, and adds
+// into the PyTorch-layout gradient with coalesced stores (one atomic add per group when the
+// splits are divided into several groups).
+constexpr int kWgFinishGroup = 32;
+__global__ __launch_bounds__(256) void wgrad_finish_kernel(const float* ws, int splits, int K,
+                                                           int R, int S, int C, int Creal,
+                                                           float* dw) {
+  extern __shared__ __attribute__((aligned(16))) float row[];
+  const int k = blockIdx.x;
+  const int RS = R * S, RSC = RS * C;
+  const size_t slab = (size_t)K * RSC;
+  const int z0 = blockIdx.y * kWgFinishGroup, z1 = min(splits, z0 + kWgFinishGroup);
+  for (int j = threadIdx.x; j < RSC; j += blockDim.x) {
+    float v = 0.f;
+    for (int z = z0; z < z1; ++z) v += ws[z * slab + (size_t)k * RSC + j];
+    row[j] = v;
+  }
+  __syncthreads();
+  float* out = dw + (size_t)k * Creal * RS;
+  const bool single = gridDim.y == 1;
+  // consecutive threads take consecutive channels: conflict-free LDS reads; each thread's
+  // RS outputs are contiguous in dW (the lines are completed by neighbouring lanes in L2)
+  for (int c = threadIdx.x; c < Creal; c += blockDim.x) {
+    for (int rs = 0; rs < RS; ++rs) {
+      const float v = row[rs * C + c];
+      if (single) out[c * RS + rs] += v;
+      else atomicAdd(out + c * RS + rs, v);
+    }
   }
 }
 
@@ -338,95 +481,135 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(const float* ws, uns
 // ------------------------------- host launcher -------------------------------
 using namespace ddp_amd;
 
-template <int MODE, int BM, int BN, int BK>
-static void launch_cfg(ConvArgs& a, int target_blocks, hipStream_t st) {
+// Split-K factor for a tile config: aim for >= 2 workgroups per CU, keep >= 4 k-steps per
+// split, fit the slab workspace.
+static int pick_splits(int tiles, int ksteps, size_t slab, const ConvArgs& a, size_t ws_elems) {
+  if (a.splits > 0) return std::max(1, std::min(a.splits, ksteps));
+  if (a.ws == nullptr) return 1;
+  int s = (512 + tiles - 1) / tiles;
+  s = std::max(1, std::min(s, ksteps / 4));
+  s = (int)std::min<size_t>((size_t)s, std::max<size_t>(1, ws_elems / slab));
+  return s;
+}
+
+// Rough cost model (arbitrary units): MFMA work / (tile efficiency x chip fill) + split slab
+// traffic. Tile efficiency reflects LDS-bytes-per-MFMA of the 2x2-wave tile; fill = fraction of
+// the 256 CUs x resident blocks that the grid occupies.
+static double tile_cost(int BM, int BN, const ConvArgs& a, size_t ws_elems, int* splits_out) {
+  const int tiles = ((a.Mg + BM - 1) / BM) * ((a.Ng + BN - 1) / BN);
+  const int ksteps = (a.Kg + 63) / 64;
+  const size_t slab = (size_t)a.Mg * a.Ng;
+  const int splits = pick_splits(tiles, ksteps, slab, a, ws_elems);
+  *splits_out = splits;
+  const double eff = (BM == 128 && BN == 128) ? 1.0 : ((BM == 64 && BN == 64) ? 0.55 : 0.8);
+  const int resident = (BM == 128 && BN == 128) ? 2 : ((BM == 64 && BN == 64) ? 4 : 3);
+  const double blocks = (double)tiles * splits;
+  const double fill = std::min(1.0, blocks / (256.0 * resident));
+  // padded work actually issued
+  const double work = (double)tiles * BM * BN * ksteps * 64.0;
+  const double t_mfma = work / (eff * fill) / 1.0e15 * 2.0;
+  // slab write + read at ~4 TB/s plus the finish launch (~3 us)
+  const double t_split = splits > 1 ? 8.0 * splits * (double)slab / 4.0e12 + 3.0e-6 : 0.0;
+  return t_mfma + t_split;
+}
+
+template <int MODE, int BM, int BN>
+static void launch_cfg(ConvArgs& a, int splits, hipStream_t st) {
+  constexpr int BK = 64;
   const int tiles = ((a.Mg + BM - 1) / BM) * ((a.Ng + BN - 1) / BN);
   const int ksteps = (a.Kg + BK - 1) / BK;
-  int splits = 1;
-  if (a.splits <= 0) {  // auto split-K: fill the chip, keep >= 4 k-steps per split
-    splits = (target_blocks + tiles - 1) / tiles;
-    splits = max(1, min(splits, ksteps / 4));
-  } else {
-    splits = min(a.splits, ksteps);
-  }
-  if (MODE != MODE_WGRAD && splits > 1 && a.out_f32 == nullptr) splits = 1;  // no workspace
   const int per = (ksteps + splits - 1) / splits;
   splits = (ksteps + per - 1) / per;
   a.splits = splits;
   a.ksteps_per_split = per;
-  if (MODE != MODE_WGRAD && splits > 1)
-    (void)hipMemsetAsync(a.out_f32, 0, sizeof(float) * (size_t)a.Mg * a.Ng, st);
   dim3 grid(tiles, 1, splits);
-  hipLaunchKernelGGL((conv_igemm_kernel<MODE, BM, BN, BK>), grid, dim3(256), 0, st, a);
-  if (MODE != MODE_WGRAD && splits > 1) {
+  hipLaunchKernelGGL((conv_igemm_kernel<MODE, BM, BN>), grid, dim3(256), 0, st, a);
+  if (splits == 1) return;
+  if (MODE == MODE_WGRAD) {
+    const int groups = (splits + kWgFinishGroup - 1) / kWgFinishGroup;
+    const size_t lds = sizeof(float) * a.g.R * a.g.S * a.g.C;
+    hipLaunchKernelGGL(wgrad_finish_kernel, dim3(a.g.K, groups), dim3(256), lds, st, a.ws, splits,
+                       a.g.K, a.g.R, a.g.S, a.g.C, a.g.Creal, a.dw);
+  } else {
     const int G = a.Ng / 8;
     const int Gb = G < 256 ? G : 256;
     const int chunks = (G + Gb - 1) / Gb;
-    const int rows_per_block = 256 / Gb;
-    // ~8 rows per thread keeps the per-block atomics cheap while filling the chip
-    int bx = (a.Mg + rows_per_block * 8 - 1) / (rows_per_block * 8);
-    bx = std::max(1, std::min(bx, 1024 / chunks + 1));
-    hipLaunchKernelGGL(splitk_finish_kernel, dim3(bx, chunks), dim3(256), 0, st, a.out_f32, a.out,
-                       MODE == MODE_FWD ? a.bias : nullptr, MODE == MODE_FWD ? a.stats : nullptr,
-                       a.Mg, a.Ng);
+    const int rows_per_block = std::max(1, 256 / Gb);
+    // ~2 rows per thread: enough workgroups in flight for a bandwidth-bound pass
+    int bx = (a.Mg + rows_per_block * 2 - 1) / (rows_per_block * 2);
+    bx = std::max(1, std::min(bx, 2048 / chunks + 1));
+    hipLaunchKernelGGL(splitk_finish_kernel, dim3(bx, chunks), dim3(256), 0, st, a.ws, splits,
+                       a.out, MODE == MODE_FWD ? a.bias : nullptr,
+                       MODE == MODE_FWD ? a.stats : nullptr, a.Mg, a.Ng);
   }
 }
 
 template <int MODE>
-static void launch_mode(ConvArgs& a, hipStream_t st) {
-  const long long area = (long long)a.Mg * a.Ng;
-  const int target = 1024;  // >= 4 workgroups per CU on 256 CUs
-  if (area >= (long long)128 * 128 * 512)
-    launch_cfg<MODE, 128, 128, 32>(a, target, st);
-  else
-    launch_cfg<MODE, 64, 64, 32>(a, target, st);
+static void launch_mode(ConvArgs& a, size_t ws_elems, hipStream_t st) {
+  int sp[4];
+  const double c[4] = {tile_cost(128, 128, a, ws_elems, &sp[0]), tile_cost(128, 64, a, ws_elems, &sp[1]),
+                       tile_cost(64, 128, a, ws_elems, &sp[2]), tile_cost(64, 64, a, ws_elems, &sp[3])};
+  int best = 0;
+  for (int i = 1; i < 4; ++i)
+    if (c[i] < c[best]) best = i;
+  switch (best) {
+    case 0: launch_cfg<MODE, 128, 128>(a, sp[0], st); break;
+    case 1: launch_cfg<MODE, 128, 64>(a, sp[1], st); break;
+    case 2: launch_cfg<MODE, 64, 128>(a, sp[2], st); break;
+    default: launch_cfg<MODE, 64, 64>(a, sp[3], st); break;
+  }
 }
 
 extern "C" int ddp_conv_fwd(const ConvGeom* g, const void* x, const void* wc, const float* bias,
-                            void* y, float* stats, float* ws, int splits, hipStream_t st) {
+                            void* y, float* stats, float* ws, size_t ws_elems, int splits,
+                            hipStream_t st) {
+  if (g->C % 8 || g->K % 8) return -1;
   ConvArgs a{};
   a.g = *g;
   a.a = (const unsigned short*)x;
   a.b = (const unsigned short*)wc;
   a.out = (unsigned short*)y;
-  a.out_f32 = ws;
+  a.ws = ws;
   a.bias = bias;
   a.stats = stats;
   a.Mg = g->N * g->P * g->Q;
   a.Ng = g->K;
   a.Kg = g->R * g->S * g->C;
   a.splits = splits;
-  launch_mode<MODE_FWD>(a, st);
+  launch_mode<MODE_FWD>(a, ws_elems, st);
   return (int)hipGetLastError();
 }
 
 extern "C" int ddp_conv_dgrad(const ConvGeom* g, const void* dy, const void* wt, void* dx,
-                              float* ws, int splits, hipStream_t st) {
+                              float* ws, size_t ws_elems, int splits, hipStream_t st) {
+  if (g->C % 8 || g->K % 8) return -1;
   ConvArgs a{};
   a.g = *g;
   a.a = (const unsigned short*)dy;
   a.b = (const unsigned short*)wt;
   a.out = (unsigned short*)dx;
-  a.out_f32 = ws;
+  a.ws = ws;
   a.Mg = g->N * g->H * g->W;
   a.Ng = g->C;
   a.Kg = g->R * g->S * g->K;
   a.splits = splits;
-  launch_mode<MODE_DGRAD>(a, st);
+  launch_mode<MODE_DGRAD>(a, ws_elems, st);
   return (int)hipGetLastError();
 }
 
 extern "C" int ddp_conv_wgrad(const ConvGeom* g, const void* dy, const void* x, float* dw,
-                              int splits, hipStream_t st) {
+                              float* ws, size_t ws_elems, int splits, hipStream_t st) {
+  if (g->C % 8 || g->K % 8) return -1;
   ConvArgs a{};
   a.g = *g;
   a.a = (const unsigned short*)dy;
   a.b = (const unsigned short*)x;
-  a.out_f32 = dw;
+  a.dw = dw;
+  a.ws = ws;
   a.Mg = g->K;
   a.Ng = g->R * g->S * g->C;
   a.Kg = g->N * g->P * g->Q;
   a.splits = splits;
-  launch_mode<MODE_WGRAD>(a, st);
+  launch_mode<MODE_WGRAD>(a, ws_elems, st);
   return (int)hipGetLastError();
 }

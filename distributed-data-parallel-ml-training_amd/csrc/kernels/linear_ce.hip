@@ -111,7 +111,7 @@ __global__ __launch_bounds__(256) void linear_dx_kernel(const float* __restrict_
 
 // dW / db: block = 64 feature columns x one 64-row batch chunk (4 row groups of 16 rows);
 // partial sums reduced through LDS, one atomic per (j, f) per block.
-constexpr int kDwRows = 64;
+constexpr int kDwRows = 8;  // many small row chunks: latency-bound otherwise
 __global__ __launch_bounds__(256) void linear_dw_kernel(const float* __restrict__ dlogits,
                                                         const unsigned short* __restrict__ x,
                                                         int B, int F, int J, const float* gscale,

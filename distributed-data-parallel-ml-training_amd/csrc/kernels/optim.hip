@@ -87,6 +87,110 @@ __global__ __launch_bounds__(256) void pack_conv_weights_kernel(PackTable t) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Fused SGD + weight re-pack: ONE launch updates the whole arena and writes the bf16 MFMA
+// operand copies of every conv weight from the freshly updated values (no second pass over the
+// fp32 weights). Work items (int4): {0, offset, count, -} = plain elementwise chunk;
+// {1, desc, k0, c0} = one TK x TC x (R*S) tile of a conv weight, staged through LDS so that
+// both the Wc ([k][r][s][c], c fastest) and Wt ([c][r][s][k], k fastest) writes are coalesced.
+// Conv descriptor (int64 x 8): {p_offset, K, Cr, C, R, S, wc_ptr, wt_ptr}.
+constexpr int kTileElems = 9216;  // fp32 LDS tile (36 KB)
+
+__device__ __forceinline__ void tile_dims(int RS, int* TK, int* TC) {
+  if (RS == 1) { *TK = 64; *TC = 64; }
+  else if (RS <= 9) { *TK = 32; *TC = 32; }
+  else { *TK = 8; *TC = 16; }
+}
+
+struct SgdHyper {
+  float lr, momentum, wd, grad_scale;
+  int nesterov;
+};
+
+__device__ __forceinline__ float sgd1(float p, float g, float& b, const SgdHyper& h) {
+  float d = g * h.grad_scale + h.wd * p;
+  if (h.momentum != 0.f) {
+    b = h.momentum * b + d;
+    d = h.nesterov ? d + h.momentum * b : b;
+  }
+  return p - h.lr * d;
+}
+
+__global__ __launch_bounds__(256) void sgd_pack_kernel(const int4* __restrict__ items,
+                                                       const long long* __restrict__ descs,
+                                                       float* __restrict__ p,
+                                                       const float* __restrict__ g,
+                                                       float* __restrict__ buf, SgdHyper h) {
+  __shared__ float tile[kTileElems];
+  const int4 it = items[blockIdx.x];
+  const int tid = threadIdx.x;
+  if (it.x == 0) {
+    const size_t off = (size_t)(unsigned)it.y;
+    const int cnt = it.z;
+    for (int i = tid * 4; i < cnt; i += 256 * 4) {
+      if (i + 4 <= cnt && ((off + i) & 3) == 0) {
+        float4 pv = *reinterpret_cast<float4*>(p + off + i);
+        const float4 gv = *reinterpret_cast<const float4*>(g + off + i);
+        float4 bv = *reinterpret_cast<float4*>(buf + off + i);
+        pv.x = sgd1(pv.x, gv.x, bv.x, h);
+        pv.y = sgd1(pv.y, gv.y, bv.y, h);
+        pv.z = sgd1(pv.z, gv.z, bv.z, h);
+        pv.w = sgd1(pv.w, gv.w, bv.w, h);
+        *reinterpret_cast<float4*>(p + off + i) = pv;
+        *reinterpret_cast<float4*>(buf + off + i) = bv;
+      } else {
+        for (int e = i; e < min(cnt, i + 4); ++e) {
+          float b = buf[off + e];
+          p[off + e] = sgd1(p[off + e], g[off + e], b, h);
+          buf[off + e] = b;
+        }
+      }
+    }
+    return;
+  }
+  const long long* d = descs + 8 * it.y;
+  const size_t poff = (size_t)d[0];
+  const int K = (int)d[1], Cr = (int)d[2], C = (int)d[3], R = (int)d[4], S = (int)d[5];
+  unsigned short* wc = reinterpret_cast<unsigned short*>(d[6]);
+  unsigned short* wt = reinterpret_cast<unsigned short*>(d[7]);
+  const int RS = R * S;
+  int TK, TC;
+  tile_dims(RS, &TK, &TC);
+  const int k0 = it.z, c0 = it.w;
+  const int tk = min(TK, K - k0);
+  const int tcr = max(0, min(TC, Cr - c0));  // real channels in this tile
+  const int tcp = min(TC, C - c0);           // padded channels in this tile (Wc width)
+  // 1) SGD on p[k][c][r][s] for the tile's real channels; runs of tcr*RS contiguous floats
+  const int run = tcr * RS;
+  for (int idx = tid; idx < tk * run; idx += 256) {
+    const int kl = idx / run, e = idx - kl * run;
+    const size_t gi = poff + (size_t)(k0 + kl) * Cr * RS + (size_t)c0 * RS + e;
+    float b = buf[gi];
+    const float np = sgd1(p[gi], g[gi], b, h);
+    p[gi] = np;
+    buf[gi] = b;
+    tile[kl * TC * RS + e] = np;  // tile layout [kl][cl][rs]
+  }
+  __syncthreads();
+  // 2) Wc[k][r][s][c] (c fastest, zero for padded channels)
+  if (wc) {
+    for (int idx = tid; idx < tk * RS * tcp; idx += 256) {
+      const int cl = idx % tcp, t = idx / tcp;
+      const int rs = t % RS, kl = t / RS;
+      const float v = cl < tcr ? tile[(kl * TC + cl) * RS + rs] : 0.f;
+      wc[((size_t)(k0 + kl) * RS + rs) * C + c0 + cl] = f2bf(v);
+    }
+  }
+  // 3) Wt[c][r][s][k] (k fastest)
+  if (wt) {
+    for (int idx = tid; idx < tcr * RS * tk; idx += 256) {
+      const int kl = idx % tk, t = idx / tk;
+      const int rs = t % RS, cl = t / RS;
+      wt[((size_t)(c0 + cl) * RS + rs) * K + k0 + kl] = f2bf(tile[(kl * TC + cl) * RS + rs]);
+    }
+  }
+}
+
 __global__ void counter_add_kernel(int* c, int delta) {
   if (threadIdx.x == 0 && blockIdx.x == 0) *c += delta;
 }
@@ -120,6 +224,23 @@ extern "C" int ddp_pack_conv_weights(const PackDesc* descs, int n, hipStream_t s
     hipLaunchKernelGGL(pack_conv_weights_kernel, dim3((unsigned)bx, t.n), dim3(256), 0, st, t);
   }
   return (int)hipGetLastError();
+}
+
+extern "C" int ddp_sgd_pack(const void* items, int n_items, const long long* descs, float* p,
+                            const float* g, float* buf, float lr, float momentum, float wd,
+                            float grad_scale, int nesterov, hipStream_t st) {
+  SgdHyper h{lr, momentum, wd, grad_scale, nesterov};
+  if (n_items <= 0) return 0;
+  hipLaunchKernelGGL(sgd_pack_kernel, dim3(n_items), dim3(256), 0, st, (const int4*)items, descs,
+                     p, g, buf, h);
+  return (int)hipGetLastError();
+}
+
+// Host-side tile shape (must match tile_dims above) so Python can build the item table.
+extern "C" void ddp_sgd_tile_dims(int RS, int* TK, int* TC) {
+  if (RS == 1) { *TK = 64; *TC = 64; }
+  else if (RS <= 9) { *TK = 32; *TC = 32; }
+  else { *TK = 8; *TC = 16; }
 }
 
 extern "C" int ddp_counter_add(int* c, int delta, hipStream_t st) {

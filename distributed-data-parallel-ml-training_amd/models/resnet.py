@@ -1,0 +1,150 @@
+"""ResNet-50 (torchvision-compatible module tree and state_dict keys) for the driver's
+large-gradient config: synthetic ImageNet 3x224x224, 1000 classes, bucketed DDP on 8 MI355X
+(BASELINE.json configs[4]; SURVEY.md §2.D "Extra ops for the driver's ResNet-50 config").
+
+Not part of the CS744 reference itself. 53 convolutions (1x1 / 3x3 / 7x7, stride 1/2),
+BatchNorm with running statistics (track_running_stats=True, eval uses them), bottleneck
+residual adds, 3x3/s2 max-pool, global average pool, Linear 2048 -> 1000; 161 parameter
+tensors, 25 557 032 parameters.
+
+GPU execution: every conv+BN(+residual)+ReLU is one ConvBNAct Function (implicit-GEMM MFMA
+conv with fused BN statistics + one streaming BN/add/ReLU pass), the classifier is the same
+MFMA GEMM (1x1 conv), pooling uses the pool.hip kernels; CPU execution is plain ATen.
+"""
+import torch
+import torch.nn as nn
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride=stride, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.conv3 = nn.Conv2d(planes, planes * self.expansion, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * self.expansion)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+        self._specs = None
+
+    def forward(self, x):  # CPU / ATen path
+        identity = x
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.relu(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out))
+        if self.downsample is not None:
+            identity = self.downsample(x)
+        return self.relu(out + identity)
+
+    def specs(self):
+        from ..ops.layers import ConvBNActSpec
+        if self._specs is None:
+            ds = None
+            if self.downsample is not None:
+                ds = ConvBNActSpec(self.downsample[0], self.downsample[1], relu=False)
+            self._specs = (ConvBNActSpec(self.conv1, self.bn1, relu=True),
+                           ConvBNActSpec(self.conv2, self.bn2, relu=True),
+                           ConvBNActSpec(self.conv3, self.bn3, relu=True, residual=True), ds)
+        return self._specs
+
+    def forward_fused(self, h):
+        from ..ops.layers import conv_bn_act
+        s1, s2, s3, sd = self.specs()
+        out = conv_bn_act(h, s1)
+        out = conv_bn_act(out, s2)
+        identity = conv_bn_act(h, sd) if sd is not None else h
+        return conv_bn_act(out, s3, residual=identity)
+
+
+class ResNet(nn.Module):
+    def __init__(self, layers=(3, 4, 6, 3), num_classes=1000, zero_init_residual=False):
+        super().__init__()
+        self.inplanes = 64
+        self.conv1 = nn.Conv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        self.layer1 = self._make_layer(64, layers[0])
+        self.layer2 = self._make_layer(128, layers[1], stride=2)
+        self.layer3 = self._make_layer(256, layers[2], stride=2)
+        self.layer4 = self._make_layer(512, layers[3], stride=2)
+        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.fc = nn.Linear(512 * Bottleneck.expansion, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.constant_(m.weight, 1)
+                nn.init.constant_(m.bias, 0)
+        if zero_init_residual:
+            for m in self.modules():
+                if isinstance(m, Bottleneck):
+                    nn.init.constant_(m.bn3.weight, 0)
+        self._stem = None
+        self._fc_spec = None
+
+    def _make_layer(self, planes, blocks, stride=1):
+        downsample = None
+        if stride != 1 or self.inplanes != planes * Bottleneck.expansion:
+            downsample = nn.Sequential(
+                nn.Conv2d(self.inplanes, planes * Bottleneck.expansion, 1, stride=stride, bias=False),
+                nn.BatchNorm2d(planes * Bottleneck.expansion))
+        layers = [Bottleneck(self.inplanes, planes, stride, downsample)]
+        self.inplanes = planes * Bottleneck.expansion
+        for _ in range(1, blocks):
+            layers.append(Bottleneck(self.inplanes, planes))
+        return nn.Sequential(*layers)
+
+    def blocks(self):
+        for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
+            yield from layer
+
+    def _gpu_specs(self):
+        from ..ops.layers import ConvBNActSpec, LinearGemmSpec
+        if self._stem is None:
+            self._stem = ConvBNActSpec(self.conv1, self.bn1, relu=True, cin_pad=8)
+            self._fc_spec = LinearGemmSpec(self.fc)
+            for b in self.blocks():
+                b.specs()
+        return self._stem, self._fc_spec
+
+    def fused_plan(self):
+        stem, fc = self._gpu_specs()
+        out = [stem]
+        for b in self.blocks():
+            out += [s for s in b.specs() if s is not None]
+        return out + [fc]
+
+    def forward(self, x):
+        if not x.is_cuda:
+            x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+            x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+            return self.fc(torch.flatten(self.avgpool(x), 1))
+        from ..ops.common import step_scratch
+        from ..ops.layers import conv_bn_act, global_avg_pool, linear_gemm, max_pool, to_nhwc_input
+        stem, fc = self._gpu_specs()
+        step_scratch(x.device).zero()
+        if self.training:
+            self._bump_batches_tracked()
+        h = to_nhwc_input(x, 8)
+        h = max_pool(conv_bn_act(h, stem), 3, 2, 1)
+        for b in self.blocks():
+            h = b.forward_fused(h)
+        return linear_gemm(global_avg_pool(h), fc)
+
+    def _bump_batches_tracked(self):
+        nbt = getattr(self, "_nbt", None)
+        if nbt is None:
+            nbt = [m.num_batches_tracked for m in self.modules()
+                   if isinstance(m, nn.BatchNorm2d) and m.num_batches_tracked is not None]
+            self._nbt = nbt
+        if nbt:
+            torch._foreach_add_(nbt, 1)
+
+
+def resnet50(num_classes=1000):
+    return ResNet((3, 4, 6, 3), num_classes)

@@ -85,8 +85,11 @@ class _VGG(nn.Module):
             y = y.view(y.size(0), -1)
             return self.fc1(y)
         from ..ops.layers import conv_bn_act, linear_small, to_nhwc_input
+        from ..ops.common import step_scratch
+        plan = self.fused_plan()
+        step_scratch(x.device).zero()  # BN statistics / backward sums of every layer: one fill
         h = to_nhwc_input(x, IN_CHANNELS_PADDED)
-        for spec in self.fused_plan():
+        for spec in plan:
             h = conv_bn_act(h, spec)
         if h.shape[1] != 1 or h.shape[2] != 1:
             raise RuntimeError("VGG head expects 1x1 spatial features (32x32 input)")

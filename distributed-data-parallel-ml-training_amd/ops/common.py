@@ -37,6 +37,61 @@ def check(t, dtype=None, shape=None, name="tensor"):
     return t
 
 
+# ---------------------------------------------------------------- split-K slab workspace
+# One persistent fp32 buffer per device, shared by every conv launch (they are stream-ordered).
+# Allocated once, before any hipGraph capture, so captured graphs reference a static address.
+WORKSPACE_ELEMS = 32 << 20  # 128 MiB of the 288 GB HBM
+_WS = {}
+
+
+def workspace(device):
+    key = str(device)
+    ws = _WS.get(key)
+    if ws is None:
+        ws = torch.empty(WORKSPACE_ELEMS, dtype=torch.float32, device=device)
+        _WS[key] = ws
+    return ws
+
+
+# ---------------------------------------------------------------- per-step accumulator scratch
+# Every fused layer owns fixed slices of one persistent fp32 buffer for the accumulators that
+# must start at zero each step (BatchNorm statistics replicas, BN-backward sums). The model's
+# forward zeroes the used prefix with ONE fill instead of one memset per layer and direction.
+# Constraint: a forward must be followed by its backward before the next training forward.
+STAT_REPLICAS = 16  # == kStatRep in csrc/kernels/api.h
+SCRATCH_ELEMS = 8 << 20
+
+
+class StepScratch:
+    def __init__(self, device):
+        self.buf = torch.zeros(SCRATCH_ELEMS, dtype=torch.float32, device=device)
+        self.used = 0
+
+    def take(self, n):
+        off = self.used
+        n = (n + 63) // 64 * 64
+        if off + n > self.buf.numel():
+            raise RuntimeError("StepScratch exhausted; raise ops.common.SCRATCH_ELEMS")
+        self.used = off + n
+        return self.buf[off:off + n]
+
+    def zero(self):
+        if self.used:
+            self.buf[:self.used].zero_()
+
+
+_SCRATCH = {}
+
+
+def step_scratch(device):
+    key = str(device)
+    s = _SCRATCH.get(key)
+    if s is None:
+        s = StepScratch(device)
+        _SCRATCH[key] = s
+    return s
+
+
 # ---------------------------------------------------------------- gradient-ready hooks
 # Fused backward kernels write parameter gradients straight into the flat gradient arena
 # (param.grad is a view into it) and return None to autograd. They announce completion here;

@@ -13,7 +13,8 @@ Activations between blocks are NHWC bf16; the first conv's input is zero-padded 
 """
 import torch
 
-from .common import native, ptr, stream_handle, check, grad_ready, ensure_grad
+from .common import (native, ptr, stream_handle, check, grad_ready, ensure_grad, workspace,
+                     step_scratch, STAT_REPLICAS)
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -45,6 +46,11 @@ class ConvBNActSpec:
         self.wt = torch.empty(self.C, R, S, K, dtype=BF16, device=dev) if self.C == Cr else None
         self._packed_version = None
         conv.weight._ddp_amd_pack = self.pack_desc  # the fused optimizer repacks after its step
+        # per-step zeroed accumulators (StepScratch): BN statistics replicas + BN-backward sums
+        sc = step_scratch(dev)
+        self.scratch = sc
+        self.stats = sc.take(STAT_REPLICAS * 2 * K)[:STAT_REPLICAS * 2 * K]
+        self.sums = sc.take(2 * K)[:2 * K]
 
     def pack_desc(self):
         return (ptr(self.conv.weight), ptr(self.wc), ptr(self.wt), self.K, self.Cr, self.C,
@@ -67,18 +73,9 @@ class ConvBNActSpec:
         return (N, H, W, self.C, self.K, self.R, self.S, self.stride, self.pad, P, Q, self.Cr)
 
 
-# split-K workspaces are only needed when the GEMM output is small (few tiles)
-_WS_LIMIT = 8 << 20
-
-
-def _ws_for(elems, device):
-    if elems * 4 > _WS_LIMIT:
-        return None
-    return torch.empty(elems, dtype=F32, device=device)
-
-
 def conv_forward(spec, x, bias=None, stats=None):
-    """z = conv(x) + bias (bf16 NHWC); stats[2K] += per-channel sum / sumsq of z."""
+    """z = conv(x) + bias (bf16 NHWC); stats[16][2][K] += per-channel sum / sumsq of z
+    (accumulated into STAT_REPLICAS replicas; the consumer sums them)."""
     N, H, W, C = x.shape
     check(x, BF16, name="conv input")
     if C != spec.C:
@@ -86,9 +83,9 @@ def conv_forward(spec, x, bias=None, stats=None):
     g = spec.geom(N, H, W)
     P, Q = g[9], g[10]
     z = torch.empty(N, P, Q, spec.K, dtype=BF16, device=x.device)
-    ws = _ws_for(N * P * Q * spec.K, x.device)
-    native().conv_fwd(g, ptr(x), ptr(spec.wc), ptr(bias), ptr(z), ptr(stats), ptr(ws), 0,
-                      stream_handle())
+    ws = workspace(x.device)
+    native().conv_fwd(g, ptr(x), ptr(spec.wc), ptr(bias), ptr(z), ptr(stats), ptr(ws), ws.numel(),
+                      0, stream_handle())
     return z
 
 
@@ -96,14 +93,14 @@ def conv_backward(spec, x, dz, dweight, need_dx):
     N, H, W, C = x.shape
     g = spec.geom(N, H, W)
     s = stream_handle()
-    native().conv_wgrad(g, ptr(dz), ptr(x), ptr(dweight), 0, s)
+    ws = workspace(x.device)
+    native().conv_wgrad(g, ptr(dz), ptr(x), ptr(dweight), ptr(ws), ws.numel(), 0, s)
     if not need_dx:
         return None
     if spec.wt is None:
         raise RuntimeError("dgrad requested for a channel-padded input layer")
     dx = torch.empty_like(x)
-    ws = _ws_for(N * H * W * spec.C, x.device)
-    native().conv_dgrad(g, ptr(dz), ptr(spec.wt), ptr(dx), ptr(ws), 0, s)
+    native().conv_dgrad(g, ptr(dz), ptr(spec.wt), ptr(dx), ptr(ws), ws.numel(), 0, s)
     return dx
 
 
@@ -112,16 +109,23 @@ class _ConvBNActFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, gamma, beta, residual, spec):
         spec.maybe_pack()
         N, H, W, _ = x.shape
-        stats = torch.zeros(2 * spec.K, dtype=F32, device=x.device)
+        stats = spec.stats  # zeroed by the model's per-forward StepScratch.zero()
         z = conv_forward(spec, x, bias, stats)
         P, Q = z.shape[1], z.shape[2]
         Ho, Wo = (P // 2, Q // 2) if spec.pool else (P, Q)
         y = torch.empty(N, Ho, Wo, spec.K, dtype=BF16, device=x.device)
         if residual is not None:
             check(residual, BF16, (N, P, Q, spec.K), "residual")
+        bn = spec.bn
+        rm = rv = None
+        use_running = 0
+        if bn.track_running_stats and bn.running_mean is not None:
+            rm, rv = bn.running_mean, bn.running_var
+            use_running = 0 if bn.training else 1
         native().bn_act_fwd(N, P, Q, spec.K, int(spec.pool), int(spec.relu), spec.eps, ptr(z),
                             ptr(residual), ptr(stats), ptr(gamma), ptr(beta), ptr(y),
-                            stream_handle())
+                            stream_handle(), ptr(rm), ptr(rv),
+                            float(bn.momentum if bn.momentum is not None else 0.1), use_running)
         ctx.spec = spec
         ctx.has_res = residual is not None
         ctx.save_for_backward(x, z, stats, weight, bias, gamma, beta, residual)
@@ -134,7 +138,7 @@ class _ConvBNActFn(torch.autograd.Function):
         dy = dy.contiguous()
         N, P, Q, K = z.shape
         dz = torch.empty_like(z)
-        sums = torch.empty(2 * K, dtype=F32, device=z.device)
+        sums = spec.sums  # zeroed together with the statistics at the start of the forward
         dres = torch.empty_like(z) if (ctx.has_res and ctx.needs_input_grad[5]) else None
         gw = ensure_grad(weight)
         gb = ensure_grad(bias) if bias is not None else None
@@ -195,12 +199,14 @@ class _CrossEntropyFn(torch.autograd.Function):
     def forward(ctx, logits, labels):
         B, J = logits.shape
         logits = logits.contiguous()
-        check(logits, F32, name="logits")
+        if logits.dtype not in (F32, BF16):
+            raise ValueError("logits must be fp32 or bf16")
+        is_bf16 = int(logits.dtype == BF16)
         labels = labels.to(torch.int64).contiguous()
         loss = torch.zeros((), dtype=F32, device=logits.device)
-        dl = torch.empty(B, J, dtype=F32, device=logits.device)
-        native().softmax_ce(ptr(logits), 0, ptr(labels), B, J, ptr(loss), 0, ptr(dl), 0,
-                            stream_handle())
+        dl = torch.empty(B, J, dtype=logits.dtype, device=logits.device)  # dlogits in logits dtype
+        native().softmax_ce(ptr(logits), is_bf16, ptr(labels), B, J, ptr(loss), 0, ptr(dl),
+                            is_bf16, stream_handle())
         ctx.save_for_backward(dl)
         return loss
 
@@ -224,3 +230,114 @@ def to_nhwc_input(x, cpad=8):
     out = torch.empty(N, H, W, cpad, dtype=BF16, device=x.device)
     native().nchw_to_nhwc(ptr(x), N, C, H, W, cpad, ptr(out), stream_handle())
     return out
+
+
+# ------------------------------------------------------------------ ResNet building blocks
+class _MaxPoolFn(torch.autograd.Function):
+    """MaxPool2d(k, stride, padding) on NHWC bf16 with a 1-byte argmax per output element."""
+
+    @staticmethod
+    def forward(ctx, x, k, stride, pad):
+        check(x, BF16, name="maxpool input")
+        N, H, W, C = x.shape
+        Ho = (H + 2 * pad - k) // stride + 1
+        Wo = (W + 2 * pad - k) // stride + 1
+        y = torch.empty(N, Ho, Wo, C, dtype=BF16, device=x.device)
+        idx = torch.empty(N, Ho, Wo, C, dtype=torch.uint8, device=x.device)
+        native().maxpool_fwd(ptr(x), N, H, W, C, k, k, stride, pad, Ho, Wo, ptr(y), ptr(idx),
+                             stream_handle())
+        ctx.save_for_backward(idx)
+        ctx.cfg = (N, H, W, C, k, stride, pad, Ho, Wo)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        N, H, W, C, k, stride, pad, Ho, Wo = ctx.cfg
+        dy = dy.contiguous()
+        dx = torch.empty(N, H, W, C, dtype=BF16, device=dy.device)
+        native().maxpool_bwd(ptr(dy), ptr(idx), N, H, W, C, k, k, stride, pad, Ho, Wo, ptr(dx),
+                             stream_handle())
+        return dx, None, None, None
+
+
+def max_pool(x, k=3, stride=2, pad=1):
+    return _MaxPoolFn.apply(x, k, stride, pad)
+
+
+class _GlobalAvgPoolFn(torch.autograd.Function):
+    """AdaptiveAvgPool2d(1) + flatten: NHWC bf16 [N, H, W, C] -> [N, C]."""
+
+    @staticmethod
+    def forward(ctx, x):
+        check(x, BF16, name="avgpool input")
+        N, H, W, C = x.shape
+        y = torch.empty(N, C, dtype=BF16, device=x.device)
+        native().avgpool_fwd(ptr(x), N, H * W, C, ptr(y), stream_handle())
+        ctx.cfg = (N, H, W, C)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, H, W, C = ctx.cfg
+        dx = torch.empty(N, H, W, C, dtype=BF16, device=dy.device)
+        native().avgpool_bwd(ptr(dy.contiguous()), N, H * W, C, ptr(dx), stream_handle())
+        return dx
+
+
+def global_avg_pool(x):
+    return _GlobalAvgPoolFn.apply(x)
+
+
+class LinearGemmSpec(ConvBNActSpec):
+    """nn.Linear(F, J) run as a 1x1 convolution on the MFMA implicit-GEMM kernels
+    (weight [J][F] is exactly a [J][F][1][1] conv weight; J and F multiples of 8)."""
+
+    def __init__(self, linear):  # noqa: super().__init__ is not used (no BN, 2-D weight)
+        J, F = linear.weight.shape
+        if J % 8 or F % 8:
+            raise ValueError("GEMM linear needs in/out features divisible by 8")
+        self.linear = linear
+        self.conv, self.bn = linear, None
+        self.K, self.Cr, self.R, self.S, self.C = J, F, 1, 1, F
+        self.stride, self.pad = 1, 0
+        self.relu, self.pool, self.residual = False, False, False
+        self.eps = 1e-5
+        dev = linear.weight.device
+        self.wc = torch.empty(J, F, dtype=BF16, device=dev)
+        self.wt = torch.empty(F, J, dtype=BF16, device=dev)
+        self._packed_version = None
+        linear.weight._ddp_amd_pack = self.pack_desc
+        self.stats = None
+        self.sums = None
+
+
+class _LinearGemmFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, spec):
+        spec.maybe_pack()
+        B, F = x.shape
+        check(x, BF16, name="linear input")
+        x4 = x.view(B, 1, 1, F)
+        y = conv_forward(spec, x4, bias, None)
+        ctx.spec = spec
+        ctx.save_for_backward(x4, weight, bias)
+        return y.view(B, spec.K)
+
+    @staticmethod
+    def backward(ctx, dy):
+        spec = ctx.spec
+        x4, weight, bias = ctx.saved_tensors
+        B = x4.shape[0]
+        dy = dy.contiguous().to(BF16)
+        gw = ensure_grad(weight)
+        if bias is not None:
+            native().colsum(ptr(dy), B, spec.K, ptr(ensure_grad(bias)), stream_handle())
+        dx = conv_backward(spec, x4, dy.view(B, 1, 1, spec.K), gw, ctx.needs_input_grad[0])
+        grad_ready([weight, bias])
+        return (dx.view(B, -1) if dx is not None else None), None, None, None
+
+
+def linear_gemm(x, spec):
+    lin = spec.linear
+    return _LinearGemmFn.apply(x, lin.weight, lin.bias, spec)

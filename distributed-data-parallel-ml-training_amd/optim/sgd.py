@@ -31,6 +31,42 @@ class FusedSGD(torch.optim.SGD):
     def _packs(self):
         return [p._ddp_amd_pack() for p in self.arena.params if hasattr(p, "_ddp_amd_pack")]
 
+    def _work_table(self):
+        """Device work-item table of the fused SGD + re-pack kernel (rebuilt when the set of
+        packed conv weights changes, e.g. after the model's fused plan is first built)."""
+        from ..ops.common import native
+        a = self.arena
+        key = tuple(self._packs())
+        if getattr(self, "_table_key", None) == key:
+            return self._items, self._n_items, self._descs
+        descs, items, conv = [], [], set()
+        for i, p in enumerate(a.params):
+            if not hasattr(p, "_ddp_amd_pack"):
+                continue
+            pp, wc, wt, K, Cr, C, R, S = p._ddp_amd_pack()
+            if pp != a.data.data_ptr() + 4 * a.offsets[i]:
+                raise RuntimeError("packed conv weight is not a view into the parameter arena")
+            d = len(descs)
+            descs.append([a.offsets[i], K, Cr, C, R, S, wc, wt])
+            TK, TC = native().sgd_tile_dims(R * S)
+            for k0 in range(0, K, TK):
+                for c0 in range(0, C, TC):
+                    items.append([1, d, k0, c0])
+            conv.add(i)
+        chunk = 8192
+        for i in range(len(a.params)):
+            if i in conv:
+                continue
+            o, n = a.offsets[i], a.numels[i]
+            for s in range(0, n, chunk):
+                items.append([0, o + s, min(chunk, n - s), 0])
+        dev = a.data.device
+        self._items = torch.tensor(items, dtype=torch.int32, device=dev)
+        self._descs = torch.tensor(descs if descs else [[0] * 8], dtype=torch.int64, device=dev)
+        self._n_items = len(items)
+        self._table_key = key
+        return self._items, self._n_items, self._descs
+
     def zero_grad(self, set_to_none=False):
         if self._fused:
             self.arena.zero_grad()  # kernels accumulate into the arena: always zero, never None
@@ -45,12 +81,12 @@ class FusedSGD(torch.optim.SGD):
         g = self.param_groups[0]
         s = stream_handle()
         a = self.arena
-        native().sgd(a.data.data_ptr(), a.grad.data_ptr(), self.momentum_buffer.data_ptr(), a.total,
-                     float(g["lr"]), float(g["momentum"]), float(g["weight_decay"]),
-                     float(self._grad_scale_factor), int(bool(g["nesterov"])), s)
-        packs = self._packs()
-        if packs:
-            native().pack_conv_weights(packs, s)
+        items, n_items, descs = self._work_table()
+        # one launch: SGD over every tensor + bf16 re-pack of every conv weight
+        native().sgd_pack(items.data_ptr(), n_items, descs.data_ptr(), a.data.data_ptr(),
+                          a.grad.data_ptr(), self.momentum_buffer.data_ptr(), float(g["lr"]),
+                          float(g["momentum"]), float(g["weight_decay"]),
+                          float(self._grad_scale_factor), int(bool(g["nesterov"])), s)
         return None
 
     def state_dict(self):

@@ -121,3 +121,18 @@ def test_part1_cpu_output_format():
     assert any(l.startswith("Total time for 1-39 iteration in ns: ") for l in out)
     assert any(l.startswith("Average time for 1-39 iteration in ns: ") for l in out)
     assert any(l.startswith("Test set: Average loss: ") and "Accuracy: " in l and "/64 (" in l for l in out)
+
+
+def test_resnet50_layout_cpu():
+    from ddp_amd.models.resnet import resnet50
+    m = resnet50()
+    params = list(m.parameters())
+    assert len(params) == 161
+    assert sum(p.numel() for p in params) == 25557032
+    sd = m.state_dict()
+    for k in ["conv1.weight", "bn1.running_mean", "bn1.num_batches_tracked",
+              "layer1.0.downsample.0.weight", "layer4.2.bn3.bias", "fc.weight", "fc.bias"]:
+        assert k in sd, k
+    with torch.no_grad():
+        out = m(torch.randn(1, 3, 64, 64))
+    assert out.shape == (1, 1000)

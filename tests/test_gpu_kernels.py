@@ -53,8 +53,9 @@ def test_conv_fwd_stats(native_ext, case):
     N, Cin, H, W, K, R, stride, pad = case
     Creal = 3 if Cin == 8 else Cin
     conv, spec, x, xn = _conv_setup(N, Cin, H, W, K, R, stride, pad, Creal)
-    stats = torch.zeros(2 * K, device=DEV)
+    stats = torch.zeros(16 * 2 * K, device=DEV)
     z = conv_forward(spec, xn, conv.bias, stats)
+    stats = stats.view(16, 2 * K).sum(0)
     ref = F.conv2d(x, conv.weight, conv.bias, stride, pad).permute(0, 2, 3, 1)
     assert z.shape == ref.shape
     assert rel_err(z, ref) < 1e-2
@@ -118,7 +119,8 @@ def test_bn_act_fwd_bwd(native_ext, C, H, pool, res):
     zn = z.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
     rn = r.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16) if res else None
     zf = zn.float().reshape(-1, C)
-    stats = torch.cat([zf.sum(0), (zf * zf).sum(0)])
+    stats = torch.zeros(16, 2 * C, device=DEV)  # 16 contention-spreading replicas
+    stats[3] = torch.cat([zf.sum(0), (zf * zf).sum(0)])
     Ho = H // 2 if pool else H
     out = torch.empty(N, Ho, Ho, C, device=DEV, dtype=torch.bfloat16)
     s = stream_handle()
@@ -133,7 +135,7 @@ def test_bn_act_fwd_bwd(native_ext, C, H, pool, res):
     dout = bf(torch.randn_like(ref))
     ref.backward(dout)
     doutn = dout.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
-    sums = torch.empty(2 * C, device=DEV)
+    sums = torch.zeros(2 * C, device=DEV)
     dz = torch.empty_like(zn)
     dres = torch.empty_like(zn) if res else None
     dg = torch.zeros(C, device=DEV)
@@ -247,3 +249,55 @@ def test_synthetic_and_augment_match_cpu(native_ext):
     assert torch.allclose(got, ref.to(torch.bfloat16).float(), rtol=8e-3, atol=1e-2)
     assert torch.all(x[..., 3:] == 0)
     assert torch.equal(y.cpu(), torch.from_numpy(labels_c[idx]))
+
+
+@pytest.mark.parametrize("shape,cpad", [((64, 3, 3, 3), 8), ((128, 64, 3, 3), None),
+                                        ((256, 64, 1, 1), None), ((64, 3, 7, 7), 8),
+                                        ((48, 40, 3, 3), None)])
+def test_fused_sgd_repacks_conv_weights(native_ext, shape, cpad):
+    from ddp_amd.ops.layers import ConvBNActSpec
+    from ddp_amd.optim import FusedSGD
+    K, Cr, R, S = shape
+    conv = torch.nn.Conv2d(Cr, K, R, padding=R // 2).to(DEV)
+    bn = torch.nn.BatchNorm2d(K).to(DEV)
+    spec = ConvBNActSpec(conv, bn, cin_pad=cpad)
+    params = list(conv.parameters()) + list(bn.parameters())
+    ref = [torch.nn.Parameter(p.detach().clone()) for p in params]
+    opt = FusedSGD(params, lr=0.1, momentum=0.9, weight_decay=1e-4)
+    ropt = torch.optim.SGD(ref, lr=0.1, momentum=0.9, weight_decay=1e-4)
+    for _ in range(2):
+        gs = [torch.randn_like(p) for p in params]
+        opt.zero_grad()
+        for p, g in zip(params, gs):
+            p.grad.copy_(g)
+        for p, g in zip(ref, gs):
+            p.grad = g.clone()
+        opt.step()
+        ropt.step()
+    torch.cuda.synchronize()
+    for p, r in zip(params, ref):
+        assert torch.allclose(p, r, rtol=1e-5, atol=1e-6)
+    w = conv.weight.detach()
+    C = spec.C
+    exp_wc = torch.zeros(K, R, S, C, device=DEV)
+    exp_wc[..., :Cr] = w.permute(0, 2, 3, 1)
+    assert torch.equal(spec.wc.float(), exp_wc.to(torch.bfloat16).float())
+    if spec.wt is not None:
+        assert torch.equal(spec.wt.float(), w.permute(1, 2, 3, 0).to(torch.bfloat16).float())
+
+
+def test_maxpool3x3s2_and_avgpool(native_ext):
+    from ddp_amd.ops.layers import max_pool, global_avg_pool
+    x = bf(torch.randn(4, 64, 15, 15, device=DEV))
+    xn = x.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).requires_grad_(True)
+    y = max_pool(xn, 3, 2, 1)
+    xr = x.clone().requires_grad_(True)
+    yr = F.max_pool2d(xr, 3, 2, 1)
+    assert torch.equal(y.permute(0, 3, 1, 2).float(), yr)
+    g = bf(torch.randn_like(yr))
+    y.backward(g.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16))
+    yr.backward(g)
+    assert rel_err(xn.grad.permute(0, 3, 1, 2), xr.grad) < 1e-2
+    a = global_avg_pool(xn.detach().requires_grad_(True))
+    ar = x.mean((2, 3))
+    assert rel_err(a, ar) < 1e-2

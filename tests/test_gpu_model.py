@@ -85,9 +85,10 @@ def test_vgg11_forward_backward_matches_cpu_oracle(native_ext):
     cos, errs = {}, {}
     for (n, pe), pg in zip(emu.named_parameters(), gpu.parameters()):
         g, e = pg.grad.cpu().reshape(-1), pe.grad.reshape(-1)
-        if n.startswith("layers.") and n.endswith("bias") and int(n.split(".")[1]) % 4 in (0, 1) \
-                and e.norm() < 1e-4 * (e.numel() ** 0.5):
-            # conv bias followed by batch-stat BN: the gradient is analytically zero
+        if n.startswith("layers.") and n.endswith("bias") and \
+                isinstance(emu.layers[int(n.split(".")[1])], torch.nn.Conv2d):
+            # conv bias followed by batch-stat BN: the gradient is analytically zero, both
+            # sides only carry rounding noise
             assert float(g.abs().max()) < 1e-3, n
             continue
         cos[n] = float(torch.dot(g, e) / (g.norm() * e.norm() + 1e-20))

@@ -18,7 +18,7 @@ def main(prefix, title="rocprofv3 kernel summary"):
     for r in sorted(stats, key=lambda r: -float(r["TotalDurationNs"]))[:20]:
         print(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.3f} | "
               f"{float(r['AverageNs']) / 1e3:.1f} | {float(r['Percentage']):.1f} |")
-    idx = [i for i, r in enumerate(trace) if "sgd_kernel" in r["Kernel_Name"]]
+    idx = [i for i, r in enumerate(trace) if "sgd" in r["Kernel_Name"]]
     if len(idx) >= 2:
         a, b = idx[-2], idx[-1]
         step = trace[a + 1:b + 1]
