@@ -103,6 +103,13 @@ def main():
         except Exception as e:  # fall back to eager steps, loudly
             print(f"[bench] hipGraph capture failed ({e!r}); timing eager steps", file=sys.stderr)
             step.graph = None
+    arena = model.arena if hasattr(model, "arena") else opt.arena
+    if graph_ok and world > 1:
+        if not step.validate_distributed(arena, world):
+            graph_ok = False
+            print("[bench] replicas diverged under graph replay; timing eager steps",
+                  file=sys.stderr)
+        nwarm = max(nwarm - 1, 2)
     for _ in range(nwarm - 2):
         step.step()
     torch.cuda.synchronize()

@@ -57,6 +57,38 @@ class TrainStep:
         else:
             self._body()
 
+    def wait(self, timeout_s=None, poll_s=0.001):
+        """Synchronise with the device, optionally bounded: returns False on timeout instead of
+        blocking forever (a collective whose peer died would otherwise hang the process)."""
+        if timeout_s is None:
+            torch.cuda.synchronize()
+            return True
+        import time
+        ev = torch.cuda.Event()
+        ev.record()
+        t0 = time.monotonic()
+        while not ev.query():
+            if time.monotonic() - t0 > timeout_s:
+                return False
+            time.sleep(poll_s)
+        return True
+
+    def validate_distributed(self, arena, world, timeout_s=120.0):
+        """After capture on >1 ranks: replay once under a time limit and check that every
+        replica is still bit-identical. Falls back to eager execution if the replicas diverged;
+        raises if the replay did not finish (hung collective)."""
+        from ..parallel.ddp import check_replicas
+        if world <= 1:
+            return True
+        self.step()
+        if not self.wait(timeout_s):
+            raise RuntimeError(f"captured step did not finish within {timeout_s}s "
+                               "(collective hang inside the hipGraph?)")
+        if check_replicas(arena, world):
+            return True
+        self.graph = None  # divergent replicas under replay: run eagerly from now on
+        return False
+
     def pop_loss(self):
         """Mean-free running loss sum since the last call (forces a device sync)."""
         v = float(self.loss_sum.item())

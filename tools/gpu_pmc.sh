@@ -1,0 +1,16 @@
+#!/bin/bash
+# PMC counters for the VGG-11 step (separate passes; --pmc only with --kernel-trace/--stats).
+cd "$GRAFT_REPO_ROOT" || exit 2
+root="$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/pmc
+i=0
+for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+           "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVES"; do
+  i=$((i+1))
+  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --pmc $set \
+      --output-format csv -d "$root/gpurun_out/pmc/p$i" -o vgg -- \
+      python3 "$root/bench.py" --steps 3 --warmup 2 > "$root/gpurun_out/pmc/p$i.log" 2>&1)
+  rc=$?; echo "pass $i rc=$rc"; tail -1 gpurun_out/pmc/p$i.log
+  if [ $rc -ne 0 ]; then exit $rc; fi
+done
+ls -R gpurun_out/pmc | head -20
