@@ -32,17 +32,18 @@ static void check(int rc, const char* what) {
 }
 
 static ddp_amd::ConvGeom geom(py::tuple g) {
-  if (g.size() != 12) throw std::runtime_error("conv geometry needs 12 ints");
+  if (g.size() != 12 && g.size() != 13) throw std::runtime_error("conv geometry needs 12/13 ints");
   ddp_amd::ConvGeom c;
+  c.wkrsc = 0;
   int* f = &c.N;
-  for (int i = 0; i < 12; ++i) f[i] = g[i].cast<int>();
+  for (size_t i = 0; i < g.size(); ++i) f[i] = g[i].cast<int>();
   return c;
 }
 
 PYBIND11_MODULE(_native, m) {
   m.doc() = "ddp_amd native extension: gfx950 HIP kernels + RCCL runtime";
 
-  // geometry tuple: (N,H,W,C,K,R,S,stride,pad,P,Q,Creal)
+  // geometry tuple: (N,H,W,C,K,R,S,stride,pad,P,Q,Creal[,wkrsc])
   // ws / ws_elems: fp32 split-K slab workspace (0 disables split-K); splits 0 = automatic
   m.def("conv_fwd", [](py::tuple g, uintptr_t x, uintptr_t wc, uintptr_t bias, uintptr_t y,
                        uintptr_t stats, uintptr_t ws, size_t ws_elems, int splits, uintptr_t st) {
@@ -66,8 +67,9 @@ PYBIND11_MODULE(_native, m) {
   m.def("bn_act_fwd", [](int N, int H, int W, int C, int pool, int relu, float eps, uintptr_t z,
                          uintptr_t res, uintptr_t stats, uintptr_t gamma, uintptr_t beta,
                          uintptr_t out, uintptr_t st, uintptr_t running_mean,
-                         uintptr_t running_var, float momentum, int use_running) {
+                         uintptr_t running_var, float momentum, int use_running, uintptr_t coef) {
     ddp_amd::BnArgs a{};
+    a.coef = P<float>(coef);
     a.N = N; a.H = H; a.W = W; a.C = C; a.pool = pool; a.relu = relu; a.eps = eps;
     a.z = P<unsigned short>(z); a.res = P<unsigned short>(res); a.stats = P<float>(stats);
     a.gamma = P<float>(gamma); a.beta = P<float>(beta); a.out = P<unsigned short>(out);
@@ -77,7 +79,8 @@ PYBIND11_MODULE(_native, m) {
   }, py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("pool"), py::arg("relu"),
      py::arg("eps"), py::arg("z"), py::arg("res"), py::arg("stats"), py::arg("gamma"),
      py::arg("beta"), py::arg("out"), py::arg("stream"), py::arg("running_mean") = 0,
-     py::arg("running_var") = 0, py::arg("momentum") = 0.1f, py::arg("use_running") = 0);
+     py::arg("running_var") = 0, py::arg("momentum") = 0.1f, py::arg("use_running") = 0,
+     py::arg("coef") = 0);
   m.def("maxpool_fwd", [](uintptr_t x, int N, int H, int W, int C, int KH, int KW, int stride,
                           int pad, int Ho, int Wo, uintptr_t y, uintptr_t idx, uintptr_t st) {
     check(ddp_maxpool_fwd(P<void>(x), N, H, W, C, KH, KW, stride, pad, Ho, Wo, P<void>(y),
@@ -100,8 +103,10 @@ PYBIND11_MODULE(_native, m) {
   m.def("bn_act_bwd", [](int N, int H, int W, int C, int pool, int relu, float eps, uintptr_t z,
                          uintptr_t res, uintptr_t stats, uintptr_t gamma, uintptr_t beta,
                          uintptr_t dout, uintptr_t sums, uintptr_t dz, uintptr_t dres,
-                         uintptr_t dgamma, uintptr_t dbeta, uintptr_t dbias, uintptr_t st) {
+                         uintptr_t dgamma, uintptr_t dbeta, uintptr_t dbias, uintptr_t st,
+                         uintptr_t coef) {
     ddp_amd::BnArgs a{};
+    a.coef = P<float>(coef);
     a.N = N; a.H = H; a.W = W; a.C = C; a.pool = pool; a.relu = relu; a.eps = eps;
     a.z = P<unsigned short>(z); a.res = P<unsigned short>(res); a.stats = P<float>(stats);
     a.gamma = P<float>(gamma); a.beta = P<float>(beta); a.dout = P<unsigned short>(dout);
@@ -135,9 +140,11 @@ PYBIND11_MODULE(_native, m) {
     check(ddp_sgd(P<float>(p), P<float>(g), P<float>(buf), n, lr, momentum, wd, grad_scale,
                   nesterov, S(st)), "sgd");
   });
-  // descs: list of (p, wc, wt, K, Cr, C, R, S)
+  m.def("conv_options", [](int wgrad_atomic) { ddp_conv_options(wgrad_atomic); },
+        py::arg("wgrad_atomic") = 0);
+  // descs: list of (p, wc, wt, K, Cr, C, R, S, krsc)
   m.def("pack_conv_weights", [](std::vector<std::tuple<uintptr_t, uintptr_t, uintptr_t, int, int,
-                                                       int, int, int>> descs, uintptr_t st) {
+                                                       int, int, int, int>> descs, uintptr_t st) {
     std::vector<ddp_amd::PackDesc> d;
     for (auto& t : descs) {
       ddp_amd::PackDesc x;
@@ -146,6 +153,7 @@ PYBIND11_MODULE(_native, m) {
       x.wt = P<unsigned short>(std::get<2>(t));
       x.K = std::get<3>(t); x.Cr = std::get<4>(t); x.C = std::get<5>(t);
       x.R = std::get<6>(t); x.S = std::get<7>(t);
+      x.krsc = std::get<8>(t);
       d.push_back(x);
     }
     check(ddp_pack_conv_weights(d.data(), (int)d.size(), S(st)), "pack_conv_weights");

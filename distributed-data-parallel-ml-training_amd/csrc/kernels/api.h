@@ -17,6 +17,7 @@ struct ConvGeom {
   int R, S, stride, pad;
   int P, Q;           // output spatial
   int Creal;          // real (unpadded) input channels — weight-gradient layout
+  int wkrsc;          // fp32 weight / weight-gradient layout: 0 = [K][Cr][R][S], 1 = [K][R][S][Cr]
 };
 
 struct BnArgs {
@@ -26,12 +27,12 @@ struct BnArgs {
   float eps;
   const unsigned short* z;      // conv output (bf16)
   const unsigned short* res;    // optional residual added before ReLU (bf16, same shape as z)
-  const float* stats;           // [2C] sum, sumsq over N*H*W
+  const float* stats;           // [kStatRep][2][C] sum, sumsq over N*H*W
   const float* gamma;           // [C]
   const float* beta;            // [C]
   unsigned short* out;          // forward output (bf16, pooled shape)
   const unsigned short* dout;   // backward: grad wrt block output (pooled shape)
-  float* sums;                  // backward scratch [2C]: S1 = sum dy_bn, S2 = sum dy_bn*xhat
+  float* sums;                  // backward scratch [kStatRep][2][C]: S1 = sum dy_bn, S2 = sum dy_bn*xhat
   unsigned short* dz;           // backward: grad wrt conv output
   unsigned short* dres;         // backward: grad wrt residual (optional)
   float* dgamma;                // grad arena slices (accumulated)
@@ -41,13 +42,16 @@ struct BnArgs {
   float* running_var;
   float momentum;
   int use_running;              // eval with running statistics instead of batch statistics
+  float* coef;                  // [6][C] scale, shift, mean, invstd (fwd) and k1, k2 (bwd); the
+                                // backward reads the table its forward wrote
 };
 
 struct PackDesc {
-  const float* p;          // fp32 master [K][Cr][R][S]
+  const float* p;          // fp32 master [K][Cr][R][S] (krsc == 0) or [K][R][S][Cr] (krsc == 1)
   unsigned short* wc;      // bf16 [K][R][S][C]   (may be null)
   unsigned short* wt;      // bf16 [C][R][S][K]   (may be null)
   int K, Cr, C, R, S;
+  int krsc;
 };
 
 struct AugArgs {
@@ -83,6 +87,7 @@ int ddp_softmax_ce(const void* logits, int logits_bf16, const long long* labels,
                    hipStream_t st);
 int ddp_sgd(float* p, const float* g, float* buf, size_t n, float lr, float momentum, float wd,
             float grad_scale, int nesterov, hipStream_t st);
+void ddp_conv_options(int wgrad_atomic);
 int ddp_pack_conv_weights(const ddp_amd::PackDesc* descs, int n, hipStream_t st);
 int ddp_sgd_pack(const void* items, int n_items, const long long* descs, float* p, const float* g,
                  float* buf, float lr, float momentum, float wd, float grad_scale, int nesterov,

@@ -2,273 +2,226 @@
 //
 // Reference parity: BatchNorm2d(track_running_stats=False) -> ReLU(inplace) -> MaxPool2d(2,2)
 // from part1/model.py:16,24-25. Batch statistics are used in
-// both train and eval mode (no running buffers), exactly like the reference.
+// both train and eval mode (no running buffers), exactly like the reference; the ResNet-50
+// path (track_running_stats=True) also updates / uses running statistics.
 //
-// Forward statistics (per-channel sum / sum of squares of the bf16 conv output) are produced
-// by the conv epilogue (conv_igemm.hip), so the forward here is a single streaming pass:
-//     a = pool( relu( gamma * (z - mean) * invstd + beta (+ res) ) )
-// Backward is two streaming passes that RECOMPUTE the pre-activation from z (no saved masks
-// or pool indices):
-//     reduce : dy_bn = route_pool(dout) * [y > 0];  S1 += dy_bn, S2 += dy_bn * xhat
-//     apply  : dz = gamma*invstd*(dy_bn - S1/M - xhat*S2/M); dgamma += S2, dbeta += S1,
-//              dbias(conv) += sum(dz), d_res = dy_bn (residual branch)
-// Every thread owns 8 contiguous channels (one 16-byte vector) of one output pixel.
+// Forward statistics (per-channel sum / sum of squares of the bf16 conv output, in kStatRep
+// contention-spreading replicas) are produced by the conv epilogue (conv_igemm.hip).
+//   fwd : finalize  — one thread per channel: replicas -> mean, invstd, scale, shift (coef
+//                     table, [6][C]); running-statistics update
+//         apply     — a = pool( relu( scale * z + shift (+ res) ) ), one streaming pass
+//   bwd : reduce    — RECOMPUTES the pre-activation from z (no saved masks / pool indices):
+//                     dy_bn = route_pool(dout) * [y > 0];  S1 += dy_bn, S2 += dy_bn * xhat
+//                     (replicated partial sums, fp32 atomics)
+//         finalize  — one thread per channel: k1 = S1/M, k2 = S2/M; dgamma += S2, dbeta += S1
+//         apply     — dz = scale * (dy_bn - k1 - xhat * k2);  d_res = dy_bn (residual branch)
+// The coefficient table is built ONCE per layer (a table rebuilt by every block would re-read
+// 16 replicas x C channels per block: ~800 MB per ResNet-50 BN layer).
+// Every apply/reduce thread owns 8 contiguous channels (one 16-byte vector) of an output pixel
+// and reads its coefficients straight from the (L2-resident) table: no LDS, no barrier before
+// the streaming loads.
+//
+// The conv-bias gradient is NOT accumulated: for train-mode BN the gradient w.r.t. its input
+// sums to exactly zero over (N, H, W) per channel (BN is invariant to a per-channel constant
+// shift), so d(bias) of the producing convolution is identically 0 — PyTorch's value is
+// rounding noise around 0 (part1/model.py:18-24: conv with bias followed by BatchNorm2d).
 #include "common.h"
 #include "api.h"
 
 namespace ddp_amd {
 
-__device__ __forceinline__ void bn_coeffs(const BnArgs& a, int c0, float* scale, float* shift,
-                                          float* mean, float* invstd) {
+enum { kSc = 0, kSh = 1, kMu = 2, kIs = 3, kK1 = 4, kK2 = 5 };  // coef table rows
+
+__device__ __forceinline__ void ld8f(const float* p, float* v) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0];
+  const float4 b = reinterpret_cast<const float4*>(p)[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+// ------------------------------- finalize kernels -------------------------------
+__global__ __launch_bounds__(256) void bn_finalize_fwd_kernel(BnArgs a) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.C) return;
+  float mu, is;
   if (a.use_running) {  // eval mode of track_running_stats=True BatchNorm
+    mu = a.running_mean[c];
+    is = rsqrtf(a.running_var[c] + a.eps);
+  } else {
+    const float M = (float)a.N * a.H * a.W;
+    float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int c = c0 + e;
-      const float mu = a.running_mean[c];
-      const float is = rsqrtf(a.running_var[c] + a.eps);
-      const float sc = a.gamma[c] * is;
-      scale[e] = sc;
-      shift[e] = a.beta[c] - mu * sc;
-      mean[e] = mu;
-      invstd[e] = is;
+    for (int r = 0; r < kStatRep; ++r) {
+      s1 += a.stats[r * 2 * a.C + c];
+      s2 += a.stats[r * 2 * a.C + a.C + c];
     }
-    return;
-  }
-  const float inv_m = 1.f / (float)(a.N * a.H * a.W);
-  float s1[8], s2[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
-  for (int r = 0; r < kStatRep; ++r) {  // sum the contention-spreading replicas
-    const float4* p1 = reinterpret_cast<const float4*>(a.stats + r * 2 * a.C + c0);
-    const float4* p2 = reinterpret_cast<const float4*>(a.stats + r * 2 * a.C + a.C + c0);
-    const float4 x0 = p1[0], x1 = p1[1], y0 = p2[0], y1 = p2[1];
-    s1[0] += x0.x; s1[1] += x0.y; s1[2] += x0.z; s1[3] += x0.w;
-    s1[4] += x1.x; s1[5] += x1.y; s1[6] += x1.z; s1[7] += x1.w;
-    s2[0] += y0.x; s2[1] += y0.y; s2[2] += y0.z; s2[3] += y0.w;
-    s2[4] += y1.x; s2[5] += y1.y; s2[6] += y1.z; s2[7] += y1.w;
-  }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int c = c0 + e;
-    const float mu = s1[e] * inv_m;
-    const float var = fmaxf(s2[e] * inv_m - mu * mu, 0.f);
-    const float is = rsqrtf(var + a.eps);
-    const float sc = a.gamma[c] * is;
-    scale[e] = sc;
-    shift[e] = a.beta[c] - mu * sc;
-    mean[e] = mu;
-    invstd[e] = is;
-  }
-}
-
-// Block-cooperative per-channel coefficients for channels [c_begin, c_begin + n): the 16
-// statistics replicas are summed ONCE per channel per block (not once per thread) into LDS.
-__device__ __forceinline__ void block_coeffs(const BnArgs& a, int c_begin, int n, float* l_sc,
-                                             float* l_sh, float* l_mu, float* l_is) {
-  const float inv_m = 1.f / (float)(a.N * a.H * a.W);
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const int c = c_begin + i;
-    float mu, is;
-    if (a.use_running) {
-      mu = a.running_mean[c];
-      is = rsqrtf(a.running_var[c] + a.eps);
-    } else {
-      float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int r = 0; r < kStatRep; ++r) {
-        s1 += a.stats[r * 2 * a.C + c];
-        s2 += a.stats[r * 2 * a.C + a.C + c];
-      }
-      mu = s1 * inv_m;
-      is = rsqrtf(fmaxf(s2 * inv_m - mu * mu, 0.f) + a.eps);
-    }
-    const float sc = a.gamma[c] * is;
-    l_sc[i] = sc;
-    l_sh[i] = a.beta[c] - mu * sc;
-    if (l_mu) l_mu[i] = mu;
-    if (l_is) l_is[i] = is;
-  }
-  __syncthreads();
-}
-
-// ------------------------------- forward -------------------------------
-__global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnArgs a) {
-  const int G = a.C / 8;
-  const int Ho = a.pool ? a.H / 2 : a.H, Wo = a.pool ? a.W / 2 : a.W;
-  const size_t total = (size_t)a.N * Ho * Wo * G;
-  // running statistics (track_running_stats=True, training): block 0 updates every channel
-  if (a.running_mean && !a.use_running && blockIdx.x == 0) {
-    const float M = (float)(a.N * a.H * a.W);
-    for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
-      float s1 = 0.f, s2 = 0.f;
-      for (int r = 0; r < kStatRep; ++r) {
-        s1 += a.stats[r * 2 * a.C + c];
-        s2 += a.stats[r * 2 * a.C + a.C + c];
-      }
-      const float mu = s1 / M;
-      const float var = fmaxf(s2 / M - mu * mu, 0.f);
+    mu = s1 / M;
+    const float var = fmaxf(s2 / M - mu * mu, 0.f);
+    is = rsqrtf(var + a.eps);
+    if (a.running_mean) {  // training with track_running_stats=True (unbiased variance)
       const float unbiased = M > 1.f ? var * M / (M - 1.f) : var;
       a.running_mean[c] = (1.f - a.momentum) * a.running_mean[c] + a.momentum * mu;
       a.running_var[c] = (1.f - a.momentum) * a.running_var[c] + a.momentum * unbiased;
     }
   }
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  block_coeffs(a, 0, a.C, lds, lds + a.C, nullptr, nullptr);
-  float sc[8], sh[8];
-  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total;
-       t += (size_t)gridDim.x * blockDim.x) {
-    const int cg = (int)(t % G);
-    const size_t pix = t / G;
+  const float sc = a.gamma[c] * is;
+  a.coef[kSc * a.C + c] = sc;
+  a.coef[kSh * a.C + c] = a.beta[c] - mu * sc;
+  a.coef[kMu * a.C + c] = mu;
+  a.coef[kIs * a.C + c] = is;
+}
+
+__global__ __launch_bounds__(256) void bn_finalize_bwd_kernel(BnArgs a) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.C) return;
+  const float inv_m = 1.f / ((float)a.N * a.H * a.W);
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int r = 0; r < kStatRep; ++r) {
+    s1 += a.sums[r * 2 * a.C + c];
+    s2 += a.sums[r * 2 * a.C + a.C + c];
+  }
+  a.coef[kK1 * a.C + c] = s1 * inv_m;
+  a.coef[kK2 * a.C + c] = s2 * inv_m;
+  if (a.dgamma) a.dgamma[c] += s2;  // one writer per channel: plain accumulate into the arena
+  if (a.dbeta) a.dbeta[c] += s1;
+}
+
+// ------------------------------- forward apply -------------------------------
+// One thread = IPT items (output pixels) x 8 channels; every load is issued up front.
+template <bool POOL, int IPT>
+__global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnArgs a) {
+  constexpr int NP = POOL ? 4 : 1;
+  const int G = a.C / 8;
+  const int Ho = POOL ? a.H / 2 : a.H, Wo = POOL ? a.W / 2 : a.W;
+  const size_t total = (size_t)a.N * Ho * Wo * G;
+  u16x8 zv[IPT][NP], rv[IPT][POOL ? 1 : NP];
+  float sc[IPT][8], sh[IPT][8];
+  const size_t t0 = (size_t)blockIdx.x * 256 * IPT + threadIdx.x;
+#pragma unroll
+  for (int it = 0; it < IPT; ++it) {
+    const size_t t = t0 + it * 256;
+    const size_t tt = t < total ? t : 0;
+    const int cg = (int)(tt % G);
+    const size_t pix = tt / G;
     const int wo = (int)(pix % Wo);
     const int ho = (int)((pix / Wo) % Ho);
     const int n = (int)(pix / ((size_t)Wo * Ho));
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      sc[e] = lds[cg * 8 + e];
-      sh[e] = lds[a.C + cg * 8 + e];
+    for (int d = 0; d < NP; ++d) {
+      const int h = POOL ? 2 * ho + (d >> 1) : ho, w = POOL ? 2 * wo + (d & 1) : wo;
+      const size_t off = (((size_t)n * a.H + h) * a.W + w) * a.C + cg * 8;
+      zv[it][d] = ld8(a.z + off);
+      if (!POOL && a.res) rv[it][POOL ? 0 : d] = ld8(a.res + off);
     }
-    u16x8 o;
-    if (!a.pool) {
-      const size_t off = (((size_t)n * a.H + ho) * a.W + wo) * a.C + cg * 8;
-      const u16x8 zv = ld8(a.z + off);
-      u16x8 rv = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (a.res) rv = ld8(a.res + off);
+    ld8f(a.coef + kSc * a.C + cg * 8, sc[it]);
+    ld8f(a.coef + kSh * a.C + cg * 8, sh[it]);
+  }
+#pragma unroll
+  for (int it = 0; it < IPT; ++it) {
+    const size_t t = t0 + it * 256;
+    if (t >= total) break;
+    const int cg = (int)(t % G);
+    const size_t pix = t / G;
+    float best[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) best[e] = -INFINITY;
+#pragma unroll
+    for (int d = 0; d < NP; ++d) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        float y = bf2f(zv[e]) * sc[e] + sh[e];
-        if (a.res) y += bf2f(rv[e]);
+        float y = bf2f(zv[it][d][e]) * sc[it][e] + sh[it][e];
+        if (!POOL && a.res) y += bf2f(rv[it][POOL ? 0 : d][e]);
         if (a.relu) y = fmaxf(y, 0.f);
-        o[e] = f2bf(y);
+        if (!POOL || y > best[e] || y != y) best[e] = y;
       }
-    } else {
-      float best[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) best[e] = -INFINITY;
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const int h = 2 * ho + (d >> 1), w = 2 * wo + (d & 1);
-        const size_t off = (((size_t)n * a.H + h) * a.W + w) * a.C + cg * 8;
-        const u16x8 zv = ld8(a.z + off);
-        u16x8 rv = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (a.res) rv = ld8(a.res + off);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float y = bf2f(zv[e]) * sc[e] + sh[e];
-          if (a.res) y += bf2f(rv[e]);
-          if (a.relu) y = fmaxf(y, 0.f);
-          if (y > best[e] || y != y) best[e] = y;
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = f2bf(best[e]);
     }
-    st8(a.out + (((size_t)n * Ho + ho) * Wo + wo) * a.C + cg * 8, o);
+    u16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(best[e]);
+    st8(a.out + pix * a.C + cg * 8, o);
   }
 }
 
 // ------------------------------- backward -------------------------------
-// Computes dy_bn for the (up to 4) pre-pool pixels owned by thread item t.
-// POOL: 4 pixels per item, else 1; fills offsets, xhat and dy_bn.
-template <bool POOL>
-__device__ __forceinline__ void bwd_item(const BnArgs& a, size_t t, int G, int Ho, int Wo,
-                                        const float* sc, const float* sh, const float* mu,
-                                        const float* is, size_t* offs, float (*xh)[8],
-                                        float (*dyb)[8], int* cg_out) {
-  const int cg = (int)(t % G);
-  *cg_out = cg;
-  const size_t pix = t / G;
-  const int wo = (int)(pix % Wo);
-  const int ho = (int)((pix / Wo) % Ho);
-  const int n = (int)(pix / ((size_t)Wo * Ho));
-  const u16x8 dv = ld8(a.dout + (((size_t)n * Ho + ho) * Wo + wo) * a.C + cg * 8);
-  if (!POOL) {
-    const size_t off = (((size_t)n * a.H + ho) * a.W + wo) * a.C + cg * 8;
-    offs[0] = off;
-    const u16x8 zv = ld8(a.z + off);
-    u16x8 rv = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (a.res) rv = ld8(a.res + off);
+// One thread = IPT items x 8 channels. Each item is one (post-pool) output pixel; with POOL its
+// 4 pre-pool pixels are recomputed to route the gradient to the window's argmax.
+template <bool POOL, int IPT>
+struct BwdItems {
+  static constexpr int NP = POOL ? 4 : 1;
+  u16x8 dv[IPT];
+  u16x8 zv[IPT][NP];
+  u16x8 rv[IPT][POOL ? 1 : NP];  // residual: only without pooling (host rejects pool + res)
+  size_t off[IPT][NP];
+  bool ok[IPT];
+};
+
+template <bool POOL, int IPT>
+__device__ __forceinline__ void bwd_load(const BnArgs& a, BwdItems<POOL, IPT>& L, size_t p0,
+                                         size_t pstride, size_t npix, int cg, int Ho, int Wo) {
+  constexpr int NP = POOL ? 4 : 1;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float zf = bf2f(zv[e]);
-      float y = zf * sc[e] + sh[e];
-      if (a.res) y += bf2f(rv[e]);
-      xh[0][e] = (zf - mu[e]) * is[e];
-      const float g = bf2f(dv[e]);
-      dyb[0][e] = (a.relu && !(y > 0.f)) ? 0.f : g;
+  for (int it = 0; it < IPT; ++it) {
+    const size_t p = p0 + it * pstride;
+    L.ok[it] = p < npix;
+    const size_t pp = L.ok[it] ? p : 0;
+    const int wo = (int)(pp % Wo);
+    const int ho = (int)((pp / Wo) % Ho);
+    const int n = (int)(pp / ((size_t)Wo * Ho));
+    L.dv[it] = ld8(a.dout + pp * a.C + cg * 8);
+#pragma unroll
+    for (int d = 0; d < NP; ++d) {
+      const int h = POOL ? 2 * ho + (d >> 1) : ho, w = POOL ? 2 * wo + (d & 1) : wo;
+      const size_t off = (((size_t)n * a.H + h) * a.W + w) * a.C + cg * 8;
+      L.off[it][d] = off;
+      L.zv[it][d] = ld8(a.z + off);
+      if (!POOL && a.res) L.rv[it][POOL ? 0 : d] = ld8(a.res + off);
     }
-    return;
   }
-  float best[8], yv[4][8];
+}
+
+// dy_bn (gradient at the BN output, after ReLU mask and pool routing) and xhat for one item
+template <bool POOL>
+__device__ __forceinline__ void bwd_compute(const BnArgs& a, const u16x8& dv, const u16x8* zv,
+                                            const u16x8* rv, const float* sc, const float* sh,
+                                            const float* mu, const float* is, float (*xh)[8],
+                                            float (*dyb)[8]) {
+  constexpr int NP = POOL ? 4 : 1;
+  float best[8], yv[NP][8];
   int arg[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; arg[e] = 0; }
 #pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    const int h = 2 * ho + (d >> 1), w = 2 * wo + (d & 1);
-    const size_t off = (((size_t)n * a.H + h) * a.W + w) * a.C + cg * 8;
-    offs[d] = off;
-    const u16x8 zv = ld8(a.z + off);
-    u16x8 rv = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (a.res) rv = ld8(a.res + off);
+  for (int d = 0; d < NP; ++d) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float zf = bf2f(zv[e]);
+      const float zf = bf2f(zv[d][e]);
       float y = zf * sc[e] + sh[e];
-      if (a.res) y += bf2f(rv[e]);
+      if (!POOL && a.res) y += bf2f(rv[POOL ? 0 : d][e]);
       xh[d][e] = (zf - mu[e]) * is[e];
       yv[d][e] = y;
-      const float yr = a.relu ? fmaxf(y, 0.f) : y;
-      if (yr > best[e] || yr != yr) { best[e] = yr; arg[e] = d; }
+      if (POOL) {
+        const float yr = a.relu ? fmaxf(y, 0.f) : y;
+        if (yr > best[e] || yr != yr) { best[e] = yr; arg[e] = d; }
+      }
     }
   }
 #pragma unroll
-  for (int d = 0; d < 4; ++d)
+  for (int d = 0; d < NP; ++d)
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float g = (arg[e] == d) ? bf2f(dv[e]) : 0.f;
+      const float g = (!POOL || arg[e] == d) ? bf2f(dv[e]) : 0.f;
       dyb[d][e] = (a.relu && !(yv[d][e] > 0.f)) ? 0.f : g;
     }
 }
 
-// Block-wide reduction of 8-channel partial sums for threads that share a channel group.
-// Threads are laid out cg_local = tid % Gb; 256/Gb threads share each group.
-template <int NV>
-__device__ __forceinline__ void block_reduce_atomic(float (&v)[NV][8], int Gb, int cg_base,
-                                                    float* const* dst, float* red) {
-  const int tid = threadIdx.x;
-  const int rows = 256 / Gb;
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    __syncthreads();
-#pragma unroll
-    for (int e = 0; e < 8; ++e) red[e * 256 + tid] = v[k][e];
-    __syncthreads();
-    for (int idx = tid; idx < Gb * 8; idx += 256) {
-      const int cgl = idx / 8, e = idx % 8;
-      float s = 0.f;
-      for (int r = 0; r < rows; ++r) s += red[e * 256 + r * Gb + cgl];
-      if (dst[k]) atomicAdd(dst[k] + (cg_base + cgl) * 8 + e, s);
-    }
-  }
-}
-
-// Grid: x = blocks over pixels, y = channel chunks of (at most) 256 groups.
-// Per-thread copy of the block's LDS coefficient tables for its 8 channels.
-__device__ __forceinline__ void load_coeffs(const float* lds, int nch, int cl0, float* sc,
-                                            float* sh, float* mu, float* is) {
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    sc[e] = lds[cl0 + e];
-    sh[e] = lds[nch + cl0 + e];
-    mu[e] = lds[2 * nch + cl0 + e];
-    is[e] = lds[3 * nch + cl0 + e];
-  }
-}
-
-template <bool POOL>
+// Grid: x = blocks of (256/Gb) x IPT items, y = channel chunks of (at most) 256 groups.
+// Partial sums go to kStatRep replicas of [2][C] (replica = blockIdx.x % kStatRep): the number
+// of atomic adders per address drops 16x (memory-side atomics serialise per address).
+template <bool POOL, int IPT>
 __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
+  constexpr int NP = POOL ? 4 : 1;
   __shared__ float red[8 * 256];
-  extern __shared__ __attribute__((aligned(16))) float lds[];
   const int G = a.C / 8;
   const int Gb = G < 256 ? G : 256;
   const int Ho = POOL ? a.H / 2 : a.H, Wo = POOL ? a.W / 2 : a.W;
@@ -276,19 +229,23 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
   const int cg_base = blockIdx.y * Gb;
   const int cgl = threadIdx.x % Gb;
   const int prow = threadIdx.x / Gb, prows = 256 / Gb;
-  const int nch = Gb * 8;
-  block_coeffs(a, cg_base * 8, nch, lds, lds + nch, lds + 2 * nch, lds + 3 * nch);
+  const int c0 = (cg_base + cgl) * 8;
+  BwdItems<POOL, IPT> L;
+  bwd_load<POOL, IPT>(a, L, (size_t)blockIdx.x * prows * IPT + prow, prows, npix, cg_base + cgl,
+                      Ho, Wo);
   float sc[8], sh[8], mu[8], is[8];
-  load_coeffs(lds, nch, cgl * 8, sc, sh, mu, is);
+  ld8f(a.coef + kSc * a.C + c0, sc);
+  ld8f(a.coef + kSh * a.C + c0, sh);
+  ld8f(a.coef + kMu * a.C + c0, mu);
+  ld8f(a.coef + kIs * a.C + c0, is);
   float acc[2][8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { acc[0][e] = 0.f; acc[1][e] = 0.f; }
-  for (size_t p = blockIdx.x * (size_t)prows + prow; p < npix; p += (size_t)gridDim.x * prows) {
-    constexpr int NP = POOL ? 4 : 1;
-    size_t offs[NP];
+#pragma unroll
+  for (int it = 0; it < IPT; ++it) {
+    if (!L.ok[it]) continue;
     float xh[NP][8], dyb[NP][8];
-    int cg;
-    bwd_item<POOL>(a, p * G + cg_base + cgl, G, Ho, Wo, sc, sh, mu, is, offs, xh, dyb, &cg);
+    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], sc, sh, mu, is, xh, dyb);
 #pragma unroll
     for (int d = 0; d < NP; ++d)
 #pragma unroll
@@ -297,14 +254,28 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
         acc[1][e] += dyb[d][e] * xh[d][e];
       }
   }
-  float* dst[2] = {a.sums, a.sums + a.C};
-  block_reduce_atomic<2>(acc, Gb, cg_base, dst, red);
+  // block reduction over the 256/Gb threads sharing each channel group, then one atomic per
+  // channel per block into this block's replica
+  float* rep = a.sums + (blockIdx.x % kStatRep) * 2 * a.C;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    if (k) __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[e * 256 + tid] = acc[k][e];
+    __syncthreads();
+    for (int idx = tid; idx < Gb * 8; idx += 256) {
+      const int g = idx / 8, e = idx % 8;
+      float s = 0.f;
+      for (int r = 0; r < prows; ++r) s += red[e * 256 + r * Gb + g];
+      atomicAdd(rep + k * a.C + (cg_base + g) * 8 + e, s);
+    }
+  }
 }
 
-template <bool POOL>
+template <bool POOL, int IPT>
 __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(BnArgs a) {
-  __shared__ float red[8 * 256];
-  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int NP = POOL ? 4 : 1;
   const int G = a.C / 8;
   const int Gb = G < 256 ? G : 256;
   const int Ho = POOL ? a.H / 2 : a.H, Wo = POOL ? a.W / 2 : a.W;
@@ -312,52 +283,33 @@ __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(BnArgs a) {
   const int cg_base = blockIdx.y * Gb;
   const int cgl = threadIdx.x % Gb;
   const int prow = threadIdx.x / Gb, prows = 256 / Gb;
-  const float inv_m = 1.f / (float)(a.N * a.H * a.W);
-  float sc[8], sh[8], mu[8], is[8], k1[8], k2[8], gi[8];
   const int c0 = (cg_base + cgl) * 8;
-  const int nch = Gb * 8;
-  block_coeffs(a, cg_base * 8, nch, lds, lds + nch, lds + 2 * nch, lds + 3 * nch);
-  load_coeffs(lds, nch, cgl * 8, sc, sh, mu, is);
+  BwdItems<POOL, IPT> L;
+  bwd_load<POOL, IPT>(a, L, (size_t)blockIdx.x * prows * IPT + prow, prows, npix, cg_base + cgl,
+                      Ho, Wo);
+  float sc[8], sh[8], mu[8], is[8], k1[8], k2[8];
+  ld8f(a.coef + kSc * a.C + c0, sc);
+  ld8f(a.coef + kSh * a.C + c0, sh);
+  ld8f(a.coef + kMu * a.C + c0, mu);
+  ld8f(a.coef + kIs * a.C + c0, is);
+  ld8f(a.coef + kK1 * a.C + c0, k1);
+  ld8f(a.coef + kK2 * a.C + c0, k2);
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    k1[e] = a.sums[c0 + e] * inv_m;
-    k2[e] = a.sums[a.C + c0 + e] * inv_m;
-    gi[e] = a.gamma[c0 + e] * is[e];
-  }
-  // dgamma / dbeta: one contribution per channel from the first block row
-  if (blockIdx.x == 0 && prow == 0) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      if (a.dgamma) atomicAdd(a.dgamma + c0 + e, a.sums[a.C + c0 + e]);
-      if (a.dbeta) atomicAdd(a.dbeta + c0 + e, a.sums[c0 + e]);
-    }
-  }
-  float acc[1][8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) acc[0][e] = 0.f;
-  for (size_t p = blockIdx.x * (size_t)prows + prow; p < npix; p += (size_t)gridDim.x * prows) {
-    constexpr int NP = POOL ? 4 : 1;
-    size_t offs[NP];
+  for (int it = 0; it < IPT; ++it) {
+    if (!L.ok[it]) continue;
     float xh[NP][8], dyb[NP][8];
-    int cg;
-    bwd_item<POOL>(a, p * G + cg_base + cgl, G, Ho, Wo, sc, sh, mu, is, offs, xh, dyb, &cg);
+    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], sc, sh, mu, is, xh, dyb);
 #pragma unroll
     for (int d = 0; d < NP; ++d) {
       u16x8 o, r;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float dz = gi[e] * (dyb[d][e] - k1[e] - xh[d][e] * k2[e]);
-        o[e] = f2bf(dz);
-        acc[0][e] += bf2f(o[e]);
+        o[e] = f2bf(sc[e] * (dyb[d][e] - k1[e] - xh[d][e] * k2[e]));  // sc = gamma * invstd
         r[e] = f2bf(dyb[d][e]);
       }
-      st8(a.dz + offs[d], o);
-      if (a.dres) st8(a.dres + offs[d], r);
+      st8(a.dz + L.off[it][d], o);
+      if (a.dres) st8(a.dres + L.off[it][d], r);
     }
-  }
-  if (a.dbias) {
-    float* dst[1] = {a.dbias};
-    block_reduce_atomic<1>(acc, Gb, cg_base, dst, red);
   }
 }
 
@@ -365,47 +317,62 @@ __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(BnArgs a) {
 
 using namespace ddp_amd;
 
-static int grid_for(size_t items, int cap) {
-  size_t b = (items + 255) / 256;
-  if (b > (size_t)cap) b = cap;
-  if (b < 1) b = 1;
-  return (int)b;
+static unsigned blocks_for(size_t items, size_t per_block) {
+  size_t b = (items + per_block - 1) / per_block;
+  return (unsigned)(b < 1 ? 1 : b);
 }
 
 extern "C" int ddp_bn_act_fwd(const BnArgs* args, hipStream_t st) {
   BnArgs a = *args;
+  if (a.C % 8 || a.coef == nullptr) return -1;
+  if (a.pool && a.res) return -1;  // residual add is only fused without pooling
   const int Ho = a.pool ? a.H / 2 : a.H, Wo = a.pool ? a.W / 2 : a.W;
   const size_t items = (size_t)a.N * Ho * Wo * (a.C / 8);
-  if (a.C % 8) return -1;
-  // each block builds the [scale|shift] table of all C channels in LDS, then streams items
-  hipLaunchKernelGGL(bn_act_fwd_kernel, dim3(grid_for(items / 4, 1024)), dim3(256),
-                     2 * a.C * sizeof(float), st, a);
+  hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3(blocks_for(a.C, 256)), dim3(256), 0, st, a);
+  // 1 item per thread for small layers; 2 (pooled) / 4 (plain) when there are enough to keep
+  // every CU busy with several resident blocks
+  if (a.pool) {
+    if (items >= 256 * 2048)
+      hipLaunchKernelGGL((bn_act_fwd_kernel<true, 2>), dim3(blocks_for(items, 512)), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((bn_act_fwd_kernel<true, 1>), dim3(blocks_for(items, 256)), dim3(256), 0, st, a);
+  } else {
+    if (items >= 256 * 4096)
+      hipLaunchKernelGGL((bn_act_fwd_kernel<false, 4>), dim3(blocks_for(items, 1024)), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((bn_act_fwd_kernel<false, 1>), dim3(blocks_for(items, 256)), dim3(256), 0, st, a);
+  }
   return (int)hipGetLastError();
 }
 
+template <bool POOL, int IPT>
+static void launch_bwd(const BnArgs& a, size_t npix, int Gb, int chunks, hipStream_t st) {
+  const unsigned bx = blocks_for(npix, (size_t)(256 / Gb) * IPT);
+  hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<POOL, IPT>), dim3(bx, chunks), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3(blocks_for(a.C, 256)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT>), dim3(bx, chunks), dim3(256), 0, st, a);
+}
+
+// a.coef must hold the table written by the matching forward; a.sums ([kStatRep][2][C]) must be
+// zero on entry (per-step scratch, zeroed once per forward).
 extern "C" int ddp_bn_act_bwd(const BnArgs* args, hipStream_t st) {
   BnArgs a = *args;
-  if (a.C % 8) return -1;
+  if (a.C % 8 || a.coef == nullptr || a.sums == nullptr) return -1;
+  if (a.pool && a.res) return -1;
   const int G = a.C / 8;
   const int Gb = G < 256 ? G : 256;
   if ((Gb < 256 && 256 % Gb) || (G > 256 && G % 256)) return -1;  // channel groups must tile 256 threads
   const int chunks = (G + Gb - 1) / Gb;
   const int Ho = a.pool ? a.H / 2 : a.H, Wo = a.pool ? a.W / 2 : a.W;
   const size_t npix = (size_t)a.N * Ho * Wo;
-  const size_t rows_per_block = 256 / Gb;
-  // enough blocks to fill the chip, but each thread still loops over several pixels
-  size_t bx = (npix + rows_per_block * 4 - 1) / (rows_per_block * 4);
-  const size_t cap = (size_t)(1024 / chunks > 0 ? 1024 / chunks : 1);
-  const size_t lds = 4 * (size_t)Gb * 8 * sizeof(float);
-  if (bx > cap) bx = cap;
-  if (bx < 1) bx = 1;
-  // a.sums must be zero on entry (the caller's per-step scratch is zeroed once per forward)
+  // one item per thread while that leaves few blocks; two (loads of both issued together) for
+  // the big layers. Pooled items already carry 4 pixels: one per thread keeps registers down.
+  const bool two = !a.pool && npix * chunks / (256 / Gb) >= 4096;
   if (a.pool) {
-    hipLaunchKernelGGL(bn_act_bwd_reduce_kernel<true>, dim3((unsigned)bx, chunks), dim3(256), lds, st, a);
-    hipLaunchKernelGGL(bn_act_bwd_apply_kernel<true>, dim3((unsigned)bx, chunks), dim3(256), lds, st, a);
+    launch_bwd<true, 1>(a, npix, Gb, chunks, st);
   } else {
-    hipLaunchKernelGGL(bn_act_bwd_reduce_kernel<false>, dim3((unsigned)bx, chunks), dim3(256), lds, st, a);
-    hipLaunchKernelGGL(bn_act_bwd_apply_kernel<false>, dim3((unsigned)bx, chunks), dim3(256), lds, st, a);
+    if (two) launch_bwd<false, 2>(a, npix, Gb, chunks, st);
+    else launch_bwd<false, 1>(a, npix, Gb, chunks, st);
   }
   return (int)hipGetLastError();
 }

@@ -54,6 +54,7 @@ struct ConvArgs {
   int Mg, Ng, Kg;            // GEMM dims
   int splits;
   int ksteps_per_split;
+  int wg_atomic;             // WGRAD split-K: fp32 atomics into dw instead of slabs + finish
 };
 
 // ------------------------------------------------------------------ operand gathers
@@ -150,15 +151,32 @@ __device__ __forceinline__ u16x8 gather_x_wgrad(const ConvArgs& A, const KInfo& 
 }
 
 // ------------------------------------------------------------------ LDS addressing
-// [row][k] tile, 64 bf16 per row = 8 chunks of 16 B; chunk XOR (row>>1)&7.
+// [row][k] tile, 64 bf16 per row = 8 chunks of 16 B; chunk XOR (row>>1)&7 (ds_read_b128 reads
+// of 16 consecutive rows at one logical chunk hit 16 distinct slots).
 __device__ __forceinline__ int rk_off(int row, int chunk) {
   return row * 64 + ((chunk ^ ((row >> 1) & 7)) << 3);
 }
-// [m][col] tile with NCOL bf16 per row; chunk XOR (m mod chunks-per-row).
+// [m][col] tile with NCOL bf16 per row (WGRAD), read with ds_read_b64_tr_b16. A half-wave reads
+// rows {m0..m0+3} and {m0+8..m0+11} at the same two 16-B chunks; the XOR makes those 16
+// (row, chunk) pairs land on 16 distinct bank slots (conflict-free).
+template <int NCOL>
+__device__ __forceinline__ int mc_swz(int m) {
+  if (NCOL >= 128) return (((m & 3) | (((m >> 3) & 1) << 2)) << 1) & (NCOL / 8 - 1);
+  return ((((m >> 1) & 1) | (((m >> 3) & 1) << 1)) << 1);  // 8 chunks: row parity splits banks
+}
 template <int NCOL>
 __device__ __forceinline__ int mc_off(int m, int col) {
-  constexpr int NCH = NCOL / 8;
-  return m * NCOL + (((col >> 3) ^ (m & (NCH - 1))) << 3) + (col & 7);
+  return m * NCOL + (((col >> 3) ^ mc_swz<NCOL>(m)) << 3) + (col & 7);
+}
+
+// 16 zero bytes: the source of every LDS-DMA lane whose im2col element lies in the padding.
+__device__ __attribute__((aligned(64))) unsigned short g_zero16[32];
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ void dma16(const void* src, unsigned short* lds_wave_base) {
+  // global_load_lds_dwordx4: LDS destination = wave-uniform base + lane * 16 (no VGPR staging)
+  __builtin_amdgcn_global_load_lds(src, (lds_void*)lds_wave_base, 16, 0, 0);
 }
 
 template <int MODE, int BM, int BN>
@@ -173,7 +191,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
   __shared__ __attribute__((aligned(16))) unsigned short smem[2 * (TILE_A + TILE_B)];
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wid = tid >> 6;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
 
   const int tiles_n = (args.Ng + BN - 1) / BN;
@@ -192,22 +211,46 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  u16x8 ra[CA], rb[CB];
-
-  // Per-thread constants of the gathers. FWD/DGRAD: chunk c = tid + 256 i covers GEMM row
-  // (tid>>3) + 32 i and reduction chunk tid&7 (same for every i). WGRAD: chunk c covers
-  // reduction row c / (BX/8) and channel group tid % (BX/8) (same for every i).
   const ConvGeom& gg = args.g;
-  const float invC = 1.f / (float)(MODE == MODE_FWD ? gg.C : gg.K);
-  const float invS = 1.f / (float)gg.S;
+  const unsigned short* zero = g_zero16;
+
+  // ---------------- per-thread gather state (index math hoisted out of the k-loop) ----------------
+  // FWD/DGRAD: DMA chunk c = tid + 256 i lands at LDS byte 16 c = row (tid>>3)+32i, physical
+  // chunk tid&7; it must carry LOGICAL chunk lc = (tid&7) ^ ((row>>1)&7) = constant per thread.
+  // WGRAD: row = m (reduction), physical chunk tid % (BX/8), logical = phys ^ swz(m) (constant).
+  constexpr int NA = (MODE != MODE_WGRAD) ? CA : 1;
+  int a_rowoff[NA];      // FWD: n*H*W*C + (h0*W + w0)*C ; DGRAD: n*P*Q*K + (h0*Q + w0)*K
+  int a_h0[NA], a_w0[NA];
+  int b_col_ok = 0;      // bit i: B row i valid
+  int lcA, lcB;
+  int kr = 0, ks_ = 0, kc = 0;  // (r, s, c) of this thread's reduction chunk for the current k-step
+  KInfo xk;              // WGRAD: (r,s,c) of this thread's B' column group
   const float invPQ = 1.f / (float)(gg.P * gg.Q), invQ = 1.f / (float)gg.Q;
-  RowInfo rinfo[MODE != MODE_WGRAD ? CA : 1];
-  KInfo xk;  // WGRAD: (r,s,c) of this thread's B' column group
   if (MODE != MODE_WGRAD) {
+    lcA = lcB = (tid & 7) ^ ((tid >> 4) & 7);
 #pragma unroll
-    for (int i = 0; i < CA; ++i) rinfo[i] = row_info<MODE>(args, row0 + (tid >> 3) + 32 * i);
+    for (int i = 0; i < CA; ++i) {
+      const RowInfo ri = row_info<MODE>(args, row0 + (tid >> 3) + 32 * i);
+      a_h0[i] = ri.h0;
+      a_w0[i] = ri.w0;
+      a_rowoff[i] = (MODE == MODE_FWD) ? ri.base + (ri.h0 * gg.W + ri.w0) * gg.C
+                                       : ri.base + (ri.h0 * gg.Q + ri.w0) * gg.K;
+    }
+#pragma unroll
+    for (int i = 0; i < CB; ++i)
+      if (col0 + (tid >> 3) + 32 * i < args.Ng) b_col_ok |= 1 << i;
+    // decomposition of the first reduction index this thread loads
+    const int cdim = MODE == MODE_FWD ? gg.C : gg.K;
+    const int kk = ks_begin * BK + lcA * 8;
+    const int rs = kk / cdim;
+    kc = kk - rs * cdim;
+    kr = rs / gg.S;
+    ks_ = rs - kr * gg.S;
   } else {
-    const int j = col0 + (tid % (BN / 8)) * 8;
+    constexpr int NCA = BM / 8, NCB = BN / 8;
+    lcA = (tid % NCA) ^ mc_swz<BM>(tid / NCA);
+    lcB = (tid % NCB) ^ mc_swz<BN>(tid / NCB);
+    const int j = col0 + lcB * 8;
     const int rs = j / gg.C;
     xk.c = j - rs * gg.C;
     xk.r = rs / gg.S;
@@ -215,60 +258,96 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
     xk.ok = j < args.Ng;
   }
 
-  auto gload = [&](int ks) {
+  // issue the LDS-DMA of k-step ks into buffer buf (and advance the incremental k state)
+  auto issue = [&](int ks, int buf) {
+    unsigned short* As = smem + buf * (TILE_A + TILE_B);
+    unsigned short* Bs = As + TILE_A;
     const int k0 = ks * BK;
     if (MODE != MODE_WGRAD) {
-      const int kk = k0 + (tid & 7) * 8;
-      const KInfo k = k_info<MODE>(args, kk, invC, invS);
+      const int kk = k0 + lcA * 8;
+      const bool kok = kk < args.Kg;
+      const int W_ = MODE == MODE_FWD ? gg.W : gg.Q;
+      const int cdim = MODE == MODE_FWD ? gg.C : gg.K;
+      const int tap = MODE == MODE_FWD ? (kr * W_ + ks_) * cdim + kc : kc - (kr * W_ + ks_) * cdim;
 #pragma unroll
-      for (int i = 0; i < CA; ++i) ra[i] = gather_a<MODE>(args, rinfo[i], k);
+      for (int i = 0; i < CA; ++i) {
+        const void* src = zero;
+        if (MODE == MODE_FWD) {
+          const int h = a_h0[i] + kr, w = a_w0[i] + ks_;
+          if (kok && (unsigned)h < (unsigned)gg.H && (unsigned)w < (unsigned)gg.W)
+            src = args.a + a_rowoff[i] + tap;
+        } else {
+          int ph = a_h0[i] - kr, pw = a_w0[i] - ks_;
+          bool ok = kok && ph >= 0 && pw >= 0;
+          if (gg.stride == 1) {
+            ok = ok && ph < gg.P && pw < gg.Q;
+            if (ok) src = args.a + a_rowoff[i] + tap;
+          } else {  // strided conv: only taps that hit an output pixel contribute
+            ok = ok && (ph % gg.stride) == 0 && (pw % gg.stride) == 0;
+            ph /= gg.stride;
+            pw /= gg.stride;
+            ok = ok && ph < gg.P && pw < gg.Q;
+            if (ok) {
+              const int base = a_rowoff[i] - (a_h0[i] * gg.Q + a_w0[i]) * gg.K;
+              src = args.a + base + (ph * gg.Q + pw) * gg.K + kc;
+            }
+          }
+        }
+        dma16(src, As + (wid * 64 + 256 * i) * 8);
+      }
 #pragma unroll
       for (int i = 0; i < CB; ++i) {
         const int col = col0 + (tid >> 3) + 32 * i;
-        u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-        rb[i] = (col < args.Ng && kk < args.Kg) ? ld8(args.b + (size_t)col * args.Kg + kk) : z;
+        const void* src = (kok && ((b_col_ok >> i) & 1)) ? (const void*)(args.b + (size_t)col * args.Kg + kk) : zero;
+        dma16(src, Bs + (wid * 64 + 256 * i) * 8);
+      }
+      // advance (r, s, c) by BK reduction elements
+      kc += BK;
+      while (kc >= cdim) {
+        kc -= cdim;
+        if (++ks_ == gg.S) { ks_ = 0; ++kr; }
       }
     } else {
-      const int kc = row0 + (tid % (BM / 8)) * 8;
+      constexpr int NCA = BM / 8, NCB = BN / 8;
+      const int kout = row0 + lcA * 8;
 #pragma unroll
-      for (int i = 0; i < CA; ++i) {  // dy[m][kout]: row of BM channels per m
-        const int m = k0 + (tid + i * 256) / (BM / 8);
-        u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-        ra[i] = (m < args.Kg && kc < args.Mg) ? ld8(args.a + (size_t)m * gg.K + kc) : z;
+      for (int i = 0; i < CA; ++i) {  // dy[m][kout]
+        const int m = k0 + (tid + i * 256) / NCA;
+        const void* src = (m < args.Kg && kout < args.Mg) ? (const void*)(args.a + (size_t)m * gg.K + kout) : zero;
+        dma16(src, As + (wid * 64 + 256 * i) * 8);
       }
 #pragma unroll
-      for (int i = 0; i < CB; ++i)
-        rb[i] = gather_x_wgrad(args, xk, k0 + (tid + i * 256) / (BN / 8), invPQ, invQ);
+      for (int i = 0; i < CB; ++i) {  // x gather at pixel m for columns (r, s, c..c+7)
+        const int m = k0 + (tid + i * 256) / NCB;
+        const void* src = zero;
+        if (xk.ok && m < args.Kg) {
+          const int pq = gg.P * gg.Q;
+          const int n = fdiv(m, pq, invPQ), rem = m - n * pq;
+          const int p = fdiv(rem, gg.Q, invQ), q = rem - p * gg.Q;
+          const int h = p * gg.stride - gg.pad + xk.r, w = q * gg.stride - gg.pad + xk.s;
+          if ((unsigned)h < (unsigned)gg.H && (unsigned)w < (unsigned)gg.W)
+            src = args.b + ((n * gg.H + h) * gg.W + w) * gg.C + xk.c;
+        }
+        dma16(src, Bs + (wid * 64 + 256 * i) * 8);
+      }
     }
   };
 
-  auto lstore = [&](int buf) {
-    unsigned short* As = smem + buf * (TILE_A + TILE_B);
-    unsigned short* Bs = As + TILE_A;
-    if (MODE != MODE_WGRAD) {
+  // fragment LDS offsets (elements), loop-invariant
+  int fa_off[TM], fb_off[TN];
+  if (MODE != MODE_WGRAD) {
 #pragma unroll
-      for (int i = 0; i < CA; ++i) {
-        const int c = tid + i * 256;
-        st8(As + rk_off(c >> 3, c & 7), ra[i]);
-      }
+    for (int i = 0; i < TM; ++i) fa_off[i] = rk_off(wm * WTM + i * 16 + (lane & 15), lane >> 4);
 #pragma unroll
-      for (int i = 0; i < CB; ++i) {
-        const int c = tid + i * 256;
-        st8(Bs + rk_off(c >> 3, c & 7), rb[i]);
-      }
-    } else {
+    for (int j = 0; j < TN; ++j) fb_off[j] = rk_off(wn * WTN + j * 16 + (lane & 15), lane >> 4);
+  } else {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int m0 = 8 * g + q;
 #pragma unroll
-      for (int i = 0; i < CA; ++i) {
-        const int c = tid + i * 256;
-        st8(As + mc_off<BM>(c / (BM / 8), (c % (BM / 8)) * 8), ra[i]);
-      }
+    for (int i = 0; i < TM; ++i) fa_off[i] = mc_off<BM>(m0, wm * WTM + i * 16 + 4 * p);
 #pragma unroll
-      for (int i = 0; i < CB; ++i) {
-        const int c = tid + i * 256;
-        st8(Bs + mc_off<BN>(c / (BN / 8), (c % (BN / 8)) * 8), rb[i]);
-      }
-    }
-  };
+    for (int j = 0; j < TN; ++j) fb_off[j] = mc_off<BN>(m0, wn * WTN + j * 16 + 4 * p);
+  }
 
   auto compute = [&](int buf) {
     const unsigned short* As = smem + buf * (TILE_A + TILE_B);
@@ -277,31 +356,30 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
     for (int kk = 0; kk < BK; kk += 32) {
       bf16x8 fa[TM], fb[TN];
       if (MODE != MODE_WGRAD) {
-        const int ch = (kk >> 3) + (lane >> 4);
+        // logical chunk kk/8 + (lane>>4): the XOR swizzle is linear in the chunk index, so the
+        // kk = 32 read is the kk = 0 address with chunk bit 2 flipped
 #pragma unroll
         for (int i = 0; i < TM; ++i)
-          fa[i] = *reinterpret_cast<const bf16x8*>(As + rk_off(wm * WTM + i * 16 + (lane & 15), ch));
+          fa[i] = *reinterpret_cast<const bf16x8*>(As + (fa_off[i] ^ (kk ? 32 : 0)));
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          fb[j] = *reinterpret_cast<const bf16x8*>(Bs + rk_off(wn * WTN + j * 16 + (lane & 15), ch));
+          fb[j] = *reinterpret_cast<const bf16x8*>(Bs + (fb_off[j] ^ (kk ? 32 : 0)));
       } else {
         // ds_read_b64_tr_b16: lane 4q+p of each 16-lane group supplies row q, columns 4p..4p+3;
         // lane i receives column i of the 4 rows. Two reads give the 8 k-values of a fragment.
-        const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-        const int m0 = kk + 8 * g + q;
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
-          const int col = wm * WTM + i * 16 + 4 * p;
-          v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(As + mc_off<BM>(m0, col)));
-          v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(As + mc_off<BM>(m0 + 4, col)));
+          const unsigned short* base = As + fa_off[i] + kk * BM;
+          v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)base);
+          v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + 4 * BM));
           const short8_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
           fa[i] = __builtin_bit_cast(bf16x8, v);
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          const int col = wn * WTN + j * 16 + 4 * p;
-          v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(Bs + mc_off<BN>(m0, col)));
-          v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(Bs + mc_off<BN>(m0 + 4, col)));
+          const unsigned short* base = Bs + fb_off[j] + kk * BN;
+          v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)base);
+          v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + 4 * BN));
           const short8_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
           fb[j] = __builtin_bit_cast(bf16x8, v);
         }
@@ -310,74 +388,103 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+          // operands swapped (D^T = B^T A^T): each lane ends up owning ONE output row and FOUR
+          // consecutive output columns, so the epilogue stores 8 B (bf16) / 16 B (fp32) per lane
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
     }
   };
 
   if (ks_begin < ks_end) {
-    gload(ks_begin);
-    lstore(0);
-    __syncthreads();
+    issue(ks_begin, 0);
+    __syncthreads();  // waits for the DMA (vmcnt(0)) and publishes buffer 0
     int buf = 0;
     for (int ks = ks_begin; ks < ks_end; ++ks) {
-      const bool more = ks + 1 < ks_end;
-      if (more) gload(ks + 1);  // in flight during the MFMA phase
+      if (ks + 1 < ks_end) issue(ks + 1, buf ^ 1);  // lands during this step's MFMAs
       compute(buf);
-      if (more) lstore(buf ^ 1);  // the other buffer was last read before the previous barrier
-      __syncthreads();
+      __syncthreads();  // next buffer landed + everyone done reading this one
       buf ^= 1;
     }
   }
 
   // ---------------- epilogue ----------------
+  // acc[i][j][v] = D[row0 + wm*WTM + i*16 + (lane&15)][col0 + wn*WTN + j*16 + 4*(lane>>4) + v]
+  // Ng % 8 == 0 for every mode (C, K multiples of 8), so a lane's 4 columns are all valid or not.
   const ConvGeom& g = args.g;
   const bool split = args.splits > 1;
   float* slab = split ? args.ws + (size_t)blockIdx.z * args.Mg * args.Ng : nullptr;
+  const int rl = lane & 15, cq = 4 * (lane >> 4);
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int col = col0 + wn * WTN + j * 16 + (lane & 15);
+    const int col = col0 + wn * WTN + j * 16 + cq;
     const bool cok = col < args.Ng;
-    float bias = 0.f;
-    if (MODE == MODE_FWD && !split && args.bias && cok) bias = args.bias[col];
-    float s = 0.f, ss = 0.f;
-    int wr = 0, wsx = 0, wc = 0;
-    if (MODE == MODE_WGRAD) {
-      const int rs = col / g.C;
-      wc = col - rs * g.C;
-      wr = rs / g.S;
-      wsx = rs - wr * g.S;
+    float4 bias = {0.f, 0.f, 0.f, 0.f};
+    if (MODE == MODE_FWD && !split && args.bias && cok)
+      bias = (float4){args.bias[col], args.bias[col + 1], args.bias[col + 2], args.bias[col + 3]};
+    float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
+    int wrs = 0, wc = 0;
+    if (MODE == MODE_WGRAD) {  // GEMM column -> (r*S + s, c); c..c+3 share the tap
+      wrs = col / g.C;
+      wc = col - wrs * g.C;
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
+      const int row = row0 + wm * WTM + i * 16 + rl;
+      if (!cok || row >= args.Mg) continue;
+      const f32x4 v = acc[i][j];
+      if (MODE == MODE_WGRAD && (!split || args.wg_atomic)) {
+        if (g.wkrsc && g.Creal == g.C) {
+          float* d = args.dw + ((size_t)row * g.R * g.S + wrs) * g.C + wc;
+          if (split) {
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int row = row0 + wm * WTM + i * 16 + 4 * (lane >> 4) + v;
-        if (!cok || row >= args.Mg) continue;
-        const float val = acc[i][j][v];
-        if (split) {
-          slab[(size_t)row * args.Ng + col] = val;
-        } else if (MODE == MODE_WGRAD) {
-          if (wc < g.Creal) args.dw[(((size_t)row * g.Creal + wc) * g.R + wr) * g.S + wsx] += val;
-        } else {
-          const unsigned short h = f2bf(val + bias);
-          args.out[(size_t)row * args.Ng + col] = h;
-          if (MODE == MODE_FWD) {
-            const float r = bf2f(h);
-            s += r;
-            ss += r * r;
+            for (int t = 0; t < 4; ++t) unsafeAtomicAdd(d + t, v[t]);
+          } else {
+            float4 o = *reinterpret_cast<float4*>(d);
+            o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
+            *reinterpret_cast<float4*>(d) = o;
           }
+        } else {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            if (wc + t >= g.Creal) break;
+            const size_t di = g.wkrsc ? ((size_t)row * g.R * g.S + wrs) * g.Creal + wc + t
+                                      : ((size_t)row * g.Creal + wc + t) * g.R * g.S + wrs;
+            if (split) unsafeAtomicAdd(args.dw + di, v[t]);
+            else args.dw[di] += v[t];
+          }
+        }
+      } else if (split) {
+        *reinterpret_cast<float4*>(slab + (size_t)row * args.Ng + col) = (float4){v[0], v[1], v[2], v[3]};
+      } else {
+        const unsigned short h0 = f2bf(v[0] + bias.x), h1 = f2bf(v[1] + bias.y);
+        const unsigned short h2 = f2bf(v[2] + bias.z), h3 = f2bf(v[3] + bias.w);
+        uint2 pk;
+        pk.x = (unsigned)h0 | ((unsigned)h1 << 16);
+        pk.y = (unsigned)h2 | ((unsigned)h3 << 16);
+        *reinterpret_cast<uint2*>(args.out + (size_t)row * args.Ng + col) = pk;
+        if (MODE == MODE_FWD) {
+          const float r0 = bf2f(h0), r1 = bf2f(h1), r2 = bf2f(h2), r3 = bf2f(h3);
+          s[0] += r0; s[1] += r1; s[2] += r2; s[3] += r3;
+          ss[0] += r0 * r0; ss[1] += r1 * r1; ss[2] += r2 * r2; ss[3] += r3 * r3;
         }
       }
     }
     if (MODE == MODE_FWD && !split && args.stats) {
-      s += __shfl_xor(s, 16, kWave);
-      s += __shfl_xor(s, 32, kWave);
-      ss += __shfl_xor(ss, 16, kWave);
-      ss += __shfl_xor(ss, 32, kWave);
-      if ((lane >> 4) == 0 && cok) {
+      // reduce over the 16 rows held by lanes (lane & 15) of each 16-lane group
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+#pragma unroll
+        for (int m = 1; m < 16; m <<= 1) {
+          s[t] += __shfl_xor(s[t], m, kWave);
+          ss[t] += __shfl_xor(ss[t], m, kWave);
+        }
+      }
+      if (rl == 0 && cok) {
         float* st = args.stats + (blockIdx.x % kStatRep) * 2 * args.Ng;  // spread contention
-        atomicAdd(st + col, s);
-        atomicAdd(st + args.Ng + col, ss);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          atomicAdd(st + col + t, s[t]);
+          atomicAdd(st + args.Ng + col + t, ss[t]);
+        }
       }
     }
   }
@@ -476,15 +583,61 @@ __global__ __launch_bounds__(256) void wgrad_finish_kernel(const float* ws, int 
   }
 }
 
+// Split-K finish for WGRAD into a [K][R][S][Cr] gradient: the GEMM row IS the gradient row, so
+// this is a vectorised sum of the slabs — no transpose. blockIdx.y = group of kWgFinishGroupKrsc
+// slabs (fixed order inside a group); several groups combine with atomics.
+constexpr int kWgFinishGroupKrsc = 16;
+__global__ __launch_bounds__(256) void wgrad_finish_krsc_kernel(const float* __restrict__ ws,
+                                                                int splits, int K, int RS, int C,
+                                                                int Creal, float* __restrict__ dw) {
+  const size_t slab = (size_t)K * RS * C;
+  const size_t n4 = slab / 4;
+  const int z0 = blockIdx.y * kWgFinishGroupKrsc, z1 = min(splits, z0 + kWgFinishGroupKrsc);
+  const bool single = gridDim.y == 1;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4;
+       i += (size_t)gridDim.x * blockDim.x) {
+    float4 v = reinterpret_cast<const float4*>(ws + z0 * slab)[i];
+    for (int z = z0 + 1; z < z1; ++z) {
+      const float4 a = reinterpret_cast<const float4*>(ws + z * slab)[i];
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    }
+    const float vv[4] = {v.x, v.y, v.z, v.w};
+    if (Creal == C) {
+      if (single) {
+        float4* o = reinterpret_cast<float4*>(dw) + i;
+        float4 d = *o;
+        d.x += v.x; d.y += v.y; d.z += v.z; d.w += v.w;
+        *o = d;
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) unsafeAtomicAdd(dw + i * 4 + t, vv[t]);
+      }
+    } else {  // channel-padded input layer: drop the pad channels
+      const size_t e = i * 4;
+      const int c = (int)(e % C);
+      const size_t krs = e / C;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (c + t >= Creal) continue;
+        if (single) dw[krs * Creal + c + t] += vv[t];
+        else unsafeAtomicAdd(dw + krs * Creal + c + t, vv[t]);
+      }
+    }
+  }
+}
+
 }  // namespace ddp_amd
 
 // ------------------------------- host launcher -------------------------------
 using namespace ddp_amd;
 
+constexpr int kMaxAtomicSplits = 32;
+
 // Split-K factor for a tile config: aim for >= 2 workgroups per CU, keep >= 4 k-steps per
 // split, fit the slab workspace.
 static int pick_splits(int tiles, int ksteps, size_t slab, const ConvArgs& a, size_t ws_elems) {
   if (a.splits > 0) return std::max(1, std::min(a.splits, ksteps));
+
   if (a.ws == nullptr) return 1;
   int s = (512 + tiles - 1) / tiles;
   s = std::max(1, std::min(s, ksteps / 4));
@@ -508,8 +661,12 @@ static double tile_cost(int BM, int BN, const ConvArgs& a, size_t ws_elems, int*
   // padded work actually issued
   const double work = (double)tiles * BM * BN * ksteps * 64.0;
   const double t_mfma = work / (eff * fill) / 1.0e15 * 2.0;
-  // slab write + read at ~4 TB/s plus the finish launch (~3 us)
-  const double t_split = splits > 1 ? 8.0 * splits * (double)slab / 4.0e12 + 3.0e-6 : 0.0;
+  // slab write + read at ~4 TB/s plus the finish launch (~3 us); atomics: one RMW per element
+  // per split, no finish pass
+  double t_split = 0.0;
+  if (splits > 1)
+    t_split = (a.wg_atomic && splits <= kMaxAtomicSplits) ? 4.0 * splits * (double)slab / 1.3e12
+                          : 8.0 * splits * (double)slab / 4.0e12 + 3.0e-6;
   return t_mfma + t_split;
 }
 
@@ -522,10 +679,20 @@ static void launch_cfg(ConvArgs& a, int splits, hipStream_t st) {
   splits = (ksteps + per - 1) / per;
   a.splits = splits;
   a.ksteps_per_split = per;
+  // same-address fp32 atomics serialise: beyond kMaxAtomicSplits partial sums per element the
+  // slab + grouped-finish reduction is cheaper
+  if (a.wg_atomic && splits > kMaxAtomicSplits) a.wg_atomic = 0;
   dim3 grid(tiles, 1, splits);
   hipLaunchKernelGGL((conv_igemm_kernel<MODE, BM, BN>), grid, dim3(256), 0, st, a);
   if (splits == 1) return;
-  if (MODE == MODE_WGRAD) {
+  if (MODE == MODE_WGRAD && a.wg_atomic) return;
+  if (MODE == MODE_WGRAD && a.g.wkrsc) {
+    const size_t n4 = (size_t)a.Mg * a.Ng / 4;
+    const int groups = (splits + kWgFinishGroupKrsc - 1) / kWgFinishGroupKrsc;
+    const int bx = (int)std::min<size_t>((n4 + 255) / 256, std::max(1, 2048 / groups));
+    hipLaunchKernelGGL(wgrad_finish_krsc_kernel, dim3(bx, groups), dim3(256), 0, st, a.ws, splits,
+                       a.g.K, a.g.R * a.g.S, a.g.C, a.g.Creal, a.dw);
+  } else if (MODE == MODE_WGRAD) {
     const int groups = (splits + kWgFinishGroup - 1) / kWgFinishGroup;
     const size_t lds = sizeof(float) * a.g.R * a.g.S * a.g.C;
     hipLaunchKernelGGL(wgrad_finish_kernel, dim3(a.g.K, groups), dim3(256), lds, st, a.ws, splits,
@@ -559,6 +726,9 @@ static void launch_mode(ConvArgs& a, size_t ws_elems, hipStream_t st) {
     default: launch_cfg<MODE, 64, 64>(a, sp[3], st); break;
   }
 }
+
+static int g_wgrad_atomic = 0;
+extern "C" void ddp_conv_options(int wgrad_atomic) { g_wgrad_atomic = wgrad_atomic; }
 
 extern "C" int ddp_conv_fwd(const ConvGeom* g, const void* x, const void* wc, const float* bias,
                             void* y, float* stats, float* ws, size_t ws_elems, int splits,
@@ -606,6 +776,7 @@ extern "C" int ddp_conv_wgrad(const ConvGeom* g, const void* dy, const void* x, 
   a.b = (const unsigned short*)x;
   a.dw = dw;
   a.ws = ws;
+  a.wg_atomic = g_wgrad_atomic;
   a.Mg = g->K;
   a.Ng = g->R * g->S * g->C;
   a.Kg = g->N * g->P * g->Q;

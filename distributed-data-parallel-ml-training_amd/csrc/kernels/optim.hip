@@ -58,6 +58,11 @@ struct PackTable {
   int n;
 };
 
+__device__ __forceinline__ size_t master_index(const PackDesc& d, int k, int c, int r, int s) {
+  return d.krsc ? (((size_t)k * d.R + r) * d.S + s) * d.Cr + c
+                : (((size_t)k * d.Cr + c) * d.R + r) * d.S + s;
+}
+
 __global__ __launch_bounds__(256) void pack_conv_weights_kernel(PackTable t) {
   const PackDesc d = t.d[blockIdx.y];
   const int rs = d.R * d.S;
@@ -71,7 +76,7 @@ __global__ __launch_bounds__(256) void pack_conv_weights_kernel(PackTable t) {
       const size_t t2 = t1 / d.S;
       const int r = (int)(t2 % d.R);
       const int k = (int)(t2 / d.R);
-      const float v = c < d.Cr ? d.p[(((size_t)k * d.Cr + c) * d.R + r) * d.S + s] : 0.f;
+      const float v = c < d.Cr ? d.p[master_index(d, k, c, r, s)] : 0.f;
       d.wc[i] = f2bf(v);
     }
     if (d.wt) {  // i indexes Wt [c][r][s][k]
@@ -81,7 +86,7 @@ __global__ __launch_bounds__(256) void pack_conv_weights_kernel(PackTable t) {
       const size_t t2 = t1 / d.S;
       const int r = (int)(t2 % d.R);
       const int c = (int)(t2 / d.R);
-      const float v = c < d.Cr ? d.p[(((size_t)k * d.Cr + c) * d.R + r) * d.S + s] : 0.f;
+      const float v = c < d.Cr ? d.p[master_index(d, k, c, r, s)] : 0.f;
       d.wt[i] = f2bf(v);
     }
   }
@@ -93,7 +98,8 @@ __global__ __launch_bounds__(256) void pack_conv_weights_kernel(PackTable t) {
 // fp32 weights). Work items (int4): {0, offset, count, -} = plain elementwise chunk;
 // {1, desc, k0, c0} = one TK x TC x (R*S) tile of a conv weight, staged through LDS so that
 // both the Wc ([k][r][s][c], c fastest) and Wt ([c][r][s][k], k fastest) writes are coalesced.
-// Conv descriptor (int64 x 8): {p_offset, K, Cr, C, R, S, wc_ptr, wt_ptr}.
+// Conv descriptor (int64 x 12): {p_offset, K, Cr, C, R, S, wc_ptr, wt_ptr, krsc, -, -, -};
+// krsc selects the fp32 master layout ([K][R][S][Cr] vs [K][Cr][R][S]).
 constexpr int kTileElems = 9216;  // fp32 LDS tile (36 KB)
 
 __device__ __forceinline__ void tile_dims(int RS, int* TK, int* TC) {
@@ -148,7 +154,7 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(const int4* __restrict__ 
     }
     return;
   }
-  const long long* d = descs + 8 * it.y;
+  const long long* d = descs + 12 * it.y;
   const size_t poff = (size_t)d[0];
   const int K = (int)d[1], Cr = (int)d[2], C = (int)d[3], R = (int)d[4], S = (int)d[5];
   unsigned short* wc = reinterpret_cast<unsigned short*>(d[6]);
@@ -160,16 +166,31 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(const int4* __restrict__ 
   const int tk = min(TK, K - k0);
   const int tcr = max(0, min(TC, Cr - c0));  // real channels in this tile
   const int tcp = min(TC, C - c0);           // padded channels in this tile (Wc width)
-  // 1) SGD on p[k][c][r][s] for the tile's real channels; runs of tcr*RS contiguous floats
-  const int run = tcr * RS;
-  for (int idx = tid; idx < tk * run; idx += 256) {
-    const int kl = idx / run, e = idx - kl * run;
-    const size_t gi = poff + (size_t)(k0 + kl) * Cr * RS + (size_t)c0 * RS + e;
-    float b = buf[gi];
-    const float np = sgd1(p[gi], g[gi], b, h);
-    p[gi] = np;
-    buf[gi] = b;
-    tile[kl * TC * RS + e] = np;  // tile layout [kl][cl][rs]
+  const bool krsc = d[8] != 0;
+  if (!krsc) {
+    // 1) SGD on p[k][c][r][s] for the tile's real channels; runs of tcr*RS contiguous floats
+    const int run = tcr * RS;
+    for (int idx = tid; idx < tk * run; idx += 256) {
+      const int kl = idx / run, e = idx - kl * run;
+      const size_t gi = poff + (size_t)(k0 + kl) * Cr * RS + (size_t)c0 * RS + e;
+      float b = buf[gi];
+      const float np = sgd1(p[gi], g[gi], b, h);
+      p[gi] = np;
+      buf[gi] = b;
+      tile[kl * TC * RS + e] = np;  // tile layout [kl][cl][rs]
+    }
+  } else {
+    // 1) SGD on p[k][r][s][c]: runs of tcr contiguous channels per (k, r, s)
+    for (int idx = tid; idx < tk * RS * tcr; idx += 256) {
+      const int cl = idx % tcr, t = idx / tcr;
+      const int rs = t % RS, kl = t / RS;
+      const size_t gi = poff + ((size_t)(k0 + kl) * RS + rs) * Cr + c0 + cl;
+      float b = buf[gi];
+      const float np = sgd1(p[gi], g[gi], b, h);
+      p[gi] = np;
+      buf[gi] = b;
+      tile[kl * TC * RS + cl * RS + rs] = np;
+    }
   }
   __syncthreads();
   // 2) Wc[k][r][s][c] (c fastest, zero for padded channels)

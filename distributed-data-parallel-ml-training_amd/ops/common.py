@@ -1,4 +1,6 @@
 """Shared helpers for the op wrappers: native handle, raw pointers, streams, grad-ready hooks."""
+import os
+
 import torch
 
 from .._ext import load as _load
@@ -10,7 +12,19 @@ def native():
     global _NATIVE
     if _NATIVE is None:
         _NATIVE = _load()
+        # DDP_AMD_WGRAD_ATOMIC=1: split-K weight gradients accumulate with fp32 atomics (no
+        # finish pass, but memory-side atomics run at ~1.3 TB/s vs ~6 TB/s for slab stores);
+        # default 0 = slab + grouped finish reduction
+        _NATIVE.conv_options(int(os.environ.get("DDP_AMD_WGRAD_ATOMIC", "0")))
     return _NATIVE
+
+
+def weight_krsc(w):
+    """1 if a 4-D fp32 weight (or weight gradient) is stored [K][R][S][C] (the GPU arena layout,
+    optim/arena.py), 0 for the standard [K][C][R][S]. 1x1 kernels: both layouts coincide -> 0."""
+    if w is None or w.dim() != 4 or w.shape[2] * w.shape[3] == 1 or w.shape[1] == 1:
+        return 0
+    return int(w.stride(1) == 1)
 
 
 def ptr(t):
@@ -127,6 +141,7 @@ def ensure_grad(p):
     if p.grad is None:
         p.grad = torch.zeros_like(p, memory_format=torch.contiguous_format)
     g = p.grad
-    if not g.is_contiguous() or g.dtype != torch.float32:
-        raise ValueError("fused kernels need contiguous fp32 .grad buffers")
+    dense = g.is_contiguous() or (g.dim() == 4 and g.is_contiguous(memory_format=torch.channels_last))
+    if not dense or g.dtype != torch.float32:
+        raise ValueError("fused kernels need dense fp32 .grad buffers ([K][C][R][S] or [K][R][S][C])")
     return g

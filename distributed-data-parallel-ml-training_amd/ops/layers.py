@@ -14,7 +14,7 @@ Activations between blocks are NHWC bf16; the first conv's input is zero-padded 
 import torch
 
 from .common import (native, ptr, stream_handle, check, grad_ready, ensure_grad, workspace,
-                     step_scratch, STAT_REPLICAS)
+                     step_scratch, weight_krsc, STAT_REPLICAS)
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -50,11 +50,15 @@ class ConvBNActSpec:
         sc = step_scratch(dev)
         self.scratch = sc
         self.stats = sc.take(STAT_REPLICAS * 2 * K)[:STAT_REPLICAS * 2 * K]
-        self.sums = sc.take(2 * K)[:2 * K]
+        self.sums = sc.take(STAT_REPLICAS * 2 * K)[:STAT_REPLICAS * 2 * K]
+        # per-layer BN coefficient table [6][K] (scale, shift, mean, invstd | k1, k2): written
+        # by the forward's finalize kernel, read by the backward (one use per step per layer)
+        self.coef = torch.empty(6 * K, dtype=F32, device=dev)
 
     def pack_desc(self):
-        return (ptr(self.conv.weight), ptr(self.wc), ptr(self.wt), self.K, self.Cr, self.C,
-                self.R, self.S)
+        w = self.conv.weight
+        return (ptr(w), ptr(self.wc), ptr(self.wt), self.K, self.Cr, self.C,
+                self.R, self.S, weight_krsc(w))
 
     def maybe_pack(self):
         w = self.conv.weight
@@ -68,9 +72,10 @@ class ConvBNActSpec:
         Q = (W + 2 * self.pad - self.S) // self.stride + 1
         return P, Q
 
-    def geom(self, N, H, W):
+    def geom(self, N, H, W, wkrsc=0):
         P, Q = self.out_hw(H, W)
-        return (N, H, W, self.C, self.K, self.R, self.S, self.stride, self.pad, P, Q, self.Cr)
+        return (N, H, W, self.C, self.K, self.R, self.S, self.stride, self.pad, P, Q, self.Cr,
+                wkrsc)
 
 
 def conv_forward(spec, x, bias=None, stats=None):
@@ -91,7 +96,7 @@ def conv_forward(spec, x, bias=None, stats=None):
 
 def conv_backward(spec, x, dz, dweight, need_dx):
     N, H, W, C = x.shape
-    g = spec.geom(N, H, W)
+    g = spec.geom(N, H, W, weight_krsc(dweight))
     s = stream_handle()
     ws = workspace(x.device)
     native().conv_wgrad(g, ptr(dz), ptr(x), ptr(dweight), ptr(ws), ws.numel(), 0, s)
@@ -125,7 +130,8 @@ class _ConvBNActFn(torch.autograd.Function):
         native().bn_act_fwd(N, P, Q, spec.K, int(spec.pool), int(spec.relu), spec.eps, ptr(z),
                             ptr(residual), ptr(stats), ptr(gamma), ptr(beta), ptr(y),
                             stream_handle(), ptr(rm), ptr(rv),
-                            float(bn.momentum if bn.momentum is not None else 0.1), use_running)
+                            float(bn.momentum if bn.momentum is not None else 0.1), use_running,
+                            ptr(spec.coef))
         ctx.spec = spec
         ctx.has_res = residual is not None
         ctx.save_for_backward(x, z, stats, weight, bias, gamma, beta, residual)
@@ -146,7 +152,8 @@ class _ConvBNActFn(torch.autograd.Function):
         gbt = ensure_grad(beta)
         native().bn_act_bwd(N, P, Q, K, int(spec.pool), int(spec.relu), spec.eps, ptr(z),
                             ptr(residual), ptr(stats), ptr(gamma), ptr(beta), ptr(dy), ptr(sums),
-                            ptr(dz), ptr(dres), ptr(gg), ptr(gbt), ptr(gb), stream_handle())
+                            ptr(dz), ptr(dres), ptr(gg), ptr(gbt), ptr(gb), stream_handle(),
+                            ptr(spec.coef))
         grad_ready([gamma, beta, bias])
         dx = conv_backward(spec, x, dz, gw, ctx.needs_input_grad[0])
         grad_ready([weight])

@@ -43,11 +43,11 @@ class FusedSGD(torch.optim.SGD):
         for i, p in enumerate(a.params):
             if not hasattr(p, "_ddp_amd_pack"):
                 continue
-            pp, wc, wt, K, Cr, C, R, S = p._ddp_amd_pack()
-            if pp != a.data.data_ptr() + 4 * a.offsets[i]:
+            pp, wc, wt, K, Cr, C, R, S, krsc = p._ddp_amd_pack()
+            if pp != a.data.data_ptr() + 4 * a.offsets[i] or (R * S > 1 and bool(krsc) != a.krsc[i]):
                 raise RuntimeError("packed conv weight is not a view into the parameter arena")
             d = len(descs)
-            descs.append([a.offsets[i], K, Cr, C, R, S, wc, wt])
+            descs.append([a.offsets[i], K, Cr, C, R, S, wc, wt, int(krsc), 0, 0, 0])
             TK, TC = native().sgd_tile_dims(R * S)
             for k0 in range(0, K, TK):
                 for c0 in range(0, C, TC):
@@ -62,7 +62,7 @@ class FusedSGD(torch.optim.SGD):
                 items.append([0, o + s, min(chunk, n - s), 0])
         dev = a.data.device
         self._items = torch.tensor(items, dtype=torch.int32, device=dev)
-        self._descs = torch.tensor(descs if descs else [[0] * 8], dtype=torch.int64, device=dev)
+        self._descs = torch.tensor(descs if descs else [[0] * 12], dtype=torch.int64, device=dev)
         self._n_items = len(items)
         self._table_key = key
         return self._items, self._n_items, self._descs
@@ -95,8 +95,7 @@ class FusedSGD(torch.optim.SGD):
             # expose the momentum buffers in torch.optim.SGD's per-parameter layout
             a = self.arena
             for i, p in enumerate(a.params):
-                o, n = a.offsets[i], a.numels[i]
-                sd["state"][i] = {"momentum_buffer": self.momentum_buffer[o:o + n].view(p.shape).clone()}
+                    sd["state"][i] = {"momentum_buffer": a.shaped(self.momentum_buffer, i).contiguous()}
         return sd
 
     def load_state_dict(self, sd):
@@ -105,10 +104,9 @@ class FusedSGD(torch.optim.SGD):
         a = self.arena
         st = sd.get("state", {})
         for i, p in enumerate(a.params):
-            o, n = a.offsets[i], a.numels[i]
             buf = st.get(i, st.get(str(i), {})).get("momentum_buffer")
             if buf is not None:
-                self.momentum_buffer[o:o + n].copy_(buf.reshape(-1).to(self.momentum_buffer.device))
+                a.shaped(self.momentum_buffer, i).copy_(buf.reshape(p.shape))
         for k in ("lr", "momentum", "weight_decay", "nesterov"):
             if sd.get("param_groups"):
                 self.param_groups[0][k] = sd["param_groups"][0].get(k, self.param_groups[0][k])

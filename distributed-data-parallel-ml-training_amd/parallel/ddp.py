@@ -171,7 +171,7 @@ class DistributedDataParallel(nn.Module):
 
     def _on_accumulated(self, p):
         i = self._index[id(p)]
-        view = self.arena.grad_view(i).view(p.shape)
+        view = self.arena.shaped(self.arena.grad, i)
         if p.grad.data_ptr() != view.data_ptr():  # someone replaced .grad: fold it back
             view.copy_(p.grad)
             p.grad = view

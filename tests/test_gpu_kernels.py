@@ -64,16 +64,25 @@ def test_conv_fwd_stats(native_ext, case):
     assert torch.allclose(stats[K:], (zf * zf).sum(0), rtol=1e-3, atol=1e-2)
 
 
+@pytest.mark.parametrize("layout", ["kcrs", "krsc", "krsc_atomic"])
 @pytest.mark.parametrize("case", [c for c in CONV_CASES if c[1] != 8])
-def test_conv_dgrad(native_ext, case):
+def test_conv_dgrad(native_ext, case, layout):
+    """dgrad + wgrad; the weight gradient in the standard [K][C][R][S] layout, the GPU arena's
+    [K][R][S][C] layout, and with the atomic split-K reduction."""
     from ddp_amd.ops.layers import conv_backward
     N, Cin, H, W, K, R, stride, pad = case
     conv, spec, x, xn = _conv_setup(N, Cin, H, W, K, R, stride, pad)
     P = (H + 2 * pad - R) // stride + 1
     dz = bf(torch.randn(N, K, P, P, device=DEV))
     dzn = dz.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
-    dw = torch.zeros_like(conv.weight)
-    dx = conv_backward(spec, xn, dzn, dw, True)
+    fmt = torch.contiguous_format if layout == "kcrs" else torch.channels_last
+    dw = torch.zeros_like(conv.weight, memory_format=fmt)
+    native_ext.conv_options(int(layout == "krsc_atomic"))
+    try:
+        dx = conv_backward(spec, xn, dzn, dw, True)
+        torch.cuda.synchronize()
+    finally:
+        native_ext.conv_options(0)
     xr = x.clone().requires_grad_(True)
     wr = conv.weight.detach().clone().requires_grad_(True)
     out = F.conv2d(xr, wr, None, stride, pad)
@@ -82,11 +91,12 @@ def test_conv_dgrad(native_ext, case):
     assert rel_err(dw, wr.grad) < 1e-2
 
 
-def test_conv_wgrad_padded_layer0(native_ext):
+@pytest.mark.parametrize("fmt", [torch.contiguous_format, torch.channels_last])
+def test_conv_wgrad_padded_layer0(native_ext, fmt):
     from ddp_amd.ops.layers import conv_backward
     conv, spec, x, xn = _conv_setup(4, 8, 32, 32, 64, 3, 1, 1, Creal=3)
     dz = bf(torch.randn(4, 64, 32, 32, device=DEV))
-    dw = torch.zeros_like(conv.weight)
+    dw = torch.zeros_like(conv.weight, memory_format=fmt)
     conv_backward(spec, xn, dz.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16), dw, False)
     wr = conv.weight.detach().clone().requires_grad_(True)
     F.conv2d(x, wr, None, 1, 1).backward(dz)
@@ -124,8 +134,9 @@ def test_bn_act_fwd_bwd(native_ext, C, H, pool, res):
     Ho = H // 2 if pool else H
     out = torch.empty(N, Ho, Ho, C, device=DEV, dtype=torch.bfloat16)
     s = stream_handle()
+    coef = torch.empty(6 * C, device=DEV)
     nat.bn_act_fwd(N, H, H, C, int(pool), 1, 1e-5, ptr(zn), ptr(rn), ptr(stats), ptr(gamma),
-                   ptr(beta), ptr(out), s)
+                   ptr(beta), ptr(out), s, coef=ptr(coef))
     zr = z.clone().requires_grad_(True)
     gr = gamma.clone().requires_grad_(True)
     br = beta.clone().requires_grad_(True)
@@ -135,7 +146,7 @@ def test_bn_act_fwd_bwd(native_ext, C, H, pool, res):
     dout = bf(torch.randn_like(ref))
     ref.backward(dout)
     doutn = dout.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
-    sums = torch.zeros(2 * C, device=DEV)
+    sums = torch.zeros(16 * 2 * C, device=DEV)  # 16 replicas of [2][C]
     dz = torch.empty_like(zn)
     dres = torch.empty_like(zn) if res else None
     dg = torch.zeros(C, device=DEV)
@@ -143,11 +154,12 @@ def test_bn_act_fwd_bwd(native_ext, C, H, pool, res):
     dbias = torch.zeros(C, device=DEV)
     nat.bn_act_bwd(N, H, H, C, int(pool), 1, 1e-5, ptr(zn), ptr(rn), ptr(stats), ptr(gamma),
                    ptr(beta), ptr(doutn), ptr(sums), ptr(dz), ptr(dres), ptr(dg), ptr(db),
-                   ptr(dbias), s)
+                   ptr(dbias), s, ptr(coef))
     torch.cuda.synchronize()
     assert rel_err(dz.permute(0, 3, 1, 2), zr.grad) < 2e-2
     assert rel_err(dg, gr.grad) < 1e-2
     assert rel_err(db, br.grad) < 1e-2
+    # conv-bias gradient through train-mode BN is identically zero (left untouched)
     assert torch.allclose(dbias, zr.grad.sum((0, 2, 3)), atol=5e-2)
     if res:
         assert rel_err(dres.permute(0, 3, 1, 2), rr.grad) < 1e-2
@@ -230,6 +242,14 @@ def test_pack_weights(native_ext):
     s2 = ConvBNActSpec(conv2, None)
     s2.maybe_pack()
     assert torch.equal(s2.wt.float(), conv2.weight.detach().permute(1, 2, 3, 0).to(torch.bfloat16).float())
+    # [K][R][S][C] fp32 master (GPU arena layout)
+    conv3 = torch.nn.Conv2d(3, 64, 3, padding=1).to(DEV)
+    conv3.weight.data = conv3.weight.data.contiguous(memory_format=torch.channels_last)
+    s3 = ConvBNActSpec(conv3, None, cin_pad=8)
+    s3.maybe_pack()
+    exp = torch.zeros(64, 3, 3, 8, device=DEV)
+    exp[..., :3] = conv3.weight.detach().permute(0, 2, 3, 1)
+    assert torch.equal(s3.wc.float(), exp.to(torch.bfloat16).float())
 
 
 def test_synthetic_and_augment_match_cpu(native_ext):

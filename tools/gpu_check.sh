@@ -18,6 +18,12 @@ for s in $steps; do
     bench)
       timeout -k 10 300 python bench.py --steps 40 --warmup 10 > gpurun_out/bench1.log 2>&1
       rc=$?; tail -3 gpurun_out/bench1.log; ok_or_stop $rc bench ;;
+    benchatomic)  # split-K weight gradients with fp32 atomics
+      DDP_AMD_WGRAD_ATOMIC=1 timeout -k 10 300 python bench.py --steps 40 --warmup 10 > gpurun_out/bench_atomic.log 2>&1
+      rc=$?; tail -1 gpurun_out/bench_atomic.log; ok_or_stop $rc bench_atomic ;;
+    benchresnet)
+      timeout -k 10 300 python bench.py --model resnet50 --steps 20 --warmup 5 > gpurun_out/bench_resnet.log 2>&1
+      rc=$?; tail -1 gpurun_out/bench_resnet.log; ok_or_stop $rc bench_resnet ;;
     bench8w)  # weak-scaling point and eager (no graph) comparison
       timeout -k 10 300 python bench.py --steps 40 --warmup 10 --no-graph > gpurun_out/bench_eager.log 2>&1
       rc=$?; tail -1 gpurun_out/bench_eager.log; ok_or_stop $rc bench_eager ;;
