@@ -117,11 +117,13 @@ PYBIND11_MODULE(_native, m) {
 
   m.def("linear_ce_fwd", [](uintptr_t x, uintptr_t W, uintptr_t b, uintptr_t labels, int B, int F,
                             int J, uintptr_t logits, uintptr_t dlogits, uintptr_t loss_sum,
-                            uintptr_t correct, uintptr_t st) {
+                            uintptr_t correct, uintptr_t st, uintptr_t loss_acc) {
     check(ddp_linear_ce_fwd(P<void>(x), P<float>(W), P<float>(b), P<long long>(labels), B, F, J,
                             P<float>(logits), P<float>(dlogits), P<float>(loss_sum),
-                            P<int>(correct), S(st)), "linear_ce_fwd");
-  });
+                            P<int>(correct), P<float>(loss_acc), S(st)), "linear_ce_fwd");
+  }, py::arg("x"), py::arg("W"), py::arg("b"), py::arg("labels"), py::arg("B"), py::arg("F"),
+     py::arg("J"), py::arg("logits"), py::arg("dlogits"), py::arg("loss_sum"), py::arg("correct"),
+     py::arg("stream"), py::arg("loss_acc") = 0);
   m.def("linear_bwd", [](uintptr_t dlogits, uintptr_t x, uintptr_t W, int B, int F, int J,
                          uintptr_t gscale, uintptr_t dx, uintptr_t dW, uintptr_t db,
                          uintptr_t st) {
@@ -140,8 +142,9 @@ PYBIND11_MODULE(_native, m) {
     check(ddp_sgd(P<float>(p), P<float>(g), P<float>(buf), n, lr, momentum, wd, grad_scale,
                   nesterov, S(st)), "sgd");
   });
-  m.def("conv_options", [](int wgrad_atomic) { ddp_conv_options(wgrad_atomic); },
-        py::arg("wgrad_atomic") = 0);
+  m.def("conv_options", [](int wgrad_atomic, int persistent) {
+    ddp_conv_options(wgrad_atomic, persistent);
+  }, py::arg("wgrad_atomic") = 0, py::arg("persistent") = 0);
   // descs: list of (p, wc, wt, K, Cr, C, R, S, krsc)
   m.def("pack_conv_weights", [](std::vector<std::tuple<uintptr_t, uintptr_t, uintptr_t, int, int,
                                                        int, int, int, int>> descs, uintptr_t st) {

@@ -79,7 +79,7 @@ int ddp_bn_act_fwd(const ddp_amd::BnArgs* a, hipStream_t st);
 int ddp_bn_act_bwd(const ddp_amd::BnArgs* a, hipStream_t st);
 int ddp_linear_ce_fwd(const void* x, const float* W, const float* b, const long long* labels,
                       int B, int F, int J, float* logits, float* dlogits, float* loss_sum,
-                      int* correct, hipStream_t st);
+                      int* correct, float* loss_acc, hipStream_t st);
 int ddp_linear_bwd(const float* dlogits, const void* x, const float* W, int B, int F, int J,
                    const float* gscale, void* dx, float* dW, float* db, hipStream_t st);
 int ddp_softmax_ce(const void* logits, int logits_bf16, const long long* labels, int B, int J,
@@ -87,7 +87,7 @@ int ddp_softmax_ce(const void* logits, int logits_bf16, const long long* labels,
                    hipStream_t st);
 int ddp_sgd(float* p, const float* g, float* buf, size_t n, float lr, float momentum, float wd,
             float grad_scale, int nesterov, hipStream_t st);
-void ddp_conv_options(int wgrad_atomic);
+void ddp_conv_options(int wgrad_atomic, int persistent);
 int ddp_pack_conv_weights(const ddp_amd::PackDesc* descs, int n, hipStream_t st);
 int ddp_sgd_pack(const void* items, int n_items, const long long* descs, float* p, const float* g,
                  float* buf, float lr, float momentum, float wd, float grad_scale, int nesterov,

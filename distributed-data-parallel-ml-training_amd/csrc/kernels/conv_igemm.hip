@@ -10,24 +10,30 @@
 //   y  [N][P][Q][K]      bf16  conv output (pre-BN)
 //   Wc [K][R][S][C]      bf16  forward weight copy   (GEMM B operand, k-contiguous)
 //   Wt [C][R][S][K]      bf16  dgrad weight copy     (GEMM B operand, k-contiguous)
-//   dW [K][Creal][R][S]  fp32  PyTorch-layout weight gradient (accumulated)
+//   dW [K][R][S][Creal]  fp32  weight gradient in the GPU arena layout (optim/arena.py), or
+//      [K][Creal][R][S]        the standard layout (ConvGeom::wkrsc selects), accumulated
 //
 // GEMM views (rows x cols, reduction):
 //   FWD   : M=N*P*Q, N=K,      red=R*S*C   A=im2col(x)          B=Wc
 //   DGRAD : M=N*H*W, N=C,      red=R*S*K   A=col2im-gather(dy)  B=Wt
+//           (strided convs: one stride-1 GEMM per output phase, see ConvArgs::phase)
 //   WGRAD : M=K,     N=R*S*C,  red=N*P*Q   A=dy^T               B=im2col(x)^T
 //
 // Kernel structure (256 threads = 4 waves in 2x2, BK = 64):
-//   * operands are gathered global->registers (implicit im2col with zero fill), written to a
-//     double-buffered LDS tile AFTER the MFMA phase that overlaps their flight, one barrier per
-//     k-step (cdna_hip_programming.md §5.5 T14 / Guideline 15);
+//   * operands go global -> LDS by buffer_load_dwordx4 ... lds (no VGPR staging); padding and
+//     tails are out-of-range buffer offsets that read as zero; the k-step's tap is uniform
+//     over the block whenever the channel dimension is a multiple of 64, so the per-chunk cost
+//     is one bounds test (cdna_hip_programming.md T14 / Guideline 15);
+//   * double-buffered LDS: the DMA of k-step s+1 is in flight during the MFMAs of step s;
 //   * FWD/DGRAD tiles are [row][k] with the 16-B chunk index XOR-swizzled by (row>>1)&7, read
 //     by ds_read_b128 conflict-free (T2);
 //   * WGRAD tiles keep the global order [m][channel] (m = the reduction index) and the MFMA
 //     fragments are read with ds_read_b64_tr_b16 (gfx950 transposing LDS read, T10), chunk
 //     XOR-swizzled by m so both 16-lane groups of a half-wave hit disjoint banks;
+//   * MFMA operands are swapped (D^T = B^T A^T) so each lane owns one output row and four
+//     consecutive columns: 8-B bf16 / 16-B fp32 stores in the epilogue;
 //   * XCD-aware bijective tile order (T1); split-K writes plain fp32 slabs [split][M][N] that a
-//     finish kernel reduces in a fixed order (no float atomics on the GEMM output);
+//     finish kernel reduces in a fixed order (WGRAD optionally uses fp32 atomics instead);
 //   * FWD epilogue adds the bias, rounds to bf16 and accumulates the per-channel BatchNorm
 //     statistics of the rounded output (sum, sum of squares) — BN needs no separate stats pass.
 #include "common.h"
@@ -42,6 +48,15 @@ typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef short short8_t __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 
+// x / d for 0 <= x < 2^31 with a precomputed multiplier (d >= 1):  q = (mulhi(x, mul) + x) >> sh
+struct FastDiv {
+  unsigned mul;
+  int sh;
+};
+__device__ __forceinline__ int fast_div(int x, FastDiv d) {
+  return (int)((__umulhi((unsigned)x, d.mul) + (unsigned)x) >> d.sh);
+}
+
 struct ConvArgs {
   ConvGeom g;
   const unsigned short* a;   // FWD: x, DGRAD: dy, WGRAD: dy
@@ -55,6 +70,14 @@ struct ConvArgs {
   int splits;
   int ksteps_per_split;
   int wg_atomic;             // WGRAD split-K: fp32 atomics into dw instead of slabs + finish
+  // DGRAD of a strided conv, one output phase (pa, pb): GEMM rows are the input pixels
+  // h = pa + stride*i, w = pb + stride*j (i < Hp, j < Wp); the only taps that reach them are
+  // r = r0 + stride*t (t < Rt), s = s0 + stride*u (u < St), read from dy at (i + qa - t,
+  // j + qb - u): a stride-1 problem with 1/stride^2 of the rows and taps (sub-pixel split).
+  int phase;
+  int pa, pb, Hp, Wp, r0, s0, Rt, St, qa, qb;
+  int a_bytes, b_bytes;      // operand sizes: buffer-resource bounds (reads past them give 0)
+  FastDiv dPQ, dQ;           // WGRAD pixel decomposition
 };
 
 // ------------------------------------------------------------------ operand gathers
@@ -85,6 +108,13 @@ __device__ __forceinline__ RowInfo row_info(const ConvArgs& A, int row) {
     ri.base = n * g.H * g.W * g.C;
     ri.h0 = p * g.stride - g.pad;
     ri.w0 = q * g.stride - g.pad;
+  } else if (A.phase) {
+    const int hw = A.Hp * A.Wp;
+    const int n = row / hw, rem = row - n * hw;
+    const int i = rem / A.Wp, j = rem - i * A.Wp;
+    ri.base = n * g.P * g.Q * g.K;
+    ri.h0 = i + A.qa;
+    ri.w0 = j + A.qb;
   } else {
     const int hw = g.H * g.W;
     const int n = row / hw, rem = row - n * hw;
@@ -100,55 +130,6 @@ struct KInfo {
   int r, s, c;  // kernel tap and channel of the chunk's first reduction element
   bool ok;
 };
-
-template <int MODE>
-__device__ __forceinline__ KInfo k_info(const ConvArgs& A, int kk, float invC, float invS) {
-  const ConvGeom& g = A.g;
-  KInfo k;
-  k.ok = kk < A.Kg;
-  const int cdim = MODE == MODE_FWD ? g.C : g.K;
-  const int rs = fdiv(kk, cdim, invC);
-  k.c = kk - rs * cdim;
-  k.r = fdiv(rs, g.S, invS);
-  k.s = rs - k.r * g.S;
-  return k;
-}
-
-template <int MODE>
-__device__ __forceinline__ u16x8 gather_a(const ConvArgs& A, const RowInfo& ri, const KInfo& k) {
-  const ConvGeom& g = A.g;
-  u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (!k.ok) return z;
-  if (MODE == MODE_FWD) {
-    const int h = ri.h0 + k.r, w = ri.w0 + k.s;
-    if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) return z;
-    return ld8(A.a + ri.base + (h * g.W + w) * g.C + k.c);
-  } else {
-    int ph = ri.h0 - k.r, pw = ri.w0 - k.s;
-    if (ph < 0 || pw < 0) return z;
-    if (g.stride != 1) {
-      if ((ph % g.stride) | (pw % g.stride)) return z;
-      ph /= g.stride;
-      pw /= g.stride;
-    }
-    if (ph >= g.P || pw >= g.Q) return z;
-    return ld8(A.a + ri.base + (ph * g.Q + pw) * g.K + k.c);
-  }
-}
-
-// WGRAD B' chunk: x at pixel-index m for the 8 consecutive (r,s,c) columns described by k.
-__device__ __forceinline__ u16x8 gather_x_wgrad(const ConvArgs& A, const KInfo& k, int m,
-                                                float invPQ, float invQ) {
-  const ConvGeom& g = A.g;
-  u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (!k.ok || m >= A.Kg) return z;
-  const int pq = g.P * g.Q;
-  const int n = fdiv(m, pq, invPQ), rem = m - n * pq;
-  const int p = fdiv(rem, g.Q, invQ), q = rem - p * g.Q;
-  const int h = p * g.stride - g.pad + k.r, w = q * g.stride - g.pad + k.s;
-  if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) return z;
-  return ld8(A.b + ((n * g.H + h) * g.W + w) * g.C + k.c);
-}
 
 // ------------------------------------------------------------------ LDS addressing
 // [row][k] tile, 64 bf16 per row = 8 chunks of 16 B; chunk XOR (row>>1)&7 (ds_read_b128 reads
@@ -169,14 +150,18 @@ __device__ __forceinline__ int mc_off(int m, int col) {
   return m * NCOL + (((col >> 3) ^ mc_swz<NCOL>(m)) << 3) + (col & 7);
 }
 
-// 16 zero bytes: the source of every LDS-DMA lane whose im2col element lies in the padding.
-__device__ __attribute__((aligned(64))) unsigned short g_zero16[32];
+// Buffer resource over a tensor (raw, stride 0): offsets >= num_records read as zero.
+constexpr unsigned kOOB = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+}
 
 typedef __attribute__((address_space(3))) void lds_void;
 
-__device__ __forceinline__ void dma16(const void* src, unsigned short* lds_wave_base) {
-  // global_load_lds_dwordx4: LDS destination = wave-uniform base + lane * 16 (no VGPR staging)
-  __builtin_amdgcn_global_load_lds(src, (lds_void*)lds_wave_base, 16, 0, 0);
+__device__ __forceinline__ void dma_buf(__amdgpu_buffer_rsrc_t rs, int byte_off,
+                                        unsigned short* lds_wave_base) {
+  // buffer_load_dwordx4 ... lds: LDS destination = wave-uniform base (M0) + lane * 16
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lds_wave_base, 16, byte_off, 0, 0, 0);
 }
 
 template <int MODE, int BM, int BN>
@@ -195,68 +180,92 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
 
+  // Persistent work loop: item = (split z, tile); a block walks items blockIdx.x, +gridDim.x, ...
+  // and prefetches the first k-step of its NEXT item while it finishes (last MFMAs + epilogue)
+  // the current one, so short-K tiles do not pay the DMA latency once per tile.
   const int tiles_n = (args.Ng + BN - 1) / BN;
   const int tiles_m = (args.Mg + BM - 1) / BM;
-  const int tile = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
-  const int row0 = tm * BM, col0 = tn * BN;
-
+  const int tiles = tiles_m * tiles_n;
+  const int nitems = tiles * args.splits;
   const int ksteps = (args.Kg + BK - 1) / BK;
-  const int ks_begin = blockIdx.z * args.ksteps_per_split;
-  const int ks_end = min(ksteps, ks_begin + args.ksteps_per_split);
 
   f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
   const ConvGeom& gg = args.g;
-  const unsigned short* zero = g_zero16;
 
   // ---------------- per-thread gather state (index math hoisted out of the k-loop) ----------------
+  // Operands are fetched with buffer_load_dwordx4 ... lds (LDS-DMA through a buffer resource):
+  // an out-of-range byte offset returns zeros, so padding / tails cost one v_cndmask to the
+  // kOOB sentinel instead of a pointer select, and all offsets are 32-bit.
   // FWD/DGRAD: DMA chunk c = tid + 256 i lands at LDS byte 16 c = row (tid>>3)+32i, physical
   // chunk tid&7; it must carry LOGICAL chunk lc = (tid&7) ^ ((row>>1)&7) = constant per thread.
   // WGRAD: row = m (reduction), physical chunk tid % (BX/8), logical = phys ^ swz(m) (constant).
   constexpr int NA = (MODE != MODE_WGRAD) ? CA : 1;
-  int a_rowoff[NA];      // FWD: n*H*W*C + (h0*W + w0)*C ; DGRAD: n*P*Q*K + (h0*Q + w0)*K
+  int a_off[CA];         // FWD/DGRAD: byte offset of the row's (tap 0) pixel + lcA*8 channels
+                         // WGRAD: byte offset of (m-row within the k-step, kout) or kOOB
   int a_h0[NA], a_w0[NA];
-  int b_col_ok = 0;      // bit i: B row i valid
-  int lcA, lcB;
-  int kr = 0, ks_ = 0, kc = 0;  // (r, s, c) of this thread's reduction chunk for the current k-step
+  int b_off[CB];         // FWD/DGRAD: byte offset of B row + lcB*8 (kOOB past Ng)
+  int kr = 0, ks_ = 0, kc = 0;  // slow path: (r, s, c) of this thread's chunk; fast path: uniform
   KInfo xk;              // WGRAD: (r,s,c) of this thread's B' column group
-  const float invPQ = 1.f / (float)(gg.P * gg.Q), invQ = 1.f / (float)gg.Q;
-  if (MODE != MODE_WGRAD) {
-    lcA = lcB = (tid & 7) ^ ((tid >> 4) & 7);
+  int xk_same = 0;       // WGRAD "same" conv: byte offset of tap (r,s) channel c relative to m
+  int row0 = 0, col0 = 0, zsplit = 0, ks_begin = 0, ks_end = 0;
+  const bool phase = MODE == MODE_DGRAD && args.phase;
+  const int Sdec = phase ? args.St : gg.S;  // taps per kernel row in the reduction index
+  const int cdim = MODE == MODE_FWD ? gg.C : gg.K;
+  // k-step = one tap x 64 channels (uniform over the block) when the channel dim is a multiple
+  // of 64; otherwise (C = 8 input layers, K = 32 tests) every chunk decodes its own tap
+  const bool fast = MODE != MODE_WGRAD && (cdim % BK) == 0;
+  const int lcA = (MODE != MODE_WGRAD) ? ((tid & 7) ^ ((tid >> 4) & 7))
+                                       : ((tid % (BM / 8)) ^ mc_swz<BM>(tid / (BM / 8)));
+  const int lcB = (MODE != MODE_WGRAD) ? lcA : ((tid % (BN / 8)) ^ mc_swz<BN>(tid / (BN / 8)));
+  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(args.a, args.a_bytes);
+  const __amdgpu_buffer_rsrc_t rsB = make_rsrc(args.b, args.b_bytes);
+
+  auto setup = [&](int item) {
+    zsplit = item / tiles;
+    const int tile = xcd_remap(item - zsplit * tiles, tiles);
+    const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+    row0 = tm * BM;
+    col0 = tn * BN;
+    ks_begin = zsplit * args.ksteps_per_split;
+    ks_end = min(ksteps, ks_begin + args.ksteps_per_split);
+    if (MODE != MODE_WGRAD) {
 #pragma unroll
-    for (int i = 0; i < CA; ++i) {
-      const RowInfo ri = row_info<MODE>(args, row0 + (tid >> 3) + 32 * i);
-      a_h0[i] = ri.h0;
-      a_w0[i] = ri.w0;
-      a_rowoff[i] = (MODE == MODE_FWD) ? ri.base + (ri.h0 * gg.W + ri.w0) * gg.C
-                                       : ri.base + (ri.h0 * gg.Q + ri.w0) * gg.K;
+      for (int i = 0; i < CA; ++i) {
+        const RowInfo ri = row_info<MODE>(args, row0 + (tid >> 3) + 32 * i);
+        a_h0[i] = ri.h0;
+        a_w0[i] = ri.w0;
+        const int e = (MODE == MODE_FWD) ? ri.base + (ri.h0 * gg.W + ri.w0) * gg.C
+                                         : ri.base + (ri.h0 * gg.Q + ri.w0) * gg.K;
+        a_off[i] = 2 * (e + (fast ? lcA * 8 : 0));
+      }
+      const int bstride = phase ? gg.R * gg.S * gg.K : args.Kg;
+#pragma unroll
+      for (int i = 0; i < CB; ++i) {
+        const int col = col0 + (tid >> 3) + 32 * i;
+        b_off[i] = col < args.Ng ? 2 * (col * bstride + lcB * 8) : (int)kOOB;
+      }
+      // decomposition of the first reduction index (fast: of the k-step; slow: of the chunk)
+      const int kk = ks_begin * BK + (fast ? 0 : lcA * 8);
+      const int rs = kk / cdim;
+      kc = kk - rs * cdim;
+      kr = rs / Sdec;
+      ks_ = rs - kr * Sdec;
+    } else {
+      constexpr int NCA = BM / 8;
+      const int kout = row0 + lcA * 8;
+#pragma unroll
+      for (int i = 0; i < CA; ++i)
+        a_off[i] = kout < args.Mg ? 2 * (((tid + i * 256) / NCA) * gg.K + kout) : (int)kOOB;
+      const int j = col0 + lcB * 8;
+      const int rs = j / gg.C;
+      xk.c = j - rs * gg.C;
+      xk.r = rs / gg.S;
+      xk.s = rs - xk.r * gg.S;
+      xk.ok = j < args.Ng;
+      if (!xk.ok) xk.r = -(1 << 20);  // every border test fails -> zeros
+      xk_same = 2 * (((xk.r - gg.pad) * gg.W + (xk.s - gg.pad)) * gg.C + xk.c);
     }
-#pragma unroll
-    for (int i = 0; i < CB; ++i)
-      if (col0 + (tid >> 3) + 32 * i < args.Ng) b_col_ok |= 1 << i;
-    // decomposition of the first reduction index this thread loads
-    const int cdim = MODE == MODE_FWD ? gg.C : gg.K;
-    const int kk = ks_begin * BK + lcA * 8;
-    const int rs = kk / cdim;
-    kc = kk - rs * cdim;
-    kr = rs / gg.S;
-    ks_ = rs - kr * gg.S;
-  } else {
-    constexpr int NCA = BM / 8, NCB = BN / 8;
-    lcA = (tid % NCA) ^ mc_swz<BM>(tid / NCA);
-    lcB = (tid % NCB) ^ mc_swz<BN>(tid / NCB);
-    const int j = col0 + lcB * 8;
-    const int rs = j / gg.C;
-    xk.c = j - rs * gg.C;
-    xk.r = rs / gg.S;
-    xk.s = rs - xk.r * gg.S;
-    xk.ok = j < args.Ng;
-  }
+  };
 
   // issue the LDS-DMA of k-step ks into buffer buf (and advance the incremental k state)
   auto issue = [&](int ks, int buf) {
@@ -264,71 +273,86 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
     unsigned short* Bs = As + TILE_A;
     const int k0 = ks * BK;
     if (MODE != MODE_WGRAD) {
-      const int kk = k0 + lcA * 8;
-      const bool kok = kk < args.Kg;
       const int W_ = MODE == MODE_FWD ? gg.W : gg.Q;
-      const int cdim = MODE == MODE_FWD ? gg.C : gg.K;
-      const int tap = MODE == MODE_FWD ? (kr * W_ + ks_) * cdim + kc : kc - (kr * W_ + ks_) * cdim;
+      if (fast) {
+        // uniform tap (kr, ks_) and channel block kc: the per-chunk work is one bounds test
+        const int tap = 2 * (MODE == MODE_FWD ? (kr * W_ + ks_) * cdim + kc : kc - (kr * W_ + ks_) * cdim);
 #pragma unroll
-      for (int i = 0; i < CA; ++i) {
-        const void* src = zero;
-        if (MODE == MODE_FWD) {
-          const int h = a_h0[i] + kr, w = a_w0[i] + ks_;
-          if (kok && (unsigned)h < (unsigned)gg.H && (unsigned)w < (unsigned)gg.W)
-            src = args.a + a_rowoff[i] + tap;
-        } else {
-          int ph = a_h0[i] - kr, pw = a_w0[i] - ks_;
-          bool ok = kok && ph >= 0 && pw >= 0;
-          if (gg.stride == 1) {
-            ok = ok && ph < gg.P && pw < gg.Q;
-            if (ok) src = args.a + a_rowoff[i] + tap;
-          } else {  // strided conv: only taps that hit an output pixel contribute
-            ok = ok && (ph % gg.stride) == 0 && (pw % gg.stride) == 0;
-            ph /= gg.stride;
-            pw /= gg.stride;
-            ok = ok && ph < gg.P && pw < gg.Q;
-            if (ok) {
-              const int base = a_rowoff[i] - (a_h0[i] * gg.Q + a_w0[i]) * gg.K;
-              src = args.a + base + (ph * gg.Q + pw) * gg.K + kc;
-            }
-          }
+        for (int i = 0; i < CA; ++i) {
+          bool ok;
+          if (MODE == MODE_FWD)
+            ok = (unsigned)(a_h0[i] + kr) < (unsigned)gg.H && (unsigned)(a_w0[i] + ks_) < (unsigned)gg.W;
+          else
+            ok = (unsigned)(a_h0[i] - kr) < (unsigned)gg.P && (unsigned)(a_w0[i] - ks_) < (unsigned)gg.Q;
+          dma_buf(rsA, ok ? a_off[i] + tap : (int)kOOB, As + (wid * 64 + 256 * i) * 8);
         }
-        dma16(src, As + (wid * 64 + 256 * i) * 8);
-      }
+        const int boff = 2 * (phase ? ((args.r0 + gg.stride * kr) * gg.S + args.s0 + gg.stride * ks_) * gg.K + kc
+                                    : k0);
 #pragma unroll
-      for (int i = 0; i < CB; ++i) {
-        const int col = col0 + (tid >> 3) + 32 * i;
-        const void* src = (kok && ((b_col_ok >> i) & 1)) ? (const void*)(args.b + (size_t)col * args.Kg + kk) : zero;
-        dma16(src, Bs + (wid * 64 + 256 * i) * 8);
-      }
-      // advance (r, s, c) by BK reduction elements
-      kc += BK;
-      while (kc >= cdim) {
-        kc -= cdim;
-        if (++ks_ == gg.S) { ks_ = 0; ++kr; }
+        for (int i = 0; i < CB; ++i) dma_buf(rsB, b_off[i] + boff, Bs + (wid * 64 + 256 * i) * 8);
+        kc += BK;
+        if (kc == cdim) {
+          kc = 0;
+          if (++ks_ == Sdec) { ks_ = 0; ++kr; }
+        }
+      } else {
+        const int kk = k0 + lcA * 8;
+        const bool kok = kk < args.Kg;
+        const int tap = 2 * (MODE == MODE_FWD ? (kr * W_ + ks_) * cdim + kc : kc - (kr * W_ + ks_) * cdim);
+#pragma unroll
+        for (int i = 0; i < CA; ++i) {
+          bool ok;
+          if (MODE == MODE_FWD)
+            ok = (unsigned)(a_h0[i] + kr) < (unsigned)gg.H && (unsigned)(a_w0[i] + ks_) < (unsigned)gg.W;
+          else
+            ok = (unsigned)(a_h0[i] - kr) < (unsigned)gg.P && (unsigned)(a_w0[i] - ks_) < (unsigned)gg.Q;
+          dma_buf(rsA, (kok && ok) ? a_off[i] + tap : (int)kOOB, As + (wid * 64 + 256 * i) * 8);
+        }
+        // (kc already includes this thread's lcA*8, which b_off carries too)
+        const int boff = 2 * (phase ? ((args.r0 + gg.stride * kr) * gg.S + args.s0 + gg.stride * ks_) * gg.K + kc - lcA * 8
+                                    : k0);
+#pragma unroll
+        for (int i = 0; i < CB; ++i)
+          dma_buf(rsB, kok ? b_off[i] + boff : (int)kOOB, Bs + (wid * 64 + 256 * i) * 8);
+        kc += BK;
+        while (kc >= cdim) {
+          kc -= cdim;
+          if (++ks_ == Sdec) { ks_ = 0; ++kr; }
+        }
       }
     } else {
-      constexpr int NCA = BM / 8, NCB = BN / 8;
-      const int kout = row0 + lcA * 8;
+      constexpr int NCB = BN / 8;
+      const int ka = 2 * k0 * gg.K;
 #pragma unroll
-      for (int i = 0; i < CA; ++i) {  // dy[m][kout]
-        const int m = k0 + (tid + i * 256) / NCA;
-        const void* src = (m < args.Kg && kout < args.Mg) ? (const void*)(args.a + (size_t)m * gg.K + kout) : zero;
-        dma16(src, As + (wid * 64 + 256 * i) * 8);
-      }
+      for (int i = 0; i < CA; ++i)  // dy[m][kout]; m >= Kg lands past the buffer -> zeros
+        dma_buf(rsA, a_off[i] + ka, As + (wid * 64 + 256 * i) * 8);
+      // "same" convolution (stride 1, P == H, Q == W): the input pixel of output pixel m at tap
+      // (r, s) is m + (r - pad) * W + (s - pad), so the offset is linear in m; only the border
+      // test needs (p, q)
+      if (gg.stride == 1 && gg.P == gg.H && gg.Q == gg.W) {
 #pragma unroll
-      for (int i = 0; i < CB; ++i) {  // x gather at pixel m for columns (r, s, c..c+7)
-        const int m = k0 + (tid + i * 256) / NCB;
-        const void* src = zero;
-        if (xk.ok && m < args.Kg) {
-          const int pq = gg.P * gg.Q;
-          const int n = fdiv(m, pq, invPQ), rem = m - n * pq;
-          const int p = fdiv(rem, gg.Q, invQ), q = rem - p * gg.Q;
-          const int h = p * gg.stride - gg.pad + xk.r, w = q * gg.stride - gg.pad + xk.s;
-          if ((unsigned)h < (unsigned)gg.H && (unsigned)w < (unsigned)gg.W)
-            src = args.b + ((n * gg.H + h) * gg.W + w) * gg.C + xk.c;
+        for (int i = 0; i < CB; ++i) {  // x gather at pixel m for columns (r, s, c..c+7)
+          const int m = k0 + (tid + i * 256) / NCB;
+          const int rem = m - fast_div(m, args.dPQ) * (gg.P * gg.Q);
+          const int p = fast_div(rem, args.dQ);
+          const int q = rem - p * gg.Q;
+          const bool ok = m < args.Kg && (unsigned)(p - gg.pad + xk.r) < (unsigned)gg.H &&
+                          (unsigned)(q - gg.pad + xk.s) < (unsigned)gg.W;
+          dma_buf(rsB, ok ? m * (2 * gg.C) + xk_same : (int)kOOB, Bs + (wid * 64 + 256 * i) * 8);
         }
-        dma16(src, Bs + (wid * 64 + 256 * i) * 8);
+      } else {
+#pragma unroll
+        for (int i = 0; i < CB; ++i) {
+          const int m = k0 + (tid + i * 256) / NCB;
+          const int n = fast_div(m, args.dPQ);
+          const int rem = m - n * (gg.P * gg.Q);
+          const int p = fast_div(rem, args.dQ);
+          const int q = rem - p * gg.Q;
+          const int h = p * gg.stride - gg.pad + xk.r, w = q * gg.stride - gg.pad + xk.s;
+          const bool ok = m < args.Kg && (unsigned)h < (unsigned)gg.H && (unsigned)w < (unsigned)gg.W;
+          dma_buf(rsB, ok ? 2 * (((n * gg.H + h) * gg.W + w) * gg.C + xk.c) : (int)kOOB,
+                  Bs + (wid * 64 + 256 * i) * 8);
+        }
       }
     }
   };
@@ -394,24 +418,13 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
     }
   };
 
-  if (ks_begin < ks_end) {
-    issue(ks_begin, 0);
-    __syncthreads();  // waits for the DMA (vmcnt(0)) and publishes buffer 0
-    int buf = 0;
-    for (int ks = ks_begin; ks < ks_end; ++ks) {
-      if (ks + 1 < ks_end) issue(ks + 1, buf ^ 1);  // lands during this step's MFMAs
-      compute(buf);
-      __syncthreads();  // next buffer landed + everyone done reading this one
-      buf ^= 1;
-    }
-  }
-
   // ---------------- epilogue ----------------
   // acc[i][j][v] = D[row0 + wm*WTM + i*16 + (lane&15)][col0 + wn*WTN + j*16 + 4*(lane>>4) + v]
   // Ng % 8 == 0 for every mode (C, K multiples of 8), so a lane's 4 columns are all valid or not.
+  auto epilogue = [&](const int row0, const int col0, const int zs) {
   const ConvGeom& g = args.g;
   const bool split = args.splits > 1;
-  float* slab = split ? args.ws + (size_t)blockIdx.z * args.Mg * args.Ng : nullptr;
+  float* slab = split ? args.ws + (size_t)zs * args.Mg * args.Ng : nullptr;
   const int rl = lane & 15, cq = 4 * (lane >> 4);
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -460,7 +473,14 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
         uint2 pk;
         pk.x = (unsigned)h0 | ((unsigned)h1 << 16);
         pk.y = (unsigned)h2 | ((unsigned)h3 << 16);
-        *reinterpret_cast<uint2*>(args.out + (size_t)row * args.Ng + col) = pk;
+        size_t orow = row;
+        if (phase) {  // phase-local row -> input pixel
+          const int hw = args.Hp * args.Wp;
+          const int n = row / hw, rem = row - n * hw;
+          const int i = rem / args.Wp, j = rem - i * args.Wp;
+          orow = ((size_t)n * gg.H + args.pa + gg.stride * i) * gg.W + args.pb + gg.stride * j;
+        }
+        *reinterpret_cast<uint2*>(args.out + orow * args.Ng + col) = pk;
         if (MODE == MODE_FWD) {
           const float r0 = bf2f(h0), r1 = bf2f(h1), r2 = bf2f(h2), r3 = bf2f(h3);
           s[0] += r0; s[1] += r1; s[2] += r2; s[3] += r3;
@@ -488,16 +508,64 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
       }
     }
   }
+  };
+
+  int item = blockIdx.x;
+  if (item >= nitems) return;
+  setup(item);
+  issue(ks_begin, 0);
+  __syncthreads();  // waits for the DMA (vmcnt(0)) and publishes buffer 0
+  int buf = 0;
+  while (true) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int e_row0 = row0, e_col0 = col0, e_z = zsplit;
+    const int kb = ks_begin, ke = ks_end;  // host guarantees kb < ke for every item
+    const int next = item + gridDim.x;
+    const bool has_next = next < nitems;
+    for (int ks = kb; ks < ke; ++ks) {
+      if (ks + 1 < ke) {
+        issue(ks + 1, buf ^ 1);  // lands during this step's MFMAs
+      } else if (has_next) {
+        setup(next);             // buffer buf^1 is free: everyone passed the last barrier
+        issue(ks_begin, buf ^ 1);
+      }
+      compute(buf);
+      if (ks + 1 < ke) {
+        __syncthreads();  // next buffer landed + everyone done reading this one
+        buf ^= 1;
+      }
+    }
+    epilogue(e_row0, e_col0, e_z);
+    if (!has_next) break;
+    __syncthreads();  // next item's first k-step landed; this buffer fully consumed
+    buf ^= 1;
+    item = next;
+  }
 }
 
 // Split-K finish for FWD/DGRAD: sum the slabs in split order -> (+bias) bf16 output
 // (+ per-channel stats of the rounded output for FWD).
 // Thread layout: cg_local = tid % Gb (8 channels each), rows strided; stats reduced in
 // registers, then through LDS, then ONE atomic per channel per block.
+struct RowMap {  // phase-local GEMM row -> output pixel (strided DGRAD); stride 0 = identity
+  int stride, Hp, Wp, H, W, pa, pb;
+};
+
+__device__ __forceinline__ size_t map_row(const RowMap& m, int row) {
+  if (m.stride == 0) return row;
+  const int hw = m.Hp * m.Wp;
+  const int n = row / hw, rem = row - n * hw;
+  const int i = rem / m.Wp, j = rem - i * m.Wp;
+  return ((size_t)n * m.H + m.pa + m.stride * i) * m.W + m.pb + m.stride * j;
+}
+
 __global__ __launch_bounds__(256) void splitk_finish_kernel(const float* ws, int splits,
                                                             unsigned short* out,
                                                             const float* bias, float* stats,
-                                                            int Mg, int Ng) {
+                                                            int Mg, int Ng, RowMap rmap) {
   __shared__ float red[2][8][256];
   const int G = Ng / 8;
   const int Gb = G < 256 ? G : 256;
@@ -530,7 +598,7 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(const float* ws, int
       s[e] += r;
       ss[e] += r * r;
     }
-    st8(out + (size_t)row * Ng + cg * 8, o);
+    st8(out + map_row(rmap, row) * Ng + cg * 8, o);
   }
   if (!stats) return;
 #pragma unroll
@@ -631,7 +699,21 @@ __global__ __launch_bounds__(256) void wgrad_finish_krsc_kernel(const float* __r
 // ------------------------------- host launcher -------------------------------
 using namespace ddp_amd;
 
+static FastDiv make_fastdiv(int d) {
+  FastDiv f;
+  int sh = 0;
+  while ((1ll << sh) < d) ++sh;
+  f.sh = sh;
+  f.mul = (unsigned)((((1ull << sh) - (unsigned long long)d) << 32) / (unsigned long long)d + 1);
+  return f;
+}
+
+static bool fits_buffer(size_t elems) { return elems * 2 < (size_t)kOOB; }
+
+static int g_wgrad_atomic = 0;  // WGRAD split-K through fp32 atomics instead of slabs
+static int g_persistent = 0;    // grid = resident slots, blocks loop over work items
 constexpr int kMaxAtomicSplits = 32;
+constexpr int kNumCUs = 256;
 
 // Split-K factor for a tile config: aim for >= 2 workgroups per CU, keep >= 4 k-steps per
 // split, fit the slab workspace.
@@ -682,8 +764,17 @@ static void launch_cfg(ConvArgs& a, int splits, hipStream_t st) {
   // same-address fp32 atomics serialise: beyond kMaxAtomicSplits partial sums per element the
   // slab + grouped-finish reduction is cheaper
   if (a.wg_atomic && splits > kMaxAtomicSplits) a.wg_atomic = 0;
-  dim3 grid(tiles, 1, splits);
-  hipLaunchKernelGGL((conv_igemm_kernel<MODE, BM, BN>), grid, dim3(256), 0, st, a);
+  // persistent grid: at most the resident workgroup slots (queried once per instantiation)
+  static int resident = 0;
+  if (resident == 0) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, conv_igemm_kernel<MODE, BM, BN>, 256, 0) != hipSuccess || nb < 1)
+      nb = 1;
+    resident = nb;
+  }
+  const int items = tiles * splits;
+  const int grid = g_persistent ? std::min(items, kNumCUs * resident) : items;
+  hipLaunchKernelGGL((conv_igemm_kernel<MODE, BM, BN>), dim3(grid), dim3(256), 0, st, a);
   if (splits == 1) return;
   if (MODE == MODE_WGRAD && a.wg_atomic) return;
   if (MODE == MODE_WGRAD && a.g.wkrsc) {
@@ -705,9 +796,11 @@ static void launch_cfg(ConvArgs& a, int splits, hipStream_t st) {
     // ~2 rows per thread: enough workgroups in flight for a bandwidth-bound pass
     int bx = (a.Mg + rows_per_block * 2 - 1) / (rows_per_block * 2);
     bx = std::max(1, std::min(bx, 2048 / chunks + 1));
+    RowMap rm{0, 0, 0, 0, 0, 0, 0};
+    if (a.phase) rm = RowMap{a.g.stride, a.Hp, a.Wp, a.g.H, a.g.W, a.pa, a.pb};
     hipLaunchKernelGGL(splitk_finish_kernel, dim3(bx, chunks), dim3(256), 0, st, a.ws, splits,
                        a.out, MODE == MODE_FWD ? a.bias : nullptr,
-                       MODE == MODE_FWD ? a.stats : nullptr, a.Mg, a.Ng);
+                       MODE == MODE_FWD ? a.stats : nullptr, a.Mg, a.Ng, rm);
   }
 }
 
@@ -727,8 +820,10 @@ static void launch_mode(ConvArgs& a, size_t ws_elems, hipStream_t st) {
   }
 }
 
-static int g_wgrad_atomic = 0;
-extern "C" void ddp_conv_options(int wgrad_atomic) { g_wgrad_atomic = wgrad_atomic; }
+extern "C" void ddp_conv_options(int wgrad_atomic, int persistent) {
+  g_wgrad_atomic = wgrad_atomic;
+  g_persistent = persistent;
+}
 
 extern "C" int ddp_conv_fwd(const ConvGeom* g, const void* x, const void* wc, const float* bias,
                             void* y, float* stats, float* ws, size_t ws_elems, int splits,
@@ -746,6 +841,10 @@ extern "C" int ddp_conv_fwd(const ConvGeom* g, const void* x, const void* wc, co
   a.Ng = g->K;
   a.Kg = g->R * g->S * g->C;
   a.splits = splits;
+  const size_t xa = (size_t)g->N * g->H * g->W * g->C, wb = (size_t)a.Ng * a.Kg;
+  if (!fits_buffer(xa) || !fits_buffer(wb)) return -2;
+  a.a_bytes = (int)(2 * xa);
+  a.b_bytes = (int)(2 * wb);
   launch_mode<MODE_FWD>(a, ws_elems, st);
   return (int)hipGetLastError();
 }
@@ -759,11 +858,50 @@ extern "C" int ddp_conv_dgrad(const ConvGeom* g, const void* dy, const void* wt,
   a.b = (const unsigned short*)wt;
   a.out = (unsigned short*)dx;
   a.ws = ws;
-  a.Mg = g->N * g->H * g->W;
   a.Ng = g->C;
-  a.Kg = g->R * g->S * g->K;
   a.splits = splits;
-  launch_mode<MODE_DGRAD>(a, ws_elems, st);
+  const size_t dya = (size_t)g->N * g->P * g->Q * g->K, wb = (size_t)g->C * g->R * g->S * g->K;
+  if (!fits_buffer(dya) || !fits_buffer(wb)) return -2;
+  a.a_bytes = (int)(2 * dya);
+  a.b_bytes = (int)(2 * wb);
+  if (g->stride == 1) {
+    a.Mg = g->N * g->H * g->W;
+    a.Kg = g->R * g->S * g->K;
+    launch_mode<MODE_DGRAD>(a, ws_elems, st);
+    return (int)hipGetLastError();
+  }
+  // strided conv: one stride-1 GEMM per output phase; phases no tap reaches get zeros
+  const int sd = g->stride;
+  bool zero_fill = false;
+  for (int pa = 0; pa < sd && !zero_fill; ++pa)
+    for (int pb = 0; pb < sd; ++pb) {
+      const int r0 = (pa + g->pad) % sd, s0 = (pb + g->pad) % sd;
+      if ((r0 >= g->R || s0 >= g->S) && pa < g->H && pb < g->W) zero_fill = true;
+    }
+  if (zero_fill) {
+    const hipError_t e = hipMemsetAsync(dx, 0, (size_t)g->N * g->H * g->W * g->C * 2, st);
+    if (e != hipSuccess) return (int)e;
+  }
+  for (int pa = 0; pa < sd; ++pa) {
+    for (int pb = 0; pb < sd; ++pb) {
+      ConvArgs p = a;
+      p.phase = 1;
+      p.pa = pa;
+      p.pb = pb;
+      p.r0 = (pa + g->pad) % sd;
+      p.s0 = (pb + g->pad) % sd;
+      p.Rt = p.r0 < g->R ? (g->R - p.r0 + sd - 1) / sd : 0;
+      p.St = p.s0 < g->S ? (g->S - p.s0 + sd - 1) / sd : 0;
+      p.Hp = pa < g->H ? (g->H - pa + sd - 1) / sd : 0;
+      p.Wp = pb < g->W ? (g->W - pb + sd - 1) / sd : 0;
+      if (p.Rt * p.St == 0 || p.Hp * p.Wp == 0) continue;
+      p.qa = (pa + g->pad - p.r0) / sd;
+      p.qb = (pb + g->pad - p.s0) / sd;
+      p.Mg = g->N * p.Hp * p.Wp;
+      p.Kg = p.Rt * p.St * g->K;
+      launch_mode<MODE_DGRAD>(p, ws_elems, st);
+    }
+  }
   return (int)hipGetLastError();
 }
 
@@ -777,10 +915,17 @@ extern "C" int ddp_conv_wgrad(const ConvGeom* g, const void* dy, const void* x, 
   a.dw = dw;
   a.ws = ws;
   a.wg_atomic = g_wgrad_atomic;
+  if (g->R * g->S == 1) a.g.wkrsc = 1;  // 1x1: [K][C][1][1] == [K][1][1][C]
   a.Mg = g->K;
   a.Ng = g->R * g->S * g->C;
   a.Kg = g->N * g->P * g->Q;
   a.splits = splits;
+  const size_t dya = (size_t)g->N * g->P * g->Q * g->K, xb = (size_t)g->N * g->H * g->W * g->C;
+  if (!fits_buffer(dya) || !fits_buffer(xb)) return -2;
+  a.a_bytes = (int)(2 * dya);
+  a.b_bytes = (int)(2 * xb);
+  a.dPQ = make_fastdiv(g->P * g->Q);
+  a.dQ = make_fastdiv(g->Q);
   launch_mode<MODE_WGRAD>(a, ws_elems, st);
   return (int)hipGetLastError();
 }

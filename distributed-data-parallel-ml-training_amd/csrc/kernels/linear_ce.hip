@@ -21,7 +21,7 @@ constexpr int kMaxJ = 16;
 __global__ __launch_bounds__(256) void linear_ce_fwd_kernel(
     const unsigned short* __restrict__ x, const float* __restrict__ W, const float* __restrict__ b,
     const long long* __restrict__ labels, int B, int F, int J, float inv_b, float* logits_out,
-    float* dlogits, float* loss_sum, int* correct) {
+    float* dlogits, float* loss_sum, int* correct, float* loss_acc) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= B) return;
@@ -75,6 +75,7 @@ __global__ __launch_bounds__(256) void linear_ce_fwd_kernel(
     for (int j = 0; j < kMaxJ; ++j)
       if (j == y) ly = acc[j];
     if (loss_sum) atomicAdd(loss_sum, (lse - ly) * inv_b);
+    if (loss_acc) atomicAdd(loss_acc, (lse - ly) * inv_b);  // running sum across steps
     if (correct && arg == y) atomicAdd(correct, 1);
   }
 }
@@ -209,11 +210,12 @@ using namespace ddp_amd;
 
 extern "C" int ddp_linear_ce_fwd(const void* x, const float* W, const float* b,
                                  const long long* labels, int B, int F, int J, float* logits,
-                                 float* dlogits, float* loss_sum, int* correct, hipStream_t st) {
+                                 float* dlogits, float* loss_sum, int* correct, float* loss_acc,
+                                 hipStream_t st) {
   if (J > kMaxJ || F % 8) return -1;
   hipLaunchKernelGGL(linear_ce_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, st,
                      (const unsigned short*)x, W, b, labels, B, F, J, 1.f / (float)B, logits,
-                     dlogits, loss_sum, correct);
+                     dlogits, loss_sum, correct, loss_acc);
   return (int)hipGetLastError();
 }
 

@@ -21,17 +21,29 @@ class TrainStep:
         dev = loader.device
         self.loss_sum = torch.zeros((), dtype=torch.float32, device=dev)
         self.graph = None
+        self.fused = self._fused_loss()
+
+    def _fused_loss(self):
+        """Use the model's fused classifier+loss when the criterion is the plain mean CE."""
+        from .trainer import CrossEntropyLoss
+        inner = getattr(self.model, "module", self.model)
+        return (hasattr(self.model, "forward_loss") and hasattr(inner, "forward_loss")
+                and type(self.criterion) is CrossEntropyLoss)
 
     def _body(self):
         self.optimizer.zero_grad()
         x, y = self.loader.fill()
-        out = self.model(x)
-        loss = self.criterion(out, y)
+        if self.fused:
+            # classifier + loss + loss meter in one kernel (no logits tensor, no extra adds)
+            loss = self.model.forward_loss(x, y, acc=self.loss_sum)
+        else:
+            loss = self.criterion(self.model(x), y)
         loss.backward()
         if self.sync is not None:
             self.sync(self.model)
         self.optimizer.step()
-        self.loss_sum.add_(loss.detach())
+        if not self.fused:
+            self.loss_sum.add_(loss.detach())
 
     def warmup(self, steps):
         """Eager steps on a side stream (also the fallback execution path)."""

@@ -79,12 +79,8 @@ class _VGG(nn.Module):
     def packed_specs(self):
         return self.fused_plan() if self.fc1.weight.is_cuda else []
 
-    def forward(self, x):
-        if not x.is_cuda:
-            y = self.layers(x)
-            y = y.view(y.size(0), -1)
-            return self.fc1(y)
-        from ..ops.layers import conv_bn_act, linear_small, to_nhwc_input
+    def _features_fused(self, x):
+        from ..ops.layers import conv_bn_act, to_nhwc_input
         from ..ops.common import step_scratch
         plan = self.fused_plan()
         step_scratch(x.device).zero()  # BN statistics / backward sums of every layer: one fill
@@ -93,8 +89,28 @@ class _VGG(nn.Module):
             h = conv_bn_act(h, spec)
         if h.shape[1] != 1 or h.shape[2] != 1:
             raise RuntimeError("VGG head expects 1x1 spatial features (32x32 input)")
-        h = h.view(h.shape[0], -1)  # NHWC with H=W=1: identical to the NCHW flatten
-        return linear_small(h, self.fc1)
+        return h.view(h.shape[0], -1)  # NHWC with H=W=1: identical to the NCHW flatten
+
+    def forward(self, x):
+        if not x.is_cuda:
+            y = self.layers(x)
+            y = y.view(y.size(0), -1)
+            return self.fc1(y)
+        from ..ops.layers import linear_small
+        return linear_small(self._features_fused(x), self.fc1)
+
+    def forward_loss(self, x, labels, acc=None):
+        """``CrossEntropyLoss()(self(x), labels)`` with the classifier and the loss fused into one
+        kernel on the GPU (engine/step.py uses it for the captured training step). ``acc`` (fp32
+        scalar) additionally accumulates the loss across calls. The returned loss tensor is only
+        valid until the next forward (it lives in the per-forward scratch)."""
+        if not x.is_cuda:
+            loss = nn.functional.cross_entropy(self.forward(x), labels)
+            if acc is not None:
+                acc.add_(loss.detach())
+            return loss
+        from ..ops.layers import linear_cross_entropy
+        return linear_cross_entropy(self._features_fused(x), self.fc1, labels, acc)
 
 
 def VGG11():

@@ -15,7 +15,10 @@ def native():
         # DDP_AMD_WGRAD_ATOMIC=1: split-K weight gradients accumulate with fp32 atomics (no
         # finish pass, but memory-side atomics run at ~1.3 TB/s vs ~6 TB/s for slab stores);
         # default 0 = slab + grouped finish reduction
-        _NATIVE.conv_options(int(os.environ.get("DDP_AMD_WGRAD_ATOMIC", "0")))
+        # DDP_AMD_CONV_PERSISTENT=1: conv grids sized to the resident slots, blocks loop over
+        # tiles and prefetch the next tile's first k-step (default 0: one tile per workgroup)
+        _NATIVE.conv_options(int(os.environ.get("DDP_AMD_WGRAD_ATOMIC", "0")),
+                             int(os.environ.get("DDP_AMD_CONV_PERSISTENT", "0")))
     return _NATIVE
 
 
@@ -89,9 +92,22 @@ class StepScratch:
         self.used = off + n
         return self.buf[off:off + n]
 
+    def take_transient(self, n):
+        """A zeroed slice valid until the next zero(): consecutive calls within one forward get
+        distinct slices (used for per-forward outputs such as the fused loss)."""
+        if not hasattr(self, "_transient"):
+            self._transient = self.take(256)
+            self._tcur = 0
+        if self._tcur + n > self._transient.numel():
+            return torch.zeros(n, dtype=torch.float32, device=self.buf.device)
+        out = self._transient[self._tcur:self._tcur + n]
+        self._tcur += n
+        return out
+
     def zero(self):
         if self.used:
             self.buf[:self.used].zero_()
+        self._tcur = 0
 
 
 _SCRATCH = {}

@@ -195,6 +195,48 @@ class _LinearSmallFn(torch.autograd.Function):
         return dx, None, None
 
 
+class _LinearCEFn(torch.autograd.Function):
+    """Classifier head fused with the mean softmax cross-entropy: ONE kernel computes the logits,
+    the loss and dlogits = (softmax - onehot) / B; the backward consumes dlogits scaled by the
+    incoming scalar gradient through a device pointer (no elementwise kernel). The loss lives in
+    the per-forward zeroed step scratch (no fill kernel); ``acc`` optionally receives a running
+    sum of the loss across steps (TrainStep's meter) from the same kernel."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, labels, acc):
+        B, F = x.shape
+        J = weight.shape[0]
+        check(x, BF16, name="linear input")
+        labels = labels.to(torch.int64).contiguous()
+        loss = step_scratch(x.device).take_transient(1).view(())
+        dl = torch.empty(B, J, dtype=F32, device=x.device)
+        native().linear_ce_fwd(ptr(x), ptr(weight), ptr(bias), ptr(labels), B, F, J, 0, ptr(dl),
+                               ptr(loss), 0, stream_handle(), loss_acc=ptr(acc))
+        ctx.save_for_backward(x, weight, bias, dl)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight, bias, dl = ctx.saved_tensors
+        B, F = x.shape
+        J = weight.shape[0]
+        g = g.contiguous().float()
+        gw = ensure_grad(weight)
+        gb = ensure_grad(bias) if bias is not None else None
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        native().linear_bwd(ptr(dl), ptr(x), ptr(weight), B, F, J, ptr(g), ptr(dx), ptr(gw),
+                            ptr(gb), stream_handle())
+        grad_ready([weight, bias])
+        return dx, None, None, None, None
+
+
+def linear_cross_entropy(x, linear, labels, acc=None):
+    """mean CE(linear(x), labels) in one kernel (J <= 16); see _LinearCEFn."""
+    if linear.weight.shape[0] > 16:
+        raise ValueError("linear_cross_entropy supports at most 16 outputs")
+    return _LinearCEFn.apply(x, linear.weight, linear.bias, labels, acc)
+
+
 def linear_small(x, linear):
     if linear.weight.shape[0] > 16:
         raise ValueError("linear_small supports at most 16 outputs")

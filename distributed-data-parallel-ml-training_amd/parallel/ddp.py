@@ -147,14 +147,22 @@ class DistributedDataParallel(nn.Module):
                 self.comm.broadcast(b, 0)
 
     # ------------------------------------------------------------ per-step
-    def forward(self, *args, **kwargs):
+    def _sync_buffers(self):
         if self.broadcast_buffers and self.comm.world > 1 and torch.is_grad_enabled():
             bufs = list(self.module.buffers())
             if bufs:
                 with torch.no_grad():
                     for b in bufs:
                         self.comm.broadcast(b, 0)
+
+    def forward(self, *args, **kwargs):
+        self._sync_buffers()
         return self.module(*args, **kwargs)
+
+    def forward_loss(self, *args, **kwargs):
+        """Fused forward + loss of the wrapped model (if it provides ``forward_loss``)."""
+        self._sync_buffers()
+        return self.module.forward_loss(*args, **kwargs)
 
     def _queue_finalize(self):
         if not self._in_backward:

@@ -77,12 +77,12 @@ def test_conv_dgrad(native_ext, case, layout):
     dzn = dz.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
     fmt = torch.contiguous_format if layout == "kcrs" else torch.channels_last
     dw = torch.zeros_like(conv.weight, memory_format=fmt)
-    native_ext.conv_options(int(layout == "krsc_atomic"))
+    native_ext.conv_options(int(layout == "krsc_atomic"), int(layout == "krsc_atomic"))
     try:
         dx = conv_backward(spec, xn, dzn, dw, True)
         torch.cuda.synchronize()
     finally:
-        native_ext.conv_options(0)
+        native_ext.conv_options(0, 0)
     xr = x.clone().requires_grad_(True)
     wr = conv.weight.detach().clone().requires_grad_(True)
     out = F.conv2d(xr, wr, None, stride, pad)

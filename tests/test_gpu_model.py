@@ -155,3 +155,31 @@ def test_training_reduces_loss(native_ext):
         v = st.pop_loss() / 10
         first = v if first is None else first
     assert v < first, (first, v)
+
+
+def test_fused_forward_loss_matches_unfused(native_ext):
+    """VGG.forward_loss (classifier + CE + loss meter in one kernel) == CE(model(x)) exactly in
+    value and gradients (same kernels upstream, same head math)."""
+    from ddp_amd.models import VGG11
+    from ddp_amd.engine import CrossEntropyLoss
+    from ddp_amd.optim import FusedSGD
+    torch.manual_seed(0)
+    a = VGG11().cuda()
+    b = copy.deepcopy(a)
+    oa, ob = FusedSGD(a.parameters(), lr=0.1), FusedSGD(b.parameters(), lr=0.1)
+    x = torch.randn(32, 3, 32, 32, device="cuda")
+    y = torch.randint(0, 10, (32,), device="cuda")
+    acc = torch.zeros((), device="cuda")
+    oa.zero_grad()
+    la = a.forward_loss(x, y, acc=acc)
+    la.backward()
+    ob.zero_grad()
+    lb = CrossEntropyLoss()(b(x), y)
+    lb.backward()
+    torch.cuda.synchronize()
+    assert abs(float(la) - float(lb)) < 1e-4 * max(1.0, abs(float(lb)))
+    assert abs(float(acc) - float(lb)) < 1e-4 * max(1.0, abs(float(lb)))
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        if pb.grad.norm() == 0:
+            continue
+        assert rel(pa.grad, pb.grad) < 1e-3, n

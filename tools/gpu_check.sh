@@ -24,6 +24,22 @@ for s in $steps; do
     benchresnet)
       timeout -k 10 300 python bench.py --model resnet50 --steps 20 --warmup 5 > gpurun_out/bench_resnet.log 2>&1
       rc=$?; tail -1 gpurun_out/bench_resnet.log; ok_or_stop $rc bench_resnet ;;
+    profresnet)
+      root="$GRAFT_REPO_ROOT"
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats \
+          --output-format csv -d "$root/gpurun_out/prof_resnet" -o resnet -- \
+          python3 "$root/bench.py" --model resnet50 --steps 6 --warmup 3 > "$root/gpurun_out/prof_resnet.log" 2>&1)
+      rc=$?; tail -1 gpurun_out/prof_resnet.log; ok_or_stop $rc prof_resnet ;;
+    convbench)
+      timeout -k 10 300 python tools/conv_bench.py --model vgg11 --json gpurun_out/conv_vgg.json > gpurun_out/conv_vgg.log 2>&1
+      rc=$?; tail -1 gpurun_out/conv_vgg.log; ok_or_stop $rc convbench_vgg
+      timeout -k 10 300 python tools/conv_bench.py --model resnet50 --json gpurun_out/conv_resnet.json > gpurun_out/conv_resnet.log 2>&1
+      rc=$?; tail -1 gpurun_out/conv_resnet.log; ok_or_stop $rc convbench_resnet ;;
+    convbenchp)  # persistent conv grids
+      DDP_AMD_CONV_PERSISTENT=1 timeout -k 10 300 python tools/conv_bench.py --model vgg11 --json gpurun_out/conv_vgg_p.json > gpurun_out/conv_vgg_p.log 2>&1
+      rc=$?; tail -1 gpurun_out/conv_vgg_p.log; ok_or_stop $rc convbench_vgg_p
+      DDP_AMD_CONV_PERSISTENT=1 timeout -k 10 300 python tools/conv_bench.py --model resnet50 --json gpurun_out/conv_resnet_p.json > gpurun_out/conv_resnet_p.log 2>&1
+      rc=$?; tail -1 gpurun_out/conv_resnet_p.log; ok_or_stop $rc convbench_resnet_p ;;
     bench8w)  # weak-scaling point and eager (no graph) comparison
       timeout -k 10 300 python bench.py --steps 40 --warmup 10 --no-graph > gpurun_out/bench_eager.log 2>&1
       rc=$?; tail -1 gpurun_out/bench_eager.log; ok_or_stop $rc bench_eager ;;
