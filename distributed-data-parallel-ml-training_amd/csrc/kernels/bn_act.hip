@@ -16,7 +16,10 @@
 //         finalize  — one thread per channel: k1 = S1/M, k2 = S2/M; dgamma += S2, dbeta += S1
 //         apply     — dz = scale * (dy_bn - k1 - xhat * k2);  d_res = dy_bn (residual branch)
 // The coefficient table is built ONCE per layer (a table rebuilt by every block would re-read
-// 16 replicas x C channels per block: ~800 MB per ResNet-50 BN layer).
+// 16 replicas x C channels per block: ~800 MB per ResNet-50 BN layer). For small layers
+// (blocks x channels x replicas below kFoldBytes) the finalize step is FOLDED into the apply
+// kernel instead: every block reduces the replicas it needs into LDS, saving a launch (each
+// dispatch costs ~4-5 us of the captured step).
 // Every apply/reduce thread owns 8 contiguous channels (one 16-byte vector) of an output pixel
 // and reads its coefficients straight from the (L2-resident) table: no LDS, no barrier before
 // the streaming loads.
@@ -87,9 +90,48 @@ __global__ __launch_bounds__(256) void bn_finalize_bwd_kernel(BnArgs a) {
   if (a.dbeta) a.dbeta[c] += s1;
 }
 
+// Replica reduction + coefficients of ALL channels into LDS (sc | sh), done by every block of a
+// FOLDed launch (small C x blocks: cheaper than a separate finalize launch); block 0 also writes
+// the coef table for the backward and updates the running statistics.
+__device__ __forceinline__ void fold_fwd_coeffs(const BnArgs& a, float* l_sc, float* l_sh) {
+  const float M = (float)a.N * a.H * a.W;
+  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+    float mu, is;
+    if (a.use_running) {
+      mu = a.running_mean[c];
+      is = rsqrtf(a.running_var[c] + a.eps);
+    } else {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int r = 0; r < kStatRep; ++r) {
+        s1 += a.stats[r * 2 * a.C + c];
+        s2 += a.stats[r * 2 * a.C + a.C + c];
+      }
+      mu = s1 / M;
+      const float var = fmaxf(s2 / M - mu * mu, 0.f);
+      is = rsqrtf(var + a.eps);
+      if (a.running_mean && blockIdx.x == 0) {
+        const float unbiased = M > 1.f ? var * M / (M - 1.f) : var;
+        a.running_mean[c] = (1.f - a.momentum) * a.running_mean[c] + a.momentum * mu;
+        a.running_var[c] = (1.f - a.momentum) * a.running_var[c] + a.momentum * unbiased;
+      }
+    }
+    const float sc = a.gamma[c] * is, sh = a.beta[c] - mu * sc;
+    l_sc[c] = sc;
+    l_sh[c] = sh;
+    if (blockIdx.x == 0) {
+      a.coef[kSc * a.C + c] = sc;
+      a.coef[kSh * a.C + c] = sh;
+      a.coef[kMu * a.C + c] = mu;
+      a.coef[kIs * a.C + c] = is;
+    }
+  }
+  __syncthreads();
+}
+
 // ------------------------------- forward apply -------------------------------
 // One thread = IPT items (output pixels) x 8 channels; every load is issued up front.
-template <bool POOL, int IPT>
+template <bool POOL, int IPT, bool FOLD>
 __global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnArgs a) {
   constexpr int NP = POOL ? 4 : 1;
   const int G = a.C / 8;
@@ -114,8 +156,24 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnArgs a) {
       zv[it][d] = ld8(a.z + off);
       if (!POOL && a.res) rv[it][POOL ? 0 : d] = ld8(a.res + off);
     }
-    ld8f(a.coef + kSc * a.C + cg * 8, sc[it]);
-    ld8f(a.coef + kSh * a.C + cg * 8, sh[it]);
+    if (!FOLD) {
+      ld8f(a.coef + kSc * a.C + cg * 8, sc[it]);
+      ld8f(a.coef + kSh * a.C + cg * 8, sh[it]);
+    }
+  }
+  if (FOLD) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    fold_fwd_coeffs(a, lds, lds + a.C);
+#pragma unroll
+    for (int it = 0; it < IPT; ++it) {
+      const size_t t = t0 + it * 256;
+      const int cg = (int)((t < total ? t : 0) % G);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sc[it][e] = lds[cg * 8 + e];
+        sh[it][e] = lds[a.C + cg * 8 + e];
+      }
+    }
   }
 #pragma unroll
   for (int it = 0; it < IPT; ++it) {
@@ -273,7 +331,7 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
   }
 }
 
-template <bool POOL, int IPT>
+template <bool POOL, int IPT, bool FOLD>
 __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(BnArgs a) {
   constexpr int NP = POOL ? 4 : 1;
   const int G = a.C / 8;
@@ -292,8 +350,37 @@ __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(BnArgs a) {
   ld8f(a.coef + kSh * a.C + c0, sh);
   ld8f(a.coef + kMu * a.C + c0, mu);
   ld8f(a.coef + kIs * a.C + c0, is);
-  ld8f(a.coef + kK1 * a.C + c0, k1);
-  ld8f(a.coef + kK2 * a.C + c0, k2);
+  if (!FOLD) {
+    ld8f(a.coef + kK1 * a.C + c0, k1);
+    ld8f(a.coef + kK2 * a.C + c0, k2);
+  } else {
+    // replica reduction of this block's channel chunk (small layers: no finalize launch);
+    // block row 0 owns the dgamma / dbeta accumulation
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int nch = Gb * 8;
+    const float inv_m = 1.f / ((float)a.N * a.H * a.W);
+    for (int i = threadIdx.x; i < nch; i += blockDim.x) {
+      const int c = cg_base * 8 + i;
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int r = 0; r < kStatRep; ++r) {
+        s1 += a.sums[r * 2 * a.C + c];
+        s2 += a.sums[r * 2 * a.C + a.C + c];
+      }
+      lds[i] = s1 * inv_m;
+      lds[nch + i] = s2 * inv_m;
+      if (blockIdx.x == 0) {
+        if (a.dgamma) a.dgamma[c] += s2;
+        if (a.dbeta) a.dbeta[c] += s1;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      k1[e] = lds[cgl * 8 + e];
+      k2[e] = lds[nch + cgl * 8 + e];
+    }
+  }
 #pragma unroll
   for (int it = 0; it < IPT; ++it) {
     if (!L.ok[it]) continue;
@@ -322,25 +409,37 @@ static unsigned blocks_for(size_t items, size_t per_block) {
   return (unsigned)(b < 1 ? 1 : b);
 }
 
+// Folding the finalize into the apply kernel costs every block a replica reduction of its
+// channels; worth it (one launch fewer) while that re-read traffic stays small.
+constexpr size_t kFoldBytes = 24u << 20;
+constexpr bool kFoldBwd = false;
+
+template <bool POOL, int IPT>
+static void launch_fwd(const BnArgs& a, size_t items, hipStream_t st) {
+  const unsigned nb = blocks_for(items, 256 * IPT);
+  if ((size_t)nb * a.C * 2 * kStatRep * sizeof(float) <= kFoldBytes) {
+    hipLaunchKernelGGL((bn_act_fwd_kernel<POOL, IPT, true>), dim3(nb), dim3(256),
+                       2 * a.C * sizeof(float), st, a);
+  } else {
+    hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3(blocks_for(a.C, 256)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((bn_act_fwd_kernel<POOL, IPT, false>), dim3(nb), dim3(256), 0, st, a);
+  }
+}
+
 extern "C" int ddp_bn_act_fwd(const BnArgs* args, hipStream_t st) {
   BnArgs a = *args;
   if (a.C % 8 || a.coef == nullptr) return -1;
   if (a.pool && a.res) return -1;  // residual add is only fused without pooling
   const int Ho = a.pool ? a.H / 2 : a.H, Wo = a.pool ? a.W / 2 : a.W;
   const size_t items = (size_t)a.N * Ho * Wo * (a.C / 8);
-  hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3(blocks_for(a.C, 256)), dim3(256), 0, st, a);
   // 1 item per thread for small layers; 2 (pooled) / 4 (plain) when there are enough to keep
   // every CU busy with several resident blocks
   if (a.pool) {
-    if (items >= 256 * 2048)
-      hipLaunchKernelGGL((bn_act_fwd_kernel<true, 2>), dim3(blocks_for(items, 512)), dim3(256), 0, st, a);
-    else
-      hipLaunchKernelGGL((bn_act_fwd_kernel<true, 1>), dim3(blocks_for(items, 256)), dim3(256), 0, st, a);
+    if (items >= 256 * 2048) launch_fwd<true, 2>(a, items, st);
+    else launch_fwd<true, 1>(a, items, st);
   } else {
-    if (items >= 256 * 4096)
-      hipLaunchKernelGGL((bn_act_fwd_kernel<false, 4>), dim3(blocks_for(items, 1024)), dim3(256), 0, st, a);
-    else
-      hipLaunchKernelGGL((bn_act_fwd_kernel<false, 1>), dim3(blocks_for(items, 256)), dim3(256), 0, st, a);
+    if (items >= 256 * 4096) launch_fwd<false, 4>(a, items, st);
+    else launch_fwd<false, 1>(a, items, st);
   }
   return (int)hipGetLastError();
 }
@@ -349,8 +448,17 @@ template <bool POOL, int IPT>
 static void launch_bwd(const BnArgs& a, size_t npix, int Gb, int chunks, hipStream_t st) {
   const unsigned bx = blocks_for(npix, (size_t)(256 / Gb) * IPT);
   hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<POOL, IPT>), dim3(bx, chunks), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3(blocks_for(a.C, 256)), dim3(256), 0, st, a);
-  hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT>), dim3(bx, chunks), dim3(256), 0, st, a);
+  // (measured: folding the backward finalize made the apply 3-4x slower — the replicated sums
+  // were just written by memory-side atomics and every block re-reads them uncached — so the
+  // backward keeps its separate finalize launch)
+  const size_t nch = (size_t)Gb * 8;
+  if (kFoldBwd && (size_t)bx * chunks * nch * 2 * kStatRep * sizeof(float) <= kFoldBytes) {
+    hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT, true>), dim3(bx, chunks), dim3(256),
+                       2 * nch * sizeof(float), st, a);
+  } else {
+    hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3(blocks_for(a.C, 256)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT, false>), dim3(bx, chunks), dim3(256), 0, st, a);
+  }
 }
 
 // a.coef must hold the table written by the matching forward; a.sums ([kStatRep][2][C]) must be

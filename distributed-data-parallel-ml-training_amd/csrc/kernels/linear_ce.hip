@@ -9,6 +9,7 @@
 //        dlogits = (softmax - onehot) / B is written for the backward (mean reduction).
 // bwd  : dx[b][:] = g * dlogits[b] @ W     (one wave per row, bf16 out)
 //        dW[j][f] += g * sum_b dlogits[b][j] x[b][f]; db[j] += g * sum_b dlogits[b][j]
+//        (both in one launch; g is read from device memory: autograd's incoming gradient)
 // The Linear weight is read straight from the fp32 master copy (20 KB).
 // A separate generic softmax-CE (any J, logits from the MFMA GEMM) serves ResNet-50's 1000-way head.
 #include "common.h"
@@ -23,8 +24,9 @@ __global__ __launch_bounds__(256) void linear_ce_fwd_kernel(
     const long long* __restrict__ labels, int B, int F, int J, float inv_b, float* logits_out,
     float* dlogits, float* loss_sum, int* correct, float* loss_acc) {
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= B) return;
+  const int row_raw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const bool live = row_raw < B;
+  const int row = live ? row_raw : B - 1;  // dead waves recompute the last row, store nothing
   float acc[kMaxJ];
 #pragma unroll
   for (int j = 0; j < kMaxJ; ++j) acc[j] = 0.f;
@@ -58,7 +60,7 @@ __global__ __launch_bounds__(256) void linear_ce_fwd_kernel(
     if (j < J) se += __expf(acc[j] - mx);
   const float lse = mx + __logf(se);
   const int y = labels ? (int)labels[row] : -1;
-  if (lane < J) {
+  if (live && lane < J) {
     float lj = 0.f;
 #pragma unroll
     for (int j = 0; j < kMaxJ; ++j)
@@ -69,24 +71,34 @@ __global__ __launch_bounds__(256) void linear_ce_fwd_kernel(
       dlogits[(size_t)row * J + lane] = (p - (lane == y ? 1.f : 0.f)) * inv_b;
     }
   }
-  if (lane == 0 && labels) {
+  // per-block reduction of the 4 rows' loss / hit terms, then one atomic per accumulator
+  __shared__ float lrow[4];
+  __shared__ int hrow[4];
+  if (lane == 0) {
     float ly = 0.f;
 #pragma unroll
     for (int j = 0; j < kMaxJ; ++j)
       if (j == y) ly = acc[j];
-    if (loss_sum) atomicAdd(loss_sum, (lse - ly) * inv_b);
-    if (loss_acc) atomicAdd(loss_acc, (lse - ly) * inv_b);  // running sum across steps
-    if (correct && arg == y) atomicAdd(correct, 1);
+    lrow[threadIdx.x >> 6] = (live && labels) ? (lse - ly) * inv_b : 0.f;
+    hrow[threadIdx.x >> 6] = (live && labels && arg == y) ? 1 : 0;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && labels) {
+    float l = 0.f;
+    int h = 0;
+    for (int r = 0; r < 4; ++r) { l += lrow[r]; h += hrow[r]; }
+    if (loss_sum) atomicAdd(loss_sum, l);
+    if (loss_acc) atomicAdd(loss_acc, l);  // running sum across steps
+    if (correct) atomicAdd(correct, h);
   }
 }
 
-// dx: one wave per row.
-__global__ __launch_bounds__(256) void linear_dx_kernel(const float* __restrict__ dlogits,
-                                                        const float* __restrict__ W, int B, int F,
-                                                        int J, const float* gscale,
-                                                        unsigned short* dx) {
+// dx: one wave per row (block bx covers rows 4 bx .. 4 bx + 3).
+__device__ __forceinline__ void linear_dx_block(const float* __restrict__ dlogits,
+                                                const float* __restrict__ W, int B, int F, int J,
+                                                const float* gscale, unsigned short* dx, int bx) {
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int row = bx * 4 + (threadIdx.x >> 6);
   if (row >= B) return;
   const float g = gscale ? *gscale : 1.f;
   float dl[kMaxJ];
@@ -113,14 +125,14 @@ __global__ __launch_bounds__(256) void linear_dx_kernel(const float* __restrict_
 // dW / db: block = 64 feature columns x one 64-row batch chunk (4 row groups of 16 rows);
 // partial sums reduced through LDS, one atomic per (j, f) per block.
 constexpr int kDwRows = 8;  // many small row chunks: latency-bound otherwise
-__global__ __launch_bounds__(256) void linear_dw_kernel(const float* __restrict__ dlogits,
-                                                        const unsigned short* __restrict__ x,
-                                                        int B, int F, int J, const float* gscale,
-                                                        float* dW, float* db) {
+__device__ __forceinline__ void linear_dw_block(const float* __restrict__ dlogits,
+                                                const unsigned short* __restrict__ x, int B, int F,
+                                                int J, const float* gscale, float* dW, float* db,
+                                                int bx, int by) {
   __shared__ float red[4][kMaxJ][64];
   const int fl = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int f = blockIdx.x * 64 + fl;
-  const int r0 = blockIdx.y * kDwRows;
+  const int f = bx * 64 + fl;
+  const int r0 = by * kDwRows;
   const int r1 = min(B, r0 + kDwRows);
   const float g = gscale ? *gscale : 1.f;
   float acc[kMaxJ];
@@ -143,10 +155,26 @@ __global__ __launch_bounds__(256) void linear_dw_kernel(const float* __restrict_
         atomicAdd(dW + (size_t)j * F + f,
                   (red[0][j][fl] + red[1][j][fl] + red[2][j][fl] + red[3][j][fl]) * g);
   }
-  if (blockIdx.x == 0 && threadIdx.x < J && db) {
+  if (bx == 0 && threadIdx.x < J && db) {
     float s = 0.f;
     for (int r = r0; r < r1; ++r) s += dlogits[(size_t)r * J + threadIdx.x];
     atomicAdd(db + threadIdx.x, s * g);
+  }
+}
+
+// dx and dW/db in ONE launch: blocks [0, ndx) compute dx rows, the rest dW chunks.
+__global__ __launch_bounds__(256) void linear_bwd_kernel(const float* __restrict__ dlogits,
+                                                         const unsigned short* __restrict__ x,
+                                                         const float* __restrict__ W, int B,
+                                                         int F, int J, const float* gscale,
+                                                         unsigned short* dx, float* dW, float* db,
+                                                         int ndx, int nfx) {
+  const int b = blockIdx.x;
+  if (b < ndx) {
+    linear_dx_block(dlogits, W, B, F, J, gscale, dx, b);
+  } else {
+    const int t = b - ndx;
+    linear_dw_block(dlogits, x, B, F, J, gscale, dW, db, t % nfx, t / nfx);
   }
 }
 
@@ -223,12 +251,11 @@ extern "C" int ddp_linear_bwd(const float* dlogits, const void* x, const float* 
                               int J, const float* gscale, void* dx, float* dW, float* db,
                               hipStream_t st) {
   if (J > kMaxJ || F % 8) return -1;
-  if (dx)
-    hipLaunchKernelGGL(linear_dx_kernel, dim3((B + 3) / 4), dim3(256), 0, st, dlogits, W, B, F, J,
-                       gscale, (unsigned short*)dx);
-  hipLaunchKernelGGL(linear_dw_kernel, dim3((F + 63) / 64, (B + kDwRows - 1) / kDwRows), dim3(256),
-                     0, st, dlogits,
-                     (const unsigned short*)x, B, F, J, gscale, dW, db);
+  const int ndx = dx ? (B + 3) / 4 : 0;
+  const int nfx = (F + 63) / 64, nry = (B + kDwRows - 1) / kDwRows;
+  hipLaunchKernelGGL(linear_bwd_kernel, dim3(ndx + nfx * nry), dim3(256), 0, st, dlogits,
+                     (const unsigned short*)x, W, B, F, J, gscale, (unsigned short*)dx, dW, db,
+                     ndx, nfx);
   return (int)hipGetLastError();
 }
 

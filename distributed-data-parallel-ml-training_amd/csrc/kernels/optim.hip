@@ -111,6 +111,9 @@ __device__ __forceinline__ void tile_dims(int RS, int* TK, int* TC) {
 struct SgdHyper {
   float lr, momentum, wd, grad_scale;
   int nesterov;
+  int zero_grad;  // write 0 to every gradient after use (replaces the next step's zero_grad fill)
+  int* counter;   // optional step counter (data cursor): += delta by one thread
+  int delta;
 };
 
 __device__ __forceinline__ float sgd1(float p, float g, float& b, const SgdHyper& h) {
@@ -125,11 +128,12 @@ __device__ __forceinline__ float sgd1(float p, float g, float& b, const SgdHyper
 __global__ __launch_bounds__(256) void sgd_pack_kernel(const int4* __restrict__ items,
                                                        const long long* __restrict__ descs,
                                                        float* __restrict__ p,
-                                                       const float* __restrict__ g,
+                                                       float* __restrict__ g,
                                                        float* __restrict__ buf, SgdHyper h) {
   __shared__ float tile[kTileElems];
   const int4 it = items[blockIdx.x];
   const int tid = threadIdx.x;
+  if (h.counter && blockIdx.x == 0 && tid == 0) atomicAdd(h.counter, h.delta);
   if (it.x == 0) {
     const size_t off = (size_t)(unsigned)it.y;
     const int cnt = it.z;
@@ -144,11 +148,13 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(const int4* __restrict__ 
         pv.w = sgd1(pv.w, gv.w, bv.w, h);
         *reinterpret_cast<float4*>(p + off + i) = pv;
         *reinterpret_cast<float4*>(buf + off + i) = bv;
+        if (h.zero_grad) *reinterpret_cast<float4*>(g + off + i) = make_float4(0.f, 0.f, 0.f, 0.f);
       } else {
         for (int e = i; e < min(cnt, i + 4); ++e) {
           float b = buf[off + e];
           p[off + e] = sgd1(p[off + e], g[off + e], b, h);
           buf[off + e] = b;
+          if (h.zero_grad) g[off + e] = 0.f;
         }
       }
     }
@@ -177,6 +183,7 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(const int4* __restrict__ 
       const float np = sgd1(p[gi], g[gi], b, h);
       p[gi] = np;
       buf[gi] = b;
+      if (h.zero_grad) g[gi] = 0.f;
       tile[kl * TC * RS + e] = np;  // tile layout [kl][cl][rs]
     }
   } else {
@@ -189,6 +196,7 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(const int4* __restrict__ 
       const float np = sgd1(p[gi], g[gi], b, h);
       p[gi] = np;
       buf[gi] = b;
+      if (h.zero_grad) g[gi] = 0.f;
       tile[kl * TC * RS + cl * RS + rs] = np;
     }
   }
@@ -248,9 +256,10 @@ extern "C" int ddp_pack_conv_weights(const PackDesc* descs, int n, hipStream_t s
 }
 
 extern "C" int ddp_sgd_pack(const void* items, int n_items, const long long* descs, float* p,
-                            const float* g, float* buf, float lr, float momentum, float wd,
-                            float grad_scale, int nesterov, hipStream_t st) {
-  SgdHyper h{lr, momentum, wd, grad_scale, nesterov};
+                            float* g, float* buf, float lr, float momentum, float wd,
+                            float grad_scale, int nesterov, int zero_grad, int* counter,
+                            int delta, hipStream_t st) {
+  SgdHyper h{lr, momentum, wd, grad_scale, nesterov, zero_grad, counter, delta};
   if (n_items <= 0) return 0;
   hipLaunchKernelGGL(sgd_pack_kernel, dim3(n_items), dim3(256), 0, st, (const int4*)items, descs,
                      p, g, buf, h);

@@ -168,15 +168,22 @@ class DeviceLoader:
             self._static = (x, y)
         return self._static
 
-    def fill(self):
+    def fill(self, advance=True):
         """Write the next batch (cursor-addressed, wraps around the shard) into the static
-        buffers and advance the device cursor. Safe to capture into a hipGraph."""
+        buffers and advance the device cursor. Safe to capture into a hipGraph.
+        ``advance=False`` leaves the increment to the caller (engine/step.py folds it into the
+        optimizer launch: see ``cursor_advance``)."""
         from ..ops.common import native, stream_handle
         x, y = self.static_batch()
         self._launch(x, y, self.idx.data_ptr(), self.idx.numel(), self.batch_size,
                      self.cursor.data_ptr())
-        native().counter_add(self.cursor.data_ptr(), 1, stream_handle())
+        if advance:
+            native().counter_add(self.cursor.data_ptr(), 1, stream_handle())
         return x, y
+
+    def cursor_advance(self):
+        """(device pointer, delta) of the pending cursor increment after ``fill(advance=False)``."""
+        return (self.cursor.data_ptr(), 1)
 
 
 def make_loader(dataset, batch_size, device, num_replicas=1, rank=0, train=True, shard=True,

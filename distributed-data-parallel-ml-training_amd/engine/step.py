@@ -20,8 +20,12 @@ class TrainStep:
         self.use_graph = use_graph
         dev = loader.device
         self.loss_sum = torch.zeros((), dtype=torch.float32, device=dev)
+        self._one = torch.ones((), dtype=torch.float32, device=dev)
         self.graph = None
         self.fused = self._fused_loss()
+        self.fold_opt = bool(getattr(optimizer, "_fused", False)) and hasattr(loader, "cursor_advance")
+        if self.fold_opt:
+            optimizer.zero_grad()  # later steps get clean gradients from the previous step's launch
 
     def _fused_loss(self):
         """Use the model's fused classifier+loss when the criterion is the plain mean CE."""
@@ -31,17 +35,23 @@ class TrainStep:
                 and type(self.criterion) is CrossEntropyLoss)
 
     def _body(self):
-        self.optimizer.zero_grad()
-        x, y = self.loader.fill()
+        if not self.fold_opt:
+            self.optimizer.zero_grad()
+        x, y = self.loader.fill(advance=not self.fold_opt)
         if self.fused:
             # classifier + loss + loss meter in one kernel (no logits tensor, no extra adds)
-            loss = self.model.forward_loss(x, y, acc=self.loss_sum)
+            loss = self.model.forward_loss(x, y, acc=self.loss_sum, transient=True)
         else:
             loss = self.criterion(self.model(x), y)
-        loss.backward()
+        loss.backward(self._one)  # persistent ones: no fill kernel for the seed gradient
         if self.sync is not None:
             self.sync(self.model)
-        self.optimizer.step()
+        if self.fold_opt:
+            # the optimizer launch also clears the gradients for the next step and advances
+            # the data cursor: no zero_grad fill, no counter kernel
+            self.optimizer.step(zero_grad=True, counter=self.loader.cursor_advance())
+        else:
+            self.optimizer.step()
         if not self.fused:
             self.loss_sum.add_(loss.detach())
 

@@ -99,18 +99,19 @@ class _VGG(nn.Module):
         from ..ops.layers import linear_small
         return linear_small(self._features_fused(x), self.fc1)
 
-    def forward_loss(self, x, labels, acc=None):
+    def forward_loss(self, x, labels, acc=None, transient=False):
         """``CrossEntropyLoss()(self(x), labels)`` with the classifier and the loss fused into one
         kernel on the GPU (engine/step.py uses it for the captured training step). ``acc`` (fp32
         scalar) additionally accumulates the loss across calls. The returned loss tensor is only
-        valid until the next forward (it lives in the per-forward scratch)."""
+        valid until the next forward when ``transient`` (it then lives in the per-forward
+        scratch and costs no fill launch)."""
         if not x.is_cuda:
             loss = nn.functional.cross_entropy(self.forward(x), labels)
             if acc is not None:
                 acc.add_(loss.detach())
             return loss
         from ..ops.layers import linear_cross_entropy
-        return linear_cross_entropy(self._features_fused(x), self.fc1, labels, acc)
+        return linear_cross_entropy(self._features_fused(x), self.fc1, labels, acc, transient)
 
 
 def VGG11():

@@ -198,17 +198,18 @@ class _LinearSmallFn(torch.autograd.Function):
 class _LinearCEFn(torch.autograd.Function):
     """Classifier head fused with the mean softmax cross-entropy: ONE kernel computes the logits,
     the loss and dlogits = (softmax - onehot) / B; the backward consumes dlogits scaled by the
-    incoming scalar gradient through a device pointer (no elementwise kernel). The loss lives in
-    the per-forward zeroed step scratch (no fill kernel); ``acc`` optionally receives a running
-    sum of the loss across steps (TrainStep's meter) from the same kernel."""
+    incoming scalar gradient through a device pointer (no elementwise kernel). ``acc``
+    optionally receives a running sum of the loss across steps (TrainStep's meter) from the
+    same kernel."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, labels, acc):
+    def forward(ctx, x, weight, bias, labels, acc, transient):
         B, F = x.shape
         J = weight.shape[0]
         check(x, BF16, name="linear input")
         labels = labels.to(torch.int64).contiguous()
-        loss = step_scratch(x.device).take_transient(1).view(())
+        loss = (step_scratch(x.device).take_transient(1).view(()) if transient
+                else torch.zeros((), dtype=F32, device=x.device))
         dl = torch.empty(B, J, dtype=F32, device=x.device)
         native().linear_ce_fwd(ptr(x), ptr(weight), ptr(bias), ptr(labels), B, F, J, 0, ptr(dl),
                                ptr(loss), 0, stream_handle(), loss_acc=ptr(acc))
@@ -227,14 +228,16 @@ class _LinearCEFn(torch.autograd.Function):
         native().linear_bwd(ptr(dl), ptr(x), ptr(weight), B, F, J, ptr(g), ptr(dx), ptr(gw),
                             ptr(gb), stream_handle())
         grad_ready([weight, bias])
-        return dx, None, None, None, None
+        return dx, None, None, None, None, None
 
 
-def linear_cross_entropy(x, linear, labels, acc=None):
-    """mean CE(linear(x), labels) in one kernel (J <= 16); see _LinearCEFn."""
+def linear_cross_entropy(x, linear, labels, acc=None, transient=False):
+    """mean CE(linear(x), labels) in one kernel (J <= 16); see _LinearCEFn. ``transient=True``
+    returns the loss in the per-forward scratch (saves a fill launch; valid until the next
+    model forward on this device — the captured training step uses it)."""
     if linear.weight.shape[0] > 16:
         raise ValueError("linear_cross_entropy supports at most 16 outputs")
-    return _LinearCEFn.apply(x, linear.weight, linear.bias, labels, acc)
+    return _LinearCEFn.apply(x, linear.weight, linear.bias, labels, acc, transient)
 
 
 def linear_small(x, linear):

@@ -74,9 +74,15 @@ class FusedSGD(torch.optim.SGD):
             super().zero_grad(set_to_none=set_to_none)
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, zero_grad=False, counter=None):
+        """One fused launch. ``zero_grad=True`` also clears every gradient after its use (the
+        next step then needs no zero_grad fill); ``counter=(int32 device ptr, delta)`` is
+        advanced by the same launch (the on-device data cursor of engine/step.py)."""
         if not self._fused:
-            return super().step(closure)
+            out = super().step(closure)
+            if zero_grad:
+                super().zero_grad(set_to_none=False)
+            return out
         from ..ops.common import native, stream_handle
         g = self.param_groups[0]
         s = stream_handle()
@@ -86,7 +92,10 @@ class FusedSGD(torch.optim.SGD):
         native().sgd_pack(items.data_ptr(), n_items, descs.data_ptr(), a.data.data_ptr(),
                           a.grad.data_ptr(), self.momentum_buffer.data_ptr(), float(g["lr"]),
                           float(g["momentum"]), float(g["weight_decay"]),
-                          float(self._grad_scale_factor), int(bool(g["nesterov"])), s)
+                          float(self._grad_scale_factor), int(bool(g["nesterov"])), s,
+                          zero_grad=int(bool(zero_grad)),
+                          counter=int(counter[0]) if counter else 0,
+                          delta=int(counter[1]) if counter else 0)
         return None
 
     def state_dict(self):

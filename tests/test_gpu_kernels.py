@@ -321,3 +321,30 @@ def test_maxpool3x3s2_and_avgpool(native_ext):
     a = global_avg_pool(xn.detach().requires_grad_(True))
     ar = x.mean((2, 3))
     assert rel_err(a, ar) < 1e-2
+
+
+def test_fused_sgd_zero_grad_and_counter(native_ext):
+    """step(zero_grad=True, counter=...) == step() + zero_grad() + counter += delta."""
+    from ddp_amd.optim import FusedSGD
+    from ddp_amd.ops.layers import ConvBNActSpec
+    torch.manual_seed(0)
+    conv = torch.nn.Conv2d(64, 128, 3, padding=1).to(DEV)
+    ConvBNActSpec(conv, None)  # packed conv weight: exercises the tile path too
+    ps = list(conv.parameters()) + [torch.nn.Parameter(torch.randn(33, device=DEV))]
+    ref = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    opt = FusedSGD(ps, lr=0.1, momentum=0.9, weight_decay=1e-4)
+    ropt = torch.optim.SGD(ref, lr=0.1, momentum=0.9, weight_decay=1e-4)
+    cnt = torch.zeros(1, dtype=torch.int32, device=DEV)
+    for _ in range(2):
+        gs = [torch.randn_like(p) for p in ps]
+        for p, g in zip(ps, gs):
+            p.grad.copy_(g)
+        for p, g in zip(ref, gs):
+            p.grad = g.clone()
+        opt.step(zero_grad=True, counter=(cnt.data_ptr(), 3))
+        ropt.step()
+        torch.cuda.synchronize()
+        assert all(float(p.grad.abs().max()) == 0.0 for p in ps)
+    assert int(cnt.item()) == 6
+    for p, r in zip(ps, ref):
+        assert torch.allclose(p, r, rtol=1e-5, atol=1e-6)
