@@ -12,6 +12,8 @@ structures), then ``torch.cuda.graph`` capture; replays are bit-identical to eag
 """
 import torch
 
+from ..utils.trace import trace_range
+
 
 class TrainStep:
     def __init__(self, model, optimizer, criterion, loader, sync=None, use_graph=True):
@@ -37,21 +39,26 @@ class TrainStep:
     def _body(self):
         if not self.fold_opt:
             self.optimizer.zero_grad()
-        x, y = self.loader.fill(advance=not self.fold_opt)
-        if self.fused:
-            # classifier + loss + loss meter in one kernel (no logits tensor, no extra adds)
-            loss = self.model.forward_loss(x, y, acc=self.loss_sum, transient=True)
-        else:
-            loss = self.criterion(self.model(x), y)
-        loss.backward(self._one)  # persistent ones: no fill kernel for the seed gradient
+        with trace_range("data"):
+            x, y = self.loader.fill(advance=not self.fold_opt)
+        with trace_range("forward"):
+            if self.fused:
+                # classifier + loss + loss meter in one kernel (no logits tensor, no extra adds)
+                loss = self.model.forward_loss(x, y, acc=self.loss_sum, transient=True)
+            else:
+                loss = self.criterion(self.model(x), y)
+        with trace_range("backward"):
+            loss.backward(self._one)  # persistent ones: no fill kernel for the seed gradient
         if self.sync is not None:
-            self.sync(self.model)
-        if self.fold_opt:
-            # the optimizer launch also clears the gradients for the next step and advances
-            # the data cursor: no zero_grad fill, no counter kernel
-            self.optimizer.step(zero_grad=True, counter=self.loader.cursor_advance())
-        else:
-            self.optimizer.step()
+            with trace_range("sync"):
+                self.sync(self.model)
+        with trace_range("optimizer"):
+            if self.fold_opt:
+                # the optimizer launch also clears the gradients for the next step and advances
+                # the data cursor: no zero_grad fill, no counter kernel
+                self.optimizer.step(zero_grad=True, counter=self.loader.cursor_advance())
+            else:
+                self.optimizer.step()
         if not self.fused:
             self.loss_sum.add_(loss.detach())
 

@@ -12,6 +12,8 @@ sync call at :143) and ``test_model`` (part1/main.py:96-111):
 import time
 
 import torch
+
+from ..utils.trace import trace_range
 import torch.nn as nn
 
 
@@ -32,15 +34,20 @@ def train_model(model, train_loader, optimizer, criterion, epoch, device="cpu", 
     stats = {"iter_ns": []}
     for batch_idx, (data, target) in enumerate(train_loader):
         start_time = time.perf_counter_ns()
-        data, target = data.to(device), target.to(device)
+        with trace_range("data"):
+            data, target = data.to(device), target.to(device)
 
         optimizer.zero_grad()
-        output = model(data)
-        loss = criterion(output, target)
-        loss.backward()
+        with trace_range("forward"):
+            output = model(data)
+            loss = criterion(output, target)
+        with trace_range("backward"):
+            loss.backward()
         if sync is not None:
-            sync(model)
-        optimizer.step()
+            with trace_range("sync"):
+                sync(model)
+        with trace_range("optimizer"):
+            optimizer.step()
 
         running_loss += loss.item()
         if batch_idx % 20 == 19:
