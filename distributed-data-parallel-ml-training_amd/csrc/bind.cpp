@@ -52,11 +52,12 @@ PYBIND11_MODULE(_native, m) {
                        P<float>(ws), ws_elems, splits, S(st)), "conv_fwd");
   });
   m.def("conv_dgrad", [](py::tuple g, uintptr_t dy, uintptr_t wt, uintptr_t dx, uintptr_t ws,
-                         size_t ws_elems, int splits, uintptr_t st) {
+                         size_t ws_elems, int splits, uintptr_t st, int accumulate) {
     auto c = geom(g);
     check(ddp_conv_dgrad(&c, P<void>(dy), P<void>(wt), P<void>(dx), P<float>(ws), ws_elems,
-                         splits, S(st)), "conv_dgrad");
-  });
+                         splits, accumulate, S(st)), "conv_dgrad");
+  }, py::arg("g"), py::arg("dy"), py::arg("wt"), py::arg("dx"), py::arg("ws"),
+     py::arg("ws_elems"), py::arg("splits"), py::arg("stream"), py::arg("accumulate") = 0);
   m.def("conv_wgrad", [](py::tuple g, uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws,
                          size_t ws_elems, int splits, uintptr_t st) {
     auto c = geom(g);

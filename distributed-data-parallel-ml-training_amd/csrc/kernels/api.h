@@ -72,7 +72,7 @@ extern "C" {
 int ddp_conv_fwd(const ddp_amd::ConvGeom* g, const void* x, const void* wc, const float* bias,
                  void* y, float* stats, float* ws, size_t ws_elems, int splits, hipStream_t st);
 int ddp_conv_dgrad(const ddp_amd::ConvGeom* g, const void* dy, const void* wt, void* dx,
-                   float* ws, size_t ws_elems, int splits, hipStream_t st);
+                   float* ws, size_t ws_elems, int splits, int accumulate, hipStream_t st);
 int ddp_conv_wgrad(const ddp_amd::ConvGeom* g, const void* dy, const void* x, float* dw,
                    float* ws, size_t ws_elems, int splits, hipStream_t st);
 int ddp_bn_act_fwd(const ddp_amd::BnArgs* a, hipStream_t st);

@@ -76,6 +76,7 @@ struct ConvArgs {
   // j + qb - u): a stride-1 problem with 1/stride^2 of the rows and taps (sub-pixel split).
   int phase;
   int pa, pb, Hp, Wp, r0, s0, Rt, St, qa, qb;
+  int accumulate;            // DGRAD: dx = bf16(dx + result) (merges a second gradient branch)
   int a_bytes, b_bytes;      // operand sizes: buffer-resource bounds (reads past them give 0)
   FastDiv dPQ, dQ;           // WGRAD pixel decomposition
 };
@@ -480,7 +481,17 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
           const int i = rem / args.Wp, j = rem - i * args.Wp;
           orow = ((size_t)n * gg.H + args.pa + gg.stride * i) * gg.W + args.pb + gg.stride * j;
         }
-        *reinterpret_cast<uint2*>(args.out + orow * args.Ng + col) = pk;
+        if (MODE == MODE_DGRAD && args.accumulate) {  // dx += (second gradient branch)
+          uint2* dst = reinterpret_cast<uint2*>(args.out + orow * args.Ng + col);
+          const uint2 old = *dst;
+          pk.x = (unsigned)f2bf(v[0] + bf2f((unsigned short)(old.x & 0xffff))) |
+                 ((unsigned)f2bf(v[1] + bf2f((unsigned short)(old.x >> 16))) << 16);
+          pk.y = (unsigned)f2bf(v[2] + bf2f((unsigned short)(old.y & 0xffff))) |
+                 ((unsigned)f2bf(v[3] + bf2f((unsigned short)(old.y >> 16))) << 16);
+          *dst = pk;
+        } else {
+          *reinterpret_cast<uint2*>(args.out + orow * args.Ng + col) = pk;
+        }
         if (MODE == MODE_FWD) {
           const float r0 = bf2f(h0), r1 = bf2f(h1), r2 = bf2f(h2), r3 = bf2f(h3);
           s[0] += r0; s[1] += r1; s[2] += r2; s[3] += r3;
@@ -565,7 +576,8 @@ __device__ __forceinline__ size_t map_row(const RowMap& m, int row) {
 __global__ __launch_bounds__(256) void splitk_finish_kernel(const float* ws, int splits,
                                                             unsigned short* out,
                                                             const float* bias, float* stats,
-                                                            int Mg, int Ng, RowMap rmap) {
+                                                            int Mg, int Ng, RowMap rmap,
+                                                            int accumulate) {
   __shared__ float red[2][8][256];
   const int G = Ng / 8;
   const int Gb = G < 256 ? G : 256;
@@ -590,6 +602,12 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(const float* ws, int
       v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
       v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
     }
+    unsigned short* dst = out + map_row(rmap, row) * Ng + cg * 8;
+    if (accumulate) {
+      const u16x8 old = ld8(dst);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += bf2f(old[e]);
+    }
     u16x8 o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -598,7 +616,7 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(const float* ws, int
       s[e] += r;
       ss[e] += r * r;
     }
-    st8(out + map_row(rmap, row) * Ng + cg * 8, o);
+    st8(dst, o);
   }
   if (!stats) return;
 #pragma unroll
@@ -800,7 +818,7 @@ static void launch_cfg(ConvArgs& a, int splits, hipStream_t st) {
     if (a.phase) rm = RowMap{a.g.stride, a.Hp, a.Wp, a.g.H, a.g.W, a.pa, a.pb};
     hipLaunchKernelGGL(splitk_finish_kernel, dim3(bx, chunks), dim3(256), 0, st, a.ws, splits,
                        a.out, MODE == MODE_FWD ? a.bias : nullptr,
-                       MODE == MODE_FWD ? a.stats : nullptr, a.Mg, a.Ng, rm);
+                       MODE == MODE_FWD ? a.stats : nullptr, a.Mg, a.Ng, rm, a.accumulate);
   }
 }
 
@@ -850,9 +868,11 @@ extern "C" int ddp_conv_fwd(const ConvGeom* g, const void* x, const void* wc, co
 }
 
 extern "C" int ddp_conv_dgrad(const ConvGeom* g, const void* dy, const void* wt, void* dx,
-                              float* ws, size_t ws_elems, int splits, hipStream_t st) {
+                              float* ws, size_t ws_elems, int splits, int accumulate,
+                              hipStream_t st) {
   if (g->C % 8 || g->K % 8) return -1;
   ConvArgs a{};
+  a.accumulate = accumulate;
   a.g = *g;
   a.a = (const unsigned short*)dy;
   a.b = (const unsigned short*)wt;
@@ -878,7 +898,7 @@ extern "C" int ddp_conv_dgrad(const ConvGeom* g, const void* dy, const void* wt,
       const int r0 = (pa + g->pad) % sd, s0 = (pb + g->pad) % sd;
       if ((r0 >= g->R || s0 >= g->S) && pa < g->H && pb < g->W) zero_fill = true;
     }
-  if (zero_fill) {
+  if (zero_fill && !accumulate) {  // (accumulating: untouched phases keep their values)
     const hipError_t e = hipMemsetAsync(dx, 0, (size_t)g->N * g->H * g->W * g->C * 2, st);
     if (e != hipSuccess) return (int)e;
   }

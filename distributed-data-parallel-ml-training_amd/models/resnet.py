@@ -52,12 +52,17 @@ class Bottleneck(nn.Module):
         return self._specs
 
     def forward_fused(self, h):
-        from ..ops.layers import conv_bn_act
+        from ..ops.layers import conv_bn_act, GradLink
         s1, s2, s3, sd = self.specs()
-        out = conv_bn_act(h, s1)
+        # the block input feeds two branches; their gradients meet in a GradLink (the second
+        # one accumulates from its dgrad epilogue) instead of an autograd add kernel
+        link = GradLink() if (h.requires_grad and torch.is_grad_enabled()) else None
+        out = conv_bn_act(h, s1, in_link=link)
         out = conv_bn_act(out, s2)
-        identity = conv_bn_act(h, sd) if sd is not None else h
-        return conv_bn_act(out, s3, residual=identity)
+        if sd is not None:
+            identity = conv_bn_act(h, sd, in_link=link)
+            return conv_bn_act(out, s3, residual=identity)
+        return conv_bn_act(out, s3, residual=h, res_link=link)
 
 
 class ResNet(nn.Module):

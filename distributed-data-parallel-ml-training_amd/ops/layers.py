@@ -94,7 +94,36 @@ def conv_forward(spec, x, bias=None, stats=None):
     return z
 
 
-def conv_backward(spec, x, dz, dweight, need_dx):
+class GradLink:
+    """Merges the two gradient branches that meet at a residual block's input without an add
+    kernel. Both consumers of the tensor (the first conv of the branch and the identity /
+    downsample path) report to the link during backward: the first one to run leaves its
+    gradient in the link and returns None to autograd; the second one adds its contribution in
+    place — a conv dgrad writes ``dx += ...`` from its epilogue — and returns the sum. Autograd's
+    own accumulation (None + sum) then needs no kernel. One link serves one forward."""
+
+    def __init__(self, consumers=2):
+        self.expected = consumers
+        self.seen = 0
+        self.buf = None
+
+    def offer(self, t):
+        """A consumer whose gradient is already a tensor (the BN residual gradient)."""
+        self.seen += 1
+        if self.buf is None:
+            self.buf = t
+        else:
+            self.buf.add_(t)  # (not hit by the built-in models: the residual producer runs first)
+        return self.result()
+
+    def result(self):
+        if self.seen < self.expected:
+            return None
+        out, self.buf = self.buf, None
+        return out
+
+
+def conv_backward(spec, x, dz, dweight, need_dx, link=None):
     N, H, W, C = x.shape
     g = spec.geom(N, H, W, weight_krsc(dweight))
     s = stream_handle()
@@ -104,14 +133,24 @@ def conv_backward(spec, x, dz, dweight, need_dx):
         return None
     if spec.wt is None:
         raise RuntimeError("dgrad requested for a channel-padded input layer")
+    if link is not None and link.buf is not None:
+        # second branch: accumulate into the first branch's gradient from the GEMM epilogue
+        native().conv_dgrad(g, ptr(dz), ptr(spec.wt), ptr(link.buf), ptr(ws), ws.numel(), 0, s,
+                            accumulate=1)
+        link.seen += 1
+        return link.result()
     dx = torch.empty_like(x)
     native().conv_dgrad(g, ptr(dz), ptr(spec.wt), ptr(dx), ptr(ws), ws.numel(), 0, s)
+    if link is not None:
+        link.seen += 1
+        link.buf = dx
+        return link.result()
     return dx
 
 
 class _ConvBNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, gamma, beta, residual, spec):
+    def forward(ctx, x, weight, bias, gamma, beta, residual, spec, in_link=None, res_link=None):
         spec.maybe_pack()
         N, H, W, _ = x.shape
         stats = spec.stats  # zeroed by the model's per-forward StepScratch.zero()
@@ -134,6 +173,7 @@ class _ConvBNActFn(torch.autograd.Function):
                             ptr(spec.coef))
         ctx.spec = spec
         ctx.has_res = residual is not None
+        ctx.in_link, ctx.res_link = in_link, res_link
         ctx.save_for_backward(x, z, stats, weight, bias, gamma, beta, residual)
         return y
 
@@ -155,14 +195,19 @@ class _ConvBNActFn(torch.autograd.Function):
                             ptr(dz), ptr(dres), ptr(gg), ptr(gbt), ptr(gb), stream_handle(),
                             ptr(spec.coef))
         grad_ready([gamma, beta, bias])
-        dx = conv_backward(spec, x, dz, gw, ctx.needs_input_grad[0])
+        if ctx.res_link is not None and dres is not None:
+            dres = ctx.res_link.offer(dres)
+        dx = conv_backward(spec, x, dz, gw, ctx.needs_input_grad[0], ctx.in_link)
         grad_ready([weight])
-        return dx, None, None, None, None, dres, None
+        return dx, None, None, None, None, dres, None, None, None
 
 
-def conv_bn_act(x, spec, residual=None):
+def conv_bn_act(x, spec, residual=None, in_link=None, res_link=None):
+    """Fused conv -> BN (+residual) -> ReLU (-> 2x2 pool). ``in_link`` / ``res_link``: GradLink
+    through which the input / residual gradient is merged with the other branch (ResNet)."""
     conv, bn = spec.conv, spec.bn
-    return _ConvBNActFn.apply(x, conv.weight, conv.bias, bn.weight, bn.bias, residual, spec)
+    return _ConvBNActFn.apply(x, conv.weight, conv.bias, bn.weight, bn.bias, residual, spec,
+                              in_link, res_link)
 
 
 # ------------------------------------------------------------------ classifier head
