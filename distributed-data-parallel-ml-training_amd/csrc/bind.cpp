@@ -143,9 +143,9 @@ PYBIND11_MODULE(_native, m) {
     check(ddp_sgd(P<float>(p), P<float>(g), P<float>(buf), n, lr, momentum, wd, grad_scale,
                   nesterov, S(st)), "sgd");
   });
-  m.def("conv_options", [](int wgrad_atomic, int persistent) {
-    ddp_conv_options(wgrad_atomic, persistent);
-  }, py::arg("wgrad_atomic") = 0, py::arg("persistent") = 0);
+  m.def("conv_options", [](int wgrad_atomic, int persistent, int stages) {
+    ddp_conv_options(wgrad_atomic, persistent, stages);
+  }, py::arg("wgrad_atomic") = 0, py::arg("persistent") = 0, py::arg("stages") = 2);
   // descs: list of (p, wc, wt, K, Cr, C, R, S, krsc)
   m.def("pack_conv_weights", [](std::vector<std::tuple<uintptr_t, uintptr_t, uintptr_t, int, int,
                                                        int, int, int, int>> descs, uintptr_t st) {

@@ -165,7 +165,16 @@ __device__ __forceinline__ void dma_buf(__amdgpu_buffer_rsrc_t rs, int byte_off,
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lds_wave_base, 16, byte_off, 0, 0, 0);
 }
 
-template <int MODE, int BM, int BN>
+// LDS-DMA completion + workgroup barrier without the vmcnt(0) that __syncthreads implies:
+// waits until at most N of this wave's vector-memory ops are outstanding (the DMAs of the
+// stages issued after the one about to be read), then s_barrier. The "memory" clobber keeps the
+// compiler from moving LDS accesses across it.
+template <int N>
+__device__ __forceinline__ void wait_dma_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+template <int MODE, int BM, int BN, int NST>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
   constexpr int BK = 64;
   constexpr int WTM = BM / 2, WTN = BN / 2;
@@ -174,7 +183,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
   constexpr int CB = BN * BK / 8 / 256;
   constexpr int TILE_A = BM * BK, TILE_B = BN * BK;
   static_assert(CA >= 1 && CB >= 1, "tile too small for 256 threads");
-  __shared__ __attribute__((aligned(16))) unsigned short smem[2 * (TILE_A + TILE_B)];
+  static_assert(NST >= 2 && NST <= 4, "2..4 LDS stages");
+  __shared__ __attribute__((aligned(16))) unsigned short smem[NST * (TILE_A + TILE_B)];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -521,39 +531,32 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
   }
   };
 
-  int item = blockIdx.x;
-  if (item >= nitems) return;
-  setup(item);
-  issue(ks_begin, 0);
-  __syncthreads();  // waits for the DMA (vmcnt(0)) and publishes buffer 0
-  int buf = 0;
-  while (true) {
+  // NST-stage LDS ring: the DMAs of up to NST-1 k-steps are in flight while one is computed.
+  constexpr int DMA = CA + CB;  // vector-memory instructions per thread per stage
+  for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
+    setup(item);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const int e_row0 = row0, e_col0 = col0, e_z = zsplit;
     const int kb = ks_begin, ke = ks_end;  // host guarantees kb < ke for every item
-    const int next = item + gridDim.x;
-    const bool has_next = next < nitems;
+#pragma unroll
+    for (int s = 0; s < NST - 1; ++s)
+      if (kb + s < ke) issue(kb + s, s);
+    int stage = 0;
     for (int ks = kb; ks < ke; ++ks) {
-      if (ks + 1 < ke) {
-        issue(ks + 1, buf ^ 1);  // lands during this step's MFMAs
-      } else if (has_next) {
-        setup(next);             // buffer buf^1 is free: everyone passed the last barrier
-        issue(ks_begin, buf ^ 1);
-      }
-      compute(buf);
-      if (ks + 1 < ke) {
-        __syncthreads();  // next buffer landed + everyone done reading this one
-        buf ^= 1;
-      }
+      // stages issued after ks and still allowed in flight: min(NST-2, ke-1-ks)
+      const int ahead = ke - 1 - ks;
+      if (NST >= 4 && ahead >= 2) wait_dma_barrier<(NST >= 4 ? 2 : 0) * DMA>();
+      else if (NST >= 3 && ahead >= 1) wait_dma_barrier<(NST >= 3 ? 1 : 0) * DMA>();
+      else wait_dma_barrier<0>();
+      // every wave finished computing ks-1: its buffer takes k-step ks+NST-1
+      if (ks + NST - 1 < ke) issue(ks + NST - 1, stage == 0 ? NST - 1 : stage - 1);
+      compute(stage);
+      stage = stage + 1 == NST ? 0 : stage + 1;
     }
-    epilogue(e_row0, e_col0, e_z);
-    if (!has_next) break;
-    __syncthreads();  // next item's first k-step landed; this buffer fully consumed
-    buf ^= 1;
-    item = next;
+    epilogue(row0, col0, zsplit);
+    wait_dma_barrier<0>();  // all reads of the ring done before the next item's prologue DMA
   }
 }
 
@@ -730,6 +733,7 @@ static bool fits_buffer(size_t elems) { return elems * 2 < (size_t)kOOB; }
 
 static int g_wgrad_atomic = 0;  // WGRAD split-K through fp32 atomics instead of slabs
 static int g_persistent = 0;    // grid = resident slots, blocks loop over work items
+static int g_stages = 2;        // LDS ring depth policy (see stages_for)
 constexpr int kMaxAtomicSplits = 32;
 constexpr int kNumCUs = 256;
 
@@ -770,6 +774,29 @@ static double tile_cost(int BM, int BN, const ConvArgs& a, size_t ws_elems, int*
   return t_mfma + t_split;
 }
 
+// LDS ring depth per tile shape (DDP_AMD_CONV_STAGES selects the policy; 2 = double buffer).
+// Bytes per stage: (BM + BN) x 64 x 2 — 32 KB at 128x128, 24 KB at 128x64, 16 KB at 64x64.
+static int stages_for(int BM, int BN) {
+  if (g_stages <= 2) return 2;
+  if (BM == 128 && BN == 128) return g_stages >= 4 ? 4 : 2;  // 3 would not fit 2 blocks either
+  if (BM == 64 && BN == 64) return g_stages >= 4 ? 4 : 3;
+  return 3;
+}
+
+template <int MODE, int BM, int BN, int NST>
+static void launch_gemm(const ConvArgs& a, int items, hipStream_t st) {
+  // persistent grid: at most the resident workgroup slots (queried once per instantiation)
+  static int resident = 0;
+  if (resident == 0) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, conv_igemm_kernel<MODE, BM, BN, NST>, 256, 0) != hipSuccess || nb < 1)
+      nb = 1;
+    resident = nb;
+  }
+  const int grid = g_persistent ? std::min(items, kNumCUs * resident) : items;
+  hipLaunchKernelGGL((conv_igemm_kernel<MODE, BM, BN, NST>), dim3(grid), dim3(256), 0, st, a);
+}
+
 template <int MODE, int BM, int BN>
 static void launch_cfg(ConvArgs& a, int splits, hipStream_t st) {
   constexpr int BK = 64;
@@ -782,17 +809,11 @@ static void launch_cfg(ConvArgs& a, int splits, hipStream_t st) {
   // same-address fp32 atomics serialise: beyond kMaxAtomicSplits partial sums per element the
   // slab + grouped-finish reduction is cheaper
   if (a.wg_atomic && splits > kMaxAtomicSplits) a.wg_atomic = 0;
-  // persistent grid: at most the resident workgroup slots (queried once per instantiation)
-  static int resident = 0;
-  if (resident == 0) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, conv_igemm_kernel<MODE, BM, BN>, 256, 0) != hipSuccess || nb < 1)
-      nb = 1;
-    resident = nb;
-  }
   const int items = tiles * splits;
-  const int grid = g_persistent ? std::min(items, kNumCUs * resident) : items;
-  hipLaunchKernelGGL((conv_igemm_kernel<MODE, BM, BN>), dim3(grid), dim3(256), 0, st, a);
+  const int nst = stages_for(BM, BN);
+  if (nst == 4) launch_gemm<MODE, BM, BN, (BM == 128 && BN == 128) ? 4 : 4>(a, items, st);
+  else if (nst == 3) launch_gemm<MODE, BM, BN, 3>(a, items, st);
+  else launch_gemm<MODE, BM, BN, 2>(a, items, st);
   if (splits == 1) return;
   if (MODE == MODE_WGRAD && a.wg_atomic) return;
   if (MODE == MODE_WGRAD && a.g.wkrsc) {
@@ -838,9 +859,10 @@ static void launch_mode(ConvArgs& a, size_t ws_elems, hipStream_t st) {
   }
 }
 
-extern "C" void ddp_conv_options(int wgrad_atomic, int persistent) {
+extern "C" void ddp_conv_options(int wgrad_atomic, int persistent, int stages) {
   g_wgrad_atomic = wgrad_atomic;
   g_persistent = persistent;
+  g_stages = stages;
 }
 
 extern "C" int ddp_conv_fwd(const ConvGeom* g, const void* x, const void* wc, const float* bias,

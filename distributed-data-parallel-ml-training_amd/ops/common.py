@@ -6,6 +6,7 @@ import torch
 from .._ext import load as _load
 
 _NATIVE = None
+CONV_STAGES = 2  # default LDS ring depth policy (env DDP_AMD_CONV_STAGES overrides)
 
 
 def native():
@@ -17,8 +18,10 @@ def native():
         # default 0 = slab + grouped finish reduction
         # DDP_AMD_CONV_PERSISTENT=1: conv grids sized to the resident slots, blocks loop over
         # tiles and prefetch the next tile's first k-step (default 0: one tile per workgroup)
+        # DDP_AMD_CONV_STAGES: LDS ring depth policy of the conv GEMMs (2 = double buffering)
         _NATIVE.conv_options(int(os.environ.get("DDP_AMD_WGRAD_ATOMIC", "0")),
-                             int(os.environ.get("DDP_AMD_CONV_PERSISTENT", "0")))
+                             int(os.environ.get("DDP_AMD_CONV_PERSISTENT", "0")),
+                             int(os.environ.get("DDP_AMD_CONV_STAGES", str(CONV_STAGES))))
     return _NATIVE
 
 

@@ -77,12 +77,15 @@ def test_conv_dgrad(native_ext, case, layout):
     dzn = dz.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
     fmt = torch.contiguous_format if layout == "kcrs" else torch.channels_last
     dw = torch.zeros_like(conv.weight, memory_format=fmt)
-    native_ext.conv_options(int(layout == "krsc_atomic"), int(layout == "krsc_atomic"))
+    # the atomic variant also exercises the persistent grid and the deepest LDS ring
+    native_ext.conv_options(int(layout == "krsc_atomic"), int(layout == "krsc_atomic"),
+                            4 if layout == "krsc_atomic" else (3 if layout == "krsc" else 2))
     try:
         dx = conv_backward(spec, xn, dzn, dw, True)
         torch.cuda.synchronize()
     finally:
-        native_ext.conv_options(0, 0)
+        from ddp_amd.ops.common import CONV_STAGES
+        native_ext.conv_options(0, 0, CONV_STAGES)
     xr = x.clone().requires_grad_(True)
     wr = conv.weight.detach().clone().requires_grad_(True)
     out = F.conv2d(xr, wr, None, stride, pad)
