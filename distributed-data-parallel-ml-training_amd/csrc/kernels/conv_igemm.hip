@@ -9,13 +9,12 @@
 //   x  [N][H][W][C]      bf16  activations
 //   y  [N][P][Q][K]      bf16  conv output (pre-BN)
 //   Wc [K][R][S][C]      bf16  forward weight copy   (GEMM B operand, k-contiguous)
-//   Wt [C][R][S][K]      bf16  dgrad weight copy     (GEMM B operand, k-contiguous)
 //   dW [K][R][S][Creal]  fp32  weight gradient in the GPU arena layout (optim/arena.py), or
 //      [K][Creal][R][S]        the standard layout (ConvGeom::wkrsc selects), accumulated
 //
 // GEMM views (rows x cols, reduction):
 //   FWD   : M=N*P*Q, N=K,      red=R*S*C   A=im2col(x)          B=Wc
-//   DGRAD : M=N*H*W, N=C,      red=R*S*K   A=col2im-gather(dy)  B=Wt
+//   DGRAD : M=N*H*W, N=C,      red=R*S*K   A=col2im-gather(dy)  B=Wc read k-major
 //           (strided convs: one stride-1 GEMM per output phase, see ConvArgs::phase)
 //   WGRAD : M=K,     N=R*S*C,  red=N*P*Q   A=dy^T               B=im2col(x)^T
 //
@@ -227,7 +226,11 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
   const bool fast = MODE != MODE_WGRAD && (cdim % BK) == 0;
   const int lcA = (MODE != MODE_WGRAD) ? ((tid & 7) ^ ((tid >> 4) & 7))
                                        : ((tid % (BM / 8)) ^ mc_swz<BM>(tid / (BM / 8)));
-  const int lcB = (MODE != MODE_WGRAD) ? lcA : ((tid % (BN / 8)) ^ mc_swz<BN>(tid / (BN / 8)));
+  // B operand: FWD reads Wc [K][RSC] k-contiguous into a [col][k] tile; DGRAD and WGRAD fill a
+  // k-major [k][col] tile (DGRAD straight from Wc: 8 consecutive input channels of one output
+  // channel and tap per chunk — no transposed weight copy) read with ds_read_b64_tr_b16
+  constexpr bool BKM = MODE != MODE_FWD;
+  const int lcB = !BKM ? lcA : ((tid % (BN / 8)) ^ mc_swz<BN>(tid / (BN / 8)));
   const __amdgpu_buffer_rsrc_t rsA = make_rsrc(args.a, args.a_bytes);
   const __amdgpu_buffer_rsrc_t rsB = make_rsrc(args.b, args.b_bytes);
 
@@ -249,11 +252,18 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
                                          : ri.base + (ri.h0 * gg.Q + ri.w0) * gg.K;
         a_off[i] = 2 * (e + (fast ? lcA * 8 : 0));
       }
-      const int bstride = phase ? gg.R * gg.S * gg.K : args.Kg;
+      if (MODE == MODE_FWD) {
 #pragma unroll
-      for (int i = 0; i < CB; ++i) {
-        const int col = col0 + (tid >> 3) + 32 * i;
-        b_off[i] = col < args.Ng ? 2 * (col * bstride + lcB * 8) : (int)kOOB;
+        for (int i = 0; i < CB; ++i) {
+          const int col = col0 + (tid >> 3) + 32 * i;
+          b_off[i] = col < args.Ng ? 2 * (col * args.Kg + lcB * 8) : (int)kOOB;
+        }
+      } else {  // DGRAD: row m of the k-step = output channel kc + m, columns = input channels
+        const int col = col0 + lcB * 8;
+#pragma unroll
+        for (int i = 0; i < CB; ++i)
+          b_off[i] = col < args.Ng ? 2 * (((tid + i * 256) / (BN / 8)) * gg.R * gg.S * gg.C + col)
+                                   : (int)kOOB;
       }
       // decomposition of the first reduction index (fast: of the k-step; slow: of the chunk)
       const int kk = ks_begin * BK + (fast ? 0 : lcA * 8);
@@ -297,8 +307,13 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
             ok = (unsigned)(a_h0[i] - kr) < (unsigned)gg.P && (unsigned)(a_w0[i] - ks_) < (unsigned)gg.Q;
           dma_buf(rsA, ok ? a_off[i] + tap : (int)kOOB, As + (wid * 64 + 256 * i) * 8);
         }
-        const int boff = 2 * (phase ? ((args.r0 + gg.stride * kr) * gg.S + args.s0 + gg.stride * ks_) * gg.K + kc
-                                    : k0);
+        int boff;
+        if (MODE == MODE_FWD) {
+          boff = 2 * k0;
+        } else {  // Wc[kc + m][r][s][c]
+          const int rr = phase ? args.r0 + gg.stride * kr : kr, ss = phase ? args.s0 + gg.stride * ks_ : ks_;
+          boff = 2 * ((kc * gg.R * gg.S + rr * gg.S + ss) * gg.C);
+        }
 #pragma unroll
         for (int i = 0; i < CB; ++i) dma_buf(rsB, b_off[i] + boff, Bs + (wid * 64 + 256 * i) * 8);
         kc += BK;
@@ -319,12 +334,25 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
             ok = (unsigned)(a_h0[i] - kr) < (unsigned)gg.P && (unsigned)(a_w0[i] - ks_) < (unsigned)gg.Q;
           dma_buf(rsA, (kok && ok) ? a_off[i] + tap : (int)kOOB, As + (wid * 64 + 256 * i) * 8);
         }
-        // (kc already includes this thread's lcA*8, which b_off carries too)
-        const int boff = 2 * (phase ? ((args.r0 + gg.stride * kr) * gg.S + args.s0 + gg.stride * ks_) * gg.K + kc - lcA * 8
-                                    : k0);
+        if (MODE == MODE_FWD) {
 #pragma unroll
-        for (int i = 0; i < CB; ++i)
-          dma_buf(rsB, kok ? b_off[i] + boff : (int)kOOB, Bs + (wid * 64 + 256 * i) * 8);
+          for (int i = 0; i < CB; ++i)
+            dma_buf(rsB, kok ? b_off[i] + 2 * k0 : (int)kOOB, Bs + (wid * 64 + 256 * i) * 8);
+        } else {
+          // DGRAD, K % 64 != 0: the k-step spans taps; decode every row's reduction index
+          const int RSC = gg.R * gg.S * gg.C;
+#pragma unroll
+          for (int i = 0; i < CB; ++i) {
+            const int m = (tid + i * 256) / (BN / 8);
+            const int kkr = k0 + m;
+            const int tap = kkr / gg.K, kout = kkr - tap * gg.K;
+            const int tr = tap / Sdec, ts = tap - tr * Sdec;
+            const int rr = phase ? args.r0 + gg.stride * tr : tr, ss = phase ? args.s0 + gg.stride * ts : ts;
+            const int off = b_off[i] - 2 * m * RSC + 2 * ((kout * gg.R * gg.S + rr * gg.S + ss) * gg.C);
+            dma_buf(rsB, (kkr < args.Kg && b_off[i] != (int)kOOB) ? off : (int)kOOB,
+                    Bs + (wid * 64 + 256 * i) * 8);
+          }
+        }
         kc += BK;
         while (kc >= cdim) {
           kc -= cdim;
@@ -370,18 +398,17 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
 
   // fragment LDS offsets (elements), loop-invariant
   int fa_off[TM], fb_off[TN];
-  if (MODE != MODE_WGRAD) {
-#pragma unroll
-    for (int i = 0; i < TM; ++i) fa_off[i] = rk_off(wm * WTM + i * 16 + (lane & 15), lane >> 4);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) fb_off[j] = rk_off(wn * WTN + j * 16 + (lane & 15), lane >> 4);
-  } else {
+  {
     const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
     const int m0 = 8 * g + q;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) fa_off[i] = mc_off<BM>(m0, wm * WTM + i * 16 + 4 * p);
+    for (int i = 0; i < TM; ++i)
+      fa_off[i] = MODE != MODE_WGRAD ? rk_off(wm * WTM + i * 16 + (lane & 15), lane >> 4)
+                                     : mc_off<BM>(m0, wm * WTM + i * 16 + 4 * p);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) fb_off[j] = mc_off<BN>(m0, wn * WTN + j * 16 + 4 * p);
+    for (int j = 0; j < TN; ++j)
+      fb_off[j] = !BKM ? rk_off(wn * WTN + j * 16 + (lane & 15), lane >> 4)
+                       : mc_off<BN>(m0, wn * WTN + j * 16 + 4 * p);
   }
 
   auto compute = [&](int buf) {
@@ -390,18 +417,15 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 32) {
       bf16x8 fa[TM], fb[TN];
+      // [row][k] tiles: logical chunk kk/8 + (lane>>4); the XOR swizzle is linear in the chunk
+      // index, so the kk = 32 read is the kk = 0 address with chunk bit 2 flipped.
+      // [k][col] tiles: ds_read_b64_tr_b16 — lane 4q+p of each 16-lane group supplies row q,
+      // columns 4p..4p+3; lane i receives column i of the 4 rows; two reads = 8 k-values.
       if (MODE != MODE_WGRAD) {
-        // logical chunk kk/8 + (lane>>4): the XOR swizzle is linear in the chunk index, so the
-        // kk = 32 read is the kk = 0 address with chunk bit 2 flipped
 #pragma unroll
         for (int i = 0; i < TM; ++i)
           fa[i] = *reinterpret_cast<const bf16x8*>(As + (fa_off[i] ^ (kk ? 32 : 0)));
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          fb[j] = *reinterpret_cast<const bf16x8*>(Bs + (fb_off[j] ^ (kk ? 32 : 0)));
       } else {
-        // ds_read_b64_tr_b16: lane 4q+p of each 16-lane group supplies row q, columns 4p..4p+3;
-        // lane i receives column i of the 4 rows. Two reads give the 8 k-values of a fragment.
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const unsigned short* base = As + fa_off[i] + kk * BM;
@@ -410,6 +434,12 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
           const short8_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
           fa[i] = __builtin_bit_cast(bf16x8, v);
         }
+      }
+      if (!BKM) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          fb[j] = *reinterpret_cast<const bf16x8*>(Bs + (fb_off[j] ^ (kk ? 32 : 0)));
+      } else {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const unsigned short* base = Bs + fb_off[j] + kk * BN;
@@ -889,7 +919,7 @@ extern "C" int ddp_conv_fwd(const ConvGeom* g, const void* x, const void* wc, co
   return (int)hipGetLastError();
 }
 
-extern "C" int ddp_conv_dgrad(const ConvGeom* g, const void* dy, const void* wt, void* dx,
+extern "C" int ddp_conv_dgrad(const ConvGeom* g, const void* dy, const void* wc, void* dx,
                               float* ws, size_t ws_elems, int splits, int accumulate,
                               hipStream_t st) {
   if (g->C % 8 || g->K % 8) return -1;
@@ -897,12 +927,13 @@ extern "C" int ddp_conv_dgrad(const ConvGeom* g, const void* dy, const void* wt,
   a.accumulate = accumulate;
   a.g = *g;
   a.a = (const unsigned short*)dy;
-  a.b = (const unsigned short*)wt;
+  a.b = (const unsigned short*)wc;
   a.out = (unsigned short*)dx;
   a.ws = ws;
   a.Ng = g->C;
   a.splits = splits;
-  const size_t dya = (size_t)g->N * g->P * g->Q * g->K, wb = (size_t)g->C * g->R * g->S * g->K;
+  // B = the forward weight copy Wc [K][R][S][C] (read k-major, see BKM in the kernel)
+  const size_t dya = (size_t)g->N * g->P * g->Q * g->K, wb = (size_t)g->K * g->R * g->S * g->C;
   if (!fits_buffer(dya) || !fits_buffer(wb)) return -2;
   a.a_bytes = (int)(2 * dya);
   a.b_bytes = (int)(2 * wb);

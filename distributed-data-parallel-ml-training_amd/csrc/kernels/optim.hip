@@ -96,8 +96,11 @@ __global__ __launch_bounds__(256) void pack_conv_weights_kernel(PackTable t) {
 // Fused SGD + weight re-pack: ONE launch updates the whole arena and writes the bf16 MFMA
 // operand copies of every conv weight from the freshly updated values (no second pass over the
 // fp32 weights). Work items (int4): {0, offset, count, -} = plain elementwise chunk;
-// {1, desc, k0, c0} = one TK x TC x (R*S) tile of a conv weight, staged through LDS so that
-// both the Wc ([k][r][s][c], c fastest) and Wt ([c][r][s][k], k fastest) writes are coalesced.
+// {2, rel_offset, count, desc} = elementwise chunk of a conv weight stored [K][R][S][C] (the GPU
+// arena layout): its bf16 copy Wc has the same index order, so it is written in the same pass;
+// {1, desc, k0, c0} = one TK x TC x (R*S) tile of a conv weight that needs a layout change
+// (channel-padded input layer, or a [K][C][R][S] master), staged through LDS so that the Wc
+// ([k][r][s][c], c fastest) and optional Wt ([c][r][s][k], k fastest) writes are coalesced.
 // Conv descriptor (int64 x 12): {p_offset, K, Cr, C, R, S, wc_ptr, wt_ptr, krsc, -, -, -};
 // krsc selects the fp32 master layout ([K][R][S][Cr] vs [K][Cr][R][S]).
 constexpr int kTileElems = 9216;  // fp32 LDS tile (36 KB)
@@ -157,6 +160,31 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(const int4* __restrict__ 
           if (h.zero_grad) g[off + e] = 0.f;
         }
       }
+    }
+    return;
+  }
+  if (it.x == 2) {
+    // conv weight whose bf16 operand copy has the master's own index order ([K][R][S][C] with
+    // C == Cr, or 1x1): elementwise update + bf16 store, no LDS staging
+    const long long* d = descs + 12 * it.w;
+    const size_t base = (size_t)d[0] + (unsigned)it.y;
+    unsigned short* wc = reinterpret_cast<unsigned short*>(d[6]) + (unsigned)it.y;
+    const int cnt = it.z;  // multiple of 4, base 4-aligned (arena tensors are 64-aligned)
+    for (int i = tid * 4; i < cnt; i += 256 * 4) {
+      float4 pv = *reinterpret_cast<float4*>(p + base + i);
+      const float4 gv = *reinterpret_cast<const float4*>(g + base + i);
+      float4 bv = *reinterpret_cast<float4*>(buf + base + i);
+      pv.x = sgd1(pv.x, gv.x, bv.x, h);
+      pv.y = sgd1(pv.y, gv.y, bv.y, h);
+      pv.z = sgd1(pv.z, gv.z, bv.z, h);
+      pv.w = sgd1(pv.w, gv.w, bv.w, h);
+      *reinterpret_cast<float4*>(p + base + i) = pv;
+      *reinterpret_cast<float4*>(buf + base + i) = bv;
+      if (h.zero_grad) *reinterpret_cast<float4*>(g + base + i) = make_float4(0.f, 0.f, 0.f, 0.f);
+      uint2 pk;
+      pk.x = (unsigned)f2bf(pv.x) | ((unsigned)f2bf(pv.y) << 16);
+      pk.y = (unsigned)f2bf(pv.z) | ((unsigned)f2bf(pv.w) << 16);
+      *reinterpret_cast<uint2*>(wc + i) = pk;
     }
     return;
   }

@@ -43,7 +43,8 @@ class ConvBNActSpec:
         self.eps = float(bn.eps) if bn is not None else 1e-5
         dev = conv.weight.device
         self.wc = torch.empty(K, R, S, self.C, dtype=BF16, device=dev)
-        self.wt = torch.empty(self.C, R, S, K, dtype=BF16, device=dev) if self.C == Cr else None
+        # (no transposed copy: the dgrad GEMM reads Wc k-major through transposing LDS reads)
+        self.wt = None
         self._packed_version = None
         conv.weight._ddp_amd_pack = self.pack_desc  # the fused optimizer repacks after its step
         # per-step zeroed accumulators (StepScratch): BN statistics replicas + BN-backward sums
@@ -131,16 +132,16 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None):
     native().conv_wgrad(g, ptr(dz), ptr(x), ptr(dweight), ptr(ws), ws.numel(), 0, s)
     if not need_dx:
         return None
-    if spec.wt is None:
+    if spec.C != spec.Cr:
         raise RuntimeError("dgrad requested for a channel-padded input layer")
     if link is not None and link.buf is not None:
         # second branch: accumulate into the first branch's gradient from the GEMM epilogue
-        native().conv_dgrad(g, ptr(dz), ptr(spec.wt), ptr(link.buf), ptr(ws), ws.numel(), 0, s,
+        native().conv_dgrad(g, ptr(dz), ptr(spec.wc), ptr(link.buf), ptr(ws), ws.numel(), 0, s,
                             accumulate=1)
         link.seen += 1
         return link.result()
     dx = torch.empty_like(x)
-    native().conv_dgrad(g, ptr(dz), ptr(spec.wt), ptr(dx), ptr(ws), ws.numel(), 0, s)
+    native().conv_dgrad(g, ptr(dz), ptr(spec.wc), ptr(dx), ptr(ws), ws.numel(), 0, s)
     if link is not None:
         link.seen += 1
         link.buf = dx
@@ -402,7 +403,7 @@ class LinearGemmSpec(ConvBNActSpec):
         self.eps = 1e-5
         dev = linear.weight.device
         self.wc = torch.empty(J, F, dtype=BF16, device=dev)
-        self.wt = torch.empty(F, J, dtype=BF16, device=dev)
+        self.wt = None
         self._packed_version = None
         linear.weight._ddp_amd_pack = self.pack_desc
         self.stats = None

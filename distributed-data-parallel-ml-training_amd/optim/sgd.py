@@ -48,11 +48,17 @@ class FusedSGD(torch.optim.SGD):
                 raise RuntimeError("packed conv weight is not a view into the parameter arena")
             d = len(descs)
             descs.append([a.offsets[i], K, Cr, C, R, S, wc, wt, int(krsc), 0, 0, 0])
+            conv.add(i)
+            n = a.numels[i]
+            if not wt and C == Cr and (krsc or R * S == 1) and n % 4 == 0:
+                # bf16 copy in the master's own index order: elementwise items
+                for s0 in range(0, n, 8192):
+                    items.append([2, s0, min(8192, n - s0), d])
+                continue
             TK, TC = native().sgd_tile_dims(R * S)
             for k0 in range(0, K, TK):
                 for c0 in range(0, C, TC):
                     items.append([1, d, k0, c0])
-            conv.add(i)
         chunk = 8192
         for i in range(len(a.params)):
             if i in conv:

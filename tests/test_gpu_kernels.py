@@ -244,7 +244,8 @@ def test_pack_weights(native_ext):
     conv2 = torch.nn.Conv2d(64, 128, 3, padding=1).to(DEV)
     s2 = ConvBNActSpec(conv2, None)
     s2.maybe_pack()
-    assert torch.equal(s2.wt.float(), conv2.weight.detach().permute(1, 2, 3, 0).to(torch.bfloat16).float())
+    assert s2.wt is None  # dgrad reads Wc k-major: no transposed copy
+    assert torch.equal(s2.wc.float(), conv2.weight.detach().permute(0, 2, 3, 1).to(torch.bfloat16).float())
     # [K][R][S][C] fp32 master (GPU arena layout)
     conv3 = torch.nn.Conv2d(3, 64, 3, padding=1).to(DEV)
     conv3.weight.data = conv3.weight.data.contiguous(memory_format=torch.channels_last)
