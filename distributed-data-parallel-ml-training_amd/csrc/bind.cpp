@@ -51,6 +51,15 @@ PYBIND11_MODULE(_native, m) {
     check(ddp_conv_fwd(&c, P<void>(x), P<void>(wc), P<float>(bias), P<void>(y), P<float>(stats),
                        P<float>(ws), ws_elems, splits, S(st)), "conv_fwd");
   });
+  // direct MFMA conv for C = 8 input layers; returns False when the shape is not served
+  m.def("conv_fwd_smallk", [](py::tuple g, uintptr_t x, uintptr_t wc, uintptr_t bias, uintptr_t y,
+                              uintptr_t stats, uintptr_t st) {
+    auto c = geom(g);
+    const int rc = ddp_conv_fwd_smallk(&c, P<void>(x), P<void>(wc), P<float>(bias), P<void>(y),
+                                       P<float>(stats), S(st));
+    if (rc > 0) check(rc, "conv_fwd_smallk");
+    return rc == 0;
+  });
   m.def("conv_dgrad", [](py::tuple g, uintptr_t dy, uintptr_t wt, uintptr_t dx, uintptr_t ws,
                          size_t ws_elems, int splits, uintptr_t st, int accumulate) {
     auto c = geom(g);

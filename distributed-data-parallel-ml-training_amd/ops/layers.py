@@ -89,6 +89,9 @@ def conv_forward(spec, x, bias=None, stats=None):
     g = spec.geom(N, H, W)
     P, Q = g[9], g[10]
     z = torch.empty(N, P, Q, spec.K, dtype=BF16, device=x.device)
+    if spec.C == 8 and native().conv_fwd_smallk(g, ptr(x), ptr(spec.wc), ptr(bias), ptr(z),
+                                                ptr(stats), stream_handle()):
+        return z  # input layer (3 channels padded to 8): direct MFMA kernel, conv_smallk.hip
     ws = workspace(x.device)
     native().conv_fwd(g, ptr(x), ptr(spec.wc), ptr(bias), ptr(z), ptr(stats), ptr(ws), ws.numel(),
                       0, stream_handle())
