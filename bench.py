@@ -37,7 +37,8 @@ def parse():
     p.add_argument("--global-batch", type=int, default=None, help="strong scaling")
     p.add_argument("--per-gpu-batch", type=int, default=None,
                    help="weak scaling (default 256 for VGG, 64 for ResNet-50)")
-    p.add_argument("--strategy", default="ddp", choices=["ddp", "allreduce", "gather_scatter"])
+    p.add_argument("--strategy", default="ddp",
+                   choices=["ddp", "allreduce", "gather_scatter", "gather_broadcast"])
     # buckets sized for xGMI: ~8 MB fp32 buckets give every link a >= 512 KiB
     # ring chunk at 8 GPUs and let the 512x512 conv gradients (ready first in backward) start
     # all-reducing while the rest of the backward runs; the reference DDP default is 25 MB
@@ -158,7 +159,8 @@ def main():
         "config": {"model": args.model, "global_batch": global_batch, "per_gpu_batch": B,
                    "seq_len": None, "parallelism": f"dp{world}",
                    "strategy": {"ddp": "part3 bucketed DDP", "allreduce": "part2b all_reduce",
-                                "gather_scatter": "part2a gather/scatter"}[args.strategy],
+                                "gather_scatter": "part2a gather/scatter",
+                                "gather_broadcast": "part2a gather/broadcast"}[args.strategy],
                    "hipgraph": graph_ok, "bucket_mb": args.bucket_mb,
                    "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4) fused"},
         "train_loss_mean": round(loss, 4),

@@ -74,14 +74,25 @@ def test_model(model, test_loader, criterion, device="cpu", log=print):
     test_loss = 0
     correct = 0
     nb = 0
+    inner = getattr(model, "module", model)
+    fused = (torch.device(device).type == "cuda" and hasattr(inner, "forward_metrics")
+             and type(criterion) is CrossEntropyLoss)
+    if fused:  # loss + argmax hits accumulated on the device by the classifier kernel
+        loss_acc = torch.zeros((), dtype=torch.float32, device=device)
+        hits = torch.zeros((), dtype=torch.int32, device=device)
     with torch.no_grad():
         for data, target in test_loader:
             data, target = data.to(device), target.to(device)
-            output = model(data)
-            test_loss += criterion(output, target)
-            pred = output.max(1, keepdim=True)[1]
-            correct += pred.eq(target.view_as(pred)).sum().item()
+            if fused:
+                inner.forward_metrics(data, target, loss_acc, hits)
+            else:
+                output = model(data)
+                test_loss += criterion(output, target)
+                pred = output.max(1, keepdim=True)[1]
+                correct += pred.eq(target.view_as(pred)).sum().item()
             nb += 1
+    if fused:
+        test_loss, correct = float(loss_acc), int(hits)
     n = len(test_loader.dataset)
     test_loss = float(test_loss) / max(nb, 1)
     log('Test set: Average loss: {:.4f}, Accuracy: {}/{} ({:.0f}%)\n'.format(

@@ -99,6 +99,19 @@ class _VGG(nn.Module):
         from ..ops.layers import linear_small
         return linear_small(self._features_fused(x), self.fc1)
 
+    @torch.no_grad()
+    def forward_metrics(self, x, labels, loss_acc, correct_acc):
+        """Evaluation in one classifier kernel (GPU): loss_acc (fp32 scalar) += mean CE of the
+        batch, correct_acc (int32 scalar) += number of argmax hits (reference test_model,
+        part1/main.py:96-111). No logits tensor, no host sync per batch."""
+        from ..ops.common import native, ptr, stream_handle
+        h = self._features_fused(x)
+        B, F = h.shape
+        labels = labels.to(torch.int64).contiguous()
+        native().linear_ce_fwd(ptr(h), ptr(self.fc1.weight), ptr(self.fc1.bias), ptr(labels), B, F,
+                               self.fc1.weight.shape[0], 0, 0, ptr(loss_acc), ptr(correct_acc),
+                               stream_handle())
+
     def forward_loss(self, x, labels, acc=None, transient=False):
         """``CrossEntropyLoss()(self(x), labels)`` with the classifier and the loss fused into one
         kernel on the GPU (engine/step.py uses it for the captured training step). ``acc`` (fp32

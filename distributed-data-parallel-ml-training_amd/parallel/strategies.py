@@ -46,6 +46,32 @@ def sync_gradients_gather_scatter(model, comm, root=0):
         comm.scatter_replicated(g, src=root)
 
 
+def sync_gradients_gather_broadcast(model, comm, root=0):
+    """2A variant (BASELINE.json's "manual gather + broadcast"): rank-0 gather and mean as in
+    ``sync_gradients_gather_scatter``, then ONE broadcast of the mean per parameter (RCCL runs
+    it as a pipelined ring/tree over xGMI instead of world-1 point-to-point sends from rank 0)."""
+    params = _params_with_grad(model)
+    if comm.kind == "torch":
+        for p in params:
+            lst = comm.gather(p.grad, dst=root)
+            if comm.rank == root:
+                p.grad.copy_(torch.mean(torch.stack(lst), dim=0))
+            comm.broadcast(p.grad, src=root)
+        return
+    from ..ops.common import native, stream_handle
+    maxn = max(p.grad.numel() for p in params)
+    staging = _staging(params[0].grad.device, comm.world, maxn) if comm.rank == root else None
+    s = stream_handle()
+    for p in params:
+        g = p.grad
+        n = g.numel()
+        buf = staging[:comm.world * n].view(comm.world, n) if staging is not None else None
+        comm.gather_into(g, buf, dst=root)
+        if comm.rank == root:
+            native().mean_ws(buf.data_ptr(), n, comm.world, g.data_ptr(), s)
+        comm.broadcast(g, src=root)
+
+
 _STAGING = {}
 
 
@@ -76,6 +102,7 @@ def sync_gradients_allreduce(model, comm):
 
 
 STRATEGIES = {
-    "gather_scatter": sync_gradients_gather_scatter,  # part 2A
+    "gather_scatter": sync_gradients_gather_scatter,  # part 2A (reference: scatter)
+    "gather_broadcast": sync_gradients_gather_broadcast,  # part 2A variant (gather + broadcast)
     "allreduce": sync_gradients_allreduce,            # part 2B
 }

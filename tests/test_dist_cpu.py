@@ -1,6 +1,6 @@
 """Sync-strategy equivalence on CPU with Gloo, world size 2.
 
-2A (gather/mean/scatter) == 2B (all-reduce/ws) == 3 (bucketed DDP) == the average of the
+2A (gather/mean/scatter, and the gather/mean/broadcast variant) == 2B (all-reduce/ws) == 3 (bucketed DDP) == the average of the
 per-rank gradients, and every strategy leaves the replicas bit-identical.
 """
 import pytest
@@ -16,7 +16,7 @@ B = 4
 @pytest.fixture(scope="module")
 def results():
     out = {}
-    for strat in ["gather_scatter", "allreduce", "ddp"]:
+    for strat in ["gather_scatter", "gather_broadcast", "allreduce", "ddp"]:
         out[strat] = run_workers(train_worker, WORLD, strat, STEPS, B, 4.0)
         for r, v in out[strat].items():
             assert "error" not in v, v.get("error")
@@ -25,7 +25,7 @@ def results():
 
 
 def test_replicas_identical_every_strategy(results):
-    for strat in ["gather_scatter", "allreduce", "ddp"]:
+    for strat in ["gather_scatter", "gather_broadcast", "allreduce", "ddp"]:
         r = results[strat]
         assert torch.equal(r[0]["params"], r[1]["params"]), strat
         assert torch.equal(r[0]["grads0"], r[1]["grads0"]), strat
@@ -34,14 +34,14 @@ def test_replicas_identical_every_strategy(results):
 def test_synced_grad_is_mean_of_local_grads(results):
     loc = results["local"]
     expected = (loc[0]["grads0"] + loc[1]["grads0"]) / WORLD
-    for strat in ["gather_scatter", "allreduce", "ddp"]:
+    for strat in ["gather_scatter", "gather_broadcast", "allreduce", "ddp"]:
         g = results[strat][0]["grads0"]
         assert torch.allclose(g, expected, rtol=1e-5, atol=1e-7), strat
 
 
 def test_strategies_agree(results):
     a = results["gather_scatter"][0]["params"]
-    for strat in ["allreduce", "ddp"]:
+    for strat in ["gather_broadcast", "allreduce", "ddp"]:
         assert torch.allclose(results[strat][0]["params"], a, rtol=1e-5, atol=1e-6), strat
 
 

@@ -185,3 +185,23 @@ def test_fused_forward_loss_matches_unfused(native_ext):
             continue
         ga, gb = pa.grad.reshape(-1), pb.grad.reshape(-1)
         assert float(torch.dot(ga, gb) / (ga.norm() * gb.norm())) > 0.98, n
+
+
+def test_fused_eval_metrics_match(native_ext):
+    """VGG.forward_metrics (one classifier kernel, device accumulators) == logits path."""
+    from ddp_amd.models import VGG11
+    from ddp_amd.engine import CrossEntropyLoss
+    torch.manual_seed(0)
+    m = VGG11().cuda().eval()
+    x = torch.randn(64, 3, 32, 32, device="cuda")
+    y = torch.randint(0, 10, (64,), device="cuda")
+    la = torch.zeros((), device="cuda")
+    hits = torch.zeros((), dtype=torch.int32, device="cuda")
+    m.forward_metrics(x, y, la, hits)
+    with torch.no_grad():
+        out = m(x)
+        lb = CrossEntropyLoss()(out, y)
+        cb = int((out.argmax(1) == y).sum())
+    torch.cuda.synchronize()
+    assert abs(float(la) - float(lb)) < 5e-3 * max(1.0, abs(float(lb)))
+    assert abs(int(hits) - cb) <= 1  # a near-tie may round differently
