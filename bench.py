@@ -7,7 +7,8 @@
 
 Config = BASELINE.json: VGG-11 (reference architecture, random init), synthetic CIFAR-10-shaped
 data (3x32x32, 10 classes, on-device crop/flip/normalise), bf16 compute with fp32 master
-weights/grads, SGD(0.1, 0.9, 1e-4), part-3 strategy (bucketed backward-overlapped DDP on RCCL).
+weights/grads, SGD(0.1, 0.9, 1e-4), part-3 strategy (bucketed DDP on RCCL, collectives issued in
+stream order inside the captured step).
 Default protocol: each GPU trains on the reference's batch of 256 images per step (weak scaling:
 per-GPU work is fixed as N grows; at N=1 this is exactly the reference's global batch 256).
 ``--global-batch B`` instead splits a fixed global batch int(B/N) per GPU (strong scaling, the
@@ -39,11 +40,14 @@ def parse():
                    help="weak scaling (default 256 for VGG, 64 for ResNet-50)")
     p.add_argument("--strategy", default="ddp",
                    choices=["ddp", "allreduce", "gather_scatter", "gather_broadcast"])
-    # buckets sized for xGMI: ~8 MB fp32 buckets give every link a >= 512 KiB
-    # ring chunk at 8 GPUs and let the 512x512 conv gradients (ready first in backward) start
-    # all-reducing while the rest of the backward runs; the reference DDP default is 25 MB
-    p.add_argument("--bucket-mb", type=float, default=8.0)
-    p.add_argument("--first-bucket-mb", type=float, default=1.0)
+    # Bucket sizing for xGMI. The collectives run inline on the step's single
+    # stream (parallel/ddp.py: a separate comm stream measured 2.3x slower on ROCm 7), so there
+    # is no backward overlap to buy with small buckets; what remains is per-collective latency
+    # and ring efficiency, both best with ONE bucket: VGG-11's 36.9 MB fp32 gradient arena in a
+    # single ncclAllReduce gives each of the 7 links multi-MiB chunks. The reference DDP default
+    # is 25 MB (+1 MB first bucket); pass --bucket-mb 25 --first-bucket-mb 1 for that plan.
+    p.add_argument("--bucket-mb", type=float, default=256.0)
+    p.add_argument("--first-bucket-mb", type=float, default=256.0)
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--train-size", type=int, default=None)
     p.add_argument("--json-out", default=None)
@@ -162,6 +166,8 @@ def main():
                                 "gather_scatter": "part2a gather/scatter",
                                 "gather_broadcast": "part2a gather/broadcast"}[args.strategy],
                    "hipgraph": graph_ok, "bucket_mb": args.bucket_mb,
+                   "comm": ("overlap-stream" if getattr(getattr(model, "reducer", None), "overlap",
+                                                         lambda: False)() else "inline"),
                    "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4) fused"},
         "train_loss_mean": round(loss, 4),
         "warmup_loss_sum": round(warm_loss, 4),

@@ -278,6 +278,9 @@ PYBIND11_MODULE(_native, m) {
       .def("mark_ready", [](Reducer& r, int p, uintptr_t st) { r.mark_ready(p, S(st)); })
       .def("finalize", [](Reducer& r, uintptr_t st) { r.finalize(S(st)); })
       .def("set_debug_sync", &Reducer::set_debug_sync)
+      .def("set_overlap", &Reducer::set_overlap)
+      .def("overlap", &Reducer::overlap)
+      .def("set_emulate", &Reducer::set_emulate)
       .def("launched", &Reducer::launched)
       .def("comm_stream", [](Reducer& r) { return reinterpret_cast<uintptr_t>(r.comm_stream()); });
 }

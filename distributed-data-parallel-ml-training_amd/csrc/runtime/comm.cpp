@@ -1,6 +1,9 @@
 // Native communication runtime — see comm.h.
 #include "comm.h"
+#include "../kernels/api.h"
 
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -217,20 +220,25 @@ Reducer::Reducer(RcclComm* comm, float* arena, std::vector<size_t> offsets,
     for (int p = buckets_[b].first_param; p < buckets_[b].last_param; ++p) bucket_of_param_[p] = (int)b;
   pending_.assign(buckets_.size(), 0);
   ready_.assign(buckets_.size(), 0);
-  ready_ev_.resize(buckets_.size());
+  contrib_.assign(buckets_.size(), {});
+  ready_ev_.assign(buckets_.size(), {});
   done_ev_.resize(buckets_.size());
-  for (size_t b = 0; b < buckets_.size(); ++b) {
-    HIP_OK(hipEventCreateWithFlags(&ready_ev_[b], hipEventDisableTiming));
+  done_stream_.assign(buckets_.size(), nullptr);
+  for (size_t b = 0; b < buckets_.size(); ++b)
     HIP_OK(hipEventCreateWithFlags(&done_ev_[b], hipEventDisableTiming));
-  }
+  // DDP_AMD_COMM_PRIORITY=high: comm stream at the highest stream priority (default: normal)
   int lo = 0, hi = 0;
   HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-  HIP_OK(hipStreamCreateWithPriority(&comm_stream_, hipStreamNonBlocking, hi));
+  const char* pe = std::getenv("DDP_AMD_COMM_PRIORITY");
+  const bool high = pe && std::string(pe) == "high";
+  HIP_OK(hipStreamCreateWithPriority(&comm_stream_, hipStreamNonBlocking, high ? hi : lo));
   prepare();
 }
 
 Reducer::~Reducer() {
-  for (auto e : ready_ev_) hipEventDestroy(e);
+  for (auto& v : ready_ev_)
+    for (auto e : v)
+      if (e) hipEventDestroy(e);
   for (auto e : done_ev_) hipEventDestroy(e);
   if (comm_stream_) hipStreamDestroy(comm_stream_);
 }
@@ -239,6 +247,7 @@ void Reducer::prepare() {
   for (size_t b = 0; b < buckets_.size(); ++b) {
     pending_[b] = buckets_[b].last_param - buckets_[b].first_param;
     ready_[b] = 0;
+    contrib_[b].clear();
   }
   next_launch_ = 0;
 }
@@ -247,22 +256,46 @@ void Reducer::mark_ready(int p, hipStream_t compute) {
   if (p < 0 || p >= (int)bucket_of_param_.size()) throw std::runtime_error("bad param index");
   const int b = bucket_of_param_[p];
   if (pending_[b] <= 0) throw std::runtime_error("parameter marked ready twice in one backward");
+  auto& cs = contrib_[b];
+  if (std::find(cs.begin(), cs.end(), compute) == cs.end()) cs.push_back(compute);
   if (--pending_[b] == 0) {
     ready_[b] = 1;
-    launch_ready(compute);
+    launch_ready();
   }
 }
 
 // Launch buckets strictly in plan order so every rank issues collectives identically.
-void Reducer::launch_ready(hipStream_t compute) {
+// The comm stream waits on an event recorded NOW on every stream that produced part of the
+// bucket: that covers each producer's work up to its last contribution.
+void Reducer::launch_ready() {
   while (next_launch_ < (int)buckets_.size() && ready_[next_launch_]) {
     const int b = next_launch_++;
     const BucketSpec& bs = buckets_[b];
-    HIP_OK(hipEventRecord(ready_ev_[b], compute));
-    HIP_OK(hipStreamWaitEvent(comm_stream_, ready_ev_[b], 0));
-    comm_->all_reduce(arena_ + bs.offset, bs.count, /*fp32*/ 0, average_ ? 4 : 0, comm_stream_);
-    HIP_OK(hipEventRecord(done_ev_[b], comm_stream_));
-    if (debug_sync_) HIP_OK(hipStreamSynchronize(comm_stream_));
+    auto& evs = ready_ev_[b];
+    // overlap: the collective runs on the comm stream; inline: on the stream that completed the
+    // bucket (stream order = no cross-stream edge in a captured graph)
+    // (world 1 without emulation has no collective: nothing to order against)
+    const bool real = comm_->world() > 1 || emulate_;
+    hipStream_t target = (overlap_ && real) ? comm_stream_ : contrib_[b].back();
+    for (size_t i = 0; i < contrib_[b].size(); ++i) {
+      if (contrib_[b][i] == target) continue;
+      if (i >= evs.size()) evs.resize(i + 1, nullptr);
+      if (!evs[i]) HIP_OK(hipEventCreateWithFlags(&evs[i], hipEventDisableTiming));
+      HIP_OK(hipEventRecord(evs[i], contrib_[b][i]));
+      HIP_OK(hipStreamWaitEvent(target, evs[i], 0));
+    }
+    float* buf = arena_ + bs.offset;
+    if (comm_->world() > 1) {
+      comm_->all_reduce(buf, bs.count, /*fp32*/ 0, average_ ? 4 : 0, target);
+    } else if (emulate_) {
+      // world 1 stand-in for the collective (graph-structure / overlap studies on one GPU):
+      // one pass over the bucket, like the reduction kernel of an all-reduce
+      const int rc = ddp_scale(buf, bs.count, 1.0f, target);
+      if (rc != 0) throw std::runtime_error("emulated collective launch failed");
+    }
+    done_stream_[b] = target;
+    HIP_OK(hipEventRecord(done_ev_[b], target));
+    if (debug_sync_) HIP_OK(hipStreamSynchronize(target));
   }
 }
 
@@ -274,8 +307,9 @@ void Reducer::finalize(hipStream_t compute) {
                                  " has parameters whose gradient was never produced "
                                  "(unused parameters are not supported)");
     }
-  launch_ready(compute);
-  for (int b = 0; b < next_launch_; ++b) HIP_OK(hipStreamWaitEvent(compute, done_ev_[b], 0));
+  launch_ready();
+  for (int b = 0; b < next_launch_; ++b)
+    if (done_stream_[b] != compute) HIP_OK(hipStreamWaitEvent(compute, done_ev_[b], 0));
   prepare();
 }
 

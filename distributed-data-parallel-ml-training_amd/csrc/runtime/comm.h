@@ -73,18 +73,28 @@ class Reducer {
   const std::vector<BucketSpec>& buckets() const { return buckets_; }
   // Start of a backward pass: reset readiness counters.
   void prepare();
-  // Gradient for parameter `p` has been fully written on `compute` (stream order).
+  // Gradient for parameter `p` has been fully written on `compute` (stream order). A bucket's
+  // gradients may come from several streams (the backward runs weight gradients on a side
+  // stream): its all-reduce waits on every stream that contributed to it.
   void mark_ready(int p, hipStream_t compute);
   // Launch any not-yet-launched bucket (all params must be ready), then make `compute`
   // wait for every bucket's all-reduce.
   void finalize(hipStream_t compute);
   // Debug/race-check mode: synchronise the comm stream after every bucket.
   void set_debug_sync(bool on) { debug_sync_ = on; }
+  // overlap (default): bucket collectives on the high-priority comm stream, overlapped with
+  // the rest of the backward. Off: each collective is issued inline on the stream that
+  // completed the bucket (no overlap, but a captured step stays a single-stream graph).
+  void set_overlap(bool on) { overlap_ = on; }
+  bool overlap() const { return overlap_; }
+  // world 1 only: run a bucket-sized pass in place of each (no-op) collective, so the graph
+  // shape and stream traffic of a multi-GPU step can be studied on one GPU
+  void set_emulate(bool on) { emulate_ = on; }
   int launched() const { return next_launch_; }
   hipStream_t comm_stream() const { return comm_stream_; }
 
  private:
-  void launch_ready(hipStream_t compute);
+  void launch_ready();
   RcclComm* comm_;
   float* arena_;
   std::vector<size_t> offsets_, numels_;
@@ -92,10 +102,15 @@ class Reducer {
   std::vector<int> bucket_of_param_;
   std::vector<int> pending_;  // params still missing per bucket
   std::vector<char> ready_;   // bucket complete
-  std::vector<hipEvent_t> ready_ev_, done_ev_;
+  std::vector<std::vector<hipStream_t>> contrib_;  // distinct producer streams per bucket
+  std::vector<std::vector<hipEvent_t>> ready_ev_;  // one event per producer stream slot
+  std::vector<hipEvent_t> done_ev_;
+  std::vector<hipStream_t> done_stream_;  // stream each bucket's collective ran on
   int next_launch_ = 0;
   bool average_;
   bool debug_sync_ = false;
+  bool overlap_ = true;
+  bool emulate_ = false;
   hipStream_t comm_stream_ = nullptr;
 };
 

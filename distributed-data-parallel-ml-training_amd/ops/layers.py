@@ -14,7 +14,8 @@ Activations between blocks are NHWC bf16; the first conv's input is zero-padded 
 import torch
 
 from .common import (native, ptr, stream_handle, check, grad_ready, ensure_grad, workspace,
-                     step_scratch, weight_krsc, STAT_REPLICAS)
+                     step_scratch, weight_krsc, side_stream, STAT_REPLICAS)
+from . import common as _common
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -127,12 +128,25 @@ class GradLink:
         return out
 
 
-def conv_backward(spec, x, dz, dweight, need_dx, link=None):
+def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None):
+    """dW += wgrad(dz, x); returns dx (or None). With ``weight`` (the parameter whose gradient
+    is dweight) and the backward side stream enabled, the wgrad runs on the side stream and the
+    parameter is announced ready there (common.side_stream); otherwise everything is stream-
+    ordered on the current stream and the caller announces the gradient."""
     N, H, W, C = x.shape
     g = spec.geom(N, H, W, weight_krsc(dweight))
     s = stream_handle()
     ws = workspace(x.device)
-    native().conv_wgrad(g, ptr(dz), ptr(x), ptr(dweight), ptr(ws), ws.numel(), 0, s)
+    if weight is not None and _common.BWD_SIDE_STREAM:
+        side = side_stream(x.device, x, dz)
+        with torch.cuda.stream(side.stream):
+            native().conv_wgrad(g, ptr(dz), ptr(x), ptr(dweight), ptr(side.ws), side.ws.numel(), 0,
+                                side.stream.cuda_stream)
+            grad_ready([weight])
+    else:
+        native().conv_wgrad(g, ptr(dz), ptr(x), ptr(dweight), ptr(ws), ws.numel(), 0, s)
+        if weight is not None:
+            grad_ready([weight])
     if not need_dx:
         return None
     if spec.C != spec.Cr:
@@ -201,8 +215,7 @@ class _ConvBNActFn(torch.autograd.Function):
         grad_ready([gamma, beta, bias])
         if ctx.res_link is not None and dres is not None:
             dres = ctx.res_link.offer(dres)
-        dx = conv_backward(spec, x, dz, gw, ctx.needs_input_grad[0], ctx.in_link)
-        grad_ready([weight])
+        dx = conv_backward(spec, x, dz, gw, ctx.needs_input_grad[0], ctx.in_link, weight=weight)
         return dx, None, None, None, None, dres, None, None, None
 
 

@@ -12,11 +12,13 @@ MI355X design:
 * gradients live in one flat fp32 arena (optim/arena.py); a bucket is a slice of it in reverse
   parameter order, so buckets are all-reduced in place with no pack/unpack copies;
 * GPU: the native C++ ``Reducer`` (csrc/runtime/comm.cpp) launches ncclAllReduce(avg) for each
-  full bucket on a high-priority comm stream gated by an event recorded on the compute stream;
-  the fused backward kernels announce finished gradients through ops.common.grad_ready. A final
-  autograd callback makes the compute stream wait on every bucket before the optimizer runs.
-  All of this is stream/event-ordered, so a whole training step (including the bucket
-  all-reduces) can be captured into one hipGraph (engine/step.py).
+  full bucket as soon as the fused backward kernels announce its last gradient
+  (ops.common.grad_ready). By default the collective is issued INLINE on the backward stream:
+  on MI355X / ROCm 7 a second (comm) stream makes every cross-queue edge of the step expensive
+  (measured 2.3x slower captured steps, see ``overlap`` below), so the step — forward,
+  backward, bucket all-reduces, optimizer — is one single-stream hipGraph (engine/step.py).
+  ``overlap=True`` keeps the classic design (high-priority comm stream gated by events, a final
+  autograd callback makes the compute stream wait on every bucket).
 * CPU/Gloo: the same bucket plan driven from post-accumulate-grad hooks with async all-reduce.
 * Bucket sizing for xGMI: each MI355X has 7 point-to-point links; a ring all-reduce moves
   2(w-1)/w of the bucket over one link per hop, so buckets must be large enough (>= a few MiB)
@@ -24,6 +26,8 @@ MI355X design:
   first bucket (the big 512x512 conv gradients, ready first) starts early. Defaults: 25 MiB
   (reference) with a 1 MiB first bucket; ``bucket_cap_mb`` is tunable.
 """
+import os
+
 import torch
 import torch.distributed as dist
 import torch.nn as nn
@@ -94,7 +98,7 @@ class _PyReducer:
 
 class DistributedDataParallel(nn.Module):
     def __init__(self, module, comm, bucket_cap_mb=25.0, first_bucket_cap_mb=1.0,
-                 broadcast_buffers=True, average=True):
+                 broadcast_buffers=True, average=True, overlap=None):
         super().__init__()
         self.module = module
         self.comm = comm
@@ -115,6 +119,16 @@ class DistributedDataParallel(nn.Module):
             self.reducer = native().Reducer(comm.comm, a.grad.data_ptr(), list(a.offsets),
                                             list(a.numels), cap, cap_first, bool(average))
             self.buckets = [tuple(b) for b in self.reducer.buckets()]
+            # overlap=False (default, DDP_AMD_COMM_OVERLAP=0): bucket collectives are issued inline
+            # on the backward stream as buckets fill; overlap=True: on a separate comm stream.
+            # Measured on MI355X / ROCm 7 (one GPU, stand-in collectives DDP_AMD_EMULATE_COMM=1,
+            # VGG-11 b256): inline 1.04 ms/step; comm stream 2.39 ms captured, 1.39 ms eager —
+            # every cross-queue edge of the step costs far more than the overlap can win back, so
+            # the step stays on ONE stream (profiles/r1_comm_stream_study.md).
+            if overlap is None:
+                overlap = os.environ.get("DDP_AMD_COMM_OVERLAP", "0") == "1"
+            self.reducer.set_overlap(bool(overlap))
+            self.reducer.set_emulate(os.environ.get("DDP_AMD_EMULATE_COMM", "0") == "1")
             self._hook = register_grad_ready_hook(self._on_grad_ready)
         else:
             self.reducer = _PyReducer(comm, self.arena, cap, cap_first, average)
@@ -173,7 +187,11 @@ class DistributedDataParallel(nn.Module):
         i = self._index.get(id(p))
         if i is None:
             return
-        self._stream = stream
+        if self._stream is None:
+            # the backward's main stream (the first announcement comes from the classifier);
+            # weight gradients may later be announced from the backward side stream — the
+            # reducer then waits on both streams for the buckets they share
+            self._stream = stream
         self._queue_finalize()
         self.reducer.mark_ready(i, stream.cuda_stream)
 
@@ -189,7 +207,8 @@ class DistributedDataParallel(nn.Module):
     def _finalize(self):
         self._in_backward = False
         if self.cuda:
-            self.reducer.finalize(self._stream.cuda_stream)
+            stream, self._stream = self._stream, None
+            self.reducer.finalize(stream.cuda_stream)
         else:
             self.reducer.finalize()
 
