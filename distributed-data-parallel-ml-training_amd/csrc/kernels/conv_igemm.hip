@@ -38,6 +38,7 @@
 #include "common.h"
 #include "api.h"
 #include <algorithm>
+#include <map>
 
 namespace ddp_amd {
 
@@ -873,6 +874,21 @@ static void launch_cfg(ConvArgs& a, int splits, hipStream_t st) {
   }
 }
 
+// Measured tile / split-K choices per GEMM problem (tools/conv_tune.py sweeps every candidate
+// on the GPU and writes ops/conv_tuning.json, loaded into this table at import). Problems not
+// in the table fall back to the cost model. g_force_tile (sweeps only) overrides both.
+struct TuneKey {
+  int mode, M, N, K;
+  bool operator<(const TuneKey& o) const {
+    if (mode != o.mode) return mode < o.mode;
+    if (M != o.M) return M < o.M;
+    if (N != o.N) return N < o.N;
+    return K < o.K;
+  }
+};
+static std::map<TuneKey, std::pair<int, int>> g_tuned;  // -> (tile index, splits)
+static int g_force_tile = 0;                             // 1..4 = tile index + 1
+
 template <int MODE>
 static void launch_mode(ConvArgs& a, size_t ws_elems, hipStream_t st) {
   int sp[4];
@@ -881,6 +897,22 @@ static void launch_mode(ConvArgs& a, size_t ws_elems, hipStream_t st) {
   int best = 0;
   for (int i = 1; i < 4; ++i)
     if (c[i] < c[best]) best = i;
+  if (g_force_tile >= 1 && g_force_tile <= 4) {
+    best = g_force_tile - 1;
+  } else if (a.splits <= 0) {
+    auto it = g_tuned.find(TuneKey{MODE, a.Mg, a.Ng, a.Kg});
+    if (it != g_tuned.end()) {
+      const int BM = it->second.first < 2 ? 128 : 64;
+      const int BN = (it->second.first & 1) ? 64 : 128;
+      const size_t slab = (size_t)a.Mg * a.Ng;
+      const int ksteps = (a.Kg + 63) / 64;
+      int spl = std::max(1, std::min(it->second.second, ksteps));
+      if (spl > 1 && (size_t)spl * slab > ws_elems) spl = std::max<int>(1, (int)(ws_elems / slab));
+      (void)BM; (void)BN;
+      best = it->second.first;
+      sp[best] = spl;
+    }
+  }
   switch (best) {
     case 0: launch_cfg<MODE, 128, 128>(a, sp[0], st); break;
     case 1: launch_cfg<MODE, 128, 64>(a, sp[1], st); break;
@@ -894,6 +926,14 @@ extern "C" void ddp_conv_options(int wgrad_atomic, int persistent, int stages) {
   g_persistent = persistent;
   g_stages = stages;
 }
+
+// tile: 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64
+extern "C" void ddp_conv_tune_set(int mode, int M, int N, int K, int tile, int splits) {
+  if (tile < 0 || tile > 3) return;
+  g_tuned[TuneKey{mode, M, N, K}] = {tile, std::max(1, splits)};
+}
+extern "C" void ddp_conv_tune_clear() { g_tuned.clear(); }
+extern "C" void ddp_conv_force_tile(int tile_plus_one) { g_force_tile = tile_plus_one; }
 
 extern "C" int ddp_conv_fwd(const ConvGeom* g, const void* x, const void* wc, const float* bias,
                             void* y, float* stats, float* ws, size_t ws_elems, int splits,

@@ -22,7 +22,28 @@ def native():
         _NATIVE.conv_options(int(os.environ.get("DDP_AMD_WGRAD_ATOMIC", "0")),
                              int(os.environ.get("DDP_AMD_CONV_PERSISTENT", "0")),
                              int(os.environ.get("DDP_AMD_CONV_STAGES", str(CONV_STAGES))))
+        load_conv_tuning(_NATIVE)
     return _NATIVE
+
+
+TUNING_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "conv_tuning.json")
+
+
+def load_conv_tuning(n=None, path=None):
+    """Load the measured conv tile / split-K table (tools/conv_tune.py) into the native launcher.
+    DDP_AMD_CONV_TUNING=0 ignores it (cost-model choices only). Returns the number of entries."""
+    import json
+    n = n or native()
+    n.conv_tune_clear()
+    path = path or os.environ.get("DDP_AMD_CONV_TUNING_FILE", TUNING_FILE)
+    if os.environ.get("DDP_AMD_CONV_TUNING", "1") == "0" or not os.path.exists(path):
+        return 0
+    with open(path) as f:
+        table = json.load(f)
+    for e in table.get("entries", []):
+        n.conv_tune_set(int(e["mode"]), int(e["M"]), int(e["N"]), int(e["K"]), int(e["tile"]),
+                        int(e["splits"]))
+    return len(table.get("entries", []))
 
 
 def weight_krsc(w):

@@ -1,0 +1,27 @@
+"""The measured conv tile / split-K table (ops/conv_tuning.json, written by tools/conv_tune.py)
+is well-formed: every entry names a valid tile and split factor for a GEMM problem, and the
+recorded winner was not slower than the cost-model choice it replaces."""
+import json
+import os
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TABLE = os.path.join(ROOT, "distributed-data-parallel-ml-training_amd", "ops", "conv_tuning.json")
+
+
+@pytest.mark.skipif(not os.path.exists(TABLE), reason="no tuning table")
+def test_tuning_table_well_formed():
+    with open(TABLE) as f:
+        t = json.load(f)
+    keys = set()
+    for e in t["entries"]:
+        assert e["mode"] in (0, 1, 2)
+        assert 0 <= e["tile"] <= 3
+        assert 1 <= e["splits"] <= 64
+        assert min(e["M"], e["N"], e["K"]) > 0
+        assert e["us"] <= e["auto_us"] + 1e-6
+        keys.add((e["mode"], e["M"], e["N"], e["K"]))
+    assert len(keys) == len({(e["mode"], e["M"], e["N"], e["K"]) for e in t["entries"]})
+    # the flagship VGG-11 b256 problems are covered (e.g. layers.18 fwd: M=256*4*4, N=512)
+    assert (0, 256 * 16, 512, 9 * 512) in keys

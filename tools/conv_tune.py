@@ -1,0 +1,148 @@
+#!/usr/bin/env python3
+"""Measure every tile / split-K candidate of the implicit-GEMM conv for the training shapes and
+write the winners to the launcher's tuning table (ops/conv_tuning.json).
+
+    python tools/conv_tune.py [--out PATH] [--reps 30] [--quick]
+
+Shapes: VGG-11 at per-GPU batch 256/128/64/32 (weak scaling and the reference's strong-scaling
+split of 256 over 1/2/4/8 GPUs) and ResNet-50 at 64. For each GEMM problem (mode, M, N, K) every
+tile (128x128, 128x64, 64x128, 64x64) x split-K factor is launched exactly as the training step
+launches it (same kernels, same finish passes), timed with HIP events, and the fastest is kept;
+the cost-model choice is timed too and reported next to it. Like MIOpen's find-db, but for our
+own kernels. Strided dgrad problems (several phase GEMMs) are tuned as a whole and the winner is
+recorded for every phase.
+"""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tools"))
+
+TILES = ["128x128", "128x64", "64x128", "64x64"]
+
+
+def dgrad_phases(N, H, W, K, R, S, stride, pad):
+    """(M, K) of each phase GEMM of a strided dgrad (mirrors ddp_conv_dgrad)."""
+    if stride == 1:
+        return [(N * H * W, R * S * K)]
+    out = []
+    for pa in range(stride):
+        for pb in range(stride):
+            r0, s0 = (pa + pad) % stride, (pb + pad) % stride
+            Rt = (R - r0 + stride - 1) // stride if r0 < R else 0
+            St = (S - s0 + stride - 1) // stride if s0 < S else 0
+            Hp = (H - pa + stride - 1) // stride if pa < H else 0
+            Wp = (W - pb + stride - 1) // stride if pb < W else 0
+            if Rt * St == 0 or Hp * Wp == 0:
+                continue
+            out.append((N * Hp * Wp, Rt * St * K))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--quick", action="store_true", help="VGG-11 b256 only")
+    args = ap.parse_args()
+    import torch
+    import ddp_amd  # noqa: F401
+    from ddp_amd.ops import common
+    from ddp_amd.ops.common import native, ptr, workspace, TUNING_FILE
+    from ddp_amd.ops.layers import ConvBNActSpec
+    from conv_bench import vgg_layers, resnet_layers
+
+    n = native()
+    n.conv_tune_clear()  # time the cost-model choice without a previous table
+    dev = torch.device("cuda", 0)
+    ws = workspace(dev)
+    st = torch.cuda.current_stream().cuda_stream
+    sets = [("vgg11", 256)] if args.quick else [("vgg11", 256), ("vgg11", 128), ("vgg11", 64),
+                                                ("vgg11", 32), ("resnet50", 64)]
+    entries, seen = [], set()
+    saved_total = 0.0
+
+    def timeit(fn):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1000.0 / args.reps
+
+    for model, B in sets:
+        layers = vgg_layers(B) if model == "vgg11" else resnet_layers(B)
+        for (N, C, H, W, K, R, stride, pad, Cr) in layers:
+            conv = torch.nn.Conv2d(Cr, K, R, stride, pad, bias=False).to(dev)
+            conv.weight.data = conv.weight.data.contiguous(memory_format=torch.channels_last)
+            spec = ConvBNActSpec(conv, None, cin_pad=C if C != Cr else None)
+            spec.maybe_pack()
+            P = (H + 2 * pad - R) // stride + 1
+            x = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
+            z = torch.empty(N, P, P, K, device=dev, dtype=torch.bfloat16)
+            dz = torch.randn(N, P, P, K, device=dev).to(torch.bfloat16)
+            dx = torch.empty_like(x)
+            dw = torch.zeros_like(conv.weight)
+            stats = torch.zeros(16 * 2 * K, device=dev)
+            g = spec.geom(N, H, W)
+            gw = spec.geom(N, H, W, common.weight_krsc(dw))
+            probs = []
+            if C != 8:  # C = 8 input layers use the direct kernel forward (conv_smallk.hip)
+                probs.append((0, [(N * P * P, K, R * R * C)],
+                              lambda s: n.conv_fwd(g, ptr(x), ptr(spec.wc), 0, ptr(z), ptr(stats),
+                                                   ptr(ws), ws.numel(), s, st)))
+            if C == Cr:
+                probs.append((1, [(m, C, k) for m, k in dgrad_phases(N, H, W, K, R, R, stride, pad)],
+                              lambda s: n.conv_dgrad(g, ptr(dz), ptr(spec.wc), ptr(dx), ptr(ws),
+                                                     ws.numel(), s, st)))
+            probs.append((2, [(K, R * R * C, N * P * P)],
+                          lambda s: n.conv_wgrad(gw, ptr(dz), ptr(x), ptr(dw), ptr(ws), ws.numel(),
+                                                 s, st)))
+            label = f"{model} N{N} {Cr}->{K} {H}x{W} k{R} s{stride}"
+            for mode, gemms, fn in probs:
+                key = (mode, tuple(gemms))
+                if key in seen:
+                    continue
+                seen.add(key)
+                n.conv_force_tile(0)
+                auto_us = timeit(lambda: fn(0))
+                best = (auto_us, None, None)
+                M0, N0, K0 = gemms[0]
+                ksteps = (K0 + 63) // 64
+                for t in range(4):
+                    n.conv_force_tile(t + 1)
+                    for s in (1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64):
+                        if s > 1 and (ksteps // s < 2 or s * M0 * N0 > ws.numel()):
+                            continue
+                        us = timeit(lambda: fn(s))
+                        if us < best[0]:
+                            best = (us, t, s)
+                n.conv_force_tile(0)
+                us, t, s = best
+                names = ["fwd", "dgrad", "wgrad"]
+                if t is None:
+                    print(f"{label:42s} {names[mode]:5s} auto {auto_us:7.1f} us (kept)", flush=True)
+                    continue
+                saved_total += auto_us - us
+                print(f"{label:42s} {names[mode]:5s} auto {auto_us:7.1f} us -> {TILES[t]} "
+                      f"split {s:2d} {us:7.1f} us", flush=True)
+                for (M, Nn, Kk) in gemms:
+                    entries.append({"mode": mode, "M": M, "N": Nn, "K": Kk, "tile": t,
+                                    "splits": s, "us": round(us, 2), "auto_us": round(auto_us, 2),
+                                    "shape": label})
+    out = args.out or TUNING_FILE
+    with open(out, "w") as f:
+        json.dump({"device": torch.cuda.get_device_name(0), "reps": args.reps,
+                   "entries": entries}, f, indent=1)
+    print(f"wrote {len(entries)} entries to {out}; summed per-op saving {saved_total:.1f} us")
+
+
+if __name__ == "__main__":
+    main()
