@@ -114,16 +114,21 @@ PYBIND11_MODULE(_native, m) {
                          uintptr_t res, uintptr_t stats, uintptr_t gamma, uintptr_t beta,
                          uintptr_t dout, uintptr_t sums, uintptr_t dz, uintptr_t dres,
                          uintptr_t dgamma, uintptr_t dbeta, uintptr_t dbias, uintptr_t st,
-                         uintptr_t coef) {
+                         uintptr_t coef, uintptr_t counter) {
     ddp_amd::BnArgs a{};
     a.coef = P<float>(coef);
+    a.counter = P<int>(counter);
     a.N = N; a.H = H; a.W = W; a.C = C; a.pool = pool; a.relu = relu; a.eps = eps;
     a.z = P<unsigned short>(z); a.res = P<unsigned short>(res); a.stats = P<float>(stats);
     a.gamma = P<float>(gamma); a.beta = P<float>(beta); a.dout = P<unsigned short>(dout);
     a.sums = P<float>(sums); a.dz = P<unsigned short>(dz); a.dres = P<unsigned short>(dres);
     a.dgamma = P<float>(dgamma); a.dbeta = P<float>(dbeta); a.dbias = P<float>(dbias);
     check(ddp_bn_act_bwd(&a, S(st)), "bn_act_bwd");
-  });
+  }, py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("pool"), py::arg("relu"),
+     py::arg("eps"), py::arg("z"), py::arg("res"), py::arg("stats"), py::arg("gamma"),
+     py::arg("beta"), py::arg("dout"), py::arg("sums"), py::arg("dz"), py::arg("dres"),
+     py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("stream"), py::arg("coef"),
+     py::arg("counter") = 0);
 
   m.def("linear_ce_fwd", [](uintptr_t x, uintptr_t W, uintptr_t b, uintptr_t labels, int B, int F,
                             int J, uintptr_t logits, uintptr_t dlogits, uintptr_t loss_sum,

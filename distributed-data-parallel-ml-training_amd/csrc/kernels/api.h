@@ -44,6 +44,8 @@ struct BnArgs {
   int use_running;              // eval with running statistics instead of batch statistics
   float* coef;                  // [6][C] scale, shift, mean, invstd (fwd) and k1, k2 (bwd); the
                                 // backward reads the table its forward wrote
+  int* counter;                 // backward: zeroed ticket counter -> the reduce kernel's last
+                                // block finalizes k1/k2, dgamma, dbeta (no finalize launch)
 };
 
 struct PackDesc {

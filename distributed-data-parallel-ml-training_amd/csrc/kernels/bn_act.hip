@@ -329,6 +329,37 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
       atomicAdd(rep + k * a.C + (cg_base + g) * 8 + e, s);
     }
   }
+  if (a.counter == nullptr) return;
+  // In-launch finalize (cdna_hip_programming.md §6 Guideline 16, counter form with sc1 hand-off):
+  // the replica sums are written by device-scope atomics (performed past the XCD L2s), so no
+  // release fence is needed — every wave drains its atomics (vmcnt), a barrier, then one ticket
+  // per block; the block that draws the last ticket reads the replicas with sc1 loads and turns
+  // them into k1 / k2 and the dgamma / dbeta contributions (no separate finalize launch).
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(red);
+  if (tid == 0) {
+    const int nblk = gridDim.x * gridDim.y;
+    const int t = __hip_atomic_fetch_add(a.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[0] = (t == nblk - 1);
+    if (t == nblk - 1) *a.counter = 0;  // ready for the next backward (scratch fill zeroes it too)
+  }
+  __syncthreads();
+  if (!flag[0]) return;
+  const float inv_m = 1.f / ((float)a.N * a.H * a.W);
+  for (int c = tid; c < a.C; c += 256) {
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int r = 0; r < kStatRep; ++r) {
+      s1 += __hip_atomic_load(a.sums + r * 2 * a.C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s2 += __hip_atomic_load(a.sums + r * 2 * a.C + a.C + c, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+    }
+    a.coef[kK1 * a.C + c] = s1 * inv_m;
+    a.coef[kK2 * a.C + c] = s2 * inv_m;
+    if (a.dgamma) a.dgamma[c] += s2;
+    if (a.dbeta) a.dbeta[c] += s1;
+  }
 }
 
 template <bool POOL, int IPT, bool FOLD>
@@ -452,7 +483,9 @@ static void launch_bwd(const BnArgs& a, size_t npix, int Gb, int chunks, hipStre
   // were just written by memory-side atomics and every block re-reads them uncached — so the
   // backward keeps its separate finalize launch)
   const size_t nch = (size_t)Gb * 8;
-  if (kFoldBwd && (size_t)bx * chunks * nch * 2 * kStatRep * sizeof(float) <= kFoldBytes) {
+  if (a.counter) {  // finalized by the reduce kernel's last block
+    hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT, false>), dim3(bx, chunks), dim3(256), 0, st, a);
+  } else if (kFoldBwd && (size_t)bx * chunks * nch * 2 * kStatRep * sizeof(float) <= kFoldBytes) {
     hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT, true>), dim3(bx, chunks), dim3(256),
                        2 * nch * sizeof(float), st, a);
   } else {

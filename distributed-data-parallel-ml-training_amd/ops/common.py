@@ -151,6 +151,15 @@ def join_side_streams():
         st.join()
 
 
+# BatchNorm backward: DDP_AMD_BN_LAST_BLOCK=1 lets the reduce kernel's last block (ticket
+# counter) finalize the coefficients instead of a separate one-block launch. OFF by default:
+# measured slower on MI355X (VGG-11 b256 1.020 vs 0.965 ms/step, ResNet-50 b64 11.81 vs 10.07;
+# with an agent release fence per block 1.044 / 15.29) — every block must drain its memory-side
+# atomics before its ticket, and the single ticket address serialises thousands of blocks,
+# which costs more than the ~5 us launch it saves.
+BN_LAST_BLOCK = os.environ.get("DDP_AMD_BN_LAST_BLOCK", "0") == "1"
+
+
 # ---------------------------------------------------------------- per-step accumulator scratch
 # Every fused layer owns fixed slices of one persistent fp32 buffer for the accumulators that
 # must start at zero each step (BatchNorm statistics replicas, BN-backward sums). The model's

@@ -52,7 +52,11 @@ class ConvBNActSpec:
         sc = step_scratch(dev)
         self.scratch = sc
         self.stats = sc.take(STAT_REPLICAS * 2 * K)[:STAT_REPLICAS * 2 * K]
-        self.sums = sc.take(STAT_REPLICAS * 2 * K)[:STAT_REPLICAS * 2 * K]
+        sums = sc.take(STAT_REPLICAS * 2 * K + 64)
+        self.sums = sums[:STAT_REPLICAS * 2 * K]
+        # ticket counter of the BN-backward reduce kernel's in-launch finalize (zeroed with the
+        # rest of the scratch each forward, and reset by the finalizing block)
+        self.bwd_counter = sums[STAT_REPLICAS * 2 * K:STAT_REPLICAS * 2 * K + 1]
         # per-layer BN coefficient table [6][K] (scale, shift, mean, invstd | k1, k2): written
         # by the forward's finalize kernel, read by the backward (one use per step per layer)
         self.coef = torch.empty(6 * K, dtype=F32, device=dev)
@@ -211,7 +215,7 @@ class _ConvBNActFn(torch.autograd.Function):
         native().bn_act_bwd(N, P, Q, K, int(spec.pool), int(spec.relu), spec.eps, ptr(z),
                             ptr(residual), ptr(stats), ptr(gamma), ptr(beta), ptr(dy), ptr(sums),
                             ptr(dz), ptr(dres), ptr(gg), ptr(gbt), ptr(gb), stream_handle(),
-                            ptr(spec.coef))
+                            ptr(spec.coef), ptr(spec.bwd_counter) if _common.BN_LAST_BLOCK else 0)
         grad_ready([gamma, beta, bias])
         if ctx.res_link is not None and dres is not None:
             dres = ctx.res_link.offer(dres)

@@ -121,7 +121,10 @@ def _bn_ref(z, gamma, beta, eps, relu, pool, res=None):
 @pytest.mark.parametrize("C,H,pool,res", [(64, 8, True, False), (128, 4, False, False),
                                           (512, 2, True, False), (256, 8, False, True),
                                           (2048, 2, False, True)])
-def test_bn_act_fwd_bwd(native_ext, C, H, pool, res):
+@pytest.mark.parametrize("last_block", [False, True])
+def test_bn_act_fwd_bwd(native_ext, C, H, pool, res, last_block):
+    """last_block: the reduce kernel's final block finalizes k1/k2/dgamma/dbeta (ticket counter,
+    agent release/acquire) instead of a separate finalize launch."""
     from ddp_amd.ops.common import ptr, stream_handle
     nat = native_ext
     N = 8
@@ -155,10 +158,13 @@ def test_bn_act_fwd_bwd(native_ext, C, H, pool, res):
     dg = torch.zeros(C, device=DEV)
     db = torch.zeros(C, device=DEV)
     dbias = torch.zeros(C, device=DEV)
+    counter = torch.zeros(1, dtype=torch.int32, device=DEV) if last_block else None
     nat.bn_act_bwd(N, H, H, C, int(pool), 1, 1e-5, ptr(zn), ptr(rn), ptr(stats), ptr(gamma),
                    ptr(beta), ptr(doutn), ptr(sums), ptr(dz), ptr(dres), ptr(dg), ptr(db),
-                   ptr(dbias), s, ptr(coef))
+                   ptr(dbias), s, ptr(coef), ptr(counter))
     torch.cuda.synchronize()
+    if last_block:
+        assert int(counter.item()) == 0  # reset by the finalizing block
     assert rel_err(dz.permute(0, 3, 1, 2), zr.grad) < 2e-2
     assert rel_err(dg, gr.grad) < 1e-2
     assert rel_err(db, br.grad) < 1e-2
