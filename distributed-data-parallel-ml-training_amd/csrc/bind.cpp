@@ -162,11 +162,13 @@ PYBIND11_MODULE(_native, m) {
   }, py::arg("wgrad_atomic") = 0, py::arg("persistent") = 0, py::arg("stages") = 2);
   // measured tile/split table (mode 0 fwd, 1 dgrad, 2 wgrad; GEMM dims M, N, K; tile 0..3 =
   // 128x128, 128x64, 64x128, 64x64) and the forced-tile switch used by tools/conv_tune.py
-  m.def("conv_tune_set", [](int mode, int M, int N, int K, int tile, int splits) {
-    ddp_conv_tune_set(mode, M, N, K, tile, splits);
-  });
+  m.def("conv_tune_set", [](int mode, int M, int N, int K, int tile, int splits, int stages) {
+    ddp_conv_tune_set(mode, M, N, K, tile, splits, stages);
+  }, py::arg("mode"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("tile"),
+     py::arg("splits"), py::arg("stages") = 0);
   m.def("conv_tune_clear", []() { ddp_conv_tune_clear(); });
-  m.def("conv_force_tile", [](int t) { ddp_conv_force_tile(t); });
+  m.def("conv_force_tile", [](int t, int stages) { ddp_conv_force_tile(t, stages); },
+        py::arg("tile_plus_one"), py::arg("stages") = 0);
   // descs: list of (p, wc, wt, K, Cr, C, R, S, krsc)
   m.def("pack_conv_weights", [](std::vector<std::tuple<uintptr_t, uintptr_t, uintptr_t, int, int,
                                                        int, int, int, int>> descs, uintptr_t st) {

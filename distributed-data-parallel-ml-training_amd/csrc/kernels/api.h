@@ -92,9 +92,9 @@ int ddp_sgd(float* p, const float* g, float* buf, size_t n, float lr, float mome
 int ddp_conv_fwd_smallk(const ddp_amd::ConvGeom* g, const void* x, const void* wc,
                         const float* bias, void* y, float* stats, hipStream_t st);
 void ddp_conv_options(int wgrad_atomic, int persistent, int stages);
-void ddp_conv_tune_set(int mode, int M, int N, int K, int tile, int splits);
+void ddp_conv_tune_set(int mode, int M, int N, int K, int tile, int splits, int stages);
 void ddp_conv_tune_clear();
-void ddp_conv_force_tile(int tile_plus_one);
+void ddp_conv_force_tile(int tile_plus_one, int stages);
 int ddp_pack_conv_weights(const ddp_amd::PackDesc* descs, int n, hipStream_t st);
 int ddp_sgd_pack(const void* items, int n_items, const long long* descs, float* p, float* g,
                  float* buf, float lr, float momentum, float wd, float grad_scale, int nesterov,

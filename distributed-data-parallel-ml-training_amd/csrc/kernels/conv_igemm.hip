@@ -829,7 +829,7 @@ static void launch_gemm(const ConvArgs& a, int items, hipStream_t st) {
 }
 
 template <int MODE, int BM, int BN>
-static void launch_cfg(ConvArgs& a, int splits, hipStream_t st) {
+static void launch_cfg(ConvArgs& a, int splits, hipStream_t st, int nst_req = 0) {
   constexpr int BK = 64;
   const int tiles = ((a.Mg + BM - 1) / BM) * ((a.Ng + BN - 1) / BN);
   const int ksteps = (a.Kg + BK - 1) / BK;
@@ -841,8 +841,8 @@ static void launch_cfg(ConvArgs& a, int splits, hipStream_t st) {
   // slab + grouped-finish reduction is cheaper
   if (a.wg_atomic && splits > kMaxAtomicSplits) a.wg_atomic = 0;
   const int items = tiles * splits;
-  const int nst = stages_for(BM, BN);
-  if (nst == 4) launch_gemm<MODE, BM, BN, (BM == 128 && BN == 128) ? 4 : 4>(a, items, st);
+  const int nst = nst_req >= 2 && nst_req <= 4 ? nst_req : stages_for(BM, BN);
+  if (nst == 4) launch_gemm<MODE, BM, BN, 4>(a, items, st);
   else if (nst == 3) launch_gemm<MODE, BM, BN, 3>(a, items, st);
   else launch_gemm<MODE, BM, BN, 2>(a, items, st);
   if (splits == 1) return;
@@ -886,15 +886,19 @@ struct TuneKey {
     return K < o.K;
   }
 };
-static std::map<TuneKey, std::pair<int, int>> g_tuned;  // -> (tile index, splits)
-static int g_force_tile = 0;                             // 1..4 = tile index + 1
+struct TuneVal {
+  int tile, splits, stages;
+};
+static std::map<TuneKey, TuneVal> g_tuned;  // -> (tile index, splits, LDS stages)
+static int g_force_tile = 0;                // 1..4 = tile index + 1
+static int g_force_stages = 0;              // 2..4 (sweeps), 0 = policy
 
 template <int MODE>
 static void launch_mode(ConvArgs& a, size_t ws_elems, hipStream_t st) {
   int sp[4];
   const double c[4] = {tile_cost(128, 128, a, ws_elems, &sp[0]), tile_cost(128, 64, a, ws_elems, &sp[1]),
                        tile_cost(64, 128, a, ws_elems, &sp[2]), tile_cost(64, 64, a, ws_elems, &sp[3])};
-  int best = 0;
+  int best = 0, nst = g_force_stages;
   for (int i = 1; i < 4; ++i)
     if (c[i] < c[best]) best = i;
   if (g_force_tile >= 1 && g_force_tile <= 4) {
@@ -902,22 +906,21 @@ static void launch_mode(ConvArgs& a, size_t ws_elems, hipStream_t st) {
   } else if (a.splits <= 0) {
     auto it = g_tuned.find(TuneKey{MODE, a.Mg, a.Ng, a.Kg});
     if (it != g_tuned.end()) {
-      const int BM = it->second.first < 2 ? 128 : 64;
-      const int BN = (it->second.first & 1) ? 64 : 128;
       const size_t slab = (size_t)a.Mg * a.Ng;
       const int ksteps = (a.Kg + 63) / 64;
-      int spl = std::max(1, std::min(it->second.second, ksteps));
+      int spl = std::max(1, std::min(it->second.splits, ksteps));
       if (spl > 1 && (size_t)spl * slab > ws_elems) spl = std::max<int>(1, (int)(ws_elems / slab));
-      (void)BM; (void)BN;
-      best = it->second.first;
+      if (ws_elems == 0) spl = 1;
+      best = it->second.tile;
       sp[best] = spl;
+      nst = it->second.stages;
     }
   }
   switch (best) {
-    case 0: launch_cfg<MODE, 128, 128>(a, sp[0], st); break;
-    case 1: launch_cfg<MODE, 128, 64>(a, sp[1], st); break;
-    case 2: launch_cfg<MODE, 64, 128>(a, sp[2], st); break;
-    default: launch_cfg<MODE, 64, 64>(a, sp[3], st); break;
+    case 0: launch_cfg<MODE, 128, 128>(a, sp[0], st, nst); break;
+    case 1: launch_cfg<MODE, 128, 64>(a, sp[1], st, nst); break;
+    case 2: launch_cfg<MODE, 64, 128>(a, sp[2], st, nst); break;
+    default: launch_cfg<MODE, 64, 64>(a, sp[3], st, nst); break;
   }
 }
 
@@ -928,12 +931,15 @@ extern "C" void ddp_conv_options(int wgrad_atomic, int persistent, int stages) {
 }
 
 // tile: 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64
-extern "C" void ddp_conv_tune_set(int mode, int M, int N, int K, int tile, int splits) {
+extern "C" void ddp_conv_tune_set(int mode, int M, int N, int K, int tile, int splits, int stages) {
   if (tile < 0 || tile > 3) return;
-  g_tuned[TuneKey{mode, M, N, K}] = {tile, std::max(1, splits)};
+  g_tuned[TuneKey{mode, M, N, K}] = {tile, std::max(1, splits), stages};
 }
 extern "C" void ddp_conv_tune_clear() { g_tuned.clear(); }
-extern "C" void ddp_conv_force_tile(int tile_plus_one) { g_force_tile = tile_plus_one; }
+extern "C" void ddp_conv_force_tile(int tile_plus_one, int stages) {
+  g_force_tile = tile_plus_one;
+  g_force_stages = stages;
+}
 
 extern "C" int ddp_conv_fwd(const ConvGeom* g, const void* x, const void* wc, const float* bias,
                             void* y, float* stats, float* ws, size_t ws_elems, int splits,

@@ -42,7 +42,7 @@ def load_conv_tuning(n=None, path=None):
         table = json.load(f)
     for e in table.get("entries", []):
         n.conv_tune_set(int(e["mode"]), int(e["M"]), int(e["N"]), int(e["K"]), int(e["tile"]),
-                        int(e["splits"]))
+                        int(e["splits"]), int(e.get("stages", 0)))
     return len(table.get("entries", []))
 
 

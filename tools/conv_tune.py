@@ -6,7 +6,7 @@ write the winners to the launcher's tuning table (ops/conv_tuning.json).
 
 Shapes: VGG-11 at per-GPU batch 256/128/64/32 (weak scaling and the reference's strong-scaling
 split of 256 over 1/2/4/8 GPUs) and ResNet-50 at 64. For each GEMM problem (mode, M, N, K) every
-tile (128x128, 128x64, 64x128, 64x64) x split-K factor is launched exactly as the training step
+tile (128x128, 128x64, 64x128, 64x64) x LDS ring depth (2-4 stages) x split-K factor is launched exactly as the training step
 launches it (same kernels, same finish passes), timed with HIP events, and the fastest is kept;
 the cost-model choice is timed too and reported next to it. Like MIOpen's find-db, but for our
 own kernels. Strided dgrad problems (several phase GEMMs) are tuned as a whole and the winner is
@@ -111,31 +111,32 @@ def main():
                 if key in seen:
                     continue
                 seen.add(key)
-                n.conv_force_tile(0)
+                n.conv_force_tile(0, 0)
                 auto_us = timeit(lambda: fn(0))
-                best = (auto_us, None, None)
+                best = (auto_us, None, None, None)
                 M0, N0, K0 = gemms[0]
                 ksteps = (K0 + 63) // 64
                 for t in range(4):
-                    n.conv_force_tile(t + 1)
-                    for s in (1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64):
-                        if s > 1 and (ksteps // s < 2 or s * M0 * N0 > ws.numel()):
-                            continue
-                        us = timeit(lambda: fn(s))
-                        if us < best[0]:
-                            best = (us, t, s)
-                n.conv_force_tile(0)
-                us, t, s = best
+                    for nst in (2, 3, 4):
+                        n.conv_force_tile(t + 1, nst)
+                        for s in (1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64):
+                            if s > 1 and (ksteps // s < 2 or s * M0 * N0 > ws.numel()):
+                                continue
+                            us = timeit(lambda: fn(s))
+                            if us < best[0] * 0.99:  # ties keep the simpler (earlier) config
+                                best = (us, t, s, nst)
+                n.conv_force_tile(0, 0)
+                us, t, s, nst = best
                 names = ["fwd", "dgrad", "wgrad"]
                 if t is None:
                     print(f"{label:42s} {names[mode]:5s} auto {auto_us:7.1f} us (kept)", flush=True)
                     continue
                 saved_total += auto_us - us
                 print(f"{label:42s} {names[mode]:5s} auto {auto_us:7.1f} us -> {TILES[t]} "
-                      f"split {s:2d} {us:7.1f} us", flush=True)
+                      f"split {s:2d} stages {nst} {us:7.1f} us", flush=True)
                 for (M, Nn, Kk) in gemms:
                     entries.append({"mode": mode, "M": M, "N": Nn, "K": Kk, "tile": t,
-                                    "splits": s, "us": round(us, 2), "auto_us": round(auto_us, 2),
+                                    "splits": s, "stages": nst, "us": round(us, 2), "auto_us": round(auto_us, 2),
                                     "shape": label})
     out = args.out or TUNING_FILE
     with open(out, "w") as f:
