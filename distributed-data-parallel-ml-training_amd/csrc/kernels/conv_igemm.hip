@@ -468,6 +468,9 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
   const bool split = args.splits > 1;
   float* slab = split ? args.ws + (size_t)zs * args.Mg * args.Ng : nullptr;
   const int rl = lane & 15, cq = 4 * (lane >> 4);
+  float stat_s[TN][4], stat_ss[TN][4];
+  // the LDS operand ring is reused for the statistics hand-off: every wave must be done with it
+  if (MODE == MODE_FWD && !split && args.stats) __syncthreads();
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = col0 + wn * WTN + j * 16 + cq;
@@ -550,12 +553,32 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
           ss[t] += __shfl_xor(ss[t], m, kWave);
         }
       }
-      if (rl == 0 && cok) {
-        float* st = args.stats + (blockIdx.x % kStatRep) * 2 * args.Ng;  // spread contention
+      // wave row 1 parks its column sums in LDS slot [wn][j][lane>>4][8]; row 0 adds them
+      float* slot = reinterpret_cast<float*>(smem) + (((wn * TN + j) * 4 + (lane >> 4)) * 8);
+      if (wm == 1 && rl == 0) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          atomicAdd(st + col + t, s[t]);
-          atomicAdd(st + args.Ng + col + t, ss[t]);
+          slot[t] = s[t];
+          slot[4 + t] = ss[t];
+        }
+      }
+      stat_s[j][0] = s[0]; stat_s[j][1] = s[1]; stat_s[j][2] = s[2]; stat_s[j][3] = s[3];
+      stat_ss[j][0] = ss[0]; stat_ss[j][1] = ss[1]; stat_ss[j][2] = ss[2]; stat_ss[j][3] = ss[3];
+    }
+  }
+  if (MODE == MODE_FWD && !split && args.stats) {
+    __syncthreads();
+    if (wm == 0 && rl == 0) {
+      float* st = args.stats + (blockIdx.x % kStatRep) * 2 * args.Ng;  // spread contention
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = col0 + wn * WTN + j * 16 + cq;
+        if (col >= args.Ng) continue;
+        const float* slot = reinterpret_cast<const float*>(smem) + (((wn * TN + j) * 4 + (lane >> 4)) * 8);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          atomicAdd(st + col + t, stat_s[j][t] + slot[t]);
+          atomicAdd(st + args.Ng + col + t, stat_ss[j][t] + slot[4 + t]);
         }
       }
     }

@@ -22,6 +22,9 @@
 #include "common.h"
 #include "api.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace ddp_amd {
 
 namespace {
@@ -168,7 +171,9 @@ __global__ __launch_bounds__(256) void conv_smallk_fwd_kernel(SmallKArgs a) {
     }
   }
   if (!a.stats) return;
-  // reduce over the 16 pixel lanes of each group, one atomic per channel per wave
+  // reduce over the 16 pixel lanes of each group, then over the block's 4 waves through LDS:
+  // ONE atomic per channel per block (memory-side float atomics serialise per address; per-wave
+  // atomics cost this kernel more than its MFMA work: 38.6 vs 17.4 us with / without stats)
 #pragma unroll
   for (int j = 0; j < NT; ++j)
 #pragma unroll
@@ -178,22 +183,32 @@ __global__ __launch_bounds__(256) void conv_smallk_fwd_kernel(SmallKArgs a) {
         s1[j][v] += __shfl_xor(s1[j][v], m, kWave);
         s2[j][v] += __shfl_xor(s2[j][v], m, kWave);
       }
+  __shared__ float red[4][2][64];
+  const int wib = threadIdx.x >> 6;
   if (rl == 0) {
-    float* st = a.stats + (wave % kStatRep) * 2 * a.K;
 #pragma unroll
     for (int j = 0; j < NT; ++j)
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        atomicAdd(st + j * 16 + 4 * g + v, s1[j][v]);
-        atomicAdd(st + a.K + j * 16 + 4 * g + v, s2[j][v]);
+        red[wib][0][j * 16 + 4 * g + v] = s1[j][v];
+        red[wib][1][j * 16 + 4 * g + v] = s2[j][v];
       }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * a.K) {
+    const int k = threadIdx.x / a.K, c = threadIdx.x - k * a.K;
+    const float t = red[0][k][c] + red[1][k][c] + red[2][k][c] + red[3][k][c];
+    atomicAdd(a.stats + (blockIdx.x % kStatRep) * 2 * a.K + k * a.K + c, t);
   }
 }
 
+int kSmallkTilesPerWave = 8;
+
 template <int NT, int NKS>
 void launch_smallk(const SmallKArgs& a, hipStream_t st) {
-  // ~4 tiles per wave: enough waves to fill the chip, weight-register loads amortised
-  const int waves = (a.tiles + 3) / 4;
+  // ~TPW tiles per wave: enough waves to fill the chip, weight-register loads and the per-block
+  // statistics atomics amortised
+  const int waves = (a.tiles + kSmallkTilesPerWave - 1) / kSmallkTilesPerWave;
   const int blocks = (waves + 3) / 4;
   hipLaunchKernelGGL((conv_smallk_fwd_kernel<NT, NKS, (NKS <= 4)>), dim3(blocks), dim3(256), 0, st, a);
 }
@@ -207,6 +222,7 @@ using namespace ddp_amd;
 extern "C" int ddp_conv_fwd_smallk(const ConvGeom* g, const void* x, const void* wc,
                                    const float* bias, void* y, float* stats, hipStream_t st) {
   if (g->C != 8 || g->K % 16 || g->K > 64) return -1;
+  if (const char* e = std::getenv("DDP_AMD_SMALLK_TPW")) kSmallkTilesPerWave = std::max(1, std::atoi(e));
   const int taps = g->R * g->S;
   const int nks = (taps + 3) / 4;
   SmallKArgs a;
