@@ -31,6 +31,9 @@
 #include "common.h"
 #include "api.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace ddp_amd {
 
 enum { kSc = 0, kSh = 1, kMu = 2, kIs = 3, kK1 = 4, kK2 = 5 };  // coef table rows
@@ -444,6 +447,7 @@ static unsigned blocks_for(size_t items, size_t per_block) {
 // channels; worth it (one launch fewer) while that re-read traffic stays small.
 constexpr size_t kFoldBytes = 24u << 20;
 constexpr bool kFoldBwd = false;
+static size_t kBwdBlocks = 1024;  // target reduce-grid size (DDP_AMD_BN_BWD_BLOCKS overrides)
 
 template <bool POOL, int IPT>
 static void launch_fwd(const BnArgs& a, size_t items, hipStream_t st) {
@@ -497,6 +501,11 @@ static void launch_bwd(const BnArgs& a, size_t npix, int Gb, int chunks, hipStre
 // a.coef must hold the table written by the matching forward; a.sums ([kStatRep][2][C]) must be
 // zero on entry (per-step scratch, zeroed once per forward).
 extern "C" int ddp_bn_act_bwd(const BnArgs* args, hipStream_t st) {
+  static const bool init = [] {
+    if (const char* e = std::getenv("DDP_AMD_BN_BWD_BLOCKS")) kBwdBlocks = std::max(1, std::atoi(e));
+    return true;
+  }();
+  (void)init;
   BnArgs a = *args;
   if (a.C % 8 || a.coef == nullptr || a.sums == nullptr) return -1;
   if (a.pool && a.res) return -1;
@@ -506,13 +515,23 @@ extern "C" int ddp_bn_act_bwd(const BnArgs* args, hipStream_t st) {
   const int chunks = (G + Gb - 1) / Gb;
   const int Ho = a.pool ? a.H / 2 : a.H, Wo = a.pool ? a.W / 2 : a.W;
   const size_t npix = (size_t)a.N * Ho * Wo;
-  // one item per thread while that leaves few blocks; two (loads of both issued together) for
-  // the big layers. Pooled items already carry 4 pixels: one per thread keeps registers down.
-  const bool two = !a.pool && npix * chunks / (256 / Gb) >= 4096;
+  // Items per thread: enough to keep the reduce grid near kBwdBlocks blocks. Every reduce block
+  // adds one partial sum per channel into one of kStatRep replicas, and memory-side float atomics
+  // serialise per address: 2048 one-item blocks (VGG layer 0) put 128 adders on every address.
+  const size_t per1 = (size_t)(256 / Gb);  // items per block at one item per thread
+  const size_t blocks1 = (npix + per1 - 1) / per1 * chunks;
+  // Measured: VGG-11's layers (<= 2048 one-item blocks) are fastest at one item per thread;
+  // ResNet-50's 56x56 layers (6272 blocks) gain 0.7 ms/step from 4 items per thread.
+  int ipt = 1;
+  if (blocks1 > 2 * kBwdBlocks)
+    while (ipt < 4 && blocks1 / ipt > kBwdBlocks) ipt *= 2;
   if (a.pool) {
-    launch_bwd<true, 1>(a, npix, Gb, chunks, st);
+    if (ipt >= 4) launch_bwd<true, 4>(a, npix, Gb, chunks, st);
+    else if (ipt == 2) launch_bwd<true, 2>(a, npix, Gb, chunks, st);
+    else launch_bwd<true, 1>(a, npix, Gb, chunks, st);
   } else {
-    if (two) launch_bwd<false, 2>(a, npix, Gb, chunks, st);
+    if (ipt >= 4) launch_bwd<false, 4>(a, npix, Gb, chunks, st);
+    else if (ipt == 2) launch_bwd<false, 2>(a, npix, Gb, chunks, st);
     else launch_bwd<false, 1>(a, npix, Gb, chunks, st);
   }
   return (int)hipGetLastError();
