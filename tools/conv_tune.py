@@ -5,7 +5,7 @@ write the winners to the launcher's tuning table (ops/conv_tuning.json).
     python tools/conv_tune.py [--out PATH] [--reps 30] [--quick]
 
 Shapes: VGG-11 at per-GPU batch 256/128/64/32 (weak scaling and the reference's strong-scaling
-split of 256 over 1/2/4/8 GPUs) and ResNet-50 at 64. For each GEMM problem (mode, M, N, K) every
+split of 256 over 1/2/4/8 GPUs) and ResNet-50 at 64 and 256. For each GEMM problem (mode, M, N, K) every
 tile (128x128, 128x64, 64x128, 64x64) x LDS ring depth (2-4 stages) x split-K factor is launched exactly as the training step
 launches it (same kernels, same finish passes), timed with HIP events, and the fastest is kept;
 the cost-model choice is timed too and reported next to it. Like MIOpen's find-db, but for our
@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--quick", action="store_true", help="VGG-11 b256 only")
+    ap.add_argument("--sets", default="all", choices=["all", "resnet256"])
+    ap.add_argument("--merge", default=None, help="existing table to extend (entries kept)")
     args = ap.parse_args()
     import torch
     import ddp_amd  # noqa: F401
@@ -60,8 +62,11 @@ def main():
     dev = torch.device("cuda", 0)
     ws = workspace(dev)
     st = torch.cuda.current_stream().cuda_stream
-    sets = [("vgg11", 256)] if args.quick else [("vgg11", 256), ("vgg11", 128), ("vgg11", 64),
-                                                ("vgg11", 32), ("resnet50", 64)]
+    ap_sets = {"quick": [("vgg11", 256)],
+               "resnet256": [("resnet50", 256)],
+               "all": [("vgg11", 256), ("vgg11", 128), ("vgg11", 64), ("vgg11", 32),
+                       ("resnet50", 64), ("resnet50", 256)]}
+    sets = ap_sets["quick" if args.quick else args.sets]
     entries, seen = [], set()
     saved_total = 0.0
 
@@ -138,6 +143,11 @@ def main():
                     entries.append({"mode": mode, "M": M, "N": Nn, "K": Kk, "tile": t,
                                     "splits": s, "stages": nst, "us": round(us, 2), "auto_us": round(auto_us, 2),
                                     "shape": label})
+    if args.merge and os.path.exists(args.merge):
+        with open(args.merge) as f:
+            old = json.load(f)["entries"]
+        have = {(e["mode"], e["M"], e["N"], e["K"]) for e in entries}
+        entries = [e for e in old if (e["mode"], e["M"], e["N"], e["K"]) not in have] + entries
     out = args.out or TUNING_FILE
     with open(out, "w") as f:
         json.dump({"device": torch.cuda.get_device_name(0), "reps": args.reps,
