@@ -60,13 +60,30 @@ PYBIND11_MODULE(_native, m) {
     if (rc > 0) check(rc, "conv_fwd_smallk");
     return rc == 0;
   });
+  // bn: optional (z, coef, sums, pool, relu, Hz, Wz) of the preceding Conv->BN->ReLU(->pool)
+  // block whose BatchNorm-backward sums the dgrad epilogue accumulates (api.h BnBwdFuse)
   m.def("conv_dgrad", [](py::tuple g, uintptr_t dy, uintptr_t wt, uintptr_t dx, uintptr_t ws,
-                         size_t ws_elems, int splits, uintptr_t st, int accumulate) {
+                         size_t ws_elems, int splits, uintptr_t st, int accumulate, py::object bn) {
     auto c = geom(g);
-    check(ddp_conv_dgrad(&c, P<void>(dy), P<void>(wt), P<void>(dx), P<float>(ws), ws_elems,
-                         splits, accumulate, S(st)), "conv_dgrad");
+    if (bn.is_none()) {
+      check(ddp_conv_dgrad(&c, P<void>(dy), P<void>(wt), P<void>(dx), P<float>(ws), ws_elems,
+                           splits, accumulate, S(st)), "conv_dgrad");
+      return;
+    }
+    auto t = bn.cast<py::tuple>();
+    ddp_amd::BnBwdFuse f{};
+    f.z = P<unsigned short>(t[0].cast<uintptr_t>());
+    f.coef = P<float>(t[1].cast<uintptr_t>());
+    f.sums = P<float>(t[2].cast<uintptr_t>());
+    f.pool = t[3].cast<int>();
+    f.relu = t[4].cast<int>();
+    f.Hz = t[5].cast<int>();
+    f.Wz = t[6].cast<int>();
+    check(ddp_conv_dgrad_bn(&c, P<void>(dy), P<void>(wt), P<void>(dx), P<float>(ws), ws_elems,
+                            splits, &f, S(st)), "conv_dgrad_bn");
   }, py::arg("g"), py::arg("dy"), py::arg("wt"), py::arg("dx"), py::arg("ws"),
-     py::arg("ws_elems"), py::arg("splits"), py::arg("stream"), py::arg("accumulate") = 0);
+     py::arg("ws_elems"), py::arg("splits"), py::arg("stream"), py::arg("accumulate") = 0,
+     py::arg("bn") = py::none());
   m.def("conv_wgrad", [](py::tuple g, uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws,
                          size_t ws_elems, int splits, uintptr_t st) {
     auto c = geom(g);
@@ -114,10 +131,11 @@ PYBIND11_MODULE(_native, m) {
                          uintptr_t res, uintptr_t stats, uintptr_t gamma, uintptr_t beta,
                          uintptr_t dout, uintptr_t sums, uintptr_t dz, uintptr_t dres,
                          uintptr_t dgamma, uintptr_t dbeta, uintptr_t dbias, uintptr_t st,
-                         uintptr_t coef, uintptr_t counter) {
+                         uintptr_t coef, uintptr_t counter, int sums_ready) {
     ddp_amd::BnArgs a{};
     a.coef = P<float>(coef);
     a.counter = P<int>(counter);
+    a.sums_ready = sums_ready;
     a.N = N; a.H = H; a.W = W; a.C = C; a.pool = pool; a.relu = relu; a.eps = eps;
     a.z = P<unsigned short>(z); a.res = P<unsigned short>(res); a.stats = P<float>(stats);
     a.gamma = P<float>(gamma); a.beta = P<float>(beta); a.dout = P<unsigned short>(dout);
@@ -128,7 +146,7 @@ PYBIND11_MODULE(_native, m) {
      py::arg("eps"), py::arg("z"), py::arg("res"), py::arg("stats"), py::arg("gamma"),
      py::arg("beta"), py::arg("dout"), py::arg("sums"), py::arg("dz"), py::arg("dres"),
      py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("stream"), py::arg("coef"),
-     py::arg("counter") = 0);
+     py::arg("counter") = 0, py::arg("sums_ready") = 0);
 
   m.def("linear_ce_fwd", [](uintptr_t x, uintptr_t W, uintptr_t b, uintptr_t labels, int B, int F,
                             int J, uintptr_t logits, uintptr_t dlogits, uintptr_t loss_sum,

@@ -46,6 +46,21 @@ struct BnArgs {
                                 // backward reads the table its forward wrote
   int* counter;                 // backward: zeroed ticket counter -> the reduce kernel's last
                                 // block finalizes k1/k2, dgamma, dbeta (no finalize launch)
+  int sums_ready;               // backward: sums already accumulated (BnBwdFuse in the next
+                                // layer's dgrad) -> finalize + apply only
+};
+
+// BatchNorm-backward statistics fused into a conv dgrad: the dgrad output IS the gradient at the
+// output of the preceding Conv->BN->ReLU(->2x2 max-pool) block, so its epilogue can accumulate
+// that block's backward sums S1 = sum dy_bn, S2 = sum dy_bn * xhat (recomputing the ReLU mask /
+// pool routing from the block's conv output z) — the block's BN backward then skips its reduce
+// pass (BnArgs::sums_ready).
+struct BnBwdFuse {
+  const unsigned short* z;  // preceding block's conv output [N][Hz][Wz][C] (bf16, pre-pool)
+  const float* coef;        // its coefficient table [6][C] (scale, shift, mean, invstd, ..)
+  float* sums;              // its backward sums [kStatRep][2][C] (zeroed per forward)
+  int pool, relu;           // 2x2/s2 max-pool between z and the dgrad output; ReLU
+  int Hz, Wz;               // z spatial dims (2x the dgrad output's when pooled)
 };
 
 struct PackDesc {
@@ -75,6 +90,9 @@ int ddp_conv_fwd(const ddp_amd::ConvGeom* g, const void* x, const void* wc, cons
                  void* y, float* stats, float* ws, size_t ws_elems, int splits, hipStream_t st);
 int ddp_conv_dgrad(const ddp_amd::ConvGeom* g, const void* dy, const void* wt, void* dx,
                    float* ws, size_t ws_elems, int splits, int accumulate, hipStream_t st);
+int ddp_conv_dgrad_bn(const ddp_amd::ConvGeom* g, const void* dy, const void* wt, void* dx,
+                      float* ws, size_t ws_elems, int splits, const ddp_amd::BnBwdFuse* bn,
+                      hipStream_t st);
 int ddp_conv_wgrad(const ddp_amd::ConvGeom* g, const void* dy, const void* x, float* dw,
                    float* ws, size_t ws_elems, int splits, hipStream_t st);
 int ddp_bn_act_fwd(const ddp_amd::BnArgs* a, hipStream_t st);

@@ -482,12 +482,13 @@ extern "C" int ddp_bn_act_fwd(const BnArgs* args, hipStream_t st) {
 template <bool POOL, int IPT>
 static void launch_bwd(const BnArgs& a, size_t npix, int Gb, int chunks, hipStream_t st) {
   const unsigned bx = blocks_for(npix, (size_t)(256 / Gb) * IPT);
-  hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<POOL, IPT>), dim3(bx, chunks), dim3(256), 0, st, a);
+  if (!a.sums_ready)  // (else: accumulated by the next layer's dgrad epilogue, BnBwdFuse)
+    hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<POOL, IPT>), dim3(bx, chunks), dim3(256), 0, st, a);
   // (measured: folding the backward finalize made the apply 3-4x slower — the replicated sums
   // were just written by memory-side atomics and every block re-reads them uncached — so the
   // backward keeps its separate finalize launch)
   const size_t nch = (size_t)Gb * 8;
-  if (a.counter) {  // finalized by the reduce kernel's last block
+  if (a.counter && !a.sums_ready) {  // finalized by the reduce kernel's last block
     hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT, false>), dim3(bx, chunks), dim3(256), 0, st, a);
   } else if (kFoldBwd && (size_t)bx * chunks * nch * 2 * kStatRep * sizeof(float) <= kFoldBytes) {
     hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT, true>), dim3(bx, chunks), dim3(256),

@@ -79,6 +79,8 @@ struct ConvArgs {
   int accumulate;            // DGRAD: dx = bf16(dx + result) (merges a second gradient branch)
   int a_bytes, b_bytes;      // operand sizes: buffer-resource bounds (reads past them give 0)
   FastDiv dPQ, dQ;           // WGRAD pixel decomposition
+  int has_bnf;               // DGRAD (stride 1, no accumulate): accumulate the preceding
+  BnBwdFuse bnf;             //   block's BatchNorm-backward sums in the epilogue (api.h)
 };
 
 // ------------------------------------------------------------------ operand gathers
@@ -174,7 +176,9 @@ __device__ __forceinline__ void wait_dma_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-template <int MODE, int BM, int BN, int NST>
+// BNF (DGRAD only): the epilogue also accumulates the preceding block's BatchNorm-backward sums
+// (ConvArgs::bnf) — a separate instantiation so the plain kernels keep their register budget
+template <int MODE, int BM, int BN, int NST, bool BNF = false>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
   constexpr int BK = 64;
   constexpr int WTM = BM / 2, WTN = BN / 2;
@@ -469,8 +473,12 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
   float* slab = split ? args.ws + (size_t)zs * args.Mg * args.Ng : nullptr;
   const int rl = lane & 15, cq = 4 * (lane >> 4);
   float stat_s[TN][4], stat_ss[TN][4];
+  // per-channel sums reduced in the epilogue: FWD = BatchNorm statistics of the output, DGRAD with
+  // a BnBwdFuse = the preceding block's BatchNorm-backward sums
+  const bool red = (MODE == MODE_FWD && !split && args.stats != nullptr) ||
+                   (MODE == MODE_DGRAD && BNF && !split);
   // the LDS operand ring is reused for the statistics hand-off: every wave must be done with it
-  if (MODE == MODE_FWD && !split && args.stats) __syncthreads();
+  if (red) __syncthreads();
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = col0 + wn * WTN + j * 16 + cq;
@@ -479,6 +487,14 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
     if (MODE == MODE_FWD && !split && args.bias && cok)
       bias = (float4){args.bias[col], args.bias[col + 1], args.bias[col + 2], args.bias[col + 3]};
     float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
+    float4 bsc = {0.f, 0.f, 0.f, 0.f}, bsh = bsc, bmu = bsc, bis = bsc;
+    if (MODE == MODE_DGRAD && BNF && red && cok) {  // coefficients of the 4 channels (coef [6][C])
+      const float* cf = args.bnf.coef;
+      bsc = *reinterpret_cast<const float4*>(cf + 0 * args.Ng + col);
+      bsh = *reinterpret_cast<const float4*>(cf + 1 * args.Ng + col);
+      bmu = *reinterpret_cast<const float4*>(cf + 2 * args.Ng + col);
+      bis = *reinterpret_cast<const float4*>(cf + 3 * args.Ng + col);
+    }
     int wrs = 0, wc = 0;
     if (MODE == MODE_WGRAD) {  // GEMM column -> (r*S + s, c); c..c+3 share the tap
       wrs = col / g.C;
@@ -541,9 +557,48 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
           s[0] += r0; s[1] += r1; s[2] += r2; s[3] += r3;
           ss[0] += r0 * r0; ss[1] += r1 * r1; ss[2] += r2 * r2; ss[3] += r3 * r3;
         }
+        if (MODE == MODE_DGRAD && BNF && red) {
+          // this row is pixel (n, h, w) of the preceding block's output; its gradient (as
+          // stored, bf16-rounded) flows to the window argmax of relu(bn(z)) (pool) and through
+          // the ReLU mask: dy_bn; S1 += dy_bn, S2 += dy_bn * xhat — bn_act.hip bwd_compute
+          const float gv[4] = {bf2f(h0), bf2f(h1), bf2f(h2), bf2f(h3)};
+          const float fsc[4] = {bsc.x, bsc.y, bsc.z, bsc.w}, fsh[4] = {bsh.x, bsh.y, bsh.z, bsh.w};
+          const float fmu[4] = {bmu.x, bmu.y, bmu.z, bmu.w}, fis[4] = {bis.x, bis.y, bis.z, bis.w};
+          const BnBwdFuse& f = args.bnf;
+          const int hw = g.H * g.W;
+          const int n = (int)orow / hw, rem = (int)orow - n * hw;
+          const int h = rem / g.W, w = rem - h * g.W;
+          const int np = f.pool ? 4 : 1;
+          float zf[4][4];
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {
+            if (d >= np) break;
+            const int zh = f.pool ? 2 * h + (d >> 1) : h, zw = f.pool ? 2 * w + (d & 1) : w;
+            const uint2 zz = *reinterpret_cast<const uint2*>(
+                f.z + (((size_t)n * f.Hz + zh) * f.Wz + zw) * args.Ng + col);
+            zf[d][0] = bf2f((unsigned short)(zz.x & 0xffff));
+            zf[d][1] = bf2f((unsigned short)(zz.x >> 16));
+            zf[d][2] = bf2f((unsigned short)(zz.y & 0xffff));
+            zf[d][3] = bf2f((unsigned short)(zz.y >> 16));
+          }
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            float best = -INFINITY, yarg = 0.f, zarg = 0.f;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+              if (d >= np) break;
+              const float y = zf[d][t] * fsc[t] + fsh[t];
+              const float yr = f.relu ? fmaxf(y, 0.f) : y;
+              if (d == 0 || yr > best || yr != yr) { best = yr; yarg = y; zarg = zf[d][t]; }
+            }
+            const float dyb = (f.relu && !(yarg > 0.f)) ? 0.f : gv[t];
+            s[t] += dyb;
+            ss[t] += dyb * ((zarg - fmu[t]) * fis[t]);
+          }
+        }
       }
     }
-    if (MODE == MODE_FWD && !split && args.stats) {
+    if (red) {
       // reduce over the 16 rows held by lanes (lane & 15) of each 16-lane group
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -566,10 +621,11 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
       stat_ss[j][0] = ss[0]; stat_ss[j][1] = ss[1]; stat_ss[j][2] = ss[2]; stat_ss[j][3] = ss[3];
     }
   }
-  if (MODE == MODE_FWD && !split && args.stats) {
+  if (red) {
     __syncthreads();
     if (wm == 0 && rl == 0) {
-      float* st = args.stats + (blockIdx.x % kStatRep) * 2 * args.Ng;  // spread contention
+      float* st = (MODE == MODE_FWD ? args.stats : args.bnf.sums) +
+                  (blockIdx.x % kStatRep) * 2 * args.Ng;  // spread contention
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int col = col0 + wn * WTN + j * 16 + cq;
@@ -630,11 +686,14 @@ __device__ __forceinline__ size_t map_row(const RowMap& m, int row) {
   return ((size_t)n * m.H + m.pa + m.stride * i) * m.W + m.pb + m.stride * j;
 }
 
+template <bool BNF>
 __global__ __launch_bounds__(256) void splitk_finish_kernel(const float* ws, int splits,
                                                             unsigned short* out,
                                                             const float* bias, float* stats,
                                                             int Mg, int Ng, RowMap rmap,
-                                                            int accumulate) {
+                                                            int accumulate, BnBwdFuse bnf,
+                                                            int H, int W) {
+  constexpr bool has_bnf = BNF;
   __shared__ float red[2][8][256];
   const int G = Ng / 8;
   const int Gb = G < 256 ? G : 256;
@@ -643,11 +702,23 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(const float* ws, int
   const bool active = prow < prows && cg < G;  // Gb need not divide 256 (e.g. 1000 classes)
   const size_t slab = (size_t)Mg * Ng;
   float s[8], ss[8], bv[8];
+  float fsc[8], fsh[8], fmu[8], fis[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     s[e] = 0.f;
     ss[e] = 0.f;
     bv[e] = (bias && cg < G) ? bias[cg * 8 + e] : 0.f;
+    fsc[e] = fsh[e] = fmu[e] = fis[e] = 0.f;
+  }
+  if (has_bnf && cg < G) {  // DGRAD with the preceding block's BN-backward sums (BnBwdFuse)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      fsc[e] = bnf.coef[0 * Ng + cg * 8 + e];
+      fsh[e] = bnf.coef[1 * Ng + cg * 8 + e];
+      fmu[e] = bnf.coef[2 * Ng + cg * 8 + e];
+      fis[e] = bnf.coef[3 * Ng + cg * 8 + e];
+    }
+    stats = bnf.sums;
   }
   for (int row = blockIdx.x * prows + prow; active && row < Mg; row += gridDim.x * prows) {
     float v[8];
@@ -670,10 +741,38 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(const float* ws, int
     for (int e = 0; e < 8; ++e) {
       o[e] = f2bf(v[e]);
       const float r = bf2f(o[e]);
-      s[e] += r;
-      ss[e] += r * r;
+      if (!has_bnf) {
+        s[e] += r;
+        ss[e] += r * r;
+      }
     }
     st8(dst, o);
+    if (has_bnf) {  // same recomputation as the GEMM epilogue / bn_act.hip bwd_compute
+      const int hw = H * W;
+      const int n = row / hw, rem = row - n * hw;
+      const int h = rem / W, w = rem - h * W;
+      const int np = bnf.pool ? 4 : 1;
+      float best[8], yarg[8], zarg[8];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        if (d >= np) break;
+        const int zh = bnf.pool ? 2 * h + (d >> 1) : h, zw = bnf.pool ? 2 * w + (d & 1) : w;
+        const u16x8 zz = ld8(bnf.z + (((size_t)n * bnf.Hz + zh) * bnf.Wz + zw) * Ng + cg * 8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float zf = bf2f(zz[e]);
+          const float y = zf * fsc[e] + fsh[e];
+          const float yr = bnf.relu ? fmaxf(y, 0.f) : y;
+          if (d == 0 || yr > best[e] || yr != yr) { best[e] = yr; yarg[e] = y; zarg[e] = zf; }
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float dyb = (bnf.relu && !(yarg[e] > 0.f)) ? 0.f : bf2f(o[e]);
+        s[e] += dyb;
+        ss[e] += dyb * ((zarg[e] - fmu[e]) * fis[e]);
+      }
+    }
   }
   if (!stats) return;
 #pragma unroll
@@ -837,18 +936,26 @@ static int stages_for(int BM, int BN) {
   return 3;
 }
 
-template <int MODE, int BM, int BN, int NST>
-static void launch_gemm(const ConvArgs& a, int items, hipStream_t st) {
+template <int MODE, int BM, int BN, int NST, bool BNF>
+static void launch_gemm_t(const ConvArgs& a, int items, hipStream_t st) {
   // persistent grid: at most the resident workgroup slots (queried once per instantiation)
   static int resident = 0;
   if (resident == 0) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, conv_igemm_kernel<MODE, BM, BN, NST>, 256, 0) != hipSuccess || nb < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, conv_igemm_kernel<MODE, BM, BN, NST, BNF>, 256, 0) != hipSuccess || nb < 1)
       nb = 1;
     resident = nb;
   }
   const int grid = g_persistent ? std::min(items, kNumCUs * resident) : items;
-  hipLaunchKernelGGL((conv_igemm_kernel<MODE, BM, BN, NST>), dim3(grid), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((conv_igemm_kernel<MODE, BM, BN, NST, BNF>), dim3(grid), dim3(256), 0, st, a);
+}
+
+template <int MODE, int BM, int BN, int NST>
+static void launch_gemm(const ConvArgs& a, int items, hipStream_t st) {
+  if constexpr (MODE == MODE_DGRAD) {
+    if (a.has_bnf && a.splits <= 1) return launch_gemm_t<MODE, BM, BN, NST, true>(a, items, st);
+  }
+  launch_gemm_t<MODE, BM, BN, NST, false>(a, items, st);
 }
 
 template <int MODE, int BM, int BN>
@@ -891,9 +998,15 @@ static void launch_cfg(ConvArgs& a, int splits, hipStream_t st, int nst_req = 0)
     bx = std::max(1, std::min(bx, 2048 / chunks + 1));
     RowMap rm{0, 0, 0, 0, 0, 0, 0};
     if (a.phase) rm = RowMap{a.g.stride, a.Hp, a.Wp, a.g.H, a.g.W, a.pa, a.pb};
-    hipLaunchKernelGGL(splitk_finish_kernel, dim3(bx, chunks), dim3(256), 0, st, a.ws, splits,
-                       a.out, MODE == MODE_FWD ? a.bias : nullptr,
-                       MODE == MODE_FWD ? a.stats : nullptr, a.Mg, a.Ng, rm, a.accumulate);
+    if (MODE == MODE_DGRAD && a.has_bnf)
+      hipLaunchKernelGGL(splitk_finish_kernel<true>, dim3(bx, chunks), dim3(256), 0, st, a.ws,
+                         splits, a.out, nullptr, nullptr, a.Mg, a.Ng, rm, a.accumulate, a.bnf,
+                         a.g.H, a.g.W);
+    else
+      hipLaunchKernelGGL(splitk_finish_kernel<false>, dim3(bx, chunks), dim3(256), 0, st, a.ws,
+                         splits, a.out, MODE == MODE_FWD ? a.bias : nullptr,
+                         MODE == MODE_FWD ? a.stats : nullptr, a.Mg, a.Ng, rm, a.accumulate,
+                         a.bnf, a.g.H, a.g.W);
   }
 }
 
@@ -988,12 +1101,17 @@ extern "C" int ddp_conv_fwd(const ConvGeom* g, const void* x, const void* wc, co
   return (int)hipGetLastError();
 }
 
-extern "C" int ddp_conv_dgrad(const ConvGeom* g, const void* dy, const void* wc, void* dx,
-                              float* ws, size_t ws_elems, int splits, int accumulate,
-                              hipStream_t st) {
+static int conv_dgrad_impl(const ConvGeom* g, const void* dy, const void* wc, void* dx,
+                           float* ws, size_t ws_elems, int splits, int accumulate,
+                           const BnBwdFuse* bn, hipStream_t st) {
   if (g->C % 8 || g->K % 8) return -1;
+  if (bn && (accumulate || g->stride != 1)) return -3;  // fused BN sums: plain stride-1 dgrad only
   ConvArgs a{};
   a.accumulate = accumulate;
+  if (bn) {
+    a.has_bnf = 1;
+    a.bnf = *bn;
+  }
   a.g = *g;
   a.a = (const unsigned short*)dy;
   a.b = (const unsigned short*)wc;
@@ -1045,6 +1163,18 @@ extern "C" int ddp_conv_dgrad(const ConvGeom* g, const void* dy, const void* wc,
     }
   }
   return (int)hipGetLastError();
+}
+
+extern "C" int ddp_conv_dgrad(const ConvGeom* g, const void* dy, const void* wc, void* dx,
+                              float* ws, size_t ws_elems, int splits, int accumulate,
+                              hipStream_t st) {
+  return conv_dgrad_impl(g, dy, wc, dx, ws, ws_elems, splits, accumulate, nullptr, st);
+}
+
+extern "C" int ddp_conv_dgrad_bn(const ConvGeom* g, const void* dy, const void* wc, void* dx,
+                                 float* ws, size_t ws_elems, int splits, const BnBwdFuse* bn,
+                                 hipStream_t st) {
+  return conv_dgrad_impl(g, dy, wc, dx, ws, ws_elems, splits, 0, bn, st);
 }
 
 extern "C" int ddp_conv_wgrad(const ConvGeom* g, const void* dy, const void* x, float* dw,

@@ -70,6 +70,9 @@ class _VGG(nn.Module):
             pool = i + 3 < len(mods) and isinstance(mods[i + 3], nn.MaxPool2d)
             spec = ConvBNActSpec(conv, bn, relu=True, pool=pool,
                                  cin_pad=IN_CHANNELS_PADDED if first else None)
+            # this block's dgrad produces the gradient at the previous block's output: it
+            # accumulates that block's BatchNorm-backward sums (ops.layers, BnBwdFuse)
+            spec.prev = stages[-1] if stages else None
             stages.append(spec)
             first = False
             i += 4 if pool else 3

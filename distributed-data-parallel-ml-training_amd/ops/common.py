@@ -160,6 +160,12 @@ def join_side_streams():
 BN_LAST_BLOCK = os.environ.get("DDP_AMD_BN_LAST_BLOCK", "0") == "1"
 
 
+# BatchNorm-backward sums of a Conv->BN->ReLU(->pool) block accumulated by the NEXT block's
+# dgrad epilogue (BnBwdFuse, conv_igemm.hip): the block's backward skips its reduce pass.
+# DDP_AMD_BN_BWD_FUSE=0 restores the separate reduce kernel.
+BN_BWD_FUSE = os.environ.get("DDP_AMD_BN_BWD_FUSE", "1") != "0"
+
+
 # ---------------------------------------------------------------- per-step accumulator scratch
 # Every fused layer owns fixed slices of one persistent fp32 buffer for the accumulators that
 # must start at zero each step (BatchNorm statistics replicas, BN-backward sums). The model's

@@ -60,6 +60,12 @@ class ConvBNActSpec:
         # per-layer BN coefficient table [6][K] (scale, shift, mean, invstd | k1, k2): written
         # by the forward's finalize kernel, read by the backward (one use per step per layer)
         self.coef = torch.empty(6 * K, dtype=F32, device=dev)
+        # BnBwdFuse chaining (VGG): ``prev`` is the Conv->BN->ReLU(->pool) block that produces
+        # this block's input; this block's dgrad accumulates prev's BatchNorm-backward sums in
+        # its epilogue and sets ``prev.sums_ready`` so prev's backward skips its reduce pass
+        self.prev = None
+        self.fwd_z = None
+        self.sums_ready = False
 
     def pack_desc(self):
         w = self.conv.weight
@@ -132,7 +138,19 @@ class GradLink:
         return out
 
 
-def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None):
+BN_BWD_FUSE_MAX_ELEMS = 1 << 21
+
+
+def bn_bwd_fuse_pays(dx_numel):
+    """Fuse the preceding block's BatchNorm-backward sums into this dgrad only for small dgrad
+    outputs. Measured (VGG-11 b256, tools/conv_tune.py): on the 4x4 / 2x2 layers the fused
+    epilogue costs 2-5 us less than the reduce kernel it replaces; on the 16x16 / 8x8 layers
+    its per-tile z gather (exposed after the MFMA loop) costs 10-15 us MORE than the streaming
+    reduce kernel."""
+    return dx_numel <= BN_BWD_FUSE_MAX_ELEMS
+
+
+def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=None):
     """dW += wgrad(dz, x); returns dx (or None). With ``weight`` (the parameter whose gradient
     is dweight) and the backward side stream enabled, the wgrad runs on the side stream and the
     parameter is announced ready there (common.side_stream); otherwise everything is stream-
@@ -162,7 +180,7 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None):
         link.seen += 1
         return link.result()
     dx = torch.empty_like(x)
-    native().conv_dgrad(g, ptr(dz), ptr(spec.wc), ptr(dx), ptr(ws), ws.numel(), 0, s)
+    native().conv_dgrad(g, ptr(dz), ptr(spec.wc), ptr(dx), ptr(ws), ws.numel(), 0, s, bn=bnf)
     if link is not None:
         link.seen += 1
         link.buf = dx
@@ -196,6 +214,9 @@ class _ConvBNActFn(torch.autograd.Function):
         ctx.spec = spec
         ctx.has_res = residual is not None
         ctx.in_link, ctx.res_link = in_link, res_link
+        spec.fwd_z = z
+        # the preceding block's conv output of THIS forward (for the fused BN-backward sums)
+        ctx.prev_z = spec.prev.fwd_z if spec.prev is not None else None
         ctx.save_for_backward(x, z, stats, weight, bias, gamma, beta, residual)
         return y
 
@@ -212,14 +233,29 @@ class _ConvBNActFn(torch.autograd.Function):
         gb = ensure_grad(bias) if bias is not None else None
         gg = ensure_grad(gamma)
         gbt = ensure_grad(beta)
+        sums_ready, spec.sums_ready = spec.sums_ready, False
+        spec.fwd_z = None
         native().bn_act_bwd(N, P, Q, K, int(spec.pool), int(spec.relu), spec.eps, ptr(z),
                             ptr(residual), ptr(stats), ptr(gamma), ptr(beta), ptr(dy), ptr(sums),
                             ptr(dz), ptr(dres), ptr(gg), ptr(gbt), ptr(gb), stream_handle(),
-                            ptr(spec.coef), ptr(spec.bwd_counter) if _common.BN_LAST_BLOCK else 0)
+                            ptr(spec.coef), ptr(spec.bwd_counter) if _common.BN_LAST_BLOCK else 0,
+                            sums_ready=int(sums_ready))
         grad_ready([gamma, beta, bias])
         if ctx.res_link is not None and dres is not None:
             dres = ctx.res_link.offer(dres)
-        dx = conv_backward(spec, x, dz, gw, ctx.needs_input_grad[0], ctx.in_link, weight=weight)
+        bnf = None
+        prev = spec.prev
+        if (_common.BN_BWD_FUSE and prev is not None and ctx.prev_z is not None
+                and ctx.needs_input_grad[0] and ctx.in_link is None and spec.stride == 1
+                and not prev.residual and prev.K == spec.C and spec.C == spec.Cr
+                and bn_bwd_fuse_pays(x.numel())):
+            pz = ctx.prev_z
+            bnf = (ptr(pz), ptr(prev.coef), ptr(prev.sums), int(prev.pool), int(prev.relu),
+                   pz.shape[1], pz.shape[2])
+            prev.sums_ready = True
+        dx = conv_backward(spec, x, dz, gw, ctx.needs_input_grad[0], ctx.in_link, weight=weight,
+                           bnf=bnf)
+        ctx.prev_z = None
         return dx, None, None, None, None, dres, None, None, None
 
 

@@ -54,7 +54,7 @@ def main():
     import ddp_amd  # noqa: F401
     from ddp_amd.ops import common
     from ddp_amd.ops.common import native, ptr, workspace, TUNING_FILE
-    from ddp_amd.ops.layers import ConvBNActSpec
+    from ddp_amd.ops.layers import ConvBNActSpec, bn_bwd_fuse_pays
     from conv_bench import vgg_layers, resnet_layers
 
     n = native()
@@ -84,7 +84,20 @@ def main():
 
     for model, B in sets:
         layers = vgg_layers(B) if model == "vgg11" else resnet_layers(B)
+        prev_hw = None
         for (N, C, H, W, K, R, stride, pad, Cr) in layers:
+            # VGG training dgrads carry the preceding block's fused BatchNorm-backward sums
+            # (ops.layers BnBwdFuse): tune that variant. prev block's z is 2x larger if pooled.
+            bn = None
+            if (model == "vgg11" and prev_hw is not None and C == Cr
+                    and bn_bwd_fuse_pays(N * H * W * C)):
+                zh = prev_hw
+                pz = torch.randn(N, zh, zh, C, device=dev).to(torch.bfloat16)
+                pcoef = torch.rand(6 * C, device=dev)
+                psums = torch.zeros(16 * 2 * C, device=dev)
+                _keep = (pz, pcoef, psums)  # noqa: F841  (alive while timed)
+                bn = (ptr(pz), ptr(pcoef), ptr(psums), int(zh != H), 1, zh, zh)
+            prev_hw = H if model == "vgg11" else None
             conv = torch.nn.Conv2d(Cr, K, R, stride, pad, bias=False).to(dev)
             conv.weight.data = conv.weight.data.contiguous(memory_format=torch.channels_last)
             spec = ConvBNActSpec(conv, None, cin_pad=C if C != Cr else None)
@@ -106,7 +119,7 @@ def main():
             if C == Cr:
                 probs.append((1, [(m, C, k) for m, k in dgrad_phases(N, H, W, K, R, R, stride, pad)],
                               lambda s: n.conv_dgrad(g, ptr(dz), ptr(spec.wc), ptr(dx), ptr(ws),
-                                                     ws.numel(), s, st)))
+                                                     ws.numel(), s, st, bn=bn)))
             probs.append((2, [(K, R * R * C, N * P * P)],
                           lambda s: n.conv_wgrad(gw, ptr(dz), ptr(x), ptr(dw), ptr(ws), ws.numel(),
                                                  s, st)))
