@@ -11,6 +11,8 @@ reducer can launch bucket all-reduces while the rest of the backward is still ru
 Reference parity: part1/model.py:11-27 (the Sequential it fuses) and SURVEY.md §2.D kernel list.
 Activations between blocks are NHWC bf16; the first conv's input is zero-padded 3 -> 8 channels.
 """
+import os
+
 import torch
 
 from .common import (native, ptr, stream_handle, check, grad_ready, ensure_grad, workspace,
@@ -138,7 +140,7 @@ class GradLink:
         return out
 
 
-BN_BWD_FUSE_MAX_ELEMS = 1 << 21
+BN_BWD_FUSE_MAX_ELEMS = int(os.environ.get("DDP_AMD_BN_BWD_FUSE_MAX", str(1 << 21)))
 
 
 def bn_bwd_fuse_pays(dx_numel):
