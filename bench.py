@@ -48,6 +48,9 @@ def parse():
     # is 25 MB (+1 MB first bucket); pass --bucket-mb 25 --first-bucket-mb 1 for that plan.
     p.add_argument("--bucket-mb", type=float, default=256.0)
     p.add_argument("--first-bucket-mb", type=float, default=256.0)
+    p.add_argument("--grad-comm", default="fp32", choices=["fp32", "bf16"],
+                   help="DDP gradient all-reduce dtype (bf16 halves the xGMI bytes; default "
+                        "fp32 = the reference's gradient precision)")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--train-size", type=int, default=None)
     p.add_argument("--json-out", default=None)
@@ -96,7 +99,8 @@ def main():
     sync = None
     if args.strategy == "ddp":
         model = DistributedDataParallel(model, comm, bucket_cap_mb=args.bucket_mb,
-                                        first_bucket_cap_mb=args.first_bucket_mb)
+                                        first_bucket_cap_mb=args.first_bucket_mb,
+                                        grad_comm_dtype=args.grad_comm)
     else:
         fn = STRATEGIES[args.strategy]
         sync = lambda m: fn(m, comm)  # noqa: E731
@@ -168,6 +172,7 @@ def main():
                                 "gather_scatter": "part2a gather/scatter",
                                 "gather_broadcast": "part2a gather/broadcast"}[args.strategy],
                    "hipgraph": graph_ok, "bucket_mb": args.bucket_mb,
+                   "grad_comm": args.grad_comm,
                    "comm": ("overlap-stream" if getattr(getattr(model, "reducer", None), "overlap",
                                                          lambda: False)() else "inline"),
                    "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4) fused"},

@@ -313,6 +313,8 @@ PYBIND11_MODULE(_native, m) {
       .def("set_overlap", &Reducer::set_overlap)
       .def("overlap", &Reducer::overlap)
       .def("set_emulate", &Reducer::set_emulate)
+      .def("set_comm_dtype", &Reducer::set_comm_dtype)
+      .def("comm_dtype", &Reducer::comm_dtype)
       .def("launched", &Reducer::launched)
       .def("comm_stream", [](Reducer& r) { return reinterpret_cast<uintptr_t>(r.comm_stream()); });
 }

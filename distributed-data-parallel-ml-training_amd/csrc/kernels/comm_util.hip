@@ -5,6 +5,9 @@
 //           part2/part2a/main.py:108).
 // scale   : x *= s (2B's `param.grad /= world_size`, part2/part2b/main.py:103, when the
 //           backend has no native average).
+// pack / unpack bf16 : fp32 gradient bucket <-> bf16 communication buffer (DDP with
+//           grad_comm_dtype="bf16": half the bytes on the xGMI links; like PyTorch's
+//           bf16_compress_hook). Round-to-nearest-even on the way in, exact widening back.
 #include "common.h"
 #include "api.h"
 
@@ -26,6 +29,36 @@ __global__ __launch_bounds__(256) void scale_kernel(float* x, size_t n, float s)
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += stride) x[i] *= s;
 }
 
+__global__ __launch_bounds__(256) void pack_bf16_kernel(const float* __restrict__ x, size_t n,
+                                                        unsigned short* __restrict__ y) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  const size_t n4 = n / 4;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    uint2 o;
+    o.x = (unsigned)f2bf(v.x) | ((unsigned)f2bf(v.y) << 16);
+    o.y = (unsigned)f2bf(v.z) | ((unsigned)f2bf(v.w) << 16);
+    reinterpret_cast<uint2*>(y)[i] = o;
+  }
+  for (size_t i = n4 * 4 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += stride)
+    y[i] = f2bf(x[i]);
+}
+
+__global__ __launch_bounds__(256) void unpack_bf16_kernel(const unsigned short* __restrict__ y,
+                                                          size_t n, float* __restrict__ x) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  const size_t n4 = n / 4;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const uint2 v = reinterpret_cast<const uint2*>(y)[i];
+    reinterpret_cast<float4*>(x)[i] = (float4){bf2f((unsigned short)(v.x & 0xffff)),
+                                               bf2f((unsigned short)(v.x >> 16)),
+                                               bf2f((unsigned short)(v.y & 0xffff)),
+                                               bf2f((unsigned short)(v.y >> 16))};
+  }
+  for (size_t i = n4 * 4 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += stride)
+    x[i] = bf2f(y[i]);
+}
+
 }  // namespace ddp_amd
 
 using namespace ddp_amd;
@@ -44,5 +77,19 @@ extern "C" int ddp_mean_ws(const float* in, size_t n, int ws, float* out, hipStr
 
 extern "C" int ddp_scale(float* x, size_t n, float s, hipStream_t st) {
   hipLaunchKernelGGL(scale_kernel, dim3(blocks_for(n)), dim3(256), 0, st, x, n, s);
+  return (int)hipGetLastError();
+}
+
+// x / y must be 16- / 8-byte aligned (arena tensors start on 64-element boundaries, so every
+// bucket does); a count that is not a multiple of 4 is finished by the scalar tail loop
+extern "C" int ddp_pack_bf16(const float* x, size_t n, unsigned short* y, hipStream_t st) {
+  if ((uintptr_t)x % 16 || (uintptr_t)y % 8) return -1;
+  hipLaunchKernelGGL(pack_bf16_kernel, dim3(blocks_for(n / 4 + 1)), dim3(256), 0, st, x, n, y);
+  return (int)hipGetLastError();
+}
+
+extern "C" int ddp_unpack_bf16(const unsigned short* y, size_t n, float* x, hipStream_t st) {
+  if ((uintptr_t)x % 16 || (uintptr_t)y % 8) return -1;
+  hipLaunchKernelGGL(unpack_bf16_kernel, dim3(blocks_for(n / 4 + 1)), dim3(256), 0, st, y, n, x);
   return (int)hipGetLastError();
 }

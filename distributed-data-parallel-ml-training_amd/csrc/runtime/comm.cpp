@@ -235,7 +235,18 @@ Reducer::Reducer(RcclComm* comm, float* arena, std::vector<size_t> offsets,
   prepare();
 }
 
+void Reducer::set_comm_dtype(int dtype) {
+  if (dtype != 0 && dtype != 1) throw std::runtime_error("gradient comm dtype: 0 = fp32, 1 = bf16");
+  comm_bf16_ = dtype == 1;
+  if (comm_bf16_ && !stage_) {
+    size_t n = 0;
+    for (const auto& b : buckets_) n = std::max(n, b.offset + b.count);
+    HIP_OK(hipMalloc(reinterpret_cast<void**>(&stage_), (n + 64) * sizeof(unsigned short)));
+  }
+}
+
 Reducer::~Reducer() {
+  if (stage_) hipFree(stage_);
   for (auto& v : ready_ev_)
     for (auto e : v)
       if (e) hipEventDestroy(e);
@@ -285,7 +296,14 @@ void Reducer::launch_ready() {
       HIP_OK(hipStreamWaitEvent(target, evs[i], 0));
     }
     float* buf = arena_ + bs.offset;
-    if (comm_->world() > 1) {
+    if (real && comm_bf16_) {
+      unsigned short* sb = stage_ + bs.offset;
+      if (ddp_pack_bf16(buf, bs.count, sb, target) != 0)
+        throw std::runtime_error("bf16 pack of a gradient bucket failed (alignment)");
+      if (comm_->world() > 1) comm_->all_reduce(sb, bs.count, /*bf16*/ 1, average_ ? 4 : 0, target);
+      if (ddp_unpack_bf16(sb, bs.count, buf, target) != 0)
+        throw std::runtime_error("bf16 unpack of a gradient bucket failed (alignment)");
+    } else if (comm_->world() > 1) {
       comm_->all_reduce(buf, bs.count, /*fp32*/ 0, average_ ? 4 : 0, target);
     } else if (emulate_) {
       // world 1 stand-in for the collective (graph-structure / overlap studies on one GPU):

@@ -90,6 +90,11 @@ class Reducer {
   // world 1 only: run a bucket-sized pass in place of each (no-op) collective, so the graph
   // shape and stream traffic of a multi-GPU step can be studied on one GPU
   void set_emulate(bool on) { emulate_ = on; }
+  // Gradient communication dtype: 0 = fp32 (default, the reference's), 1 = bf16 — each bucket
+  // is packed into a bf16 staging buffer, all-reduced (avg) in bf16 (half the xGMI bytes) and
+  // widened back into the fp32 arena. Allocates the staging buffer (call before capture).
+  void set_comm_dtype(int dtype);
+  int comm_dtype() const { return comm_bf16_ ? 1 : 0; }
   int launched() const { return next_launch_; }
   hipStream_t comm_stream() const { return comm_stream_; }
 
@@ -111,6 +116,8 @@ class Reducer {
   bool debug_sync_ = false;
   bool overlap_ = true;
   bool emulate_ = false;
+  bool comm_bf16_ = false;
+  unsigned short* stage_ = nullptr;  // bf16 staging buffer, arena-sized
   hipStream_t comm_stream_ = nullptr;
 };
 

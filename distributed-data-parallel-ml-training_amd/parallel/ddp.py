@@ -57,8 +57,9 @@ def plan_buckets(offsets, numels, elem_bytes, cap_bytes, cap_first_bytes):
 class _PyReducer:
     """Bucketed reducer for torch.distributed backends (Gloo on CPU)."""
 
-    def __init__(self, comm, arena, cap, cap_first, average):
+    def __init__(self, comm, arena, cap, cap_first, average, comm_dtype=torch.float32):
         self.comm, self.arena, self.average = comm, arena, average
+        self.comm_dtype = comm_dtype
         self.buckets = plan_buckets(arena.offsets, arena.numels, 4, cap, cap_first)
         self.bucket_of = {}
         for b, (s, e, _, _) in enumerate(self.buckets):
@@ -82,15 +83,18 @@ class _PyReducer:
             while self.next_launch < len(self.buckets) and self.ready[self.next_launch]:
                 _, _, off, cnt = self.buckets[self.next_launch]
                 view = self.arena.grad[off:off + cnt]
-                self.works.append((view, self.comm.all_reduce_async(view)))
+                buf = view if self.comm_dtype == view.dtype else view.to(self.comm_dtype)
+                self.works.append((view, buf, self.comm.all_reduce_async(buf)))
                 self.next_launch += 1
 
     def finalize(self):
         if self.next_launch != len(self.buckets):
             raise RuntimeError("DDP finalize: some parameters did not receive gradients "
                                "(unused parameters are not supported)")
-        for view, w in self.works:
+        for view, buf, w in self.works:
             w.wait()
+            if buf is not view:
+                view.copy_(buf)
             if self.average:
                 view /= self.comm.world
         self.prepare()
@@ -98,7 +102,7 @@ class _PyReducer:
 
 class DistributedDataParallel(nn.Module):
     def __init__(self, module, comm, bucket_cap_mb=25.0, first_bucket_cap_mb=1.0,
-                 broadcast_buffers=True, average=True, overlap=None):
+                 broadcast_buffers=True, average=True, overlap=None, grad_comm_dtype="fp32"):
         super().__init__()
         self.module = module
         self.comm = comm
@@ -127,11 +131,17 @@ class DistributedDataParallel(nn.Module):
             # the step stays on ONE stream (profiles/r1_comm_stream_study.md).
             if overlap is None:
                 overlap = os.environ.get("DDP_AMD_COMM_OVERLAP", "0") == "1"
+            if grad_comm_dtype not in ("fp32", "bf16"):
+                raise ValueError("grad_comm_dtype must be 'fp32' or 'bf16'")
             self.reducer.set_overlap(bool(overlap))
             self.reducer.set_emulate(os.environ.get("DDP_AMD_EMULATE_COMM", "0") == "1")
+            # bf16 gradient communication (PyTorch's bf16_compress_hook): half the xGMI bytes;
+            # the fp32 arena keeps the bf16-rounded average. Default fp32 = the reference.
+            self.reducer.set_comm_dtype(1 if grad_comm_dtype == "bf16" else 0)
             self._hook = register_grad_ready_hook(self._on_grad_ready)
         else:
-            self.reducer = _PyReducer(comm, self.arena, cap, cap_first, average)
+            self.reducer = _PyReducer(comm, self.arena, cap, cap_first, average,
+                                      torch.bfloat16 if grad_comm_dtype == "bf16" else torch.float32)
             self.buckets = self.reducer.buckets
             for p in self.arena.params:
                 p.register_post_accumulate_grad_hook(self._on_accumulated)

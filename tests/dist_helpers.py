@@ -62,9 +62,11 @@ def train_worker(rank, world, port, q, strategy, steps, per_rank_batch, bucket_m
         torch.manual_seed(89395)
         model = VGG11()
         comm = TorchCommunicator()
-        if strategy == "ddp":
+        if strategy in ("ddp", "ddp_bf16"):
             model = DistributedDataParallel(model, comm, bucket_cap_mb=bucket_mb,
-                                            first_bucket_cap_mb=min(bucket_mb, 1.0))
+                                            first_bucket_cap_mb=min(bucket_mb, 1.0),
+                                            grad_comm_dtype="bf16" if strategy == "ddp_bf16"
+                                            else "fp32")
         opt = FusedSGD(model.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
         crit = CrossEntropyLoss()
         loader = CPULoader(SyntheticCIFAR10(True, n=per_rank_batch * world * steps),
@@ -83,7 +85,7 @@ def train_worker(rank, world, port, q, strategy, steps, per_rank_batch, bucket_m
             opt.step()
         params = torch.cat([p.detach().reshape(-1).clone() for p in model.parameters()])
         consistent = None
-        if strategy == "ddp":
+        if strategy in ("ddp", "ddp_bf16"):
             consistent = check_replicas(model.arena, world)
             info = {"buckets": list(model.buckets)}
         else:

@@ -20,6 +20,9 @@ def results():
         out[strat] = run_workers(train_worker, WORLD, strat, STEPS, B, 4.0)
         for r, v in out[strat].items():
             assert "error" not in v, v.get("error")
+    out["ddp_bf16"] = run_workers(train_worker, WORLD, "ddp_bf16", STEPS, B, 4.0)
+    for r, v in out["ddp_bf16"].items():
+        assert "error" not in v, v.get("error")
     out["local"] = run_workers(local_grad_worker, WORLD, B)
     return out
 
@@ -54,3 +57,18 @@ def test_ddp_buckets_cover_all_params_in_reverse(results):
     assert sorted(covered) == list(range(34))
     assert buckets[0][1] == 34  # first bucket holds the LAST parameters (ready first)
     assert results["ddp"][0]["consistent"] is True
+
+
+def test_ddp_bf16_grad_comm(results):
+    """grad_comm_dtype="bf16": replicas stay bit-identical and the synced gradient is the
+    mean of the local gradients up to bf16 rounding of the communicated values."""
+    r = results["ddp_bf16"]
+    assert torch.equal(r[0]["params"], r[1]["params"])
+    assert r[0]["consistent"] is True
+    loc = results["local"]
+    expected = (loc[0]["grads0"] + loc[1]["grads0"]) / WORLD
+    g = r[0]["grads0"]
+    rel = float((g - expected).norm() / expected.norm())
+    assert 0 < rel < 1e-2, rel
+    # the communicated values were bf16: the result carries at most 8 significant bits + 1 add
+    assert not torch.equal(g, results["ddp"][0]["grads0"])

@@ -282,3 +282,33 @@ def test_bn_backward_fused_sums_match_reduce_kernel(native_ext):
         # the last block's BN sums come from the head, not a dgrad: identical up to atomics
         if n.startswith("fc1") or n.startswith("layers.26"):
             assert cos(ga, gb) > 0.999, n
+
+
+def test_ddp_bf16_grad_comm_path(native_ext):
+    """DDP(grad_comm_dtype="bf16") on one GPU with the world-1 collective stand-in: every
+    gradient passes through the bf16 pack -> (all-reduce) -> unpack path, so it is exactly
+    bf16-representable afterwards, and it agrees with the fp32-communicated gradient."""
+    from ddp_amd.models import VGG11
+    from ddp_amd.engine import CrossEntropyLoss
+    from ddp_amd.optim import FusedSGD
+    from ddp_amd.parallel import DistributedDataParallel, RcclCommunicator
+    torch.manual_seed(0)
+    base = VGG11().cuda()
+    x = torch.randn(32, 3, 32, 32, device="cuda")
+    y = torch.randint(0, 10, (32,), device="cuda")
+    comm = RcclCommunicator(0, 1, 0)
+    grads = {}
+    for dt in ("fp32", "bf16"):
+        m = DistributedDataParallel(copy.deepcopy(base), comm, grad_comm_dtype=dt)
+        m.reducer.set_emulate(True)
+        opt = FusedSGD(m.parameters(), lr=0.1)
+        opt.zero_grad()
+        CrossEntropyLoss()(m(x), y).backward()
+        torch.cuda.synchronize()
+        grads[dt] = m.arena.grad.clone()
+        m.close()
+    g = grads["bf16"]
+    assert torch.equal(g, g.to(torch.bfloat16).float())
+    assert not torch.equal(grads["fp32"], grads["fp32"].to(torch.bfloat16).float())
+    c = float(torch.dot(g, grads["fp32"]) / (g.norm() * grads["fp32"].norm()))
+    assert c > 0.98, c
