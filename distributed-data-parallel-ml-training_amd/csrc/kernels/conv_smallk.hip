@@ -202,10 +202,157 @@ __global__ __launch_bounds__(256) void conv_smallk_fwd_kernel(SmallKArgs a) {
   }
 }
 
+// Long reductions (ResNet-50 stem: 7x7 s2, 13 k-steps of 4 taps): the weights (64 x 49 x 8 bf16 =
+// 50 KB) do not fit the 32 KB vector L1, so re-reading a weight fragment per MFMA from global
+// memory streams ~10 GB through L2 per step at batch 256. Here the block stages all weights in
+// LDS once, and every wave works on PT pixel tiles at a time: each LDS weight fragment feeds PT
+// MFMAs (register blocking), activation fragments of the next k-step are prefetched.
+constexpr int kStemMaxTaps = 52;  // 13 k-steps x 4 taps (7x7 = 49 padded)
+
+template <int NT, int NKS, int PT>
+__global__ __launch_bounds__(256) void conv_smallk_lds_kernel(SmallKArgs a) {
+  // LDS weight image [NT*16 rows][NKS*4 taps + 1 pad][8 ch] (the pad tap spreads the rows over
+  // the LDS banks for the 16-row ds_read_b128 groups)
+  constexpr int TAPS = NKS * 4;
+  constexpr int ROW = TAPS + 1;
+  __shared__ __attribute__((aligned(16))) uint4 wl[NT * 16 * ROW];
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, rl = lane & 15;
+  const int RS = a.R * a.S;
+  const int M = a.N * a.P * a.Q;
+  for (int i = threadIdx.x; i < NT * 16 * TAPS; i += 256) {
+    const int k = i / TAPS, tap = i - k * TAPS;
+    wl[k * ROW + tap] = tap < RS ? *reinterpret_cast<const uint4*>(a.wc + ((size_t)k * RS + tap) * 8)
+                                 : make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
+  float bias[NT][4];
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) bias[j][v] = a.bias ? a.bias[j * 16 + 4 * g + v] : 0.f;
+  float s1[NT][4], s2[NT][4];
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) { s1[j][v] = 0.f; s2[j][v] = 0.f; }
+
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nwaves = gridDim.x * 4;
+  const int groups = (a.tiles + PT - 1) / PT;  // PT consecutive 16-pixel tiles per group
+  const int pq = a.P * a.Q;
+  for (int grp = wave; grp < groups; grp += nwaves) {
+    int base[PT], h0[PT], w0[PT];
+    bool rok[PT];
+#pragma unroll
+    for (int u = 0; u < PT; ++u) {
+      const int row = (grp * PT + u) * 16 + rl;
+      rok[u] = row < M;
+      const int rr = rok[u] ? row : 0;
+      const int n = rr / pq, rem = rr - n * pq;
+      const int p = rem / a.Q, q = rem - p * a.Q;
+      base[u] = n * a.H * a.W * 8;
+      h0[u] = p * a.stride - a.pad;
+      w0[u] = q * a.stride - a.pad;
+    }
+    auto load_act = [&](int t, uint4 (&xf)[PT]) {
+      const int tap = 4 * t + g;
+      const int r = tap / a.S, sx = tap - r * a.S;
+#pragma unroll
+      for (int u = 0; u < PT; ++u) {
+        const int h = h0[u] + r, w = w0[u] + sx;
+        xf[u] = (rok[u] && tap < RS && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W)
+                    ? *reinterpret_cast<const uint4*>(a.x + base[u] + ((size_t)h * a.W + w) * 8)
+                    : make_uint4(0, 0, 0, 0);
+      }
+    };
+    f32x4 acc[PT][NT];
+#pragma unroll
+    for (int u = 0; u < PT; ++u)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[u][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    uint4 xa[PT], xb[PT];
+    load_act(0, xa);
+#pragma unroll 1
+    for (int t = 0; t < NKS; ++t) {
+      if (t + 1 < NKS) load_act(t + 1, xb);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const uint4 wv = wl[(j * 16 + rl) * ROW + 4 * t + g];
+#pragma unroll
+        for (int u = 0; u < PT; ++u)
+          acc[u][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(wv), as_bf16x8(xa[u]), acc[u][j], 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < PT; ++u) xa[u] = xb[u];
+    }
+#pragma unroll
+    for (int u = 0; u < PT; ++u) {
+      const int row = (grp * PT + u) * 16 + rl;
+      if (row >= M) continue;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        unsigned short hv[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          hv[v] = f2bf(acc[u][j][v] + bias[j][v]);
+          const float r = bf2f(hv[v]);
+          s1[j][v] += r;
+          s2[j][v] += r * r;
+        }
+        uint2 pk;
+        pk.x = (unsigned)hv[0] | ((unsigned)hv[1] << 16);
+        pk.y = (unsigned)hv[2] | ((unsigned)hv[3] << 16);
+        *reinterpret_cast<uint2*>(a.y + (size_t)row * a.K + j * 16 + 4 * g) = pk;
+      }
+    }
+  }
+  if (!a.stats) return;
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) {
+        s1[j][v] += __shfl_xor(s1[j][v], m, kWave);
+        s2[j][v] += __shfl_xor(s2[j][v], m, kWave);
+      }
+  // block reduction through LDS (the weight image is no longer needed), one atomic per channel
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(wl);  // [4 waves][2][64]
+  const int wib = threadIdx.x >> 6;
+  if (rl == 0) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        red[(wib * 2 + 0) * 64 + j * 16 + 4 * g + v] = s1[j][v];
+        red[(wib * 2 + 1) * 64 + j * 16 + 4 * g + v] = s2[j][v];
+      }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * a.K) {
+    const int k = threadIdx.x / a.K, c = threadIdx.x - k * a.K;
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) t += red[(w * 2 + k) * 64 + c];
+    atomicAdd(a.stats + (blockIdx.x % kStatRep) * 2 * a.K + k * a.K + c, t);
+  }
+}
+
 int kSmallkTilesPerWave = 8;
 
 template <int NT, int NKS>
 void launch_smallk(const SmallKArgs& a, hipStream_t st) {
+  if constexpr (NKS > 4) {
+    // weights staged in LDS once per block: few, long-lived blocks (~2 per CU), each wave
+    // walking groups of kStemPT pixel tiles
+    constexpr int PT = 4;
+    const int groups = (a.tiles + PT - 1) / PT;
+    const int waves = std::max(1, std::min(groups, 2048));
+    hipLaunchKernelGGL((conv_smallk_lds_kernel<NT, NKS, PT>), dim3((waves + 3) / 4), dim3(256), 0, st, a);
+    return;
+  }
   // ~TPW tiles per wave: enough waves to fill the chip, weight-register loads and the per-block
   // statistics atomics amortised
   const int waves = (a.tiles + kSmallkTilesPerWave - 1) / kSmallkTilesPerWave;

@@ -29,6 +29,7 @@ CONV_CASES = [
     (2, 128, 14, 14, 256, 1, 1, 0),  # 1x1
     (2, 64, 14, 14, 128, 1, 2, 0),   # 1x1 stride 2
     (2, 8, 32, 32, 64, 7, 2, 3),     # 7x7 stem-like
+    (3, 8, 40, 40, 64, 7, 2, 3),     # stem, partial last pixel-tile group
 ]
 
 
