@@ -140,16 +140,16 @@ class GradLink:
         return out
 
 
-BN_BWD_FUSE_MAX_ELEMS = int(os.environ.get("DDP_AMD_BN_BWD_FUSE_MAX", str(1 << 21)))
+BN_BWD_FUSE_MAX_HW = int(os.environ.get("DDP_AMD_BN_BWD_FUSE_MAX_HW", "16"))
 
 
-def bn_bwd_fuse_pays(dx_numel):
-    """Fuse the preceding block's BatchNorm-backward sums into this dgrad only for small dgrad
-    outputs. Measured (VGG-11 b256, tools/conv_tune.py): on the 4x4 / 2x2 layers the fused
-    epilogue costs 2-5 us less than the reduce kernel it replaces; on the 16x16 / 8x8 layers
-    its per-tile z gather (exposed after the MFMA loop) costs 10-15 us MORE than the streaming
-    reduce kernel."""
-    return dx_numel <= BN_BWD_FUSE_MAX_ELEMS
+def bn_bwd_fuse_pays(H, W):
+    """Fuse the preceding block's BatchNorm-backward sums into this dgrad only when the dgrad
+    output is spatially small (H*W <= 16: VGG's 4x4 / 2x2 layers). Measured (VGG-11 b256 and
+    b32, tools/conv_tune.py and the step profiles): there the fused epilogue costs 2-5 us less
+    than the reduce kernel it replaces; on 16x16 / 8x8 outputs its z gather (4 loads per pooled
+    pixel, exposed after the MFMA loop) costs 10-15 us MORE than the streaming reduce kernel."""
+    return H * W <= BN_BWD_FUSE_MAX_HW
 
 
 def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=None):
@@ -250,7 +250,7 @@ class _ConvBNActFn(torch.autograd.Function):
         if (_common.BN_BWD_FUSE and prev is not None and ctx.prev_z is not None
                 and ctx.needs_input_grad[0] and ctx.in_link is None and spec.stride == 1
                 and not prev.residual and prev.K == spec.C and spec.C == spec.Cr
-                and bn_bwd_fuse_pays(x.numel())):
+                and bn_bwd_fuse_pays(x.shape[1], x.shape[2])):
             pz = ctx.prev_z
             bnf = (ptr(pz), ptr(prev.coef), ptr(prev.sums), int(prev.pool), int(prev.relu),
                    pz.shape[1], pz.shape[2])

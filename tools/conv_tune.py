@@ -90,7 +90,7 @@ def main():
             # (ops.layers BnBwdFuse): tune that variant. prev block's z is 2x larger if pooled.
             bn = None
             if (model == "vgg11" and prev_hw is not None and C == Cr
-                    and bn_bwd_fuse_pays(N * H * W * C)):
+                    and bn_bwd_fuse_pays(H, W)):
                 zh = prev_hw
                 pz = torch.randn(N, zh, zh, C, device=dev).to(torch.bfloat16)
                 pcoef = torch.rand(6 * C, device=dev)
