@@ -446,7 +446,9 @@ static unsigned blocks_for(size_t items, size_t per_block) {
 // Folding the finalize into the apply kernel costs every block a replica reduction of its
 // channels; worth it (one launch fewer) while that re-read traffic stays small.
 constexpr size_t kFoldBytes = 24u << 20;
-constexpr bool kFoldBwd = false;
+// Backward fold threshold (replica bytes re-read by all apply blocks): measured 3-4x slower
+// applies when folding the big layers; small grids (strong-scaling batches) may gain the launch.
+static size_t kFoldBwdBytes = 0;  // DDP_AMD_BN_FOLD_BWD_KB overrides (0 = never fold)
 static size_t kBwdBlocks = 1024;  // target reduce-grid size (DDP_AMD_BN_BWD_BLOCKS overrides)
 
 template <bool POOL, int IPT>
@@ -490,7 +492,7 @@ static void launch_bwd(const BnArgs& a, size_t npix, int Gb, int chunks, hipStre
   const size_t nch = (size_t)Gb * 8;
   if (a.counter && !a.sums_ready) {  // finalized by the reduce kernel's last block
     hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT, false>), dim3(bx, chunks), dim3(256), 0, st, a);
-  } else if (kFoldBwd && (size_t)bx * chunks * nch * 2 * kStatRep * sizeof(float) <= kFoldBytes) {
+  } else if ((size_t)bx * chunks * nch * 2 * kStatRep * sizeof(float) <= kFoldBwdBytes) {
     hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT, true>), dim3(bx, chunks), dim3(256),
                        2 * nch * sizeof(float), st, a);
   } else {
@@ -504,6 +506,7 @@ static void launch_bwd(const BnArgs& a, size_t npix, int Gb, int chunks, hipStre
 extern "C" int ddp_bn_act_bwd(const BnArgs* args, hipStream_t st) {
   static const bool init = [] {
     if (const char* e = std::getenv("DDP_AMD_BN_BWD_BLOCKS")) kBwdBlocks = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("DDP_AMD_BN_FOLD_BWD_KB")) kFoldBwdBytes = (size_t)std::max(0, std::atoi(e)) << 10;
     return true;
   }();
   (void)init;
