@@ -29,7 +29,17 @@ _TORCH_OP = {SUM: dist.ReduceOp.SUM, PROD: dist.ReduceOp.PRODUCT, MAX: dist.Redu
 
 def init_distributed_setup(master_ip, master_port, rank, world_size, backend="gloo",
                            timeout_s=1800):
-    """Reference-compatible bootstrap (part2/part2a/main.py:52-58)."""
+    """Reference-compatible bootstrap (part2/part2a/main.py:52-58).
+
+    Under torchrun (TORCHELASTIC_USE_AGENT_STORE) the launcher's rendezvous store is the one the
+    process group joins, so --master-ip/--master-port must not redirect it: a mismatch would
+    make every rank wait for a store nobody hosts. The launcher's MASTER_ADDR/PORT win there."""
+    if os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True" and "MASTER_PORT" in os.environ:
+        env = (os.environ.get("MASTER_ADDR"), os.environ["MASTER_PORT"])
+        if (str(master_ip), str(master_port)) != env:
+            print(f"[ddp_amd] launched by torchrun: using its rendezvous {env[0]}:{env[1]} "
+                  f"instead of --master-ip/--master-port {master_ip}:{master_port}", flush=True)
+        master_ip, master_port = env
     os.environ["MASTER_ADDR"] = str(master_ip)
     os.environ["MASTER_PORT"] = str(master_port)
     dist.init_process_group(backend, rank=rank, world_size=world_size,
