@@ -971,10 +971,19 @@ static void launch_cfg(ConvArgs& a, int splits, hipStream_t st, int nst_req = 0)
   // slab + grouped-finish reduction is cheaper
   if (a.wg_atomic && splits > kMaxAtomicSplits) a.wg_atomic = 0;
   const int items = tiles * splits;
-  const int nst = nst_req >= 2 && nst_req <= 4 ? nst_req : stages_for(BM, BN);
-  if (nst == 4) launch_gemm<MODE, BM, BN, 4>(a, items, st);
-  else if (nst == 3) launch_gemm<MODE, BM, BN, 3>(a, items, st);
-  else launch_gemm<MODE, BM, BN, 2>(a, items, st);
+  // deepest ring that fits the 160 KiB LDS for this tile ((BM + BN) x 64 bf16 per stage)
+  constexpr int kStageBytes = (BM + BN) * 64 * 2;
+  constexpr int kMaxStages = kStageBytes * 4 <= 163840 ? 4 : (kStageBytes * 3 <= 163840 ? 3 : 2);
+  int nst = nst_req >= 2 && nst_req <= 4 ? nst_req : stages_for(BM, BN);
+  nst = std::min(nst, kMaxStages);
+  if constexpr (kMaxStages >= 4) {
+    if (nst == 4) { launch_gemm<MODE, BM, BN, 4>(a, items, st); goto launched; }
+  }
+  if constexpr (kMaxStages >= 3) {
+    if (nst == 3) { launch_gemm<MODE, BM, BN, 3>(a, items, st); goto launched; }
+  }
+  launch_gemm<MODE, BM, BN, 2>(a, items, st);
+launched:
   if (splits == 1) return;
   if (MODE == MODE_WGRAD && a.wg_atomic) return;
   if (MODE == MODE_WGRAD && a.g.wkrsc) {
@@ -1029,16 +1038,25 @@ static std::map<TuneKey, TuneVal> g_tuned;  // -> (tile index, splits, LDS stage
 static int g_force_tile = 0;                // 1..4 = tile index + 1
 static int g_force_stages = 0;              // 2..4 (sweeps), 0 = policy
 
+// tile index: 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64 (cost model + table), and the
+// big tiles 4 = 256x64, 5 = 64x256, 6 = 256x128, 7 = 128x256 (measured table entries only: less
+// L2 -> LDS traffic per MFMA, fewer tiles)
+constexpr int kNumTiles = 8;
+
 template <int MODE>
 static void launch_mode(ConvArgs& a, size_t ws_elems, hipStream_t st) {
-  int sp[4];
+  int sp[kNumTiles];
   const double c[4] = {tile_cost(128, 128, a, ws_elems, &sp[0]), tile_cost(128, 64, a, ws_elems, &sp[1]),
                        tile_cost(64, 128, a, ws_elems, &sp[2]), tile_cost(64, 64, a, ws_elems, &sp[3])};
   int best = 0, nst = g_force_stages;
   for (int i = 1; i < 4; ++i)
     if (c[i] < c[best]) best = i;
-  if (g_force_tile >= 1 && g_force_tile <= 4) {
+  if (g_force_tile >= 1 && g_force_tile <= kNumTiles) {
     best = g_force_tile - 1;
+    if (best >= 4) {
+      static const int bmn[4][2] = {{256, 64}, {64, 256}, {256, 128}, {128, 256}};
+      tile_cost(bmn[best - 4][0], bmn[best - 4][1], a, ws_elems, &sp[best]);
+    }
   } else if (a.splits <= 0) {
     auto it = g_tuned.find(TuneKey{MODE, a.Mg, a.Ng, a.Kg});
     if (it != g_tuned.end()) {
@@ -1056,7 +1074,11 @@ static void launch_mode(ConvArgs& a, size_t ws_elems, hipStream_t st) {
     case 0: launch_cfg<MODE, 128, 128>(a, sp[0], st, nst); break;
     case 1: launch_cfg<MODE, 128, 64>(a, sp[1], st, nst); break;
     case 2: launch_cfg<MODE, 64, 128>(a, sp[2], st, nst); break;
-    default: launch_cfg<MODE, 64, 64>(a, sp[3], st, nst); break;
+    case 3: launch_cfg<MODE, 64, 64>(a, sp[3], st, nst); break;
+    case 4: launch_cfg<MODE, 256, 64>(a, sp[4], st, nst); break;
+    case 5: launch_cfg<MODE, 64, 256>(a, sp[5], st, nst); break;
+    case 6: launch_cfg<MODE, 256, 128>(a, sp[6], st, nst); break;
+    default: launch_cfg<MODE, 128, 256>(a, sp[7], st, nst); break;
   }
 }
 
@@ -1066,9 +1088,9 @@ extern "C" void ddp_conv_options(int wgrad_atomic, int persistent, int stages) {
   g_stages = stages;
 }
 
-// tile: 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64
+// tile: index into the launch_mode table (0..kNumTiles-1)
 extern "C" void ddp_conv_tune_set(int mode, int M, int N, int K, int tile, int splits, int stages) {
-  if (tile < 0 || tile > 3) return;
+  if (tile < 0 || tile >= kNumTiles) return;
   g_tuned[TuneKey{mode, M, N, K}] = {tile, std::max(1, splits), stages};
 }
 extern "C" void ddp_conv_tune_clear() { g_tuned.clear(); }

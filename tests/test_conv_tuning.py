@@ -17,7 +17,7 @@ def test_tuning_table_well_formed():
     keys = set()
     for e in t["entries"]:
         assert e["mode"] in (0, 1, 2)
-        assert 0 <= e["tile"] <= 3
+        assert 0 <= e["tile"] <= 7
         assert 1 <= e["splits"] <= 64
         assert min(e["M"], e["N"], e["K"]) > 0
         assert e["us"] <= e["auto_us"] + 1e-6

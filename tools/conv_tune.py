@@ -6,7 +6,7 @@ write the winners to the launcher's tuning table (ops/conv_tuning.json).
 
 Shapes: VGG-11 at per-GPU batch 256/128/64/32 (weak scaling and the reference's strong-scaling
 split of 256 over 1/2/4/8 GPUs) and ResNet-50 at 64 and 256. For each GEMM problem (mode, M, N, K) every
-tile (128x128, 128x64, 64x128, 64x64) x LDS ring depth (2-4 stages) x split-K factor is launched exactly as the training step
+tile (128x128, 128x64, 64x128, 64x64, and the big 256x64, 64x256, 256x128, 128x256) x LDS ring depth (2-4 stages) x split-K factor is launched exactly as the training step
 launches it (same kernels, same finish passes), timed with HIP events, and the fastest is kept;
 the cost-model choice is timed too and reported next to it. Like MIOpen's find-db, but for our
 own kernels. Strided dgrad problems (several phase GEMMs) are tuned as a whole and the winner is
@@ -21,7 +21,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tools"))
 
-TILES = ["128x128", "128x64", "64x128", "64x64"]
+TILES = ["128x128", "128x64", "64x128", "64x64", "256x64", "64x256", "256x128", "128x256"]
 
 
 def dgrad_phases(N, H, W, K, R, S, stride, pad):
@@ -134,8 +134,11 @@ def main():
                 best = (auto_us, None, None, None)
                 M0, N0, K0 = gemms[0]
                 ksteps = (K0 + 63) // 64
-                for t in range(4):
+                for t in range(len(TILES)):
+                    tbm, tbn = (int(v) for v in TILES[t].split("x"))
                     for nst in (2, 3, 4):
+                        if (tbm + tbn) * 64 * 2 * nst > 163840:
+                            continue  # the ring would not fit the LDS (clamped by the launcher)
                         n.conv_force_tile(t + 1, nst)
                         for s in (1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64):
                             if s > 1 and (ksteps // s < 2 or s * M0 * N0 > ws.numel()):
