@@ -26,6 +26,7 @@ MI355X design:
   first bucket (the big 512x512 conv gradients, ready first) starts early. Defaults: 25 MiB
   (reference) with a 1 MiB first bucket; ``bucket_cap_mb`` is tunable.
 """
+import contextlib
 import os
 
 import torch
@@ -116,6 +117,7 @@ class DistributedDataParallel(nn.Module):
         cap_first = int(first_bucket_cap_mb * (1 << 20))
         self._index = {id(p): i for i, p in enumerate(self.arena.params)}
         self._in_backward = False
+        self._sync_enabled = True
         self._stream = None
         if self.cuda:
             from ..ops.common import native, register_grad_ready_hook
@@ -188,6 +190,18 @@ class DistributedDataParallel(nn.Module):
         self._sync_buffers()
         return self.module.forward_loss(*args, **kwargs)
 
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Gradient accumulation without communication (torch DDP's ``no_sync``): backward
+        passes inside the context accumulate into the gradient arena locally; the first backward
+        after it all-reduces the accumulated gradients. (The reference has no accumulation —
+        its report lists skipping synchronisations as future work.)"""
+        prev, self._sync_enabled = self._sync_enabled, False
+        try:
+            yield
+        finally:
+            self._sync_enabled = prev
+
     def _queue_finalize(self):
         if not self._in_backward:
             self._in_backward = True
@@ -195,7 +209,7 @@ class DistributedDataParallel(nn.Module):
 
     def _on_grad_ready(self, p, stream):
         i = self._index.get(id(p))
-        if i is None:
+        if i is None or not self._sync_enabled:
             return
         if self._stream is None:
             # the backward's main stream (the first announcement comes from the classifier);
@@ -211,6 +225,8 @@ class DistributedDataParallel(nn.Module):
         if p.grad.data_ptr() != view.data_ptr():  # someone replaced .grad: fold it back
             view.copy_(p.grad)
             p.grad = view
+        if not self._sync_enabled:
+            return
         self._queue_finalize()
         self.reducer.mark_ready(i)
 

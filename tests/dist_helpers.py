@@ -115,3 +115,44 @@ def local_grad_worker(rank, world, port, q, per_rank_batch):
     g = torch.cat([p.grad.reshape(-1).clone() for p in model.parameters()])
     dist.destroy_process_group()
     q.put((rank, {"grads0": g.numpy()}))
+
+
+def nosync_worker(rank, world, port, q, per_rank_batch):
+    """DDP.no_sync gradient accumulation vs manual accumulate-then-average."""
+    try:
+        _init(rank, world, port)
+        import torch.distributed as dist
+        from ddp_amd.models import VGG11
+        from ddp_amd.optim import FusedSGD
+        from ddp_amd.parallel import TorchCommunicator, DistributedDataParallel
+        from ddp_amd.engine import CrossEntropyLoss
+        from ddp_amd.data import SyntheticCIFAR10, CPULoader
+        torch.manual_seed(89395)
+        plain = VGG11()
+        torch.manual_seed(89395)
+        ddp = DistributedDataParallel(VGG11(), TorchCommunicator(), bucket_cap_mb=4.0)
+        opt_p = FusedSGD(plain.parameters(), lr=0.05)
+        opt_d = FusedSGD(ddp.parameters(), lr=0.05)
+        crit = CrossEntropyLoss()
+        loader = CPULoader(SyntheticCIFAR10(True, n=per_rank_batch * world * 2), per_rank_batch,
+                           num_replicas=world, rank=rank)
+        batches = [b for _, b in zip(range(2), loader)]
+        opt_p.zero_grad()
+        opt_d.zero_grad()
+        for x, y in batches:
+            crit(plain(x), y).backward()
+        with ddp.no_sync():
+            crit(ddp(batches[0][0]), batches[0][1]).backward()
+        local_after_nosync = torch.cat([p.grad.reshape(-1).clone() for p in ddp.parameters()])
+        crit(ddp(batches[1][0]), batches[1][1]).backward()
+        g_ddp = torch.cat([p.grad.reshape(-1).clone() for p in ddp.parameters()])
+        g_man = torch.cat([p.grad.reshape(-1).clone() for p in plain.parameters()])
+        dist.all_reduce(g_man)
+        g_man /= world
+        dist.destroy_process_group()
+        q.put((rank, {"ddp": g_ddp.numpy(), "manual": g_man.numpy(),
+                      "after_nosync": local_after_nosync.numpy()}))
+    except Exception:
+        import traceback
+        q.put((rank, {"error": traceback.format_exc()}))
+        raise

@@ -72,3 +72,16 @@ def test_ddp_bf16_grad_comm(results):
     assert 0 < rel < 1e-2, rel
     # the communicated values were bf16: the result carries at most 8 significant bits + 1 add
     assert not torch.equal(g, results["ddp"][0]["grads0"])
+
+
+def test_ddp_no_sync_accumulation():
+    """DDP.no_sync: the first backward accumulates locally (no communication, replicas differ),
+    the next one all-reduces the accumulated gradient = mean over ranks of (g1 + g2)."""
+    from dist_helpers import nosync_worker
+    out = run_workers(nosync_worker, WORLD, B)
+    for r, v in out.items():
+        assert "error" not in v, v.get("error")
+    assert not torch.allclose(out[0]["after_nosync"], out[1]["after_nosync"])
+    for r in range(WORLD):
+        assert torch.allclose(out[r]["ddp"], out[r]["manual"], rtol=1e-4, atol=1e-6)
+    assert torch.equal(out[0]["ddp"], out[1]["ddp"])

@@ -312,3 +312,33 @@ def test_ddp_bf16_grad_comm_path(native_ext):
     assert not torch.equal(grads["fp32"], grads["fp32"].to(torch.bfloat16).float())
     c = float(torch.dot(g, grads["fp32"]) / (g.norm() * grads["fp32"].norm()))
     assert c > 0.98, c
+
+
+def test_ddp_no_sync_accumulates_on_gpu(native_ext):
+    """Fused kernels accumulate parameter gradients (+=): DDP.no_sync + a synced backward on
+    one GPU == two plain backward passes accumulating into the same arena."""
+    from ddp_amd.models import VGG11
+    from ddp_amd.engine import CrossEntropyLoss
+    from ddp_amd.optim import FusedSGD
+    from ddp_amd.parallel import DistributedDataParallel, RcclCommunicator
+    torch.manual_seed(0)
+    base = VGG11().cuda()
+    plain = copy.deepcopy(base)
+    ddp = DistributedDataParallel(copy.deepcopy(base), RcclCommunicator(0, 1, 0))
+    xs = [torch.randn(16, 3, 32, 32, device="cuda") for _ in range(2)]
+    ys = [torch.randint(0, 10, (16,), device="cuda") for _ in range(2)]
+    op, od = FusedSGD(plain.parameters(), lr=0.1), FusedSGD(ddp.parameters(), lr=0.1)
+    op.zero_grad()
+    od.zero_grad()
+    crit = CrossEntropyLoss()
+    for x, y in zip(xs, ys):
+        crit(plain(x), y).backward()
+    with ddp.no_sync():
+        crit(ddp(xs[0]), ys[0]).backward()
+    crit(ddp(xs[1]), ys[1]).backward()
+    torch.cuda.synchronize()
+    ddp.close()
+    a, b = op.arena.grad, od.arena.grad
+    c = float(torch.dot(a, b) / (a.norm() * b.norm()))
+    assert c > 0.98, c
+    assert abs(float(a.norm()) / float(b.norm()) - 1) < 0.05
