@@ -76,7 +76,15 @@ class TrainStep:
             return
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # Multi-GPU: RCCL keeps helper threads of its own; with the default "global" capture
+        # mode any unsafe HIP call they make during the capture would invalidate it. Only the
+        # capturing thread must stay capture-safe ("thread_local"); the replay is validated
+        # against every replica afterwards (validate_distributed).
+        import torch.distributed as dist
+        mode = "global"
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            mode = "thread_local"
+        with torch.cuda.graph(g, capture_error_mode=mode):
             self._body()
         self.graph = g
 
