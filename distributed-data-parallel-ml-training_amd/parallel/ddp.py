@@ -118,6 +118,7 @@ class DistributedDataParallel(nn.Module):
         self._index = {id(p): i for i, p in enumerate(self.arena.params)}
         self._in_backward = False
         self._sync_enabled = True
+        self._flat_buffers = None
         self._stream = None
         if self.cuda:
             from ..ops.common import native, register_grad_ready_hook
@@ -172,14 +173,36 @@ class DistributedDataParallel(nn.Module):
             for b in self.module.buffers():
                 self.comm.broadcast(b, 0)
 
+    @torch.no_grad()
+    def _flatten_buffers(self):
+        """Re-point every module buffer (BatchNorm running statistics) at a view of one flat
+        tensor per dtype, so the per-forward buffer broadcast is ONE collective per dtype instead
+        of one per buffer (ResNet-50: 2 instead of 159)."""
+        groups = {}
+        for mod in self.module.modules():
+            for name, b in mod._buffers.items():
+                if b is not None:
+                    groups.setdefault(b.dtype, []).append((mod, name, b))
+        self._flat_buffers = []
+        for dtype, items in groups.items():
+            flat = torch.empty(sum(b.numel() for _, _, b in items), dtype=dtype,
+                               device=items[0][2].device)
+            off = 0
+            for mod, name, b in items:
+                view = flat[off:off + b.numel()].view_as(b)
+                view.copy_(b)
+                mod._buffers[name] = view
+                off += b.numel()
+            self._flat_buffers.append(flat)
+
     # ------------------------------------------------------------ per-step
     def _sync_buffers(self):
         if self.broadcast_buffers and self.comm.world > 1 and torch.is_grad_enabled():
-            bufs = list(self.module.buffers())
-            if bufs:
-                with torch.no_grad():
-                    for b in bufs:
-                        self.comm.broadcast(b, 0)
+            if self._flat_buffers is None:
+                self._flatten_buffers()
+            with torch.no_grad():
+                for flat in self._flat_buffers:
+                    self.comm.broadcast(flat, 0)
 
     def forward(self, *args, **kwargs):
         self._sync_buffers()

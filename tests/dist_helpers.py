@@ -156,3 +156,33 @@ def nosync_worker(rank, world, port, q, per_rank_batch):
         import traceback
         q.put((rank, {"error": traceback.format_exc()}))
         raise
+
+
+def buffers_worker(rank, world, port, q):
+    """DDP broadcast_buffers with flattened buffers: after a forward every rank holds rank 0's
+    running statistics, and the module's buffers are views into the flat per-dtype tensors."""
+    try:
+        _init(rank, world, port)
+        import torch.nn as nn
+        import torch.distributed as dist
+        from ddp_amd.parallel import TorchCommunicator, DistributedDataParallel
+        torch.manual_seed(0)
+        m = nn.Sequential(nn.Conv2d(3, 8, 3, padding=1), nn.BatchNorm2d(8), nn.ReLU(),
+                          nn.Conv2d(8, 8, 3, padding=1), nn.BatchNorm2d(8), nn.Flatten(),
+                          nn.Linear(8 * 8 * 8, 4))
+        ddp = DistributedDataParallel(m, TorchCommunicator())
+        with torch.no_grad():  # diverge the replicas' running stats
+            m[1].running_mean.fill_(float(rank + 1))
+            m[4].running_var.fill_(float(10 * (rank + 1)))
+        x = torch.randn(4, 3, 8, 8) + rank
+        ddp(x).sum().backward()
+        bufs = {n: b.clone() for n, b in m.named_buffers()}
+        flat_views = all(b.untyped_storage().data_ptr() in
+                         {f.untyped_storage().data_ptr() for f in ddp._flat_buffers}
+                         for b in m.buffers())
+        dist.destroy_process_group()
+        q.put((rank, {"bufs": {k: v.numpy() for k, v in bufs.items()}, "flat": flat_views}))
+    except Exception:
+        import traceback
+        q.put((rank, {"error": traceback.format_exc()}))
+        raise

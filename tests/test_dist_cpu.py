@@ -85,3 +85,23 @@ def test_ddp_no_sync_accumulation():
     for r in range(WORLD):
         assert torch.allclose(out[r]["ddp"], out[r]["manual"], rtol=1e-4, atol=1e-6)
     assert torch.equal(out[0]["ddp"], out[1]["ddp"])
+
+
+def test_ddp_broadcast_buffers_flat():
+    """Buffers (BN running statistics) are broadcast from rank 0 before every forward as one
+    collective per dtype, so every replica's forward starts from rank 0's running statistics
+    (the forward's own momentum update then mixes in each rank's batch statistics)."""
+    from dist_helpers import buffers_worker
+    out = run_workers(buffers_worker, WORLD)
+    for r, v in out.items():
+        assert "error" not in v, v.get("error")
+        assert v["flat"] is True
+    b0 = {k: torch.as_tensor(v) for k, v in out[0]["bufs"].items()}
+    b1 = {k: torch.as_tensor(v) for k, v in out[1]["bufs"].items()}
+    # both ranks started the forward from rank 0's statistics (mean filled with 1.0, var 10.0);
+    # the forward's own update then mixes in each rank's batch statistics with momentum 0.1
+    for k in b0:
+        if k.endswith("num_batches_tracked"):
+            assert torch.equal(b0[k], b1[k])
+    assert float(b1["1.running_mean"].mean()) < 1.5  # started from rank 0's 1.0, not rank 1's 2.0
+    assert float(b1["4.running_var"].mean()) < 15.0  # started from 10.0, not 20.0
