@@ -230,15 +230,20 @@ PYBIND11_MODULE(_native, m) {
   m.def("augment", [](uintptr_t images, uintptr_t labels, uintptr_t indices, uintptr_t cursor,
                       int L, int B, int H, int W, int Cp, int pad, int flip, unsigned int seed,
                       unsigned int epoch, std::vector<float> mean, std::vector<float> std_,
-                      uintptr_t x, uintptr_t y, uintptr_t st) {
+                      uintptr_t x, uintptr_t y, uintptr_t st, uintptr_t zero, size_t zero_n) {
     ddp_amd::AugArgs a{};
+    a.zero = P<float>(zero);
+    a.zero_n = zero ? zero_n : 0;
     a.images = P<unsigned char>(images); a.labels = P<int>(labels); a.indices = P<int>(indices);
     a.cursor = P<int>(cursor); a.L = L; a.B = B; a.H = H; a.W = W; a.Cp = Cp; a.pad = pad;
     a.flip = flip; a.seed = seed; a.epoch = epoch;
     for (int c = 0; c < 3; ++c) { a.mean[c] = mean.at(c); a.inv_std[c] = 1.f / std_.at(c); }
     a.x = P<unsigned short>(x); a.y = P<long long>(y);
     check(ddp_augment(&a, S(st)), "augment");
-  });
+  }, py::arg("images"), py::arg("labels"), py::arg("indices"), py::arg("cursor"), py::arg("L"),
+     py::arg("B"), py::arg("H"), py::arg("W"), py::arg("Cp"), py::arg("pad"), py::arg("flip"),
+     py::arg("seed"), py::arg("epoch"), py::arg("mean"), py::arg("std"), py::arg("x"),
+     py::arg("y"), py::arg("stream"), py::arg("zero") = 0, py::arg("zero_n") = 0);
   m.def("nchw_to_nhwc", [](uintptr_t x, int N, int C, int H, int W, int Cp, uintptr_t out,
                            uintptr_t st) {
     check(ddp_nchw_to_nhwc(P<float>(x), N, C, H, W, Cp, P<void>(out), S(st)), "nchw_to_nhwc");

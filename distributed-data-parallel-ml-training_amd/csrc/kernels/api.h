@@ -81,6 +81,8 @@ struct AugArgs {
   float mean[3], inv_std[3];
   unsigned short* x;            // [B][H][W][Cp] bf16
   long long* y;                 // [B]
+  float* zero;                  // optional side job: zero this many floats (the next forward's
+  size_t zero_n;                //   per-step accumulator scratch, ops/common.py StepScratch)
 };
 
 }  // namespace ddp_amd

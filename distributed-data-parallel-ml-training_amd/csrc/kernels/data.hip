@@ -77,6 +77,9 @@ __global__ __launch_bounds__(256) void augment_kernel(AugArgs a) {
     }
     if (pix == 0) a.y[b] = a.labels[idx];
   }
+  // side job: clear the next forward's BN-statistics scratch (saves a fill launch per step)
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < a.zero_n; i += stride)
+    a.zero[i] = 0.f;
 }
 
 // NCHW fp32 -> NHWC bf16 with channel zero-padding (generic model input).

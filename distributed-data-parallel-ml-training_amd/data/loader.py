@@ -136,12 +136,16 @@ class DeviceLoader:
         return min(n, self.max_batches) if self.max_batches else n
 
     def _launch(self, x, y, indices_ptr, L, B, cursor_ptr):
-        from ..ops.common import native, stream_handle
+        from ..ops.common import native, stream_handle, step_scratch
         pad, flip = (4, 1) if self.train else (0, 0)
+        # the augment launch also clears the per-step BN-statistics scratch that the next
+        # forward would otherwise zero with a fill kernel of its own (StepScratch.zero)
+        sc = step_scratch(self.device)
+        zp, zn = sc.claim_zero()
         native().augment(self.images.data_ptr(), self.labels.data_ptr(), indices_ptr, cursor_ptr,
                          L, B, self.ds.height, self.ds.width, self.cpad, pad, flip,
                          self.ds.seed & 0xFFFFFFFF, self.epoch, CIFAR_MEAN, CIFAR_STD,
-                         x.data_ptr(), y.data_ptr(), stream_handle())
+                         x.data_ptr(), y.data_ptr(), stream_handle(), zero=zp, zero_n=zn)
 
     def batch(self, start, B):
         """Materialise samples [start, start+B) of this rank's shard (new tensors)."""

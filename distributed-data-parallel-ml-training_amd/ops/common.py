@@ -200,8 +200,19 @@ class StepScratch:
         self._tcur += n
         return out
 
+    def claim_zero(self):
+        """For a kernel that runs right before the next forward (the batch loader's augment
+        launch): returns (pointer, count) of the region to clear and marks it cleared, so the
+        forward's zero() skips its fill launch."""
+        if not self.used:
+            return 0, 0
+        self._pre_zeroed = True
+        return self.buf.data_ptr(), self.used
+
     def zero(self):
-        if self.used:
+        if getattr(self, "_pre_zeroed", False):
+            self._pre_zeroed = False  # cleared by the loader's launch for this forward
+        elif self.used:
             self.buf[:self.used].zero_()
         self._tcur = 0
 
