@@ -127,8 +127,12 @@ class DeviceLoader:
 
     def set_epoch(self, e):
         self.epoch = e
-        idx = shard_indices(len(self.ds), self.num_replicas, self.rank, epoch=e)
-        self.idx = torch.tensor(idx, dtype=torch.int32, device=self.device)
+        idx = torch.tensor(shard_indices(len(self.ds), self.num_replicas, self.rank, epoch=e),
+                           dtype=torch.int32)
+        if getattr(self, "idx", None) is not None and self.idx.numel() == idx.numel():
+            self.idx.copy_(idx)  # in place: a captured step keeps pointing at live memory
+        else:
+            self.idx = idx.to(self.device)
         self.cursor.zero_()
 
     def __len__(self):

@@ -21,7 +21,7 @@ from ..parallel import (DistributedDataParallel, STRATEGIES, destroy, init_distr
                         make_communicator, test_distributed_setup)
 from ..utils import MetricsSink, load_checkpoint, parse_all, pick_device, save_checkpoint, \
     seed_everything
-from .trainer import CrossEntropyLoss, test_model, train_model
+from .trainer import CrossEntropyLoss, test_model, train_model, train_model_graph
 
 PART_STRATEGY = {"part1": None, "part2a": "gather_scatter", "part2b": "allreduce", "part3": "ddp"}
 
@@ -63,9 +63,35 @@ def main(part, argv=None):
         sync = functools.partial(_sync, STRATEGIES[strategy], comm)
     metrics = MetricsSink(args.metrics, rank)
 
+    step = None
+    if args.graph and torch.device(device).type == "cuda":
+        # opt-in: each iteration is one replay of the captured step (the warm-up steps consume
+        # the first batches of the shard, like any other iteration would)
+        # the warm-up steps train on the first batches: snapshot the training state and roll
+        # it back after the capture, so the epoch starts exactly where the eager loop would
+        from .step import TrainStep
+        arena = model.arena if hasattr(model, "arena") else optimizer.arena
+        snap = (arena.data.clone(), optimizer.momentum_buffer.clone())
+        step = TrainStep(model, optimizer, criterion, train_loader, sync=sync)
+        step.warmup(2)
+        step.capture()
+        torch.cuda.synchronize()
+        arena.data.copy_(snap[0])
+        optimizer.momentum_buffer.copy_(snap[1])
+        optimizer.repack()
+        train_loader.cursor.zero_()
+        del snap
+
     for epoch in range(args.epochs):
-        train_loader.set_epoch(epoch)
-        train_model(model, train_loader, optimizer, criterion, epoch, device, sync, metrics=metrics)
+        if step is not None:
+            if epoch > 0:
+                train_loader.set_epoch(epoch)
+                step.capture()  # the augmentation seed is a launch argument: new epoch, new graph
+            train_model_graph(step, train_loader, epoch, metrics=metrics)
+        else:
+            train_loader.set_epoch(epoch)
+            train_model(model, train_loader, optimizer, criterion, epoch, device, sync,
+                        metrics=metrics)
         if not args.no_test:
             test_model(model, test_loader, criterion, device)
 

@@ -69,6 +69,37 @@ def train_model(model, train_loader, optimizer, criterion, epoch, device="cpu", 
     return stats
 
 
+def train_model_graph(step, train_loader, epoch, log=print, metrics=None, watchdog=None):
+    """``train_model`` over a captured TrainStep (engine/step.py): every iteration is ONE graph
+    replay (augment + forward + backward + sync + optimizer) followed by a device synchronize,
+    so the per-iteration timer keeps the reference's meaning (the reference's ``loss.item()``
+    synchronises each iteration too). The loss print every 20 batches reads the device loss
+    accumulator (same running mean as the reference)."""
+    total_time = 0
+    stats = {"iter_ns": []}
+    nb = len(train_loader)
+    step.pop_loss()
+    for batch_idx in range(nb):
+        start_time = time.perf_counter_ns()
+        step.step()
+        torch.cuda.synchronize()
+        if batch_idx % 20 == 19:
+            log(f'[{epoch + 1}, {batch_idx + 1:5d}] loss: {step.pop_loss() / 20:.3f}')
+        dt = time.perf_counter_ns() - start_time
+        stats["iter_ns"].append(dt)
+        if 0 < batch_idx < 40:
+            total_time += dt
+        if batch_idx == 39:
+            log(f'Total time for 1-39 iteration in ns: {total_time}')
+            log(f'Average time for 1-39 iteration in ns: {total_time / 39.0}')
+        if metrics is not None:
+            metrics.log(event="iter", epoch=epoch, batch=batch_idx, ns=dt)
+        if watchdog is not None:
+            watchdog.beat()
+    stats["total_1_39_ns"] = total_time
+    return stats
+
+
 def test_model(model, test_loader, criterion, device="cpu", log=print):
     model.eval()
     test_loss = 0

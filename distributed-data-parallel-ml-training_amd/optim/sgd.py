@@ -31,6 +31,14 @@ class FusedSGD(torch.optim.SGD):
     def _packs(self):
         return [p._ddp_amd_pack() for p in self.arena.params if hasattr(p, "_ddp_amd_pack")]
 
+    def repack(self):
+        """Rebuild every bf16 conv-weight copy from the fp32 master weights (after the master
+        weights were written outside the optimizer, e.g. a state rollback or checkpoint load)."""
+        descs = self._packs()
+        if descs and self.arena.data.is_cuda:
+            from ..ops.common import native, stream_handle
+            native().pack_conv_weights(descs, stream_handle())
+
     def _work_table(self):
         """Device work-item table of the fused SGD + re-pack kernel (rebuilt when the set of
         packed conv weights changes, e.g. after the model's fused plan is first built)."""

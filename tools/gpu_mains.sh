@@ -16,3 +16,11 @@ done
 timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
   --master-port 29631 part3/main.py --max-batches 45 > gpurun_out/part3_torchrun.log 2>&1 || { echo "torchrun part3 failed"; tail -8 gpurun_out/part3_torchrun.log; exit 1; }
 echo "== part3 (torchrun)"; tail -4 gpurun_out/part3_torchrun.log
+for p in part1 part3; do
+  if [ $p = part1 ]; then
+    timeout -k 10 240 python part1/main.py --graph --max-batches 45 > gpurun_out/${p}_graph.log 2>&1 || { echo "$p --graph failed"; tail -8 gpurun_out/${p}_graph.log; exit 1; }
+  else
+    timeout -k 10 240 python part3/main.py --graph --num-nodes 1 --rank 0 --master-ip 127.0.0.1 --master-port 29641 --max-batches 45 > gpurun_out/${p}_graph.log 2>&1 || { echo "$p --graph failed"; tail -8 gpurun_out/${p}_graph.log; exit 1; }
+  fi
+  echo "== $p --graph"; grep -v "amdgpu.ids\|socket.cpp" gpurun_out/${p}_graph.log | tail -5
+done
