@@ -141,6 +141,10 @@ class DistributedDataParallel(nn.Module):
             # bf16 gradient communication (PyTorch's bf16_compress_hook): half the xGMI bytes;
             # the fp32 arena keeps the bf16-rounded average. Default fp32 = the reference.
             self.reducer.set_comm_dtype(1 if grad_comm_dtype == "bf16" else 0)
+            # race-check mode (eager steps only — a host synchronise cannot be
+            # captured): synchronise after every bucket collective, so a stream-ordering bug
+            # shows up as a mismatch against the serial 2B path
+            self.reducer.set_debug_sync(os.environ.get("DDP_AMD_DEBUG_SYNC", "0") == "1")
             self._hook = register_grad_ready_hook(self._on_grad_ready)
         else:
             self.reducer = _PyReducer(comm, self.arena, cap, cap_first, average,

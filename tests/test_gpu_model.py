@@ -342,3 +342,32 @@ def test_ddp_no_sync_accumulates_on_gpu(native_ext):
     c = float(torch.dot(a, b) / (a.norm() * b.norm()))
     assert c > 0.98, c
     assert abs(float(a.norm()) / float(b.norm()) - 1) < 0.05
+
+
+def test_ddp_debug_sync_mode_matches(native_ext):
+    """Race-check mode (Reducer debug sync after every bucket, stand-in collectives on the comm
+    stream): gradients agree with the default single-stream DDP step."""
+    from ddp_amd.models import VGG11
+    from ddp_amd.engine import CrossEntropyLoss
+    from ddp_amd.optim import FusedSGD
+    from ddp_amd.parallel import DistributedDataParallel, RcclCommunicator
+    torch.manual_seed(0)
+    base = VGG11().cuda()
+    x = torch.randn(32, 3, 32, 32, device="cuda")
+    y = torch.randint(0, 10, (32,), device="cuda")
+    comm = RcclCommunicator(0, 1, 0)
+    grads = []
+    for debug in (False, True):
+        m = DistributedDataParallel(copy.deepcopy(base), comm, bucket_cap_mb=4.0,
+                                    overlap=debug)
+        m.reducer.set_emulate(debug)
+        m.reducer.set_debug_sync(debug)
+        opt = FusedSGD(m.parameters(), lr=0.1)
+        opt.zero_grad()
+        CrossEntropyLoss()(m(x), y).backward()
+        torch.cuda.synchronize()
+        grads.append(m.arena.grad.clone())
+        m.close()
+    a, b = grads
+    c = float(torch.dot(a, b) / (a.norm() * b.norm()))
+    assert c > 0.98, c
