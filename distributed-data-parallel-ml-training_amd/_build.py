@@ -67,7 +67,10 @@ def build(verbose=True, jobs=None):
     hipcc = _hipcc()
     os.makedirs(BUILD, exist_ok=True)
     inc = _includes()
-    common = ["-O3", "-std=c++17", "-fPIC", "-Wno-unused-result"]
+    # DDP_AMD_DEBUG_BUILD=1: -O1 -g and the DDP_DEVICE_CHECK bounds checks (common.h)
+    debug = os.environ.get("DDP_AMD_DEBUG_BUILD", "0") == "1"
+    common = (["-O1", "-g", "-DDDP_AMD_DEBUG"] if debug else ["-O3"]) + \
+        ["-std=c++17", "-fPIC", "-Wno-unused-result"]
     hdr_time = _newest_header()
     tasks = []
     for src in sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))):

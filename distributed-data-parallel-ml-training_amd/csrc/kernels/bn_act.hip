@@ -283,6 +283,7 @@ template <bool POOL, int IPT>
 __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
   constexpr int NP = POOL ? 4 : 1;
   __shared__ float red[8 * 256];
+  DDP_DEVICE_CHECK(a.C % 8 == 0 && (!POOL || (a.H % 2 == 0 && a.W % 2 == 0)));
   const int G = a.C / 8;
   const int Gb = G < 256 ? G : 256;
   const int Ho = POOL ? a.H / 2 : a.H, Wo = POOL ? a.W / 2 : a.W;

@@ -13,6 +13,25 @@ typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kWave = 64;  // CDNA wavefront width (never 32)
 
+// Debug builds (DDP_AMD_DEBUG_BUILD=1 -> -DDDP_AMD_DEBUG, see _build.py): device-side bounds /
+// shape checks that print the failing condition and stop the offending thread's work. No-ops
+// in release builds. (GPU sanitizers are not available on this pool; this plus
+// HIP_LAUNCH_BLOCKING=1 localises a faulting kernel)
+#ifdef DDP_AMD_DEBUG
+#define DDP_DEVICE_CHECK(cond)                                                              \
+  do {                                                                                      \
+    if (!(cond)) {                                                                          \
+      printf("[ddp_amd debug] %s:%d check failed: %s (block %d thread %d)\n", __FILE__,     \
+             __LINE__, #cond, (int)blockIdx.x, (int)threadIdx.x);                           \
+      return;                                                                               \
+    }                                                                                       \
+  } while (0)
+#else
+#define DDP_DEVICE_CHECK(cond) \
+  do {                        \
+  } while (0)
+#endif
+
 // bf16 <-> fp32 bit conversions. round-to-nearest-even; NaN kept NaN.
 __device__ __forceinline__ float bf2f(unsigned short h) {
   return __uint_as_float(((unsigned int)h) << 16);

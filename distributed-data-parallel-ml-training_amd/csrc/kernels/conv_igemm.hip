@@ -194,6 +194,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
   const int lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
+  DDP_DEVICE_CHECK(blockDim.x == 256 && args.g.C % 8 == 0 && args.g.K % 8 == 0);
+  DDP_DEVICE_CHECK(args.splits >= 1 && args.ksteps_per_split >= 1);
 
   // Persistent work loop: item = (split z, tile); a block walks items blockIdx.x, +gridDim.x, ...
   // and prefetches the first k-step of its NEXT item while it finishes (last MFMAs + epilogue)
