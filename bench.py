@@ -51,6 +51,12 @@ def parse():
     p.add_argument("--grad-comm", default="fp32", choices=["fp32", "bf16"],
                    help="DDP gradient all-reduce dtype (bf16 halves the xGMI bytes; default "
                         "fp32 = the reference's gradient precision)")
+    p.add_argument("--segmented", type=int, default=None,
+                   help="DDP: split the captured step at this fused stage and overlap the late "
+                        "layers' gradient all-reduce with the early layers' backward "
+                        "(engine/step.py SegmentedDDPStep); 0 = one graph, inline collectives. "
+                        "Default: 4 on >1 GPUs (VGG, fp32 gradients), else 0; env "
+                        "DDP_AMD_SEGMENTED overrides")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--train-size", type=int, default=None)
     p.add_argument("--json-out", default=None)
@@ -63,7 +69,7 @@ def main():
     import torch.distributed as dist
     import ddp_amd
     from ddp_amd.data import SyntheticCIFAR10, SyntheticImageNet, DeviceLoader
-    from ddp_amd.engine import TrainStep, CrossEntropyLoss
+    from ddp_amd.engine import TrainStep, SegmentedDDPStep, CrossEntropyLoss
     from ddp_amd.models import build
     from ddp_amd.optim import FusedSGD
     from ddp_amd.parallel import (DistributedDataParallel, RcclCommunicator, STRATEGIES,
@@ -105,7 +111,20 @@ def main():
         fn = STRATEGIES[args.strategy]
         sync = lambda m: fn(m, comm)  # noqa: E731
     opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
-    step = TrainStep(model, opt, criterion, loader, sync=sync, use_graph=not args.no_graph)
+    # Multi-GPU default: the late layers' bucket (89% of the gradient bytes) is all-reduced on a
+    # second stream while the early layers' backward runs (one-GPU study with a 32-CU stand-in
+    # collective at 100-300 GB/s: 1.11-1.36 ms inline vs 1.01-1.08 ms segmented,
+    # profiles/r1_segmented_overlap.md); one GPU has no collective to hide -> one graph.
+    if args.segmented is None:
+        args.segmented = int(os.environ.get("DDP_AMD_SEGMENTED", "4" if world > 1 else "0"))
+    segmented = (bool(args.segmented) and args.strategy == "ddp" and not resnet
+                 and args.grad_comm == "fp32" and not args.no_graph)
+    if segmented:
+        step = SegmentedDDPStep(model, opt, criterion, loader, split=args.segmented,
+                                emulate=int(os.environ.get("DDP_AMD_EMULATE_COMM", "0")),
+                                emulate_gbps=float(os.environ.get("DDP_AMD_EMULATE_COMM_GBPS", "0")))
+    else:
+        step = TrainStep(model, opt, criterion, loader, sync=sync, use_graph=not args.no_graph)
 
     graph_ok = False
     nwarm = max(args.warmup, 2)
@@ -173,7 +192,7 @@ def main():
                                 "gather_broadcast": "part2a gather/broadcast"}[args.strategy],
                    "hipgraph": graph_ok, "bucket_mb": args.bucket_mb,
                    "grad_comm": args.grad_comm,
-                   "comm": ("overlap-stream" if getattr(getattr(model, "reducer", None), "overlap",
+                   "comm": (f"segmented@{args.segmented}" if segmented else "overlap-stream" if getattr(getattr(model, "reducer", None), "overlap",
                                                          lambda: False)() else "inline"),
                    "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4) fused"},
         "train_loss_mean": round(loss, 4),

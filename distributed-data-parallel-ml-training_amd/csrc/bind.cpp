@@ -31,6 +31,27 @@ static void check(int rc, const char* what) {
   }
 }
 
+// Cross-stream ordering edge with a DEVICE-scope release: record on `from`, wait on `to`.
+// torch.cuda.Stream.wait_stream uses a default event, whose record is a system-scope release
+// (an L2 write-back of everything dirty) — measured ~15 us per edge between graph segments.
+// Both streams are on this GPU (and RCCL fences its own peer traffic), so device scope suffices.
+struct StreamLink {
+  hipEvent_t ev = nullptr;
+  StreamLink() {
+    check((int)hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventReleaseToDevice),
+          "hipEventCreateWithFlags");
+  }
+  ~StreamLink() {
+    if (ev) (void)hipEventDestroy(ev);
+  }
+  void link(uintptr_t from, uintptr_t to) {
+    check((int)hipEventRecord(ev, S(from)), "hipEventRecord");
+    check((int)hipStreamWaitEvent(S(to), ev, 0), "hipStreamWaitEvent");
+  }
+  void record(uintptr_t s) { check((int)hipEventRecord(ev, S(s)), "hipEventRecord"); }
+  void wait(uintptr_t s) { check((int)hipStreamWaitEvent(S(s), ev, 0), "hipStreamWaitEvent"); }
+};
+
 static ddp_amd::ConvGeom geom(py::tuple g) {
   if (g.size() != 12 && g.size() != 13) throw std::runtime_error("conv geometry needs 12/13 ints");
   ddp_amd::ConvGeom c;
@@ -251,6 +272,9 @@ PYBIND11_MODULE(_native, m) {
   m.def("mean_ws", [](uintptr_t in, size_t n, int ws, uintptr_t out, uintptr_t st) {
     check(ddp_mean_ws(P<float>(in), n, ws, P<float>(out), S(st)), "mean_ws");
   });
+  m.def("comm_standin", [](uintptr_t x, size_t n, int blocks, float usec, float scale, uintptr_t st) {
+    check(ddp_comm_standin(P<float>(x), n, blocks, usec, scale, S(st)), "comm_standin");
+  });
   m.def("scale", [](uintptr_t x, size_t n, float s, uintptr_t st) {
     check(ddp_scale(P<float>(x), n, s, S(st)), "scale");
   });
@@ -265,6 +289,11 @@ PYBIND11_MODULE(_native, m) {
   });
   m.def("make_unique_id", []() { return py::bytes(RcclComm::make_unique_id()); });
 
+  py::class_<StreamLink>(m, "StreamLink")
+      .def(py::init<>())
+      .def("link", &StreamLink::link)
+      .def("record", &StreamLink::record)
+      .def("wait", &StreamLink::wait);
   py::class_<RcclComm>(m, "RcclComm")
       .def(py::init([](int rank, int world, std::string uid, int device) {
              // ncclCommInitRank blocks until every rank joins: release the GIL meanwhile
@@ -318,6 +347,8 @@ PYBIND11_MODULE(_native, m) {
       .def("set_overlap", &Reducer::set_overlap)
       .def("overlap", &Reducer::overlap)
       .def("set_emulate", &Reducer::set_emulate)
+      .def("set_emulate_passes", &Reducer::set_emulate_passes)
+      .def("set_emulate_bw", &Reducer::set_emulate_bw, py::arg("gbps"), py::arg("blocks") = 32)
       .def("set_comm_dtype", &Reducer::set_comm_dtype)
       .def("comm_dtype", &Reducer::comm_dtype)
       .def("launched", &Reducer::launched)

@@ -5,6 +5,9 @@
 //           part2/part2a/main.py:108).
 // scale   : x *= s (2B's `param.grad /= world_size`, part2/part2b/main.py:103, when the
 //           backend has no native average).
+// comm_standin : world-1 stand-in for a collective (overlap studies on one GPU): a few blocks
+//           (like RCCL's channels) make one read+write pass over the bucket, then hold their
+//           CUs until the modelled transfer time has elapsed (s_sleep on the constant clock).
 // pack / unpack bf16 : fp32 gradient bucket <-> bf16 communication buffer (DDP with
 //           grad_comm_dtype="bf16": half the bytes on the xGMI links; like PyTorch's
 //           bf16_compress_hook). Round-to-nearest-even on the way in, exact widening back.
@@ -27,6 +30,23 @@ __global__ __launch_bounds__(256) void mean_ws_kernel(const float* __restrict__ 
 __global__ __launch_bounds__(256) void scale_kernel(float* x, size_t n, float s) {
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += stride) x[i] *= s;
+}
+
+__global__ __launch_bounds__(256) void comm_standin_kernel(float* x, size_t n, long long ticks,
+                                                           float scale) {
+  // hold the CU for the modelled transfer time, THEN write the bucket (x *= scale): with
+  // scale != 1 a consumer that does not wait for the collective reads the old values (tests)
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(4);
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n / 4; i += stride) {
+    float4 v = reinterpret_cast<float4*>(x)[i];
+    v.x *= scale; v.y *= scale; v.z *= scale; v.w *= scale;
+    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));  // keep the store at scale 1
+    reinterpret_cast<float4*>(x)[i] = v;
+  }
+  if (blockIdx.x == 0)
+    for (size_t i = (n / 4) * 4 + threadIdx.x; i < n; i += blockDim.x) x[i] *= scale;
 }
 
 __global__ __launch_bounds__(256) void pack_bf16_kernel(const float* __restrict__ x, size_t n,
@@ -77,6 +97,22 @@ extern "C" int ddp_mean_ws(const float* in, size_t n, int ws, float* out, hipStr
 
 extern "C" int ddp_scale(float* x, size_t n, float s, hipStream_t st) {
   hipLaunchKernelGGL(scale_kernel, dim3(blocks_for(n)), dim3(256), 0, st, x, n, s);
+  return (int)hipGetLastError();
+}
+
+extern "C" int ddp_comm_standin(float* x, size_t n, int blocks, float usec, float scale,
+                                hipStream_t st) {
+  static int khz = 0;  // constant "wall clock" rate (kHz), queried once (first call is eager)
+  if (khz == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
+      khz = 100000;
+  }
+  if ((uintptr_t)x % 16) return -1;
+  const long long ticks = (long long)((double)usec * khz / 1000.0);
+  hipLaunchKernelGGL(comm_standin_kernel, dim3(blocks < 1 ? 1 : blocks), dim3(256), 0, st, x, n, ticks,
+                     scale);
   return (int)hipGetLastError();
 }
 

@@ -276,8 +276,15 @@ void Reducer::launch_ready() {
     } else if (emulate_) {
       // world 1 stand-in for the collective (graph-structure / overlap studies on one GPU):
       // one pass over the bucket, like the reduction kernel of an all-reduce
-      const int rc = ddp_scale(buf, bs.count, 1.0f, target);
-      if (rc != 0) throw std::runtime_error("emulated collective launch failed");
+      if (emulate_gbps_ > 0.0) {
+        const float us = (float)(4.0 * bs.count / (emulate_gbps_ * 1e3));
+        if (ddp_comm_standin(buf, bs.count, emulate_blocks_, us, 1.0f, target) != 0)
+          throw std::runtime_error("emulated collective launch failed");
+      } else {
+        for (int i = 0; i < emulate_passes_; ++i)
+          if (ddp_scale(buf, bs.count, 1.0f, target) != 0)
+            throw std::runtime_error("emulated collective launch failed");
+      }
     }
     done_stream_[b] = target;
     HIP_OK(hipEventRecord(done_ev_[b], target));

@@ -81,6 +81,10 @@ class Reducer {
   // world 1 only: run a bucket-sized pass in place of each (no-op) collective, so the graph
   // shape and stream traffic of a multi-GPU step can be studied on one GPU
   void set_emulate(bool on) { emulate_ = on; }
+  // stand-in collective length: number of bucket-sized passes per emulated collective
+  void set_emulate_passes(int n) { emulate_passes_ = n < 1 ? 1 : n; }
+  // or: a timed stand-in (ddp_comm_standin) lasting bytes / gbps on `blocks` CUs (gbps > 0)
+  void set_emulate_bw(double gbps, int blocks) { emulate_gbps_ = gbps; emulate_blocks_ = blocks; }
   // Gradient communication dtype: 0 = fp32 (default, the reference's), 1 = bf16 — each bucket
   // is packed into a bf16 staging buffer, all-reduced (avg) in bf16 (half the xGMI bytes) and
   // widened back into the fp32 arena. Allocates the staging buffer (call before capture).
@@ -107,6 +111,9 @@ class Reducer {
   bool debug_sync_ = false;
   bool overlap_ = true;
   bool emulate_ = false;
+  int emulate_passes_ = 1;
+  double emulate_gbps_ = 0.0;
+  int emulate_blocks_ = 32;
   bool comm_bf16_ = false;
   unsigned short* stage_ = nullptr;  // bf16 staging buffer, arena-sized
   hipStream_t comm_stream_ = nullptr;

@@ -131,3 +131,144 @@ class TrainStep:
         v = float(self.loss_sum.item())
         self.loss_sum.zero_()
         return v
+
+
+class SegmentedDDPStep(TrainStep):
+    """DDP step as three captured graphs with the late layers' gradient all-reduce overlapped
+    with the early layers' backward, launched on a second stream BETWEEN the graphs.
+
+    Why: one captured graph whose comm-stream branch stays open across the backward runs 2.4-3x
+    slower on ROCm 7 (profiles/r1_comm_stream_study.md: the graph executor spreads it over
+    several hardware queues); graph segments joined by event edges keep every segment a fast
+    single-queue graph.
+
+        g1: augment + forward (cut after stage ``split``) + backward of the late stages
+        --  comm stream waits for g1 (device-scope event), all-reduces bucket A = the late
+            stages' gradients (VGG-11 split 4: stages 4-7 + fc1, 89% of the bytes) on a SECOND
+            RCCL communicator, records event A                          ... overlaps ...
+        g2: backward of the early stages + bucket B (early stages) all-reduced inline on the
+            DDP communicator
+        --  the main stream waits for event A
+        g3: fused SGD (+ gradient clear, data-cursor advance)
+
+    Measured on one MI355X with a 32-CU stand-in collective (DDP_AMD_EMULATE_COMM_GBPS,
+    profiles/r1_segmented_overlap.md). Two communicators because the two buckets' collectives
+    may run concurrently on two streams; each is issued in the same order on every rank.
+    The DDP wrapper's own reducer is bypassed (``no_sync`` during the segments); the arena is in
+    parameter order, so the late stages are its tail. Models provide ``forward_loss_split`` /
+    ``first_param_of_stage`` (models/vgg.py). World size 1: the collectives are no-ops unless
+    ``emulate`` > 0 (bucket-sized stand-in passes) or ``emulate_gbps`` > 0 (a 32-CU stand-in
+    lasting bytes / emulate_gbps that then multiplies the bucket by ``emulate_scale``).
+    (Folding g3 into g2 behind a captured hipEventWaitExternal node would save one graph
+    boundary, ~14 us, but that capture crashes inside HIP on ROCm 7.2.)
+    """
+
+    def __init__(self, ddp, optimizer, criterion, loader, split=4, emulate=0, emulate_gbps=0.0,
+                 emulate_scale=1.0):
+        super().__init__(ddp, optimizer, criterion, loader, sync=None, use_graph=True)
+        from ..ops.common import native
+        inner = getattr(ddp, "module", None)
+        if inner is None or not hasattr(inner, "forward_loss_split") or not self.fold_opt:
+            raise ValueError("SegmentedDDPStep needs a DDP-wrapped model with forward_loss_split, "
+                             "the fused optimizer and the device loader")
+        self.ddp, self.split, self.emulate = ddp, split, int(emulate)
+        self.emulate_gbps, self.emulate_scale = float(emulate_gbps), float(emulate_scale)
+        arena = ddp.arena
+        first = inner.first_param_of_stage(split)
+        idx = next(i for i, p in enumerate(arena.params) if p is first)
+        self.cut = arena.offsets[idx]
+        self.total = arena.total
+        self.comm_stream = torch.cuda.Stream()
+        self.comm_a = None
+        if ddp.comm.world > 1:
+            from ..parallel.comm import RcclCommunicator
+            self.comm_a = RcclCommunicator(ddp.comm.rank, ddp.comm.world, ddp.comm.device,
+                                           key="ddp_amd/rccl_uid_overlap")
+        self._fork = native().StreamLink()   # main -> comm stream (g1 done)
+        self._done = native().StreamLink()   # comm stream -> main (bucket A reduced)
+        self.graphs = None
+        self._h = self._h_leaf = None
+
+    def _allreduce(self, lo, hi, stream, comm):
+        from ..ops.common import native
+        from ..parallel.comm import AVG
+        g = self.ddp.arena.grad
+        n = hi - lo
+        if comm is not None:
+            comm.comm.all_reduce(g.data_ptr() + 4 * lo, n, 0, AVG, stream.cuda_stream)
+        elif self.emulate_gbps > 0:  # timed 32-CU stand-in (comm_util.hip comm_standin)
+            native().comm_standin(g.data_ptr() + 4 * lo, n, 32, 4.0 * n / (self.emulate_gbps * 1e3),
+                                  self.emulate_scale, stream.cuda_stream)
+        else:
+            for _ in range(self.emulate):
+                native().scale(g.data_ptr() + 4 * lo, n, 1.0, stream.cuda_stream)
+
+    def _seg1(self):
+        self.ddp._sync_buffers()  # what DDP.forward would do (no-op without buffers / at world 1)
+        with self.ddp.no_sync():
+            with trace_range("data"):
+                x, y = self.loader.fill(advance=False)
+            with trace_range("forward"):
+                loss, h, h_leaf = self.ddp.module.forward_loss_split(
+                    x, y, self.split, acc=self.loss_sum, transient=True)
+            with trace_range("backward_late"):
+                loss.backward(self._one)
+        self._h, self._h_leaf = h, h_leaf
+
+    def _comm_late(self):
+        """Eager, between the graphs: bucket A on the comm stream."""
+        main = torch.cuda.current_stream()
+        self._fork.link(main.cuda_stream, self.comm_stream.cuda_stream)
+        with trace_range("sync_late"):
+            self._allreduce(self.cut, self.total, self.comm_stream, self.comm_a)
+        self._done.record(self.comm_stream.cuda_stream)
+
+    def _seg2(self):
+        with self.ddp.no_sync():
+            with trace_range("backward_early"):
+                self._h.backward(self._h_leaf.grad)
+        self._h = self._h_leaf = None
+        main = torch.cuda.current_stream()
+        with trace_range("sync_early"):  # bucket B, inline on the DDP communicator
+            comm = self.ddp.comm if self.ddp.comm.world > 1 else None
+            self._allreduce(0, self.cut, main, comm)
+
+    def _join(self):
+        self._done.wait(torch.cuda.current_stream().cuda_stream)
+
+    def _seg3(self):
+        with trace_range("optimizer"):
+            self.optimizer.step(zero_grad=True, counter=self.loader.cursor_advance())
+
+    def _body(self):
+        self._seg1()
+        self._comm_late()
+        self._seg2()
+        self._join()
+        self._seg3()
+
+    def capture(self):
+        import torch.distributed as dist
+        torch.cuda.synchronize()
+        mode = "global"
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            mode = "thread_local"
+        pool = torch.cuda.graph_pool_handle()  # activations of g1 are read by g2
+        graphs = []
+        for seg in (self._seg1, self._seg2, self._seg3):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool, capture_error_mode=mode):
+                seg()
+            graphs.append(g)
+        self.graphs = graphs
+        self.graph = graphs[0]  # "captured" marker for the shared helpers
+
+    def step(self):
+        if self.graph is None:  # never captured, or validate_distributed fell back to eager
+            self._body()
+            return
+        self.graphs[0].replay()
+        self._comm_late()
+        self.graphs[1].replay()
+        self._join()
+        self.graphs[2].replay()

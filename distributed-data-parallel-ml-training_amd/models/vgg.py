@@ -115,6 +115,33 @@ class _VGG(nn.Module):
                                self.fc1.weight.shape[0], 0, 0, ptr(loss_acc), ptr(correct_acc),
                                stream_handle())
 
+    def forward_loss_split(self, x, labels, split, acc=None, transient=False):
+        """``forward_loss`` cut after fused stage ``split`` (GPU): returns (loss, h, h_leaf) with
+        ``h`` the output of stages[:split] and ``h_leaf = h.detach().requires_grad_()`` the input
+        of the rest. ``loss.backward()`` then produces the gradients of stages[split:] + fc1 (the
+        late layers, most of the gradient bytes) and ``h.backward(h_leaf.grad)`` those of the
+        early layers — two backward segments the DDP engine can put a collective between
+        (engine/step.py SegmentedDDPStep)."""
+        from ..ops.layers import conv_bn_act, to_nhwc_input, linear_cross_entropy
+        from ..ops.common import step_scratch
+        plan = self.fused_plan()
+        if not 0 < split < len(plan):
+            raise ValueError(f"split must be in 1..{len(plan) - 1}")
+        step_scratch(x.device).zero()
+        h = to_nhwc_input(x, IN_CHANNELS_PADDED)
+        for spec in plan[:split]:
+            h = conv_bn_act(h, spec)
+        h_leaf = h.detach().requires_grad_(True)
+        t = h_leaf
+        for spec in plan[split:]:
+            t = conv_bn_act(t, spec)
+        loss = linear_cross_entropy(t.view(t.shape[0], -1), self.fc1, labels, acc, transient)
+        return loss, h, h_leaf
+
+    def first_param_of_stage(self, i):
+        """Parameter that starts fused stage ``i`` in ``parameters()`` order (its conv weight)."""
+        return self.fused_plan()[i].conv.weight
+
     def forward_loss(self, x, labels, acc=None, transient=False):
         """``CrossEntropyLoss()(self(x), labels)`` with the classifier and the loss fused into one
         kernel on the GPU (engine/step.py uses it for the captured training step). ``acc`` (fp32

@@ -137,7 +137,14 @@ class DistributedDataParallel(nn.Module):
             if grad_comm_dtype not in ("fp32", "bf16"):
                 raise ValueError("grad_comm_dtype must be 'fp32' or 'bf16'")
             self.reducer.set_overlap(bool(overlap))
-            self.reducer.set_emulate(os.environ.get("DDP_AMD_EMULATE_COMM", "0") == "1")
+            # world-1 stand-in collectives (one-GPU studies of the multi-GPU step):
+            # DDP_AMD_EMULATE_COMM=N: N bucket-sized full-GPU passes per collective;
+            # DDP_AMD_EMULATE_COMM_GBPS=G: a 32-CU kernel lasting bytes/G (RCCL-like footprint)
+            emu = int(os.environ.get("DDP_AMD_EMULATE_COMM", "0"))
+            gbps = float(os.environ.get("DDP_AMD_EMULATE_COMM_GBPS", "0"))
+            self.reducer.set_emulate(emu > 0 or gbps > 0)
+            self.reducer.set_emulate_passes(max(emu, 1))
+            self.reducer.set_emulate_bw(gbps)
             # bf16 gradient communication (PyTorch's bf16_compress_hook): half the xGMI bytes;
             # the fp32 arena keeps the bf16-rounded average. Default fp32 = the reference.
             self.reducer.set_comm_dtype(1 if grad_comm_dtype == "bf16" else 0)

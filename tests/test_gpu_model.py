@@ -371,3 +371,64 @@ def test_ddp_debug_sync_mode_matches(native_ext):
     a, b = grads
     c = float(torch.dot(a, b) / (a.norm() * b.norm()))
     assert c > 0.98, c
+
+
+def test_segmented_ddp_step_matches_single_graph(native_ext):
+    """SegmentedDDPStep (three graphs, late-layer bucket collective on a second stream in
+    between) applies the same update as the single-graph TrainStep from the same state (same
+    model, optimizer and loader; eager and replayed), and advances the data cursor once. A slow
+    stand-in collective that doubles bucket A proves the optimizer waits for it: the replayed
+    step must see the doubled gradients exactly like the eager one."""
+    from ddp_amd.models import VGG11
+    from ddp_amd.engine import CrossEntropyLoss, TrainStep, SegmentedDDPStep
+    from ddp_amd.optim import FusedSGD
+    from ddp_amd.data import SyntheticCIFAR10, DeviceLoader
+    from ddp_amd.parallel import DistributedDataParallel, RcclCommunicator
+    torch.manual_seed(4)
+    m = DistributedDataParallel(VGG11().cuda(), RcclCommunicator(0, 1, 0), bucket_cap_mb=256.0,
+                                first_bucket_cap_mb=256.0)
+    opt = FusedSGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    ld = DeviceLoader(SyntheticCIFAR10(True, n=512), 64, "cuda")
+    crit = CrossEntropyLoss()
+    ts = TrainStep(m, opt, crit, ld)
+    ss = SegmentedDDPStep(m, opt, crit, ld, split=4, emulate_gbps=171.0)
+    slow = SegmentedDDPStep(m, opt, crit, ld, split=4, emulate_gbps=20.0, emulate_scale=2.0)
+    assert 0 < ss.cut < ss.total == m.arena.total
+    ts.warmup(2)
+    torch.cuda.synchronize()
+    snap = (m.arena.data.clone(), opt.momentum_buffer.clone(), ld.cursor.clone())
+
+    def run(fn):
+        m.arena.data.copy_(snap[0]); opt.momentum_buffer.copy_(snap[1]); ld.cursor.copy_(snap[2])
+        m.arena.grad.zero_()
+        for sp in m.module.fused_plan():
+            sp._packed_version = None
+            sp.maybe_pack()
+        torch.cuda.synchronize()
+        fn()
+        torch.cuda.synchronize()
+        assert int(ld.cursor.item()) == int(snap[2].item()) + 1
+        return m.arena.data - snap[0]
+
+    def cos(a, b):
+        return float(torch.dot(a, b) / (a.norm() * b.norm()))
+
+    ref, ref2 = run(ts._body), run(ts._body)
+    base = cos(ref, ref2)  # two executions differ by float-atomic ordering
+    seg = run(ss._body)
+    ss.warmup(1)
+    ss.capture()
+    graph = run(ss.step)
+    assert float(ref.norm()) > 0
+    for d in (seg, graph):
+        assert cos(ref, d) > min(0.99, base - 0.005), (cos(ref, d), base)
+        assert abs(float(d.norm()) / float(ref.norm()) - 1) < 0.02
+    slow_eager = run(slow._body)
+    slow.warmup(1)
+    slow.capture()
+    slow_graph = run(slow.step)
+    lo = ss.cut
+    assert float(slow_eager[lo:].norm()) / float(ref[lo:].norm()) > 1.3  # doubled grads seen
+    assert cos(slow_eager, slow_graph) > min(0.99, base - 0.005)
+    assert abs(float(slow_graph.norm()) / float(slow_eager.norm()) - 1) < 0.02
+    m.close()
