@@ -186,3 +186,15 @@ def buffers_worker(rank, world, port, q):
         import traceback
         q.put((rank, {"error": traceback.format_exc()}))
         raise
+
+
+def commbench_worker(rank, world, port, q):
+    try:
+        _init(rank, world, port)
+        from ddp_amd.parallel import TorchCommunicator
+        from ddp_amd.parallel.commbench import allreduce_sweep
+        rows = allreduce_sweep(TorchCommunicator(), [1 << 12, 1 << 16], iters=3, warmup=1)
+        q.put((rank, {"rows": rows}))
+    except Exception as e:  # pragma: no cover - surfaced by the parent
+        import traceback
+        q.put((rank, {"error": traceback.format_exc() + repr(e)}))

@@ -105,3 +105,16 @@ def test_ddp_broadcast_buffers_flat():
             assert torch.equal(b0[k], b1[k])
     assert float(b1["1.running_mean"].mean()) < 1.5  # started from rank 0's 1.0, not rank 1's 2.0
     assert float(b1["4.running_var"].mean()) < 15.0  # started from 10.0, not 20.0
+
+
+def test_allreduce_bandwidth_sweep():
+    """parallel/commbench.py (the tools/comm_bench.py sweep) on Gloo: correct sums, positive
+    timings, the same (max-over-ranks) numbers on every rank."""
+    from dist_helpers import commbench_worker
+    out = run_workers(commbench_worker, WORLD)
+    for r, v in out.items():
+        assert "error" not in v, v.get("error")
+        assert [row["bytes"] for row in v["rows"]] == [1 << 12, 1 << 16]
+        for row in v["rows"]:
+            assert row["correct"] and row["us"] > 0 and row["busbw_GBps"] > 0
+    assert out[0]["rows"] == out[1]["rows"]
