@@ -10,6 +10,7 @@ On a GPU the same program runs on the gfx950 kernels with the native RCCL commun
 on a CPU it runs on ATen + Gloo, exactly like the reference.
 """
 import functools
+import os
 
 import torch
 
@@ -69,10 +70,17 @@ def main(part, argv=None):
         # the first batches of the shard, like any other iteration would)
         # the warm-up steps train on the first batches: snapshot the training state and roll
         # it back after the capture, so the epoch starts exactly where the eager loop would
-        from .step import TrainStep
+        from .step import TrainStep, SegmentedDDPStep
         arena = model.arena if hasattr(model, "arena") else optimizer.arena
         snap = (arena.data.clone(), optimizer.momentum_buffer.clone())
-        step = TrainStep(model, optimizer, criterion, train_loader, sync=sync)
+        split = int(os.environ.get("DDP_AMD_SEGMENTED", "4"))
+        if (strategy == "ddp" and world > 1 and split > 0
+                and hasattr(model.module, "forward_loss_split")):
+            # late layers' bucket all-reduced on a second stream during the early backward
+            # (profiles/r1_segmented_overlap.md)
+            step = SegmentedDDPStep(model, optimizer, criterion, train_loader, split=split)
+        else:
+            step = TrainStep(model, optimizer, criterion, train_loader, sync=sync)
         step.warmup(2)
         step.capture()
         torch.cuda.synchronize()
