@@ -113,7 +113,7 @@ def main():
     opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
     # Multi-GPU default: the late layers' bucket (89% of the gradient bytes) is all-reduced on a
     # second stream while the early layers' backward runs (one-GPU study with a 32-CU stand-in
-    # collective at 100-300 GB/s: 1.11-1.36 ms inline vs 1.01-1.08 ms segmented,
+    # collective at 100-300 GB/s: 1.11-1.36 ms inline vs 0.95-1.01 ms segmented,
     # profiles/r1_segmented_overlap.md); one GPU has no collective to hide -> one graph.
     if args.segmented is None:
         args.segmented = int(os.environ.get("DDP_AMD_SEGMENTED", "4" if world > 1 else "0"))

@@ -275,6 +275,15 @@ PYBIND11_MODULE(_native, m) {
   m.def("comm_standin", [](uintptr_t x, size_t n, int blocks, float usec, float scale, uintptr_t st) {
     check(ddp_comm_standin(P<float>(x), n, blocks, usec, scale, S(st)), "comm_standin");
   });
+  m.def("flag_signal", [](uintptr_t flag, uintptr_t st) {
+    check(ddp_flag_signal(P<unsigned>(flag), S(st)), "flag_signal");
+  });
+  m.def("flag_wait", [](uintptr_t flag, uintptr_t expected, uintptr_t err, float timeout_s,
+                        uintptr_t st) {
+    check(ddp_flag_wait(P<unsigned>(flag), P<unsigned>(expected), P<unsigned>(err), timeout_s,
+                        S(st)),
+          "flag_wait");
+  });
   m.def("scale", [](uintptr_t x, size_t n, float s, uintptr_t st) {
     check(ddp_scale(P<float>(x), n, s, S(st)), "scale");
   });

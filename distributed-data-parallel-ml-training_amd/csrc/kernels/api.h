@@ -136,6 +136,9 @@ int ddp_colsum(const void* dl, int B, int J, float* db, hipStream_t st);
 int ddp_mean_ws(const float* in, size_t n, int ws, float* out, hipStream_t st);
 int ddp_scale(float* x, size_t n, float s, hipStream_t st);
 int ddp_comm_standin(float* x, size_t n, int blocks, float usec, float scale, hipStream_t st);
+int ddp_flag_signal(unsigned* flag, hipStream_t st);
+int ddp_flag_wait(const unsigned* flag, unsigned* expected, unsigned* err, float timeout_s,
+                  hipStream_t st);
 int ddp_pack_bf16(const float* x, size_t n, unsigned short* y, hipStream_t st);
 int ddp_unpack_bf16(const unsigned short* y, size_t n, float* x, hipStream_t st);
 }

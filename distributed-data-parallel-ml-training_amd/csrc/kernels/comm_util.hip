@@ -8,6 +8,11 @@
 // comm_standin : world-1 stand-in for a collective (overlap studies on one GPU): a few blocks
 //           (like RCCL's channels) make one read+write pass over the bucket, then hold their
 //           CUs until the modelled transfer time has elapsed (s_sleep on the constant clock).
+// flag_signal / flag_wait : device-side stream edge between the step graph and the comm stream
+//           (engine/step.py SegmentedDDPStep): signal = one agent-scope release increment of a
+//           counter; wait = one wave spins (s_sleep) until the counter reaches the next expected
+//           value (its own monotonic counter), acquire. Bounded: after `timeout` it records an
+//           error code and returns instead of hanging the GPU.
 // pack / unpack bf16 : fp32 gradient bucket <-> bf16 communication buffer (DDP with
 //           grad_comm_dtype="bf16": half the bytes on the xGMI links; like PyTorch's
 //           bf16_compress_hook). Round-to-nearest-even on the way in, exact widening back.
@@ -47,6 +52,27 @@ __global__ __launch_bounds__(256) void comm_standin_kernel(float* x, size_t n, l
   }
   if (blockIdx.x == 0)
     for (size_t i = (n / 4) * 4 + threadIdx.x; i < n; i += blockDim.x) x[i] *= scale;
+}
+
+__global__ __launch_bounds__(64) void flag_signal_kernel(unsigned* flag) {
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(64) void flag_wait_kernel(const unsigned* flag, unsigned* expected,
+                                                       unsigned* err, long long timeout_ticks) {
+  if (threadIdx.x != 0) return;
+  // vector load/store of the private counter (never a scalar-cache read of a value this kernel
+  // itself rewrites every launch)
+  const unsigned target = __hip_atomic_load(expected, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  __hip_atomic_store(expected, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const long long t0 = wall_clock64();
+  while ((int)(__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+    if (wall_clock64() - t0 > timeout_ticks) {
+      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
 }
 
 __global__ __launch_bounds__(256) void pack_bf16_kernel(const float* __restrict__ x, size_t n,
@@ -90,6 +116,17 @@ static unsigned blocks_for(size_t n) {
   return (unsigned)b;
 }
 
+static int wall_khz() {
+  static int khz = 0;
+  if (khz == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
+      khz = 100000;
+  }
+  return khz;
+}
+
 extern "C" int ddp_mean_ws(const float* in, size_t n, int ws, float* out, hipStream_t st) {
   hipLaunchKernelGGL(mean_ws_kernel, dim3(blocks_for(n)), dim3(256), 0, st, in, n, ws, out);
   return (int)hipGetLastError();
@@ -102,17 +139,23 @@ extern "C" int ddp_scale(float* x, size_t n, float s, hipStream_t st) {
 
 extern "C" int ddp_comm_standin(float* x, size_t n, int blocks, float usec, float scale,
                                 hipStream_t st) {
-  static int khz = 0;  // constant "wall clock" rate (kHz), queried once (first call is eager)
-  if (khz == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
-      khz = 100000;
-  }
+  const int khz = wall_khz();
   if ((uintptr_t)x % 16) return -1;
   const long long ticks = (long long)((double)usec * khz / 1000.0);
   hipLaunchKernelGGL(comm_standin_kernel, dim3(blocks < 1 ? 1 : blocks), dim3(256), 0, st, x, n, ticks,
                      scale);
+  return (int)hipGetLastError();
+}
+
+extern "C" int ddp_flag_signal(unsigned* flag, hipStream_t st) {
+  hipLaunchKernelGGL(flag_signal_kernel, dim3(1), dim3(64), 0, st, flag);
+  return (int)hipGetLastError();
+}
+
+extern "C" int ddp_flag_wait(const unsigned* flag, unsigned* expected, unsigned* err,
+                             float timeout_s, hipStream_t st) {
+  const long long ticks = (long long)((double)timeout_s * wall_khz() * 1000.0);
+  hipLaunchKernelGGL(flag_wait_kernel, dim3(1), dim3(64), 0, st, flag, expected, err, ticks);
   return (int)hipGetLastError();
 }
 

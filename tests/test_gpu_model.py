@@ -373,8 +373,9 @@ def test_ddp_debug_sync_mode_matches(native_ext):
     assert c > 0.98, c
 
 
-def test_segmented_ddp_step_matches_single_graph(native_ext):
-    """SegmentedDDPStep (three graphs, late-layer bucket collective on a second stream in
+@pytest.mark.parametrize("mode", ["flags", "events"])
+def test_segmented_ddp_step_matches_single_graph(native_ext, mode):
+    """SegmentedDDPStep (one graph + device flags, or three graphs + events; late-layer bucket collective on a second stream in
     between) applies the same update as the single-graph TrainStep from the same state (same
     model, optimizer and loader; eager and replayed), and advances the data cursor once. A slow
     stand-in collective that doubles bucket A proves the optimizer waits for it: the replayed
@@ -391,9 +392,11 @@ def test_segmented_ddp_step_matches_single_graph(native_ext):
     ld = DeviceLoader(SyntheticCIFAR10(True, n=512), 64, "cuda")
     crit = CrossEntropyLoss()
     ts = TrainStep(m, opt, crit, ld)
-    ss = SegmentedDDPStep(m, opt, crit, ld, split=4, emulate_gbps=171.0)
-    slow = SegmentedDDPStep(m, opt, crit, ld, split=4, emulate_gbps=20.0, emulate_scale=2.0)
+    ss = SegmentedDDPStep(m, opt, crit, ld, split=4, emulate_gbps=171.0, mode=mode)
+    slow = SegmentedDDPStep(m, opt, crit, ld, split=4, emulate_gbps=20.0, emulate_scale=2.0,
+                            mode=mode)
     assert 0 < ss.cut < ss.total == m.arena.total
+    ss.WAIT_TIMEOUT_S = slow.WAIT_TIMEOUT_S = 20.0  # a broken edge fails in seconds, not minutes
     ts.warmup(2)
     torch.cuda.synchronize()
     snap = (m.arena.data.clone(), opt.momentum_buffer.clone(), ld.cursor.clone())
@@ -431,4 +434,6 @@ def test_segmented_ddp_step_matches_single_graph(native_ext):
     assert float(slow_eager[lo:].norm()) / float(ref[lo:].norm()) > 1.3  # doubled grads seen
     assert cos(slow_eager, slow_graph) > min(0.99, base - 0.005)
     assert abs(float(slow_graph.norm()) / float(slow_eager.norm()) - 1) < 0.02
+    for st in (ss, slow):
+        st.check_error()
     m.close()

@@ -11,9 +11,10 @@ echo "|---|---|---|"
 for i in 1 2; do
 b base "DDP_AMD_EMULATE_COMM=0"
 b seg4_nocomm "DDP_AMD_EMULATE_COMM=0" --segmented 4
+b seg4_nocomm_events "DDP_AMD_SEG_MODE=events" --segmented 4
 for g in 300 171 100; do
 b inline_$g "DDP_AMD_EMULATE_COMM_GBPS=$g"
 b seg4_$g "DDP_AMD_EMULATE_COMM_GBPS=$g" --segmented 4
-b seg3_$g "DDP_AMD_EMULATE_COMM_GBPS=$g" --segmented 3
+b seg4_events_$g "DDP_AMD_SEG_MODE=events DDP_AMD_EMULATE_COMM_GBPS=$g" --segmented 4
 done
 done

@@ -37,12 +37,13 @@ def main():
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--priority", type=int, default=0, help="side stream priority (-1 = high)")
     ap.add_argument("--segmented", action="store_true")
+    ap.add_argument("--nseg", type=int, default=8)
     ap.add_argument("--join-end", action="store_true", help="fork often, join once at the end")
     a = ap.parse_args()
     global JOIN_END
     JOIN_END = a.join_end
     if a.segmented:
-        segmented(a.nk, 8, a.iters)
+        segmented(a.nk, a.nseg, a.iters)
         return
     dev = torch.device("cuda", 0)
     x = torch.ones(1 << 16, device=dev)
@@ -100,8 +101,20 @@ def segmented(nk=80, nseg=8, iters=200):
             for _ in range(per):
                 x.mul_(1.0001)
         graphs.append(g)
+    single = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(single, pool=pool):
+        for _ in range(per * nseg):
+            x.mul_(1.0001)
     main = torch.cuda.current_stream()
     res = {}
+    for rep in range(2):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        n = 10 if rep == 0 else iters
+        for _ in range(n):
+            single.replay()
+        torch.cuda.synchronize()
+        res["single"] = (time.perf_counter() - t0) / n * 1e6
     for mode in ("segments_only", "segments_side"):
         for rep in range(2):
             torch.cuda.synchronize()
