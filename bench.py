@@ -51,7 +51,7 @@ def parse():
     p.add_argument("--grad-comm", default="fp32", choices=["fp32", "bf16"],
                    help="DDP gradient all-reduce dtype (bf16 halves the xGMI bytes; default "
                         "fp32 = the reference's gradient precision)")
-    p.add_argument("--segmented", type=int, default=None,
+    p.add_argument("--segmented", default=None,
                    help="DDP: split the captured step at this fused stage and overlap the late "
                         "layers' gradient all-reduce with the early layers' backward "
                         "(engine/step.py SegmentedDDPStep); 0 = one graph, inline collectives. "
@@ -113,14 +113,14 @@ def main():
     opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
     # Multi-GPU default: the late layers' bucket (89% of the gradient bytes) is all-reduced on a
     # second stream while the early layers' backward runs (one-GPU study with a 32-CU stand-in
-    # collective at 100-300 GB/s: 1.11-1.36 ms inline vs 0.95-1.01 ms segmented,
+    # collective at 100-300 GB/s: 1.11-1.36 ms inline vs 0.96-1.01 ms segmented,
     # profiles/r1_segmented_overlap.md); one GPU has no collective to hide -> one graph.
     if args.segmented is None:
-        args.segmented = int(os.environ.get("DDP_AMD_SEGMENTED", "4" if world > 1 else "0"))
-    segmented = (bool(args.segmented) and args.strategy == "ddp" and not resnet
+        args.segmented = os.environ.get("DDP_AMD_SEGMENTED", "4" if world > 1 else "0")
+    segmented = (int(args.segmented) > 0 and args.strategy == "ddp" and not resnet
                  and args.grad_comm == "fp32" and not args.no_graph)
     if segmented:
-        step = SegmentedDDPStep(model, opt, criterion, loader, split=args.segmented,
+        step = SegmentedDDPStep(model, opt, criterion, loader, split=int(args.segmented),
                                 emulate=int(os.environ.get("DDP_AMD_EMULATE_COMM", "0")),
                                 emulate_gbps=float(os.environ.get("DDP_AMD_EMULATE_COMM_GBPS", "0")))
     else:

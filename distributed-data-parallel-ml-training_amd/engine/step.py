@@ -134,52 +134,49 @@ class TrainStep:
 
 
 class SegmentedDDPStep(TrainStep):
-    """DDP step with the late layers' gradient all-reduce overlapped with the early layers'
-    backward, without a comm branch inside the captured graph.
+    """DDP step whose late-layer gradient all-reduce overlaps the early layers' backward,
+    without a comm branch inside a captured graph.
 
     Why: one captured graph whose comm-stream branch stays open across the backward runs 2.4-3x
     slower on ROCm 7 (profiles/r1_comm_stream_study.md: the graph executor spreads it over
-    several hardware queues). Here the graph stays single-stream and the bucket collective is
-    issued EAGERLY on a second stream, ordered against the graph by device-side flags
-    (comm_util.hip flag_signal / flag_wait: a release increment and a bounded one-wave spin):
+    several hardware queues). Here the step is two single-stream graphs:
 
-        comm stream (enqueued before the graph):  wait(F1) -> all-reduce bucket A -> signal(FA)
-        main stream, ONE graph:  augment + forward + backward of stages >= split -> signal(F1)
-                                 -> backward of stages < split -> all-reduce bucket B inline
-                                 -> wait(FA) -> fused SGD (+ grad clear, cursor advance)
+        g1 (main):  augment + forward + backward of the stages >= ``split`` -> flag_signal(S)
+        eager:      comm stream: flag_wait(S) -> all-reduce bucket A (those stages' gradients,
+                    VGG-11 split 4: 89% of the bytes; SECOND RCCL communicator) -> flag_signal(D)
+        g2 (main):  backward of the stages < split -> all-reduce bucket B inline (DDP
+                    communicator) -> flag_wait(D) -> fused SGD (+ grad clear, cursor advance)
 
-    Bucket A (VGG-11 split 4: stages 4-7 + fc1) is 89% of the gradient bytes. It runs on a
-    SECOND RCCL communicator, so the two buckets' collectives may be in flight at once on two
-    streams; every rank issues both in the same order. ``mode="events"`` is the earlier variant
-    — three graphs with event edges between them, ~38 us of graph boundaries per step
-    (profiles/r1_segmented_overlap.md).
+    flag_signal / flag_wait (comm_util.hip) are an agent-scope release increment and a bounded
+    one-wave spin (on timeout it records an error and returns) — cheaper than event edges
+    between graph launches (~15 us idle per edge measured). Deadlock-free however HIP maps
+    streams onto hardware queues: every wait's producer is enqueued before the wait in host
+    order (the comm stream's wait follows g1's launch, g2's wait follows the all-reduce's
+    launch), so a queue shared by producer and waiter holds the producer first. (A single-graph
+    variant — comm work enqueued before the graph — measured faster but has the comm-side spin
+    enqueued BEFORE its producer: on a shared hardware queue it deadlocks.)
 
     The DDP wrapper's own reducer is bypassed (``no_sync``); the arena is in parameter order, so
-    the late stages are its tail. Models provide ``forward_loss_split`` /
-    ``first_param_of_stage`` (models/vgg.py). World size 1: the collectives are no-ops unless
-    ``emulate`` > 0 (bucket-sized stand-in passes) or ``emulate_gbps`` > 0 (a 32-CU stand-in
-    lasting bytes / emulate_gbps that then multiplies the bucket by ``emulate_scale``), for
-    overlap studies on one GPU.
+    bucket A is its tail. Models provide ``forward_loss_split`` / ``first_param_of_stage``
+    (models/vgg.py). Measured with a 32-CU stand-in collective: profiles/r1_segmented_overlap.md.
+    World size 1: the collectives are no-ops unless ``emulate`` > 0 (bucket-sized stand-in
+    passes) or ``emulate_gbps`` > 0 (a 32-CU stand-in lasting bytes / emulate_gbps that then
+    multiplies the bucket by ``emulate_scale``: an optimizer that did not wait would miss it).
     """
 
     WAIT_TIMEOUT_S = 100.0  # a device-side wait that exceeds this records an error and returns
 
     def __init__(self, ddp, optimizer, criterion, loader, split=4, emulate=0, emulate_gbps=0.0,
-                 emulate_scale=1.0, mode=None):
+                 emulate_scale=1.0):
         super().__init__(ddp, optimizer, criterion, loader, sync=None, use_graph=True)
-        import os
-        from ..ops.common import native
         inner = getattr(ddp, "module", None)
         if inner is None or not hasattr(inner, "forward_loss_split") or not self.fold_opt:
             raise ValueError("SegmentedDDPStep needs a DDP-wrapped model with forward_loss_split, "
                              "the fused optimizer and the device loader")
-        self.ddp, self.split, self.emulate = ddp, split, int(emulate)
+        self.ddp, self.split, self.emulate = ddp, int(split), int(emulate)
         self.emulate_gbps, self.emulate_scale = float(emulate_gbps), float(emulate_scale)
-        self.mode = mode or os.environ.get("DDP_AMD_SEG_MODE", "flags")
-        if self.mode not in ("flags", "events"):
-            raise ValueError("mode must be 'flags' or 'events'")
         arena = ddp.arena
-        first = inner.first_param_of_stage(split)
+        first = inner.first_param_of_stage(self.split)
         idx = next(i for i, p in enumerate(arena.params) if p is first)
         self.cut = arena.offsets[idx]
         self.total = arena.total
@@ -189,19 +186,17 @@ class SegmentedDDPStep(TrainStep):
             from ..parallel.comm import RcclCommunicator
             self.comm_a = RcclCommunicator(ddp.comm.rank, ddp.comm.world, ddp.comm.device,
                                            key="ddp_amd/rccl_uid_overlap")
-            # connect the second communicator now (its first collective sets up the transports,
-            # which must not count against the device-side wait timeout)
+            # connect the communicator now: its first collective sets up the transports, which
+            # must not count against the device-side wait timeout
             warm = torch.zeros(64, dtype=torch.float32, device=loader.device)
             self.comm_a.all_reduce(warm)
             torch.cuda.synchronize()
-        # flags: [F1, FA, expected F1 (comm side), expected FA (main side), error]
+        # [0] = S (late backward done), [1] = D (bucket A reduced), [2], [3] = the waiters'
+        # expected counts, [4] = error word
         self._flags = torch.zeros(8, dtype=torch.int32, device=loader.device)
-        self._fork = native().StreamLink()   # events mode: main -> comm stream (g1 done)
-        self._done = native().StreamLink()   # events mode: comm stream -> main (bucket A)
         self.graphs = None
         self._h = self._h_leaf = None
 
-    # ------------------------------------------------------------ pieces
     def _fp(self, i):
         return self._flags.data_ptr() + 4 * i
 
@@ -220,32 +215,21 @@ class SegmentedDDPStep(TrainStep):
                 native().scale(g.data_ptr() + 4 * lo, n, 1.0, stream.cuda_stream)
 
     def _seg1(self):
+        from ..ops.common import native
         self.ddp._sync_buffers()  # what DDP.forward would do (no-op without buffers / at world 1)
         with self.ddp.no_sync():
             with trace_range("data"):
                 x, y = self.loader.fill(advance=False)
             with trace_range("forward"):
-                loss, h, h_leaf = self.ddp.module.forward_loss_split(
+                loss, cuts = self.ddp.module.forward_loss_split(
                     x, y, self.split, acc=self.loss_sum, transient=True)
             with trace_range("backward_late"):
                 loss.backward(self._one)
-        self._h, self._h_leaf = h, h_leaf
+        self._h, self._h_leaf = cuts[0]
+        native().flag_signal(self._fp(0), torch.cuda.current_stream().cuda_stream)
 
-    def _seg2(self):
-        with self.ddp.no_sync():
-            with trace_range("backward_early"):
-                self._h.backward(self._h_leaf.grad)
-        self._h = self._h_leaf = None
-        with trace_range("sync_early"):  # bucket B, inline on the DDP communicator
-            comm = self.ddp.comm if self.ddp.comm.world > 1 else None
-            self._allreduce(0, self.cut, torch.cuda.current_stream(), comm)
-
-    def _seg3(self):
-        with trace_range("optimizer"):
-            self.optimizer.step(zero_grad=True, counter=self.loader.cursor_advance())
-
-    def _comm_late_flags(self):
-        """Comm-stream work of one step, enqueued BEFORE the step's main-stream work."""
+    def _comm_late(self):
+        """Eager, between the graphs: wait S, bucket A on the comm stream, signal D."""
         from ..ops.common import native
         cs = self.comm_stream.cuda_stream
         native().flag_wait(self._fp(0), self._fp(2), self._fp(4), self.WAIT_TIMEOUT_S, cs)
@@ -253,37 +237,25 @@ class SegmentedDDPStep(TrainStep):
             self._allreduce(self.cut, self.total, self.comm_stream, self.comm_a)
         native().flag_signal(self._fp(1), cs)
 
-    def _main_flags(self):
-        """The step's main-stream work (captured as ONE graph)."""
+    def _seg2(self):
         from ..ops.common import native
-        self._seg1()
-        main = torch.cuda.current_stream().cuda_stream
-        native().flag_signal(self._fp(0), main)
-        self._seg2()
-        native().flag_wait(self._fp(1), self._fp(3), self._fp(4), self.WAIT_TIMEOUT_S, main)
-        self._seg3()
-
-    def _comm_late_events(self):
+        with self.ddp.no_sync():
+            with trace_range("backward_early"):
+                self._h.backward(self._h_leaf.grad)
+        self._h = self._h_leaf = None
         main = torch.cuda.current_stream()
-        self._fork.link(main.cuda_stream, self.comm_stream.cuda_stream)
-        with trace_range("sync_late"):
-            self._allreduce(self.cut, self.total, self.comm_stream, self.comm_a)
-        self._done.record(self.comm_stream.cuda_stream)
+        with trace_range("sync_early"):  # bucket B, inline on the DDP communicator
+            comm = self.ddp.comm if self.ddp.comm.world > 1 else None
+            self._allreduce(0, self.cut, main, comm)
+        native().flag_wait(self._fp(1), self._fp(3), self._fp(4), self.WAIT_TIMEOUT_S,
+                           main.cuda_stream)
+        with trace_range("optimizer"):
+            self.optimizer.step(zero_grad=True, counter=self.loader.cursor_advance())
 
-    def _join_events(self):
-        self._done.wait(torch.cuda.current_stream().cuda_stream)
-
-    # ------------------------------------------------------------ TrainStep interface
     def _body(self):
-        if self.mode == "flags":
-            self._comm_late_flags()
-            self._main_flags()
-        else:
-            self._seg1()
-            self._comm_late_events()
-            self._seg2()
-            self._join_events()
-            self._seg3()
+        self._seg1()
+        self._comm_late()
+        self._seg2()
 
     def capture(self):
         import torch.distributed as dist
@@ -292,10 +264,9 @@ class SegmentedDDPStep(TrainStep):
         mode = "global"
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             mode = "thread_local"
-        pool = torch.cuda.graph_pool_handle()  # (events mode) activations of g1 are read by g2
-        segs = (self._main_flags,) if self.mode == "flags" else (self._seg1, self._seg2, self._seg3)
+        pool = torch.cuda.graph_pool_handle()  # activations of g1 are read by g2
         graphs = []
-        for seg in segs:
+        for seg in (self._seg1, self._seg2):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool, capture_error_mode=mode):
                 seg()
@@ -307,18 +278,12 @@ class SegmentedDDPStep(TrainStep):
         if self.graph is None:  # never captured, or validate_distributed fell back to eager
             self._body()
             return
-        if self.mode == "flags":
-            self._comm_late_flags()
-            self.graphs[0].replay()
-        else:
-            self.graphs[0].replay()
-            self._comm_late_events()
-            self.graphs[1].replay()
-            self._join_events()
-            self.graphs[2].replay()
+        self.graphs[0].replay()
+        self._comm_late()
+        self.graphs[1].replay()
 
     def check_error(self):
-        """Raise if a device-side wait gave up (its peer never signalled within the timeout)."""
+        """Raise if the device-side wait gave up (bucket A never completed within the timeout)."""
         if int(self._flags[4].item()) != 0:
             raise RuntimeError("SegmentedDDPStep: a device-side stream wait timed out "
                                f"(> {self.WAIT_TIMEOUT_S}s); the step's results are invalid")

@@ -116,27 +116,32 @@ class _VGG(nn.Module):
                                stream_handle())
 
     def forward_loss_split(self, x, labels, split, acc=None, transient=False):
-        """``forward_loss`` cut after fused stage ``split`` (GPU): returns (loss, h, h_leaf) with
-        ``h`` the output of stages[:split] and ``h_leaf = h.detach().requires_grad_()`` the input
-        of the rest. ``loss.backward()`` then produces the gradients of stages[split:] + fc1 (the
-        late layers, most of the gradient bytes) and ``h.backward(h_leaf.grad)`` those of the
-        early layers — two backward segments the DDP engine can put a collective between
+        """``forward_loss`` cut after fused stage(s) ``split`` (GPU; an int or ascending list of
+        stage indices): returns (loss, cuts) with cuts[k] = (h_k, leaf_k), h_k the output of the
+        stages before split[k] and ``leaf_k = h_k.detach().requires_grad_()`` the input of the
+        stages from split[k] on. ``loss.backward()`` produces the gradients of the stages from
+        split[-1] (+ fc1) and ``h_k.backward(leaf_k.grad)`` for k = len-1 .. 0 those of each
+        earlier segment — backward segments the DDP engine can put collectives between
         (engine/step.py SegmentedDDPStep)."""
         from ..ops.layers import conv_bn_act, to_nhwc_input, linear_cross_entropy
         from ..ops.common import step_scratch
         plan = self.fused_plan()
-        if not 0 < split < len(plan):
-            raise ValueError(f"split must be in 1..{len(plan) - 1}")
+        splits = [split] if isinstance(split, int) else list(split)
+        if not splits or splits != sorted(set(splits)) or not 0 < splits[0] or splits[-1] >= len(plan):
+            raise ValueError(f"split stages must be ascending in 1..{len(plan) - 1}")
         step_scratch(x.device).zero()
         h = to_nhwc_input(x, IN_CHANNELS_PADDED)
-        for spec in plan[:split]:
-            h = conv_bn_act(h, spec)
-        h_leaf = h.detach().requires_grad_(True)
-        t = h_leaf
-        for spec in plan[split:]:
-            t = conv_bn_act(t, spec)
-        loss = linear_cross_entropy(t.view(t.shape[0], -1), self.fc1, labels, acc, transient)
-        return loss, h, h_leaf
+        cuts, prev = [], 0
+        for sp in splits + [len(plan)]:
+            for spec in plan[prev:sp]:
+                h = conv_bn_act(h, spec)
+            if sp < len(plan):
+                leaf = h.detach().requires_grad_(True)
+                cuts.append((h, leaf))
+                h = leaf
+            prev = sp
+        loss = linear_cross_entropy(h.view(h.shape[0], -1), self.fc1, labels, acc, transient)
+        return loss, cuts
 
     def first_param_of_stage(self, i):
         """Parameter that starts fused stage ``i`` in ``parameters()`` order (its conv weight)."""
