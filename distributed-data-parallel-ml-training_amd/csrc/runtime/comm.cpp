@@ -61,7 +61,7 @@ static ncclRedOp_t to_op(int op) {
 RcclComm::RcclComm(int rank, int world, const std::string& uid_bytes, int device)
     : rank_(rank), world_(world), device_(device) {
   HIP_OK(hipSetDevice(device));
-  if (world > 1) {
+  if (world > 1 || !uid_bytes.empty()) {
     if (uid_bytes.size() != sizeof(ncclUniqueId))
       throw std::runtime_error("bad ncclUniqueId size");
     ncclUniqueId id;
@@ -81,17 +81,17 @@ std::string RcclComm::make_unique_id() {
 }
 
 void RcclComm::all_reduce(void* buf, size_t count, int dtype, int op, hipStream_t st) {
-  if (world_ == 1 || count == 0) return;
+  if (comm_ == nullptr || count == 0) return;
   NCCL_OK(ncclAllReduce(buf, buf, count, to_nccl(dtype), to_op(op), comm_, st));
 }
 
 void RcclComm::broadcast(void* buf, size_t count, int dtype, int root, hipStream_t st) {
-  if (world_ == 1 || count == 0) return;
+  if (comm_ == nullptr || count == 0) return;
   NCCL_OK(ncclBroadcast(buf, buf, count, to_nccl(dtype), root, comm_, st));
 }
 
 void RcclComm::all_gather(const void* send, void* recv, size_t count, int dtype, hipStream_t st) {
-  if (world_ == 1) {
+  if (comm_ == nullptr) {
     if (send != recv) HIP_OK(hipMemcpyAsync(recv, send, count * dtype_bytes(dtype), hipMemcpyDeviceToDevice, st));
     return;
   }
@@ -100,7 +100,7 @@ void RcclComm::all_gather(const void* send, void* recv, size_t count, int dtype,
 
 void RcclComm::reduce_scatter(const void* send, void* recv, size_t count, int dtype, int op,
                               hipStream_t st) {
-  if (world_ == 1) {
+  if (comm_ == nullptr) {
     if (send != recv) HIP_OK(hipMemcpyAsync(recv, send, count * dtype_bytes(dtype), hipMemcpyDeviceToDevice, st));
     return;
   }
@@ -254,7 +254,7 @@ void Reducer::launch_ready() {
     // overlap: the collective runs on the comm stream; inline: on the stream that completed the
     // bucket (stream order = no cross-stream edge in a captured graph)
     // (world 1 without emulation has no collective: nothing to order against)
-    const bool real = comm_->world() > 1 || emulate_;
+    const bool real = comm_->live() || emulate_;
     hipStream_t target = (overlap_ && real) ? comm_stream_ : contrib_[b].back();
     for (size_t i = 0; i < contrib_[b].size(); ++i) {
       if (contrib_[b][i] == target) continue;
@@ -268,10 +268,10 @@ void Reducer::launch_ready() {
       unsigned short* sb = stage_ + bs.offset;
       if (ddp_pack_bf16(buf, bs.count, sb, target) != 0)
         throw std::runtime_error("bf16 pack of a gradient bucket failed (alignment)");
-      if (comm_->world() > 1) comm_->all_reduce(sb, bs.count, /*bf16*/ 1, average_ ? 4 : 0, target);
+      if (comm_->live()) comm_->all_reduce(sb, bs.count, /*bf16*/ 1, average_ ? 4 : 0, target);
       if (ddp_unpack_bf16(sb, bs.count, buf, target) != 0)
         throw std::runtime_error("bf16 unpack of a gradient bucket failed (alignment)");
-    } else if (comm_->world() > 1) {
+    } else if (comm_->live()) {
       comm_->all_reduce(buf, bs.count, /*fp32*/ 0, average_ ? 4 : 0, target);
     } else if (emulate_) {
       // world 1 stand-in for the collective (graph-structure / overlap studies on one GPU):

@@ -24,12 +24,17 @@ namespace ddp_amd {
 
 class RcclComm {
  public:
+  // world > 1: uid_bytes is rank 0's ncclUniqueId. world == 1: no communicator (collectives are
+  // no-ops) unless uid_bytes is given — then a real single-rank RCCL communicator is created so
+  // the collective code paths (graph capture of ncclAllReduce, second communicator, ...) run on a
+  // one-GPU box exactly as they do on a node.
   RcclComm(int rank, int world, const std::string& uid_bytes, int device);
   ~RcclComm();
   static std::string make_unique_id();
 
   int rank() const { return rank_; }
   int world() const { return world_; }
+  bool live() const { return comm_ != nullptr; }  // collectives reach RCCL
   ncclComm_t raw() const { return comm_; }
 
   void all_reduce(void* buf, size_t count, int dtype, int op, hipStream_t st);

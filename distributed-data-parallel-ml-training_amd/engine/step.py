@@ -12,7 +12,18 @@ structures), then ``torch.cuda.graph`` capture; replays are bit-identical to eag
 """
 import torch
 
+from ..parallel.comm import is_live
 from ..utils.trace import trace_range
+
+
+def capture_mode():
+    """hipGraph capture mode: "thread_local" whenever RCCL communicators are live (several
+    ranks, or a single-rank self communicator), else "global"."""
+    import torch.distributed as dist
+    from ..parallel import comm as _comm
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return "thread_local"
+    return "thread_local" if _comm.SELF_COMM_ACTIVE else "global"
 
 
 class TrainStep:
@@ -80,10 +91,7 @@ class TrainStep:
         # mode any unsafe HIP call they make during the capture would invalidate it. Only the
         # capturing thread must stay capture-safe ("thread_local"); the replay is validated
         # against every replica afterwards (validate_distributed).
-        import torch.distributed as dist
-        mode = "global"
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            mode = "thread_local"
+        mode = capture_mode()
         with torch.cuda.graph(g, capture_error_mode=mode):
             self._body()
         self.graph = g
@@ -182,10 +190,10 @@ class SegmentedDDPStep(TrainStep):
         self.total = arena.total
         self.comm_stream = torch.cuda.Stream()
         self.comm_a = None
-        if ddp.comm.world > 1:
+        if is_live(ddp.comm):
             from ..parallel.comm import RcclCommunicator
             self.comm_a = RcclCommunicator(ddp.comm.rank, ddp.comm.world, ddp.comm.device,
-                                           key="ddp_amd/rccl_uid_overlap")
+                                           key="ddp_amd/rccl_uid_overlap", self_comm=True)
             # connect the communicator now: its first collective sets up the transports, which
             # must not count against the device-side wait timeout
             warm = torch.zeros(64, dtype=torch.float32, device=loader.device)
@@ -245,7 +253,7 @@ class SegmentedDDPStep(TrainStep):
         self._h = self._h_leaf = None
         main = torch.cuda.current_stream()
         with trace_range("sync_early"):  # bucket B, inline on the DDP communicator
-            comm = self.ddp.comm if self.ddp.comm.world > 1 else None
+            comm = self.ddp.comm if is_live(self.ddp.comm) else None
             self._allreduce(0, self.cut, main, comm)
         native().flag_wait(self._fp(1), self._fp(3), self._fp(4), self.WAIT_TIMEOUT_S,
                            main.cuda_stream)
@@ -258,12 +266,9 @@ class SegmentedDDPStep(TrainStep):
         self._seg2()
 
     def capture(self):
-        import torch.distributed as dist
         torch.cuda.synchronize()
         self.check_error()
-        mode = "global"
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            mode = "thread_local"
+        mode = capture_mode()
         pool = torch.cuda.graph_pool_handle()  # activations of g1 are read by g2
         graphs = []
         for seg in (self._seg1, self._seg2):

@@ -23,6 +23,9 @@ import torch.distributed as dist
 _DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.int32: 3, torch.int64: 4,
        torch.uint8: 5}
 SUM, PROD, MAX, MIN, AVG = 0, 1, 2, 3, 4
+# set once a single-rank RCCL communicator exists (RcclCommunicator self_comm): graph captures
+# then use the multi-GPU "thread_local" mode, exactly as on a node
+SELF_COMM_ACTIVE = False
 _TORCH_OP = {SUM: dist.ReduceOp.SUM, PROD: dist.ReduceOp.PRODUCT, MAX: dist.ReduceOp.MAX,
              MIN: dist.ReduceOp.MIN}
 
@@ -73,6 +76,7 @@ class TorchCommunicator:
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
+        self.live = self.world > 1
 
     def all_reduce(self, t, op=SUM):
         if op == AVG:
@@ -120,11 +124,16 @@ class RcclCommunicator:
 
     kind = "rccl"
 
-    def __init__(self, rank=None, world=None, device=None, key="ddp_amd/rccl_uid"):
+    def __init__(self, rank=None, world=None, device=None, key="ddp_amd/rccl_uid", self_comm=None):
+        """``self_comm`` (default: env ``DDP_AMD_RCCL_SELF=1``): at world size 1, create a real
+        single-rank RCCL communicator instead of skipping every collective, so a one-GPU box runs
+        the same RCCL calls (inside captured graphs, on a second communicator, ...) as a node."""
         from ..ops.common import native
         self.rank = dist.get_rank() if rank is None else rank
         self.world = dist.get_world_size() if world is None else world
         self.device = torch.cuda.current_device() if device is None else device
+        if self_comm is None:
+            self_comm = os.environ.get("DDP_AMD_RCCL_SELF", "0") == "1"
         n = native()
         uid = b""
         if self.world > 1:
@@ -135,7 +144,12 @@ class RcclCommunicator:
             else:
                 store.wait([key])
                 uid = store.get(key)
+        elif self_comm:
+            global SELF_COMM_ACTIVE
+            uid = n.make_unique_id()
+            SELF_COMM_ACTIVE = True
         self.comm = n.RcclComm(self.rank, self.world, uid, self.device)
+        self.live = bool(self.comm.live)  # collectives reach RCCL (world > 1 or self_comm)
 
     @staticmethod
     def _s():
@@ -174,6 +188,12 @@ class RcclCommunicator:
 
     def abort(self):
         self.comm.abort()
+
+
+def is_live(comm):
+    """True when ``comm``'s collectives actually run (world > 1, or a single-rank RCCL
+    communicator created with ``self_comm``)."""
+    return bool(getattr(comm, "live", comm.world > 1))
 
 
 def make_communicator(device):

@@ -34,7 +34,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..optim.arena import arena_for
-from .comm import AVG, SUM
+from .comm import AVG, SUM, is_live
 
 
 def plan_buckets(offsets, numels, elem_bytes, cap_bytes, cap_first_bytes):
@@ -177,7 +177,7 @@ class DistributedDataParallel(nn.Module):
 
     @torch.no_grad()
     def _sync_module_states(self):
-        if self.comm.world == 1:
+        if not is_live(self.comm):
             return
         self.comm.broadcast(self.arena.data, 0)  # ONE coalesced broadcast of all parameters
         if self.broadcast_buffers:
@@ -208,7 +208,7 @@ class DistributedDataParallel(nn.Module):
 
     # ------------------------------------------------------------ per-step
     def _sync_buffers(self):
-        if self.broadcast_buffers and self.comm.world > 1 and torch.is_grad_enabled():
+        if self.broadcast_buffers and is_live(self.comm) and torch.is_grad_enabled():
             if self._flat_buffers is None:
                 self._flatten_buffers()
             with torch.no_grad():

@@ -13,7 +13,7 @@ overlap) — that is what part 3 (parallel/ddp.py) improves on.
 """
 import torch
 
-from .comm import SUM
+from .comm import SUM, is_live
 
 
 def _params_with_grad(model):
@@ -22,7 +22,7 @@ def _params_with_grad(model):
 
 def sync_gradients_gather_scatter(model, comm, root=0):
     """2A: rank-0 gather, mean, scatter of ``[mean] * world`` for every parameter."""
-    if comm.world == 1:
+    if not is_live(comm):
         return  # the mean over one replica is the gradient itself
     params = _params_with_grad(model)
     if comm.kind == "torch":
@@ -52,7 +52,7 @@ def sync_gradients_gather_broadcast(model, comm, root=0):
     """2A variant (BASELINE.json's "manual gather + broadcast"): rank-0 gather and mean as in
     ``sync_gradients_gather_scatter``, then ONE broadcast of the mean per parameter (RCCL runs
     it as a pipelined ring/tree over xGMI instead of world-1 point-to-point sends from rank 0)."""
-    if comm.world == 1:
+    if not is_live(comm):
         return
     params = _params_with_grad(model)
     if comm.kind == "torch":
@@ -90,7 +90,7 @@ def _staging(device, world, maxn):
 
 def sync_gradients_allreduce(model, comm):
     """2B: all_reduce(SUM) then divide by world size, one parameter at a time."""
-    if comm.world == 1:
+    if not is_live(comm):
         return  # the mean over one replica is the gradient itself
     params = _params_with_grad(model)
     if comm.kind == "torch":

@@ -1,0 +1,118 @@
+"""RCCL code paths on a one-GPU box through a single-rank communicator (``self_comm``).
+
+At world size 1 the communicators normally skip every collective; with ``self_comm`` they own a
+real one-rank RCCL communicator, so ncclAllReduce / ncclBroadcast / ncclAllGather run — eagerly,
+inside captured hipGraphs ("thread_local" capture, like a node), and on the second communicator
+of the segmented DDP step — exactly as the multi-GPU step issues them. Results must equal the
+no-collective path (a one-rank average is the identity).
+"""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _cos(a, b):
+    return float(torch.dot(a, b) / (a.norm() * b.norm()))
+
+
+def test_self_comm_collectives(native_ext):
+    from ddp_amd.parallel import RcclCommunicator
+    from ddp_amd.parallel.comm import AVG, is_live
+    c = RcclCommunicator(0, 1, 0, self_comm=True)
+    assert c.live and is_live(c)
+    assert not RcclCommunicator(0, 1, 0, self_comm=False).live
+    x = torch.randn(1 << 20, device="cuda")
+    ref = x.clone()
+    c.all_reduce(x, AVG)
+    c.broadcast(x, 0)
+    xb = x.to(torch.bfloat16)
+    c.all_reduce(xb)
+    (g,) = c.all_gather(x)
+    torch.cuda.synchronize()
+    assert torch.equal(x, ref) and torch.equal(g, ref)
+    assert torch.equal(xb, ref.to(torch.bfloat16))
+    assert c.comm.async_error() == 0
+
+
+def _restore(m, opt, ld, snap):
+    m.arena.data.copy_(snap[0])
+    opt.momentum_buffer.copy_(snap[1])
+    ld.cursor.copy_(snap[2])
+    m.arena.grad.zero_()
+    for sp in m.module.fused_plan():
+        sp._packed_version = None
+        sp.maybe_pack()
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("segmented", [False, True])
+def test_captured_ddp_step_with_live_rccl(native_ext, segmented):
+    """Captured DDP step (inline bucket all-reduce, or the segmented two-graph step with bucket A
+    on a second communicator between the graphs) with live RCCL collectives applies the same
+    update as the same step without collectives, from the same state, eager and replayed."""
+    from ddp_amd.models import VGG11
+    from ddp_amd.optim import FusedSGD
+    from ddp_amd.data import SyntheticCIFAR10, DeviceLoader
+    from ddp_amd.engine import TrainStep, SegmentedDDPStep, CrossEntropyLoss
+    from ddp_amd.parallel import DistributedDataParallel, RcclCommunicator
+    torch.manual_seed(7)
+    base = VGG11().cuda()
+    res = {}
+    for live in (False, True):
+        m = DistributedDataParallel(copy.deepcopy(base), RcclCommunicator(0, 1, 0, self_comm=live),
+                                    bucket_cap_mb=256.0, first_bucket_cap_mb=256.0)
+        assert m.comm.live == live
+        opt = FusedSGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+        ld = DeviceLoader(SyntheticCIFAR10(True, n=512), 64, "cuda")
+        if segmented:
+            st = SegmentedDDPStep(m, opt, CrossEntropyLoss(), ld, split=4)
+            st.WAIT_TIMEOUT_S = 20.0
+        else:
+            st = TrainStep(m, opt, CrossEntropyLoss(), ld)
+        snap = (m.arena.data.clone(), opt.momentum_buffer.clone(), ld.cursor.clone())
+
+        def run(fn):
+            _restore(m, opt, ld, snap)
+            fn()
+            torch.cuda.synchronize()
+            assert int(ld.cursor.item()) == int(snap[2].item()) + 1
+            return m.arena.data - snap[0]
+
+        eager = [run(st._body), run(st._body)]
+        st.warmup(1)
+        st.capture()
+        graph = run(st.step)
+        if segmented:
+            st.check_error()
+        res[live] = (eager, graph)
+        m.close()
+    (e0, e1), g0 = res[False]
+    (l0, _), g1 = res[True]
+    tol = min(0.99, _cos(e0, e1) - 0.005)  # two executions differ by float-atomic ordering
+    assert float(e0.norm()) > 0
+    for a, b in ((e0, l0), (g0, g1), (e0, g1)):
+        assert _cos(a, b) > tol, (_cos(a, b), tol)
+        assert abs(float(b.norm()) / float(a.norm()) - 1) < 0.02
+
+
+@pytest.mark.parametrize("strategy", ["allreduce", "gather_scatter", "gather_broadcast"])
+def test_strategies_with_live_rccl(native_ext, strategy):
+    """2A / 2B per-parameter RCCL sync (grouped send/recv gather, mean_ws, broadcast / ncclAllReduce
+    + scale) on a live one-rank communicator leaves the gradients unchanged."""
+    from ddp_amd.models import VGG11
+    from ddp_amd.engine import CrossEntropyLoss
+    from ddp_amd.parallel import RcclCommunicator, STRATEGIES
+    torch.manual_seed(3)
+    m = VGG11().cuda()
+    x = torch.randn(16, 3, 32, 32, device="cuda")
+    y = torch.randint(0, 10, (16,), device="cuda")
+    CrossEntropyLoss()(m(x), y).backward()
+    torch.cuda.synchronize()
+    ref = [p.grad.clone() for p in m.parameters()]
+    STRATEGIES[strategy](m, RcclCommunicator(0, 1, 0, self_comm=True))
+    torch.cuda.synchronize()
+    for p, r in zip(m.parameters(), ref):
+        assert torch.allclose(p.grad, r, rtol=1e-6, atol=1e-7)
