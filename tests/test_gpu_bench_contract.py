@@ -1,0 +1,49 @@
+"""bench.py output contract on one MI355X (the driver parses this line every round).
+
+Runs ``bench.py`` as a child process (one extra GPU process, bounded by a timeout) for a few
+steps and checks the single JSON line: metric / config named by BASELINE.json, whole-job
+value consistent with ms_per_step and the global batch, vs_baseline against BASELINE.md's
+part-3 number, bf16 compute, the captured hipGraph path, and a finite training loss.
+"""
+import json
+import math
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run_bench(*extra):
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "4", "--warmup", "3", *extra]
+    p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_json_contract(native_ext):
+    import bench
+    r = _run_bench()
+    for k in ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"]:
+        assert k in r, k
+    assert r["metric"].startswith("images/sec") and r["unit"] == "images/s"
+    assert r["n_gpus"] == 1 and r["steps"] == 4 and r["warmup"] == 3
+    assert r["higher_is_better"] is True and r["scaling"] == "weak"
+    assert r["dtype"] == "bf16" and r["data"].startswith("synthetic")
+    cfg = r["config"]
+    assert cfg["model"] == "vgg11" and cfg["global_batch"] == 256 and cfg["parallelism"] == "dp1"
+    assert cfg["hipgraph"] is True
+    # value is the whole-job rate implied by the timed steps
+    assert math.isclose(r["value"], cfg["global_batch"] / (r["ms_per_step"] / 1e3), rel_tol=1e-3)
+    assert math.isclose(r["vs_baseline"], r["value"] / bench.BASELINE_IMG_S, rel_tol=1e-2)
+    # lr 0.1 / momentum 0.9 from random init: the first ~10 steps spike (the 40-step default run
+    # averages ~2.4), so only finiteness and a loose bound are checked here
+    assert math.isfinite(r["train_loss_mean"]) and 0.0 < r["train_loss_mean"] < 100.0
+    assert r["replicas_consistent"] is True
