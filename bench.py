@@ -9,13 +9,17 @@ Config = BASELINE.json: VGG-11 (reference architecture, random init), synthetic 
 data (3x32x32, 10 classes, on-device crop/flip/normalise), bf16 compute with fp32 master
 weights/grads, SGD(0.1, 0.9, 1e-4), part-3 strategy (bucketed DDP on RCCL, collectives issued in
 stream order inside the captured step).
-Default protocol: each GPU trains on the reference's batch of 256 images per step (weak scaling:
-per-GPU work is fixed as N grows; at N=1 this is exactly the reference's global batch 256).
-``--global-batch B`` instead splits a fixed global batch int(B/N) per GPU (strong scaling, the
-reference's Table-1 protocol at 4 nodes). Every timed step is a full training step
-(augment + forward + backward + gradient all-reduce + optimizer), captured in one hipGraph.
+Default protocol = the reference's (/root/reference/part3/main.py:167): a FIXED
+global batch of 256 split int(256/N) per GPU (strong scaling: 256, 128, 64, 32 images per GPU at
+N = 1, 2, 4, 8; 255 in total at N = 3). ``--per-gpu-batch B`` instead fixes B images per GPU
+(weak scaling, global batch B*N). Every timed step is a full training step (augment + forward +
+backward + gradient all-reduce + optimizer), replayed from hipGraphs.
 W untimed warm-up steps, then EXACTLY K timed steps bracketed by barrier + synchronize; the
-elapsed time is the MAX over ranks; rank 0 prints one JSON line.
+elapsed time is the MAX over ranks; rank 0 prints one JSON line. After the timed region the
+reference's own timing window is also measured and reported as an extra key: 40 iterations, each
+followed by a host synchronisation (the reference's per-iteration ``loss.item()``), the wall time
+of iterations 1..39 averaged (iteration 0 excluded, /root/reference/part1/main.py:86-91) and
+then averaged over ranks (report printed p.4 §3) -> ``avg_ms_iter_1_39``.
 """
 import argparse
 import json
@@ -35,9 +39,12 @@ def parse():
     p.add_argument("--steps", type=int, default=40)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--model", default="vgg11")
-    p.add_argument("--global-batch", type=int, default=None, help="strong scaling")
+    p.add_argument("--global-batch", type=int, default=None,
+                   help="strong scaling: split int(B/N) per GPU (default 256, the reference's)")
     p.add_argument("--per-gpu-batch", type=int, default=None,
-                   help="weak scaling (default 256 images per GPU)")
+                   help="weak scaling: B images per GPU (global batch B*N)")
+    p.add_argument("--ref-window", type=int, default=40,
+                   help="iterations of the reference timing window (0 = skip)")
     p.add_argument("--strategy", default="ddp",
                    choices=["ddp", "allreduce", "gather_scatter", "gather_broadcast"])
     # Bucket sizing for xGMI. The collectives run inline on the step's single
@@ -88,15 +95,19 @@ def main():
     comm = RcclCommunicator(rank, world, local_rank)
 
     seed_everything(ddp_amd.SEED)
-    if args.global_batch:
-        B, scaling = int(args.global_batch / world), "strong"
-    else:
-        # ResNet-50: 256 images per GPU (~60 GB of activations of the 288 GB HBM; 31% more
-        # images/s than 64 per GPU on one MI355X, and 4x less gradient traffic per image)
-        B = args.per_gpu_batch or 256
-        scaling = "weak"
-    global_batch = B * world
     resnet = args.model.startswith("resnet")
+    if args.per_gpu_batch:
+        B, scaling = args.per_gpu_batch, "weak"
+    elif args.global_batch or not resnet:
+        B, scaling = int((args.global_batch or 256) / world), "strong"
+    else:
+        # ResNet-50 (the driver's large-gradient stress config, not the reference's): 256
+        # images per GPU (~60 GB of activations of the 288 GB HBM; 31% more images/s than 64 per
+        # GPU on one MI355X, and 4x less gradient traffic per image)
+        B, scaling = 256, "weak"
+    if B < 1:
+        raise SystemExit(f"global batch too small for {world} ranks")
+    global_batch = B * world
     ds = (SyntheticImageNet(True, n=args.train_size) if resnet
           else SyntheticCIFAR10(True, n=args.train_size))
     loader = DeviceLoader(ds, B, device, world, rank, train=True, cpad=8)
@@ -165,6 +176,24 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     loss = step.pop_loss() / max(args.steps, 1)
+
+    # the reference's window: per-iteration wall time incl. a host sync, iterations 1..39
+    ref_ms = None
+    if args.ref_window > 1:
+        barrier()
+        tot = 0.0
+        for i in range(args.ref_window):
+            t = time.perf_counter()
+            step.step()
+            torch.cuda.synchronize()
+            if i > 0:
+                tot += time.perf_counter() - t
+        ref = torch.tensor([tot / (args.ref_window - 1)], dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(ref)
+            ref /= world
+        ref_ms = float(ref.item()) * 1000.0
+        step.pop_loss()
     consistent = True
     if world > 1:
         consistent = check_replicas(arena, world)
@@ -195,6 +224,8 @@ def main():
                    "comm": (f"segmented@{args.segmented}" if segmented else "overlap-stream" if getattr(getattr(model, "reducer", None), "overlap",
                                                          lambda: False)() else "inline"),
                    "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4) fused"},
+        "avg_ms_iter_1_39": round(ref_ms, 4) if ref_ms is not None else None,
+        "img_s_iter_1_39": round(global_batch / ref_ms * 1000.0, 2) if ref_ms else None,
         "train_loss_mean": round(loss, 4),
         "warmup_loss_sum": round(warm_loss, 4),
         "replicas_consistent": consistent,

@@ -226,14 +226,15 @@ PYBIND11_MODULE(_native, m) {
   });
   m.def("sgd_pack", [](uintptr_t items, int n_items, uintptr_t descs, uintptr_t p, uintptr_t g,
                        uintptr_t buf, float lr, float momentum, float wd, float grad_scale,
-                       int nesterov, uintptr_t st, int zero_grad, uintptr_t counter, int delta) {
+                       int nesterov, uintptr_t st, int zero_grad, uintptr_t counter, int delta,
+                       uintptr_t skip) {
     check(ddp_sgd_pack(P<void>(items), n_items, P<long long>(descs), P<float>(p), P<float>(g),
                        P<float>(buf), lr, momentum, wd, grad_scale, nesterov, zero_grad,
-                       P<int>(counter), delta, S(st)), "sgd_pack");
+                       P<int>(counter), delta, P<const unsigned>(skip), S(st)), "sgd_pack");
   }, py::arg("items"), py::arg("n_items"), py::arg("descs"), py::arg("p"), py::arg("g"),
      py::arg("buf"), py::arg("lr"), py::arg("momentum"), py::arg("wd"), py::arg("grad_scale"),
      py::arg("nesterov"), py::arg("stream"), py::arg("zero_grad") = 0, py::arg("counter") = 0,
-     py::arg("delta") = 0);
+     py::arg("delta") = 0, py::arg("skip") = 0);
   m.def("sgd_tile_dims", [](int RS) {
     int tk, tc;
     ddp_sgd_tile_dims(RS, &tk, &tc);

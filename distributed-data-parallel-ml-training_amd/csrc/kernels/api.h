@@ -118,7 +118,7 @@ void ddp_conv_force_tile(int tile_plus_one, int stages);
 int ddp_pack_conv_weights(const ddp_amd::PackDesc* descs, int n, hipStream_t st);
 int ddp_sgd_pack(const void* items, int n_items, const long long* descs, float* p, float* g,
                  float* buf, float lr, float momentum, float wd, float grad_scale, int nesterov,
-                 int zero_grad, int* counter, int delta, hipStream_t st);
+                 int zero_grad, int* counter, int delta, const unsigned* skip, hipStream_t st);
 void ddp_sgd_tile_dims(int RS, int* TK, int* TC);
 int ddp_counter_add(int* c, int delta, hipStream_t st);
 int ddp_synth_generate(unsigned char* images, int* labels, int n, int pix_per_img,

@@ -117,6 +117,10 @@ struct SgdHyper {
   int zero_grad;  // write 0 to every gradient after use (replaces the next step's zero_grad fill)
   int* counter;   // optional step counter (data cursor): += delta by one thread
   int delta;
+  // optional error word (engine/step.py SegmentedDDPStep): non-zero when a device-side wait for
+  // a gradient bucket timed out — the update is then skipped instead of applying gradients
+  // that were never averaged (the host raises on the error at its next check)
+  const unsigned* skip;
 };
 
 __device__ __forceinline__ float sgd1(float p, float g, float& b, const SgdHyper& h) {
@@ -137,6 +141,7 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(const int4* __restrict__ 
   const int4 it = items[blockIdx.x];
   const int tid = threadIdx.x;
   if (h.counter && blockIdx.x == 0 && tid == 0) atomicAdd(h.counter, h.delta);
+  if (h.skip && __hip_atomic_load(h.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
   if (it.x == 0) {
     const size_t off = (size_t)(unsigned)it.y;
     const int cnt = it.z;
@@ -286,8 +291,8 @@ extern "C" int ddp_pack_conv_weights(const PackDesc* descs, int n, hipStream_t s
 extern "C" int ddp_sgd_pack(const void* items, int n_items, const long long* descs, float* p,
                             float* g, float* buf, float lr, float momentum, float wd,
                             float grad_scale, int nesterov, int zero_grad, int* counter,
-                            int delta, hipStream_t st) {
-  SgdHyper h{lr, momentum, wd, grad_scale, nesterov, zero_grad, counter, delta};
+                            int delta, const unsigned* skip, hipStream_t st) {
+  SgdHyper h{lr, momentum, wd, grad_scale, nesterov, zero_grad, counter, delta, skip};
   if (n_items <= 0) return 0;
   hipLaunchKernelGGL(sgd_pack_kernel, dim3(n_items), dim3(256), 0, st, (const int4*)items, descs,
                      p, g, buf, h);

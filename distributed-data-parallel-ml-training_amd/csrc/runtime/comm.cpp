@@ -110,10 +110,22 @@ void RcclComm::reduce_scatter(const void* send, void* recv, size_t count, int dt
 void RcclComm::gather(const void* send, void* recv, size_t count, int dtype, int root,
                       hipStream_t st) {
   const size_t bytes = count * dtype_bytes(dtype);
+  const ncclDataType_t dt = to_nccl(dtype);
+  if (world_ == 1) {
+    if (comm_ != nullptr && count > 0) {
+      // single-rank live communicator (one-GPU box): the root's own slot travels through a
+      // grouped self send/recv, so the point-to-point path of 2A runs exactly as on a node
+      NCCL_OK(ncclGroupStart());
+      NCCL_OK(ncclSend(send, count, dt, rank_, comm_, st));
+      NCCL_OK(ncclRecv((char*)recv + (size_t)root * bytes, count, dt, rank_, comm_, st));
+      NCCL_OK(ncclGroupEnd());
+    } else if ((const char*)recv + (size_t)root * bytes != send) {
+      HIP_OK(hipMemcpyAsync((char*)recv + (size_t)root * bytes, send, bytes, hipMemcpyDeviceToDevice, st));
+    }
+    return;
+  }
   if (rank_ == root)
     HIP_OK(hipMemcpyAsync((char*)recv + (size_t)root * bytes, send, bytes, hipMemcpyDeviceToDevice, st));
-  if (world_ == 1) return;
-  const ncclDataType_t dt = to_nccl(dtype);
   NCCL_OK(ncclGroupStart());
   if (rank_ == root) {
     for (int r = 0; r < world_; ++r)
@@ -127,10 +139,20 @@ void RcclComm::gather(const void* send, void* recv, size_t count, int dtype, int
 void RcclComm::scatter(const void* send, void* recv, size_t count, int dtype, int root,
                        hipStream_t st) {
   const size_t bytes = count * dtype_bytes(dtype);
+  const ncclDataType_t dt = to_nccl(dtype);
+  if (world_ == 1) {
+    if (comm_ != nullptr && count > 0 && (const char*)send + (size_t)root * bytes != recv) {
+      NCCL_OK(ncclGroupStart());  // self send/recv (see gather)
+      NCCL_OK(ncclSend((const char*)send + (size_t)root * bytes, count, dt, rank_, comm_, st));
+      NCCL_OK(ncclRecv(recv, count, dt, rank_, comm_, st));
+      NCCL_OK(ncclGroupEnd());
+    } else if ((const char*)send + (size_t)root * bytes != recv) {
+      HIP_OK(hipMemcpyAsync(recv, (const char*)send + (size_t)root * bytes, bytes, hipMemcpyDeviceToDevice, st));
+    }
+    return;
+  }
   if (rank_ == root && (const char*)send + (size_t)root * bytes != recv)
     HIP_OK(hipMemcpyAsync(recv, (const char*)send + (size_t)root * bytes, bytes, hipMemcpyDeviceToDevice, st));
-  if (world_ == 1) return;
-  const ncclDataType_t dt = to_nccl(dtype);
   NCCL_OK(ncclGroupStart());
   if (rank_ == root) {
     for (int r = 0; r < world_; ++r)

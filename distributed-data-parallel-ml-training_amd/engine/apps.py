@@ -20,8 +20,8 @@ from ..models import build
 from ..optim import FusedSGD
 from ..parallel import (DistributedDataParallel, STRATEGIES, destroy, init_distributed_setup,
                         make_communicator, test_distributed_setup)
-from ..utils import MetricsSink, load_checkpoint, parse_all, pick_device, save_checkpoint, \
-    seed_everything
+from ..utils import MetricsSink, Watchdog, load_checkpoint, local_rank_of, parse_all, pick_device, \
+    save_checkpoint, seed_everything
 from .trainer import CrossEntropyLoss, test_model, train_model, train_model_graph
 
 PART_STRATEGY = {"part1": None, "part2a": "gather_scatter", "part2b": "allreduce", "part3": "ddp"}
@@ -35,7 +35,7 @@ def main(part, argv=None):
     world, rank = 1, 0
     if distributed:
         world, rank = args.size, args.rank
-        device = pick_device(args.device)
+        device = pick_device(args.device, local_rank=local_rank_of(rank))
         init_distributed_setup(args.master_ip, args.master_port, rank, world, backend="gloo")
         test_distributed_setup()
     else:
@@ -63,6 +63,13 @@ def main(part, argv=None):
     if strategy in STRATEGIES:
         sync = functools.partial(_sync, STRATEGIES[strategy], comm)
     metrics = MetricsSink(args.metrics, rank)
+    # failure detection (the reference has none, part2/part2a/main.py:58): beat
+    # once per iteration; no beat for --watchdog-s seconds or an RCCL async error -> abort the
+    # communicator and exit non-zero instead of hanging on a dead peer
+    watchdog = None
+    if distributed and args.watchdog_s > 0:
+        watchdog = Watchdog(timeout_s=args.watchdog_s, comm=comm,
+                            poll_s=min(5.0, args.watchdog_s / 4)).start()
 
     step = None
     if args.graph and torch.device(device).type == "cuda":
@@ -84,6 +91,10 @@ def main(part, argv=None):
         step.warmup(2)
         step.capture()
         torch.cuda.synchronize()
+        if world > 1 and not step.validate_distributed(arena, world):
+            print("[ddp_amd] replicas diverged under graph replay; running eager steps",
+                  flush=True)
+        torch.cuda.synchronize()
         arena.data.copy_(snap[0])
         optimizer.momentum_buffer.copy_(snap[1])
         optimizer.repack()
@@ -95,16 +106,19 @@ def main(part, argv=None):
             if epoch > 0:
                 train_loader.set_epoch(epoch)
                 step.capture()  # the augmentation seed is a launch argument: new epoch, new graph
-            train_model_graph(step, train_loader, epoch, metrics=metrics)
+            train_model_graph(step, train_loader, epoch, metrics=metrics, watchdog=watchdog,
+                              rank=rank)
         else:
             train_loader.set_epoch(epoch)
             train_model(model, train_loader, optimizer, criterion, epoch, device, sync,
-                        metrics=metrics)
+                        metrics=metrics, watchdog=watchdog, rank=rank)
         if not args.no_test:
-            test_model(model, test_loader, criterion, device)
+            test_model(model, test_loader, criterion, device, watchdog=watchdog)
 
     if args.save and rank == 0:
         save_checkpoint(args.save, model, optimizer)
+    if watchdog is not None:
+        watchdog.stop()
     if distributed:
         destroy()
     return model

@@ -102,6 +102,26 @@ class TrainStep:
         else:
             self._body()
 
+    def tail_step(self, x, y):
+        """One EAGER step on an explicit batch of any size (the epoch's partial last batch,
+        engine/trainer.py train_model_graph): forward, backward, gradient sync (DDP buckets via
+        the wrapper's reducer; 2A/2B via ``sync``) and the optimizer, on the same stream as the
+        replays. Gradients are clear on entry when the optimizer launch clears them."""
+        if not self.fold_opt:
+            self.optimizer.zero_grad()
+        if self.fused:
+            loss = self.model.forward_loss(x, y, acc=self.loss_sum)
+        else:
+            loss = self.criterion(self.model(x), y)
+            self.loss_sum.add_(loss.detach())
+        loss.backward(self._one)
+        if self.sync is not None:
+            self.sync(self.model)
+        if self.fold_opt:
+            self.optimizer.step(zero_grad=True)
+        else:
+            self.optimizer.step()
+
     def wait(self, timeout_s=None, poll_s=0.001):
         """Synchronise with the device, optionally bounded: returns False on timeout instead of
         blocking forever (a collective whose peer died would otherwise hang the process)."""
@@ -258,7 +278,10 @@ class SegmentedDDPStep(TrainStep):
         native().flag_wait(self._fp(1), self._fp(3), self._fp(4), self.WAIT_TIMEOUT_S,
                            main.cuda_stream)
         with trace_range("optimizer"):
-            self.optimizer.step(zero_grad=True, counter=self.loader.cursor_advance())
+            # a timed-out wait (error word set) skips the update: never apply gradients whose
+            # bucket A was not averaged
+            self.optimizer.step(zero_grad=True, counter=self.loader.cursor_advance(),
+                                skip=self._fp(4))
 
     def _body(self):
         self._seg1()

@@ -12,9 +12,10 @@ sync call at :143) and ``test_model`` (part1/main.py:96-111):
 import time
 
 import torch
-
-from ..utils.trace import trace_range
 import torch.nn as nn
+
+from ..utils.misc import fault_point
+from ..utils.trace import trace_range
 
 
 class CrossEntropyLoss(nn.Module):
@@ -28,11 +29,12 @@ class CrossEntropyLoss(nn.Module):
 
 
 def train_model(model, train_loader, optimizer, criterion, epoch, device="cpu", sync=None,
-                log=print, metrics=None, watchdog=None):
+                log=print, metrics=None, watchdog=None, rank=0):
     running_loss = 0.0
     total_time = 0
     stats = {"iter_ns": []}
     for batch_idx, (data, target) in enumerate(train_loader):
+        fault_point(rank, batch_idx)
         start_time = time.perf_counter_ns()
         with trace_range("data"):
             data, target = data.to(device), target.to(device)
@@ -69,19 +71,30 @@ def train_model(model, train_loader, optimizer, criterion, epoch, device="cpu", 
     return stats
 
 
-def train_model_graph(step, train_loader, epoch, log=print, metrics=None, watchdog=None):
+def train_model_graph(step, train_loader, epoch, log=print, metrics=None, watchdog=None, rank=0):
     """``train_model`` over a captured TrainStep (engine/step.py): every iteration is ONE graph
     replay (augment + forward + backward + sync + optimizer) followed by a device synchronize,
     so the per-iteration timer keeps the reference's meaning (the reference's ``loss.item()``
     synchronises each iteration too). The loss print every 20 batches reads the device loss
-    accumulator (same running mean as the reference)."""
+    accumulator (same running mean as the reference).
+
+    The captured step has a fixed batch shape, so only the floor(L/B) FULL batches of the shard
+    are replays; a partial last batch (L % B samples, e.g. 80 of 50 000 at B = 256) runs as one
+    eager step on exactly those samples (``TrainStep.tail_step``) — the same samples and the
+    same partial-batch mean as the eager loop and the reference's DataLoader."""
     total_time = 0
     stats = {"iter_ns": []}
     nb = len(train_loader)
+    L, B = train_loader.idx.numel(), train_loader.batch_size
+    nfull = L // B
     step.pop_loss()
     for batch_idx in range(nb):
+        fault_point(rank, batch_idx)
         start_time = time.perf_counter_ns()
-        step.step()
+        if batch_idx < nfull:
+            step.step()
+        else:
+            step.tail_step(*train_loader.batch(batch_idx * B, L - batch_idx * B))
         torch.cuda.synchronize()
         if batch_idx % 20 == 19:
             log(f'[{epoch + 1}, {batch_idx + 1:5d}] loss: {step.pop_loss() / 20:.3f}')
@@ -96,11 +109,25 @@ def train_model_graph(step, train_loader, epoch, log=print, metrics=None, watchd
             metrics.log(event="iter", epoch=epoch, batch=batch_idx, ns=dt)
         if watchdog is not None:
             watchdog.beat()
+    if hasattr(step, "check_error"):
+        step.check_error()
     stats["total_1_39_ns"] = total_time
+    stats["graph_replays"] = min(nb, nfull)
     return stats
 
 
-def test_model(model, test_loader, criterion, device="cpu", log=print):
+def graph_epoch_plan(n_samples, batch_size, max_batches=None):
+    """(replayed full batches, eager tail size) of one --graph epoch over a shard of
+    ``n_samples`` — the CPU-checkable schedule ``train_model_graph`` follows."""
+    nb = -(-n_samples // batch_size)
+    if max_batches:
+        nb = min(nb, max_batches)
+    nfull = min(nb, n_samples // batch_size)
+    tail = n_samples - nfull * batch_size if nb > nfull else 0
+    return nfull, tail
+
+
+def test_model(model, test_loader, criterion, device="cpu", log=print, watchdog=None):
     model.eval()
     test_loss = 0
     correct = 0
@@ -122,6 +149,8 @@ def test_model(model, test_loader, criterion, device="cpu", log=print):
                 pred = output.max(1, keepdim=True)[1]
                 correct += pred.eq(target.view_as(pred)).sum().item()
             nb += 1
+            if watchdog is not None:
+                watchdog.beat()
     if fused:
         test_loss, correct = float(loss_acc), int(hits)
     n = len(test_loader.dataset)

@@ -88,10 +88,11 @@ class FusedSGD(torch.optim.SGD):
             super().zero_grad(set_to_none=set_to_none)
 
     @torch.no_grad()
-    def step(self, closure=None, zero_grad=False, counter=None):
+    def step(self, closure=None, zero_grad=False, counter=None, skip=None):
         """One fused launch. ``zero_grad=True`` also clears every gradient after its use (the
         next step then needs no zero_grad fill); ``counter=(int32 device ptr, delta)`` is
-        advanced by the same launch (the on-device data cursor of engine/step.py)."""
+        advanced by the same launch (the on-device data cursor of engine/step.py); ``skip`` =
+        device pointer of a uint32 error word: the update is skipped when it is non-zero."""
         if not self._fused:
             out = super().step(closure)
             if zero_grad:
@@ -109,7 +110,8 @@ class FusedSGD(torch.optim.SGD):
                           float(self._grad_scale_factor), int(bool(g["nesterov"])), s,
                           zero_grad=int(bool(zero_grad)),
                           counter=int(counter[0]) if counter else 0,
-                          delta=int(counter[1]) if counter else 0)
+                          delta=int(counter[1]) if counter else 0,
+                          skip=int(skip) if skip else 0)
         return None
 
     def state_dict(self):

@@ -51,6 +51,9 @@ def build_parser(description=None, distributed=True):
     g.add_argument('--resume', default=None, help='load a checkpoint before training')
     g.add_argument('--metrics', default=None, help='JSON-lines metrics sink')
     g.add_argument('--no-test', action='store_true', help='skip the evaluation pass')
+    g.add_argument('--watchdog-s', type=float, default=300.0,
+                   help='distributed runs: abort + exit non-zero after this many seconds '
+                        'without a finished iteration (0 = off)')
     g.add_argument('--graph', action='store_true',
                    help='GPU: run each iteration as one replay of the captured training step')
     return p

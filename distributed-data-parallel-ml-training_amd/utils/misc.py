@@ -27,6 +27,16 @@ def seed_everything(seed):
     np.random.seed(seed)
 
 
+def local_rank_of(rank=None):
+    """GPU index for this process: LOCAL_RANK when a launcher (torchrun) set it, else the
+    global rank — a reference-style launch (``main.py --num-nodes 8 --rank R`` once per GPU of
+    one node, /root/reference/part3/main.py:29,36-40) has no LOCAL_RANK; ``pick_device`` then
+    maps rank R to GPU ``R % device_count``."""
+    if "LOCAL_RANK" in os.environ:
+        return int(os.environ["LOCAL_RANK"])
+    return int(rank) if rank is not None else 0
+
+
 def pick_device(spec="auto", local_rank=None):
     if spec == "cpu":
         return torch.device("cpu")
@@ -85,6 +95,25 @@ def load_checkpoint(path, model, optimizer=None, map_location="cpu"):
     if optimizer is not None and isinstance(obj, dict) and "optimizer" in obj:
         optimizer.load_state_dict(obj["optimizer"])
     return obj.get("extra") if isinstance(obj, dict) else None
+
+
+def fault_point(rank, batch_idx):
+    """Fault injection for the failure-detection tests:
+    ``DDP_AMD_FAULT_INJECT=<rank>:<batch>[:exit|hang]`` makes that rank die (``os._exit(17)``)
+    or stop making progress (sleep forever) when it reaches that batch of the epoch."""
+    spec = os.environ.get("DDP_AMD_FAULT_INJECT")
+    if not spec:
+        return
+    parts = spec.split(":")
+    if int(parts[0]) != int(rank) or int(parts[1]) != int(batch_idx):
+        return
+    mode = parts[2] if len(parts) > 2 else "exit"
+    print(f"[ddp_amd] fault injected on rank {rank} at batch {batch_idx}: {mode}",
+          file=sys.stderr, flush=True)
+    if mode == "hang":
+        while True:
+            time.sleep(3600)
+    os._exit(17)
 
 
 class Watchdog:

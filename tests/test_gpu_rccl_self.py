@@ -116,3 +116,40 @@ def test_strategies_with_live_rccl(native_ext, strategy):
     torch.cuda.synchronize()
     for p, r in zip(m.parameters(), ref):
         assert torch.allclose(p.grad, r, rtol=1e-6, atol=1e-7)
+
+
+def test_self_comm_gather_runs_point_to_point(native_ext):
+    """2A's gather on a live one-rank communicator is a grouped ncclSend/ncclRecv to itself
+    (csrc/runtime/comm.cpp RcclComm::gather): the staging slot must be written by the recv — it
+    starts as NaN and must end equal to the sent gradient. The strategy path is checked the same
+    way: after sync_gradients_gather_scatter the shared staging buffer holds the LAST parameter's
+    gradient, delivered by the recv (reference: part2/part2a/main.py:97-115)."""
+    from ddp_amd.models import VGG11
+    from ddp_amd.engine import CrossEntropyLoss
+    from ddp_amd.parallel import RcclCommunicator, STRATEGIES
+    from ddp_amd.parallel import strategies as strat
+    c = RcclCommunicator(0, 1, 0, self_comm=True)
+    t = torch.randn(12345, device="cuda")
+    buf = torch.full((1, t.numel()), float("nan"), device="cuda")
+    c.gather_into(t, buf, dst=0)
+    torch.cuda.synchronize()
+    assert torch.equal(buf[0], t)
+    assert c.comm.async_error() == 0
+
+    torch.manual_seed(5)
+    m = VGG11().cuda()
+    x = torch.randn(8, 3, 32, 32, device="cuda")
+    y = torch.randint(0, 10, (8,), device="cuda")
+    CrossEntropyLoss()(m(x), y).backward()
+    params = [p for p in m.parameters() if p.grad is not None]
+    maxn = max(p.numel() for p in params)
+    st = strat._staging(params[0].grad.device, 1, maxn)
+    st.fill_(float("nan"))
+    torch.cuda.synchronize()
+    ref = [p.grad.clone() for p in params]
+    STRATEGIES["gather_scatter"](m, c)
+    torch.cuda.synchronize()
+    last = params[-1].grad
+    assert torch.equal(st[:last.numel()], ref[-1].reshape(-1))
+    for p, r in zip(params, ref):
+        assert torch.equal(p.grad, r)
