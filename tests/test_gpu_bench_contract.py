@@ -35,7 +35,8 @@ def test_bench_json_contract(native_ext):
         assert k in r, k
     assert r["metric"].startswith("images/sec") and r["unit"] == "images/s"
     assert r["n_gpus"] == 1 and r["steps"] == 4 and r["warmup"] == 3
-    assert r["higher_is_better"] is True and r["scaling"] == "weak"
+    # the reference protocol: global batch 256 split int(256/N) per GPU (strong scaling)
+    assert r["higher_is_better"] is True and r["scaling"] == "strong"
     assert r["dtype"] == "bf16" and r["data"].startswith("synthetic")
     cfg = r["config"]
     assert cfg["model"] == "vgg11" and cfg["global_batch"] == 256 and cfg["parallelism"] == "dp1"
@@ -47,3 +48,14 @@ def test_bench_json_contract(native_ext):
     # averages ~2.4), so only finiteness and a loose bound are checked here
     assert math.isfinite(r["train_loss_mean"]) and 0.0 < r["train_loss_mean"] < 100.0
     assert r["replicas_consistent"] is True
+    # the reference's own timing window (iterations 1..39, host sync per iteration)
+    assert r["avg_ms_iter_1_39"] > 0 and r["img_s_iter_1_39"] > 0
+
+
+def test_bench_protocol_batch_split(native_ext):
+    """--global-batch B splits int(B/N) per GPU (strong); --per-gpu-batch fixes it (weak)."""
+    r = _run_bench("--global-batch", "32", "--ref-window", "0")
+    assert r["scaling"] == "strong" and r["config"]["global_batch"] == 32
+    assert r["config"]["per_gpu_batch"] == 32 and r["avg_ms_iter_1_39"] is None
+    r = _run_bench("--per-gpu-batch", "64", "--ref-window", "0")
+    assert r["scaling"] == "weak" and r["config"]["global_batch"] == 64
