@@ -196,6 +196,10 @@ PYBIND11_MODULE(_native, m) {
     check(ddp_sgd(P<float>(p), P<float>(g), P<float>(buf), n, lr, momentum, wd, grad_scale,
                   nesterov, S(st)), "sgd");
   });
+  m.def("conv_fixup", [](uintptr_t facc, size_t n, uintptr_t tickets, size_t nt, int mode,
+                         size_t max_bytes) {
+    ddp_conv_fixup(P<float>(facc), n, P<unsigned>(tickets), nt, mode, max_bytes);
+  });
   m.def("conv_options", [](int wgrad_atomic, int persistent, int stages) {
     ddp_conv_options(wgrad_atomic, persistent, stages);
   }, py::arg("wgrad_atomic") = 0, py::arg("persistent") = 0, py::arg("stages") = 2);

@@ -32,7 +32,10 @@
 //   * MFMA operands are swapped (D^T = B^T A^T) so each lane owns one output row and four
 //     consecutive columns: 8-B bf16 / 16-B fp32 stores in the epilogue;
 //   * XCD-aware bijective tile order (T1); split-K writes plain fp32 slabs [split][M][N] that a
-//     finish kernel reduces in a fixed order (WGRAD optionally uses fp32 atomics instead);
+//     finish kernel reduces in a fixed order, or — for the small problems of strong-scaling
+//     batches, where the finish launch costs more than the reduction — accumulates with fp32
+//     atomics and lets the tile's last-arriving split block run the epilogue ("fixup"; WGRAD
+//     atomics go straight into the fp32 weight gradient);
 //   * FWD epilogue adds the bias, rounds to bf16 and accumulates the per-channel BatchNorm
 //     statistics of the rounded output (sum, sum of squares) — BN needs no separate stats pass.
 #include "common.h"
@@ -81,6 +84,13 @@ struct ConvArgs {
   FastDiv dPQ, dQ;           // WGRAD pixel decomposition
   int has_bnf;               // DGRAD (stride 1, no accumulate): accumulate the preceding
   BnBwdFuse bnf;             //   block's BatchNorm-backward sums in the epilogue (api.h)
+  // split-K "ticket" fixup (FWD/DGRAD, small problems): every split adds its partial tile into
+  // facc [Mg][Ng] fp32 with device-scope atomics; the LAST split block of a tile (per-tile
+  // arrival ticket) reads the total back, clears it and runs the normal epilogue — no slab
+  // workspace, no finish launch. facc / tickets are zero on entry and left zero.
+  int fixup;
+  float* facc;
+  unsigned* tickets;
 };
 
 // ------------------------------------------------------------------ operand gathers
@@ -224,7 +234,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
   int kr = 0, ks_ = 0, kc = 0;  // slow path: (r, s, c) of this thread's chunk; fast path: uniform
   KInfo xk;              // WGRAD: (r,s,c) of this thread's B' column group
   int xk_same = 0;       // WGRAD "same" conv: byte offset of tap (r,s) channel c relative to m
-  int row0 = 0, col0 = 0, zsplit = 0, ks_begin = 0, ks_end = 0;
+  int row0 = 0, col0 = 0, zsplit = 0, ks_begin = 0, ks_end = 0, cur_tile = 0;
   const bool phase = MODE == MODE_DGRAD && args.phase;
   const int Sdec = phase ? args.St : gg.S;  // taps per kernel row in the reduction index
   const int cdim = MODE == MODE_FWD ? gg.C : gg.K;
@@ -244,6 +254,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
   auto setup = [&](int item) {
     zsplit = item / tiles;
     const int tile = xcd_remap(item - zsplit * tiles, tiles);
+    cur_tile = tile;
     const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
     row0 = tm * BM;
     col0 = tn * BN;
@@ -469,9 +480,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
   // ---------------- epilogue ----------------
   // acc[i][j][v] = D[row0 + wm*WTM + i*16 + (lane&15)][col0 + wn*WTN + j*16 + 4*(lane>>4) + v]
   // Ng % 8 == 0 for every mode (C, K multiples of 8), so a lane's 4 columns are all valid or not.
-  auto epilogue = [&](const int row0, const int col0, const int zs) {
+  auto epilogue = [&](const int row0, const int col0, const int zs, const bool split) {
   const ConvGeom& g = args.g;
-  const bool split = args.splits > 1;
   float* slab = split ? args.ws + (size_t)zs * args.Mg * args.Ng : nullptr;
   const int rl = lane & 15, cq = 4 * (lane >> 4);
   float stat_s[TN][4], stat_ss[TN][4];
@@ -643,6 +653,60 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
   }
   };
 
+  // Split-K ticket fixup (FWD/DGRAD): add this split's partial tile into facc with device-scope
+  // (sc1) float atomics, drain them (vmcnt), then one arrival ticket per block. Only the block
+  // drawing the tile's last ticket continues: it reads the totals back with device-scope loads
+  // (coherent across the XCD L2s), clears facc and the ticket for the next launch, and leaves
+  // the totals in acc[][] for the plain (non-split) epilogue. No release fence is needed: the
+  // atomics are performed past the L2 before the ticket (cdna_hip_programming.md Guideline 16).
+  // (the arrival flag travels through the first word of the idle operand ring: every wave is
+  // past its last MFMA read at the barrier below, and reads the flag before the barrier that
+  // precedes the next item's DMA)
+  int* fix_last = reinterpret_cast<int*>(smem);
+  auto fixup = [&]() -> bool {
+    const int rl = lane & 15, cq = 4 * (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = col0 + wn * WTN + j * 16 + cq;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = row0 + wm * WTM + i * 16 + rl;
+        if (col >= args.Ng || row >= args.Mg) continue;
+        float* d = args.facc + (size_t)row * args.Ng + col;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          __hip_atomic_fetch_add(d + t, acc[i][j][t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned t = __hip_atomic_fetch_add(args.tickets + cur_tile, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+      const bool last = t == (unsigned)(args.splits - 1);
+      if (last) __hip_atomic_store(args.tickets + cur_tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *fix_last = last ? 1 : 0;
+    }
+    __syncthreads();
+    if (!*fix_last) return false;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = col0 + wn * WTN + j * 16 + cq;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = row0 + wm * WTM + i * 16 + rl;
+        if (col >= args.Ng || row >= args.Mg) continue;
+        float* d = args.facc + (size_t)row * args.Ng + col;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          acc[i][j][t] = __hip_atomic_load(d + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(d + t, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+    return true;
+  };
+
   // NST-stage LDS ring: the DMAs of up to NST-1 k-steps are in flight while one is computed.
   constexpr int DMA = CA + CB;  // vector-memory instructions per thread per stage
   for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
@@ -667,7 +731,11 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
       compute(stage);
       stage = stage + 1 == NST ? 0 : stage + 1;
     }
-    epilogue(row0, col0, zsplit);
+    if (MODE != MODE_WGRAD && args.splits > 1 && args.fixup) {
+      if (fixup()) epilogue(row0, col0, zsplit, false);
+    } else {
+      epilogue(row0, col0, zsplit, args.splits > 1);
+    }
     wait_dma_barrier<0>();  // all reads of the ring done before the next item's prologue DMA
   }
 }
@@ -886,7 +954,15 @@ static FastDiv make_fastdiv(int d) {
 
 static bool fits_buffer(size_t elems) { return elems * 2 < (size_t)kOOB; }
 
-static int g_wgrad_atomic = 0;  // WGRAD split-K through fp32 atomics instead of slabs
+static int g_wgrad_atomic = 0;  // WGRAD split-K through fp32 atomics: 0 never, 1 always, 2 small
+// split-K ticket fixup (FWD/DGRAD): 0 never, 1 always (when the buffers fit), 2 when the
+// atomic traffic splits x M x N x 4 B is at most g_fixup_bytes (small, launch-bound problems)
+static int g_fixup = 2;
+static size_t g_fixup_bytes = 8u << 20;
+static float* g_facc = nullptr;       // fp32 accumulation buffer (zero between launches)
+static size_t g_facc_elems = 0;
+static unsigned* g_tickets = nullptr;  // per-tile arrival tickets (zero between launches)
+static size_t g_tickets_n = 0;
 static int g_persistent = 0;    // grid = resident slots, blocks loop over work items
 static int g_stages = 2;        // LDS ring depth policy (see stages_for)
 constexpr int kMaxAtomicSplits = 32;
@@ -971,7 +1047,18 @@ static void launch_cfg(ConvArgs& a, int splits, hipStream_t st, int nst_req = 0)
   a.ksteps_per_split = per;
   // same-address fp32 atomics serialise: beyond kMaxAtomicSplits partial sums per element the
   // slab + grouped-finish reduction is cheaper
+  const size_t atomic_bytes = 4ull * (size_t)splits * a.Mg * a.Ng;
+  if (a.wg_atomic == 2) a.wg_atomic = atomic_bytes <= g_fixup_bytes ? 1 : 0;
   if (a.wg_atomic && splits > kMaxAtomicSplits) a.wg_atomic = 0;
+  if (MODE != MODE_WGRAD && splits > 1 && a.fixup >= 0 && g_facc != nullptr &&
+      (size_t)a.Mg * a.Ng <= g_facc_elems && (size_t)tiles <= g_tickets_n &&
+      (a.fixup == 1 || (g_fixup == 1) || (g_fixup == 2 && atomic_bytes <= g_fixup_bytes))) {
+    a.fixup = 1;
+    a.facc = g_facc;
+    a.tickets = g_tickets;
+  } else {
+    a.fixup = 0;
+  }
   const int items = tiles * splits;
   // deepest ring that fits the 160 KiB LDS for this tile ((BM + BN) x 64 bf16 per stage)
   constexpr int kStageBytes = (BM + BN) * 64 * 2;
@@ -988,6 +1075,7 @@ static void launch_cfg(ConvArgs& a, int splits, hipStream_t st, int nst_req = 0)
 launched:
   if (splits == 1) return;
   if (MODE == MODE_WGRAD && a.wg_atomic) return;
+  if (MODE != MODE_WGRAD && a.fixup) return;
   if (MODE == MODE_WGRAD && a.g.wkrsc) {
     const size_t n4 = (size_t)a.Mg * a.Ng / 4;
     const int groups = (splits + kWgFinishGroupKrsc - 1) / kWgFinishGroupKrsc;
@@ -1088,6 +1176,18 @@ extern "C" void ddp_conv_options(int wgrad_atomic, int persistent, int stages) {
   g_wgrad_atomic = wgrad_atomic;
   g_persistent = persistent;
   g_stages = stages;
+}
+
+// Split-K ticket fixup: the zeroed accumulation / ticket buffers (allocated once per device by
+// ops/common.py, before any graph capture) and the policy (mode 0/1/2, byte threshold).
+extern "C" void ddp_conv_fixup(float* facc, size_t facc_elems, unsigned* tickets, size_t n_tickets,
+                               int mode, size_t max_bytes) {
+  g_facc = facc;
+  g_facc_elems = facc ? facc_elems : 0;
+  g_tickets = tickets;
+  g_tickets_n = tickets ? n_tickets : 0;
+  g_fixup = mode;
+  g_fixup_bytes = max_bytes;
 }
 
 // tile: index into the launch_mode table (0..kNumTiles-1)

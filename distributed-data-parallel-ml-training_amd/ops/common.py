@@ -19,7 +19,9 @@ def native():
         # DDP_AMD_CONV_PERSISTENT=1: conv grids sized to the resident slots, blocks loop over
         # tiles and prefetch the next tile's first k-step (default 0: one tile per workgroup)
         # DDP_AMD_CONV_STAGES: LDS ring depth policy of the conv GEMMs (2 = double buffering)
-        _NATIVE.conv_options(int(os.environ.get("DDP_AMD_WGRAD_ATOMIC", "0")),
+        # DDP_AMD_WGRAD_ATOMIC: 0 = slabs + finish, 1 = atomics, 2 (default) = atomics for
+        # small problems (split x M x N x 4 B <= DDP_AMD_FIXUP_KB), slabs for large ones
+        _NATIVE.conv_options(int(os.environ.get("DDP_AMD_WGRAD_ATOMIC", "2")),
                              int(os.environ.get("DDP_AMD_CONV_PERSISTENT", "0")),
                              int(os.environ.get("DDP_AMD_CONV_STAGES", str(CONV_STAGES))))
         load_conv_tuning(_NATIVE)
@@ -84,6 +86,16 @@ def check(t, dtype=None, shape=None, name="tensor"):
 WORKSPACE_ELEMS = 32 << 20  # 128 MiB of the 288 GB HBM
 _WS = {}
 
+# Split-K ticket fixup (conv_igemm.hip): small split-K problems (the strong-scaling batches: 32
+# images per GPU at 8 GPUs) accumulate their partial tiles with fp32 atomics and the last split
+# block of each tile runs the epilogue — no slab pass, no finish launch. One zeroed accumulation
+# buffer + one ticket array per process (the kernels leave both zero). Policy:
+# DDP_AMD_FIXUP=0 never / 1 always / 2 (default) when splits x M x N x 4 B <= DDP_AMD_FIXUP_KB.
+FIXUP_ELEMS = 4 << 20
+FIXUP_TICKETS = 1 << 16
+FIXUP_MODE = int(os.environ.get("DDP_AMD_FIXUP", "2"))
+FIXUP_KB = int(os.environ.get("DDP_AMD_FIXUP_KB", "8192"))
+
 
 def workspace(device):
     key = str(device)
@@ -91,6 +103,12 @@ def workspace(device):
     if ws is None:
         ws = torch.empty(WORKSPACE_ELEMS, dtype=torch.float32, device=device)
         _WS[key] = ws
+        if not _WS.get("_fixup"):
+            facc = torch.zeros(FIXUP_ELEMS, dtype=torch.float32, device=device)
+            tickets = torch.zeros(FIXUP_TICKETS, dtype=torch.int32, device=device)
+            _WS["_fixup"] = (facc, tickets)
+            native().conv_fixup(facc.data_ptr(), FIXUP_ELEMS, tickets.data_ptr(), FIXUP_TICKETS,
+                                FIXUP_MODE, FIXUP_KB << 10)
     return ws
 
 

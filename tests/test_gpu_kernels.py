@@ -359,3 +359,53 @@ def test_fused_sgd_zero_grad_and_counter(native_ext):
     assert int(cnt.item()) == 6
     for p, r in zip(ps, ref):
         assert torch.allclose(p, r, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("fixup", [0, 1])
+@pytest.mark.parametrize("case", [(8, 512, 2, 2, 512, 3, 1, 1), (4, 64, 16, 16, 128, 3, 1, 1),
+                                  (4, 64, 15, 15, 32, 3, 2, 1), (2, 128, 14, 14, 256, 1, 1, 0)])
+def test_conv_splitk_fixup(native_ext, case, fixup):
+    """Forced split-K (4 splits) with the ticket fixup (fp32 atomics, last split block runs the
+    epilogue: bias, bf16, BN statistics) against the slab + finish-kernel path and fp32 PyTorch;
+    the buffers must be left zero for the next launch. WGRAD runs with atomics into dW."""
+    from ddp_amd.ops import common
+    from ddp_amd.ops.common import ptr, stream_handle, workspace
+    N, Cin, H, W, K, R, stride, pad = case
+    conv, spec, x, xn = _conv_setup(N, Cin, H, W, K, R, stride, pad)
+    ws = workspace(xn.device)
+    facc, tickets = common._WS["_fixup"]
+    native_ext.conv_fixup(ptr(facc), facc.numel(), ptr(tickets), tickets.numel(), fixup, 1 << 30)
+    native_ext.conv_options(fixup, 0, common.CONV_STAGES)
+    try:
+        g = spec.geom(N, H, W)
+        P, Q = g[9], g[10]
+        z = torch.empty(N, P, Q, K, dtype=torch.bfloat16, device=DEV)
+        stats = torch.zeros(16 * 2 * K, device=DEV)
+        native_ext.conv_fwd(g, ptr(xn), ptr(spec.wc), ptr(conv.bias), ptr(z), ptr(stats), ptr(ws),
+                            ws.numel(), 4, stream_handle())
+        dz = bf(torch.randn(N, K, P, Q, device=DEV))
+        dzn = dz.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+        dx = torch.empty_like(xn)
+        native_ext.conv_dgrad(g, ptr(dzn), ptr(spec.wc), ptr(dx), ptr(ws), ws.numel(), 4,
+                              stream_handle())
+        dw = torch.zeros_like(conv.weight)
+        native_ext.conv_wgrad(g, ptr(dzn), ptr(xn), ptr(dw), ptr(ws), ws.numel(), 4,
+                              stream_handle())
+        torch.cuda.synchronize()
+    finally:
+        native_ext.conv_fixup(ptr(facc), facc.numel(), ptr(tickets), tickets.numel(),
+                              common.FIXUP_MODE, common.FIXUP_KB << 10)
+        native_ext.conv_options(int(__import__("os").environ.get("DDP_AMD_WGRAD_ATOMIC", "2")), 0,
+                                common.CONV_STAGES)
+    ref = F.conv2d(x, conv.weight, conv.bias, stride, pad).permute(0, 2, 3, 1)
+    assert rel_err(z, ref) < 1e-2
+    zf = z.float().reshape(-1, K)
+    st = stats.view(16, 2 * K).sum(0)
+    assert torch.allclose(st[:K], zf.sum(0), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(st[K:], (zf * zf).sum(0), rtol=1e-3, atol=1e-2)
+    xr = x.clone().requires_grad_(True)
+    wr = conv.weight.detach().clone().requires_grad_(True)
+    F.conv2d(xr, wr, None, stride, pad).backward(dz)
+    assert rel_err(dx.permute(0, 3, 1, 2), xr.grad) < 1e-2
+    assert rel_err(dw, wr.grad) < 1e-2
+    assert int(torch.count_nonzero(facc)) == 0 and int(torch.count_nonzero(tickets)) == 0
