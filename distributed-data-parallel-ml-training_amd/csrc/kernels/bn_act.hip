@@ -448,9 +448,10 @@ static unsigned blocks_for(size_t items, size_t per_block) {
 // channels; worth it (one launch fewer) while that re-read traffic stays small.
 constexpr size_t kFoldBytes = 24u << 20;
 // Backward fold threshold (replica bytes re-read by all apply blocks): measured 3-4x slower
-// applies when folding the big layers (>= 16 MB re-read at batch 256); the small grids of the
-// strong-scaling batches (<= 2 MB at 32 images per GPU) gain the finalize launch.
-static size_t kFoldBwdBytes = 4u << 20;  // DDP_AMD_BN_FOLD_BWD_KB overrides (0 = never fold)
+// applies when folding the big layers (>= 16 MB re-read at batch 256); at the strong-scaling
+// batches folding was measured slower as well (b32 step +50 us: each apply block re-reduces the
+// 16 replicas serially, profiles/r2_launch_reduction_ab.md) -> never by default.
+static size_t kFoldBwdBytes = 0;  // DDP_AMD_BN_FOLD_BWD_KB overrides (0 = never fold)
 static size_t kBwdBlocks = 1024;  // target reduce-grid size (DDP_AMD_BN_BWD_BLOCKS overrides)
 
 template <bool POOL, int IPT>

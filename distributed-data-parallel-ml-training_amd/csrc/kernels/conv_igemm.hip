@@ -957,7 +957,7 @@ static bool fits_buffer(size_t elems) { return elems * 2 < (size_t)kOOB; }
 static int g_wgrad_atomic = 0;  // WGRAD split-K through fp32 atomics: 0 never, 1 always, 2 small
 // split-K ticket fixup (FWD/DGRAD): 0 never, 1 always (when the buffers fit), 2 when the
 // atomic traffic splits x M x N x 4 B is at most g_fixup_bytes (small, launch-bound problems)
-static int g_fixup = 2;
+static int g_fixup = 0;
 static size_t g_fixup_bytes = 8u << 20;
 static float* g_facc = nullptr;       // fp32 accumulation buffer (zero between launches)
 static size_t g_facc_elems = 0;
@@ -1031,7 +1031,10 @@ static void launch_gemm_t(const ConvArgs& a, int items, hipStream_t st) {
 template <int MODE, int BM, int BN, int NST>
 static void launch_gemm(const ConvArgs& a, int items, hipStream_t st) {
   if constexpr (MODE == MODE_DGRAD) {
-    if (a.has_bnf && a.splits <= 1) return launch_gemm_t<MODE, BM, BN, NST, true>(a, items, st);
+    // the BN-backward sums are reduced in the non-split epilogue: a single split, or the
+    // ticket fixup's last-arriving split block
+    if (a.has_bnf && (a.splits <= 1 || a.fixup))
+      return launch_gemm_t<MODE, BM, BN, NST, true>(a, items, st);
   }
   launch_gemm_t<MODE, BM, BN, NST, false>(a, items, st);
 }

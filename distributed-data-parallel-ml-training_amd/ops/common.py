@@ -19,9 +19,10 @@ def native():
         # DDP_AMD_CONV_PERSISTENT=1: conv grids sized to the resident slots, blocks loop over
         # tiles and prefetch the next tile's first k-step (default 0: one tile per workgroup)
         # DDP_AMD_CONV_STAGES: LDS ring depth policy of the conv GEMMs (2 = double buffering)
-        # DDP_AMD_WGRAD_ATOMIC: 0 = slabs + finish, 1 = atomics, 2 (default) = atomics for
+        # DDP_AMD_WGRAD_ATOMIC: 0 (default) = slabs + finish, 1 = atomics, 2 = atomics for
         # small problems (split x M x N x 4 B <= DDP_AMD_FIXUP_KB), slabs for large ones
-        _NATIVE.conv_options(int(os.environ.get("DDP_AMD_WGRAD_ATOMIC", "2")),
+        # (2 measured 6-60% slower steps, profiles/r2_launch_reduction_ab.md)
+        _NATIVE.conv_options(int(os.environ.get("DDP_AMD_WGRAD_ATOMIC", "0")),
                              int(os.environ.get("DDP_AMD_CONV_PERSISTENT", "0")),
                              int(os.environ.get("DDP_AMD_CONV_STAGES", str(CONV_STAGES))))
         load_conv_tuning(_NATIVE)
@@ -90,10 +91,13 @@ _WS = {}
 # images per GPU at 8 GPUs) accumulate their partial tiles with fp32 atomics and the last split
 # block of each tile runs the epilogue — no slab pass, no finish launch. One zeroed accumulation
 # buffer + one ticket array per process (the kernels leave both zero). Policy:
-# DDP_AMD_FIXUP=0 never / 1 always / 2 (default) when splits x M x N x 4 B <= DDP_AMD_FIXUP_KB.
+# DDP_AMD_FIXUP=0 (default) never / 1 always / 2 when splits x M x N x 4 B <= DDP_AMD_FIXUP_KB.
+# OFF by default: measured on MI355X the device-scope atomics (they bypass the per-XCD L2s) make
+# the fixed-up GEMMs 3-5x slower than slab + finish (b32 step 0.884 vs 0.548 ms,
+# profiles/r2_launch_reduction_ab.md).
 FIXUP_ELEMS = 4 << 20
 FIXUP_TICKETS = 1 << 16
-FIXUP_MODE = int(os.environ.get("DDP_AMD_FIXUP", "2"))
+FIXUP_MODE = int(os.environ.get("DDP_AMD_FIXUP", "0"))
 FIXUP_KB = int(os.environ.get("DDP_AMD_FIXUP_KB", "8192"))
 
 
