@@ -59,11 +59,11 @@ def parse():
                    help="DDP gradient all-reduce dtype (bf16 halves the xGMI bytes; default "
                         "fp32 = the reference's gradient precision)")
     p.add_argument("--segmented", default=None,
-                   help="DDP: split the captured step at this fused stage and overlap the late "
-                        "layers' gradient all-reduce with the early layers' backward "
-                        "(engine/step.py SegmentedDDPStep); 0 = one graph, inline collectives. "
-                        "Default: 4 on >1 GPUs (VGG, fp32 gradients), else 0; env "
-                        "DDP_AMD_SEGMENTED overrides")
+                   help="DDP: cut the captured step before these fused stages (comma list) and "
+                        "run each bucket's all-reduce + optimizer update on the comm stream "
+                        "while the earlier layers' backward runs (engine/step.py "
+                        "SegmentedDDPStep); 0 = one graph, inline collectives. Default on >1 "
+                        "GPUs: VGG 4, ResNet-50 8,14; on 1 GPU 0. Env DDP_AMD_SEGMENTED overrides")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--train-size", type=int, default=None)
     p.add_argument("--json-out", default=None)
@@ -81,7 +81,7 @@ def main():
     from ddp_amd.optim import FusedSGD
     from ddp_amd.parallel import (DistributedDataParallel, RcclCommunicator, STRATEGIES,
                                   check_replicas)
-    from ddp_amd.utils import seed_everything
+    from ddp_amd.utils import Watchdog, seed_everything
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -93,6 +93,17 @@ def main():
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)  # control plane (TCPStore)
     comm = RcclCommunicator(rank, world, local_rank)
+    # failure detection: on >1 ranks a watchdog thread aborts the RCCL
+    # communicator and exits non-zero when no progress is reported for DDP_AMD_WATCHDOG_S
+    # seconds (default 300) or RCCL reports an async error, instead of hanging on a dead peer
+    watchdog = None
+    wd_s = float(os.environ.get("DDP_AMD_WATCHDOG_S", "300"))
+    if world > 1 and wd_s > 0:
+        watchdog = Watchdog(timeout_s=wd_s, comm=comm, poll_s=min(5.0, wd_s / 4)).start()
+
+    def beat():
+        if watchdog is not None:
+            watchdog.beat()
 
     seed_everything(ddp_amd.SEED)
     resnet = args.model.startswith("resnet")
@@ -127,13 +138,15 @@ def main():
     # collective at 100-300 GB/s: 1.11-1.36 ms inline vs 0.96-1.01 ms segmented,
     # profiles/r1_segmented_overlap.md); one GPU has no collective to hide -> one graph.
     if args.segmented is None:
-        args.segmented = os.environ.get("DDP_AMD_SEGMENTED", "4" if world > 1 else "0")
-    segmented = (int(args.segmented) > 0 and args.strategy == "ddp" and not resnet
-                 and args.grad_comm == "fp32" and not args.no_graph)
+        args.segmented = os.environ.get("DDP_AMD_SEGMENTED",
+                                        ("8,14" if resnet else "4") if world > 1 else "0")
+    cuts = [int(v) for v in str(args.segmented).split(",") if int(v) > 0]
+    segmented = bool(cuts) and args.strategy == "ddp" and not args.no_graph
     if segmented:
-        step = SegmentedDDPStep(model, opt, criterion, loader, split=int(args.segmented),
+        step = SegmentedDDPStep(model, opt, criterion, loader, split=cuts,
                                 emulate=int(os.environ.get("DDP_AMD_EMULATE_COMM", "0")),
-                                emulate_gbps=float(os.environ.get("DDP_AMD_EMULATE_COMM_GBPS", "0")))
+                                emulate_gbps=float(os.environ.get("DDP_AMD_EMULATE_COMM_GBPS", "0")),
+                                grad_comm=args.grad_comm)
     else:
         step = TrainStep(model, opt, criterion, loader, sync=sync, use_graph=not args.no_graph)
 
@@ -154,10 +167,12 @@ def main():
             print("[bench] replicas diverged under graph replay; timing eager steps",
                   file=sys.stderr)
         nwarm = max(nwarm - 1, 2)
+    beat()
     for _ in range(nwarm - 2):
         step.step()
     torch.cuda.synchronize()
     warm_loss = step.pop_loss()
+    beat()
 
     def barrier():
         if world > 1:
@@ -171,6 +186,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    beat()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -188,6 +204,7 @@ def main():
             torch.cuda.synchronize()
             if i > 0:
                 tot += time.perf_counter() - t
+            beat()
         ref = torch.tensor([tot / (args.ref_window - 1)], dtype=torch.float64)
         if world > 1:
             dist.all_reduce(ref)
@@ -236,6 +253,8 @@ def main():
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
+    if watchdog is not None:
+        watchdog.stop()
     if world > 1:
         dist.destroy_process_group()
 

@@ -289,6 +289,12 @@ PYBIND11_MODULE(_native, m) {
                         S(st)),
           "flag_wait");
   });
+  m.def("pack_bf16", [](uintptr_t x, size_t n, uintptr_t y, uintptr_t st) {
+    check(ddp_pack_bf16(P<float>(x), n, P<unsigned short>(y), S(st)), "pack_bf16");
+  });
+  m.def("unpack_bf16", [](uintptr_t y, size_t n, uintptr_t x, uintptr_t st) {
+    check(ddp_unpack_bf16(P<unsigned short>(y), n, P<float>(x), S(st)), "unpack_bf16");
+  });
   m.def("scale", [](uintptr_t x, size_t n, float s, uintptr_t st) {
     check(ddp_scale(P<float>(x), n, s, S(st)), "scale");
   });
@@ -302,6 +308,25 @@ PYBIND11_MODULE(_native, m) {
     return out;
   });
   m.def("make_unique_id", []() { return py::bytes(RcclComm::make_unique_id()); });
+
+  // host-only readiness / launch-order state machine (no GPU needed: CPU tests drive it with
+  // the same hook orders as the Python twin, tests/test_bucket_scheduler_cpu.py)
+  py::class_<ddp_amd::BucketScheduler>(m, "BucketScheduler")
+      .def(py::init([](std::vector<std::tuple<int, int, size_t, size_t>> bs, int n_params) {
+             std::vector<ddp_amd::BucketSpec> v;
+             for (auto& t : bs)
+               v.push_back({std::get<0>(t), std::get<1>(t), std::get<2>(t), std::get<3>(t)});
+             return new ddp_amd::BucketScheduler(v, n_params);
+           }))
+      .def("mark", &ddp_amd::BucketScheduler::mark)
+      .def("finish", &ddp_amd::BucketScheduler::finish)
+      .def("prepare", &ddp_amd::BucketScheduler::prepare)
+      .def("launched", &ddp_amd::BucketScheduler::launched)
+      .def("launch_order", &ddp_amd::BucketScheduler::launch_order)
+      .def("set_launch_order", &ddp_amd::BucketScheduler::set_launch_order)
+      .def("order_from_ready", &ddp_amd::BucketScheduler::order_from_ready)
+      .def("ready_order", &ddp_amd::BucketScheduler::ready_order)
+      .def("launch_log", &ddp_amd::BucketScheduler::launch_log);
 
   py::class_<StreamLink>(m, "StreamLink")
       .def(py::init<>())
@@ -367,5 +392,10 @@ PYBIND11_MODULE(_native, m) {
       .def("set_comm_dtype", &Reducer::set_comm_dtype)
       .def("comm_dtype", &Reducer::comm_dtype)
       .def("launched", &Reducer::launched)
+      .def("launch_order", [](Reducer& r) { return r.scheduler().launch_order(); })
+      .def("set_launch_order", [](Reducer& r, std::vector<int> o) { r.scheduler().set_launch_order(o); })
+      .def("order_from_ready", [](Reducer& r, std::vector<int> seq) { return r.scheduler().order_from_ready(seq); })
+      .def("ready_order", [](Reducer& r) { return r.scheduler().ready_order(); })
+      .def("launch_log", [](Reducer& r) { return r.scheduler().launch_log(); })
       .def("comm_stream", [](Reducer& r) { return reinterpret_cast<uintptr_t>(r.comm_stream()); });
 }

@@ -203,18 +203,15 @@ Reducer::Reducer(RcclComm* comm, float* arena, std::vector<size_t> offsets,
                  std::vector<size_t> numels, size_t cap_bytes, size_t cap_first_bytes,
                  bool average)
     : comm_(comm), arena_(arena), offsets_(std::move(offsets)), numels_(std::move(numels)),
+      sched_(plan_buckets(offsets_, numels_, sizeof(float), cap_bytes, cap_first_bytes),
+             (int)numels_.size()),
       average_(average) {
-  buckets_ = plan_buckets(offsets_, numels_, sizeof(float), cap_bytes, cap_first_bytes);
-  bucket_of_param_.assign(numels_.size(), -1);
-  for (size_t b = 0; b < buckets_.size(); ++b)
-    for (int p = buckets_[b].first_param; p < buckets_[b].last_param; ++p) bucket_of_param_[p] = (int)b;
-  pending_.assign(buckets_.size(), 0);
-  ready_.assign(buckets_.size(), 0);
-  contrib_.assign(buckets_.size(), {});
-  ready_ev_.assign(buckets_.size(), {});
-  done_ev_.resize(buckets_.size());
-  done_stream_.assign(buckets_.size(), nullptr);
-  for (size_t b = 0; b < buckets_.size(); ++b)
+  const size_t nb = sched_.buckets().size();
+  contrib_.assign(nb, {});
+  ready_ev_.assign(nb, {});
+  done_ev_.resize(nb);
+  done_stream_.assign(nb, nullptr);
+  for (size_t b = 0; b < nb; ++b)
     HIP_OK(hipEventCreateWithFlags(&done_ev_[b], hipEventDisableTiming));
   // DDP_AMD_COMM_PRIORITY=high: comm stream at the highest stream priority (default: normal)
   int lo = 0, hi = 0;
@@ -230,7 +227,7 @@ void Reducer::set_comm_dtype(int dtype) {
   comm_bf16_ = dtype == 1;
   if (comm_bf16_ && !stage_) {
     size_t n = 0;
-    for (const auto& b : buckets_) n = std::max(n, b.offset + b.count);
+    for (const auto& b : sched_.buckets()) n = std::max(n, b.offset + b.count);
     HIP_OK(hipMalloc(reinterpret_cast<void**>(&stage_), (n + 64) * sizeof(unsigned short)));
   }
 }
@@ -245,87 +242,69 @@ Reducer::~Reducer() {
 }
 
 void Reducer::prepare() {
-  for (size_t b = 0; b < buckets_.size(); ++b) {
-    pending_[b] = buckets_[b].last_param - buckets_[b].first_param;
-    ready_[b] = 0;
-    contrib_[b].clear();
-  }
-  next_launch_ = 0;
+  sched_.prepare();
+  for (auto& c : contrib_) c.clear();
 }
 
 void Reducer::mark_ready(int p, hipStream_t compute) {
-  if (p < 0 || p >= (int)bucket_of_param_.size()) throw std::runtime_error("bad param index");
-  const int b = bucket_of_param_[p];
-  if (pending_[b] <= 0) throw std::runtime_error("parameter marked ready twice in one backward");
-  auto& cs = contrib_[b];
+  if (p < 0 || p >= sched_.n_params()) throw std::runtime_error("bad param index");
+  auto& cs = contrib_[sched_.bucket_of(p)];
   if (std::find(cs.begin(), cs.end(), compute) == cs.end()) cs.push_back(compute);
-  if (--pending_[b] == 0) {
-    ready_[b] = 1;
-    launch_ready();
-  }
+  for (int b : sched_.mark(p)) launch(b);
 }
 
-// Launch buckets strictly in plan order so every rank issues collectives identically.
-// The comm stream waits on an event recorded NOW on every stream that produced part of the
-// bucket: that covers each producer's work up to its last contribution.
-void Reducer::launch_ready() {
-  while (next_launch_ < (int)buckets_.size() && ready_[next_launch_]) {
-    const int b = next_launch_++;
-    const BucketSpec& bs = buckets_[b];
-    auto& evs = ready_ev_[b];
-    // overlap: the collective runs on the comm stream; inline: on the stream that completed the
-    // bucket (stream order = no cross-stream edge in a captured graph)
-    // (world 1 without emulation has no collective: nothing to order against)
-    const bool real = comm_->live() || emulate_;
-    hipStream_t target = (overlap_ && real) ? comm_stream_ : contrib_[b].back();
-    for (size_t i = 0; i < contrib_[b].size(); ++i) {
-      if (contrib_[b][i] == target) continue;
-      if (i >= evs.size()) evs.resize(i + 1, nullptr);
-      if (!evs[i]) HIP_OK(hipEventCreateWithFlags(&evs[i], hipEventDisableTiming));
-      HIP_OK(hipEventRecord(evs[i], contrib_[b][i]));
-      HIP_OK(hipStreamWaitEvent(target, evs[i], 0));
-    }
-    float* buf = arena_ + bs.offset;
-    if (real && comm_bf16_) {
-      unsigned short* sb = stage_ + bs.offset;
-      if (ddp_pack_bf16(buf, bs.count, sb, target) != 0)
-        throw std::runtime_error("bf16 pack of a gradient bucket failed (alignment)");
-      if (comm_->live()) comm_->all_reduce(sb, bs.count, /*bf16*/ 1, average_ ? 4 : 0, target);
-      if (ddp_unpack_bf16(sb, bs.count, buf, target) != 0)
-        throw std::runtime_error("bf16 unpack of a gradient bucket failed (alignment)");
-    } else if (comm_->live()) {
-      comm_->all_reduce(buf, bs.count, /*fp32*/ 0, average_ ? 4 : 0, target);
-    } else if (emulate_) {
-      // world 1 stand-in for the collective (graph-structure / overlap studies on one GPU):
-      // one pass over the bucket, like the reduction kernel of an all-reduce
-      if (emulate_gbps_ > 0.0) {
-        const float us = (float)(4.0 * bs.count / (emulate_gbps_ * 1e3));
-        if (ddp_comm_standin(buf, bs.count, emulate_blocks_, us, 1.0f, target) != 0)
-          throw std::runtime_error("emulated collective launch failed");
-      } else {
-        for (int i = 0; i < emulate_passes_; ++i)
-          if (ddp_scale(buf, bs.count, 1.0f, target) != 0)
-            throw std::runtime_error("emulated collective launch failed");
-      }
-    }
-    done_stream_[b] = target;
-    HIP_OK(hipEventRecord(done_ev_[b], target));
-    if (debug_sync_) HIP_OK(hipStreamSynchronize(target));
+// Buckets launch in the scheduler's launch order (plan order, or the rebuilt completion order)
+// so every rank issues collectives identically. The comm stream waits on an event recorded NOW
+// on every stream that produced part of the bucket: that covers each producer's work up to its
+// last contribution.
+void Reducer::launch(int b) {
+  const BucketSpec& bs = sched_.buckets()[b];
+  auto& evs = ready_ev_[b];
+  // overlap: the collective runs on the comm stream; inline: on the stream that completed the
+  // bucket (stream order = no cross-stream edge in a captured graph)
+  // (world 1 without emulation has no collective: nothing to order against)
+  const bool real = comm_->live() || emulate_;
+  hipStream_t target = (overlap_ && real) ? comm_stream_ : contrib_[b].back();
+  for (size_t i = 0; i < contrib_[b].size(); ++i) {
+    if (contrib_[b][i] == target) continue;
+    if (i >= evs.size()) evs.resize(i + 1, nullptr);
+    if (!evs[i]) HIP_OK(hipEventCreateWithFlags(&evs[i], hipEventDisableTiming));
+    HIP_OK(hipEventRecord(evs[i], contrib_[b][i]));
+    HIP_OK(hipStreamWaitEvent(target, evs[i], 0));
   }
+  float* buf = arena_ + bs.offset;
+  if (real && comm_bf16_) {
+    unsigned short* sb = stage_ + bs.offset;
+    if (ddp_pack_bf16(buf, bs.count, sb, target) != 0)
+      throw std::runtime_error("bf16 pack of a gradient bucket failed (alignment)");
+    if (comm_->live()) comm_->all_reduce(sb, bs.count, /*bf16*/ 1, average_ ? 4 : 0, target);
+    if (ddp_unpack_bf16(sb, bs.count, buf, target) != 0)
+      throw std::runtime_error("bf16 unpack of a gradient bucket failed (alignment)");
+  } else if (comm_->live()) {
+    comm_->all_reduce(buf, bs.count, /*fp32*/ 0, average_ ? 4 : 0, target);
+  } else if (emulate_) {
+    // world 1 stand-in for the collective (graph-structure / overlap studies on one GPU):
+    // one pass over the bucket, like the reduction kernel of an all-reduce
+    if (emulate_gbps_ > 0.0) {
+      const float us = (float)(4.0 * bs.count / (emulate_gbps_ * 1e3));
+      if (ddp_comm_standin(buf, bs.count, emulate_blocks_, us, 1.0f, target) != 0)
+        throw std::runtime_error("emulated collective launch failed");
+    } else {
+      for (int i = 0; i < emulate_passes_; ++i)
+        if (ddp_scale(buf, bs.count, 1.0f, target) != 0)
+          throw std::runtime_error("emulated collective launch failed");
+    }
+  }
+  done_stream_[b] = target;
+  HIP_OK(hipEventRecord(done_ev_[b], target));
+  if (debug_sync_) HIP_OK(hipStreamSynchronize(target));
 }
 
 void Reducer::finalize(hipStream_t compute) {
-  for (size_t b = 0; b < buckets_.size(); ++b)
-    if (!ready_[b]) {
-      if (pending_[b] != 0)
-        throw std::runtime_error("Reducer::finalize: bucket " + std::to_string(b) +
-                                 " has parameters whose gradient was never produced "
-                                 "(unused parameters are not supported)");
-    }
-  launch_ready();
-  for (int b = 0; b < next_launch_; ++b)
+  for (int b : sched_.finish()) launch(b);  // throws if a parameter never got a gradient
+  for (size_t b = 0; b < done_stream_.size(); ++b)
     if (done_stream_[b] != compute) HIP_OK(hipStreamWaitEvent(compute, done_ev_[b], 0));
-  prepare();
+  for (auto& c : contrib_) c.clear();
 }
 
 }  // namespace ddp_amd

@@ -66,9 +66,11 @@ class Reducer {
           size_t cap_bytes, size_t cap_first_bytes, bool average);
   ~Reducer();
 
-  const std::vector<BucketSpec>& buckets() const { return buckets_; }
+  const std::vector<BucketSpec>& buckets() const { return sched_.buckets(); }
   // Start of a backward pass: reset readiness counters.
   void prepare();
+  // readiness / launch-order state machine (buckets.h): launch order, rebuild, logs
+  BucketScheduler& scheduler() { return sched_; }
   // Gradient for parameter `p` has been fully written on `compute` (stream order). A bucket's
   // gradients may come from several streams (the backward runs weight gradients on a side
   // stream): its all-reduce waits on every stream that contributed to it.
@@ -95,23 +97,19 @@ class Reducer {
   // widened back into the fp32 arena. Allocates the staging buffer (call before capture).
   void set_comm_dtype(int dtype);
   int comm_dtype() const { return comm_bf16_ ? 1 : 0; }
-  int launched() const { return next_launch_; }
+  int launched() const { return sched_.launched(); }
   hipStream_t comm_stream() const { return comm_stream_; }
 
  private:
-  void launch_ready();
+  void launch(int b);
   RcclComm* comm_;
   float* arena_;
   std::vector<size_t> offsets_, numels_;
-  std::vector<BucketSpec> buckets_;
-  std::vector<int> bucket_of_param_;
-  std::vector<int> pending_;  // params still missing per bucket
-  std::vector<char> ready_;   // bucket complete
+  BucketScheduler sched_;
   std::vector<std::vector<hipStream_t>> contrib_;  // distinct producer streams per bucket
   std::vector<std::vector<hipEvent_t>> ready_ev_;  // one event per producer stream slot
   std::vector<hipEvent_t> done_ev_;
   std::vector<hipStream_t> done_stream_;  // stream each bucket's collective ran on
-  int next_launch_ = 0;
   bool average_;
   bool debug_sync_ = false;
   bool overlap_ = true;

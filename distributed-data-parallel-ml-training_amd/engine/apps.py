@@ -80,11 +80,13 @@ def main(part, argv=None):
         from .step import TrainStep, SegmentedDDPStep
         arena = model.arena if hasattr(model, "arena") else optimizer.arena
         snap = (arena.data.clone(), optimizer.momentum_buffer.clone())
-        split = int(os.environ.get("DDP_AMD_SEGMENTED", "4"))
-        if (strategy == "ddp" and world > 1 and split > 0
+        default_cuts = "8,14" if args.model.startswith("resnet") else "4"
+        split = [int(v) for v in os.environ.get("DDP_AMD_SEGMENTED", default_cuts).split(",")
+                 if int(v) > 0]
+        if (strategy == "ddp" and world > 1 and split
                 and hasattr(model.module, "forward_loss_split")):
-            # late layers' bucket all-reduced on a second stream during the early backward
-            # (profiles/r1_segmented_overlap.md)
+            # each bucket's all-reduce + optimizer update on the comm stream while the earlier
+            # layers' backward runs (engine/step.py SegmentedDDPStep)
             step = SegmentedDDPStep(model, optimizer, criterion, train_loader, split=split)
         else:
             step = TrainStep(model, optimizer, criterion, train_loader, sync=sync)

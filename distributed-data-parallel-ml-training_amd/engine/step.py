@@ -162,51 +162,73 @@ class TrainStep:
 
 
 class SegmentedDDPStep(TrainStep):
-    """DDP step whose late-layer gradient all-reduce overlaps the early layers' backward,
-    without a comm branch inside a captured graph.
+    """DDP step whose bucket all-reduces AND optimizer updates overlap the rest of the backward,
+    without any comm branch inside a captured graph (VGG and ResNet; fp32 or bf16 gradients).
 
     Why: one captured graph whose comm-stream branch stays open across the backward runs 2.4-3x
     slower on ROCm 7 (profiles/r1_comm_stream_study.md: the graph executor spreads it over
-    several hardware queues). Here the step is two single-stream graphs:
+    several hardware queues). The backward is therefore cut at the fused stages ``split``
+    (models: ``forward_loss_split`` / ``first_param_of_stage``) into K+1 segments, each one
+    single-stream graph on the main stream; bucket j is the arena slice of segment j's
+    parameters (the arena is in parameter order, so bucket 0 = the LAST layers, whose gradients
+    are ready first). Per step, host order:
 
-        g1 (main):  augment + forward + backward of the stages >= ``split`` -> flag_signal(S)
-        eager:      comm stream: flag_wait(S) -> all-reduce bucket A (those stages' gradients,
-                    VGG-11 split 4: 89% of the bytes; SECOND RCCL communicator) -> flag_signal(D)
-        g2 (main):  backward of the stages < split -> all-reduce bucket B inline (DDP
-                    communicator) -> flag_wait(D) -> fused SGD (+ grad clear, cursor advance)
+        g[0] (main):  flag_wait(D) -> augment + forward + backward of segment 0 -> flag_signal(S)
+        comm stream:  flag_wait(S) -> all-reduce bucket 0 -> fused SGD of bucket 0
+        g[1] (main):  backward of segment 1 -> flag_signal(S)
+        comm stream:  flag_wait(S) -> all-reduce bucket 1 -> fused SGD of bucket 1
+        ...
+        g[K] (main):  backward of segment K -> flag_signal(S)
+        comm stream:  flag_wait(S) -> all-reduce bucket K -> fused SGD of bucket K (+ data
+                      cursor advance) -> flag_signal(D)
 
-    flag_signal / flag_wait (comm_util.hip) are an agent-scope release increment and a bounded
-    one-wave spin (on timeout it records an error and returns) — cheaper than event edges
-    between graph launches (~15 us idle per edge measured). Deadlock-free however HIP maps
-    streams onto hardware queues: every wait's producer is enqueued before the wait in host
-    order (the comm stream's wait follows g1's launch, g2's wait follows the all-reduce's
-    launch), so a queue shared by producer and waiter holds the producer first. (A single-graph
-    variant — comm work enqueued before the graph — measured faster but has the comm-side spin
-    enqueued BEFORE its producer: on a shared hardware queue it deadlocks.)
+    so each bucket's collective and its share of the optimizer run while the earlier layers are
+    still back-propagating, and only the first layers' (small) bucket is exposed. The next
+    step's forward waits for D (every parameter updated). flag_signal / flag_wait
+    (comm_util.hip) are an agent-scope release increment and a bounded one-wave spin (on
+    timeout it records an error word and returns; the optimizer launches skip the update when
+    the word is set, so a timed-out step never applies unreduced gradients). Deadlock-free
+    however HIP maps streams onto hardware queues: every wait's producer is enqueued before the
+    wait in host order. The bucket collectives run eagerly on their OWN RCCL communicator
+    (never mixed with graph-captured collectives of the DDP communicator, e.g. ResNet's
+    BatchNorm-buffer broadcast inside g[0]); all of them sit on one stream, so they are
+    serialised like the reference DDP's buckets (/root/reference/part3/main.py:174).
 
-    The DDP wrapper's own reducer is bypassed (``no_sync``); the arena is in parameter order, so
-    bucket A is its tail. Models provide ``forward_loss_split`` / ``first_param_of_stage``
-    (models/vgg.py). Measured with a 32-CU stand-in collective: profiles/r1_segmented_overlap.md.
-    World size 1: the collectives are no-ops unless ``emulate`` > 0 (bucket-sized stand-in
-    passes) or ``emulate_gbps`` > 0 (a 32-CU stand-in lasting bytes / emulate_gbps that then
-    multiplies the bucket by ``emulate_scale``: an optimizer that did not wait would miss it).
+    The DDP wrapper's own reducer is bypassed (``no_sync``). World size 1 has no collective
+    unless ``emulate`` > 0 (bucket-sized stand-in passes) or ``emulate_gbps`` > 0 (a 32-CU
+    stand-in lasting bytes / emulate_gbps that then multiplies the bucket by ``emulate_scale``:
+    an optimizer that did not wait would miss it). Measurements: profiles/r1_segmented_overlap.md
+    (single cut, v4) and profiles/r2_pipelined_ddp.md.
     """
 
     WAIT_TIMEOUT_S = 100.0  # a device-side wait that exceeds this records an error and returns
 
     def __init__(self, ddp, optimizer, criterion, loader, split=4, emulate=0, emulate_gbps=0.0,
-                 emulate_scale=1.0):
+                 emulate_scale=1.0, grad_comm="fp32"):
         super().__init__(ddp, optimizer, criterion, loader, sync=None, use_graph=True)
         inner = getattr(ddp, "module", None)
         if inner is None or not hasattr(inner, "forward_loss_split") or not self.fold_opt:
             raise ValueError("SegmentedDDPStep needs a DDP-wrapped model with forward_loss_split, "
                              "the fused optimizer and the device loader")
-        self.ddp, self.split, self.emulate = ddp, int(split), int(emulate)
+        splits = [int(split)] if isinstance(split, (int, str)) else sorted(int(v) for v in split)
+        self.ddp, self.splits, self.emulate = ddp, splits, int(emulate)
+        self.split = splits[0] if len(splits) == 1 else splits
         self.emulate_gbps, self.emulate_scale = float(emulate_gbps), float(emulate_scale)
+        if grad_comm not in ("fp32", "bf16"):
+            raise ValueError("grad_comm must be 'fp32' or 'bf16'")
+        self.grad_comm = grad_comm
         arena = ddp.arena
-        first = inner.first_param_of_stage(self.split)
-        idx = next(i for i, p in enumerate(arena.params) if p is first)
-        self.cut = arena.offsets[idx]
+        pidx = {id(p): i for i, p in enumerate(arena.params)}
+        first = [pidx[id(inner.first_param_of_stage(sp))] for sp in splits]
+        # buckets (param index ranges, arena element ranges), segment order = backward order
+        bounds = [len(arena.params)] + first[::-1] + [0]
+        self.buckets = []
+        for j in range(len(bounds) - 1):
+            i1, i0 = bounds[j], bounds[j + 1]
+            lo = arena.offsets[i0]
+            hi = arena.offsets[i1] if i1 < len(arena.params) else arena.total
+            self.buckets.append(((i0, i1), (lo, hi)))
+        self.cut = self.buckets[0][1][0]  # start of the last layers' bucket (tests)
         self.total = arena.total
         self.comm_stream = torch.cuda.Stream()
         self.comm_a = None
@@ -219,11 +241,16 @@ class SegmentedDDPStep(TrainStep):
             warm = torch.zeros(64, dtype=torch.float32, device=loader.device)
             self.comm_a.all_reduce(warm)
             torch.cuda.synchronize()
-        # [0] = S (late backward done), [1] = D (bucket A reduced), [2], [3] = the waiters'
-        # expected counts, [4] = error word
+        self._stage = None
+        if grad_comm == "bf16":
+            self._stage = torch.empty(arena.total, dtype=torch.bfloat16, device=loader.device)
+        # [0] = S (segment backward done, counts up), [1] = D (step's updates done), [2], [3] =
+        # the waiters' expected counts, [4] = error word. D starts at 1: the first step's forward
+        # has nothing to wait for.
         self._flags = torch.zeros(8, dtype=torch.int32, device=loader.device)
+        self._flags[1] = 1
         self.graphs = None
-        self._h = self._h_leaf = None
+        self._cuts = None
 
     def _fp(self, i):
         return self._flags.data_ptr() + 4 * i
@@ -233,17 +260,27 @@ class SegmentedDDPStep(TrainStep):
         from ..parallel.comm import AVG
         g = self.ddp.arena.grad
         n = hi - lo
+        cs = stream.cuda_stream
         if comm is not None:
-            comm.comm.all_reduce(g.data_ptr() + 4 * lo, n, 0, AVG, stream.cuda_stream)
+            if self._stage is not None:  # bf16 wire format: half the xGMI bytes
+                sb = self._stage.data_ptr() + 2 * lo
+                native().pack_bf16(g.data_ptr() + 4 * lo, n, sb, cs)
+                comm.comm.all_reduce(sb, n, 1, AVG, cs)
+                native().unpack_bf16(sb, n, g.data_ptr() + 4 * lo, cs)
+            else:
+                comm.comm.all_reduce(g.data_ptr() + 4 * lo, n, 0, AVG, cs)
         elif self.emulate_gbps > 0:  # timed 32-CU stand-in (comm_util.hip comm_standin)
             native().comm_standin(g.data_ptr() + 4 * lo, n, 32, 4.0 * n / (self.emulate_gbps * 1e3),
-                                  self.emulate_scale, stream.cuda_stream)
+                                  self.emulate_scale, cs)
         else:
             for _ in range(self.emulate):
-                native().scale(g.data_ptr() + 4 * lo, n, 1.0, stream.cuda_stream)
+                native().scale(g.data_ptr() + 4 * lo, n, 1.0, cs)
 
-    def _seg1(self):
+    def _seg_first(self):
         from ..ops.common import native
+        main = torch.cuda.current_stream()
+        native().flag_wait(self._fp(1), self._fp(3), self._fp(4), self.WAIT_TIMEOUT_S,
+                           main.cuda_stream)
         self.ddp._sync_buffers()  # what DDP.forward would do (no-op without buffers / at world 1)
         with self.ddp.no_sync():
             with trace_range("data"):
@@ -251,50 +288,58 @@ class SegmentedDDPStep(TrainStep):
             with trace_range("forward"):
                 loss, cuts = self.ddp.module.forward_loss_split(
                     x, y, self.split, acc=self.loss_sum, transient=True)
-            with trace_range("backward_late"):
+            with trace_range("backward_seg0"):
                 loss.backward(self._one)
-        self._h, self._h_leaf = cuts[0]
+        self._cuts = cuts
+        native().flag_signal(self._fp(0), main.cuda_stream)
+
+    def _seg(self, j):
+        """Backward of segment j >= 1 (the stages before cut K-j+1)."""
+        from ..ops.common import native
+        h, leaf = self._cuts[len(self._cuts) - j]
+        with self.ddp.no_sync():
+            with trace_range(f"backward_seg{j}"):
+                h.backward(leaf.grad)
+        if j == len(self.buckets) - 1:
+            self._cuts = None
         native().flag_signal(self._fp(0), torch.cuda.current_stream().cuda_stream)
 
-    def _comm_late(self):
-        """Eager, between the graphs: wait S, bucket A on the comm stream, signal D."""
+    def _comm(self, j):
+        """Eager, after segment j's graph: wait S, all-reduce bucket j, update its parameters
+        (and after the last bucket: advance the data cursor, signal D)."""
         from ..ops.common import native
-        cs = self.comm_stream.cuda_stream
-        native().flag_wait(self._fp(0), self._fp(2), self._fp(4), self.WAIT_TIMEOUT_S, cs)
-        with trace_range("sync_late"):
-            self._allreduce(self.cut, self.total, self.comm_stream, self.comm_a)
-        native().flag_signal(self._fp(1), cs)
-
-    def _seg2(self):
-        from ..ops.common import native
-        with self.ddp.no_sync():
-            with trace_range("backward_early"):
-                self._h.backward(self._h_leaf.grad)
-        self._h = self._h_leaf = None
-        main = torch.cuda.current_stream()
-        with trace_range("sync_early"):  # bucket B, inline on the DDP communicator
-            comm = self.ddp.comm if is_live(self.ddp.comm) else None
-            self._allreduce(0, self.cut, main, comm)
-        native().flag_wait(self._fp(1), self._fp(3), self._fp(4), self.WAIT_TIMEOUT_S,
-                           main.cuda_stream)
-        with trace_range("optimizer"):
+        cs = self.comm_stream
+        native().flag_wait(self._fp(0), self._fp(2), self._fp(4), self.WAIT_TIMEOUT_S,
+                           cs.cuda_stream)
+        (i0, i1), (lo, hi) = self.buckets[j]
+        last = j == len(self.buckets) - 1
+        with trace_range(f"sync_bucket{j}"):
+            self._allreduce(lo, hi, cs, self.comm_a)
+        with trace_range(f"optimizer_bucket{j}"):
             # a timed-out wait (error word set) skips the update: never apply gradients whose
-            # bucket A was not averaged
-            self.optimizer.step(zero_grad=True, counter=self.loader.cursor_advance(),
-                                skip=self._fp(4))
+            # bucket was not averaged
+            self.optimizer.step(zero_grad=True, params=(i0, i1), stream=cs, skip=self._fp(4),
+                                counter=self.loader.cursor_advance() if last else None)
+        if last:
+            native().flag_signal(self._fp(1), cs.cuda_stream)
+
+    def _segments(self):
+        return [self._seg_first] + [(lambda j=j: self._seg(j)) for j in range(1, len(self.buckets))]
 
     def _body(self):
-        self._seg1()
-        self._comm_late()
-        self._seg2()
+        for j, seg in enumerate(self._segments()):
+            seg()
+            self._comm(j)
 
     def capture(self):
         torch.cuda.synchronize()
         self.check_error()
         mode = capture_mode()
-        pool = torch.cuda.graph_pool_handle()  # activations of g1 are read by g2
+        pool = torch.cuda.graph_pool_handle()  # activations of g[0] are read by later graphs
         graphs = []
-        for seg in (self._seg1, self._seg2):
+        # each segment is its own single-stream graph (capturing runs no kernel: the flag
+        # counters need no host-side bookkeeping)
+        for seg in self._segments():
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=pool, capture_error_mode=mode):
                 seg()
@@ -306,12 +351,12 @@ class SegmentedDDPStep(TrainStep):
         if self.graph is None:  # never captured, or validate_distributed fell back to eager
             self._body()
             return
-        self.graphs[0].replay()
-        self._comm_late()
-        self.graphs[1].replay()
+        for j, g in enumerate(self.graphs):
+            g.replay()
+            self._comm(j)
 
     def check_error(self):
-        """Raise if the device-side wait gave up (bucket A never completed within the timeout)."""
+        """Raise if a device-side wait gave up (a bucket never completed within the timeout)."""
         if int(self._flags[4].item()) != 0:
             raise RuntimeError("SegmentedDDPStep: a device-side stream wait timed out "
                                f"(> {self.WAIT_TIMEOUT_S}s); the step's results are invalid")

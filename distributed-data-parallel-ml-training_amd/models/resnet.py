@@ -141,6 +141,50 @@ class ResNet(nn.Module):
             h = b.forward_fused(h)
         return linear_gemm(global_avg_pool(h), fc)
 
+    # ------------------------------------------------------------ segmented backward (DDP)
+    # Stages: 0 = stem (conv1 + bn1 + relu + maxpool), 1..16 = the bottleneck blocks in order.
+    # A cut before stage s detaches the stage's input, so the backward runs in segments the
+    # pipelined DDP step (engine/step.py SegmentedDDPStep) puts bucket all-reduces between.
+    def n_stages(self):
+        return 1 + len(list(self.blocks()))
+
+    def first_param_of_stage(self, i):
+        """Parameter that starts stage ``i`` in ``parameters()`` order (its first conv weight):
+        a stage's parameters are contiguous in the flat arena."""
+        if i == 0:
+            return self.conv1.weight
+        return list(self.blocks())[i - 1].conv1.weight
+
+    def forward_loss_split(self, x, labels, split, acc=None, transient=False):
+        """Mean CE loss of the fused GPU forward, cut before stage(s) ``split`` (int or
+        ascending list in 1..n_stages-1): returns (loss, cuts), cuts[k] = (h_k, leaf_k) as in
+        models/vgg.py ``forward_loss_split``. A cut block input that feeds both residual
+        branches is a leaf: the two branch gradients meet in its ``.grad``."""
+        from ..ops.common import step_scratch
+        from ..ops.layers import (conv_bn_act, cross_entropy, global_avg_pool, linear_gemm,
+                                  max_pool, to_nhwc_input)
+        stem, fc = self._gpu_specs()
+        blocks = list(self.blocks())
+        n = 1 + len(blocks)
+        splits = [split] if isinstance(split, int) else list(split)
+        if not splits or splits != sorted(set(splits)) or not 0 < splits[0] or splits[-1] >= n:
+            raise ValueError(f"split stages must be ascending in 1..{n - 1}")
+        step_scratch(x.device).zero()
+        if self.training:
+            self._bump_batches_tracked()
+        h = to_nhwc_input(x, 8)
+        cuts = []
+        for st in range(n):
+            if st in splits:
+                leaf = h.detach().requires_grad_(True)
+                cuts.append((h, leaf))
+                h = leaf
+            h = max_pool(conv_bn_act(h, stem), 3, 2, 1) if st == 0 else blocks[st - 1].forward_fused(h)
+        loss = cross_entropy(linear_gemm(global_avg_pool(h), fc), labels)
+        if acc is not None:
+            acc.add_(loss.detach())
+        return loss, cuts
+
     def _bump_batches_tracked(self):
         nbt = getattr(self, "_nbt", None)
         if nbt is None:

@@ -143,6 +143,10 @@ class _VGG(nn.Module):
         loss = linear_cross_entropy(h.view(h.shape[0], -1), self.fc1, labels, acc, transient)
         return loss, cuts
 
+    def n_stages(self):
+        """Number of fused Conv->BN->ReLU(->pool) stages (cut points for forward_loss_split)."""
+        return sum(1 for v in _cfg[self.name] if v != 'M')
+
     def first_param_of_stage(self, i):
         """Parameter that starts fused stage ``i`` in ``parameters()`` order (its conv weight)."""
         return self.fused_plan()[i].conv.weight

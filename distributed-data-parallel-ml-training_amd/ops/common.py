@@ -198,17 +198,33 @@ SCRATCH_ELEMS = 8 << 20
 
 
 class StepScratch:
+    """Chunked: a process that builds many models (a test session) gets further chunks instead
+    of running out; a single model lives in the first chunk, so its forward clears its
+    accumulators with ONE fill (or none, when the loader's launch already did: claim_zero)."""
+
     def __init__(self, device):
-        self.buf = torch.zeros(SCRATCH_ELEMS, dtype=torch.float32, device=device)
-        self.used = 0
+        self.device = device
+        self.chunks = [torch.zeros(SCRATCH_ELEMS, dtype=torch.float32, device=device)]
+        self.used_in = [0]
+
+    @property
+    def buf(self):
+        return self.chunks[0]
+
+    @property
+    def used(self):
+        return self.used_in[0]
 
     def take(self, n):
-        off = self.used
         n = (n + 63) // 64 * 64
-        if off + n > self.buf.numel():
-            raise RuntimeError("StepScratch exhausted; raise ops.common.SCRATCH_ELEMS")
-        self.used = off + n
-        return self.buf[off:off + n]
+        off = self.used_in[-1]
+        if off + n > self.chunks[-1].numel():
+            self.chunks.append(torch.zeros(max(SCRATCH_ELEMS, n), dtype=torch.float32,
+                                           device=self.device))
+            self.used_in.append(0)
+            off = 0
+        self.used_in[-1] = off + n
+        return self.chunks[-1][off:off + n]
 
     def take_transient(self, n):
         """A zeroed slice valid until the next zero(): consecutive calls within one forward get
@@ -217,7 +233,7 @@ class StepScratch:
             self._transient = self.take(256)
             self._tcur = 0
         if self._tcur + n > self._transient.numel():
-            return torch.zeros(n, dtype=torch.float32, device=self.buf.device)
+            return torch.zeros(n, dtype=torch.float32, device=self.device)
         out = self._transient[self._tcur:self._tcur + n]
         self._tcur += n
         return out
@@ -226,16 +242,18 @@ class StepScratch:
         """For a kernel that runs right before the next forward (the batch loader's augment
         launch): returns (pointer, count) of the region to clear and marks it cleared, so the
         forward's zero() skips its fill launch."""
-        if not self.used:
+        if len(self.chunks) != 1 or not self.used_in[0]:
             return 0, 0
         self._pre_zeroed = True
-        return self.buf.data_ptr(), self.used
+        return self.chunks[0].data_ptr(), self.used_in[0]
 
     def zero(self):
         if getattr(self, "_pre_zeroed", False):
             self._pre_zeroed = False  # cleared by the loader's launch for this forward
-        elif self.used:
-            self.buf[:self.used].zero_()
+        else:
+            for c, u in zip(self.chunks, self.used_in):
+                if u:
+                    c[:u].zero_()
         self._tcur = 0
 
 

@@ -39,47 +39,58 @@ class FusedSGD(torch.optim.SGD):
             from ..ops.common import native, stream_handle
             native().pack_conv_weights(descs, stream_handle())
 
-    def _work_table(self):
+    def _work_table(self, prange=None):
         """Device work-item table of the fused SGD + re-pack kernel (rebuilt when the set of
-        packed conv weights changes, e.g. after the model's fused plan is first built)."""
+        packed conv weights changes, e.g. after the model's fused plan is first built).
+        ``prange = (i0, i1)`` restricts it to parameters i0 <= i < i1 (one DDP bucket: the
+        pipelined step updates each bucket as soon as its all-reduce is done)."""
         from ..ops.common import native
         a = self.arena
         key = tuple(self._packs())
-        if getattr(self, "_table_key", None) == key:
-            return self._items, self._n_items, self._descs
-        descs, items, conv = [], [], set()
-        for i, p in enumerate(a.params):
-            if not hasattr(p, "_ddp_amd_pack"):
-                continue
-            pp, wc, wt, K, Cr, C, R, S, krsc = p._ddp_amd_pack()
-            if pp != a.data.data_ptr() + 4 * a.offsets[i] or (R * S > 1 and bool(krsc) != a.krsc[i]):
-                raise RuntimeError("packed conv weight is not a view into the parameter arena")
-            d = len(descs)
-            descs.append([a.offsets[i], K, Cr, C, R, S, wc, wt, int(krsc), 0, 0, 0])
-            conv.add(i)
-            n = a.numels[i]
-            if not wt and C == Cr and (krsc or R * S == 1) and n % 4 == 0:
-                # bf16 copy in the master's own index order: elementwise items
-                for s0 in range(0, n, 8192):
-                    items.append([2, s0, min(8192, n - s0), d])
-                continue
-            TK, TC = native().sgd_tile_dims(R * S)
-            for k0 in range(0, K, TK):
-                for c0 in range(0, C, TC):
-                    items.append([1, d, k0, c0])
-        chunk = 8192
-        for i in range(len(a.params)):
-            if i in conv:
-                continue
-            o, n = a.offsets[i], a.numels[i]
-            for s in range(0, n, chunk):
-                items.append([0, o + s, min(chunk, n - s), 0])
-        dev = a.data.device
-        self._items = torch.tensor(items, dtype=torch.int32, device=dev)
-        self._descs = torch.tensor(descs if descs else [[0] * 12], dtype=torch.int64, device=dev)
-        self._n_items = len(items)
-        self._table_key = key
-        return self._items, self._n_items, self._descs
+        if getattr(self, "_table_key", None) != key:
+            self._tables = {}
+            self._table_key = key
+            descs, per_param = [], [[] for _ in a.params]
+            for i, p in enumerate(a.params):
+                if not hasattr(p, "_ddp_amd_pack"):
+                    continue
+                pp, wc, wt, K, Cr, C, R, S, krsc = p._ddp_amd_pack()
+                if pp != a.data.data_ptr() + 4 * a.offsets[i] or (R * S > 1 and bool(krsc) != a.krsc[i]):
+                    raise RuntimeError("packed conv weight is not a view into the parameter arena")
+                d = len(descs)
+                descs.append([a.offsets[i], K, Cr, C, R, S, wc, wt, int(krsc), 0, 0, 0])
+                n = a.numels[i]
+                if not wt and C == Cr and (krsc or R * S == 1) and n % 4 == 0:
+                    # bf16 copy in the master's own index order: elementwise items
+                    for s0 in range(0, n, 8192):
+                        per_param[i].append([2, s0, min(8192, n - s0), d])
+                    continue
+                TK, TC = native().sgd_tile_dims(R * S)
+                for k0 in range(0, K, TK):
+                    for c0 in range(0, C, TC):
+                        per_param[i].append([1, d, k0, c0])
+            chunk = 8192
+            for i in range(len(a.params)):
+                if per_param[i]:
+                    continue
+                o, n = a.offsets[i], a.numels[i]
+                for s in range(0, n, chunk):
+                    per_param[i].append([0, o + s, min(chunk, n - s), 0])
+            self._per_param = per_param
+            dev = a.data.device
+            self._descs = torch.tensor(descs if descs else [[0] * 12], dtype=torch.int64, device=dev)
+        rng = tuple(prange) if prange is not None else (0, len(a.params))
+        t = self._tables.get(rng)
+        if t is None:
+            # conv re-pack items first (the heavier tiles start early), then elementwise items
+            sel = [it for i in range(*rng) for it in self._per_param[i] if it[0] != 0] + \
+                  [it for i in range(*rng) for it in self._per_param[i] if it[0] == 0]
+            if not sel:
+                raise ValueError(f"no parameters in range {rng}")
+            items = torch.tensor(sel, dtype=torch.int32, device=a.data.device)
+            t = (items, len(sel))
+            self._tables[rng] = t
+        return t[0], t[1], self._descs
 
     def zero_grad(self, set_to_none=False):
         if self._fused:
@@ -88,8 +99,10 @@ class FusedSGD(torch.optim.SGD):
             super().zero_grad(set_to_none=set_to_none)
 
     @torch.no_grad()
-    def step(self, closure=None, zero_grad=False, counter=None, skip=None):
-        """One fused launch. ``zero_grad=True`` also clears every gradient after its use (the
+    def step(self, closure=None, zero_grad=False, counter=None, skip=None, params=None,
+             stream=None):
+        """One fused launch. ``params = (i0, i1)``: only parameters i0 <= i < i1 (arena order);
+        ``stream``: launch on this torch stream instead of the current one. ``zero_grad=True`` also clears every gradient after its use (the
         next step then needs no zero_grad fill); ``counter=(int32 device ptr, delta)`` is
         advanced by the same launch (the on-device data cursor of engine/step.py); ``skip`` =
         device pointer of a uint32 error word: the update is skipped when it is non-zero."""
@@ -100,9 +113,9 @@ class FusedSGD(torch.optim.SGD):
             return out
         from ..ops.common import native, stream_handle
         g = self.param_groups[0]
-        s = stream_handle()
+        s = stream.cuda_stream if stream is not None else stream_handle()
         a = self.arena
-        items, n_items, descs = self._work_table()
+        items, n_items, descs = self._work_table(params)
         # one launch: SGD over every tensor + bf16 re-pack of every conv weight
         native().sgd_pack(items.data_ptr(), n_items, descs.data_ptr(), a.data.data_ptr(),
                           a.grad.data_ptr(), self.momentum_buffer.data_ptr(), float(g["lr"]),

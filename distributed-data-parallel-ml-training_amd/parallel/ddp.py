@@ -55,50 +55,160 @@ def plan_buckets(offsets, numels, elem_bytes, cap_bytes, cap_first_bytes):
     return out
 
 
-class _PyReducer:
-    """Bucketed reducer for torch.distributed backends (Gloo on CPU)."""
+class BucketScheduler:
+    """Python twin of ddp_amd::BucketScheduler (csrc/runtime/buckets.h): per-bucket readiness
+    counters and the launch order. ``mark(p)`` returns the buckets launchable now (in launch
+    order: a bucket never overtakes an earlier one, so every rank issues collectives in the same
+    order); ``finish()`` ends the backward pass, records the observed ready order and returns
+    the remaining buckets; ``order_from_ready`` gives torch DDP's post-iteration-0 rebuild in
+    this design's terms (bucket completion order; buckets stay contiguous arena slices)."""
 
-    def __init__(self, comm, arena, cap, cap_first, average, comm_dtype=torch.float32):
-        self.comm, self.arena, self.average = comm, arena, average
-        self.comm_dtype = comm_dtype
-        self.buckets = plan_buckets(arena.offsets, arena.numels, 4, cap, cap_first)
-        self.bucket_of = {}
+    def __init__(self, buckets, n_params):
+        self.buckets = [tuple(b) for b in buckets]
+        self.bucket_of = [-1] * n_params
         for b, (s, e, _, _) in enumerate(self.buckets):
+            if not 0 <= s < e <= n_params:
+                raise RuntimeError(f"bucket {b} has a bad parameter range")
             for p in range(s, e):
+                if self.bucket_of[p] != -1:
+                    raise RuntimeError("parameter in two buckets")
                 self.bucket_of[p] = b
+        if any(b < 0 for b in self.bucket_of):
+            raise RuntimeError("parameter in no bucket")
+        self.order = list(range(len(self.buckets)))
+        self._ready_order, self._launch_log = [], []
         self.prepare()
 
     def prepare(self):
         self.pending = [e - s for (s, e, _, _) in self.buckets]
         self.ready = [False] * len(self.buckets)
+        self.seen = [False] * len(self.bucket_of)
+        self.seq, self.log = [], []
         self.next_launch = 0
-        self.works = []
+        self.marked = 0
 
-    def mark_ready(self, p):
-        b = self.bucket_of[p]
-        if self.pending[b] <= 0:
+    def _launchable(self):
+        out = []
+        while self.next_launch < len(self.order) and self.ready[self.order[self.next_launch]]:
+            b = self.order[self.next_launch]
+            self.next_launch += 1
+            out.append(b)
+            self.log.append((b, self.marked))
+        return out
+
+    def mark(self, p):
+        if not 0 <= p < len(self.bucket_of):
+            raise RuntimeError("bad param index")
+        if self.seen[p]:
             raise RuntimeError("parameter marked ready twice in one backward")
+        self.seen[p] = True
+        self.seq.append(p)
+        self.marked += 1
+        b = self.bucket_of[p]
         self.pending[b] -= 1
         if self.pending[b] == 0:
             self.ready[b] = True
-            while self.next_launch < len(self.buckets) and self.ready[self.next_launch]:
-                _, _, off, cnt = self.buckets[self.next_launch]
-                view = self.arena.grad[off:off + cnt]
-                buf = view if self.comm_dtype == view.dtype else view.to(self.comm_dtype)
-                self.works.append((view, buf, self.comm.all_reduce_async(buf)))
-                self.next_launch += 1
+            return self._launchable()
+        return []
+
+    def finish(self):
+        for b, r in enumerate(self.ready):
+            if not r:
+                raise RuntimeError(f"bucket {b} has parameters whose gradient was never produced "
+                                   "(unused parameters are not supported)")
+        rest = self._launchable()
+        self._ready_order, self._launch_log = list(self.seq), list(self.log)
+        self.prepare()
+        return rest
+
+    def launched(self):
+        return self.next_launch
+
+    def launch_order(self):
+        return list(self.order)
+
+    def set_launch_order(self, order):
+        order = [int(b) for b in order]
+        if sorted(order) != list(range(len(self.buckets))):
+            raise RuntimeError("launch order is not a permutation of the buckets")
+        if self.next_launch:
+            raise RuntimeError("launch order changed during a backward")
+        self.order = order
+
+    def order_from_ready(self, seq):
+        left = [e - s for (s, e, _, _) in self.buckets]
+        done_at = [-1] * len(self.buckets)
+        for i, p in enumerate(seq):
+            b = self.bucket_of[p]
+            left[b] -= 1
+            if left[b] == 0:
+                done_at[b] = i
+        if any(d < 0 for d in done_at):
+            raise RuntimeError("ready sequence does not complete every bucket")
+        return sorted(range(len(self.buckets)), key=lambda b: done_at[b])
+
+    def ready_order(self):
+        return list(self._ready_order)
+
+    def launch_log(self):
+        return list(self._launch_log)
+
+
+class _PyReducer:
+    """Bucketed reducer for torch.distributed backends (Gloo on CPU): async all-reduce per bucket
+    launched from post-accumulate-grad hooks (overlapped with the rest of the backward)."""
+
+    def __init__(self, comm, arena, cap, cap_first, average, comm_dtype=torch.float32):
+        self.comm, self.arena, self.average = comm, arena, average
+        self.comm_dtype = comm_dtype
+        self.sched = BucketScheduler(plan_buckets(arena.offsets, arena.numels, 4, cap, cap_first),
+                                     len(arena.numels))
+        self.buckets = self.sched.buckets
+        self.works = []
+
+    def prepare(self):
+        self.sched.prepare()
+        self.works = []
+
+    def _launch(self, b):
+        _, _, off, cnt = self.buckets[b]
+        view = self.arena.grad[off:off + cnt]
+        buf = view if self.comm_dtype == view.dtype else view.to(self.comm_dtype)
+        self.works.append((view, buf, self.comm.all_reduce_async(buf)))
+
+    def mark_ready(self, p):
+        for b in self.sched.mark(p):
+            self._launch(b)
 
     def finalize(self):
-        if self.next_launch != len(self.buckets):
-            raise RuntimeError("DDP finalize: some parameters did not receive gradients "
-                               "(unused parameters are not supported)")
+        for b in self.sched.finish():
+            self._launch(b)
         for view, buf, w in self.works:
             w.wait()
             if buf is not view:
                 view.copy_(buf)
             if self.average:
                 view /= self.comm.world
-        self.prepare()
+        self.works = []
+
+    # scheduler queries (same API as the native Reducer)
+    def launched(self):
+        return self.sched.launched()
+
+    def launch_order(self):
+        return self.sched.launch_order()
+
+    def set_launch_order(self, order):
+        self.sched.set_launch_order(order)
+
+    def order_from_ready(self, seq):
+        return self.sched.order_from_ready(seq)
+
+    def ready_order(self):
+        return self.sched.ready_order()
+
+    def launch_log(self):
+        return self.sched.launch_log()
 
 
 class DistributedDataParallel(nn.Module):
@@ -118,6 +228,10 @@ class DistributedDataParallel(nn.Module):
         self._index = {id(p): i for i, p in enumerate(self.arena.params)}
         self._in_backward = False
         self._sync_enabled = True
+        # torch DDP rebuilds its buckets after iteration 0 from the observed gradient-ready
+        # order (static_graph=False default). DDP_AMD_REBUILD_BUCKETS=0 keeps the plan order.
+        self._iters = 0
+        self._rebuilt = os.environ.get("DDP_AMD_REBUILD_BUCKETS", "1") == "0"
         self._flat_buffers = None
         self._stream = None
         if self.cuda:
@@ -126,17 +240,19 @@ class DistributedDataParallel(nn.Module):
             self.reducer = native().Reducer(comm.comm, a.grad.data_ptr(), list(a.offsets),
                                             list(a.numels), cap, cap_first, bool(average))
             self.buckets = [tuple(b) for b in self.reducer.buckets()]
-            # overlap=False (default, DDP_AMD_COMM_OVERLAP=0): bucket collectives are issued inline
-            # on the backward stream as buckets fill; overlap=True: on a separate comm stream.
-            # Measured on MI355X / ROCm 7 (one GPU, stand-in collectives DDP_AMD_EMULATE_COMM=1,
-            # VGG-11 b256): inline 1.04 ms/step; comm stream 2.39 ms captured, 1.39 ms eager —
-            # every cross-queue edge of the step costs far more than the overlap can win back, so
-            # the step stays on ONE stream (profiles/r1_comm_stream_study.md).
-            if overlap is None:
-                overlap = os.environ.get("DDP_AMD_COMM_OVERLAP", "0") == "1"
+            # Where the bucket collectives run (``overlap``; env DDP_AMD_COMM_OVERLAP=0/1 forces
+            # it): None = auto — EAGER backward passes launch each full bucket on the comm stream
+            # (event-gated), overlapped with the rest of the backward like the reference's DDP
+            # (part3/main.py:174); a backward being CAPTURED into a hipGraph issues them inline
+            # on its own stream instead: a captured comm branch that stays open across the
+            # backward runs 2.4x slower on ROCm 7 (profiles/r1_comm_stream_study.md) — the
+            # captured multi-GPU step overlaps through engine/step.py SegmentedDDPStep instead.
+            if overlap is None and "DDP_AMD_COMM_OVERLAP" in os.environ:
+                overlap = os.environ["DDP_AMD_COMM_OVERLAP"] == "1"
+            self._overlap_mode = overlap  # None = auto
             if grad_comm_dtype not in ("fp32", "bf16"):
                 raise ValueError("grad_comm_dtype must be 'fp32' or 'bf16'")
-            self.reducer.set_overlap(bool(overlap))
+            self.reducer.set_overlap(True if overlap is None else bool(overlap))
             # world-1 stand-in collectives (one-GPU studies of the multi-GPU step):
             # DDP_AMD_EMULATE_COMM=N: N bucket-sized full-GPU passes per collective;
             # DDP_AMD_EMULATE_COMM_GBPS=G: a 32-CU kernel lasting bytes/G (RCCL-like footprint)
@@ -154,6 +270,7 @@ class DistributedDataParallel(nn.Module):
             self.reducer.set_debug_sync(os.environ.get("DDP_AMD_DEBUG_SYNC", "0") == "1")
             self._hook = register_grad_ready_hook(self._on_grad_ready)
         else:
+            self._overlap_mode = True  # async Gloo all-reduces launched from the hooks
             self.reducer = _PyReducer(comm, self.arena, cap, cap_first, average,
                                       torch.bfloat16 if grad_comm_dtype == "bf16" else torch.float32)
             self.buckets = self.reducer.buckets
@@ -215,12 +332,32 @@ class DistributedDataParallel(nn.Module):
                 for flat in self._flat_buffers:
                     self.comm.broadcast(flat, 0)
 
+    def _maybe_rebuild(self):
+        """After the first synchronised backward: launch buckets in the order they completed
+        (rank 0's observation, broadcast so every rank launches identically)."""
+        if self._rebuilt or self._iters < 1 or not torch.is_grad_enabled():
+            return
+        if self.cuda and torch.cuda.is_current_stream_capturing():
+            return
+        self._rebuilt = True
+        seq = list(self.reducer.ready_order())
+        if not seq:
+            return
+        order = list(self.reducer.order_from_ready(seq))
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            box = [order]
+            dist.broadcast_object_list(box, src=0)  # control plane (TCPStore / Gloo)
+            order = box[0]
+        self.reducer.set_launch_order(order)
+
     def forward(self, *args, **kwargs):
+        self._maybe_rebuild()
         self._sync_buffers()
         return self.module(*args, **kwargs)
 
     def forward_loss(self, *args, **kwargs):
         """Fused forward + loss of the wrapped model (if it provides ``forward_loss``)."""
+        self._maybe_rebuild()
         self._sync_buffers()
         return self.module.forward_loss(*args, **kwargs)
 
@@ -250,6 +387,8 @@ class DistributedDataParallel(nn.Module):
             # weight gradients may later be announced from the backward side stream — the
             # reducer then waits on both streams for the buckets they share
             self._stream = stream
+            if self._overlap_mode is None:  # auto: comm stream when eager, inline when captured
+                self.reducer.set_overlap(not torch.cuda.is_current_stream_capturing())
         self._queue_finalize()
         self.reducer.mark_ready(i, stream.cuda_stream)
 
@@ -266,6 +405,7 @@ class DistributedDataParallel(nn.Module):
 
     def _finalize(self):
         self._in_backward = False
+        self._iters += 1
         if self.cuda:
             stream, self._stream = self._stream, None
             self.reducer.finalize(stream.cuda_stream)
@@ -296,4 +436,4 @@ def check_replicas(arena, world):
     return all(torch.equal(x, allc[0]) for x in allc)
 
 
-__all__ = ["DistributedDataParallel", "plan_buckets", "check_replicas", "replica_checksum", "SUM", "AVG"]
+__all__ = ["DistributedDataParallel", "BucketScheduler", "plan_buckets", "check_replicas", "replica_checksum", "SUM", "AVG"]

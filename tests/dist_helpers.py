@@ -198,3 +198,60 @@ def commbench_worker(rank, world, port, q):
     except Exception as e:  # pragma: no cover - surfaced by the parent
         import traceback
         q.put((rank, {"error": traceback.format_exc() + repr(e)}))
+
+
+class _Swapped(torch.nn.Module):
+    """Parameters registered in the opposite order of their use: ``late`` is defined first but
+    applied last, so its gradient is ready FIRST in backward while the reverse-parameter-order
+    bucket plan puts it in the LAST bucket (what torch DDP's post-iteration-0 rebuild fixes)."""
+
+    def __init__(self):
+        super().__init__()
+        self.late = torch.nn.Linear(32, 4)
+        self.early = torch.nn.Linear(16, 32)
+
+    def forward(self, x):
+        return self.late(torch.relu(self.early(x)))
+
+
+def overlap_worker(rank, world, port, q, model_name):
+    """DDP on Gloo: per-iteration bucket launch logs (bucket, parameters marked at launch),
+    launch order before/after the iteration-0 rebuild, final parameters and gradients."""
+    try:
+        _init(rank, world, port)
+        import torch.distributed as dist
+        from ddp_amd.parallel import TorchCommunicator, DistributedDataParallel, check_replicas
+        from ddp_amd.optim import FusedSGD
+        torch.manual_seed(7)
+        if model_name == "swapped":
+            model = _Swapped()
+            cap, first = 0.0001, 0.0001  # one bucket per parameter tensor
+            xs = [torch.randn(8, 16) + rank for _ in range(3)]
+            ys = [torch.randint(0, 4, (8,)) for _ in range(3)]
+        else:
+            from ddp_amd.models import VGG11
+            model = VGG11()
+            cap, first = 4.0, 1.0
+            xs = [torch.randn(4, 3, 32, 32) + rank for _ in range(2)]
+            ys = [torch.randint(0, 10, (4,)) for _ in range(2)]
+        ddp = DistributedDataParallel(model, TorchCommunicator(), bucket_cap_mb=cap,
+                                      first_bucket_cap_mb=first)
+        opt = FusedSGD(ddp.parameters(), lr=0.05, momentum=0.9)
+        logs, orders = [], []
+        for x, y in zip(xs, ys):
+            opt.zero_grad()
+            torch.nn.functional.cross_entropy(ddp(x), y).backward()
+            orders.append(list(ddp.reducer.launch_order()))  # the order this backward used
+            logs.append(list(ddp.reducer.launch_log()))
+            opt.step()
+        ok = check_replicas(ddp.arena, world)
+        params = torch.cat([p.detach().reshape(-1).clone() for p in ddp.parameters()])
+        nb = len(ddp.buckets)
+        dist.destroy_process_group()
+        q.put((rank, {"logs": logs, "orders": orders, "consistent": ok,
+                      "params": params.numpy(), "n_buckets": nb,
+                      "n_params": len(list(ddp.parameters()))}))
+    except Exception:
+        import traceback
+        q.put((rank, {"error": traceback.format_exc()}))
+        raise

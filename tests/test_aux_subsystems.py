@@ -65,6 +65,7 @@ def test_metrics_sink_jsonl(tmp_path):
 
 TEST_CPP = r'''
 #include <cstdio>
+#include <stdexcept>
 #include <vector>
 #include "runtime/buckets.h"
 int main() {
@@ -85,6 +86,22 @@ int main() {
       std::printf("%d %d %zu %zu\n", x.first_param, x.last_param, x.offset, x.count);
     }
     if (prev_first != 0) { std::printf("not covered\n"); return 1; }
+    // readiness / launch state machine over the same plan: natural backward order, a
+    // shuffled order, the rebuilt order, and the misuse errors
+    BucketScheduler s(b, (int)numels.size());
+    for (int it = 0; it < 3; ++it) {
+      std::vector<int> seq;
+      for (int p = (int)numels.size() - 1; p >= 0; --p) seq.push_back(p);
+      if (it == 1) for (size_t i = 0; i + 1 < seq.size(); i += 2) std::swap(seq[i], seq[i + 1]);
+      size_t launched = 0;
+      for (int p : seq) launched += s.mark(p).size();
+      launched += s.finish().size();
+      if (launched != b.size()) { std::printf("launch count\n"); return 1; }
+      s.set_launch_order(s.order_from_ready(s.ready_order()));
+    }
+    bool threw = false;
+    try { s.mark(0); s.mark(0); } catch (const std::exception&) { threw = true; }
+    if (!threw) { std::printf("double mark accepted\n"); return 1; }
     std::printf("--\n");
   }
   return 0;

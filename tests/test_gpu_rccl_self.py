@@ -48,11 +48,13 @@ def _restore(m, opt, ld, snap):
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("segmented", [False, True])
+@pytest.mark.parametrize("segmented", [None, "4", "2,5", "4:bf16"])
 def test_captured_ddp_step_with_live_rccl(native_ext, segmented):
-    """Captured DDP step (inline bucket all-reduce, or the segmented two-graph step with bucket A
-    on a second communicator between the graphs) with live RCCL collectives applies the same
-    update as the same step without collectives, from the same state, eager and replayed."""
+    """Captured DDP step (inline bucket all-reduce, or the pipelined segmented step: each
+    bucket's all-reduce — fp32 or bf16 wire — and optimizer update on the comm stream, on the
+    step's own communicator, between the segment graphs) with live RCCL collectives applies the
+    same update as the same step without collectives, from the same state, eager and
+    replayed."""
     from ddp_amd.models import VGG11
     from ddp_amd.optim import FusedSGD
     from ddp_amd.data import SyntheticCIFAR10, DeviceLoader
@@ -68,7 +70,10 @@ def test_captured_ddp_step_with_live_rccl(native_ext, segmented):
         opt = FusedSGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
         ld = DeviceLoader(SyntheticCIFAR10(True, n=512), 64, "cuda")
         if segmented:
-            st = SegmentedDDPStep(m, opt, CrossEntropyLoss(), ld, split=4)
+            cuts, _, wire = segmented.partition(":")
+            st = SegmentedDDPStep(m, opt, CrossEntropyLoss(), ld,
+                                  split=[int(v) for v in cuts.split(",")],
+                                  grad_comm=wire or "fp32")
             st.WAIT_TIMEOUT_S = 20.0
         else:
             st = TrainStep(m, opt, CrossEntropyLoss(), ld)
@@ -153,3 +158,41 @@ def test_self_comm_gather_runs_point_to_point(native_ext):
     assert torch.equal(st[:last.numel()], ref[-1].reshape(-1))
     for p, r in zip(params, ref):
         assert torch.equal(p.grad, r)
+
+
+def test_eager_ddp_overlaps_backward_on_comm_stream(native_ext):
+    """part3's eager DDP step (reference: torch DDP, part3/main.py:174): with a live
+    communicator each full bucket's ncclAllReduce is launched on the comm stream from the fused
+    backward's gradient-ready hooks while earlier layers are still back-propagating (launch
+    log: parameters announced at launch < all), the compute stream waits for every bucket
+    before the optimizer, and the averaged gradients equal the no-collective ones. A captured
+    backward issues them inline instead (one single-stream graph)."""
+    from ddp_amd.models import VGG11
+    from ddp_amd.engine import CrossEntropyLoss
+    from ddp_amd.optim import FusedSGD
+    from ddp_amd.parallel import DistributedDataParallel, RcclCommunicator
+    torch.manual_seed(9)
+    base = VGG11().cuda()
+    x = torch.randn(32, 3, 32, 32, device="cuda")
+    y = torch.randint(0, 10, (32,), device="cuda")
+    grads = {}
+    for live in (False, True):
+        m = DistributedDataParallel(copy.deepcopy(base), RcclCommunicator(0, 1, 0, self_comm=live),
+                                    bucket_cap_mb=4.0, first_bucket_cap_mb=1.0)
+        opt = FusedSGD(m.parameters(), lr=0.1)
+        opt.zero_grad()
+        CrossEntropyLoss()(m(x), y).backward()
+        torch.cuda.synchronize()
+        grads[live] = m.arena.grad.clone()
+        if live:
+            assert m.reducer.overlap()  # eager: comm stream
+            log = m.reducer.launch_log()
+            n = len(list(m.parameters()))
+            assert len(log) == len(m.buckets) > 2
+            assert log[0][1] < n and log[-2][1] < n, log
+            assert m.comm.comm.async_error() == 0
+        m.close()
+    a, b = grads[False], grads[True]
+    c = float(torch.dot(a, b) / (a.norm() * b.norm()))
+    assert c > 0.98, c
+    assert abs(float(b.norm()) / float(a.norm()) - 1) < 0.05
