@@ -47,14 +47,13 @@ def parse():
                    help="iterations of the reference timing window (0 = skip)")
     p.add_argument("--strategy", default="ddp",
                    choices=["ddp", "allreduce", "gather_scatter", "gather_broadcast"])
-    # Bucket sizing for xGMI. The collectives run inline on the step's single
-    # stream (parallel/ddp.py: a separate comm stream measured 2.3x slower on ROCm 7), so there
-    # is no backward overlap to buy with small buckets; what remains is per-collective latency
-    # and ring efficiency, both best with ONE bucket: VGG-11's 36.9 MB fp32 gradient arena in a
-    # single ncclAllReduce gives each of the 7 links multi-MiB chunks. The reference DDP default
-    # is 25 MB (+1 MB first bucket); pass --bucket-mb 25 --first-bucket-mb 1 for that plan.
-    p.add_argument("--bucket-mb", type=float, default=256.0)
-    p.add_argument("--first-bucket-mb", type=float, default=256.0)
+    # Bucket sizing for xGMI: --bucket-mb auto. The reference DDP default is
+    # 25 MB (+1 MB first bucket); pass --bucket-mb 25 --first-bucket-mb 1 for that plan.
+    p.add_argument("--bucket-mb", default="auto",
+                   help="DDP bucket cap in MiB, or 'auto' (parallel/bucket_plan.py): one bucket "
+                        "when the collectives are inline in the captured step, else sized from "
+                        "the all-reduce bandwidth table (parallel/comm_tuning.json)")
+    p.add_argument("--first-bucket-mb", default="auto")
     p.add_argument("--grad-comm", default="fp32", choices=["fp32", "bf16"],
                    help="DDP gradient all-reduce dtype (bf16 halves the xGMI bytes; default "
                         "fp32 = the reference's gradient precision)")
@@ -77,6 +76,7 @@ def main():
     import ddp_amd
     from ddp_amd.data import SyntheticCIFAR10, SyntheticImageNet, DeviceLoader
     from ddp_amd.engine import TrainStep, SegmentedDDPStep, CrossEntropyLoss
+    from ddp_amd.engine.step import default_cuts
     from ddp_amd.models import build
     from ddp_amd.optim import FusedSGD
     from ddp_amd.parallel import (DistributedDataParallel, RcclCommunicator, STRATEGIES,
@@ -125,6 +125,19 @@ def main():
     model = build(args.model).to(device)
     criterion = CrossEntropyLoss()
     sync = None
+    # Multi-GPU default: the pipelined step — each bucket's all-reduce + optimizer update runs
+    # on the comm stream while the earlier layers' backward runs (one-GPU study with an
+    # 8-GPU-sized stand-in collective: profiles/r2_pipelined_ddp.md); one GPU has no collective
+    # to hide -> one graph.
+    if args.segmented is None:
+        args.segmented = os.environ.get("DDP_AMD_SEGMENTED",
+                                        default_cuts(args.model, B) if world > 1 else "0")
+    cuts = [int(v) for v in str(args.segmented).split(",") if int(v) > 0]
+    segmented = bool(cuts) and args.strategy == "ddp" and not args.no_graph
+    if args.bucket_mb == "auto" and not args.no_graph:
+        # captured step: the DDP reducer's collectives are inline in the graph (or bypassed by
+        # the pipelined step): one bucket = one collective, the least latency
+        args.bucket_mb = args.first_bucket_mb = 1 << 16
     if args.strategy == "ddp":
         model = DistributedDataParallel(model, comm, bucket_cap_mb=args.bucket_mb,
                                         first_bucket_cap_mb=args.first_bucket_mb,
@@ -133,15 +146,6 @@ def main():
         fn = STRATEGIES[args.strategy]
         sync = lambda m: fn(m, comm)  # noqa: E731
     opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
-    # Multi-GPU default: the late layers' bucket (89% of the gradient bytes) is all-reduced on a
-    # second stream while the early layers' backward runs (one-GPU study with a 32-CU stand-in
-    # collective at 100-300 GB/s: 1.11-1.36 ms inline vs 0.96-1.01 ms segmented,
-    # profiles/r1_segmented_overlap.md); one GPU has no collective to hide -> one graph.
-    if args.segmented is None:
-        args.segmented = os.environ.get("DDP_AMD_SEGMENTED",
-                                        ("8,14" if resnet else "4") if world > 1 else "0")
-    cuts = [int(v) for v in str(args.segmented).split(",") if int(v) > 0]
-    segmented = bool(cuts) and args.strategy == "ddp" and not args.no_graph
     if segmented:
         step = SegmentedDDPStep(model, opt, criterion, loader, split=cuts,
                                 emulate=int(os.environ.get("DDP_AMD_EMULATE_COMM", "0")),
@@ -236,7 +240,8 @@ def main():
                    "strategy": {"ddp": "part3 bucketed DDP", "allreduce": "part2b all_reduce",
                                 "gather_scatter": "part2a gather/scatter",
                                 "gather_broadcast": "part2a gather/broadcast"}[args.strategy],
-                   "hipgraph": graph_ok, "bucket_mb": args.bucket_mb,
+                   "hipgraph": graph_ok,
+                   "buckets": (len(step.buckets) if segmented else len(getattr(model, "buckets", []))),
                    "grad_comm": args.grad_comm,
                    "comm": (f"segmented@{args.segmented}" if segmented else "overlap-stream" if getattr(getattr(model, "reducer", None), "overlap",
                                                          lambda: False)() else "inline"),

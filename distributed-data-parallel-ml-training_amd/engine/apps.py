@@ -77,11 +77,11 @@ def main(part, argv=None):
         # the first batches of the shard, like any other iteration would)
         # the warm-up steps train on the first batches: snapshot the training state and roll
         # it back after the capture, so the epoch starts exactly where the eager loop would
-        from .step import TrainStep, SegmentedDDPStep
+        from .step import TrainStep, SegmentedDDPStep, default_cuts
         arena = model.arena if hasattr(model, "arena") else optimizer.arena
         snap = (arena.data.clone(), optimizer.momentum_buffer.clone())
-        default_cuts = "8,14" if args.model.startswith("resnet") else "4"
-        split = [int(v) for v in os.environ.get("DDP_AMD_SEGMENTED", default_cuts).split(",")
+        split = [int(v) for v in os.environ.get("DDP_AMD_SEGMENTED",
+                                                default_cuts(args.model, batch_size)).split(",")
                  if int(v) > 0]
         if (strategy == "ddp" and world > 1 and split
                 and hasattr(model.module, "forward_loss_split")):

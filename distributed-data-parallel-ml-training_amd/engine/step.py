@@ -26,6 +26,16 @@ def capture_mode():
     return "thread_local" if _comm.SELF_COMM_ACTIVE else "global"
 
 
+def default_cuts(model_name, per_gpu_batch):
+    """Backward cut points of the pipelined multi-GPU step (SegmentedDDPStep), from the one-GPU
+    cut sweep with an 8-GPU-sized stand-in collective (profiles/r2_pipelined_ddp.md): VGG
+    before stages 3 and 6 up to 128 images per GPU, 2 and 5 above; ResNet-50 before layer3 and
+    layer4 (stages 8, 14)."""
+    if model_name.startswith("resnet"):
+        return "8,14"
+    return "3,6" if per_gpu_batch <= 128 else "2,5"
+
+
 class TrainStep:
     def __init__(self, model, optimizer, criterion, loader, sync=None, use_graph=True):
         self.model, self.optimizer, self.criterion, self.loader = model, optimizer, criterion, loader

@@ -223,8 +223,19 @@ class DistributedDataParallel(nn.Module):
         self.cuda = self.arena.data.is_cuda
         self._verify_param_shapes(params)
         self._sync_module_states()
-        cap = int(bucket_cap_mb * (1 << 20))
-        cap_first = int(first_bucket_cap_mb * (1 << 20))
+        self.bucket_plan_reason = "explicit"
+        if bucket_cap_mb == "auto" or first_bucket_cap_mb == "auto":
+            # sized from the all-reduce bandwidth table for this world size (bucket_plan.py)
+            from .bucket_plan import choose_bucket_caps
+            wire = 2 if grad_comm_dtype == "bf16" else 4
+            cap_b, first_b, self.bucket_plan_reason = choose_bucket_caps(
+                comm.world, self.arena.total * wire, overlap=True,
+                dtype="bf16" if grad_comm_dtype == "bf16" else "fp32")
+            # the planner counts fp32 arena bytes
+            cap, cap_first = cap_b * 4 // wire, first_b * 4 // wire
+        else:
+            cap = int(float(bucket_cap_mb) * (1 << 20))
+            cap_first = int(float(first_bucket_cap_mb) * (1 << 20))
         self._index = {id(p): i for i, p in enumerate(self.arena.params)}
         self._in_backward = False
         self._sync_enabled = True

@@ -44,8 +44,11 @@ def build_parser(description=None, distributed=True):
     g.add_argument('--train-size', type=int, default=None, help='synthetic train-set size')
     g.add_argument('--test-size', type=int, default=None, help='synthetic test-set size')
     g.add_argument('--max-batches', type=int, default=None, help='stop the epoch early')
-    g.add_argument('--bucket-mb', type=float, default=25.0, help='DDP bucket cap (MiB)')
-    g.add_argument('--first-bucket-mb', type=float, default=1.0)
+    g.add_argument('--bucket-mb', type=_mb, default=25.0,
+                   help="DDP bucket cap (MiB; default 25 = the reference's torch DDP default); "
+                        "'auto' = sized from the all-reduce bandwidth table "
+                        "(parallel/comm_tuning.json)")
+    g.add_argument('--first-bucket-mb', type=_mb, default=1.0)
     g.add_argument('--threads', type=int, default=4, help='torch CPU threads (reference: 4)')
     g.add_argument('--save', default=None, help='write a reference-layout checkpoint here')
     g.add_argument('--resume', default=None, help='load a checkpoint before training')
@@ -72,6 +75,10 @@ def parse_arguments(argv=None):
     """Reference-shaped: returns (master_ip, master_port, rank, size)."""
     args = finalize_args(build_parser().parse_args(argv))
     return args.master_ip, args.master_port, args.rank, args.size
+
+
+def _mb(v):
+    return v if v == "auto" else float(v)
 
 
 def parse_all(argv=None, distributed=True, description=None):

@@ -18,6 +18,9 @@ def main():
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--max-mb", type=float, default=128.0)
+    ap.add_argument("--write-table", nargs="?", const="", default=None,
+                    help="merge the measured rows into the bucket-sizing table "
+                         "(default parallel/comm_tuning.json) for this world size and dtype")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -37,6 +40,9 @@ def main():
     if rank == 0:
         for r in rows:
             print(json.dumps(dict(r, world=world, dtype=a.dtype)), flush=True)
+        if a.write_table is not None:
+            from ddp_amd.parallel.bucket_plan import TABLE_FILE, merge_rows
+            merge_rows(a.write_table or TABLE_FILE, world, a.dtype, rows)
     if world > 1:
         dist.destroy_process_group()
 
