@@ -63,6 +63,9 @@ def parse():
                         "while the earlier layers' backward runs (engine/step.py "
                         "SegmentedDDPStep); 0 = one graph, inline collectives. Default on >1 "
                         "GPUs: VGG 4, ResNet-50 8,14; on 1 GPU 0. Env DDP_AMD_SEGMENTED overrides")
+    p.add_argument("--zero", action="store_true",
+                   help="pipelined DDP step with the ZeRO-1 sharded update (reduce-scatter -> "
+                        "SGD on 1/N of the parameters -> all-gather, parallel/zero.py)")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--train-size", type=int, default=None)
     p.add_argument("--json-out", default=None)
@@ -150,7 +153,9 @@ def main():
         step = SegmentedDDPStep(model, opt, criterion, loader, split=cuts,
                                 emulate=int(os.environ.get("DDP_AMD_EMULATE_COMM", "0")),
                                 emulate_gbps=float(os.environ.get("DDP_AMD_EMULATE_COMM_GBPS", "0")),
-                                grad_comm=args.grad_comm)
+                                grad_comm=args.grad_comm, zero=args.zero)
+    elif args.zero:
+        raise SystemExit("--zero needs the pipelined DDP step (--segmented with cuts, hipGraph)")
     else:
         step = TrainStep(model, opt, criterion, loader, sync=sync, use_graph=not args.no_graph)
 
@@ -245,7 +250,8 @@ def main():
                    "grad_comm": args.grad_comm,
                    "comm": (f"segmented@{args.segmented}" if segmented else "overlap-stream" if getattr(getattr(model, "reducer", None), "overlap",
                                                          lambda: False)() else "inline"),
-                   "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4) fused"},
+                   "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4) fused" +
+                                (", ZeRO-1 sharded" if args.zero else "")},
         "avg_ms_iter_1_39": round(ref_ms, 4) if ref_ms is not None else None,
         "img_s_iter_1_39": round(global_batch / ref_ms * 1000.0, 2) if ref_ms else None,
         "train_loss_mean": round(loss, 4),

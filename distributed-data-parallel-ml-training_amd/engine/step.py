@@ -214,7 +214,7 @@ class SegmentedDDPStep(TrainStep):
     WAIT_TIMEOUT_S = 100.0  # a device-side wait that exceeds this records an error and returns
 
     def __init__(self, ddp, optimizer, criterion, loader, split=4, emulate=0, emulate_gbps=0.0,
-                 emulate_scale=1.0, grad_comm="fp32"):
+                 emulate_scale=1.0, grad_comm="fp32", zero=False):
         super().__init__(ddp, optimizer, criterion, loader, sync=None, use_graph=True)
         inner = getattr(ddp, "module", None)
         if inner is None or not hasattr(inner, "forward_loss_split") or not self.fold_opt:
@@ -251,6 +251,15 @@ class SegmentedDDPStep(TrainStep):
             warm = torch.zeros(64, dtype=torch.float32, device=loader.device)
             self.comm_a.all_reduce(warm)
             torch.cuda.synchronize()
+        # ZeRO-1 (parallel/zero.py): reduce-scatter -> SGD on this rank's shard -> all-gather of
+        # the updated parameters, per bucket, instead of all-reduce -> replicated SGD
+        self.zero = None
+        if zero:
+            if grad_comm != "fp32":
+                raise ValueError("the sharded (ZeRO-1) update communicates fp32 gradients")
+            from ..parallel.zero import ShardedUpdate
+            self.zero = ShardedUpdate(arena, optimizer, self.comm_a or ddp.comm,
+                                      [((i0, i1), (lo, hi)) for (i0, i1), (lo, hi) in self.buckets])
         self._stage = None
         if grad_comm == "bf16":
             self._stage = torch.empty(arena.total, dtype=torch.bfloat16, device=loader.device)
@@ -323,6 +332,13 @@ class SegmentedDDPStep(TrainStep):
                            cs.cuda_stream)
         (i0, i1), (lo, hi) = self.buckets[j]
         last = j == len(self.buckets) - 1
+        if self.zero is not None:
+            with trace_range(f"zero_update_bucket{j}"):
+                self.zero.step(j, stream=cs, skip=self._fp(4),
+                               counter=self.loader.cursor_advance() if last else None)
+            if last:
+                native().flag_signal(self._fp(1), cs.cuda_stream)
+            return
         with trace_range(f"sync_bucket{j}"):
             self._allreduce(lo, hi, cs, self.comm_a)
         with trace_range(f"optimizer_bucket{j}"):

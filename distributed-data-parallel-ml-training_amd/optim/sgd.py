@@ -27,6 +27,10 @@ class FusedSGD(torch.optim.SGD):
                 raise ValueError("fused SGD supports a single param group")
             self.arena = arena_for(params)
             self.momentum_buffer = torch.zeros_like(self.arena.data)
+        else:
+            # CPU: plain torch.optim.SGD; the flat arena (if the DDP wrapper built one) serves the
+            # element-range update of the ZeRO-1 path (step_elements)
+            self.arena = getattr(params[0], "_ddp_amd_arena", None) if params else None
 
     def _packs(self):
         return [p._ddp_amd_pack() for p in self.arena.params if hasattr(p, "_ddp_amd_pack")]
@@ -91,6 +95,68 @@ class FusedSGD(torch.optim.SGD):
             t = (items, len(sel))
             self._tables[rng] = t
         return t[0], t[1], self._descs
+
+    def _elem_table(self, lo, hi):
+        """Plain fp32 SGD items over arena elements [lo, hi) (no bf16 re-pack): the ZeRO-1
+        shard update (parallel/zero.py)."""
+        key = ("elems", lo, hi)
+        t = getattr(self, "_elem_tables", {}).get(key)
+        if t is None:
+            chunk = 8192
+            items = [[0, s0, min(chunk, hi - s0), 0] for s0 in range(lo, hi, chunk)]
+            if not items:
+                raise ValueError("empty element range")
+            t = (torch.tensor(items, dtype=torch.int32, device=self.arena.data.device), len(items))
+            self._elem_tables = getattr(self, "_elem_tables", {})
+            self._elem_tables[key] = t
+        return t
+
+    @torch.no_grad()
+    def step_elements(self, lo, hi, stream=None, zero_grad=False, counter=None, skip=None):
+        """SGD (fp32 master + momentum only) on arena elements [lo, hi): one launch on the GPU,
+        torch.optim.SGD's exact per-element math on the flat slices on the CPU."""
+        g = self.param_groups[0]
+        lr, m, wd = float(g["lr"]), float(g["momentum"]), float(g["weight_decay"])
+        a = self.arena
+        if not self._fused:
+            p, gr = a.data[lo:hi], a.grad[lo:hi]
+            d = gr.add(p, alpha=wd) if wd != 0 else gr
+            if m != 0:
+                if not hasattr(self, "_flat_buf"):
+                    self._flat_buf = torch.zeros_like(a.data)
+                    self._flat_init = torch.zeros(a.total, dtype=torch.bool)
+                buf = self._flat_buf[lo:hi]
+                if bool(self._flat_init[lo:hi].all()):
+                    buf.mul_(m).add_(d)
+                else:
+                    buf.copy_(d)
+                    self._flat_init[lo:hi] = True
+                d = buf
+            p.add_(d, alpha=-lr)
+            if zero_grad:
+                gr.zero_()
+            return
+        from ..ops.common import native, stream_handle
+        s = stream.cuda_stream if stream is not None else stream_handle()
+        items, n_items = self._elem_table(lo, hi)
+        native().sgd_pack(items.data_ptr(), n_items, self._descs_ptr(), a.data.data_ptr(),
+                          a.grad.data_ptr(), self.momentum_buffer.data_ptr(), lr, m, wd,
+                          float(self._grad_scale_factor), int(bool(g["nesterov"])), s,
+                          zero_grad=int(bool(zero_grad)),
+                          counter=int(counter[0]) if counter else 0,
+                          delta=int(counter[1]) if counter else 0,
+                          skip=int(skip) if skip else 0)
+
+    def _descs_ptr(self):
+        return self._work_table()[2].data_ptr()
+
+    def repack_params(self, i0, i1, stream=None):
+        """Rebuild the bf16 operand copies of the conv weights among parameters [i0, i1)."""
+        descs = [p._ddp_amd_pack() for p in self.arena.params[i0:i1] if hasattr(p, "_ddp_amd_pack")]
+        if descs and self.arena.data.is_cuda:
+            from ..ops.common import native, stream_handle
+            native().pack_conv_weights(descs, stream.cuda_stream if stream is not None
+                                       else stream_handle())
 
     def zero_grad(self, set_to_none=False):
         if self._fused:

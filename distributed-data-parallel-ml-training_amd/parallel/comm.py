@@ -96,6 +96,22 @@ class TorchCommunicator:
         dist.all_gather(out, t, group=self.group)
         return out
 
+    def reduce_scatter_inplace(self, buf, op=AVG, stream=None):
+        """Flat ``buf`` (numel divisible by world): this rank's shard
+        ``buf[rank*n/w:(rank+1)*n/w]`` receives the reduction over ranks (ZeRO-1)."""
+        n = buf.numel() // self.world
+        out = torch.empty(n, dtype=buf.dtype)
+        dist.reduce_scatter_tensor(out, buf.contiguous(), op=dist.ReduceOp.SUM, group=self.group)
+        if op == AVG:
+            out /= self.world
+        buf[self.rank * n:(self.rank + 1) * n].copy_(out)
+
+    def all_gather_inplace(self, buf, stream=None):
+        """Flat ``buf``: every rank's shard is gathered into every rank's ``buf``."""
+        n = buf.numel() // self.world
+        mine = buf[self.rank * n:(self.rank + 1) * n].clone()
+        dist.all_gather_into_tensor(buf, mine, group=self.group)
+
     def gather(self, t, dst=0):
         """Reference 2A gather (part2/part2a/main.py:104-107,114): returns the list on dst."""
         if self.rank == dst:
@@ -165,6 +181,23 @@ class RcclCommunicator:
         out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
         self.comm.all_gather(t.data_ptr(), out.data_ptr(), t.numel(), _DT[t.dtype], self._s())
         return list(out.unbind(0))
+
+    def reduce_scatter_inplace(self, buf, op=AVG, stream=None):
+        """In-place ncclReduceScatter of flat ``buf``: the shard at rank*n/w receives the result
+        (NCCL's in-place convention recvbuff = sendbuff + rank * recvcount)."""
+        n = buf.numel() // self.world
+        es = buf.element_size()
+        s = stream.cuda_stream if stream is not None else self._s()
+        self.comm.reduce_scatter(buf.data_ptr(), buf.data_ptr() + self.rank * n * es, n,
+                                 _DT[buf.dtype], op, s)
+
+    def all_gather_inplace(self, buf, stream=None):
+        """In-place ncclAllGather of flat ``buf`` (sendbuff = recvbuff + rank * sendcount)."""
+        n = buf.numel() // self.world
+        es = buf.element_size()
+        s = stream.cuda_stream if stream is not None else self._s()
+        self.comm.all_gather(buf.data_ptr() + self.rank * n * es, buf.data_ptr(), n,
+                             _DT[buf.dtype], s)
 
     def gather_into(self, t, buf, dst=0):
         """Grouped send/recv gather of t into buf[world, numel] on dst."""

@@ -255,3 +255,58 @@ def overlap_worker(rank, world, port, q, model_name):
         import traceback
         q.put((rank, {"error": traceback.format_exc()}))
         raise
+
+
+def zero_worker(rank, world, port, q, steps):
+    """Replicated DDP update (all-reduce + SGD on every parameter) vs the ZeRO-1 sharded update
+    (reduce-scatter -> SGD on this rank's shard -> all-gather), same init and data."""
+    try:
+        _init(rank, world, port)
+        import torch.distributed as dist
+        from ddp_amd.models import VGG11
+        from ddp_amd.optim import FusedSGD
+        from ddp_amd.parallel import TorchCommunicator, DistributedDataParallel, check_replicas
+        from ddp_amd.parallel.zero import ShardedUpdate, arena_buckets
+        from ddp_amd.engine import CrossEntropyLoss
+        from ddp_amd.data import SyntheticCIFAR10, CPULoader
+        comm = TorchCommunicator()
+        crit = CrossEntropyLoss()
+        loader = CPULoader(SyntheticCIFAR10(True, n=4 * world * steps), 4, num_replicas=world,
+                           rank=rank)
+        batches = [b for _, b in zip(range(steps), loader)]
+        out = {}
+        for mode in ("replicated", "zero"):
+            torch.manual_seed(89395)
+            ddp = DistributedDataParallel(VGG11(), comm, bucket_cap_mb=4.0)
+            opt = FusedSGD(ddp.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4)
+            upd = None
+            if mode == "zero":
+                a = ddp.arena
+                pidx = {id(p): i for i, p in enumerate(a.params)}
+                firsts = [pidx[id(ddp.module.layers[i].weight)] for i in (11, 22)]  # stages 3, 6
+                upd = ShardedUpdate(a, opt, comm, arena_buckets(a, firsts))
+                assert len(upd.buckets) == 3
+                shards = [upd.shard(j) for j in range(3)]
+            for x, y in batches:
+                opt.zero_grad()
+                if upd is None:
+                    crit(ddp(x), y).backward()
+                    opt.step()
+                else:
+                    with ddp.no_sync():
+                        crit(ddp(x), y).backward()
+                    for j in range(len(upd.buckets)):
+                        upd.step(j)
+            out[mode] = torch.cat([p.detach().reshape(-1).clone() for p in ddp.parameters()])
+            out[mode + "_consistent"] = check_replicas(ddp.arena, world)
+            if upd is not None:
+                out["grad_zero"] = bool((ddp.arena.grad == 0).all())
+                out["shards"] = shards
+        dist.destroy_process_group()
+        q.put((rank, {"replicated": out["replicated"].numpy(), "zero": out["zero"].numpy(),
+                      "rc": out["replicated_consistent"], "zc": out["zero_consistent"],
+                      "grad_zero": out["grad_zero"], "shards": out["shards"]}))
+    except Exception:
+        import traceback
+        q.put((rank, {"error": traceback.format_exc()}))
+        raise

@@ -437,3 +437,64 @@ def test_segmented_ddp_step_matches_single_graph(native_ext, split):
     for st in (ss, slow):
         st.check_error()
     m.close()
+
+
+def test_vgg11_20_step_trajectory_matches_cpu_fp32_oracle(native_ext):
+    """End-to-end numerics over time: 20 SGD steps (lr 0.01, momentum 0.9, wd 1e-4, batch 64)
+    of the fused bf16 GPU path vs the reference model + torch.optim.SGD in fp32 on the CPU
+    (reference loop: /root/reference/part1/main.py:65-77), on the same batches. Per-step losses
+    agree to a few percent, and the total parameter update points the same way."""
+    from ddp_amd.models import VGG11
+    from ddp_amd.engine import CrossEntropyLoss
+    from ddp_amd.optim import FusedSGD
+    torch.manual_seed(2024)
+    cpu = VGG11()
+    gpu = copy.deepcopy(cpu).cuda()
+    p0 = torch.cat([p.detach().reshape(-1).clone() for p in cpu.parameters()])
+    oc = torch.optim.SGD(cpu.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    og = FusedSGD(gpu.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    crit = CrossEntropyLoss()
+    g = torch.Generator().manual_seed(5)
+    # weakly class-dependent means: the loss falls steadily (no early collapse to ~0, where
+    # single-batch spikes make any two runs diverge)
+    means = 0.25 * torch.randn(10, 3, 1, 1, generator=g)
+    losses_c, losses_g = [], []
+    for step in range(20):
+        y = torch.randint(0, 10, (64,), generator=g)
+        x = torch.randn(64, 3, 32, 32, generator=g) + means[y]
+        x = x.to(torch.bfloat16).float()  # the GPU consumes bf16 inputs: same values on both sides
+        oc.zero_grad()
+        lc = crit(cpu(x), y)
+        lc.backward()
+        oc.step()
+        og.zero_grad()
+        lg = crit(gpu(x.cuda()), y.cuda())
+        lg.backward()
+        og.step()
+        losses_c.append(float(lc))
+        losses_g.append(float(lg))
+    torch.cuda.synchronize()
+    print("cpu fp32:", [round(v, 3) for v in losses_c])
+    print("gpu bf16:", [round(v, 3) for v in losses_g])
+    # step by step while the trajectories are close; afterwards single-batch losses (< 0.7,
+    # memorising) amplify tiny weight differences, so compare 5-step window means there
+    rel = [abs(a - b) / abs(b) for a, b in zip(losses_g, losses_c)]
+    # (two GPU runs differ from each other by float-atomic ordering of the BN statistics, which
+    # grows to several % per step by step ~8; measured run to run on the box)
+    # (observed over 4 box runs: steps 0-4 within 4%, 5-step windows within 8%)
+    assert max(rel[:3]) < 0.03 and max(rel[:5]) < 0.06, rel
+    for w in range(0, 20, 5):
+        mg, mc = sum(losses_g[w:w + 5]) / 5, sum(losses_c[w:w + 5]) / 5
+        assert abs(mg - mc) < 0.15 * mc + 0.02, (w, mg, mc)
+    assert max(abs(a - b) for a, b in zip(losses_g, losses_c)) < 0.3
+    assert losses_c[-1] < losses_c[0] and losses_g[-1] < losses_g[0]
+    pc = torch.cat([p.detach().reshape(-1) for p in cpu.parameters()]).double()
+    pg = torch.cat([p.detach().float().cpu().reshape(-1) for p in gpu.parameters()]).double()
+    p0 = p0.double()
+    dc, dg = pc - p0, pg - p0
+    cos_d = float(torch.dot(dc, dg) / (dc.norm() * dg.norm()))
+    cos_p = float(torch.dot(pc, pg) / (pc.norm() * pg.norm()))
+    print("update cosine", cos_d, "param cosine", cos_p)
+    # the total update after 20 steps is dominated by the memorising late steps, where single
+    # batches steer the weights (0.86 measured on the box); the parameters agree (0.9993)
+    assert cos_p > 0.995 and cos_d > 0.7

@@ -48,13 +48,13 @@ def _restore(m, opt, ld, snap):
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("segmented", [None, "4", "2,5", "4:bf16"])
+@pytest.mark.parametrize("segmented", [None, "4", "2,5", "4:bf16", "3,6:zero"])
 def test_captured_ddp_step_with_live_rccl(native_ext, segmented):
     """Captured DDP step (inline bucket all-reduce, or the pipelined segmented step: each
     bucket's all-reduce — fp32 or bf16 wire — and optimizer update on the comm stream, on the
-    step's own communicator, between the segment graphs) with live RCCL collectives applies the
-    same update as the same step without collectives, from the same state, eager and
-    replayed."""
+    step's own communicator, between the segment graphs; or the ZeRO-1 sharded update:
+    reduce-scatter, shard SGD, all-gather, re-pack) with live RCCL collectives applies the same
+    update as the same step without collectives, from the same state, eager and replayed."""
     from ddp_amd.models import VGG11
     from ddp_amd.optim import FusedSGD
     from ddp_amd.data import SyntheticCIFAR10, DeviceLoader
@@ -70,10 +70,11 @@ def test_captured_ddp_step_with_live_rccl(native_ext, segmented):
         opt = FusedSGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
         ld = DeviceLoader(SyntheticCIFAR10(True, n=512), 64, "cuda")
         if segmented:
-            cuts, _, wire = segmented.partition(":")
+            cuts, _, opt_ = segmented.partition(":")
             st = SegmentedDDPStep(m, opt, CrossEntropyLoss(), ld,
                                   split=[int(v) for v in cuts.split(",")],
-                                  grad_comm=wire or "fp32")
+                                  grad_comm="bf16" if opt_ == "bf16" else "fp32",
+                                  zero=opt_ == "zero")
             st.WAIT_TIMEOUT_S = 20.0
         else:
             st = TrainStep(m, opt, CrossEntropyLoss(), ld)
