@@ -397,5 +397,9 @@ PYBIND11_MODULE(_native, m) {
       .def("order_from_ready", [](Reducer& r, std::vector<int> seq) { return r.scheduler().order_from_ready(seq); })
       .def("ready_order", [](Reducer& r) { return r.scheduler().ready_order(); })
       .def("launch_log", [](Reducer& r) { return r.scheduler().launch_log(); })
+      .def("set_timing", &Reducer::set_timing)
+      .def("bucket_times", [](Reducer& r, uintptr_t ref) {
+        return r.bucket_times(reinterpret_cast<hipEvent_t>(ref));
+      })
       .def("comm_stream", [](Reducer& r) { return reinterpret_cast<uintptr_t>(r.comm_stream()); });
 }

@@ -213,11 +213,13 @@ Reducer::Reducer(RcclComm* comm, float* arena, std::vector<size_t> offsets,
   done_stream_.assign(nb, nullptr);
   for (size_t b = 0; b < nb; ++b)
     HIP_OK(hipEventCreateWithFlags(&done_ev_[b], hipEventDisableTiming));
-  // DDP_AMD_COMM_PRIORITY=high: comm stream at the highest stream priority (default: normal)
+  // comm stream at the highest stream priority (DDP_AMD_COMM_PRIORITY=normal reverts): HIP
+  // keeps high-priority streams on their own hardware queues, so the collectives cannot end up
+  // behind the backward on a queue shared round-robin with the compute stream
   int lo = 0, hi = 0;
   HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
   const char* pe = std::getenv("DDP_AMD_COMM_PRIORITY");
-  const bool high = pe && std::string(pe) == "high";
+  const bool high = !(pe && std::string(pe) == "normal");
   HIP_OK(hipStreamCreateWithPriority(&comm_stream_, hipStreamNonBlocking, high ? hi : lo));
   prepare();
 }
@@ -232,7 +234,32 @@ void Reducer::set_comm_dtype(int dtype) {
   }
 }
 
+void Reducer::set_timing(bool on) {
+  timing_ = on;
+  if (on && t_start_.empty()) {
+    t_start_.resize(done_ev_.size());
+    t_end_.resize(done_ev_.size());
+    for (size_t b = 0; b < done_ev_.size(); ++b) {
+      HIP_OK(hipEventCreate(&t_start_[b]));
+      HIP_OK(hipEventCreate(&t_end_[b]));
+    }
+  }
+}
+
+std::vector<std::pair<float, float>> Reducer::bucket_times(hipEvent_t ref) const {
+  std::vector<std::pair<float, float>> out;
+  for (size_t b = 0; b < t_start_.size(); ++b) {
+    float a = 0.f, e = 0.f;
+    HIP_OK(hipEventElapsedTime(&a, ref, t_start_[b]));
+    HIP_OK(hipEventElapsedTime(&e, ref, t_end_[b]));
+    out.emplace_back(a, e);
+  }
+  return out;
+}
+
 Reducer::~Reducer() {
+  for (auto e : t_start_) hipEventDestroy(e);
+  for (auto e : t_end_) hipEventDestroy(e);
   if (stage_) hipFree(stage_);
   for (auto& v : ready_ev_)
     for (auto e : v)
@@ -273,6 +300,7 @@ void Reducer::launch(int b) {
     HIP_OK(hipStreamWaitEvent(target, evs[i], 0));
   }
   float* buf = arena_ + bs.offset;
+  if (timing_) HIP_OK(hipEventRecord(t_start_[b], target));
   if (real && comm_bf16_) {
     unsigned short* sb = stage_ + bs.offset;
     if (ddp_pack_bf16(buf, bs.count, sb, target) != 0)
@@ -296,6 +324,7 @@ void Reducer::launch(int b) {
     }
   }
   done_stream_[b] = target;
+  if (timing_) HIP_OK(hipEventRecord(t_end_[b], target));
   HIP_OK(hipEventRecord(done_ev_[b], target));
   if (debug_sync_) HIP_OK(hipStreamSynchronize(target));
 }

@@ -98,6 +98,11 @@ class Reducer {
   void set_comm_dtype(int dtype);
   int comm_dtype() const { return comm_bf16_ ? 1 : 0; }
   int launched() const { return sched_.launched(); }
+  // Timing probe (tools/overlap_probe.py): record timing events around each bucket's collective
+  // on the stream it runs on; bucket_times(ref) = (start, end) ms of every bucket of the last
+  // backward relative to `ref` (a timing event recorded earlier on the compute stream).
+  void set_timing(bool on);
+  std::vector<std::pair<float, float>> bucket_times(hipEvent_t ref) const;
   hipStream_t comm_stream() const { return comm_stream_; }
 
  private:
@@ -110,6 +115,8 @@ class Reducer {
   std::vector<std::vector<hipEvent_t>> ready_ev_;  // one event per producer stream slot
   std::vector<hipEvent_t> done_ev_;
   std::vector<hipStream_t> done_stream_;  // stream each bucket's collective ran on
+  bool timing_ = false;
+  std::vector<hipEvent_t> t_start_, t_end_;
   bool average_;
   bool debug_sync_ = false;
   bool overlap_ = true;

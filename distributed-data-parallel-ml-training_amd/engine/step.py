@@ -10,6 +10,8 @@ replay it. Host cost per step becomes one graph launch.
 Capture protocol: a few eager warm-up steps on a side stream (lazy allocations, autograd
 structures), then ``torch.cuda.graph`` capture; replays are bit-identical to eager steps.
 """
+import os
+
 import torch
 
 from ..parallel.comm import is_live
@@ -240,7 +242,14 @@ class SegmentedDDPStep(TrainStep):
             self.buckets.append(((i0, i1), (lo, hi)))
         self.cut = self.buckets[0][1][0]  # start of the last layers' bucket (tests)
         self.total = arena.total
-        self.comm_stream = torch.cuda.Stream()
+        # The comm stream comes from HIP's HIGH-priority hardware-queue pool (env
+        # DDP_AMD_COMM_PRIORITY=normal reverts): normal-priority streams share GPU_MAX_HW_QUEUES
+        # (4) queues round-robin, and with live RCCL communicators (which create streams of
+        # their own) the comm stream landed on the main stream's queue — every bucket then ran
+        # strictly between the segment graphs, 0 us hidden; high priority: 76 of 120 us hidden
+        # (tools/overlap_probe.py, profiles/r2_pipelined_ddp.md).
+        prio = os.environ.get("DDP_AMD_COMM_PRIORITY", "high")
+        self.comm_stream = torch.cuda.Stream(priority=-1 if prio == "high" else 0)
         self.comm_a = None
         if is_live(ddp.comm):
             from ..parallel.comm import RcclCommunicator
@@ -270,6 +279,14 @@ class SegmentedDDPStep(TrainStep):
         self._flags[1] = 1
         self.graphs = None
         self._cuts = None
+        # timing probe (tools/overlap_probe.py): list receiving (bucket, start, end) timing
+        # events recorded on the comm stream around each bucket's collective + update
+        self.probe = None
+
+    def _probe_event(self, stream):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(stream)
+        return ev
 
     def _fp(self, i):
         return self._flags.data_ptr() + 4 * i
@@ -332,6 +349,13 @@ class SegmentedDDPStep(TrainStep):
                            cs.cuda_stream)
         (i0, i1), (lo, hi) = self.buckets[j]
         last = j == len(self.buckets) - 1
+        t0 = self._probe_event(cs) if self.probe is not None else None
+        self._comm_body(j, cs, i0, i1, lo, hi, last)
+        if t0 is not None:
+            self.probe.append((j, t0, self._probe_event(cs)))
+
+    def _comm_body(self, j, cs, i0, i1, lo, hi, last):
+        from ..ops.common import native
         if self.zero is not None:
             with trace_range(f"zero_update_bucket{j}"):
                 self.zero.step(j, stream=cs, skip=self._fp(4),
