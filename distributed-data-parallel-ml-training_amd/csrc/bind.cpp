@@ -105,6 +105,31 @@ PYBIND11_MODULE(_native, m) {
   }, py::arg("g"), py::arg("dy"), py::arg("wt"), py::arg("dx"), py::arg("ws"),
      py::arg("ws_elems"), py::arg("splits"), py::arg("stream"), py::arg("accumulate") = 0,
      py::arg("bn") = py::none());
+  // one layer's backward: WGRAD (dw += ...) and stride-1 DGRAD (dx = ..., optional BN-backward
+  // sums) as one grouped launch when the policy allows (ddp_conv_bwd_pair), else two
+  m.def("conv_bwd_pair", [](py::tuple g, uintptr_t dy, uintptr_t wc, uintptr_t dx, uintptr_t x,
+                            uintptr_t dw, uintptr_t ws, size_t ws_elems, uintptr_t st,
+                            py::object bn) {
+    auto c = geom(g);
+    ddp_amd::BnBwdFuse f{};
+    const ddp_amd::BnBwdFuse* fp = nullptr;
+    if (!bn.is_none()) {
+      auto t = bn.cast<py::tuple>();
+      f.z = P<unsigned short>(t[0].cast<uintptr_t>());
+      f.coef = P<float>(t[1].cast<uintptr_t>());
+      f.sums = P<float>(t[2].cast<uintptr_t>());
+      f.pool = t[3].cast<int>();
+      f.relu = t[4].cast<int>();
+      f.Hz = t[5].cast<int>();
+      f.Wz = t[6].cast<int>();
+      fp = &f;
+    }
+    check(ddp_conv_bwd_pair(&c, P<void>(dy), P<void>(wc), P<void>(dx), P<void>(x), P<float>(dw),
+                            P<float>(ws), ws_elems, fp, S(st)), "conv_bwd_pair");
+  }, py::arg("g"), py::arg("dy"), py::arg("wc"), py::arg("dx"), py::arg("x"), py::arg("dw"),
+     py::arg("ws"), py::arg("ws_elems"), py::arg("stream"), py::arg("bn") = py::none());
+  m.def("conv_pair_mode", [](int mode, int items) { ddp_conv_pair_mode(mode, items); },
+        py::arg("mode"), py::arg("items") = 0);
   m.def("conv_wgrad", [](py::tuple g, uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws,
                          size_t ws_elems, int splits, uintptr_t st) {
     auto c = geom(g);

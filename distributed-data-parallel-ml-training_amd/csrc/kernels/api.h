@@ -112,6 +112,10 @@ int ddp_sgd(float* p, const float* g, float* buf, size_t n, float lr, float mome
 int ddp_conv_fwd_smallk(const ddp_amd::ConvGeom* g, const void* x, const void* wc,
                         const float* bias, void* y, float* stats, hipStream_t st);
 void ddp_conv_options(int wgrad_atomic, int persistent, int stages);
+void ddp_conv_pair_mode(int mode, int items);
+int ddp_conv_bwd_pair(const ddp_amd::ConvGeom* g, const void* dy, const void* wc, void* dx,
+                      const void* x, float* dw, float* ws, size_t ws_elems,
+                      const ddp_amd::BnBwdFuse* bn, hipStream_t st);
 void ddp_conv_fixup(float* facc, size_t facc_elems, unsigned* tickets, size_t n_tickets, int mode,
                     size_t max_bytes);
 void ddp_conv_tune_set(int mode, int M, int N, int K, int tile, int splits, int stages);

@@ -188,8 +188,18 @@ __device__ __forceinline__ void wait_dma_barrier() {
 
 // BNF (DGRAD only): the epilogue also accumulates the preceding block's BatchNorm-backward sums
 // (ConvArgs::bnf) — a separate instantiation so the plain kernels keep their register budget
+// LDS bytes of one (BM, BN, NST) tile ring (the kernels' single __shared__ array)
+template <int BM, int BN, int NST>
+struct ConvSmem {
+  static constexpr int elems = NST * (BM + BN) * 64;
+};
+
+// The GEMM body. ``bid`` / ``nblk`` stand for blockIdx.x / gridDim.x, so a grouped launch
+// (conv_bwd_pair_kernel: the DGRAD and WGRAD GEMMs of one layer in ONE launch) can hand each
+// problem its own block range. ``smem`` = the launching kernel's single LDS array.
 template <int MODE, int BM, int BN, int NST, bool BNF = false>
-__global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
+__device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned short* smem,
+                                                const int bid, const int nblk) {
   constexpr int BK = 64;
   constexpr int WTM = BM / 2, WTN = BN / 2;
   constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -198,7 +208,6 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
   constexpr int TILE_A = BM * BK, TILE_B = BN * BK;
   static_assert(CA >= 1 && CB >= 1, "tile too small for 256 threads");
   static_assert(NST >= 2 && NST <= 4, "2..4 LDS stages");
-  __shared__ __attribute__((aligned(16))) unsigned short smem[NST * (TILE_A + TILE_B)];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -207,7 +216,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
   DDP_DEVICE_CHECK(blockDim.x == 256 && args.g.C % 8 == 0 && args.g.K % 8 == 0);
   DDP_DEVICE_CHECK(args.splits >= 1 && args.ksteps_per_split >= 1);
 
-  // Persistent work loop: item = (split z, tile); a block walks items blockIdx.x, +gridDim.x, ...
+  // Persistent work loop: item = (split z, tile); a block walks items bid, +nblk, ...
   // and prefetches the first k-step of its NEXT item while it finishes (last MFMAs + epilogue)
   // the current one, so short-K tiles do not pay the DMA latency once per tile.
   const int tiles_n = (args.Ng + BN - 1) / BN;
@@ -637,7 +646,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
     __syncthreads();
     if (wm == 0 && rl == 0) {
       float* st = (MODE == MODE_FWD ? args.stats : args.bnf.sums) +
-                  (blockIdx.x % kStatRep) * 2 * args.Ng;  // spread contention
+                  (bid % kStatRep) * 2 * args.Ng;  // spread contention
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int col = col0 + wn * WTN + j * 16 + cq;
@@ -709,7 +718,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
 
   // NST-stage LDS ring: the DMAs of up to NST-1 k-steps are in flight while one is computed.
   constexpr int DMA = CA + CB;  // vector-memory instructions per thread per stage
-  for (int item = blockIdx.x; item < nitems; item += gridDim.x) {
+  for (int item = bid; item < nitems; item += nblk) {
     setup(item);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -740,6 +749,25 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
   }
 }
 
+template <int MODE, int BM, int BN, int NST, bool BNF = false>
+__global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
+  __shared__ __attribute__((aligned(16))) unsigned short smem[ConvSmem<BM, BN, NST>::elems];
+  conv_igemm_body<MODE, BM, BN, NST, BNF>(args, smem, blockIdx.x, gridDim.x);
+}
+
+// One layer's backward GEMMs in ONE launch: blocks [0, n_dg) run the DGRAD problem, the rest
+// the WGRAD problem (independent outputs, both read dy). At the strong-scaling batches each of
+// them alone leaves most of the 256 CUs idle and pays its own latency floor; side by side they
+// fill each other's idle slots and cost one dispatch. Same tile config for both (one LDS array).
+template <int BM, int BN, int NST, bool BNF>
+__global__ __launch_bounds__(256) void conv_bwd_pair_kernel(ConvArgs dg, ConvArgs wg, int n_dg) {
+  __shared__ __attribute__((aligned(16))) unsigned short smem[ConvSmem<BM, BN, NST>::elems];
+  if ((int)blockIdx.x < n_dg)
+    conv_igemm_body<MODE_DGRAD, BM, BN, NST, BNF>(dg, smem, blockIdx.x, n_dg);
+  else
+    conv_igemm_body<MODE_WGRAD, BM, BN, NST, false>(wg, smem, blockIdx.x - n_dg, gridDim.x - n_dg);
+}
+
 // Split-K finish for FWD/DGRAD: sum the slabs in split order -> (+bias) bf16 output
 // (+ per-channel stats of the rounded output for FWD).
 // Thread layout: cg_local = tid % Gb (8 channels each), rows strided; stats reduced in
@@ -756,19 +784,38 @@ __device__ __forceinline__ size_t map_row(const RowMap& m, int row) {
   return ((size_t)n * m.H + m.pa + m.stride * i) * m.W + m.pb + m.stride * j;
 }
 
+struct FinishArgs {  // split-K finish of a FWD / DGRAD GEMM (one launch or one pair half)
+  const float* ws;
+  int splits;
+  unsigned short* out;
+  const float* bias;
+  float* stats;
+  int Mg, Ng;
+  RowMap rmap;
+  int accumulate;
+  BnBwdFuse bnf;
+  int H, W;
+};
+
+// body of splitk_finish_kernel: (bx, by) / gx stand for blockIdx.(x, y) / gridDim.x;
+// red = 2 x 8 x 256 floats of LDS
 template <bool BNF>
-__global__ __launch_bounds__(256) void splitk_finish_kernel(const float* ws, int splits,
-                                                            unsigned short* out,
-                                                            const float* bias, float* stats,
-                                                            int Mg, int Ng, RowMap rmap,
-                                                            int accumulate, BnBwdFuse bnf,
-                                                            int H, int W) {
+__device__ __forceinline__ void splitk_finish_body(const FinishArgs& fa, float* red_, int bx,
+                                                   int by, int gx) {
+  const float* ws = fa.ws;
+  const int splits = fa.splits, Mg = fa.Mg, Ng = fa.Ng, accumulate = fa.accumulate;
+  const int H = fa.H, W = fa.W;
+  unsigned short* out = fa.out;
+  const float* bias = fa.bias;
+  float* stats = fa.stats;
+  const RowMap rmap = fa.rmap;
+  const BnBwdFuse& bnf = fa.bnf;
+  float (*red)[8][256] = reinterpret_cast<float (*)[8][256]>(red_);
   constexpr bool has_bnf = BNF;
-  __shared__ float red[2][8][256];
   const int G = Ng / 8;
   const int Gb = G < 256 ? G : 256;
   const int cgl = threadIdx.x % Gb, prow = threadIdx.x / Gb, prows = 256 / Gb;
-  const int cg = blockIdx.y * Gb + cgl;
+  const int cg = by * Gb + cgl;
   const bool active = prow < prows && cg < G;  // Gb need not divide 256 (e.g. 1000 classes)
   const size_t slab = (size_t)Mg * Ng;
   float s[8], ss[8], bv[8];
@@ -790,7 +837,7 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(const float* ws, int
     }
     stats = bnf.sums;
   }
-  for (int row = blockIdx.x * prows + prow; active && row < Mg; row += gridDim.x * prows) {
+  for (int row = bx * prows + prow; active && row < Mg; row += gx * prows) {
     float v[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = bv[e];
@@ -854,12 +901,18 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(const float* ws, int
   for (int idx = threadIdx.x; idx < Gb * 16; idx += 256) {
     const int k = idx / (Gb * 8), rem = idx % (Gb * 8);
     const int c = rem / 8, e = rem % 8;
-    if (blockIdx.y * Gb + c >= G) continue;
+    if (by * Gb + c >= G) continue;
     float t = 0.f;
     for (int r = 0; r < prows; ++r) t += red[k][e][r * Gb + c];
-    float* st = stats + ((blockIdx.x + blockIdx.y) % kStatRep) * 2 * Ng;
-    atomicAdd(st + k * Ng + (blockIdx.y * Gb + c) * 8 + e, t);
+    float* st = stats + ((bx + by) % kStatRep) * 2 * Ng;
+    atomicAdd(st + k * Ng + (by * Gb + c) * 8 + e, t);
   }
+}
+
+template <bool BNF>
+__global__ __launch_bounds__(256) void splitk_finish_kernel(FinishArgs fa) {
+  __shared__ float red[2 * 8 * 256];
+  splitk_finish_body<BNF>(fa, red, blockIdx.x, blockIdx.y, gridDim.x);
 }
 
 // Split-K finish for WGRAD: dW[k][c][r][s] += sum_z slab[z][k][(r,s,c)].
@@ -899,15 +952,16 @@ __global__ __launch_bounds__(256) void wgrad_finish_kernel(const float* ws, int 
 // this is a vectorised sum of the slabs — no transpose. blockIdx.y = group of kWgFinishGroupKrsc
 // slabs (fixed order inside a group); several groups combine with atomics.
 constexpr int kWgFinishGroupKrsc = 16;
-__global__ __launch_bounds__(256) void wgrad_finish_krsc_kernel(const float* __restrict__ ws,
-                                                                int splits, int K, int RS, int C,
-                                                                int Creal, float* __restrict__ dw) {
+__device__ __forceinline__ void wgrad_finish_krsc_body(const float* __restrict__ ws, int splits,
+                                                       int K, int RS, int C, int Creal,
+                                                       float* __restrict__ dw, int bx, int by,
+                                                       int gx, int gy) {
   const size_t slab = (size_t)K * RS * C;
   const size_t n4 = slab / 4;
-  const int z0 = blockIdx.y * kWgFinishGroupKrsc, z1 = min(splits, z0 + kWgFinishGroupKrsc);
-  const bool single = gridDim.y == 1;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4;
-       i += (size_t)gridDim.x * blockDim.x) {
+  const int z0 = by * kWgFinishGroupKrsc, z1 = min(splits, z0 + kWgFinishGroupKrsc);
+  const bool single = gy == 1;
+  for (size_t i = bx * (size_t)blockDim.x + threadIdx.x; i < n4;
+       i += (size_t)gx * blockDim.x) {
     float4 v = reinterpret_cast<const float4*>(ws + z0 * slab)[i];
     for (int z = z0 + 1; z < z1; ++z) {
       const float4 a = reinterpret_cast<const float4*>(ws + z * slab)[i];
@@ -935,6 +989,36 @@ __global__ __launch_bounds__(256) void wgrad_finish_krsc_kernel(const float* __r
         else unsafeAtomicAdd(dw + krs * Creal + c + t, vv[t]);
       }
     }
+  }
+}
+
+__global__ __launch_bounds__(256) void wgrad_finish_krsc_kernel(const float* __restrict__ ws,
+                                                                int splits, int K, int RS, int C,
+                                                                int Creal, float* __restrict__ dw) {
+  wgrad_finish_krsc_body(ws, splits, K, RS, C, Creal, dw, blockIdx.x, blockIdx.y, gridDim.x,
+                         gridDim.y);
+}
+
+struct WgFinishArgs {
+  const float* ws;
+  int splits, K, RS, C, Creal;
+  float* dw;
+  int gx, gy;  // its own grid (0 x 0 = no WGRAD finish in this launch)
+};
+
+// The split-K finishes of one layer's backward pair in ONE launch: blocks [0, dgx*dgy) reduce
+// the DGRAD slabs (dgy channel chunks), the rest the WGRAD slabs ([K][R][S][C] gradient)
+template <bool BNF>
+__global__ __launch_bounds__(256) void bwd_pair_finish_kernel(FinishArgs fa, int dgx, int dgy,
+                                                              WgFinishArgs wa) {
+  __shared__ float red[2 * 8 * 256];
+  const int b = blockIdx.x;
+  if (b < dgx * dgy) {
+    splitk_finish_body<BNF>(fa, red, b % dgx, b / dgx, dgx);
+  } else {
+    const int w = b - dgx * dgy;
+    wgrad_finish_krsc_body(wa.ws, wa.splits, wa.K, wa.RS, wa.C, wa.Creal, wa.dw, w % wa.gx,
+                           w / wa.gx, wa.gx, wa.gy);
   }
 }
 
@@ -1039,8 +1123,10 @@ static void launch_gemm(const ConvArgs& a, int items, hipStream_t st) {
   launch_gemm_t<MODE, BM, BN, NST, false>(a, items, st);
 }
 
+// Normalise the split count (no empty split), decide WGRAD atomics / FWD-DGRAD fixup; returns
+// the number of work items (tiles x splits).
 template <int MODE, int BM, int BN>
-static void launch_cfg(ConvArgs& a, int splits, hipStream_t st, int nst_req = 0) {
+static int prepare_cfg(ConvArgs& a, int splits) {
   constexpr int BK = 64;
   const int tiles = ((a.Mg + BM - 1) / BM) * ((a.Ng + BN - 1) / BN);
   const int ksteps = (a.Kg + BK - 1) / BK;
@@ -1062,7 +1148,68 @@ static void launch_cfg(ConvArgs& a, int splits, hipStream_t st, int nst_req = 0)
   } else {
     a.fixup = 0;
   }
-  const int items = tiles * splits;
+  return tiles * splits;
+}
+
+// split-K finish geometry / arguments of a prepared problem
+static bool needs_finish(int mode, const ConvArgs& a) {
+  if (a.splits <= 1) return false;
+  if (mode == MODE_WGRAD) return !a.wg_atomic;
+  return !a.fixup;
+}
+
+static void dg_finish_grid(const ConvArgs& a, int* bx_out, int* chunks_out) {
+  const int G = a.Ng / 8;
+  const int Gb = G < 256 ? G : 256;
+  const int chunks = (G + Gb - 1) / Gb;
+  const int rows_per_block = std::max(1, 256 / Gb);
+  // ~2 rows per thread: enough workgroups in flight for a bandwidth-bound pass
+  int bx = (a.Mg + rows_per_block * 2 - 1) / (rows_per_block * 2);
+  *bx_out = std::max(1, std::min(bx, 2048 / chunks + 1));
+  *chunks_out = chunks;
+}
+
+static FinishArgs finish_args(int mode, const ConvArgs& a) {
+  RowMap rm{0, 0, 0, 0, 0, 0, 0};
+  if (a.phase) rm = RowMap{a.g.stride, a.Hp, a.Wp, a.g.H, a.g.W, a.pa, a.pb};
+  const bool fwd = mode == MODE_FWD;
+  return FinishArgs{a.ws, a.splits, a.out, fwd ? a.bias : nullptr, fwd ? a.stats : nullptr,
+                    a.Mg, a.Ng, rm, a.accumulate, a.bnf, a.g.H, a.g.W};
+}
+
+static WgFinishArgs wg_finish_args(const ConvArgs& a) {
+  const size_t n4 = (size_t)a.Mg * a.Ng / 4;
+  const int groups = (a.splits + kWgFinishGroupKrsc - 1) / kWgFinishGroupKrsc;
+  const int bx = (int)std::min<size_t>((n4 + 255) / 256, std::max(1, 2048 / groups));
+  return WgFinishArgs{a.ws, a.splits, a.g.K, a.g.R * a.g.S, a.g.C, a.g.Creal, a.dw, bx, groups};
+}
+
+template <int MODE>
+static void launch_finish(const ConvArgs& a, hipStream_t st) {
+  if (!needs_finish(MODE, a)) return;
+  if (MODE == MODE_WGRAD && a.g.wkrsc) {
+    const WgFinishArgs w = wg_finish_args(a);
+    hipLaunchKernelGGL(wgrad_finish_krsc_kernel, dim3(w.gx, w.gy), dim3(256), 0, st, a.ws,
+                       a.splits, a.g.K, a.g.R * a.g.S, a.g.C, a.g.Creal, a.dw);
+  } else if (MODE == MODE_WGRAD) {
+    const int groups = (a.splits + kWgFinishGroup - 1) / kWgFinishGroup;
+    const size_t lds = sizeof(float) * a.g.R * a.g.S * a.g.C;
+    hipLaunchKernelGGL(wgrad_finish_kernel, dim3(a.g.K, groups), dim3(256), lds, st, a.ws,
+                       a.splits, a.g.K, a.g.R, a.g.S, a.g.C, a.g.Creal, a.dw);
+  } else {
+    int bx, chunks;
+    dg_finish_grid(a, &bx, &chunks);
+    const FinishArgs fa = finish_args(MODE, a);
+    if (MODE == MODE_DGRAD && a.has_bnf)
+      hipLaunchKernelGGL(splitk_finish_kernel<true>, dim3(bx, chunks), dim3(256), 0, st, fa);
+    else
+      hipLaunchKernelGGL(splitk_finish_kernel<false>, dim3(bx, chunks), dim3(256), 0, st, fa);
+  }
+}
+
+template <int MODE, int BM, int BN>
+static void launch_cfg(ConvArgs& a, int splits, hipStream_t st, int nst_req = 0) {
+  const int items = prepare_cfg<MODE, BM, BN>(a, splits);
   // deepest ring that fits the 160 KiB LDS for this tile ((BM + BN) x 64 bf16 per stage)
   constexpr int kStageBytes = (BM + BN) * 64 * 2;
   constexpr int kMaxStages = kStageBytes * 4 <= 163840 ? 4 : (kStageBytes * 3 <= 163840 ? 3 : 2);
@@ -1076,40 +1223,7 @@ static void launch_cfg(ConvArgs& a, int splits, hipStream_t st, int nst_req = 0)
   }
   launch_gemm<MODE, BM, BN, 2>(a, items, st);
 launched:
-  if (splits == 1) return;
-  if (MODE == MODE_WGRAD && a.wg_atomic) return;
-  if (MODE != MODE_WGRAD && a.fixup) return;
-  if (MODE == MODE_WGRAD && a.g.wkrsc) {
-    const size_t n4 = (size_t)a.Mg * a.Ng / 4;
-    const int groups = (splits + kWgFinishGroupKrsc - 1) / kWgFinishGroupKrsc;
-    const int bx = (int)std::min<size_t>((n4 + 255) / 256, std::max(1, 2048 / groups));
-    hipLaunchKernelGGL(wgrad_finish_krsc_kernel, dim3(bx, groups), dim3(256), 0, st, a.ws, splits,
-                       a.g.K, a.g.R * a.g.S, a.g.C, a.g.Creal, a.dw);
-  } else if (MODE == MODE_WGRAD) {
-    const int groups = (splits + kWgFinishGroup - 1) / kWgFinishGroup;
-    const size_t lds = sizeof(float) * a.g.R * a.g.S * a.g.C;
-    hipLaunchKernelGGL(wgrad_finish_kernel, dim3(a.g.K, groups), dim3(256), lds, st, a.ws, splits,
-                       a.g.K, a.g.R, a.g.S, a.g.C, a.g.Creal, a.dw);
-  } else {
-    const int G = a.Ng / 8;
-    const int Gb = G < 256 ? G : 256;
-    const int chunks = (G + Gb - 1) / Gb;
-    const int rows_per_block = std::max(1, 256 / Gb);
-    // ~2 rows per thread: enough workgroups in flight for a bandwidth-bound pass
-    int bx = (a.Mg + rows_per_block * 2 - 1) / (rows_per_block * 2);
-    bx = std::max(1, std::min(bx, 2048 / chunks + 1));
-    RowMap rm{0, 0, 0, 0, 0, 0, 0};
-    if (a.phase) rm = RowMap{a.g.stride, a.Hp, a.Wp, a.g.H, a.g.W, a.pa, a.pb};
-    if (MODE == MODE_DGRAD && a.has_bnf)
-      hipLaunchKernelGGL(splitk_finish_kernel<true>, dim3(bx, chunks), dim3(256), 0, st, a.ws,
-                         splits, a.out, nullptr, nullptr, a.Mg, a.Ng, rm, a.accumulate, a.bnf,
-                         a.g.H, a.g.W);
-    else
-      hipLaunchKernelGGL(splitk_finish_kernel<false>, dim3(bx, chunks), dim3(256), 0, st, a.ws,
-                         splits, a.out, MODE == MODE_FWD ? a.bias : nullptr,
-                         MODE == MODE_FWD ? a.stats : nullptr, a.Mg, a.Ng, rm, a.accumulate,
-                         a.bnf, a.g.H, a.g.W);
-  }
+  launch_finish<MODE>(a, st);
 }
 
 // Measured tile / split-K choices per GEMM problem (tools/conv_tune.py sweeps every candidate
@@ -1136,9 +1250,9 @@ static int g_force_stages = 0;              // 2..4 (sweeps), 0 = policy
 // L2 -> LDS traffic per MFMA, fewer tiles)
 constexpr int kNumTiles = 8;
 
+// tile / split-K / LDS-stage choice for a problem: the measured table, else the cost model
 template <int MODE>
-static void launch_mode(ConvArgs& a, size_t ws_elems, hipStream_t st) {
-  int sp[kNumTiles];
+static void plan_mode(ConvArgs& a, size_t ws_elems, int* best_out, int* sp, int* nst_out) {
   const double c[4] = {tile_cost(128, 128, a, ws_elems, &sp[0]), tile_cost(128, 64, a, ws_elems, &sp[1]),
                        tile_cost(64, 128, a, ws_elems, &sp[2]), tile_cost(64, 64, a, ws_elems, &sp[3])};
   int best = 0, nst = g_force_stages;
@@ -1163,6 +1277,14 @@ static void launch_mode(ConvArgs& a, size_t ws_elems, hipStream_t st) {
       nst = it->second.stages;
     }
   }
+  *best_out = best;
+  *nst_out = nst;
+}
+
+template <int MODE>
+static void launch_mode(ConvArgs& a, size_t ws_elems, hipStream_t st) {
+  int sp[kNumTiles], best, nst;
+  plan_mode<MODE>(a, ws_elems, &best, sp, &nst);
   switch (best) {
     case 0: launch_cfg<MODE, 128, 128>(a, sp[0], st, nst); break;
     case 1: launch_cfg<MODE, 128, 64>(a, sp[1], st, nst); break;
@@ -1326,5 +1448,110 @@ extern "C" int ddp_conv_wgrad(const ConvGeom* g, const void* dy, const void* x, 
   a.dPQ = make_fastdiv(g->P * g->Q);
   a.dQ = make_fastdiv(g->Q);
   launch_mode<MODE_WGRAD>(a, ws_elems, st);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------- backward pair -------------------------------
+// DGRAD + WGRAD of one stride-1 layer in ONE launch (conv_bwd_pair_kernel) and their split-K
+// finishes in one more (bwd_pair_finish_kernel): two dispatches instead of up to four, and the
+// two latency-bound GEMMs of a small batch share the chip instead of running back to back.
+// Policy (DDP_AMD_BWD_PAIR via ddp_conv_pair_mode): 0 never; 1 when the measured / modelled
+// choice is the 64x64 tile for both problems; 2 always (both forced to 64x64); 3 (default) when
+// both pick 64x64, or when the paired 64x64 launch has at most g_pair_items work items (about
+// one wave of 4 blocks per CU: the small problems of the strong-scaling batches, where pairing
+// beat the separately tuned launches — VGG-11 b64 0.544 vs 0.608 ms, b128 0.666 vs 0.702 —
+// while forcing it on the big b256 layers lost 5%).
+static int g_pair_mode = 3;
+static int g_pair_items = 1024;
+extern "C" void ddp_conv_pair_mode(int m, int items) {
+  g_pair_mode = m;
+  if (items > 0) g_pair_items = items;
+}
+
+extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* wc, void* dx,
+                                 const void* x, float* dw, float* ws, size_t ws_elems,
+                                 const BnBwdFuse* bn, hipStream_t st) {
+  auto separate = [&]() -> int {
+    const int r = ddp_conv_wgrad(g, dy, x, dw, ws, ws_elems, 0, st);
+    if (r) return r;
+    return conv_dgrad_impl(g, dy, wc, dx, ws, ws_elems, 0, 0, bn, st);
+  };
+  if (g_pair_mode == 0 || g->stride != 1 || g->C % 8 || g->K % 8 || g->Creal != g->C)
+    return separate();
+  const size_t dya = (size_t)g->N * g->P * g->Q * g->K, wb = (size_t)g->K * g->R * g->S * g->C;
+  const size_t xb = (size_t)g->N * g->H * g->W * g->C;
+  if (!fits_buffer(dya) || !fits_buffer(wb) || !fits_buffer(xb)) return separate();
+  ConvArgs d{};  // as conv_dgrad_impl (stride 1, no accumulate)
+  d.g = *g;
+  if (bn) {
+    d.has_bnf = 1;
+    d.bnf = *bn;
+  }
+  d.a = (const unsigned short*)dy;
+  d.b = (const unsigned short*)wc;
+  d.out = (unsigned short*)dx;
+  d.ws = ws;
+  d.Mg = g->N * g->H * g->W;
+  d.Ng = g->C;
+  d.Kg = g->R * g->S * g->K;
+  d.a_bytes = (int)(2 * dya);
+  d.b_bytes = (int)(2 * wb);
+  ConvArgs w{};  // as ddp_conv_wgrad
+  w.g = *g;
+  if (g->R * g->S == 1) w.g.wkrsc = 1;
+  w.a = (const unsigned short*)dy;
+  w.b = (const unsigned short*)x;
+  w.dw = dw;
+  w.ws = ws;
+  w.wg_atomic = g_wgrad_atomic;
+  w.Mg = g->K;
+  w.Ng = g->R * g->S * g->C;
+  w.Kg = g->N * g->P * g->Q;
+  w.a_bytes = (int)(2 * dya);
+  w.b_bytes = (int)(2 * xb);
+  w.dPQ = make_fastdiv(g->P * g->Q);
+  w.dQ = make_fastdiv(g->Q);
+  int spd[kNumTiles], bd, nd, spw[kNumTiles], bw, nw;
+  plan_mode<MODE_DGRAD>(d, ws_elems, &bd, spd, &nd);
+  plan_mode<MODE_WGRAD>(w, ws_elems, &bw, spw, &nw);
+  const bool both64 = bd == 3 && bw == 3;
+  if (g_pair_mode == 1 && !both64) return separate();
+  int sd = spd[3], sw = spw[3];
+  if (bd != 3) tile_cost(64, 64, d, ws_elems, &sd);
+  if (bw != 3) tile_cost(64, 64, w, ws_elems, &sw);
+  if (bd == 3 && bw == 3 && g_force_tile == 0) {  // measured splits (plan_mode filled sp[3])
+    sd = spd[3];
+    sw = spw[3];
+  }
+  // the slab workspace is split between the two problems
+  const int itd = prepare_cfg<MODE_DGRAD, 64, 64>(d, std::max(1, sd));
+  size_t dneed = needs_finish(MODE_DGRAD, d) ? (size_t)d.splits * d.Mg * d.Ng : 0;
+  dneed = (dneed + 63) / 64 * 64;
+  w.ws = ws + dneed;
+  const int itw = prepare_cfg<MODE_WGRAD, 64, 64>(w, std::max(1, sw));
+  const size_t wneed = needs_finish(MODE_WGRAD, w) ? (size_t)w.splits * w.Mg * w.Ng : 0;
+  if (dneed + wneed > ws_elems) return separate();
+  if (g_pair_mode == 3 && !both64 && itd + itw > g_pair_items) return separate();
+  if (d.has_bnf && (d.splits <= 1 || d.fixup))
+    hipLaunchKernelGGL((conv_bwd_pair_kernel<64, 64, 3, true>), dim3(itd + itw), dim3(256), 0, st,
+                       d, w, itd);
+  else
+    hipLaunchKernelGGL((conv_bwd_pair_kernel<64, 64, 3, false>), dim3(itd + itw), dim3(256), 0, st,
+                       d, w, itd);
+  const bool fd = needs_finish(MODE_DGRAD, d), fw = needs_finish(MODE_WGRAD, w);
+  if (fd && fw && w.g.wkrsc) {
+    int bx, ch;
+    dg_finish_grid(d, &bx, &ch);
+    const FinishArgs fa = finish_args(MODE_DGRAD, d);
+    const WgFinishArgs wa = wg_finish_args(w);
+    const dim3 grid(bx * ch + wa.gx * wa.gy);
+    if (d.has_bnf)
+      hipLaunchKernelGGL(bwd_pair_finish_kernel<true>, grid, dim3(256), 0, st, fa, bx, ch, wa);
+    else
+      hipLaunchKernelGGL(bwd_pair_finish_kernel<false>, grid, dim3(256), 0, st, fa, bx, ch, wa);
+  } else {
+    launch_finish<MODE_DGRAD>(d, st);
+    launch_finish<MODE_WGRAD>(w, st);
+  }
   return (int)hipGetLastError();
 }

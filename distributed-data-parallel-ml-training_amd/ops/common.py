@@ -25,6 +25,11 @@ def native():
         _NATIVE.conv_options(int(os.environ.get("DDP_AMD_WGRAD_ATOMIC", "0")),
                              int(os.environ.get("DDP_AMD_CONV_PERSISTENT", "0")),
                              int(os.environ.get("DDP_AMD_CONV_STAGES", str(CONV_STAGES))))
+        # DDP_AMD_BWD_PAIR: one layer's wgrad + dgrad as ONE grouped launch — 0 never,
+        # 1 when both problems pick the 64x64 tile, 2 always (stride-1 layers), 3 (default)
+        # also when the paired launch has <= DDP_AMD_BWD_PAIR_ITEMS (1024) work items
+        _NATIVE.conv_pair_mode(int(os.environ.get("DDP_AMD_BWD_PAIR", "3")),
+                               int(os.environ.get("DDP_AMD_BWD_PAIR_ITEMS", "1024")))
         load_conv_tuning(_NATIVE)
     return _NATIVE
 

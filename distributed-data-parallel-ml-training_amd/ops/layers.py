@@ -161,6 +161,16 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=Non
     g = spec.geom(N, H, W, weight_krsc(dweight))
     s = stream_handle()
     ws = workspace(x.device)
+    if (need_dx and link is None and not _common.BWD_SIDE_STREAM and spec.stride == 1
+            and spec.C == spec.Cr):
+        # wgrad + dgrad of this layer as one grouped launch (+ one finish launch) when the
+        # kernel policy allows it (conv_igemm.hip ddp_conv_bwd_pair), else the two launches
+        dx = torch.empty_like(x)
+        native().conv_bwd_pair(g, ptr(dz), ptr(spec.wc), ptr(dx), ptr(x), ptr(dweight), ptr(ws),
+                               ws.numel(), s, bn=bnf)
+        if weight is not None:
+            grad_ready([weight])
+        return dx
     if weight is not None and _common.BWD_SIDE_STREAM:
         side = side_stream(x.device, x, dz)
         with torch.cuda.stream(side.stream):

@@ -95,6 +95,34 @@ def test_conv_dgrad(native_ext, case, layout):
     assert rel_err(dw, wr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+@pytest.mark.parametrize("case", [(32, 512, 2, 2, 512, 3, 1, 1), (32, 256, 4, 4, 512, 3, 1, 1),
+                                  (32, 64, 16, 16, 128, 3, 1, 1), (2, 128, 14, 14, 256, 1, 1, 0),
+                                  (4, 64, 15, 15, 32, 3, 2, 1)])
+def test_conv_bwd_pair(native_ext, case, mode):
+    """One layer's wgrad + dgrad as ONE grouped launch (+ one grouped split-K finish):
+    ddp_conv_bwd_pair, policy 0 = two launches, 1 = paired when both pick 64x64, 2 = always
+    paired (stride 1), 3 = 1 or small enough; all must match the fp32 reference."""
+    from ddp_amd.ops.layers import conv_backward
+    N, Cin, H, W, K, R, stride, pad = case
+    conv, spec, x, xn = _conv_setup(N, Cin, H, W, K, R, stride, pad)
+    P = (H + 2 * pad - R) // stride + 1
+    dz = bf(torch.randn(N, K, P, P, device=DEV))
+    dzn = dz.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    dw = torch.zeros_like(conv.weight, memory_format=torch.channels_last)
+    native_ext.conv_pair_mode(mode)
+    try:
+        dx = conv_backward(spec, xn, dzn, dw, True)
+        torch.cuda.synchronize()
+    finally:
+        native_ext.conv_pair_mode(3)
+    xr = x.clone().requires_grad_(True)
+    wr = conv.weight.detach().clone().requires_grad_(True)
+    F.conv2d(xr, wr, None, stride, pad).backward(dz)
+    assert rel_err(dx.permute(0, 3, 1, 2), xr.grad) < 1e-2
+    assert rel_err(dw, wr.grad) < 1e-2
+
+
 @pytest.mark.parametrize("fmt", [torch.contiguous_format, torch.channels_last])
 def test_conv_wgrad_padded_layer0(native_ext, fmt):
     from ddp_amd.ops.layers import conv_backward
