@@ -46,9 +46,13 @@ class Bottleneck(nn.Module):
             ds = None
             if self.downsample is not None:
                 ds = ConvBNActSpec(self.downsample[0], self.downsample[1], relu=False)
-            self._specs = (ConvBNActSpec(self.conv1, self.bn1, relu=True),
-                           ConvBNActSpec(self.conv2, self.bn2, relu=True),
-                           ConvBNActSpec(self.conv3, self.bn3, relu=True, residual=True), ds)
+            s1 = ConvBNActSpec(self.conv1, self.bn1, relu=True)
+            s2 = ConvBNActSpec(self.conv2, self.bn2, relu=True)
+            s3 = ConvBNActSpec(self.conv3, self.bn3, relu=True, residual=True)
+            # conv2's / conv3's dgrad produce the gradient at bn1's / bn2's output: their
+            # epilogues accumulate those BatchNorms' backward sums (ops/layers.py BnBwdFuse)
+            s2.prev, s3.prev = s1, s2
+            self._specs = (s1, s2, s3, ds)
         return self._specs
 
     def forward_fused(self, h):

@@ -141,14 +141,23 @@ class GradLink:
 
 
 BN_BWD_FUSE_MAX_HW = int(os.environ.get("DDP_AMD_BN_BWD_FUSE_MAX_HW", "16"))
+# preceding block without a max-pool (ResNet's conv1 -> conv2 -> conv3 chain): one z load per
+# dgrad output element in the epilogue would replace a whole dy + z pass of the reduce kernel,
+# but measured on ResNet-50 b256 the BNF epilogue makes the big dgrad GEMMs slower than the pass
+# it saves (30.65 vs 28.23 ms/step, profiles/r2_resnet50_b256.md) -> opt-in (=1)
+BN_BWD_FUSE_NOPOOL = os.environ.get("DDP_AMD_BN_BWD_FUSE_NOPOOL", "0") == "1"
 
 
-def bn_bwd_fuse_pays(H, W):
+def bn_bwd_fuse_pays(H, W, pool=True):
     """Fuse the preceding block's BatchNorm-backward sums into this dgrad only when the dgrad
     output is spatially small (H*W <= 16: VGG's 4x4 / 2x2 layers). Measured (VGG-11 b256 and
     b32, tools/conv_tune.py and the step profiles): there the fused epilogue costs 2-5 us less
     than the reduce kernel it replaces; on 16x16 / 8x8 outputs its z gather (4 loads per pooled
-    pixel, exposed after the MFMA loop) costs 10-15 us MORE than the streaming reduce kernel."""
+    pixel, exposed after the MFMA loop) costs 10-15 us MORE than the streaming reduce kernel.
+    Without a pool (one z load per element): only with DDP_AMD_BN_BWD_FUSE_NOPOOL=1 (measured
+    slower on ResNet-50, profiles/r2_resnet50_b256.md)."""
+    if not pool:
+        return BN_BWD_FUSE_NOPOOL
     return H * W <= BN_BWD_FUSE_MAX_HW
 
 
@@ -260,7 +269,7 @@ class _ConvBNActFn(torch.autograd.Function):
         if (_common.BN_BWD_FUSE and prev is not None and ctx.prev_z is not None
                 and ctx.needs_input_grad[0] and ctx.in_link is None and spec.stride == 1
                 and not prev.residual and prev.K == spec.C and spec.C == spec.Cr
-                and bn_bwd_fuse_pays(x.shape[1], x.shape[2])):
+                and bn_bwd_fuse_pays(x.shape[1], x.shape[2], prev.pool)):
             pz = ctx.prev_z
             bnf = (ptr(pz), ptr(prev.coef), ptr(prev.sums), int(prev.pool), int(prev.relu),
                    pz.shape[1], pz.shape[2])
