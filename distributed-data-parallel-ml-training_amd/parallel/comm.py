@@ -135,6 +135,9 @@ class TorchCommunicator:
         pass
 
 
+_UID_SEQ = 0
+
+
 class RcclCommunicator:
     """Native RCCL communicator (one GPU per process, collectives over xGMI)."""
 
@@ -153,6 +156,11 @@ class RcclCommunicator:
         n = native()
         uid = b""
         if self.world > 1:
+            # every communicator gets its own store key (construction order is the same on every
+            # rank), so a second communicator never reads a stale uid of an earlier one
+            global _UID_SEQ
+            _UID_SEQ += 1
+            key = f"{key}/{_UID_SEQ}"
             store = _store()
             if self.rank == 0:
                 uid = n.make_unique_id()

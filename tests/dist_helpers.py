@@ -310,3 +310,37 @@ def zero_worker(rank, world, port, q, steps):
         import traceback
         q.put((rank, {"error": traceback.format_exc()}))
         raise
+
+
+def uid_bootstrap_worker(rank, world, port, q):
+    """RcclCommunicator's ncclUniqueId exchange over the c10d TCPStore with a stand-in native
+    module (no GPU): rank 0 creates each uid, every rank constructs its communicator from it."""
+    try:
+        _init(rank, world, port)
+        import os as _os
+        import torch.distributed as dist
+        from ddp_amd.ops import common
+        from ddp_amd.parallel import comm as cm
+
+        class FakeComm:
+            def __init__(self, r, w, uid, dev):
+                self.uid, self.live = bytes(uid), True
+
+        class FakeNative:
+            RcclComm = FakeComm
+
+            @staticmethod
+            def make_unique_id():
+                return _os.urandom(128)
+
+        common._NATIVE = FakeNative()
+        a = cm.RcclCommunicator(rank, world, 0)
+        b = cm.RcclCommunicator(rank, world, 0, key="ddp_amd/rccl_uid_overlap")
+        c = cm.RcclCommunicator(rank, world, 0)
+        out = {"uids": [x.comm.uid.hex() for x in (a, b, c)], "live": a.live and c.live}
+        dist.destroy_process_group()
+        q.put((rank, out))
+    except Exception:
+        import traceback
+        q.put((rank, {"error": traceback.format_exc()}))
+        raise

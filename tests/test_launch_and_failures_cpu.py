@@ -115,3 +115,17 @@ def test_healthy_run_is_not_killed_by_the_watchdog():
     for rc, out, err, _ in res:
         assert rc == 0, err[-2000:]
         assert "Test set:" in out
+
+
+def test_rccl_uid_bootstrap_over_the_store():
+    """Three ranks, three communicators each (two with the default key): every rank builds each
+    communicator from the SAME uid published by rank 0, and no two communicators share one."""
+    from dist_helpers import run_workers, uid_bootstrap_worker
+    out = run_workers(uid_bootstrap_worker, 3)
+    for r, v in out.items():
+        assert "error" not in v, v.get("error")
+        assert v["live"]
+    u0 = out[0]["uids"]
+    assert len(set(u0)) == 3
+    for r in (1, 2):
+        assert out[r]["uids"] == u0
