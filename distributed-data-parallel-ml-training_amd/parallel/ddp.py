@@ -11,20 +11,19 @@ Reference parity: ``torch.nn.parallel.DistributedDataParallel(model)`` with defa
 MI355X design:
 * gradients live in one flat fp32 arena (optim/arena.py); a bucket is a slice of it in reverse
   parameter order, so buckets are all-reduced in place with no pack/unpack copies;
-* GPU: the native C++ ``Reducer`` (csrc/runtime/comm.cpp) launches ncclAllReduce(avg) for each
-  full bucket as soon as the fused backward kernels announce its last gradient
-  (ops.common.grad_ready). By default the collective is issued INLINE on the backward stream:
-  on MI355X / ROCm 7 a second (comm) stream makes every cross-queue edge of the step expensive
-  (measured 2.3x slower captured steps, see ``overlap`` below), so the step — forward,
-  backward, bucket all-reduces, optimizer — is one single-stream hipGraph (engine/step.py).
-  ``overlap=True`` keeps the classic design (high-priority comm stream gated by events, a final
-  autograd callback makes the compute stream wait on every bucket).
-* CPU/Gloo: the same bucket plan driven from post-accumulate-grad hooks with async all-reduce.
-* Bucket sizing for xGMI: each MI355X has 7 point-to-point links; a ring all-reduce moves
-  2(w-1)/w of the bucket over one link per hop, so buckets must be large enough (>= a few MiB)
-  for the per-link bandwidth to dominate the per-collective latency, but small enough that the
-  first bucket (the big 512x512 conv gradients, ready first) starts early. Defaults: 25 MiB
-  (reference) with a 1 MiB first bucket; ``bucket_cap_mb`` is tunable.
+* GPU: the native C++ ``Reducer`` (csrc/runtime/comm.cpp) over the host-only
+  ``BucketScheduler`` (csrc/runtime/buckets.cpp; Python twin below) launches ncclAllReduce(avg)
+  for each full bucket as soon as the fused backward kernels announce its last gradient
+  (ops.common.grad_ready). EAGER backward passes issue it on a high-priority comm stream
+  (event-gated), overlapped with the rest of the backward like torch DDP; a backward being
+  CAPTURED into a hipGraph issues it inline on its own stream (a comm branch open across a
+  captured backward runs 2.4x slower on ROCm 7, profiles/r1_comm_stream_study.md) — the captured
+  multi-GPU step overlaps through engine/step.py SegmentedDDPStep instead;
+* after iteration 0 the launch order is rebuilt from the observed gradient-ready order (torch
+  DDP's bucket rebuild; buckets stay contiguous arena slices), broadcast from rank 0;
+* CPU/Gloo: the same scheduler driven from post-accumulate-grad hooks with async all-reduce;
+* bucket sizing for xGMI: 25 MiB + 1 MiB first by default (the reference's), or
+  ``bucket_cap_mb="auto"``: from the all-reduce bus-bandwidth table (parallel/bucket_plan.py).
 """
 import contextlib
 import os
