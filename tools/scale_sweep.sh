@@ -1,8 +1,8 @@
 #!/bin/bash
 # Scaling report on ONE node with >= 8 MI355X (not runnable on a 1-GPU box): every strategy
 # (part3 DDP, part2b all_reduce, part2a gather/scatter and gather/broadcast) at 1/2/4/8 GPUs,
-# weak scaling (256 images per GPU, the bench default) and the reference's strong-scaling
-# protocol (global batch 256 split int(256/N) per GPU). One JSON line per run in
+# the reference's strong-scaling protocol (global batch 256 split int(256/N) per GPU, the bench
+# default) and weak scaling (--per-gpu-batch 256). One JSON line per run in
 # gpurun_out/scale_sweep.jsonl; summarise with python tools/scale_report.py.
 #   bash tools/scale_sweep.sh [max_gpus]
 cd "$(dirname "$0")/.." || exit 2
@@ -13,8 +13,8 @@ out=gpurun_out/scale_sweep.jsonl
 max=${1:-8}
 port=29600
 for strat in ddp allreduce gather_scatter gather_broadcast; do
-  for mode in weak strong; do
-    extra=""; [ $mode = strong ] && extra="--global-batch 256"
+  for mode in strong weak; do
+    extra=""; [ $mode = weak ] && extra="--per-gpu-batch 256"
     for n in 1 2 4 8; do
       [ $n -gt "$max" ] && continue
       port=$((port + 1))
