@@ -31,7 +31,9 @@ def load():
     if _module is not None:
         return _module
     import torch  # noqa: F401  (load torch's HIP runtime first)
-    path = so_path()
+    # DDP_AMD_NATIVE_PATH: load another build of the same extension (A/B of kernel variants in
+    # one GPU session, tools/ab_variants.sh); the in-tree build is the default
+    path = os.environ.get("DDP_AMD_NATIVE_PATH") or so_path()
     if not os.path.exists(path):
         raise RuntimeError(
             f"ddp_amd native extension not built ({path} missing). "

@@ -81,7 +81,7 @@ struct ConvArgs {
   int pa, pb, Hp, Wp, r0, s0, Rt, St, qa, qb;
   int accumulate;            // DGRAD: dx = bf16(dx + result) (merges a second gradient branch)
   int a_bytes, b_bytes;      // operand sizes: buffer-resource bounds (reads past them give 0)
-  FastDiv dPQ, dQ;           // WGRAD pixel decomposition
+  FastDiv dPQ, dQ;           // row -> pixel: FWD / WGRAD P*Q, Q; DGRAD H*W, W (phase: Hp*Wp, Wp)
   int has_bnf;               // DGRAD (stride 1, no accumulate): accumulate the preceding
   BnBwdFuse bnf;             //   block's BatchNorm-backward sums in the epilogue (api.h)
   // split-K "ticket" fixup (FWD/DGRAD, small problems): every split adds its partial tile into
@@ -114,24 +114,25 @@ __device__ __forceinline__ RowInfo row_info(const ConvArgs& A, int row) {
   const ConvGeom& g = A.g;
   RowInfo ri{0, -(1 << 24), 0};
   if (row >= A.Mg) return ri;
+  // A.dPQ / A.dQ divide by the row image size / width of the mode (prepare_cfg)
   if (MODE == MODE_FWD) {
     const int pq = g.P * g.Q;
-    const int n = row / pq, rem = row - n * pq;
-    const int p = rem / g.Q, q = rem - p * g.Q;
+    const int n = fast_div(row, A.dPQ), rem = row - n * pq;
+    const int p = fast_div(rem, A.dQ), q = rem - p * g.Q;
     ri.base = n * g.H * g.W * g.C;
     ri.h0 = p * g.stride - g.pad;
     ri.w0 = q * g.stride - g.pad;
   } else if (A.phase) {
     const int hw = A.Hp * A.Wp;
-    const int n = row / hw, rem = row - n * hw;
-    const int i = rem / A.Wp, j = rem - i * A.Wp;
+    const int n = fast_div(row, A.dPQ), rem = row - n * hw;
+    const int i = fast_div(rem, A.dQ), j = rem - i * A.Wp;
     ri.base = n * g.P * g.Q * g.K;
     ri.h0 = i + A.qa;
     ri.w0 = j + A.qb;
   } else {
     const int hw = g.H * g.W;
-    const int n = row / hw, rem = row - n * hw;
-    const int h = rem / g.W, w = rem - h * g.W;
+    const int n = fast_div(row, A.dPQ), rem = row - n * hw;
+    const int h = fast_div(rem, A.dQ), w = rem - h * g.W;
     ri.base = n * g.P * g.Q * g.K;
     ri.h0 = h + g.pad;
     ri.w0 = w + g.pad;
@@ -184,6 +185,17 @@ __device__ __forceinline__ void dma_buf(__amdgpu_buffer_rsrc_t rs, int byte_off,
 template <int N>
 __device__ __forceinline__ void wait_dma_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+// Sum over the 16 lanes of a DPP row (lanes 16r..16r+15), result in every lane of the row:
+// quad_perm [1,0,3,2] and [2,3,0,1], then row_half_mirror and row_mirror — four DPP adds
+// instead of four ds_bpermute round trips through the LDS unit (__shfl_xor).
+__device__ __forceinline__ float dpp_sum16(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
+  return v;
 }
 
 // BNF (DGRAD only): the epilogue also accumulates the preceding block's BatchNorm-backward sums
@@ -500,6 +512,89 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
                    (MODE == MODE_DGRAD && BNF && !split);
   // the LDS operand ring is reused for the statistics hand-off: every wave must be done with it
   if (red) __syncthreads();
+  // (not for 64x64 tiles: measured slower there — the VGG-11 forward convs, whose long
+  // reductions hide the epilogue anyway — the generic path below keeps their codegen)
+  if (MODE != MODE_WGRAD && !BNF && !(BM == 64 && BN == 64) && !split &&
+      !(MODE == MODE_DGRAD && args.accumulate)) {
+    // Plain bf16 output (FWD, DGRAD overwriting dx). Short-reduction GEMMs (1x1 convs over
+    // 64-128 channels: 1-2 k-steps) spend most of their VALU issue in the epilogue and the
+    // gather setup, so: one row offset per (lane, i) computed up front (column groups are
+    // immediate offsets), DPP row sums, and the statistics hand-off through LDS for both wave
+    // rows, so no per-column sums stay live across the tile.
+    const int cbase = col0 + wn * WTN + cq;
+    const bool has_bias = MODE == MODE_FWD && args.bias != nullptr;
+    int ro[TM];  // element offset of the lane's output row + cbase, -1 past Mg
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = row0 + wm * WTM + i * 16 + rl;
+      int orow = row;
+      if (phase) {  // phase-local row -> input pixel
+        const int hw = args.Hp * args.Wp;  // dPQ / dQ = Hp*Wp / Wp for a phase GEMM
+        const int n = fast_div(row, args.dPQ), rem = row - n * hw;
+        const int pi = fast_div(rem, args.dQ), pj = rem - pi * args.Wp;
+        orow = (n * g.H + args.pa + g.stride * pi) * g.W + args.pb + g.stride * pj;
+      }
+      ro[i] = row < args.Mg ? orow * args.Ng + cbase : -1;
+    }
+    float* sl = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if (cbase + j * 16 >= args.Ng) continue;  // uniform over each 16-lane DPP row
+      float4 bj = {0.f, 0.f, 0.f, 0.f};
+      if (has_bias) bj = *reinterpret_cast<const float4*>(args.bias + cbase + j * 16);
+      float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        if (ro[i] < 0) continue;
+        const f32x4 v = acc[i][j];
+        uint2 pk;
+        pk.x = (unsigned)f2bf(v[0] + bj.x) | ((unsigned)f2bf(v[1] + bj.y) << 16);
+        pk.y = (unsigned)f2bf(v[2] + bj.z) | ((unsigned)f2bf(v[3] + bj.w) << 16);
+        *reinterpret_cast<uint2*>(args.out + ro[i] + j * 16) = pk;
+        if (red) {  // statistics of the stored (bf16-rounded) values
+          const float r0 = __uint_as_float(pk.x << 16), r1 = __uint_as_float(pk.x & 0xffff0000u);
+          const float r2 = __uint_as_float(pk.y << 16), r3 = __uint_as_float(pk.y & 0xffff0000u);
+          s[0] += r0; s[1] += r1; s[2] += r2; s[3] += r3;
+          ss[0] += r0 * r0; ss[1] += r1 * r1; ss[2] += r2 * r2; ss[3] += r3 * r3;
+        }
+      }
+      if (red) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          s[t] = dpp_sum16(s[t]);
+          ss[t] = dpp_sum16(ss[t]);
+        }
+        // LDS slot [wm][wn][j][lane>>4][8]
+        float* slot = sl + ((((wm * 2 + wn) * TN + j) * 4 + (lane >> 4)) * 8);
+        if (rl == 0) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            slot[t] = s[t];
+            slot[4 + t] = ss[t];
+          }
+        }
+      }
+    }
+    if (red) {
+      __syncthreads();
+      if (wm == 0 && rl == 0) {
+        float* st = args.stats + (bid % kStatRep) * 2 * args.Ng;  // spread contention
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = cbase + j * 16;
+          if (col >= args.Ng) continue;
+          const float* s0 = sl + (((wn * TN + j) * 4 + (lane >> 4)) * 8);
+          const float* s1 = sl + ((((2 + wn) * TN + j) * 4 + (lane >> 4)) * 8);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            atomicAdd(st + col + t, s0[t] + s1[t]);
+            atomicAdd(st + args.Ng + col + t, s0[4 + t] + s1[4 + t]);
+          }
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = col0 + wn * WTN + j * 16 + cq;
@@ -558,8 +653,8 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
         size_t orow = row;
         if (phase) {  // phase-local row -> input pixel
           const int hw = args.Hp * args.Wp;
-          const int n = row / hw, rem = row - n * hw;
-          const int i = rem / args.Wp, j = rem - i * args.Wp;
+          const int n = fast_div(row, args.dPQ), rem = row - n * hw;
+          const int i = fast_div(rem, args.dQ), j = rem - i * args.Wp;
           orow = ((size_t)n * gg.H + args.pa + gg.stride * i) * gg.W + args.pb + gg.stride * j;
         }
         if (MODE == MODE_DGRAD && args.accumulate) {  // dx += (second gradient branch)
@@ -587,8 +682,8 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
           const float fmu[4] = {bmu.x, bmu.y, bmu.z, bmu.w}, fis[4] = {bis.x, bis.y, bis.z, bis.w};
           const BnBwdFuse& f = args.bnf;
           const int hw = g.H * g.W;
-          const int n = (int)orow / hw, rem = (int)orow - n * hw;
-          const int h = rem / g.W, w = rem - h * g.W;
+          const int n = fast_div((int)orow, args.dPQ), rem = (int)orow - n * hw;  // H*W, W
+          const int h = fast_div(rem, args.dQ), w = rem - h * g.W;
           const int np = f.pool ? 4 : 1;
           float zf[4][4];
 #pragma unroll
@@ -623,11 +718,8 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
       // reduce over the 16 rows held by lanes (lane & 15) of each 16-lane group
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-#pragma unroll
-        for (int m = 1; m < 16; m <<= 1) {
-          s[t] += __shfl_xor(s[t], m, kWave);
-          ss[t] += __shfl_xor(ss[t], m, kWave);
-        }
+        s[t] = dpp_sum16(s[t]);
+        ss[t] = dpp_sum16(ss[t]);
       }
       // wave row 1 parks its column sums in LDS slot [wn][j][lane>>4][8]; row 0 adds them
       float* slot = reinterpret_cast<float*>(smem) + (((wn * TN + j) * 4 + (lane >> 4)) * 8);
@@ -745,13 +837,17 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
     } else {
       epilogue(row0, col0, zsplit, args.splits > 1);
     }
-    wait_dma_barrier<0>();  // all reads of the ring done before the next item's prologue DMA
+    // all reads of the ring done before the next item's prologue DMA. Not after the last item:
+    // vmcnt also counts the epilogue's stores, and waiting for their acknowledgement would hold
+    // the workgroup slot (and its registers) for a full memory round trip after the last MFMA
+    if (item + nblk < nitems) wait_dma_barrier<0>();
   }
 }
 
 template <int MODE, int BM, int BN, int NST, bool BNF = false>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
-  __shared__ __attribute__((aligned(16))) unsigned short smem[ConvSmem<BM, BN, NST>::elems];
+  // dynamic: the launcher sizes the ring to the stages a work item can use (launch_gemm_t)
+  extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
   conv_igemm_body<MODE, BM, BN, NST, BNF>(args, smem, blockIdx.x, gridDim.x);
 }
 
@@ -1100,16 +1196,32 @@ static int stages_for(int BM, int BN) {
 
 template <int MODE, int BM, int BN, int NST, bool BNF>
 static void launch_gemm_t(const ConvArgs& a, int items, hipStream_t st) {
+  constexpr int kStageBytes = (BM + BN) * 64 * 2;
+  // A work item of k k-steps touches min(NST, k) ring stages (the prologue issues k-steps
+  // 0..NST-2, the loop refills the stage freed by the previous k-step only while k-steps
+  // remain). Short reductions — the 1x1 convs over 64/128 channels, 1-2 k-steps — thus need a
+  // fraction of the ring, and the smaller LDS footprint doubles the resident workgroups per CU
+  // (their tiles are latency-bound: DMA in, a few MFMAs, stores out).
+  const int stages = std::max(1, std::min(NST, a.ksteps_per_split));
+  const size_t lds = (size_t)stages * kStageBytes;
+  static bool attr = false;
+  if (!attr) {
+    // an error here surfaces through the caller's hipGetLastError
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_igemm_kernel<MODE, BM, BN, NST, BNF>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, NST * kStageBytes);
+    attr = true;
+  }
   // persistent grid: at most the resident workgroup slots (queried once per instantiation)
   static int resident = 0;
   if (resident == 0) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, conv_igemm_kernel<MODE, BM, BN, NST, BNF>, 256, 0) != hipSuccess || nb < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, conv_igemm_kernel<MODE, BM, BN, NST, BNF>, 256,
+                                                     NST * kStageBytes) != hipSuccess || nb < 1)
       nb = 1;
     resident = nb;
   }
   const int grid = g_persistent ? std::min(items, kNumCUs * resident) : items;
-  hipLaunchKernelGGL((conv_igemm_kernel<MODE, BM, BN, NST, BNF>), dim3(grid), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((conv_igemm_kernel<MODE, BM, BN, NST, BNF>), dim3(grid), dim3(256), lds, st, a);
 }
 
 template <int MODE, int BM, int BN, int NST>
@@ -1134,6 +1246,14 @@ static int prepare_cfg(ConvArgs& a, int splits) {
   splits = (ksteps + per - 1) / per;
   a.splits = splits;
   a.ksteps_per_split = per;
+  if (MODE == MODE_DGRAD) {
+    const int hh = a.phase ? a.Hp : a.g.H, ww = a.phase ? a.Wp : a.g.W;
+    a.dPQ = make_fastdiv(std::max(1, hh * ww));
+    a.dQ = make_fastdiv(std::max(1, ww));
+  } else {
+    a.dPQ = make_fastdiv(std::max(1, a.g.P * a.g.Q));
+    a.dQ = make_fastdiv(std::max(1, a.g.Q));
+  }
   // same-address fp32 atomics serialise: beyond kMaxAtomicSplits partial sums per element the
   // slab + grouped-finish reduction is cheaper
   const size_t atomic_bytes = 4ull * (size_t)splits * a.Mg * a.Ng;
@@ -1343,7 +1463,8 @@ extern "C" int ddp_conv_fwd(const ConvGeom* g, const void* x, const void* wc, co
   a.Kg = g->R * g->S * g->C;
   a.splits = splits;
   const size_t xa = (size_t)g->N * g->H * g->W * g->C, wb = (size_t)a.Ng * a.Kg;
-  if (!fits_buffer(xa) || !fits_buffer(wb)) return -2;
+  // (the output too: the epilogue addresses it with 32-bit element offsets)
+  if (!fits_buffer(xa) || !fits_buffer(wb) || !fits_buffer((size_t)a.Mg * a.Ng)) return -2;
   a.a_bytes = (int)(2 * xa);
   a.b_bytes = (int)(2 * wb);
   launch_mode<MODE_FWD>(a, ws_elems, st);
@@ -1370,7 +1491,8 @@ static int conv_dgrad_impl(const ConvGeom* g, const void* dy, const void* wc, vo
   a.splits = splits;
   // B = the forward weight copy Wc [K][R][S][C] (read k-major, see BKM in the kernel)
   const size_t dya = (size_t)g->N * g->P * g->Q * g->K, wb = (size_t)g->K * g->R * g->S * g->C;
-  if (!fits_buffer(dya) || !fits_buffer(wb)) return -2;
+  if (!fits_buffer(dya) || !fits_buffer(wb) || !fits_buffer((size_t)g->N * g->H * g->W * g->C))
+    return -2;
   a.a_bytes = (int)(2 * dya);
   a.b_bytes = (int)(2 * wb);
   if (g->stride == 1) {
