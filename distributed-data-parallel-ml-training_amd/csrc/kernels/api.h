@@ -113,6 +113,8 @@ int ddp_conv_fwd_smallk(const ddp_amd::ConvGeom* g, const void* x, const void* w
                         const float* bias, void* y, float* stats, hipStream_t st);
 void ddp_conv_options(int wgrad_atomic, int persistent, int stages);
 void ddp_conv_pair_mode(int mode, int items);
+// sweeps (tools/conv_tune.py --pairs): force the paired launch with these split-K factors (0 = off)
+void ddp_conv_pair_force(int splits_dg, int splits_wg);
 int ddp_conv_bwd_pair(const ddp_amd::ConvGeom* g, const void* dy, const void* wc, void* dx,
                       const void* x, float* dw, float* ws, size_t ws_elems,
                       const ddp_amd::BnBwdFuse* bn, hipStream_t st);

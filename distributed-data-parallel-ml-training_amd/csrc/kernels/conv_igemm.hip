@@ -1362,6 +1362,10 @@ struct TuneVal {
   int tile, splits, stages;
 };
 static std::map<TuneKey, TuneVal> g_tuned;  // -> (tile index, splits, LDS stages)
+// Backward-pair entries (table mode 3), keyed by the layer's DGRAD problem: tile = 1 pair with
+// splits (DGRAD) / stages (= WGRAD splits), tile = 0 the separate launches measured faster
+static std::map<TuneKey, TuneVal> g_pair_tuned;
+static int g_pair_force_dg = 0, g_pair_force_wg = 0;  // sweeps: forced pair splits (0 = off)
 static int g_force_tile = 0;                // 1..4 = tile index + 1
 static int g_force_stages = 0;              // 2..4 (sweeps), 0 = policy
 
@@ -1437,10 +1441,21 @@ extern "C" void ddp_conv_fixup(float* facc, size_t facc_elems, unsigned* tickets
 
 // tile: index into the launch_mode table (0..kNumTiles-1)
 extern "C" void ddp_conv_tune_set(int mode, int M, int N, int K, int tile, int splits, int stages) {
+  if (mode == 3) {  // backward pair: tile = pair on/off, splits / stages = DGRAD / WGRAD splits
+    g_pair_tuned[TuneKey{MODE_DGRAD, M, N, K}] = {tile ? 1 : 0, std::max(1, splits), std::max(1, stages)};
+    return;
+  }
   if (tile < 0 || tile >= kNumTiles) return;
   g_tuned[TuneKey{mode, M, N, K}] = {tile, std::max(1, splits), stages};
 }
-extern "C" void ddp_conv_tune_clear() { g_tuned.clear(); }
+extern "C" void ddp_conv_tune_clear() {
+  g_tuned.clear();
+  g_pair_tuned.clear();
+}
+extern "C" void ddp_conv_pair_force(int splits_dg, int splits_wg) {
+  g_pair_force_dg = splits_dg;
+  g_pair_force_wg = splits_wg;
+}
 extern "C" void ddp_conv_force_tile(int tile_plus_one, int stages) {
   g_force_tile = tile_plus_one;
   g_force_stages = stages;
@@ -1633,17 +1648,37 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
   w.b_bytes = (int)(2 * xb);
   w.dPQ = make_fastdiv(g->P * g->Q);
   w.dQ = make_fastdiv(g->Q);
-  int spd[kNumTiles], bd, nd, spw[kNumTiles], bw, nw;
-  plan_mode<MODE_DGRAD>(d, ws_elems, &bd, spd, &nd);
-  plan_mode<MODE_WGRAD>(w, ws_elems, &bw, spw, &nw);
-  const bool both64 = bd == 3 && bw == 3;
-  if (g_pair_mode == 1 && !both64) return separate();
-  int sd = spd[3], sw = spw[3];
-  if (bd != 3) tile_cost(64, 64, d, ws_elems, &sd);
-  if (bw != 3) tile_cost(64, 64, w, ws_elems, &sw);
-  if (bd == 3 && bw == 3 && g_force_tile == 0) {  // measured splits (plan_mode filled sp[3])
+  // measured pair entry (tools/conv_tune.py --pairs) or forced splits (its sweep) first
+  bool tuned = false;
+  int sd = 1, sw = 1;
+  if (g_pair_force_dg > 0 && g_pair_force_wg > 0) {
+    tuned = true;
+    sd = g_pair_force_dg;
+    sw = g_pair_force_wg;
+  } else if (g_force_tile == 0 && g_pair_mode == 3) {
+    auto it = g_pair_tuned.find(TuneKey{MODE_DGRAD, d.Mg, d.Ng, d.Kg});
+    if (it != g_pair_tuned.end()) {
+      if (!it->second.tile) return separate();
+      tuned = true;
+      sd = it->second.splits;
+      sw = it->second.stages;
+    }
+  }
+  bool both64 = tuned;
+  if (!tuned) {
+    int spd[kNumTiles], bd, nd, spw[kNumTiles], bw, nw;
+    plan_mode<MODE_DGRAD>(d, ws_elems, &bd, spd, &nd);
+    plan_mode<MODE_WGRAD>(w, ws_elems, &bw, spw, &nw);
+    both64 = bd == 3 && bw == 3;
+    if (g_pair_mode == 1 && !both64) return separate();
     sd = spd[3];
     sw = spw[3];
+    if (bd != 3) tile_cost(64, 64, d, ws_elems, &sd);
+    if (bw != 3) tile_cost(64, 64, w, ws_elems, &sw);
+    if (bd == 3 && bw == 3 && g_force_tile == 0) {  // measured splits (plan_mode filled sp[3])
+      sd = spd[3];
+      sw = spw[3];
+    }
   }
   // the slab workspace is split between the two problems
   const int itd = prepare_cfg<MODE_DGRAD, 64, 64>(d, std::max(1, sd));

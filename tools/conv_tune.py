@@ -49,7 +49,12 @@ def main():
     ap.add_argument("--quick", action="store_true", help="VGG-11 b256 only")
     ap.add_argument("--sets", default="all", choices=["all", "resnet256"])
     ap.add_argument("--merge", default=None, help="existing table to extend (entries kept)")
+    ap.add_argument("--pairs", action="store_true",
+                    help="tune the backward pair launch (DGRAD+WGRAD split-K factors, or separate "
+                         "launches) of the VGG-11 layers at batch 32/64/128/256 instead")
     args = ap.parse_args()
+    if args.pairs:
+        return tune_pairs(args)
     import torch
     import ddp_amd  # noqa: F401
     from ddp_amd.ops import common
@@ -169,6 +174,109 @@ def main():
         json.dump({"device": torch.cuda.get_device_name(0), "reps": args.reps,
                    "entries": entries}, f, indent=1)
     print(f"wrote {len(entries)} entries to {out}; summed per-op saving {saved_total:.1f} us")
+
+
+def tune_pairs(args):
+    """Backward pair (ddp_conv_bwd_pair): for every stride-1 VGG-11 layer with a DGRAD, time the
+    two separate launches, the policy's pair, and the forced pair over a grid of (DGRAD, WGRAD)
+    split-K factors; record the winner as a mode-3 entry keyed by the DGRAD problem
+    (tile = 1 pair with splits / stages = DGRAD / WGRAD splits, tile = 0 separate)."""
+    import torch
+    import ddp_amd  # noqa: F401
+    from ddp_amd.ops import common
+    from ddp_amd.ops.common import native, ptr, workspace, TUNING_FILE
+    from ddp_amd.ops.layers import ConvBNActSpec, bn_bwd_fuse_pays
+    from conv_bench import vgg_layers
+
+    n = native()
+    dev = torch.device("cuda", 0)
+    ws = workspace(dev)
+    st = torch.cuda.current_stream().cuda_stream
+    pair_mode = int(os.environ.get("DDP_AMD_BWD_PAIR", "3"))
+
+    def timeit(fn):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1000.0 / args.reps
+
+    entries, saved = [], 0.0
+    for B in (32, 64, 128, 256):
+        prev_hw = None
+        for (N, C, H, W, K, R, stride, pad, Cr) in vgg_layers(B):
+            bn = None
+            if prev_hw is not None and C == Cr and bn_bwd_fuse_pays(H, W):
+                pz = torch.randn(N, prev_hw, prev_hw, C, device=dev).to(torch.bfloat16)
+                pcoef = torch.rand(6 * C, device=dev)
+                psums = torch.zeros(16 * 2 * C, device=dev)
+                _keep = (pz, pcoef, psums)  # noqa: F841
+                bn = (ptr(pz), ptr(pcoef), ptr(psums), int(prev_hw != H), 1, prev_hw, prev_hw)
+            prev_hw = H
+            if C != Cr or stride != 1:
+                continue
+            conv = torch.nn.Conv2d(Cr, K, R, stride, pad, bias=False).to(dev)
+            conv.weight.data = conv.weight.data.contiguous(memory_format=torch.channels_last)
+            spec = ConvBNActSpec(conv, None)
+            spec.maybe_pack()
+            x = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
+            dy = torch.randn(N, H, W, K, device=dev).to(torch.bfloat16)
+            dx = torch.empty_like(x)
+            dw = torch.zeros_like(conv.weight)
+            gw = spec.geom(N, H, W, common.weight_krsc(dw))
+
+            def call():
+                n.conv_bwd_pair(gw, ptr(dy), ptr(spec.wc), ptr(dx), ptr(x), ptr(dw), ptr(ws),
+                                ws.numel(), st, bn=bn)
+            Md, Nd, Kd = N * H * W, C, R * R * K
+            Mw, Nw, Kw = K, R * R * C, N * H * W
+            n.conv_pair_force(0, 0)
+            n.conv_pair_mode(0, 0)
+            sep = timeit(call)
+            n.conv_pair_mode(pair_mode, 0)
+            pol = timeit(call)
+            best = (sep, 0, 1, 1)
+            kd, kw = (Kd + 63) // 64, (Kw + 63) // 64
+            for sd in (1, 2, 3, 4, 6, 8, 12, 16):
+                if sd > 1 and kd // sd < 2:
+                    continue
+                for sw in (1, 2, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128):
+                    if sw > 1 and kw // sw < 2:
+                        continue
+                    need = (sd * Md * Nd if sd > 1 else 0) + (sw * Mw * Nw if sw > 1 else 0) + 64
+                    if need > ws.numel():
+                        continue
+                    n.conv_pair_force(sd, sw)
+                    us = timeit(call)
+                    if us < best[0] * 0.99:
+                        best = (us, 1, sd, sw)
+            n.conv_pair_force(0, 0)
+            us, on, sd, sw = best
+            ref = min(sep, pol)
+            saved += ref - us
+            label = f"vgg11 N{N} {Cr}->{K} {H}x{W} k{R}"
+            print(f"{label:32s} separate {sep:6.1f}  policy {pol:6.1f}  -> "
+                  f"{'pair' if on else 'separate'} dg {sd:2d} wg {sw:3d} {us:6.1f} us", flush=True)
+            entries.append({"mode": 3, "M": Md, "N": Nd, "K": Kd, "tile": on, "splits": sd,
+                            "stages": sw, "us": round(us, 2), "auto_us": round(pol, 2),
+                            "shape": label + " bwd pair"})
+    src = args.merge or TUNING_FILE
+    old = []
+    if os.path.exists(src):
+        with open(src) as f:
+            old = json.load(f)["entries"]
+    have = {(e["mode"], e["M"], e["N"], e["K"]) for e in entries}
+    entries = [e for e in old if (e["mode"], e["M"], e["N"], e["K"]) not in have] + entries
+    out = args.out or TUNING_FILE
+    with open(out, "w") as f:
+        json.dump({"device": torch.cuda.get_device_name(0), "reps": args.reps,
+                   "entries": entries}, f, indent=1)
+    print(f"wrote {len(entries)} entries to {out}; pair saving vs policy {saved:.1f} us")
 
 
 if __name__ == "__main__":
