@@ -51,7 +51,9 @@ def main():
     ap.add_argument("--merge", default=None, help="existing table to extend (entries kept)")
     ap.add_argument("--pairs", action="store_true",
                     help="tune the backward pair launch (DGRAD+WGRAD split-K factors, or separate "
-                         "launches) of the VGG-11 layers at batch 32/64/128/256 instead")
+                         "launches) of the stride-1 layers instead (--pair-sets)")
+    ap.add_argument("--pair-sets", default="vgg11:32,64,128,256",
+                    help="model:batches[;model:batches], e.g. 'resnet50:256'")
     args = ap.parse_args()
     if args.pairs:
         return tune_pairs(args)
@@ -186,7 +188,7 @@ def tune_pairs(args):
     from ddp_amd.ops import common
     from ddp_amd.ops.common import native, ptr, workspace, TUNING_FILE
     from ddp_amd.ops.layers import ConvBNActSpec, bn_bwd_fuse_pays
-    from conv_bench import vgg_layers
+    from conv_bench import vgg_layers, resnet_layers
 
     n = native()
     dev = torch.device("cuda", 0)
@@ -206,20 +208,29 @@ def tune_pairs(args):
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) * 1000.0 / args.reps
 
-    entries, saved = [], 0.0
-    for B in (32, 64, 128, 256):
+    entries, saved, seen = [], 0.0, set()
+    sets = []
+    for item in args.pair_sets.split(";"):
+        model, bs = item.split(":")
+        sets += [(model, int(b)) for b in bs.split(",")]
+    for model, B in sets:
         prev_hw = None
-        for (N, C, H, W, K, R, stride, pad, Cr) in vgg_layers(B):
+        layers = vgg_layers(B) if model == "vgg11" else resnet_layers(B)
+        for (N, C, H, W, K, R, stride, pad, Cr) in layers:
             bn = None
-            if prev_hw is not None and C == Cr and bn_bwd_fuse_pays(H, W):
+            # (VGG: the preceding block's BN-backward sums ride in the dgrad epilogue; ResNet
+            # keeps its separate reduce pass by default, ops/common.py BN_BWD_FUSE_NOPOOL)
+            if (model == "vgg11" and prev_hw is not None and C == Cr
+                    and bn_bwd_fuse_pays(H, W)):
                 pz = torch.randn(N, prev_hw, prev_hw, C, device=dev).to(torch.bfloat16)
                 pcoef = torch.rand(6 * C, device=dev)
                 psums = torch.zeros(16 * 2 * C, device=dev)
                 _keep = (pz, pcoef, psums)  # noqa: F841
                 bn = (ptr(pz), ptr(pcoef), ptr(psums), int(prev_hw != H), 1, prev_hw, prev_hw)
             prev_hw = H
-            if C != Cr or stride != 1:
+            if C != Cr or stride != 1 or (N, C, H, K, R) in seen:
                 continue
+            seen.add((N, C, H, K, R))
             conv = torch.nn.Conv2d(Cr, K, R, stride, pad, bias=False).to(dev)
             conv.weight.data = conv.weight.data.contiguous(memory_format=torch.channels_last)
             spec = ConvBNActSpec(conv, None)
@@ -259,7 +270,7 @@ def tune_pairs(args):
             us, on, sd, sw = best
             ref = min(sep, pol)
             saved += ref - us
-            label = f"vgg11 N{N} {Cr}->{K} {H}x{W} k{R}"
+            label = f"{model} N{N} {Cr}->{K} {H}x{W} k{R}"
             print(f"{label:32s} separate {sep:6.1f}  policy {pol:6.1f}  -> "
                   f"{'pair' if on else 'separate'} dg {sd:2d} wg {sw:3d} {us:6.1f} us", flush=True)
             entries.append({"mode": 3, "M": Md, "N": Nd, "K": Kd, "tile": on, "splits": sd,
