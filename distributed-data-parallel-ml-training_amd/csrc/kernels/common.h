@@ -51,15 +51,36 @@ __device__ __forceinline__ void st8(unsigned short* p, u16x8 v) {
   *reinterpret_cast<u16x8*>(p) = v;
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+// DPP lane exchange within each 16-lane row (ctrl: quad_perm / row_half_mirror / row_mirror)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// Sum over the 16 lanes of a DPP row, result in every lane of the row: quad_perm [1,0,3,2] and
+// [2,3,0,1], row_half_mirror, row_mirror — four DPP adds instead of four ds_bpermute round
+// trips through the LDS unit (__shfl_xor).
+__device__ __forceinline__ float dpp_sum16(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  v += dpp_f<0x140>(v);
   return v;
 }
+__device__ __forceinline__ float lane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+// Full-wave reductions, result in every lane; all 64 lanes must be active (uniform control
+// flow): DPP within the rows, then the four row results through v_readlane.
+__device__ __forceinline__ float wave_sum(float v) {
+  v = dpp_sum16(v);
+  return (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
+}
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
-  return v;
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  v = fmaxf(v, dpp_f<0x140>(v));
+  return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
 }
 
 // Bijective XCD-aware block remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):

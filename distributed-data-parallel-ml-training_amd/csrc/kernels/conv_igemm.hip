@@ -187,17 +187,6 @@ __device__ __forceinline__ void wait_dma_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-// Sum over the 16 lanes of a DPP row (lanes 16r..16r+15), result in every lane of the row:
-// quad_perm [1,0,3,2] and [2,3,0,1], then row_half_mirror and row_mirror — four DPP adds
-// instead of four ds_bpermute round trips through the LDS unit (__shfl_xor).
-__device__ __forceinline__ float dpp_sum16(float v) {
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
-  return v;
-}
-
 // BNF (DGRAD only): the epilogue also accumulates the preceding block's BatchNorm-backward sums
 // (ConvArgs::bnf) — a separate instantiation so the plain kernels keep their register budget
 // LDS bytes of one (BM, BN, NST) tile ring (the kernels' single __shared__ array)
