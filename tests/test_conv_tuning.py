@@ -16,9 +16,12 @@ def test_tuning_table_well_formed():
         t = json.load(f)
     keys = set()
     for e in t["entries"]:
-        assert e["mode"] in (0, 1, 2)
-        assert 0 <= e["tile"] <= 7
-        assert 1 <= e["splits"] <= 64
+        assert e["mode"] in (0, 1, 2, 3)
+        if e["mode"] == 3:  # backward pair: tile = pair on/off, splits / stages = DGRAD / WGRAD
+            assert e["tile"] in (0, 1) and 1 <= e["splits"] <= 16 and 1 <= e["stages"] <= 128
+        else:
+            assert 0 <= e["tile"] <= 7
+            assert 1 <= e["splits"] <= 64
         assert min(e["M"], e["N"], e["K"]) > 0
         assert e["us"] <= e["auto_us"] + 1e-6
         keys.add((e["mode"], e["M"], e["N"], e["K"]))

@@ -269,6 +269,9 @@ def tune_pairs(args):
             n.conv_pair_force(0, 0)
             us, on, sd, sw = best
             ref = min(sep, pol)
+            if pol <= us:  # the policy's own choice is (within noise) the best: no entry
+                print(f"{model} N{N} {Cr}->{K} {H}x{W} k{R}: policy kept ({pol:.1f} us)", flush=True)
+                continue
             saved += ref - us
             label = f"{model} N{N} {Cr}->{K} {H}x{W} k{R}"
             print(f"{label:32s} separate {sep:6.1f}  policy {pol:6.1f}  -> "
