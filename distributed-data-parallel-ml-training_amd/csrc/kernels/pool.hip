@@ -8,6 +8,7 @@
 // (VGG's 2x2/s2 max-pool is fused into the BatchNorm/ReLU kernels, bn_act.hip.)
 #include "common.h"
 #include "api.h"
+#include <algorithm>
 
 namespace ddp_amd {
 
@@ -16,15 +17,17 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const unsigned short* 
                                                           int KW, int stride, int pad, int Ho,
                                                           int Wo, unsigned short* __restrict__ y,
                                                           unsigned char* __restrict__ idx) {
-  const int G = C / 8;
-  const size_t total = (size_t)N * Ho * Wo * G;
-  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total;
-       t += (size_t)gridDim.x * blockDim.x) {
-    const int cg = (int)(t % G);
-    const size_t pix = t / G;
-    const int wo = (int)(pix % Wo);
-    const int ho = (int)((pix / Wo) % Ho);
-    const int n = (int)(pix / ((size_t)Wo * Ho));
+  // 32-bit index math (the launcher guarantees N*Ho*Wo*C/8 < 2^31): 64-bit divisions by
+  // runtime values were most of this kernel's instruction stream
+  const unsigned G = C / 8;
+  const unsigned total = (unsigned)N * Ho * Wo * G;
+  for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const unsigned pix = t / G;
+    const int cg = (int)(t - pix * G);
+    const unsigned prow = pix / (unsigned)Wo;
+    const int wo = (int)(pix - prow * Wo);
+    const int n = (int)(prow / (unsigned)Ho);
+    const int ho = (int)(prow - (unsigned)n * Ho);
     float best[8];
     unsigned char arg[8];
 #pragma unroll
@@ -46,7 +49,7 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const unsigned short* 
     u16x8 o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = f2bf(best[e]);
-    const size_t off = pix * C + cg * 8;
+    const size_t off = (size_t)pix * C + cg * 8;
     st8(y + off, o);
     uint2 packed;
     packed.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | ((unsigned)arg[3] << 24);
@@ -60,15 +63,15 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const unsigned short* 
                                                           int N, int H, int W, int C, int KH,
                                                           int KW, int stride, int pad, int Ho,
                                                           int Wo, unsigned short* __restrict__ dx) {
-  const int G = C / 8;
-  const size_t total = (size_t)N * H * W * G;
-  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total;
-       t += (size_t)gridDim.x * blockDim.x) {
-    const int cg = (int)(t % G);
-    const size_t pix = t / G;
-    const int w = (int)(pix % W);
-    const int h = (int)((pix / W) % H);
-    const int n = (int)(pix / ((size_t)W * H));
+  const unsigned G = C / 8;
+  const unsigned total = (unsigned)N * H * W * G;  // < 2^31 (launcher)
+  for (unsigned t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
+    const unsigned pix = t / G;
+    const int cg = (int)(t - pix * G);
+    const unsigned prow = pix / (unsigned)W;
+    const int w = (int)(pix - prow * W);
+    const int n = (int)(prow / (unsigned)H);
+    const int h = (int)(prow - (unsigned)n * H);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     // output windows covering (h, w): ho*stride - pad <= h <= ho*stride - pad + KH - 1
     const int ho_lo = max(0, (h + pad - KH + stride) / stride);
@@ -96,7 +99,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const unsigned short* 
     u16x8 o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = f2bf(acc[e]);
-    st8(dx + pix * C + cg * 8, o);
+    st8(dx + (size_t)pix * C + cg * 8, o);
   }
 }
 
@@ -136,7 +139,7 @@ __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const unsigned short* 
     u16x8 o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = f2bf(bf2f(g[e]) * inv);
-    st8(dx + pix * C + cg * 8, o);
+    st8(dx + (size_t)pix * C + cg * 8, o);
   }
 }
 
@@ -164,7 +167,7 @@ static unsigned grid_items(size_t items) {
 extern "C" int ddp_maxpool_fwd(const void* x, int N, int H, int W, int C, int KH, int KW,
                                int stride, int pad, int Ho, int Wo, void* y, void* idx,
                                hipStream_t st) {
-  if (C % 8) return -1;
+  if (C % 8 || (size_t)N * std::max(H * W, Ho * Wo) * (C / 8) >= (1u << 31)) return -1;
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_items((size_t)N * Ho * Wo * (C / 8))), dim3(256),
                      0, st, (const unsigned short*)x, N, H, W, C, KH, KW, stride, pad, Ho, Wo,
                      (unsigned short*)y, (unsigned char*)idx);
@@ -174,7 +177,7 @@ extern "C" int ddp_maxpool_fwd(const void* x, int N, int H, int W, int C, int KH
 extern "C" int ddp_maxpool_bwd(const void* dy, const void* idx, int N, int H, int W, int C, int KH,
                                int KW, int stride, int pad, int Ho, int Wo, void* dx,
                                hipStream_t st) {
-  if (C % 8) return -1;
+  if (C % 8 || (size_t)N * std::max(H * W, Ho * Wo) * (C / 8) >= (1u << 31)) return -1;
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_items((size_t)N * H * W * (C / 8))), dim3(256),
                      0, st, (const unsigned short*)dy, (const unsigned char*)idx, N, H, W, C, KH,
                      KW, stride, pad, Ho, Wo, (unsigned short*)dx);
