@@ -198,11 +198,15 @@ struct ConvSmem {
 // The GEMM body. ``bid`` / ``nblk`` stand for blockIdx.x / gridDim.x, so a grouped launch
 // (conv_bwd_pair_kernel: the DGRAD and WGRAD GEMMs of one layer in ONE launch) can hand each
 // problem its own block range. ``smem`` = the launching kernel's single LDS array.
-template <int MODE, int BM, int BN, int NST, bool BNF = false>
+template <int MODE, int BM, int BN, int NST, int BNF = 0>
 __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned short* smem,
                                                 const int bid, const int nblk) {
   constexpr int BK = 64;
   constexpr int WTM = BM / 2, WTN = BN / 2;
+  // BNF: 0 none, 1 = the preceding block is pooled (generic epilogue, window-argmax routing),
+  // 2 = no pool (lean epilogue, same row offsets as the output). The generic epilogue also
+  // serves BNF 2 on 64x64 tiles, which never take the lean path.
+  constexpr bool kOldBnf = BNF == 1 || (BNF == 2 && BM == 64 && BN == 64);
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int CA = BM * BK / 8 / 256;  // 16-B chunks per thread per tile
   constexpr int CB = BN * BK / 8 / 256;
@@ -503,8 +507,11 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
   if (red) __syncthreads();
   // (not for 64x64 tiles: measured slower there — the VGG-11 forward convs, whose long
   // reductions hide the epilogue anyway — the generic path below keeps their codegen)
-  if (MODE != MODE_WGRAD && !BNF && !(BM == 64 && BN == 64) && !split &&
-      !(MODE == MODE_DGRAD && args.accumulate)) {
+  // With a BnBwdFuse the preceding block's BatchNorm-backward sums ride along when that block
+  // has no pool (its z has this output's shape: the same row offsets); pooled (VGG) fusions keep
+  // the generic path, which routes through the window argmax.
+  if (MODE != MODE_WGRAD && !(BM == 64 && BN == 64) && !split &&
+      !(MODE == MODE_DGRAD && args.accumulate) && BNF != 1) {
     // Plain bf16 output (FWD, DGRAD overwriting dx). Short-reduction GEMMs (1x1 convs over
     // 64-128 channels: 1-2 k-steps) spend most of their VALU issue in the epilogue and the
     // gather setup, so: one row offset per (lane, i) computed up front (column groups are
@@ -532,6 +539,14 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
       float4 bj = {0.f, 0.f, 0.f, 0.f};
       if (has_bias) bj = *reinterpret_cast<const float4*>(args.bias + cbase + j * 16);
       float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
+      float4 bsc = {0.f, 0.f, 0.f, 0.f}, bsh = bsc, bmu = bsc, bis = bsc;
+      if (MODE == MODE_DGRAD && BNF == 2 && red) {  // coefficients of the 4 channels ([6][C])
+        const float* cf = args.bnf.coef + cbase + j * 16;
+        bsc = *reinterpret_cast<const float4*>(cf + 0 * args.Ng);
+        bsh = *reinterpret_cast<const float4*>(cf + 1 * args.Ng);
+        bmu = *reinterpret_cast<const float4*>(cf + 2 * args.Ng);
+        bis = *reinterpret_cast<const float4*>(cf + 3 * args.Ng);
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         if (ro[i] < 0) continue;
@@ -540,11 +555,29 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
         pk.x = (unsigned)f2bf(v[0] + bj.x) | ((unsigned)f2bf(v[1] + bj.y) << 16);
         pk.y = (unsigned)f2bf(v[2] + bj.z) | ((unsigned)f2bf(v[3] + bj.w) << 16);
         *reinterpret_cast<uint2*>(args.out + ro[i] + j * 16) = pk;
-        if (red) {  // statistics of the stored (bf16-rounded) values
+        if (MODE == MODE_FWD && red) {  // statistics of the stored (bf16-rounded) values
           const float r0 = __uint_as_float(pk.x << 16), r1 = __uint_as_float(pk.x & 0xffff0000u);
           const float r2 = __uint_as_float(pk.y << 16), r3 = __uint_as_float(pk.y & 0xffff0000u);
           s[0] += r0; s[1] += r1; s[2] += r2; s[3] += r3;
           ss[0] += r0 * r0; ss[1] += r1 * r1; ss[2] += r2 * r2; ss[3] += r3 * r3;
+        }
+        if (MODE == MODE_DGRAD && BNF == 2 && red) {
+          // this row's stored gradient flows through the preceding block's ReLU mask:
+          // dy_bn; S1 += dy_bn, S2 += dy_bn * xhat (bn_act.hip bwd_compute, no pool)
+          const uint2 zz = *reinterpret_cast<const uint2*>(args.bnf.z + ro[i] + j * 16);
+          const float gv[4] = {__uint_as_float(pk.x << 16), __uint_as_float(pk.x & 0xffff0000u),
+                               __uint_as_float(pk.y << 16), __uint_as_float(pk.y & 0xffff0000u)};
+          const float zf[4] = {__uint_as_float(zz.x << 16), __uint_as_float(zz.x & 0xffff0000u),
+                               __uint_as_float(zz.y << 16), __uint_as_float(zz.y & 0xffff0000u)};
+          const float fsc[4] = {bsc.x, bsc.y, bsc.z, bsc.w}, fsh[4] = {bsh.x, bsh.y, bsh.z, bsh.w};
+          const float fmu[4] = {bmu.x, bmu.y, bmu.z, bmu.w}, fis[4] = {bis.x, bis.y, bis.z, bis.w};
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const float y = zf[t] * fsc[t] + fsh[t];
+            const float dyb = (args.bnf.relu && !(y > 0.f)) ? 0.f : gv[t];
+            s[t] += dyb;
+            ss[t] += dyb * ((zf[t] - fmu[t]) * fis[t]);
+          }
         }
       }
       if (red) {
@@ -567,7 +600,8 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
     if (red) {
       __syncthreads();
       if (wm == 0 && rl == 0) {
-        float* st = args.stats + (bid % kStatRep) * 2 * args.Ng;  // spread contention
+        float* st = (MODE == MODE_FWD ? args.stats : args.bnf.sums) +
+                    (bid % kStatRep) * 2 * args.Ng;  // spread contention
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int col = cbase + j * 16;
@@ -593,7 +627,7 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
       bias = (float4){args.bias[col], args.bias[col + 1], args.bias[col + 2], args.bias[col + 3]};
     float s[4] = {0.f, 0.f, 0.f, 0.f}, ss[4] = {0.f, 0.f, 0.f, 0.f};
     float4 bsc = {0.f, 0.f, 0.f, 0.f}, bsh = bsc, bmu = bsc, bis = bsc;
-    if (MODE == MODE_DGRAD && BNF && red && cok) {  // coefficients of the 4 channels (coef [6][C])
+    if (MODE == MODE_DGRAD && kOldBnf && red && cok) {  // coefficients of the 4 channels ([6][C])
       const float* cf = args.bnf.coef;
       bsc = *reinterpret_cast<const float4*>(cf + 0 * args.Ng + col);
       bsh = *reinterpret_cast<const float4*>(cf + 1 * args.Ng + col);
@@ -662,7 +696,7 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
           s[0] += r0; s[1] += r1; s[2] += r2; s[3] += r3;
           ss[0] += r0 * r0; ss[1] += r1 * r1; ss[2] += r2 * r2; ss[3] += r3 * r3;
         }
-        if (MODE == MODE_DGRAD && BNF && red) {
+        if (MODE == MODE_DGRAD && kOldBnf && red) {
           // this row is pixel (n, h, w) of the preceding block's output; its gradient (as
           // stored, bf16-rounded) flows to the window argmax of relu(bn(z)) (pool) and through
           // the ReLU mask: dy_bn; S1 += dy_bn, S2 += dy_bn * xhat — bn_act.hip bwd_compute
@@ -833,24 +867,33 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
   }
 }
 
-template <int MODE, int BM, int BN, int NST, bool BNF = false>
+template <int MODE, int BM, int BN, int NST, int BNF = 0>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
   // dynamic: the launcher sizes the ring to the stages a work item can use (launch_gemm_t)
   extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
   conv_igemm_body<MODE, BM, BN, NST, BNF>(args, smem, blockIdx.x, gridDim.x);
 }
 
+// BNF 2 (no-pool BN-backward sums in the lean epilogue): the extra per-column coefficients push
+// the big tiles past 256 registers (1 wave per SIMD); ask the register allocator for 2 waves.
+template <int MODE, int BM, int BN, int NST>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+void conv_igemm_bnf2_kernel(ConvArgs args) {
+  extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
+  conv_igemm_body<MODE, BM, BN, NST, 2>(args, smem, blockIdx.x, gridDim.x);
+}
+
 // One layer's backward GEMMs in ONE launch: blocks [0, n_dg) run the DGRAD problem, the rest
 // the WGRAD problem (independent outputs, both read dy). At the strong-scaling batches each of
 // them alone leaves most of the 256 CUs idle and pays its own latency floor; side by side they
 // fill each other's idle slots and cost one dispatch. Same tile config for both (one LDS array).
-template <int BM, int BN, int NST, bool BNF>
+template <int BM, int BN, int NST, int BNF>
 __global__ __launch_bounds__(256) void conv_bwd_pair_kernel(ConvArgs dg, ConvArgs wg, int n_dg) {
   __shared__ __attribute__((aligned(16))) unsigned short smem[ConvSmem<BM, BN, NST>::elems];
   if ((int)blockIdx.x < n_dg)
     conv_igemm_body<MODE_DGRAD, BM, BN, NST, BNF>(dg, smem, blockIdx.x, n_dg);
   else
-    conv_igemm_body<MODE_WGRAD, BM, BN, NST, false>(wg, smem, blockIdx.x - n_dg, gridDim.x - n_dg);
+    conv_igemm_body<MODE_WGRAD, BM, BN, NST, 0>(wg, smem, blockIdx.x - n_dg, gridDim.x - n_dg);
 }
 
 // Split-K finish for FWD/DGRAD: sum the slabs in split order -> (+bias) bf16 output
@@ -1183,7 +1226,7 @@ static int stages_for(int BM, int BN) {
   return 3;
 }
 
-template <int MODE, int BM, int BN, int NST, bool BNF>
+template <int MODE, int BM, int BN, int NST, int BNF>
 static void launch_gemm_t(const ConvArgs& a, int items, hipStream_t st) {
   constexpr int kStageBytes = (BM + BN) * 64 * 2;
   // A work item of k k-steps touches min(NST, k) ring stages (the prologue issues k-steps
@@ -1193,10 +1236,13 @@ static void launch_gemm_t(const ConvArgs& a, int items, hipStream_t st) {
   // (their tiles are latency-bound: DMA in, a few MFMAs, stores out).
   const int stages = std::max(1, std::min(NST, a.ksteps_per_split));
   const size_t lds = (size_t)stages * kStageBytes;
+  void (*kern)(ConvArgs);
+  if constexpr (BNF == 2 && MODE == MODE_DGRAD) kern = conv_igemm_bnf2_kernel<MODE, BM, BN, NST>;
+  else kern = conv_igemm_kernel<MODE, BM, BN, NST, BNF>;
   static bool attr = false;
   if (!attr) {
     // an error here surfaces through the caller's hipGetLastError
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_igemm_kernel<MODE, BM, BN, NST, BNF>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize, NST * kStageBytes);
     attr = true;
   }
@@ -1204,13 +1250,13 @@ static void launch_gemm_t(const ConvArgs& a, int items, hipStream_t st) {
   static int resident = 0;
   if (resident == 0) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, conv_igemm_kernel<MODE, BM, BN, NST, BNF>, 256,
-                                                     NST * kStageBytes) != hipSuccess || nb < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 256, NST * kStageBytes) != hipSuccess ||
+        nb < 1)
       nb = 1;
     resident = nb;
   }
   const int grid = g_persistent ? std::min(items, kNumCUs * resident) : items;
-  hipLaunchKernelGGL((conv_igemm_kernel<MODE, BM, BN, NST, BNF>), dim3(grid), dim3(256), lds, st, a);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, a);
 }
 
 template <int MODE, int BM, int BN, int NST>
@@ -1219,9 +1265,10 @@ static void launch_gemm(const ConvArgs& a, int items, hipStream_t st) {
     // the BN-backward sums are reduced in the non-split epilogue: a single split, or the
     // ticket fixup's last-arriving split block
     if (a.has_bnf && (a.splits <= 1 || a.fixup))
-      return launch_gemm_t<MODE, BM, BN, NST, true>(a, items, st);
+      return a.bnf.pool ? launch_gemm_t<MODE, BM, BN, NST, 1>(a, items, st)
+                        : launch_gemm_t<MODE, BM, BN, NST, 2>(a, items, st);
   }
-  launch_gemm_t<MODE, BM, BN, NST, false>(a, items, st);
+  launch_gemm_t<MODE, BM, BN, NST, 0>(a, items, st);
 }
 
 // Normalise the split count (no empty split), decide WGRAD atomics / FWD-DGRAD fixup; returns
@@ -1679,10 +1726,10 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
   if (dneed + wneed > ws_elems) return separate();
   if (g_pair_mode == 3 && !both64 && itd + itw > g_pair_items) return separate();
   if (d.has_bnf && (d.splits <= 1 || d.fixup))
-    hipLaunchKernelGGL((conv_bwd_pair_kernel<64, 64, 3, true>), dim3(itd + itw), dim3(256), 0, st,
+    hipLaunchKernelGGL((conv_bwd_pair_kernel<64, 64, 3, 1>), dim3(itd + itw), dim3(256), 0, st,
                        d, w, itd);
   else
-    hipLaunchKernelGGL((conv_bwd_pair_kernel<64, 64, 3, false>), dim3(itd + itw), dim3(256), 0, st,
+    hipLaunchKernelGGL((conv_bwd_pair_kernel<64, 64, 3, 0>), dim3(itd + itw), dim3(256), 0, st,
                        d, w, itd);
   const bool fd = needs_finish(MODE_DGRAD, d), fw = needs_finish(MODE_WGRAD, w);
   if (fd && fw && w.g.wkrsc) {
