@@ -42,6 +42,7 @@
 #include "api.h"
 #include <algorithm>
 #include <map>
+#include <cstdlib>
 
 namespace ddp_amd {
 
@@ -912,6 +913,32 @@ __device__ __forceinline__ size_t map_row(const RowMap& m, int row) {
   return ((size_t)n * m.H + m.pa + m.stride * i) * m.W + m.pb + m.stride * j;
 }
 
+// v[0..8) += p[z * slab + 0..8) for z = z0 .. z1-1, summed in z order (bit-identical to the
+// plain loop) but with the loads of up to kSlabBatch slabs issued before the first add: the
+// finish passes are latency-bound at the small batches (a plain loop waits one L2/HBM round
+// trip per split; 16-row grids at 32 images/GPU spent 6-8 us that way).
+constexpr int kSlabBatch = 8;
+__device__ __forceinline__ void sum_slabs8(const float* p, size_t slab, int z0, int z1, float* v) {
+  for (int zb = z0; zb < z1; zb += kSlabBatch) {
+    float4 a[kSlabBatch], b[kSlabBatch];
+#pragma unroll
+    for (int u = 0; u < kSlabBatch; ++u) {
+      if (zb + u < z1) {
+        const float4* src = reinterpret_cast<const float4*>(p + (size_t)(zb + u) * slab);
+        a[u] = src[0];
+        b[u] = src[1];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kSlabBatch; ++u) {
+      if (zb + u < z1) {
+        v[0] += a[u].x; v[1] += a[u].y; v[2] += a[u].z; v[3] += a[u].w;
+        v[4] += b[u].x; v[5] += b[u].y; v[6] += b[u].z; v[7] += b[u].w;
+      }
+    }
+  }
+}
+
 struct FinishArgs {  // split-K finish of a FWD / DGRAD GEMM (one launch or one pair half)
   const float* ws;
   int splits;
@@ -969,12 +996,7 @@ __device__ __forceinline__ void splitk_finish_body(const FinishArgs& fa, float* 
     float v[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = bv[e];
-    for (int z = 0; z < splits; ++z) {
-      const float4* src = reinterpret_cast<const float4*>(ws + z * slab + (size_t)row * Ng + cg * 8);
-      const float4 a = src[0], b = src[1];
-      v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
-      v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
-    }
+    sum_slabs8(ws + (size_t)row * Ng + cg * 8, slab, 0, splits, v);
     unsigned short* dst = out + map_row(rmap, row) * Ng + cg * 8;
     if (accumulate) {
       const u16x8 old = ld8(dst);
@@ -1091,9 +1113,15 @@ __device__ __forceinline__ void wgrad_finish_krsc_body(const float* __restrict__
   for (size_t i = bx * (size_t)blockDim.x + threadIdx.x; i < n4;
        i += (size_t)gx * blockDim.x) {
     float4 v = reinterpret_cast<const float4*>(ws + z0 * slab)[i];
-    for (int z = z0 + 1; z < z1; ++z) {
-      const float4 a = reinterpret_cast<const float4*>(ws + z * slab)[i];
-      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    // loads of up to kSlabBatch slabs in flight before the (in-order) adds
+    for (int zb = z0 + 1; zb < z1; zb += kSlabBatch) {
+      float4 a[kSlabBatch];
+#pragma unroll
+      for (int u = 0; u < kSlabBatch; ++u)
+        if (zb + u < z1) a[u] = reinterpret_cast<const float4*>(ws + (size_t)(zb + u) * slab)[i];
+#pragma unroll
+      for (int u = 0; u < kSlabBatch; ++u)
+        if (zb + u < z1) { v.x += a[u].x; v.y += a[u].y; v.z += a[u].z; v.w += a[u].w; }
     }
     const float vv[4] = {v.x, v.y, v.z, v.w};
     if (Creal == C) {
@@ -1314,13 +1342,27 @@ static bool needs_finish(int mode, const ConvArgs& a) {
   return !a.fixup;
 }
 
+// Rows per thread of the FWD / DGRAD split-K finish: 1 for small grids (<= 128 blocks at one
+// row per thread: the latency-bound finishes of the strong-scaling batches), else 2 (enough
+// workgroups in flight for a bandwidth-bound pass). Measured, same session (gpurun_out/finish,
+// profiles/r2_finish_batched.md): VGG-11 b32 0.4849 -> 0.4705 (2 rows) -> 0.4596 ms (1 row);
+// b256 0.9018 -> 0.8984 (2 rows) vs 0.908 ms (1 row everywhere). DDP_AMD_FINISH_RPT forces.
+static int finish_rows_per_thread(int Mg, int rows_per_block) {
+  static const int forced = [] {
+    const char* e = std::getenv("DDP_AMD_FINISH_RPT");
+    return e ? std::max(1, std::min(8, std::atoi(e))) : 0;
+  }();
+  if (forced) return forced;
+  return (Mg + rows_per_block - 1) / rows_per_block <= 128 ? 1 : 2;
+}
+
 static void dg_finish_grid(const ConvArgs& a, int* bx_out, int* chunks_out) {
   const int G = a.Ng / 8;
   const int Gb = G < 256 ? G : 256;
   const int chunks = (G + Gb - 1) / Gb;
   const int rows_per_block = std::max(1, 256 / Gb);
-  // ~2 rows per thread: enough workgroups in flight for a bandwidth-bound pass
-  int bx = (a.Mg + rows_per_block * 2 - 1) / (rows_per_block * 2);
+  const int rpt = finish_rows_per_thread(a.Mg, rows_per_block);
+  int bx = (a.Mg + rows_per_block * rpt - 1) / (rows_per_block * rpt);
   *bx_out = std::max(1, std::min(bx, 2048 / chunks + 1));
   *chunks_out = chunks;
 }
