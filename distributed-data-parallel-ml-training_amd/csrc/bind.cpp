@@ -52,6 +52,16 @@ struct StreamLink {
   void wait(uintptr_t s) { check((int)hipStreamWaitEvent(S(s), ev, 0), "hipStreamWaitEvent"); }
 };
 
+// (dz, dgamma, dbeta) -> BnBwdApply (None -> nullptr)
+static const ddp_amd::BnBwdApply* bn_apply(py::object o, ddp_amd::BnBwdApply* out) {
+  if (o.is_none()) return nullptr;
+  auto t = o.cast<py::tuple>();
+  out->dz = P<unsigned short>(t[0].cast<uintptr_t>());
+  out->dgamma = P<float>(t[1].cast<uintptr_t>());
+  out->dbeta = P<float>(t[2].cast<uintptr_t>());
+  return out;
+}
+
 static ddp_amd::ConvGeom geom(py::tuple g) {
   if (g.size() != 12 && g.size() != 13) throw std::runtime_error("conv geometry needs 12/13 ints");
   ddp_amd::ConvGeom c;
@@ -72,6 +82,29 @@ PYBIND11_MODULE(_native, m) {
     check(ddp_conv_fwd(&c, P<void>(x), P<void>(wc), P<float>(bias), P<void>(y), P<float>(stats),
                        P<float>(ws), ws_elems, splits, S(st)), "conv_fwd");
   });
+  // conv_fwd + the BatchNorm(+ReLU, +2x2 pool) forward fused into its split-K finish when the
+  // GEMM is small (api.h BnFwdFuse); bn = (gamma, beta, eps, relu, pool, coef, y, P, Q).
+  // Returns True when fused (y and coef written), False when the caller must run bn_act_fwd.
+  m.def("conv_fwd_bn", [](py::tuple g, uintptr_t x, uintptr_t wc, uintptr_t bias, uintptr_t z,
+                          uintptr_t stats, uintptr_t ws, size_t ws_elems, uintptr_t st,
+                          py::tuple bn) {
+    auto c = geom(g);
+    ddp_amd::BnFwdFuse f{};
+    f.gamma = P<float>(bn[0].cast<uintptr_t>());
+    f.beta = P<float>(bn[1].cast<uintptr_t>());
+    f.eps = bn[2].cast<float>();
+    f.relu = bn[3].cast<int>();
+    f.pool = bn[4].cast<int>();
+    f.coef = P<float>(bn[5].cast<uintptr_t>());
+    f.y = P<unsigned short>(bn[6].cast<uintptr_t>());
+    f.P = bn[7].cast<int>();
+    f.Q = bn[8].cast<int>();
+    const int rc = ddp_conv_fwd_bn(&c, P<void>(x), P<void>(wc), P<float>(bias), P<void>(z),
+                                   P<float>(stats), P<float>(ws), ws_elems, &f, S(st));
+    if (rc < 0) check(-rc, "conv_fwd_bn");
+    return rc == 1;
+  });
+  m.def("conv_bn_fuse_rows", [](int rows) { ddp_conv_bn_fuse_rows(rows); });
   // direct MFMA conv for C = 8 input layers; returns False when the shape is not served
   m.def("conv_fwd_smallk", [](py::tuple g, uintptr_t x, uintptr_t wc, uintptr_t bias, uintptr_t y,
                               uintptr_t stats, uintptr_t st) {
@@ -83,13 +116,16 @@ PYBIND11_MODULE(_native, m) {
   });
   // bn: optional (z, coef, sums, pool, relu, Hz, Wz) of the preceding Conv->BN->ReLU(->pool)
   // block whose BatchNorm-backward sums the dgrad epilogue accumulates (api.h BnBwdFuse)
+  // bna: optional (dz, dgamma, dbeta) — complete that block's BN backward in the split-K finish
+  // when possible (api.h BnBwdApply); returns True when it did (dx is then NOT written)
   m.def("conv_dgrad", [](py::tuple g, uintptr_t dy, uintptr_t wt, uintptr_t dx, uintptr_t ws,
-                         size_t ws_elems, int splits, uintptr_t st, int accumulate, py::object bn) {
+                         size_t ws_elems, int splits, uintptr_t st, int accumulate, py::object bn,
+                         py::object bna) {
     auto c = geom(g);
     if (bn.is_none()) {
       check(ddp_conv_dgrad(&c, P<void>(dy), P<void>(wt), P<void>(dx), P<float>(ws), ws_elems,
                            splits, accumulate, S(st)), "conv_dgrad");
-      return;
+      return false;
     }
     auto t = bn.cast<py::tuple>();
     ddp_amd::BnBwdFuse f{};
@@ -100,17 +136,24 @@ PYBIND11_MODULE(_native, m) {
     f.relu = t[4].cast<int>();
     f.Hz = t[5].cast<int>();
     f.Wz = t[6].cast<int>();
+    ddp_amd::BnBwdApply ap{};
+    const ddp_amd::BnBwdApply* app = bn_apply(bna, &ap);
+    int done = 0;
     check(ddp_conv_dgrad_bn(&c, P<void>(dy), P<void>(wt), P<void>(dx), P<float>(ws), ws_elems,
-                            splits, &f, S(st)), "conv_dgrad_bn");
+                            splits, &f, app, &done, S(st)), "conv_dgrad_bn");
+    return done == 1;
   }, py::arg("g"), py::arg("dy"), py::arg("wt"), py::arg("dx"), py::arg("ws"),
      py::arg("ws_elems"), py::arg("splits"), py::arg("stream"), py::arg("accumulate") = 0,
-     py::arg("bn") = py::none());
+     py::arg("bn") = py::none(), py::arg("bna") = py::none());
   // one layer's backward: WGRAD (dw += ...) and stride-1 DGRAD (dx = ..., optional BN-backward
   // sums) as one grouped launch when the policy allows (ddp_conv_bwd_pair), else two
   m.def("conv_bwd_pair", [](py::tuple g, uintptr_t dy, uintptr_t wc, uintptr_t dx, uintptr_t x,
                             uintptr_t dw, uintptr_t ws, size_t ws_elems, uintptr_t st,
-                            py::object bn) {
+                            py::object bn, py::object bna) {
     auto c = geom(g);
+    ddp_amd::BnBwdApply ap{};
+    const ddp_amd::BnBwdApply* app = bn_apply(bna, &ap);
+    int done = 0;
     ddp_amd::BnBwdFuse f{};
     const ddp_amd::BnBwdFuse* fp = nullptr;
     if (!bn.is_none()) {
@@ -125,9 +168,11 @@ PYBIND11_MODULE(_native, m) {
       fp = &f;
     }
     check(ddp_conv_bwd_pair(&c, P<void>(dy), P<void>(wc), P<void>(dx), P<void>(x), P<float>(dw),
-                            P<float>(ws), ws_elems, fp, S(st)), "conv_bwd_pair");
+                            P<float>(ws), ws_elems, fp, app, &done, S(st)), "conv_bwd_pair");
+    return done == 1;
   }, py::arg("g"), py::arg("dy"), py::arg("wc"), py::arg("dx"), py::arg("x"), py::arg("dw"),
-     py::arg("ws"), py::arg("ws_elems"), py::arg("stream"), py::arg("bn") = py::none());
+     py::arg("ws"), py::arg("ws_elems"), py::arg("stream"), py::arg("bn") = py::none(),
+     py::arg("bna") = py::none());
   m.def("conv_pair_mode", [](int mode, int items) { ddp_conv_pair_mode(mode, items); },
         py::arg("mode"), py::arg("items") = 0);
   m.def("conv_pair_force", [](int sd, int sw) { ddp_conv_pair_force(sd, sw); },

@@ -63,6 +63,30 @@ struct BnBwdFuse {
   int Hz, Wz;               // z spatial dims (2x the dgrad output's when pooled)
 };
 
+// The COMPLETE BatchNorm backward of that preceding block fused into a small dgrad's split-K
+// finish (conv_igemm.hip splitk_finish_bnbwd_kernel): with the sums complete inside each block,
+// the finish also writes the block's dgamma / dbeta and its conv-output gradient dz — the dgrad
+// output itself is never stored and the block skips its BN backward (finalize + apply).
+struct BnBwdApply {
+  unsigned short* dz;       // gradient wrt the preceding block's conv output [N][Hz][Wz][C]
+  float* dgamma;            // its BatchNorm weight / bias gradients (accumulated, may be null)
+  float* dbeta;
+};
+
+// Training-mode BatchNorm (+ReLU, +2x2/s2 max-pool) forward fused into the split-K finish of a
+// small conv GEMM (conv_igemm.hip splitk_finish_bnfwd_kernel): one block owns 16 channels over
+// every GEMM row, so the batch statistics are complete inside the block — no atomics, no
+// finalize, no separate apply pass. The conv output z is still written (the backward reads it).
+struct BnFwdFuse {
+  const float* gamma;       // [C]
+  const float* beta;        // [C]
+  float eps;
+  int relu, pool;
+  float* coef;              // [6][C] table for the backward: scale, shift, mean, invstd
+  unsigned short* y;        // block output [N][P/pool][Q/pool][C] (bf16)
+  int P, Q;                 // conv output spatial dims (pre-pool)
+};
+
 struct PackDesc {
   const float* p;          // fp32 master [K][Cr][R][S] (krsc == 0) or [K][R][S][Cr] (krsc == 1)
   unsigned short* wc;      // bf16 [K][R][S][C]   (may be null)
@@ -90,11 +114,21 @@ struct AugArgs {
 extern "C" {
 int ddp_conv_fwd(const ddp_amd::ConvGeom* g, const void* x, const void* wc, const float* bias,
                  void* y, float* stats, float* ws, size_t ws_elems, int splits, hipStream_t st);
+// as ddp_conv_fwd; when the GEMM is split-K and small enough, its finish also runs the BatchNorm
+// forward of ``bn`` (returns 1: y and the coefficient table are written, no bn_act_fwd needed),
+// else the plain conv with statistics (returns 0); negative on error
+int ddp_conv_fwd_bn(const ddp_amd::ConvGeom* g, const void* x, const void* wc, const float* bias,
+                    void* z, float* stats, float* ws, size_t ws_elems, const ddp_amd::BnFwdFuse* bn,
+                    hipStream_t st);
+// row limit of the BN-fused split-K finishes (default 128 or DDP_AMD_BN_FUSE_MAX_ROWS)
+void ddp_conv_bn_fuse_rows(int rows);
 int ddp_conv_dgrad(const ddp_amd::ConvGeom* g, const void* dy, const void* wt, void* dx,
                    float* ws, size_t ws_elems, int splits, int accumulate, hipStream_t st);
+// ba (optional): also run the preceding block's whole BN backward in the finish when the dgrad
+// is split-K and small (*bn_done = 1: dz / dgamma / dbeta written, dx NOT written)
 int ddp_conv_dgrad_bn(const ddp_amd::ConvGeom* g, const void* dy, const void* wt, void* dx,
                       float* ws, size_t ws_elems, int splits, const ddp_amd::BnBwdFuse* bn,
-                      hipStream_t st);
+                      const ddp_amd::BnBwdApply* ba, int* bn_done, hipStream_t st);
 int ddp_conv_wgrad(const ddp_amd::ConvGeom* g, const void* dy, const void* x, float* dw,
                    float* ws, size_t ws_elems, int splits, hipStream_t st);
 int ddp_bn_act_fwd(const ddp_amd::BnArgs* a, hipStream_t st);
@@ -117,7 +151,8 @@ void ddp_conv_pair_mode(int mode, int items);
 void ddp_conv_pair_force(int splits_dg, int splits_wg);
 int ddp_conv_bwd_pair(const ddp_amd::ConvGeom* g, const void* dy, const void* wc, void* dx,
                       const void* x, float* dw, float* ws, size_t ws_elems,
-                      const ddp_amd::BnBwdFuse* bn, hipStream_t st);
+                      const ddp_amd::BnBwdFuse* bn, const ddp_amd::BnBwdApply* ba, int* bn_done,
+                      hipStream_t st);
 void ddp_conv_fixup(float* facc, size_t facc_elems, unsigned* tickets, size_t n_tickets, int mode,
                     size_t max_bytes);
 void ddp_conv_tune_set(int mode, int M, int N, int K, int tile, int splits, int stages);

@@ -92,6 +92,14 @@ struct ConvArgs {
   int fixup;
   float* facc;
   unsigned* tickets;
+  // FWD (host-side only, never read by a kernel): BatchNorm forward to fuse into the split-K
+  // finish (splitk_finish_bnfwd_kernel) and where to report that it was fused
+  const BnFwdFuse* bnfwd;
+  int* bnfwd_done;
+  // DGRAD with has_bnf (host-side only): the preceding block's BN backward to complete in the
+  // split-K finish (splitk_finish_bnbwd_kernel) and where to report that it was
+  const BnBwdApply* bnapply;
+  int* bnapply_done;
 };
 
 // ------------------------------------------------------------------ operand gathers
@@ -1065,6 +1073,311 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(FinishArgs fa) {
   splitk_finish_body<BNF>(fa, red, blockIdx.x, blockIdx.y, gridDim.x);
 }
 
+// Split-K finish + training-mode BatchNorm + ReLU (+ 2x2/s2 max-pool) of a SMALL forward GEMM
+// (Mg <= 128 * RPT rows): block b owns channels [16b, 16b + 16) over EVERY row — waves 0-1 the
+// first 8 channels, waves 2-3 the next 8, lane l of a half the rows l, l + 128, ... — so the
+// batch statistics of its channels are complete in the block: slab sums (+bias) -> bf16 z
+// (stored: the backward reads it) -> sum / sum of squares of the rounded values (DPP wave sums,
+// 4 partials through LDS) -> mean, invstd, scale, shift (coefficient table for the backward) ->
+// y = relu(z * scale + shift), max-pooled through LDS. Replaces finish + BN-apply launches, the
+// statistic replicas and their atomics (the strong-scaling batches: 16-512-row GEMMs, where
+// every launch is a ~5 us latency step). Same formulas as bn_act.hip's finalize + apply.
+constexpr int kBnFwdFuseMaxRows = 1024;
+template <int RPT>
+__global__ __launch_bounds__(256) void splitk_finish_bnfwd_kernel(FinishArgs fa, BnFwdFuse bf) {
+  extern __shared__ __attribute__((aligned(16))) float act[];  // [Mg][16] (pooled layers)
+  __shared__ float wred[4][2][8];
+  __shared__ float cf[2][16];
+  const int Mg = fa.Mg, Ng = fa.Ng, splits = fa.splits;
+  const int half = threadIdx.x >> 7, lane = threadIdx.x & 127;
+  const int c0 = blockIdx.x * 16 + half * 8;
+  const size_t slab = (size_t)Mg * Ng;
+  float v[RPT][8];
+#pragma unroll
+  for (int r = 0; r < RPT; ++r)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[r][e] = fa.bias ? fa.bias[c0 + e] : 0.f;
+  // every row's loads of a split in flight together (split order kept per element)
+#pragma unroll 2
+  for (int z = 0; z < splits; ++z) {
+    float4 a[RPT], b[RPT];
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+      const int row = lane + r * 128;
+      if (row < Mg) {
+        const float4* src = reinterpret_cast<const float4*>(fa.ws + z * slab + (size_t)row * Ng + c0);
+        a[r] = src[0];
+        b[r] = src[1];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+      if (lane + r * 128 < Mg) {
+        v[r][0] += a[r].x; v[r][1] += a[r].y; v[r][2] += a[r].z; v[r][3] += a[r].w;
+        v[r][4] += b[r].x; v[r][5] += b[r].y; v[r][6] += b[r].z; v[r][7] += b[r].w;
+      }
+    }
+  }
+  float s[8], ss[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s[e] = 0.f; ss[e] = 0.f; }
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    const int row = lane + r * 128;
+    if (row >= Mg) continue;
+    u16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      o[e] = f2bf(v[r][e]);
+      v[r][e] = bf2f(o[e]);  // statistics and the BN input are the ROUNDED conv output
+      s[e] += v[r][e];
+      ss[e] += v[r][e] * v[r][e];
+    }
+    st8(fa.out + (size_t)row * Ng + c0, o);
+  }
+  const int wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float t1 = wave_sum(s[e]), t2 = wave_sum(ss[e]);
+    if ((threadIdx.x & 63) == 0) {
+      wred[wave][0][e] = t1;
+      wred[wave][1][e] = t2;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    const int h = threadIdx.x >> 3, e = threadIdx.x & 7;
+    const float M = (float)Mg;
+    const float s1 = wred[2 * h][0][e] + wred[2 * h + 1][0][e];
+    const float s2 = wred[2 * h][1][e] + wred[2 * h + 1][1][e];
+    const float mu = s1 / M;
+    const float var = fmaxf(s2 / M - mu * mu, 0.f);
+    const float is = rsqrtf(var + bf.eps);
+    const int c = blockIdx.x * 16 + threadIdx.x;
+    const float sc = bf.gamma[c] * is;
+    const float sh = bf.beta[c] - mu * sc;
+    bf.coef[0 * Ng + c] = sc;  // rows of bn_act.hip's coefficient table
+    bf.coef[1 * Ng + c] = sh;
+    bf.coef[2 * Ng + c] = mu;
+    bf.coef[3 * Ng + c] = is;
+    cf[0][threadIdx.x] = sc;
+    cf[1][threadIdx.x] = sh;
+  }
+  __syncthreads();
+  float sc[8], sh[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = cf[0][half * 8 + e];
+    sh[e] = cf[1][half * 8 + e];
+  }
+  if (!bf.pool) {
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+      const int row = lane + r * 128;
+      if (row >= Mg) continue;
+      u16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float y = v[r][e] * sc[e] + sh[e];
+        if (bf.relu) y = fmaxf(y, 0.f);
+        o[e] = f2bf(y);
+      }
+      st8(bf.y + (size_t)row * Ng + c0, o);
+    }
+    return;
+  }
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    const int row = lane + r * 128;
+    if (row >= Mg) continue;
+    float y[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      y[e] = v[r][e] * sc[e] + sh[e];
+      if (bf.relu) y[e] = fmaxf(y[e], 0.f);
+    }
+    float4* dst = reinterpret_cast<float4*>(act + row * 16 + half * 8);
+    dst[0] = make_float4(y[0], y[1], y[2], y[3]);
+    dst[1] = make_float4(y[4], y[5], y[6], y[7]);
+  }
+  __syncthreads();
+  const int P = bf.P, Q = bf.Q, Po = P / 2, Qo = Q / 2;
+  const int Mo = Mg / 4;
+  for (int orow = lane; orow < Mo; orow += 128) {
+    const int n = orow / (Po * Qo), rem = orow - n * (Po * Qo);
+    const int i = rem / Qo, j = rem - i * Qo;
+    const int r00 = (n * P + 2 * i) * Q + 2 * j;
+    float best[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) best[e] = -INFINITY;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {  // window order of bn_act_fwd_kernel
+      const int rr = r00 + (d >> 1) * Q + (d & 1);
+      const float4* src = reinterpret_cast<const float4*>(act + rr * 16 + half * 8);
+      const float4 p0 = src[0], p1 = src[1];
+      const float yv[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (yv[e] > best[e] || yv[e] != yv[e]) best[e] = yv[e];
+    }
+    u16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(best[e]);
+    st8(bf.y + (size_t)orow * Ng + c0, o);
+  }
+}
+
+// Split-K finish of a SMALL stride-1 DGRAD fused with the COMPLETE BatchNorm backward of the
+// preceding Conv->BN->ReLU(->2x2 pool) block (the BnBwdFuse chain, api.h BnBwdApply): block bx
+// owns channels [16 bx, 16 bx + 16) over every dgrad row (lane l of each 128-thread half: rows
+// l, l + 128, ...), so the block has the whole batch of its channels —
+//   dgrad slabs -> bf16-rounded dx (never stored: its only consumer is this BN backward)
+//   -> recompute the ReLU mask / pool routing from the block's conv output z (bn_act.hip
+//      bwd_compute) -> S1 = sum dy_bn, S2 = sum dy_bn * xhat (DPP wave sums + LDS)
+//   -> k1 = S1 / M, k2 = S2 / M; dgamma += S2, dbeta += S1 (one writer per channel)
+//   -> dz = scale * (dy_bn - k1 - xhat * k2) for all 4 pre-pool pixels.
+// Replaces the finish with memory-side sum atomics, the finalize launch and the apply launch of
+// the strong-scaling batches' 4x4 / 2x2 layers by one pass.
+template <int RPT, bool POOL>
+__device__ __forceinline__ void finish_bnbwd_body(const FinishArgs& fa, const BnBwdApply& ba,
+                                                  float (*wred)[2][8], int bx) {
+  constexpr int NP = POOL ? 4 : 1;
+  const BnBwdFuse& bn = fa.bnf;
+  const int Mg = fa.Mg, Ng = fa.Ng, splits = fa.splits;
+  const int half = threadIdx.x >> 7, lane = threadIdx.x & 127;
+  const int c0 = bx * 16 + half * 8;
+  const size_t slab = (size_t)Mg * Ng;
+  float v[RPT][8];
+#pragma unroll
+  for (int r = 0; r < RPT; ++r)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[r][e] = 0.f;
+#pragma unroll 2
+  for (int z = 0; z < splits; ++z) {
+    float4 a[RPT], b[RPT];
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+      const int row = lane + r * 128;
+      if (row < Mg) {
+        const float4* src = reinterpret_cast<const float4*>(fa.ws + z * slab + (size_t)row * Ng + c0);
+        a[r] = src[0];
+        b[r] = src[1];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+      if (lane + r * 128 < Mg) {
+        v[r][0] += a[r].x; v[r][1] += a[r].y; v[r][2] += a[r].z; v[r][3] += a[r].w;
+        v[r][4] += b[r].x; v[r][5] += b[r].y; v[r][6] += b[r].z; v[r][7] += b[r].w;
+      }
+    }
+  }
+  float sc[8], sh[8], mu[8], is[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = bn.coef[0 * Ng + c0 + e];
+    sh[e] = bn.coef[1 * Ng + c0 + e];
+    mu[e] = bn.coef[2 * Ng + c0 + e];
+    is[e] = bn.coef[3 * Ng + c0 + e];
+  }
+  // the block's z pixels (kept for the apply), dx rounded like the stored dgrad output
+  u16x8 zz[RPT][NP];
+  unsigned zoff[RPT][NP];  // (host: z has < 2^31 elements)
+  const int hw = fa.H * fa.W;
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    const int row = lane + r * 128;
+    const int rr = row < Mg ? row : 0;
+    const int n = rr / hw, rem = rr - n * hw;
+    const int h = rem / fa.W, w = rem - h * fa.W;
+#pragma unroll
+    for (int d = 0; d < NP; ++d) {
+      const int zh = POOL ? 2 * h + (d >> 1) : h, zw = POOL ? 2 * w + (d & 1) : w;
+      zoff[r][d] = (unsigned)((((size_t)n * bn.Hz + zh) * bn.Wz + zw) * Ng + c0);
+      zz[r][d] = ld8(bn.z + zoff[r][d]);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[r][e] = round_bf(v[r][e]);
+  }
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  // dy_bn of pixel d: the dgrad value routed to the window's argmax, masked by the ReLU
+  auto dyb_at = [&](int r, int d, int e, float* xh) -> float {
+    float best = -INFINITY, yarg = 0.f;
+    int arg = 0;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      const float zf = bf2f(zz[r][q][e]);
+      const float y = zf * sc[e] + sh[e];
+      const float yr = bn.relu ? fmaxf(y, 0.f) : y;
+      if (q == 0 || yr > best || yr != yr) { best = yr; arg = q; yarg = y; }
+      if (q == d) *xh = (zf - mu[e]) * is[e];
+    }
+    if (POOL && arg != d) return 0.f;  // pool routes the gradient to the argmax only
+    return (bn.relu && !(yarg > 0.f)) ? 0.f : v[r][e];
+  };
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    if (lane + r * 128 >= Mg) continue;
+#pragma unroll
+    for (int d = 0; d < NP; ++d)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float xh;
+        const float dy = dyb_at(r, d, e, &xh);
+        s1[e] += dy;
+        s2[e] += dy * xh;
+      }
+  }
+  const int wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float t1 = wave_sum(s1[e]), t2 = wave_sum(s2[e]);
+    if ((threadIdx.x & 63) == 0) {
+      wred[wave][0][e] = t1;
+      wred[wave][1][e] = t2;
+    }
+  }
+  __syncthreads();
+  // every thread needs k1 / k2 of its 8 channels: both waves of its half add the same 2 partials
+  const float inv_m = 1.f / ((float)fa.Mg * NP);
+  float k1[8], k2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float S1 = wred[2 * half][0][e] + wred[2 * half + 1][0][e];
+    const float S2 = wred[2 * half][1][e] + wred[2 * half + 1][1][e];
+    k1[e] = S1 * inv_m;
+    k2[e] = S2 * inv_m;
+    if (lane == 0) {
+      if (ba.dgamma) ba.dgamma[c0 + e] += S2;
+      if (ba.dbeta) ba.dbeta[c0 + e] += S1;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    if (lane + r * 128 >= Mg) continue;
+#pragma unroll
+    for (int d = 0; d < NP; ++d) {
+      u16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float xh;
+        const float dy = dyb_at(r, d, e, &xh);
+        o[e] = f2bf(sc[e] * (dy - k1[e] - xh * k2[e]));
+      }
+      st8(ba.dz + zoff[r][d], o);
+    }
+  }
+}
+
+constexpr int kBnBwdFuseMaxRows = 512;  // (template limit: RPT <= 4)
+template <int RPT, bool POOL>
+__global__ __launch_bounds__(256) void splitk_finish_bnbwd_kernel(FinishArgs fa, BnBwdApply ba) {
+  __shared__ float wred[4][2][8];
+  finish_bnbwd_body<RPT, POOL>(fa, ba, wred, blockIdx.x);
+}
+
 // Split-K finish for WGRAD: dW[k][c][r][s] += sum_z slab[z][k][(r,s,c)].
 // Block (k, split-group): sums its group of slabs for GEMM row k with coalesced reads
 // (reduction order fixed inside a group), transposes (r,s,c) -> (c,r,s) through LDS, and adds
@@ -1382,6 +1695,102 @@ static WgFinishArgs wg_finish_args(const ConvArgs& a) {
   return WgFinishArgs{a.ws, a.splits, a.g.K, a.g.R * a.g.S, a.g.C, a.g.Creal, a.dw, bx, groups};
 }
 
+// DGRAD split-K finish with the preceding block's complete BatchNorm backward (small stride-1
+// problems). With ``wa`` (a WGRAD finish of the same backward pair) both run in ONE launch.
+// false = not applicable (plain finish with the BnBwdFuse sums).
+// Row limit of both fused finishes (DDP_AMD_BN_FUSE_MAX_ROWS): one block owns 16 channels of
+// every row, so a bigger GEMM gives each thread several rows of serial, poorly coalesced slab
+// reads on only Ng/16 blocks. Measured on the VGG-11 b32 step (profiles/r2_bn_fused_finish.md):
+// at 128 rows (2x2 layers) the fused forward finish takes 6.4 us vs 5.1 + 4.4-5.3 us for finish
+// + BN apply, the fused backward 11.8 us vs 17 us for finish + finalize + apply; at 512 rows
+// (4x4 layers) 10-13 us (forward, no gain) and 29 us (backward, vs 16 us).
+static int g_bn_fuse_rows = -1;  // -1: not read yet (env, default 128); ddp_conv_bn_fuse_rows
+static int bn_fuse_max_rows() {
+  if (g_bn_fuse_rows < 0) {
+    const char* e = std::getenv("DDP_AMD_BN_FUSE_MAX_ROWS");
+    g_bn_fuse_rows = e ? std::max(0, std::atoi(e)) : 128;
+  }
+  return g_bn_fuse_rows;
+}
+
+static bool bnbwd_fusable(const ConvArgs& a) {
+  return a.has_bnf && a.bnapply && a.splits > 1 && !a.fixup && !a.phase && !a.accumulate &&
+         a.Mg <= bn_fuse_max_rows() && a.Mg <= kBnBwdFuseMaxRows && a.Ng % 16 == 0 &&
+         a.g.stride == 1 &&
+         (!a.bnf.pool || (a.bnf.Hz == 2 * a.g.H && a.bnf.Wz == 2 * a.g.W)) &&
+         (a.bnf.pool || (a.bnf.Hz == a.g.H && a.bnf.Wz == a.g.W));
+}
+
+template <int RPT, bool POOL>
+__global__ __launch_bounds__(256) void bwd_pair_finish_bnbwd_kernel(FinishArgs fa, BnBwdApply ba,
+                                                                    int dgx, WgFinishArgs wa) {
+  __shared__ float wred[4][2][8];
+  const int b = blockIdx.x;
+  if (b < dgx) {
+    finish_bnbwd_body<RPT, POOL>(fa, ba, wred, b);
+  } else {
+    const int w = b - dgx;
+    wgrad_finish_krsc_body(wa.ws, wa.splits, wa.K, wa.RS, wa.C, wa.Creal, wa.dw, w % wa.gx,
+                           w / wa.gx, wa.gx, wa.gy);
+  }
+}
+
+template <int RPT, bool POOL>
+static void launch_bnbwd_t(const FinishArgs& fa, const BnBwdApply& ba, int dgx,
+                           const WgFinishArgs* wa, hipStream_t st) {
+  if (wa)
+    hipLaunchKernelGGL((bwd_pair_finish_bnbwd_kernel<RPT, POOL>), dim3(dgx + wa->gx * wa->gy),
+                       dim3(256), 0, st, fa, ba, dgx, *wa);
+  else
+    hipLaunchKernelGGL((splitk_finish_bnbwd_kernel<RPT, POOL>), dim3(dgx), dim3(256), 0, st, fa, ba);
+}
+
+static bool launch_finish_bnbwd(const ConvArgs& a, hipStream_t st, const WgFinishArgs* wa) {
+  if (!bnbwd_fusable(a)) return false;
+  const FinishArgs fa = finish_args(MODE_DGRAD, a);
+  const BnBwdApply& ba = *a.bnapply;
+  const int dgx = a.Ng / 16, rpt = (a.Mg + 127) / 128;
+  if (a.bnf.pool) {
+    if (rpt <= 1) launch_bnbwd_t<1, true>(fa, ba, dgx, wa, st);
+    else if (rpt <= 2) launch_bnbwd_t<2, true>(fa, ba, dgx, wa, st);
+    else launch_bnbwd_t<4, true>(fa, ba, dgx, wa, st);
+  } else {
+    if (rpt <= 1) launch_bnbwd_t<1, false>(fa, ba, dgx, wa, st);
+    else if (rpt <= 2) launch_bnbwd_t<2, false>(fa, ba, dgx, wa, st);
+    else launch_bnbwd_t<4, false>(fa, ba, dgx, wa, st);
+  }
+  if (a.bnapply_done) *a.bnapply_done = 1;
+  return true;
+}
+
+// FWD split-K finish with the fused BatchNorm forward when the GEMM is small enough for one
+// block per 16 channels over all rows; false = not applicable (plain finish + stats).
+static bool launch_finish_bnfwd(const ConvArgs& a, hipStream_t st) {
+  const BnFwdFuse& bf = *a.bnfwd;
+  if (a.Mg > kBnFwdFuseMaxRows || a.Mg > bn_fuse_max_rows() || a.Ng % 16 || a.accumulate ||
+      a.phase)
+    return false;
+  if (bf.P * bf.Q <= 0 || a.Mg % (bf.P * bf.Q)) return false;
+  if (bf.pool && (bf.P % 2 || bf.Q % 2)) return false;
+  const FinishArgs fa = finish_args(MODE_FWD, a);
+  const dim3 grid(a.Ng / 16);
+  const size_t lds = bf.pool ? (size_t)a.Mg * 16 * sizeof(float) : 0;
+  static const bool attr = [] {  // the <8> instance needs 64 KB of dynamic + its static LDS
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(splitk_finish_bnfwd_kernel<8>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              kBnFwdFuseMaxRows * 16 * sizeof(float));
+    return true;
+  }();
+  (void)attr;
+  const int rpt = (a.Mg + 127) / 128;
+  if (rpt <= 1) hipLaunchKernelGGL(splitk_finish_bnfwd_kernel<1>, grid, dim3(256), lds, st, fa, bf);
+  else if (rpt <= 2) hipLaunchKernelGGL(splitk_finish_bnfwd_kernel<2>, grid, dim3(256), lds, st, fa, bf);
+  else if (rpt <= 4) hipLaunchKernelGGL(splitk_finish_bnfwd_kernel<4>, grid, dim3(256), lds, st, fa, bf);
+  else hipLaunchKernelGGL(splitk_finish_bnfwd_kernel<8>, grid, dim3(256), lds, st, fa, bf);
+  if (a.bnfwd_done) *a.bnfwd_done = 1;
+  return true;
+}
+
 template <int MODE>
 static void launch_finish(const ConvArgs& a, hipStream_t st) {
   if (!needs_finish(MODE, a)) return;
@@ -1395,6 +1804,8 @@ static void launch_finish(const ConvArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(wgrad_finish_kernel, dim3(a.g.K, groups), dim3(256), lds, st, a.ws,
                        a.splits, a.g.K, a.g.R, a.g.S, a.g.C, a.g.Creal, a.dw);
   } else {
+    if (MODE == MODE_FWD && a.bnfwd && launch_finish_bnfwd(a, st)) return;
+    if (MODE == MODE_DGRAD && a.has_bnf && a.bnapply && launch_finish_bnbwd(a, st, nullptr)) return;
     int bx, chunks;
     dg_finish_grid(a, &bx, &chunks);
     const FinishArgs fa = finish_args(MODE, a);
@@ -1564,9 +1975,47 @@ extern "C" int ddp_conv_fwd(const ConvGeom* g, const void* x, const void* wc, co
   return (int)hipGetLastError();
 }
 
+extern "C" void ddp_conv_bn_fuse_rows(int rows) { g_bn_fuse_rows = std::max(0, rows); }
+
+extern "C" int ddp_conv_fwd_bn(const ConvGeom* g, const void* x, const void* wc, const float* bias,
+                               void* z, float* stats, float* ws, size_t ws_elems,
+                               const BnFwdFuse* bn, hipStream_t st) {
+  static const bool enabled = [] {
+    const char* e = std::getenv("DDP_AMD_BN_FWD_FUSE");
+    return !(e && e[0] == '0');
+  }();
+  if (g->C % 8 || g->K % 8) return -1;
+  ConvArgs a{};
+  a.g = *g;
+  a.a = (const unsigned short*)x;
+  a.b = (const unsigned short*)wc;
+  a.out = (unsigned short*)z;
+  a.ws = ws;
+  a.bias = bias;
+  a.stats = stats;
+  a.Mg = g->N * g->P * g->Q;
+  a.Ng = g->K;
+  a.Kg = g->R * g->S * g->C;
+  const size_t xa = (size_t)g->N * g->H * g->W * g->C, wb = (size_t)a.Ng * a.Kg;
+  if (!fits_buffer(xa) || !fits_buffer(wb) || !fits_buffer((size_t)a.Mg * a.Ng)) return -2;
+  a.a_bytes = (int)(2 * xa);
+  a.b_bytes = (int)(2 * wb);
+  int done = 0;
+  if (enabled && bn && a.Mg <= kBnFwdFuseMaxRows) {
+    a.bnfwd = bn;
+    a.bnfwd_done = &done;
+    a.fixup = -1;  // (the fused finish needs the slabs)
+  }
+  launch_mode<MODE_FWD>(a, ws_elems, st);
+  const int e = (int)hipGetLastError();
+  return e ? -e : done;
+}
+
 static int conv_dgrad_impl(const ConvGeom* g, const void* dy, const void* wc, void* dx,
                            float* ws, size_t ws_elems, int splits, int accumulate,
-                           const BnBwdFuse* bn, hipStream_t st) {
+                           const BnBwdFuse* bn, const BnBwdApply* ba, int* bn_done,
+                           hipStream_t st) {
+  if (bn_done) *bn_done = 0;
   if (g->C % 8 || g->K % 8) return -1;
   if (bn && (accumulate || g->stride != 1)) return -3;  // fused BN sums: plain stride-1 dgrad only
   ConvArgs a{};
@@ -1574,6 +2023,8 @@ static int conv_dgrad_impl(const ConvGeom* g, const void* dy, const void* wc, vo
   if (bn) {
     a.has_bnf = 1;
     a.bnf = *bn;
+    a.bnapply = ba;
+    a.bnapply_done = bn_done;
   }
   a.g = *g;
   a.a = (const unsigned short*)dy;
@@ -1632,13 +2083,14 @@ static int conv_dgrad_impl(const ConvGeom* g, const void* dy, const void* wc, vo
 extern "C" int ddp_conv_dgrad(const ConvGeom* g, const void* dy, const void* wc, void* dx,
                               float* ws, size_t ws_elems, int splits, int accumulate,
                               hipStream_t st) {
-  return conv_dgrad_impl(g, dy, wc, dx, ws, ws_elems, splits, accumulate, nullptr, st);
+  return conv_dgrad_impl(g, dy, wc, dx, ws, ws_elems, splits, accumulate, nullptr, nullptr,
+                         nullptr, st);
 }
 
 extern "C" int ddp_conv_dgrad_bn(const ConvGeom* g, const void* dy, const void* wc, void* dx,
                                  float* ws, size_t ws_elems, int splits, const BnBwdFuse* bn,
-                                 hipStream_t st) {
-  return conv_dgrad_impl(g, dy, wc, dx, ws, ws_elems, splits, 0, bn, st);
+                                 const BnBwdApply* ba, int* bn_done, hipStream_t st) {
+  return conv_dgrad_impl(g, dy, wc, dx, ws, ws_elems, splits, 0, bn, ba, bn_done, st);
 }
 
 extern "C" int ddp_conv_wgrad(const ConvGeom* g, const void* dy, const void* x, float* dw,
@@ -1685,11 +2137,14 @@ extern "C" void ddp_conv_pair_mode(int m, int items) {
 
 extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* wc, void* dx,
                                  const void* x, float* dw, float* ws, size_t ws_elems,
-                                 const BnBwdFuse* bn, hipStream_t st) {
+                                 const BnBwdFuse* bn, const BnBwdApply* ba, int* bn_done,
+                                 hipStream_t st) {
+  if (bn_done) *bn_done = 0;
+  if (!bn) ba = nullptr;
   auto separate = [&]() -> int {
     const int r = ddp_conv_wgrad(g, dy, x, dw, ws, ws_elems, 0, st);
     if (r) return r;
-    return conv_dgrad_impl(g, dy, wc, dx, ws, ws_elems, 0, 0, bn, st);
+    return conv_dgrad_impl(g, dy, wc, dx, ws, ws_elems, 0, 0, bn, ba, bn_done, st);
   };
   if (g_pair_mode == 0 || g->stride != 1 || g->C % 8 || g->K % 8 || g->Creal != g->C)
     return separate();
@@ -1701,6 +2156,8 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
   if (bn) {
     d.has_bnf = 1;
     d.bnf = *bn;
+    d.bnapply = ba;
+    d.bnapply_done = bn_done;
   }
   d.a = (const unsigned short*)dy;
   d.b = (const unsigned short*)wc;
@@ -1774,7 +2231,10 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
     hipLaunchKernelGGL((conv_bwd_pair_kernel<64, 64, 3, 0>), dim3(itd + itw), dim3(256), 0, st,
                        d, w, itd);
   const bool fd = needs_finish(MODE_DGRAD, d), fw = needs_finish(MODE_WGRAD, w);
-  if (fd && fw && w.g.wkrsc) {
+  if (fd && fw && w.g.wkrsc && bnbwd_fusable(d)) {
+    const WgFinishArgs wa = wg_finish_args(w);
+    launch_finish_bnbwd(d, st, &wa);
+  } else if (fd && fw && w.g.wkrsc) {
     int bx, ch;
     dg_finish_grid(d, &bx, &ch);
     const FinishArgs fa = finish_args(MODE_DGRAD, d);

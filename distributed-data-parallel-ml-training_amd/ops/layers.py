@@ -68,6 +68,9 @@ class ConvBNActSpec:
         self.prev = None
         self.fwd_z = None
         self.sums_ready = False
+        # set by the next block's backward when its dgrad finish completed this block's BN
+        # backward (BN_BWD_APPLY_FUSE): the gradient at this block's conv output
+        self.dz_fused = None
 
     def pack_desc(self):
         w = self.conv.weight
@@ -92,9 +95,14 @@ class ConvBNActSpec:
                 wkrsc)
 
 
-def conv_forward(spec, x, bias=None, stats=None):
+def conv_forward(spec, x, bias=None, stats=None, bn_fuse=None):
     """z = conv(x) + bias (bf16 NHWC); stats[16][2][K] += per-channel sum / sumsq of z
-    (accumulated into STAT_REPLICAS replicas; the consumer sums them)."""
+    (accumulated into STAT_REPLICAS replicas; the consumer sums them).
+
+    ``bn_fuse`` = (gamma, beta, eps, relu, pool, coef, y, P, Q) pointers/values: when the GEMM
+    runs split-K and is small (the strong-scaling batches' deep layers), its finish kernel also
+    computes the BatchNorm forward into y and the coefficient table (conv_igemm.hip
+    splitk_finish_bnfwd_kernel). Returns (z, fused) then; plain z otherwise."""
     N, H, W, C = x.shape
     check(x, BF16, name="conv input")
     if C != spec.C:
@@ -104,8 +112,13 @@ def conv_forward(spec, x, bias=None, stats=None):
     z = torch.empty(N, P, Q, spec.K, dtype=BF16, device=x.device)
     if spec.C == 8 and native().conv_fwd_smallk(g, ptr(x), ptr(spec.wc), ptr(bias), ptr(z),
                                                 ptr(stats), stream_handle()):
-        return z  # input layer (3 channels padded to 8): direct MFMA kernel, conv_smallk.hip
+        # input layer (3 channels padded to 8): direct MFMA kernel, conv_smallk.hip
+        return (z, False) if bn_fuse is not None else z
     ws = workspace(x.device)
+    if bn_fuse is not None:
+        fused = native().conv_fwd_bn(g, ptr(x), ptr(spec.wc), ptr(bias), ptr(z), ptr(stats),
+                                     ptr(ws), ws.numel(), stream_handle(), bn_fuse)
+        return z, bool(fused)
     native().conv_fwd(g, ptr(x), ptr(spec.wc), ptr(bias), ptr(z), ptr(stats), ptr(ws), ws.numel(),
                       0, stream_handle())
     return z
@@ -140,6 +153,12 @@ class GradLink:
         return out
 
 
+# BatchNorm forward fused into the split-K finish of small conv GEMMs (conv_igemm.hip
+# splitk_finish_bnfwd_kernel; the native side also honours DDP_AMD_BN_FWD_FUSE=0)
+BN_FWD_FUSE = os.environ.get("DDP_AMD_BN_FWD_FUSE", "1") != "0"
+# the preceding block's whole BatchNorm backward completed in a small dgrad's split-K finish
+# (conv_igemm.hip splitk_finish_bnbwd_kernel; BnBwdFuse chain only)
+BN_BWD_APPLY_FUSE = os.environ.get("DDP_AMD_BN_BWD_APPLY_FUSE", "1") != "0"
 BN_BWD_FUSE_MAX_HW = int(os.environ.get("DDP_AMD_BN_BWD_FUSE_MAX_HW", "16"))
 # preceding block without a max-pool (ResNet's conv1 -> conv2 -> conv3 chain): one z load per
 # dgrad output element in the epilogue would replace a whole dy + z pass of the reduce kernel,
@@ -161,11 +180,14 @@ def bn_bwd_fuse_pays(H, W, pool=True):
     return H * W <= BN_BWD_FUSE_MAX_HW
 
 
-def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=None):
+def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=None, bna=None):
     """dW += wgrad(dz, x); returns dx (or None). With ``weight`` (the parameter whose gradient
     is dweight) and the backward side stream enabled, the wgrad runs on the side stream and the
     parameter is announced ready there (common.side_stream); otherwise everything is stream-
-    ordered on the current stream and the caller announces the gradient."""
+    ordered on the current stream and the caller announces the gradient.
+    ``bna`` = (dz_prev, dgamma_prev, dbeta_prev) pointers (with ``bnf``): the preceding block's
+    whole BatchNorm backward may be completed in the dgrad's split-K finish; the return value is
+    then (dx, done) — when done, dx was NOT written and dz_prev / dgamma / dbeta were."""
     N, H, W, C = x.shape
     g = spec.geom(N, H, W, weight_krsc(dweight))
     s = stream_handle()
@@ -175,11 +197,11 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=Non
         # wgrad + dgrad of this layer as one grouped launch (+ one finish launch) when the
         # kernel policy allows it (conv_igemm.hip ddp_conv_bwd_pair), else the two launches
         dx = torch.empty_like(x)
-        native().conv_bwd_pair(g, ptr(dz), ptr(spec.wc), ptr(dx), ptr(x), ptr(dweight), ptr(ws),
-                               ws.numel(), s, bn=bnf)
+        done = native().conv_bwd_pair(g, ptr(dz), ptr(spec.wc), ptr(dx), ptr(x), ptr(dweight),
+                                      ptr(ws), ws.numel(), s, bn=bnf, bna=bna)
         if weight is not None:
             grad_ready([weight])
-        return dx
+        return (dx, bool(done)) if bna is not None else dx
     if weight is not None and _common.BWD_SIDE_STREAM:
         side = side_stream(x.device, x, dz)
         with torch.cuda.stream(side.stream):
@@ -191,7 +213,7 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=Non
         if weight is not None:
             grad_ready([weight])
     if not need_dx:
-        return None
+        return (None, False) if bna is not None else None
     if spec.C != spec.Cr:
         raise RuntimeError("dgrad requested for a channel-padded input layer")
     if link is not None and link.buf is not None:
@@ -201,12 +223,13 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=Non
         link.seen += 1
         return link.result()
     dx = torch.empty_like(x)
-    native().conv_dgrad(g, ptr(dz), ptr(spec.wc), ptr(dx), ptr(ws), ws.numel(), 0, s, bn=bnf)
+    done = native().conv_dgrad(g, ptr(dz), ptr(spec.wc), ptr(dx), ptr(ws), ws.numel(), 0, s,
+                               bn=bnf, bna=bna)
     if link is not None:
         link.seen += 1
         link.buf = dx
         return link.result()
-    return dx
+    return (dx, bool(done)) if bna is not None else dx
 
 
 class _ConvBNActFn(torch.autograd.Function):
@@ -215,8 +238,7 @@ class _ConvBNActFn(torch.autograd.Function):
         spec.maybe_pack()
         N, H, W, _ = x.shape
         stats = spec.stats  # zeroed by the model's per-forward StepScratch.zero()
-        z = conv_forward(spec, x, bias, stats)
-        P, Q = z.shape[1], z.shape[2]
+        P, Q = spec.out_hw(H, W)
         Ho, Wo = (P // 2, Q // 2) if spec.pool else (P, Q)
         y = torch.empty(N, Ho, Wo, spec.K, dtype=BF16, device=x.device)
         if residual is not None:
@@ -227,11 +249,20 @@ class _ConvBNActFn(torch.autograd.Function):
         if bn.track_running_stats and bn.running_mean is not None:
             rm, rv = bn.running_mean, bn.running_var
             use_running = 0 if bn.training else 1
-        native().bn_act_fwd(N, P, Q, spec.K, int(spec.pool), int(spec.relu), spec.eps, ptr(z),
-                            ptr(residual), ptr(stats), ptr(gamma), ptr(beta), ptr(y),
-                            stream_handle(), ptr(rm), ptr(rv),
-                            float(bn.momentum if bn.momentum is not None else 0.1), use_running,
-                            ptr(spec.coef))
+        fused = False
+        if residual is None and rm is None and BN_FWD_FUSE:
+            # batch-statistics BN without residual (VGG): may run inside the conv's split-K finish
+            z, fused = conv_forward(spec, x, bias, stats,
+                                    bn_fuse=(ptr(gamma), ptr(beta), spec.eps, int(spec.relu),
+                                             int(spec.pool), ptr(spec.coef), ptr(y), P, Q))
+        else:
+            z = conv_forward(spec, x, bias, stats)
+        if not fused:
+            native().bn_act_fwd(N, P, Q, spec.K, int(spec.pool), int(spec.relu), spec.eps, ptr(z),
+                                ptr(residual), ptr(stats), ptr(gamma), ptr(beta), ptr(y),
+                                stream_handle(), ptr(rm), ptr(rv),
+                                float(bn.momentum if bn.momentum is not None else 0.1),
+                                use_running, ptr(spec.coef))
         ctx.spec = spec
         ctx.has_res = residual is not None
         ctx.in_link, ctx.res_link = in_link, res_link
@@ -247,7 +278,6 @@ class _ConvBNActFn(torch.autograd.Function):
         x, z, stats, weight, bias, gamma, beta, residual = ctx.saved_tensors
         dy = dy.contiguous()
         N, P, Q, K = z.shape
-        dz = torch.empty_like(z)
         sums = spec.sums  # zeroed together with the statistics at the start of the forward
         dres = torch.empty_like(z) if (ctx.has_res and ctx.needs_input_grad[5]) else None
         gw = ensure_grad(weight)
@@ -255,16 +285,24 @@ class _ConvBNActFn(torch.autograd.Function):
         gg = ensure_grad(gamma)
         gbt = ensure_grad(beta)
         sums_ready, spec.sums_ready = spec.sums_ready, False
+        dz_done, spec.dz_fused = spec.dz_fused, None
         spec.fwd_z = None
-        native().bn_act_bwd(N, P, Q, K, int(spec.pool), int(spec.relu), spec.eps, ptr(z),
-                            ptr(residual), ptr(stats), ptr(gamma), ptr(beta), ptr(dy), ptr(sums),
-                            ptr(dz), ptr(dres), ptr(gg), ptr(gbt), ptr(gb), stream_handle(),
-                            ptr(spec.coef), ptr(spec.bwd_counter) if _common.BN_LAST_BLOCK else 0,
-                            sums_ready=int(sums_ready))
+        if dz_done is not None:
+            # the next block's dgrad finish already ran this block's whole BN backward (dz,
+            # dgamma, dbeta; conv_igemm.hip splitk_finish_bnbwd_kernel): dy was never written
+            dz = dz_done
+        else:
+            dz = torch.empty_like(z)
+            native().bn_act_bwd(N, P, Q, K, int(spec.pool), int(spec.relu), spec.eps, ptr(z),
+                                ptr(residual), ptr(stats), ptr(gamma), ptr(beta), ptr(dy),
+                                ptr(sums), ptr(dz), ptr(dres), ptr(gg), ptr(gbt), ptr(gb),
+                                stream_handle(), ptr(spec.coef),
+                                ptr(spec.bwd_counter) if _common.BN_LAST_BLOCK else 0,
+                                sums_ready=int(sums_ready))
         grad_ready([gamma, beta, bias])
         if ctx.res_link is not None and dres is not None:
             dres = ctx.res_link.offer(dres)
-        bnf = None
+        bnf = bna = None
         prev = spec.prev
         if (_common.BN_BWD_FUSE and prev is not None and ctx.prev_z is not None
                 and ctx.needs_input_grad[0] and ctx.in_link is None and spec.stride == 1
@@ -273,9 +311,22 @@ class _ConvBNActFn(torch.autograd.Function):
             pz = ctx.prev_z
             bnf = (ptr(pz), ptr(prev.coef), ptr(prev.sums), int(prev.pool), int(prev.relu),
                    pz.shape[1], pz.shape[2])
-            prev.sums_ready = True
-        dx = conv_backward(spec, x, dz, gw, ctx.needs_input_grad[0], ctx.in_link, weight=weight,
-                           bnf=bnf)
+            if BN_BWD_APPLY_FUSE:
+                dz_prev = torch.empty_like(pz)
+                bna = (ptr(dz_prev), ptr(ensure_grad(prev.bn.weight)),
+                       ptr(ensure_grad(prev.bn.bias)))
+        if bna is not None:
+            dx, done = conv_backward(spec, x, dz, gw, ctx.needs_input_grad[0], ctx.in_link,
+                                     weight=weight, bnf=bnf, bna=bna)
+            if done:
+                prev.dz_fused = dz_prev  # prev's backward skips its BN backward
+            else:
+                prev.sums_ready = True
+        else:
+            if bnf is not None:
+                prev.sums_ready = True
+            dx = conv_backward(spec, x, dz, gw, ctx.needs_input_grad[0], ctx.in_link,
+                               weight=weight, bnf=bnf)
         ctx.prev_z = None
         return dx, None, None, None, None, dres, None, None, None
 

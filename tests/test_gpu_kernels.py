@@ -3,6 +3,8 @@
 Inputs are bf16-representable (the kernels consume bf16 activations/weights), references run in
 fp32 (or fp64) on the same values; tolerances are bf16-output level.
 """
+import os
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -461,3 +463,52 @@ def test_conv_splitk_fixup(native_ext, case, fixup):
     assert rel_err(dx.permute(0, 3, 1, 2), xr.grad) < 1e-2
     assert rel_err(dw, wr.grad) < 1e-2
     assert int(torch.count_nonzero(facc)) == 0 and int(torch.count_nonzero(tickets)) == 0
+
+
+@pytest.mark.parametrize("N,C,H,K,pool", [(32, 512, 4, 512, True), (32, 512, 2, 512, False),
+                                          (8, 256, 8, 512, True), (64, 256, 4, 512, False),
+                                          (16, 512, 8, 512, True)])
+def test_conv_splitk_finish_bn_fwd(native_ext, N, C, H, K, pool):
+    """BatchNorm(+ReLU, +2x2 pool) forward fused into a small conv GEMM's split-K finish
+    (conv_igemm.hip splitk_finish_bnfwd_kernel): y, z and the coefficient table against the fp32
+    PyTorch reference, and against the separate finish + bn_act_fwd path."""
+    from ddp_amd.ops.common import ptr, stream_handle, workspace
+    nat = native_ext
+    conv, spec, x, xn = _conv_setup(N, C, H, H, K, 3, 1, 1)
+    gamma = torch.rand(K, device=DEV) + 0.5
+    beta = torch.randn(K, device=DEV) * 0.1
+    Ho = H // 2 if pool else H
+    g = spec.geom(N, H, H)
+    ws = workspace(torch.device(DEV))
+    s = stream_handle()
+    y = torch.empty(N, Ho, Ho, K, device=DEV, dtype=torch.bfloat16)
+    z = torch.empty(N, H, H, K, device=DEV, dtype=torch.bfloat16)
+    coef = torch.zeros(6 * K, device=DEV)
+    stats = torch.zeros(16 * 2 * K, device=DEV)
+    nat.conv_tune_set(0, N * H * H, K, 9 * C, 3, 4, 2)  # force split-K 4 (64x64 tiles)
+    nat.conv_bn_fuse_rows(1024)  # every case fused (the shipped limit is 128 rows)
+    try:
+        fused = nat.conv_fwd_bn(g, ptr(xn), ptr(spec.wc), ptr(conv.bias), ptr(z), ptr(stats),
+                                ptr(ws), ws.numel(), s,
+                                (ptr(gamma), ptr(beta), 1e-5, 1, int(pool), ptr(coef), ptr(y), H, H))
+        # the unfused path on the same operands
+        z2 = torch.empty_like(z)
+        stats2 = torch.zeros_like(stats)
+        nat.conv_fwd(g, ptr(xn), ptr(spec.wc), ptr(conv.bias), ptr(z2), ptr(stats2), ptr(ws),
+                     ws.numel(), 0, s)
+    finally:
+        from ddp_amd.ops.common import load_conv_tuning
+        load_conv_tuning(nat)  # back to the shipped table
+        nat.conv_bn_fuse_rows(int(os.environ.get("DDP_AMD_BN_FUSE_MAX_ROWS", "128")))
+    assert fused, "the split-K GEMM must take the fused BatchNorm finish"
+    y2 = torch.empty_like(y)
+    coef2 = torch.zeros_like(coef)
+    nat.bn_act_fwd(N, H, H, K, int(pool), 1, 1e-5, ptr(z2), 0, ptr(stats2), ptr(gamma),
+                   ptr(beta), ptr(y2), s, coef=ptr(coef2))
+    torch.cuda.synchronize()
+    assert torch.equal(z, z2)  # same slabs, same per-element summation order
+    assert torch.allclose(coef[:4 * K], coef2[:4 * K], rtol=1e-4, atol=1e-5)
+    assert (y.float() - y2.float()).abs().max() <= 2e-2 * y2.float().abs().max()
+    zr = F.conv2d(x, conv.weight, conv.bias, 1, 1)
+    ref = _bn_ref(zr, gamma, beta, 1e-5, True, pool, None)
+    assert rel_err(y.permute(0, 3, 1, 2), ref) < 1e-2

@@ -284,6 +284,65 @@ def test_bn_backward_fused_sums_match_reduce_kernel(native_ext):
             assert cos(ga, gb) > 0.999, n
 
 
+def test_bn_fused_into_splitk_finishes_matches_unfused(native_ext):
+    """BatchNorm forward fused into the split-K finish of the small forward GEMMs and the
+    preceding block's whole BatchNorm backward completed in the small dgrads' finishes
+    (ops.layers BN_FWD_FUSE / BN_BWD_APPLY_FUSE, conv_igemm.hip splitk_finish_bnfwd_kernel /
+    splitk_finish_bnbwd_kernel) vs the separate finish + BN kernels, at the 8-GPU share of the
+    reference batch (32 images): same loss, gradients within the run-to-run spread of two
+    unfused runs; the fused launches must actually be taken."""
+    from ddp_amd.models import VGG11
+    from ddp_amd.engine import CrossEntropyLoss
+    from ddp_amd.optim import FusedSGD
+    from ddp_amd.ops import layers
+    from ddp_amd.ops.common import native
+    torch.manual_seed(0)
+    a = VGG11().cuda()
+    b, c = copy.deepcopy(a), copy.deepcopy(a)
+    x = torch.randn(32, 3, 32, 32, device="cuda")
+    y = torch.randint(0, 10, (32,), device="cuda")
+    nat = native()
+    taken = {"fwd": 0, "bwd": 0}
+    orig = {k: getattr(nat, k) for k in ("conv_fwd_bn", "conv_bwd_pair", "conv_dgrad")}
+
+    def spy(name, key):
+        def f(*args, **kw):
+            r = orig[name](*args, **kw)
+            taken[key] += int(bool(r))
+            return r
+        return f
+    nat.conv_fwd_bn = spy("conv_fwd_bn", "fwd")
+    nat.conv_bwd_pair = spy("conv_bwd_pair", "bwd")
+    nat.conv_dgrad = spy("conv_dgrad", "bwd")
+    losses, grads = [], []
+    saved = (layers.BN_FWD_FUSE, layers.BN_BWD_APPLY_FUSE)
+    try:
+        for m, fuse in ((a, True), (b, False), (c, False)):
+            layers.BN_FWD_FUSE = layers.BN_BWD_APPLY_FUSE = fuse
+            opt = FusedSGD(m.parameters(), lr=0.1)
+            opt.zero_grad()
+            loss = CrossEntropyLoss()(m(x), y)
+            loss.backward()
+            torch.cuda.synchronize()
+            losses.append(float(loss))
+            grads.append([p.grad.clone() for p in m.parameters()])
+    finally:
+        layers.BN_FWD_FUSE, layers.BN_BWD_APPLY_FUSE = saved
+        for k, v in orig.items():
+            setattr(nat, k, v)
+    assert taken["fwd"] >= 2 and taken["bwd"] >= 1, taken
+    assert abs(losses[0] - losses[1]) < 2e-2 * abs(losses[1]) + 1e-3, losses
+
+    def cos(u, v):
+        return float(torch.dot(u.reshape(-1), v.reshape(-1)) / (u.norm() * v.norm() + 1e-20))
+
+    for (n, _), ga, gb, gc in zip(a.named_parameters(), *grads):
+        if float(gb.norm()) < 1e-6:
+            continue
+        base = cos(gb, gc)
+        assert cos(ga, gb) > min(0.98, base - 0.05), (n, cos(ga, gb), base)
+
+
 def test_ddp_bf16_grad_comm_path(native_ext):
     """DDP(grad_comm_dtype="bf16") on one GPU with the world-1 collective stand-in: every
     gradient passes through the bf16 pack -> (all-reduce) -> unpack path, so it is exactly
