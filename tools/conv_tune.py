@@ -47,7 +47,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--quick", action="store_true", help="VGG-11 b256 only")
-    ap.add_argument("--sets", default="all", choices=["all", "resnet256"])
+    ap.add_argument("--sets", default="all", choices=["all", "vgg", "resnet256"])
     ap.add_argument("--merge", default=None, help="existing table to extend (entries kept)")
     ap.add_argument("--pairs", action="store_true",
                     help="tune the backward pair launch (DGRAD+WGRAD split-K factors, or separate "
@@ -71,6 +71,7 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     ap_sets = {"quick": [("vgg11", 256)],
                "resnet256": [("resnet50", 256)],
+               "vgg": [("vgg11", 256), ("vgg11", 128), ("vgg11", 64), ("vgg11", 32)],
                "all": [("vgg11", 256), ("vgg11", 128), ("vgg11", 64), ("vgg11", 32),
                        ("resnet50", 64), ("resnet50", 256)]}
     sets = ap_sets["quick" if args.quick else args.sets]
