@@ -66,6 +66,10 @@ def parse():
     p.add_argument("--zero", action="store_true",
                    help="pipelined DDP step with the ZeRO-1 sharded update (reduce-scatter -> "
                         "SGD on 1/N of the parameters -> all-gather, parallel/zero.py)")
+    p.add_argument("--lr", type=float, default=None,
+                   help="SGD learning rate (default: the reference's 0.1 for VGG; 0.01 for "
+                        "ResNet-50, whose random-init training on the synthetic data is chaotic "
+                        "at 0.1 in fp32 PyTorch as well: profiles/r2_resnet50_b256.md)")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--train-size", type=int, default=None)
     p.add_argument("--json-out", default=None)
@@ -148,7 +152,8 @@ def main():
     else:
         fn = STRATEGIES[args.strategy]
         sync = lambda m: fn(m, comm)  # noqa: E731
-    opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    lr = args.lr if args.lr is not None else (0.01 if resnet else 0.1)
+    opt = FusedSGD(model.parameters(), lr=lr, momentum=0.9, weight_decay=1e-4)
     if segmented:
         step = SegmentedDDPStep(model, opt, criterion, loader, split=cuts,
                                 emulate=int(os.environ.get("DDP_AMD_EMULATE_COMM", "0")),
@@ -250,7 +255,7 @@ def main():
                    "grad_comm": args.grad_comm,
                    "comm": (f"segmented@{args.segmented}" if segmented else "overlap-stream" if getattr(getattr(model, "reducer", None), "overlap",
                                                          lambda: False)() else "inline"),
-                   "optimizer": "SGD(lr=0.1, momentum=0.9, wd=1e-4) fused" +
+                   "optimizer": f"SGD(lr={lr:g}, momentum=0.9, wd=1e-4) fused" +
                                 (", ZeRO-1 sharded" if args.zero else "")},
         "avg_ms_iter_1_39": round(ref_ms, 4) if ref_ms is not None else None,
         "img_s_iter_1_39": round(global_batch / ref_ms * 1000.0, 2) if ref_ms else None,

@@ -1073,6 +1073,39 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(FinishArgs fa) {
   splitk_finish_body<BNF>(fa, red, blockIdx.x, blockIdx.y, gridDim.x);
 }
 
+// Slab sums of the BN-fused finishes: rows lane, lane + 128, ... of channels [c0, c0 + 8);
+// 8 / RPT splits of every row in flight per batch (the small layers take 4-12 splits; a plain
+// loop paid one L2 round trip per split), split order kept per element.
+template <int RPT>
+__device__ __forceinline__ void fused_finish_slabs(const float* ws, size_t slab, int Ng, int Mg,
+                                                   int splits, int lane, int c0, float (*v)[8]) {
+  constexpr int ZB = RPT >= 8 ? 1 : 8 / RPT;
+  for (int zb = 0; zb < splits; zb += ZB) {
+    float4 a[ZB][RPT], b[ZB][RPT];
+#pragma unroll
+    for (int u = 0; u < ZB; ++u)
+#pragma unroll
+      for (int r = 0; r < RPT; ++r) {
+        const int row = lane + r * 128;
+        if (zb + u < splits && row < Mg) {
+          const float4* src =
+              reinterpret_cast<const float4*>(ws + (size_t)(zb + u) * slab + (size_t)row * Ng + c0);
+          a[u][r] = src[0];
+          b[u][r] = src[1];
+        }
+      }
+#pragma unroll
+    for (int u = 0; u < ZB; ++u)
+#pragma unroll
+      for (int r = 0; r < RPT; ++r) {
+        if (zb + u < splits && lane + r * 128 < Mg) {
+          v[r][0] += a[u][r].x; v[r][1] += a[u][r].y; v[r][2] += a[u][r].z; v[r][3] += a[u][r].w;
+          v[r][4] += b[u][r].x; v[r][5] += b[u][r].y; v[r][6] += b[u][r].z; v[r][7] += b[u][r].w;
+        }
+      }
+  }
+}
+
 // Split-K finish + training-mode BatchNorm + ReLU (+ 2x2/s2 max-pool) of a SMALL forward GEMM
 // (Mg <= 128 * RPT rows): block b owns channels [16b, 16b + 16) over EVERY row — waves 0-1 the
 // first 8 channels, waves 2-3 the next 8, lane l of a half the rows l, l + 128, ... — so the
@@ -1098,26 +1131,7 @@ __global__ __launch_bounds__(256) void splitk_finish_bnfwd_kernel(FinishArgs fa,
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[r][e] = fa.bias ? fa.bias[c0 + e] : 0.f;
   // every row's loads of a split in flight together (split order kept per element)
-#pragma unroll 2
-  for (int z = 0; z < splits; ++z) {
-    float4 a[RPT], b[RPT];
-#pragma unroll
-    for (int r = 0; r < RPT; ++r) {
-      const int row = lane + r * 128;
-      if (row < Mg) {
-        const float4* src = reinterpret_cast<const float4*>(fa.ws + z * slab + (size_t)row * Ng + c0);
-        a[r] = src[0];
-        b[r] = src[1];
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < RPT; ++r) {
-      if (lane + r * 128 < Mg) {
-        v[r][0] += a[r].x; v[r][1] += a[r].y; v[r][2] += a[r].z; v[r][3] += a[r].w;
-        v[r][4] += b[r].x; v[r][5] += b[r].y; v[r][6] += b[r].z; v[r][7] += b[r].w;
-      }
-    }
-  }
+  fused_finish_slabs<RPT>(fa.ws, slab, Ng, Mg, splits, lane, c0, v);
   float s[8], ss[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s[e] = 0.f; ss[e] = 0.f; }
@@ -1252,26 +1266,7 @@ __device__ __forceinline__ void finish_bnbwd_body(const FinishArgs& fa, const Bn
   for (int r = 0; r < RPT; ++r)
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[r][e] = 0.f;
-#pragma unroll 2
-  for (int z = 0; z < splits; ++z) {
-    float4 a[RPT], b[RPT];
-#pragma unroll
-    for (int r = 0; r < RPT; ++r) {
-      const int row = lane + r * 128;
-      if (row < Mg) {
-        const float4* src = reinterpret_cast<const float4*>(fa.ws + z * slab + (size_t)row * Ng + c0);
-        a[r] = src[0];
-        b[r] = src[1];
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < RPT; ++r) {
-      if (lane + r * 128 < Mg) {
-        v[r][0] += a[r].x; v[r][1] += a[r].y; v[r][2] += a[r].z; v[r][3] += a[r].w;
-        v[r][4] += b[r].x; v[r][5] += b[r].y; v[r][6] += b[r].z; v[r][7] += b[r].w;
-      }
-    }
-  }
+  fused_finish_slabs<RPT>(fa.ws, slab, Ng, Mg, splits, lane, c0, v);
   float sc[8], sh[8], mu[8], is[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -1299,36 +1294,31 @@ __device__ __forceinline__ void finish_bnbwd_body(const FinishArgs& fa, const Bn
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[r][e] = round_bf(v[r][e]);
   }
+  // routing, once per (row, channel): the window's argmax (bn_act.hip bwd_compute order and NaN
+  // rule) and the gradient it receives, already masked by the ReLU; every other pixel gets 0
+  int arg[RPT][8];
   float s1[8], s2[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
-  // dy_bn of pixel d: the dgrad value routed to the window's argmax, masked by the ReLU
-  auto dyb_at = [&](int r, int d, int e, float* xh) -> float {
-    float best = -INFINITY, yarg = 0.f;
-    int arg = 0;
-#pragma unroll
-    for (int q = 0; q < NP; ++q) {
-      const float zf = bf2f(zz[r][q][e]);
-      const float y = zf * sc[e] + sh[e];
-      const float yr = bn.relu ? fmaxf(y, 0.f) : y;
-      if (q == 0 || yr > best || yr != yr) { best = yr; arg = q; yarg = y; }
-      if (q == d) *xh = (zf - mu[e]) * is[e];
-    }
-    if (POOL && arg != d) return 0.f;  // pool routes the gradient to the argmax only
-    return (bn.relu && !(yarg > 0.f)) ? 0.f : v[r][e];
-  };
 #pragma unroll
   for (int r = 0; r < RPT; ++r) {
-    if (lane + r * 128 >= Mg) continue;
+    const bool ok = lane + r * 128 < Mg;
 #pragma unroll
-    for (int d = 0; d < NP; ++d)
+    for (int e = 0; e < 8; ++e) {
+      float best = -INFINITY, yarg = 0.f, zarg = 0.f;
+      int a = 0;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float xh;
-        const float dy = dyb_at(r, d, e, &xh);
-        s1[e] += dy;
-        s2[e] += dy * xh;
+      for (int q = 0; q < NP; ++q) {
+        const float zf = bf2f(zz[r][q][e]);
+        const float y = zf * sc[e] + sh[e];
+        const float yr = bn.relu ? fmaxf(y, 0.f) : y;
+        if (q == 0 || yr > best || yr != yr) { best = yr; a = q; yarg = y; zarg = zf; }
       }
+      arg[r][e] = a;
+      v[r][e] = (!ok || (bn.relu && !(yarg > 0.f))) ? 0.f : v[r][e];  // now dy_bn at the argmax
+      s1[e] += v[r][e];
+      s2[e] += v[r][e] * ((zarg - mu[e]) * is[e]);
+    }
   }
   const int wave = threadIdx.x >> 6;
 #pragma unroll
@@ -1362,8 +1352,8 @@ __device__ __forceinline__ void finish_bnbwd_body(const FinishArgs& fa, const Bn
       u16x8 o;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        float xh;
-        const float dy = dyb_at(r, d, e, &xh);
+        const float xh = (bf2f(zz[r][d][e]) - mu[e]) * is[e];
+        const float dy = (!POOL || arg[r][e] == d) ? v[r][e] : 0.f;
         o[e] = f2bf(sc[e] * (dy - k1[e] - xh * k2[e]));
       }
       st8(ba.dz + zoff[r][d], o);
@@ -1712,10 +1702,18 @@ static int bn_fuse_max_rows() {
   }
   return g_bn_fuse_rows;
 }
+// the backward variant's own limit (DDP_AMD_BN_BWD_FUSE_MAX_ROWS, default: the common one)
+static int bn_bwd_fuse_max_rows() {
+  static const int v = [] {
+    const char* e = std::getenv("DDP_AMD_BN_BWD_FUSE_MAX_ROWS");
+    return e ? std::max(0, std::atoi(e)) : -1;
+  }();
+  return v >= 0 ? v : bn_fuse_max_rows();
+}
 
 static bool bnbwd_fusable(const ConvArgs& a) {
   return a.has_bnf && a.bnapply && a.splits > 1 && !a.fixup && !a.phase && !a.accumulate &&
-         a.Mg <= bn_fuse_max_rows() && a.Mg <= kBnBwdFuseMaxRows && a.Ng % 16 == 0 &&
+         a.Mg <= bn_bwd_fuse_max_rows() && a.Mg <= kBnBwdFuseMaxRows && a.Ng % 16 == 0 &&
          a.g.stride == 1 &&
          (!a.bnf.pool || (a.bnf.Hz == 2 * a.g.H && a.bnf.Wz == 2 * a.g.W)) &&
          (a.bnf.pool || (a.bnf.Hz == a.g.H && a.bnf.Wz == a.g.W));
