@@ -101,7 +101,8 @@ PYBIND11_MODULE(_native, m) {
     f.Q = bn[8].cast<int>();
     const int rc = ddp_conv_fwd_bn(&c, P<void>(x), P<void>(wc), P<float>(bias), P<void>(z),
                                    P<float>(stats), P<float>(ws), ws_elems, &f, S(st));
-    if (rc < 0) check(-rc, "conv_fwd_bn");
+    if (rc < 0) check(rc, "conv_fwd_bn");
+    if (rc >= 2) check(rc - 2, "conv_fwd_bn");
     return rc == 1;
   });
   m.def("conv_bn_fuse_rows", [](int rows) { ddp_conv_bn_fuse_rows(rows); });

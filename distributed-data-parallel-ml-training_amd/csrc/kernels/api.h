@@ -116,7 +116,8 @@ int ddp_conv_fwd(const ddp_amd::ConvGeom* g, const void* x, const void* wc, cons
                  void* y, float* stats, float* ws, size_t ws_elems, int splits, hipStream_t st);
 // as ddp_conv_fwd; when the GEMM is split-K and small enough, its finish also runs the BatchNorm
 // forward of ``bn`` (returns 1: y and the coefficient table are written, no bn_act_fwd needed),
-// else the plain conv with statistics (returns 0); negative on error
+// else the plain conv with statistics (returns 0); negative: invalid arguments; >= 2: HIP error
+// (rc - 2)
 int ddp_conv_fwd_bn(const ddp_amd::ConvGeom* g, const void* x, const void* wc, const float* bias,
                     void* z, float* stats, float* ws, size_t ws_elems, const ddp_amd::BnFwdFuse* bn,
                     hipStream_t st);

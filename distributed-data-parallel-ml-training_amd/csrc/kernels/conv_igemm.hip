@@ -2006,7 +2006,7 @@ extern "C" int ddp_conv_fwd_bn(const ConvGeom* g, const void* x, const void* wc,
   }
   launch_mode<MODE_FWD>(a, ws_elems, st);
   const int e = (int)hipGetLastError();
-  return e ? -e : done;
+  return e ? 2 + e : done;
 }
 
 static int conv_dgrad_impl(const ConvGeom* g, const void* dy, const void* wc, void* dx,
