@@ -41,6 +41,7 @@ def test_bench_json_contract(native_ext):
     cfg = r["config"]
     assert cfg["model"] == "vgg11" and cfg["global_batch"] == 256 and cfg["parallelism"] == "dp1"
     assert cfg["hipgraph"] is True
+    assert cfg["optimizer"].startswith("SGD(lr=0.1, momentum=0.9, wd=1e-4)")  # the reference's
     # value is the whole-job rate implied by the timed steps
     assert math.isclose(r["value"], cfg["global_batch"] / (r["ms_per_step"] / 1e3), rel_tol=1e-3)
     assert math.isclose(r["vs_baseline"], r["value"] / bench.BASELINE_IMG_S, rel_tol=1e-2)
