@@ -9,7 +9,7 @@ for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE
   i=$((i+1))
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --pmc $set \
       --output-format csv -d "$root/gpurun_out/pmc/p$i" -o vgg -- \
-      python3 "$root/bench.py" --steps 3 --warmup 2 > "$root/gpurun_out/pmc/p$i.log" 2>&1)
+      python3 "$root/bench.py" --steps 3 --warmup 2 --ref-window 0 ${PMC_ARGS:-} > "$root/gpurun_out/pmc/p$i.log" 2>&1)
   rc=$?; echo "pass $i rc=$rc"; tail -1 gpurun_out/pmc/p$i.log
   if [ $rc -ne 0 ]; then exit $rc; fi
 done
