@@ -106,6 +106,25 @@ PYBIND11_MODULE(_native, m) {
     return rc == 1;
   });
   m.def("conv_bn_fuse_rows", [](int rows) { ddp_conv_bn_fuse_rows(rows); });
+  // classifier-head dx + the preceding block's BN backward; bn = (z, coef, sums, pool, relu, Hz,
+  // Wz), bna = (dz, dgamma, dbeta); True when launched (dx is then not computed)
+  m.def("linear_dx_bn", [](uintptr_t dl, uintptr_t W, int B, int F, int J, uintptr_t g,
+                           py::tuple bn, py::tuple bna, uintptr_t st) {
+    ddp_amd::BnBwdFuse f{};
+    f.z = P<unsigned short>(bn[0].cast<uintptr_t>());
+    f.coef = P<float>(bn[1].cast<uintptr_t>());
+    f.sums = P<float>(bn[2].cast<uintptr_t>());
+    f.pool = bn[3].cast<int>();
+    f.relu = bn[4].cast<int>();
+    f.Hz = bn[5].cast<int>();
+    f.Wz = bn[6].cast<int>();
+    ddp_amd::BnBwdApply ap{};
+    bn_apply(bna, &ap);
+    const int rc = ddp_linear_dx_bn(P<float>(dl), P<float>(W), B, F, J, P<float>(g), &f, &ap, S(st));
+    if (rc < 0) check(rc, "linear_dx_bn");
+    if (rc >= 2) check(rc - 2, "linear_dx_bn");
+    return rc == 1;
+  });
   // direct MFMA conv for C = 8 input layers; returns False when the shape is not served
   m.def("conv_fwd_smallk", [](py::tuple g, uintptr_t x, uintptr_t wc, uintptr_t bias, uintptr_t y,
                               uintptr_t stats, uintptr_t st) {

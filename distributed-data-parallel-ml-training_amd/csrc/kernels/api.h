@@ -121,6 +121,10 @@ int ddp_conv_fwd(const ddp_amd::ConvGeom* g, const void* x, const void* wc, cons
 int ddp_conv_fwd_bn(const ddp_amd::ConvGeom* g, const void* x, const void* wc, const float* bias,
                     void* z, float* stats, float* ws, size_t ws_elems, const ddp_amd::BnFwdFuse* bn,
                     hipStream_t st);
+// classifier-head dx fused with the preceding block's whole BN backward (conv_igemm.hip
+// linear_dx_bnbwd_kernel): 1 launched, 0 not served, < 0 invalid, >= 2 HIP error (rc - 2)
+int ddp_linear_dx_bn(const float* dl, const float* W, int B, int F, int J, const float* gscale,
+                     const ddp_amd::BnBwdFuse* bn, const ddp_amd::BnBwdApply* ba, hipStream_t st);
 // row limit of the BN-fused split-K finishes (default 128 or DDP_AMD_BN_FUSE_MAX_ROWS)
 void ddp_conv_bn_fuse_rows(int rows);
 int ddp_conv_dgrad(const ddp_amd::ConvGeom* g, const void* dy, const void* wt, void* dx,

@@ -1253,9 +1253,13 @@ __global__ __launch_bounds__(256) void splitk_finish_bnfwd_kernel(FinishArgs fa,
 // Replaces the finish with memory-side sum atomics, the finalize launch and the apply launch of
 // the strong-scaling batches' 4x4 / 2x2 layers by one pass.
 template <int RPT, bool POOL>
+__device__ __forceinline__ void bnbwd_from_dx(const BnBwdFuse& bn, const BnBwdApply& ba, int Mg,
+                                              int Ng, int H, int W, float (*v)[8],
+                                              float (*wred)[2][8], int half, int lane, int c0);
+
+template <int RPT, bool POOL>
 __device__ __forceinline__ void finish_bnbwd_body(const FinishArgs& fa, const BnBwdApply& ba,
                                                   float (*wred)[2][8], int bx) {
-  constexpr int NP = POOL ? 4 : 1;
   const BnBwdFuse& bn = fa.bnf;
   const int Mg = fa.Mg, Ng = fa.Ng, splits = fa.splits;
   const int half = threadIdx.x >> 7, lane = threadIdx.x & 127;
@@ -1267,6 +1271,16 @@ __device__ __forceinline__ void finish_bnbwd_body(const FinishArgs& fa, const Bn
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[r][e] = 0.f;
   fused_finish_slabs<RPT>(fa.ws, slab, Ng, Mg, splits, lane, c0, v);
+  bnbwd_from_dx<RPT, POOL>(bn, ba, Mg, Ng, fa.H, fa.W, v, wred, half, lane, c0);
+}
+
+// The BN-backward part of finish_bnbwd_body for dx rows held in v (fp32, rounded to bf16 here
+// like a stored dgrad output): shared with the classifier-head variant (linear_dx_bnbwd_kernel).
+template <int RPT, bool POOL>
+__device__ __forceinline__ void bnbwd_from_dx(const BnBwdFuse& bn, const BnBwdApply& ba, int Mg,
+                                              int Ng, int H, int W, float (*v)[8],
+                                              float (*wred)[2][8], int half, int lane, int c0) {
+  constexpr int NP = POOL ? 4 : 1;
   float sc[8], sh[8], mu[8], is[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -1278,13 +1292,13 @@ __device__ __forceinline__ void finish_bnbwd_body(const FinishArgs& fa, const Bn
   // the block's z pixels (kept for the apply), dx rounded like the stored dgrad output
   u16x8 zz[RPT][NP];
   unsigned zoff[RPT][NP];  // (host: z has < 2^31 elements)
-  const int hw = fa.H * fa.W;
+  const int hw = H * W;
 #pragma unroll
   for (int r = 0; r < RPT; ++r) {
     const int row = lane + r * 128;
     const int rr = row < Mg ? row : 0;
     const int n = rr / hw, rem = rr - n * hw;
-    const int h = rem / fa.W, w = rem - h * fa.W;
+    const int h = rem / W, w = rem - h * W;
 #pragma unroll
     for (int d = 0; d < NP; ++d) {
       const int zh = POOL ? 2 * h + (d >> 1) : h, zw = POOL ? 2 * w + (d & 1) : w;
@@ -1331,7 +1345,7 @@ __device__ __forceinline__ void finish_bnbwd_body(const FinishArgs& fa, const Bn
   }
   __syncthreads();
   // every thread needs k1 / k2 of its 8 channels: both waves of its half add the same 2 partials
-  const float inv_m = 1.f / ((float)fa.Mg * NP);
+  const float inv_m = 1.f / ((float)Mg * NP);
   float k1[8], k2[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -1366,6 +1380,50 @@ template <int RPT, bool POOL>
 __global__ __launch_bounds__(256) void splitk_finish_bnbwd_kernel(FinishArgs fa, BnBwdApply ba) {
   __shared__ float wred[4][2][8];
   finish_bnbwd_body<RPT, POOL>(fa, ba, wred, blockIdx.x);
+}
+
+// Classifier head (Linear(F, J), J <= 16) input gradient fused with the whole BatchNorm
+// backward of the block before it (VGG: the last Conv->BN->ReLU->2x2 pool, 2x2 -> 1x1): dx =
+// (g * dlogits) . W in the order of linear_ce.hip linear_dx_block, never stored, then the same
+// per-block BN backward as the small dgrad finishes. Replaces the head's dx pass and that
+// block's reduce + finalize + apply launches (linear_bwd then only computes dW / db).
+template <int RPT>
+__global__ __launch_bounds__(256) void linear_dx_bnbwd_kernel(const float* __restrict__ dl,
+                                                              const float* __restrict__ Wt, int B,
+                                                              int F, int J, const float* gscale,
+                                                              BnBwdFuse bn, BnBwdApply ba) {
+  __shared__ float wred[4][2][8];
+  const int half = threadIdx.x >> 7, lane = threadIdx.x & 127;
+  const int c0 = blockIdx.x * 16 + half * 8;
+  const float g = gscale ? *gscale : 1.f;
+  float w[16][8];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    float4 w0 = make_float4(0.f, 0.f, 0.f, 0.f), w1 = w0;
+    if (j < J) {
+      w0 = *reinterpret_cast<const float4*>(Wt + (size_t)j * F + c0);
+      w1 = *reinterpret_cast<const float4*>(Wt + (size_t)j * F + c0 + 4);
+    }
+    w[j][0] = w0.x; w[j][1] = w0.y; w[j][2] = w0.z; w[j][3] = w0.w;
+    w[j][4] = w1.x; w[j][5] = w1.y; w[j][6] = w1.z; w[j][7] = w1.w;
+  }
+  float v[RPT][8];
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    const int row = lane + r * 128;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[r][e] = 0.f;
+    if (row >= B) continue;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (j < J) {
+        const float d = dl[(size_t)row * J + j] * g;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[r][e] += d * w[j][e];
+      }
+    }
+  }
+  bnbwd_from_dx<RPT, true>(bn, ba, B, F, 1, 1, v, wred, half, lane, c0);
 }
 
 // Split-K finish for WGRAD: dW[k][c][r][s] += sum_z slab[z][k][(r,s,c)].
@@ -1971,6 +2029,23 @@ extern "C" int ddp_conv_fwd(const ConvGeom* g, const void* x, const void* wc, co
   a.b_bytes = (int)(2 * wb);
   launch_mode<MODE_FWD>(a, ws_elems, st);
   return (int)hipGetLastError();
+}
+
+// 1: launched (dx NOT written; dz / dgamma / dbeta of the block before the head written),
+// 0: shape not served (caller runs linear_bwd with dx + that block's BN backward), < 0 invalid,
+// >= 2: HIP error (rc - 2)
+extern "C" int ddp_linear_dx_bn(const float* dl, const float* W, int B, int F, int J,
+                                const float* gscale, const BnBwdFuse* bn, const BnBwdApply* ba,
+                                hipStream_t st) {
+  if (!bn || !ba || !dl || !W) return -1;
+  if (J < 1 || J > 16 || F % 16 || B < 1 || B > 512 || !bn->pool || bn->Hz != 2 || bn->Wz != 2)
+    return 0;
+  const dim3 grid(F / 16);
+  if (B <= 128) hipLaunchKernelGGL(linear_dx_bnbwd_kernel<1>, grid, dim3(256), 0, st, dl, W, B, F, J, gscale, *bn, *ba);
+  else if (B <= 256) hipLaunchKernelGGL(linear_dx_bnbwd_kernel<2>, grid, dim3(256), 0, st, dl, W, B, F, J, gscale, *bn, *ba);
+  else hipLaunchKernelGGL(linear_dx_bnbwd_kernel<4>, grid, dim3(256), 0, st, dl, W, B, F, J, gscale, *bn, *ba);
+  const int e = (int)hipGetLastError();
+  return e ? 2 + e : 1;
 }
 
 extern "C" void ddp_conv_bn_fuse_rows(int rows) { g_bn_fuse_rows = std::max(0, rows); }

@@ -140,7 +140,8 @@ class _VGG(nn.Module):
                 cuts.append((h, leaf))
                 h = leaf
             prev = sp
-        loss = linear_cross_entropy(h.view(h.shape[0], -1), self.fc1, labels, acc, transient)
+        loss = linear_cross_entropy(h.view(h.shape[0], -1), self.fc1, labels, acc, transient,
+                                    bn_prev=plan[-1])
         return loss, cuts
 
     def n_stages(self):
@@ -163,7 +164,8 @@ class _VGG(nn.Module):
                 acc.add_(loss.detach())
             return loss
         from ..ops.layers import linear_cross_entropy
-        return linear_cross_entropy(self._features_fused(x), self.fc1, labels, acc, transient)
+        return linear_cross_entropy(self._features_fused(x), self.fc1, labels, acc, transient,
+                                    bn_prev=self.fused_plan()[-1])
 
 
 def VGG11():

@@ -159,6 +159,8 @@ BN_FWD_FUSE = os.environ.get("DDP_AMD_BN_FWD_FUSE", "1") != "0"
 # the preceding block's whole BatchNorm backward completed in a small dgrad's split-K finish
 # (conv_igemm.hip splitk_finish_bnbwd_kernel; BnBwdFuse chain only)
 BN_BWD_APPLY_FUSE = os.environ.get("DDP_AMD_BN_BWD_APPLY_FUSE", "1") != "0"
+# ... and into the classifier head's dx (linear_dx_bnbwd_kernel; needs BN_BWD_APPLY_FUSE too)
+HEAD_BN_FUSE = os.environ.get("DDP_AMD_HEAD_BN_FUSE", "1") != "0"
 BN_BWD_FUSE_MAX_HW = int(os.environ.get("DDP_AMD_BN_BWD_FUSE_MAX_HW", "16"))
 # preceding block without a max-pool (ResNet's conv1 -> conv2 -> conv3 chain): one z load per
 # dgrad output element in the epilogue would replace a whole dy + z pass of the reduce kernel,
@@ -377,8 +379,12 @@ class _LinearCEFn(torch.autograd.Function):
     same kernel."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, labels, acc, transient):
+    def forward(ctx, x, weight, bias, labels, acc, transient, bn_prev=None):
         B, F = x.shape
+        # the Conv->BN->ReLU->pool block whose output x is: its BN backward may be fused into
+        # the head's dx (conv_igemm.hip linear_dx_bnbwd_kernel)
+        ctx.bn_prev = bn_prev
+        ctx.prev_z = bn_prev.fwd_z if bn_prev is not None else None
         J = weight.shape[0]
         check(x, BF16, name="linear input")
         labels = labels.to(torch.int64).contiguous()
@@ -398,20 +404,38 @@ class _LinearCEFn(torch.autograd.Function):
         g = g.contiguous().float()
         gw = ensure_grad(weight)
         gb = ensure_grad(bias) if bias is not None else None
+        prev, pz = ctx.bn_prev, ctx.prev_z
+        ctx.prev_z = None
+        if (prev is not None and pz is not None and ctx.needs_input_grad[0] and BN_BWD_APPLY_FUSE
+                and HEAD_BN_FUSE
+                and _common.BN_BWD_FUSE and prev.pool and not prev.residual
+                and pz.shape[1] == 2 and pz.shape[2] == 2 and prev.K == F):
+            dz_prev = torch.empty_like(pz)
+            done = native().linear_dx_bn(
+                ptr(dl), ptr(weight), B, F, J, ptr(g),
+                (ptr(pz), ptr(prev.coef), ptr(prev.sums), 1, int(prev.relu), 2, 2),
+                (ptr(dz_prev), ptr(ensure_grad(prev.bn.weight)), ptr(ensure_grad(prev.bn.bias))),
+                stream_handle())
+            if done:  # dx never materialised: the block's backward takes dz_prev
+                native().linear_bwd(ptr(dl), ptr(x), ptr(weight), B, F, J, ptr(g), 0, ptr(gw),
+                                    ptr(gb), stream_handle())
+                prev.dz_fused = dz_prev
+                grad_ready([weight, bias])
+                return torch.empty_like(x), None, None, None, None, None, None
         dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
         native().linear_bwd(ptr(dl), ptr(x), ptr(weight), B, F, J, ptr(g), ptr(dx), ptr(gw),
                             ptr(gb), stream_handle())
         grad_ready([weight, bias])
-        return dx, None, None, None, None, None
+        return dx, None, None, None, None, None, None
 
 
-def linear_cross_entropy(x, linear, labels, acc=None, transient=False):
+def linear_cross_entropy(x, linear, labels, acc=None, transient=False, bn_prev=None):
     """mean CE(linear(x), labels) in one kernel (J <= 16); see _LinearCEFn. ``transient=True``
     returns the loss in the per-forward scratch (saves a fill launch; valid until the next
     model forward on this device — the captured training step uses it)."""
     if linear.weight.shape[0] > 16:
         raise ValueError("linear_cross_entropy supports at most 16 outputs")
-    return _LinearCEFn.apply(x, linear.weight, linear.bias, labels, acc, transient)
+    return _LinearCEFn.apply(x, linear.weight, linear.bias, labels, acc, transient, bn_prev)
 
 
 def linear_small(x, linear):

@@ -288,11 +288,11 @@ def test_bn_fused_into_splitk_finishes_matches_unfused(native_ext):
     """BatchNorm forward fused into the split-K finish of the small forward GEMMs and the
     preceding block's whole BatchNorm backward completed in the small dgrads' finishes
     (ops.layers BN_FWD_FUSE / BN_BWD_APPLY_FUSE, conv_igemm.hip splitk_finish_bnfwd_kernel /
-    splitk_finish_bnbwd_kernel) vs the separate finish + BN kernels, at the 8-GPU share of the
+    splitk_finish_bnbwd_kernel, and the head's linear_dx_bnbwd_kernel) vs the separate finish +
+    BN kernels, at the 8-GPU share of the
     reference batch (32 images): same loss, gradients within the run-to-run spread of two
     unfused runs; the fused launches must actually be taken."""
     from ddp_amd.models import VGG11
-    from ddp_amd.engine import CrossEntropyLoss
     from ddp_amd.optim import FusedSGD
     from ddp_amd.ops import layers
     from ddp_amd.ops.common import native
@@ -302,8 +302,9 @@ def test_bn_fused_into_splitk_finishes_matches_unfused(native_ext):
     x = torch.randn(32, 3, 32, 32, device="cuda")
     y = torch.randint(0, 10, (32,), device="cuda")
     nat = native()
-    taken = {"fwd": 0, "bwd": 0}
-    orig = {k: getattr(nat, k) for k in ("conv_fwd_bn", "conv_bwd_pair", "conv_dgrad")}
+    taken = {"fwd": 0, "bwd": 0, "head": 0}
+    orig = {k: getattr(nat, k) for k in ("conv_fwd_bn", "conv_bwd_pair", "conv_dgrad",
+                                         "linear_dx_bn")}
 
     def spy(name, key):
         def f(*args, **kw):
@@ -314,6 +315,7 @@ def test_bn_fused_into_splitk_finishes_matches_unfused(native_ext):
     nat.conv_fwd_bn = spy("conv_fwd_bn", "fwd")
     nat.conv_bwd_pair = spy("conv_bwd_pair", "bwd")
     nat.conv_dgrad = spy("conv_dgrad", "bwd")
+    nat.linear_dx_bn = spy("linear_dx_bn", "head")
     losses, grads = [], []
     saved = (layers.BN_FWD_FUSE, layers.BN_BWD_APPLY_FUSE)
     try:
@@ -321,7 +323,7 @@ def test_bn_fused_into_splitk_finishes_matches_unfused(native_ext):
             layers.BN_FWD_FUSE = layers.BN_BWD_APPLY_FUSE = fuse
             opt = FusedSGD(m.parameters(), lr=0.1)
             opt.zero_grad()
-            loss = CrossEntropyLoss()(m(x), y)
+            loss = m.forward_loss(x, y)  # the captured step's fused classifier + loss
             loss.backward()
             torch.cuda.synchronize()
             losses.append(float(loss))
@@ -330,7 +332,7 @@ def test_bn_fused_into_splitk_finishes_matches_unfused(native_ext):
         layers.BN_FWD_FUSE, layers.BN_BWD_APPLY_FUSE = saved
         for k, v in orig.items():
             setattr(nat, k, v)
-    assert taken["fwd"] >= 2 and taken["bwd"] >= 1, taken
+    assert taken["fwd"] >= 2 and taken["bwd"] >= 1 and taken["head"] == 1, taken
     assert abs(losses[0] - losses[1]) < 2e-2 * abs(losses[1]) + 1e-3, losses
 
     def cos(u, v):
