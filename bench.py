@@ -73,11 +73,33 @@ def parse():
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--train-size", type=int, default=None)
     p.add_argument("--json-out", default=None)
+    p.add_argument("--launch-timeout", type=float, default=3600.0,
+                   help="self-launch (--gpus N > 1 without torchrun): kill every rank and fail "
+                        "after this many seconds")
     return p.parse_args()
+
+
+def launch_or_check(args):
+    """``--gpus N`` without an outer launcher spawns N ranks of this script (one process per
+    GPU, ddp_amd/utils/launch.py) and returns the parent's exit code; under a launcher it checks
+    that WORLD_SIZE matches --gpus. Returns None when this process is a rank that should run."""
+    from ddp_amd.utils.launch import self_launch, under_launcher
+    if not under_launcher():
+        if args.gpus > 1:
+            return self_launch(__file__, sys.argv[1:], args.gpus, timeout_s=args.launch_timeout)
+        return None
+    world = int(os.environ["WORLD_SIZE"])
+    if world != args.gpus:
+        raise SystemExit(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report "
+                         f"a {world}-rank run as {args.gpus} GPUs")
+    return None
 
 
 def main():
     args = parse()
+    rc = launch_or_check(args)
+    if rc is not None:
+        sys.exit(rc)
     import torch
     import torch.distributed as dist
     import ddp_amd
@@ -93,13 +115,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    ndev = torch.cuda.device_count()
+    if ndev < min(world, args.gpus) or local_rank >= ndev:
+        raise SystemExit(f"[bench] rank {rank}: {ndev} GPU(s) visible for {world} ranks "
+                         f"(LOCAL_RANK {local_rank})")
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)  # control plane (TCPStore)
     comm = RcclCommunicator(rank, world, local_rank)
+    # proof of the rank count: what RCCL itself reports for the data-plane communicator
+    rccl_ranks = comm.comm.count()
+    if world > 1 and rccl_ranks != world:
+        raise SystemExit(f"[bench] RCCL communicator has {rccl_ranks} ranks, expected {world}")
     # failure detection: on >1 ranks a watchdog thread aborts the RCCL
     # communicator and exits non-zero when no progress is reported for DDP_AMD_WATCHDOG_S
     # seconds (default 300) or RCCL reports an async error, instead of hanging on a dead peer
@@ -141,14 +169,13 @@ def main():
                                         default_cuts(args.model, B) if world > 1 else "0")
     cuts = [int(v) for v in str(args.segmented).split(",") if int(v) > 0]
     segmented = bool(cuts) and args.strategy == "ddp" and not args.no_graph
-    if args.bucket_mb == "auto" and not args.no_graph:
-        # captured step: the DDP reducer's collectives are inline in the graph (or bypassed by
-        # the pipelined step): one bucket = one collective, the least latency
-        args.bucket_mb = args.first_bucket_mb = 1 << 16
     if args.strategy == "ddp":
+        # captured step (``captured``): the reducer's collectives are inline in the graph (or
+        # bypassed by the pipelined step) -> 'auto' plans one bucket = one collective
         model = DistributedDataParallel(model, comm, bucket_cap_mb=args.bucket_mb,
                                         first_bucket_cap_mb=args.first_bucket_mb,
-                                        grad_comm_dtype=args.grad_comm)
+                                        grad_comm_dtype=args.grad_comm,
+                                        captured=not args.no_graph)
     else:
         fn = STRATEGIES[args.strategy]
         sync = lambda m: fn(m, comm)  # noqa: E731
@@ -228,6 +255,7 @@ def main():
     consistent = True
     if world > 1:
         consistent = check_replicas(arena, world)
+    plan = comm_plan(args, world, step, model, cuts, segmented)
     ms = elapsed / args.steps * 1000.0
     value = global_batch * args.steps / elapsed
     out = {
@@ -257,6 +285,14 @@ def main():
                                                          lambda: False)() else "inline"),
                    "optimizer": f"SGD(lr={lr:g}, momentum=0.9, wd=1e-4) fused" +
                                 (", ZeRO-1 sharded" if args.zero else "")},
+        "launcher": os.environ.get("DDP_AMD_LAUNCHER",
+                                   "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ
+                                   else ("env" if world > 1 else "single-process")),
+        "rccl_ranks": rccl_ranks,
+        "device_count": torch.cuda.device_count(),
+        "rccl_version": _version_str(native_version()),
+        "gpu": torch.cuda.get_device_name(local_rank),
+        "comm_plan": plan,
         "avg_ms_iter_1_39": round(ref_ms, 4) if ref_ms is not None else None,
         "img_s_iter_1_39": round(global_batch / ref_ms * 1000.0, 2) if ref_ms else None,
         "train_loss_mean": round(loss, 4),
@@ -273,6 +309,43 @@ def main():
         watchdog.stop()
     if world > 1:
         dist.destroy_process_group()
+
+
+def native_version():
+    from ddp_amd.ops.common import native
+    return native().RcclComm.version()
+
+
+def _version_str(v):
+    # NCCL_VERSION_CODE = major * 10000 + minor * 100 + patch (>= 2.9)
+    return f"{v // 10000}.{v // 100 % 100}.{v % 100}" if v else None
+
+
+def comm_plan(args, world, step, model, cuts, segmented):
+    """Which gradient-communication plan this run used: collective granularity, bucket bytes
+    on the wire, wire dtype, and the all-reduce bandwidth table (parallel/comm_tuning.json,
+    "model" until tools/comm_bench.py --write-table measured a node) with its knee."""
+    from ddp_amd.parallel.bucket_plan import knee_bytes, load_table, rows_for
+    wire = 2 if args.grad_comm == "bf16" else 4
+    rows, source = rows_for(load_table(), max(world, 2), args.grad_comm)
+    out = {"wire": args.grad_comm, "comm_table": source,
+           "comm_table_knee_bytes": knee_bytes(rows) if rows else None,
+           "collectives_live": world > 1}
+    if segmented:
+        out.update(kind="pipelined segments (bucket all-reduce + its SGD under the earlier "
+                        "layers' backward)", cuts=cuts,
+                   bucket_bytes=[(hi - lo) * wire for (_, (lo, hi)) in step.buckets],
+                   zero=bool(args.zero))
+    elif args.strategy == "ddp":
+        out.update(kind="reducer buckets, inline in the captured step" if not args.no_graph
+                   else "reducer buckets, comm stream", cuts=[],
+                   bucket_bytes=[int(b[3]) * wire for b in getattr(model, "buckets", [])],
+                   reason=getattr(model, "bucket_plan_reason", None))
+    else:
+        n = sum(1 for _ in model.parameters())
+        out.update(kind=f"per-parameter {args.strategy} ({n} collectives)", cuts=[],
+                   bucket_bytes=None)
+    return out
 
 
 if __name__ == "__main__":

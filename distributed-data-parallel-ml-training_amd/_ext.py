@@ -32,7 +32,7 @@ def load():
         return _module
     import torch  # noqa: F401  (load torch's HIP runtime first)
     # DDP_AMD_NATIVE_PATH: load another build of the same extension (A/B of kernel variants in
-    # one GPU session, tools/ab_variants.sh); the in-tree build is the default
+    # one GPU session, tools/gpu/ab_build.sh); the in-tree build is the default
     path = os.environ.get("DDP_AMD_NATIVE_PATH") or so_path()
     if not os.path.exists(path):
         raise RuntimeError(

@@ -435,6 +435,8 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("rank", &RcclComm::rank)
       .def_property_readonly("world", &RcclComm::world)
       .def_property_readonly("live", &RcclComm::live)
+      .def("count", &RcclComm::count)
+      .def_static("version", &RcclComm::version)
       .def("all_reduce", [](RcclComm& c, uintptr_t buf, size_t n, int dt, int op, uintptr_t st) {
         c.all_reduce(P<void>(buf), n, dt, op, S(st));
       })

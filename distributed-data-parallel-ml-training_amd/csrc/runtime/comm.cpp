@@ -72,6 +72,20 @@ RcclComm::RcclComm(int rank, int world, const std::string& uid_bytes, int device
 
 RcclComm::~RcclComm() {
   if (comm_ && !aborted_) ncclCommDestroy(comm_);
+  if (stage_) hipFree(stage_);
+}
+
+int RcclComm::count() const {
+  if (!comm_) return 0;
+  int n = 0;
+  NCCL_OK(ncclCommCount(comm_, &n));
+  return n;
+}
+
+int RcclComm::version() {
+  int v = 0;
+  NCCL_OK(ncclGetVersion(&v));
+  return v;
 }
 
 std::string RcclComm::make_unique_id() {
@@ -164,8 +178,28 @@ void RcclComm::scatter(const void* send, void* recv, size_t count, int dtype, in
 }
 
 void RcclComm::scatter_replicated(void* buf, size_t count, int dtype, int root, hipStream_t st) {
-  if (world_ == 1 || count == 0) return;
+  if (count == 0) return;
   const ncclDataType_t dt = to_nccl(dtype);
+  if (world_ == 1) {
+    if (comm_ == nullptr) return;  // no communicator: the root already holds the data
+    // single-rank live communicator (one-GPU box): the root's copy travels through a grouped
+    // self send/recv into a staging buffer that starts as all-ones bytes (NaN for every float
+    // dtype) and is copied back, so the receive half of 2A's point-to-point plane really runs
+    // and a receive that wrote nothing shows up as NaN in buf (tests/test_gpu_rccl_self.py)
+    const size_t bytes = count * dtype_bytes(dtype);
+    if (bytes > stage_bytes_) {
+      if (stage_) HIP_OK(hipFree(stage_));
+      HIP_OK(hipMalloc(&stage_, bytes));
+      stage_bytes_ = bytes;
+    }
+    HIP_OK(hipMemsetAsync(stage_, 0xff, bytes, st));
+    NCCL_OK(ncclGroupStart());
+    NCCL_OK(ncclSend(buf, count, dt, rank_, comm_, st));
+    NCCL_OK(ncclRecv(stage_, count, dt, rank_, comm_, st));
+    NCCL_OK(ncclGroupEnd());
+    HIP_OK(hipMemcpyAsync(buf, stage_, bytes, hipMemcpyDeviceToDevice, st));
+    return;
+  }
   NCCL_OK(ncclGroupStart());
   if (rank_ == root) {
     for (int r = 0; r < world_; ++r)

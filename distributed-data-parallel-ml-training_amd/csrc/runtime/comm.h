@@ -36,6 +36,9 @@ class RcclComm {
   int world() const { return world_; }
   bool live() const { return comm_ != nullptr; }  // collectives reach RCCL
   ncclComm_t raw() const { return comm_; }
+  // ranks in the RCCL communicator (ncclCommCount; 0 without one) and the library version
+  int count() const;
+  static int version();
 
   void all_reduce(void* buf, size_t count, int dtype, int op, hipStream_t st);
   void broadcast(void* buf, size_t count, int dtype, int root, hipStream_t st);
@@ -58,6 +61,8 @@ class RcclComm {
   int rank_, world_, device_;
   ncclComm_t comm_ = nullptr;
   bool aborted_ = false;
+  void* stage_ = nullptr;     // world-1 scatter_replicated receive staging (grown on demand)
+  size_t stage_bytes_ = 0;
 };
 
 class Reducer {

@@ -54,8 +54,12 @@ def main(part, argv=None):
     model = build(args.model).to(device)
     comm = make_communicator(device) if distributed else None
     if strategy == "ddp":
+        # --graph on a GPU captures the step (TrainStep: inline collectives, one bucket is
+        # best) unless the pipelined segmented step takes over (its own per-segment buckets)
+        captured = bool(args.graph) and torch.device(device).type == "cuda"
         model = DistributedDataParallel(model, comm, bucket_cap_mb=args.bucket_mb,
-                                        first_bucket_cap_mb=args.first_bucket_mb)
+                                        first_bucket_cap_mb=args.first_bucket_mb,
+                                        captured=captured)
     optimizer = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=0.0001)
     if args.resume:
         load_checkpoint(args.resume, model, optimizer)

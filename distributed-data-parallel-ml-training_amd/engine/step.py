@@ -47,6 +47,9 @@ class TrainStep:
         self.loss_sum = torch.zeros((), dtype=torch.float32, device=dev)
         self._one = torch.ones((), dtype=torch.float32, device=dev)
         self.graph = None
+        # set when a captured step was found to diverge across replicas (validate_distributed):
+        # later capture() calls (a new epoch re-captures) keep running eager steps
+        self.eager_only = False
         self.fused = self._fused_loss()
         self.fold_opt = bool(getattr(optimizer, "_fused", False)) and hasattr(loader, "cursor_advance")
         if self.fold_opt:
@@ -95,7 +98,8 @@ class TrainStep:
         torch.cuda.current_stream().wait_stream(s)
 
     def capture(self):
-        if not self.use_graph:
+        if not self.use_graph or self.eager_only:
+            self.graph = None
             return
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
@@ -163,7 +167,8 @@ class TrainStep:
                                "(collective hang inside the hipGraph?)")
         if check_replicas(arena, world):
             return True
-        self.graph = None  # divergent replicas under replay: run eagerly from now on
+        self.graph = None  # divergent replicas under replay: run eagerly from now on ...
+        self.eager_only = True  # ... including after a later capture() (next epoch)
         return False
 
     def pop_loss(self):
@@ -382,6 +387,9 @@ class SegmentedDDPStep(TrainStep):
             self._comm(j)
 
     def capture(self):
+        if self.eager_only:
+            self.graph = self.graphs = None
+            return
         torch.cuda.synchronize()
         self.check_error()
         mode = capture_mode()

@@ -69,7 +69,11 @@ class ConvBNActSpec:
         self.fwd_z = None
         self.sums_ready = False
         # set by the next block's backward when its dgrad finish completed this block's BN
-        # backward (BN_BWD_APPLY_FUSE): the gradient at this block's conv output
+        # backward (BN_BWD_APPLY_FUSE): (gradient at this block's conv output, the conv output
+        # z of the forward it belongs to). The gradient the next block then hands autograd for
+        # this block's output is NOT materialised (uninitialised memory, also as a pipelined
+        # step's leaf.grad): this block's backward must take dz_fused instead, and checks that
+        # it belongs to the same forward; every forward clears it.
         self.dz_fused = None
 
     def pack_desc(self):
@@ -238,6 +242,7 @@ class _ConvBNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, gamma, beta, residual, spec, in_link=None, res_link=None):
         spec.maybe_pack()
+        spec.dz_fused = None  # a fused BN backward of an earlier pass must never be consumed
         N, H, W, _ = x.shape
         stats = spec.stats  # zeroed by the model's per-forward StepScratch.zero()
         P, Q = spec.out_hw(H, W)
@@ -278,7 +283,6 @@ class _ConvBNActFn(torch.autograd.Function):
     def backward(ctx, dy):
         spec = ctx.spec
         x, z, stats, weight, bias, gamma, beta, residual = ctx.saved_tensors
-        dy = dy.contiguous()
         N, P, Q, K = z.shape
         sums = spec.sums  # zeroed together with the statistics at the start of the forward
         dres = torch.empty_like(z) if (ctx.has_res and ctx.needs_input_grad[5]) else None
@@ -292,8 +296,12 @@ class _ConvBNActFn(torch.autograd.Function):
         if dz_done is not None:
             # the next block's dgrad finish already ran this block's whole BN backward (dz,
             # dgamma, dbeta; conv_igemm.hip splitk_finish_bnbwd_kernel): dy was never written
-            dz = dz_done
+            dz, zref = dz_done
+            if zref is None or zref.data_ptr() != z.data_ptr():
+                raise RuntimeError("fused BatchNorm backward belongs to another forward pass "
+                                   "(stale dz_fused): refusing to use an unwritten gradient")
         else:
+            dy = dy.contiguous()
             dz = torch.empty_like(z)
             native().bn_act_bwd(N, P, Q, K, int(spec.pool), int(spec.relu), spec.eps, ptr(z),
                                 ptr(residual), ptr(stats), ptr(gamma), ptr(beta), ptr(dy),
@@ -320,8 +328,8 @@ class _ConvBNActFn(torch.autograd.Function):
         if bna is not None:
             dx, done = conv_backward(spec, x, dz, gw, ctx.needs_input_grad[0], ctx.in_link,
                                      weight=weight, bnf=bnf, bna=bna)
-            if done:
-                prev.dz_fused = dz_prev  # prev's backward skips its BN backward
+            if done:  # prev's backward skips its BN backward; dx was not written
+                prev.dz_fused = (dz_prev, ctx.prev_z)
             else:
                 prev.sums_ready = True
         else:
@@ -419,7 +427,7 @@ class _LinearCEFn(torch.autograd.Function):
             if done:  # dx never materialised: the block's backward takes dz_prev
                 native().linear_bwd(ptr(dl), ptr(x), ptr(weight), B, F, J, ptr(g), 0, ptr(gw),
                                     ptr(gb), stream_handle())
-                prev.dz_fused = dz_prev
+                prev.dz_fused = (dz_prev, pz)
                 grad_ready([weight, bias])
                 return torch.empty_like(x), None, None, None, None, None, None
         dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None

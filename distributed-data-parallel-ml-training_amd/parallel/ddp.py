@@ -212,7 +212,8 @@ class _PyReducer:
 
 class DistributedDataParallel(nn.Module):
     def __init__(self, module, comm, bucket_cap_mb=25.0, first_bucket_cap_mb=1.0,
-                 broadcast_buffers=True, average=True, overlap=None, grad_comm_dtype="fp32"):
+                 broadcast_buffers=True, average=True, overlap=None, grad_comm_dtype="fp32",
+                 captured=False):
         super().__init__()
         self.module = module
         self.comm = comm
@@ -227,8 +228,10 @@ class DistributedDataParallel(nn.Module):
             # sized from the all-reduce bandwidth table for this world size (bucket_plan.py)
             from .bucket_plan import choose_bucket_caps
             wire = 2 if grad_comm_dtype == "bf16" else 4
+            # ``captured``: the step will be captured into one hipGraph, whose bucket
+            # collectives are issued inline (no overlap to buy): one bucket
             cap_b, first_b, self.bucket_plan_reason = choose_bucket_caps(
-                comm.world, self.arena.total * wire, overlap=True,
+                comm.world, self.arena.total * wire, overlap=not captured,
                 dtype="bf16" if grad_comm_dtype == "bf16" else "fp32")
             # the planner counts fp32 arena bytes
             cap, cap_first = cap_b * 4 // wire, first_b * 4 // wire
@@ -354,7 +357,14 @@ class DistributedDataParallel(nn.Module):
         if not seq:
             return
         order = list(self.reducer.order_from_ready(seq))
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        if self.comm.world > 1:
+            # every rank must launch the buckets in the same order: take rank 0's observation
+            # through the control plane. Without one that spans exactly this communicator's
+            # ranks, locally observed orders could differ (hang / mixed-up buckets): keep the
+            # plan order, which is identical everywhere by construction.
+            if not (dist.is_available() and dist.is_initialized()
+                    and dist.get_world_size() == self.comm.world):
+                return
             box = [order]
             dist.broadcast_object_list(box, src=0)  # control plane (TCPStore / Gloo)
             order = box[0]

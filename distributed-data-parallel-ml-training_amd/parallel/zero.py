@@ -24,19 +24,58 @@ import torch
 
 class ShardedUpdate:
     def __init__(self, arena, optimizer, comm, buckets):
-        """``buckets``: list of ((i0, i1), (lo, hi)) — parameter and element ranges."""
+        """``buckets``: list of ((i0, i1), (lo, hi)) — parameter and element ranges.
+
+        A bucket whose element count does not divide by the world size (arena slices are only
+        64-element aligned: worlds 3, 5, 6, 7) is sharded unevenly — ranks 0..e-1 own
+        ceil(n/w) elements, the rest floor(n/w) — and its collectives run on a [w, ceil(n/w)]
+        zero-padded staging image (two strided copies in, two out) so every rank's
+        reduce-scatter / all-gather chunk has the same size."""
         self.arena, self.opt, self.comm = arena, optimizer, comm
         self.world, self.rank = comm.world, comm.rank
         self.buckets = [tuple(map(tuple, b)) for b in buckets]
         for (_, (lo, hi)) in self.buckets:
-            if (hi - lo) % self.world:
-                raise ValueError(f"bucket of {hi - lo} elements is not divisible by the world "
-                                 f"size {self.world} (ZeRO-1 needs equal shards)")
+            if hi - lo < self.world:
+                raise ValueError(f"bucket of {hi - lo} elements is smaller than the world size "
+                                 f"{self.world}")
+        per = max(-(-(hi - lo) // self.world) for (_, (lo, hi)) in self.buckets)
+        self._stage = None
+        if any((hi - lo) % self.world for (_, (lo, hi)) in self.buckets):
+            self._stage = torch.zeros(2, self.world * per, dtype=arena.data.dtype,
+                                      device=arena.data.device)
+
+    def _split(self, j):
+        (_, (lo, hi)) = self.buckets[j]
+        n = hi - lo
+        base, extra = divmod(n, self.world)
+        return lo, n, base, extra
 
     def shard(self, j):
-        (_, (lo, hi)) = self.buckets[j]
-        n = (hi - lo) // self.world
-        return lo + self.rank * n, lo + (self.rank + 1) * n
+        lo, n, base, extra = self._split(j)
+        r = self.rank
+        s0 = lo + r * base + min(r, extra)
+        return s0, s0 + base + (1 if r < extra else 0)
+
+    def _image(self, buf, j):
+        """[w, per] view of staging row ``buf`` for bucket j (per = ceil(n/w))."""
+        lo, n, base, extra = self._split(j)
+        per = base + (1 if extra else 0)
+        return self._stage[buf, :self.world * per].view(self.world, per)
+
+    def _pack(self, src, img, j):
+        lo, n, base, extra = self._split(j)
+        k = extra * (base + 1)
+        if extra:
+            img[:extra, :base + 1].copy_(src[:k].view(extra, base + 1))
+            img[extra:, base:].zero_()
+        img[extra:, :base].copy_(src[k:].view(self.world - extra, base))
+
+    def _unpack(self, img, dst, j):
+        lo, n, base, extra = self._split(j)
+        k = extra * (base + 1)
+        if extra:
+            dst[:k].view(extra, base + 1).copy_(img[:extra, :base + 1])
+        dst[k:].view(self.world - extra, base).copy_(img[extra:, :base])
 
     @torch.no_grad()
     def step(self, j, stream=None, counter=None, skip=None):
@@ -47,10 +86,20 @@ class ShardedUpdate:
         ctx = torch.cuda.stream(stream) if (cuda and stream is not None) else _null()
         with ctx:
             g, p = a.grad[lo:hi], a.data[lo:hi]
-            self.comm.reduce_scatter_inplace(g, AVG, stream=stream)
             s0, s1 = self.shard(j)
-            self.opt.step_elements(s0, s1, stream=stream, counter=counter, skip=skip)
-            self.comm.all_gather_inplace(p, stream=stream)
+            if (hi - lo) % self.world == 0:
+                self.comm.reduce_scatter_inplace(g, AVG, stream=stream)
+                self.opt.step_elements(s0, s1, stream=stream, counter=counter, skip=skip)
+                self.comm.all_gather_inplace(p, stream=stream)
+            else:  # uneven shards through the padded [w, per] staging image
+                gi, pi = self._image(0, j), self._image(1, j)
+                self._pack(g, gi, j)
+                self.comm.reduce_scatter_inplace(gi.view(-1), AVG, stream=stream)
+                a.grad[s0:s1].copy_(gi[self.rank, :s1 - s0])
+                self.opt.step_elements(s0, s1, stream=stream, counter=counter, skip=skip)
+                self._pack(p, pi, j)
+                self.comm.all_gather_inplace(pi.view(-1), stream=stream)
+                self._unpack(pi, p, j)
             self.opt.repack_params(i0, i1, stream=stream)
             g.zero_()
 

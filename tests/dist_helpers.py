@@ -302,10 +302,12 @@ def zero_worker(rank, world, port, q, steps):
             if upd is not None:
                 out["grad_zero"] = bool((ddp.arena.grad == 0).all())
                 out["shards"] = shards
+                out["bucket_sizes"] = [hi - lo for (_, (lo, hi)) in upd.buckets]
         dist.destroy_process_group()
         q.put((rank, {"replicated": out["replicated"].numpy(), "zero": out["zero"].numpy(),
                       "rc": out["replicated_consistent"], "zc": out["zero_consistent"],
-                      "grad_zero": out["grad_zero"], "shards": out["shards"]}))
+                      "grad_zero": out["grad_zero"], "shards": out["shards"],
+                      "bucket_sizes": out["bucket_sizes"]}))
     except Exception:
         import traceback
         q.put((rank, {"error": traceback.format_exc()}))

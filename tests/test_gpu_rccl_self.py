@@ -141,6 +141,18 @@ def test_self_comm_gather_runs_point_to_point(native_ext):
     torch.cuda.synchronize()
     assert torch.equal(buf[0], t)
     assert c.comm.async_error() == 0
+    assert c.comm.count() == 1 and c.comm.version() > 0
+    # scatter half (part2/part2a/main.py:110,115): grouped self send/recv into a staging buffer
+    # that starts as all-ones bytes (NaN) and is copied back — a recv that wrote nothing would
+    # leave NaN in the gradient; fp32 and bf16 wires
+    for dt in (torch.float32, torch.bfloat16):
+        g = torch.randn(54321, device="cuda").to(dt)
+        ref = g.clone()
+        c.scatter_replicated(g, src=0)
+        torch.cuda.synchronize()
+        assert not torch.isnan(g.float()).any()
+        assert torch.equal(g, ref)
+    assert c.comm.async_error() == 0
 
     torch.manual_seed(5)
     m = VGG11().cuda()
@@ -159,6 +171,9 @@ def test_self_comm_gather_runs_point_to_point(native_ext):
     assert torch.equal(st[:last.numel()], ref[-1].reshape(-1))
     for p, r in zip(params, ref):
         assert torch.equal(p.grad, r)
+    # the scatter's staging (RcclComm's own) must have been written by the recv for every
+    # parameter: a NaN left by a receive that did not run would have reached p.grad above
+    assert all(not torch.isnan(p.grad).any() for p in params)
 
 
 def test_eager_ddp_overlaps_backward_on_comm_stream(native_ext):

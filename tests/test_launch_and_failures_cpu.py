@@ -37,11 +37,34 @@ def test_reference_style_rank_maps_to_its_own_gpu(monkeypatch):
     assert pick_device("auto", local_rank=local_rank_of(0)) == torch.device("cuda", 5)
 
 
-def test_apps_main_passes_the_rank_to_pick_device():
-    import inspect
+class _Stop(Exception):
+    pass
+
+
+@pytest.mark.parametrize("rank,ndev,expect", [(3, 8, 3), (3, 2, 1), (0, 4, 0)])
+def test_apps_main_puts_reference_rank_on_its_gpu(monkeypatch, rank, ndev, expect):
+    """``part3/main.py --num-nodes 4 --rank R`` (reference flags, no LOCAL_RANK) selects GPU
+    R % ndev before joining the process group: run the real main() with a mocked device count
+    and stop it at the rendezvous."""
     from ddp_amd.engine import apps
-    src = inspect.getsource(apps.main)
-    assert "pick_device(args.device, local_rank=local_rank_of(rank))" in src
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: ndev)
+    monkeypatch.setattr(torch.cuda, "set_device", lambda d: None)
+    monkeypatch.delenv("LOCAL_RANK", raising=False)
+    seen = {}
+
+    def rendezvous(ip, port, r, world, backend="gloo"):
+        seen.update(rank=r, world=world)
+        raise _Stop
+
+    chosen = []
+    real_pick = apps.pick_device
+    monkeypatch.setattr(apps, "pick_device", lambda *a, **k: chosen.append(real_pick(*a, **k)) or chosen[-1])
+    monkeypatch.setattr(apps, "init_distributed_setup", rendezvous)
+    with pytest.raises(_Stop):
+        apps.main("part3", ["--num-nodes", "4", "--rank", str(rank), "--master-ip", "127.0.0.1"])
+    assert seen == {"rank": rank, "world": 4}
+    assert chosen == [torch.device("cuda", expect)]
 
 
 @pytest.mark.parametrize("n,B,world", [(50000, 256, 1), (50000, 128, 2), (50000, 32, 8),

@@ -1,4 +1,4 @@
-"""ZeRO-1 sharded optimizer update (parallel/zero.py) on Gloo, 2 and 4 ranks: after k steps the
+"""ZeRO-1 sharded optimizer update (parallel/zero.py) on Gloo, 2, 4 and 5 ranks: after k steps the
 parameters equal the replicated DDP path's (bit-identical on 2 ranks, where a reduce-scatter
 and an all-reduce add the same two values; to fp32 rounding of the reduction order on 4), the
 replicas are bit-identical, each rank owns a disjoint 1/N shard of every bucket, and the
@@ -9,7 +9,7 @@ import torch
 from dist_helpers import run_workers, zero_worker
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 5])
 def test_zero_matches_replicated(world):
     out = run_workers(zero_worker, world, 3)
     for r, v in out.items():
@@ -20,11 +20,23 @@ def test_zero_matches_replicated(world):
     rep, zer = out[0]["replicated"], out[0]["zero"]
     if world == 2:
         assert torch.equal(rep, zer)
-    else:
+    elif world == 4:
         assert torch.allclose(rep, zer, rtol=1e-5, atol=1e-6)
+    else:
+        # 5 ranks: the reduce-scatter and the all-reduce sum in different orders; after 1-2
+        # steps the results differ by 1 ulp, by step 3 a handful of elements have drifted
+        # further through the BatchNorm backward (measured: relative norm 2.4e-6, max 1.3e-5;
+        # a wrong shard mapping would be O(1))
+        assert float((rep - zer).norm() / rep.norm()) < 2e-5
+        assert float((rep - zer).abs().max()) < 1e-3
     assert not torch.equal(zer, torch.zeros_like(zer))
-    # shards: disjoint, equal-sized, covering every bucket
+    # shards: disjoint, contiguous, sizes differing by at most one element (world 5: the
+    # 64-aligned buckets do not divide evenly -> padded staging image, parallel/zero.py)
     for j in range(3):
         spans = sorted(tuple(out[r]["shards"][j]) for r in range(world))
+        sizes = [b - a for a, b in spans]
         for (a0, a1), (b0, b1) in zip(spans, spans[1:]):
-            assert a1 == b0 and a1 - a0 == b1 - b0
+            assert a1 == b0
+        assert max(sizes) - min(sizes) <= 1 and min(sizes) > 0
+    if world == 5:
+        assert any(s % 5 for s in out[0]["bucket_sizes"]), "world 5 must exercise uneven shards"

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Same-session A/B of native-extension builds: in-tree ("cur") vs ab_so/_native_<name>.so.
-#   VARIANTS="old cur" PROF=1 bash tools/ab_variants.sh
+#   VARIANTS="old cur" PROF=1 bash tools/gpu/ab_build.sh
 # Benches interleaved over two passes; PROF=1 adds a rocprofv3 --stats run of VGG-11 b256 and
 # b32 per variant (kernel tables under gpurun_out/ab_var/prof_<variant>_b<batch>/).
 cd "$GRAFT_REPO_ROOT" || exit 2

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Same-session A/B of environment settings: GPU kernel + model tests, then bench.py for every
 # variant x config, two interleaved passes; optional rocprofv3 table of the last variant at b32.
-#   VARIANTS="base: r512:DDP_AMD_BN_BWD_FUSE_MAX_ROWS=512" CFGS="vgg11:32 vgg11:256" bash tools/gpu_ab_env.sh
+#   VARIANTS="base: r512:DDP_AMD_BN_BWD_FUSE_MAX_ROWS=512" CFGS="vgg11:32 vgg11:256" bash tools/gpu/ab_env.sh
 cd "$GRAFT_REPO_ROOT" || exit 2
 OUT=gpurun_out/abenv
 mkdir -p $OUT
