@@ -106,6 +106,44 @@ PYBIND11_MODULE(_native, m) {
     return rc == 1;
   });
   m.def("conv_bn_fuse_rows", [](int rows) { ddp_conv_bn_fuse_rows(rows); });
+  // tap-reuse 3x3 forward (conv_tr.hip): returns 0 not served, 1 served, 2 served with the
+  // BatchNorm forward fused into its split-K finish (bn = conv_fwd_bn's tuple, or None)
+  m.def("conv_fwd_tr", [](py::tuple g, uintptr_t x, uintptr_t wc, uintptr_t bias, uintptr_t z,
+                          uintptr_t stats, uintptr_t ws, size_t ws_elems, uintptr_t st,
+                          py::object bn) {
+    auto c = geom(g);
+    ddp_amd::BnFwdFuse f{};
+    const ddp_amd::BnFwdFuse* fp = nullptr;
+    if (!bn.is_none()) {
+      py::tuple b = bn.cast<py::tuple>();
+      f.gamma = P<float>(b[0].cast<uintptr_t>());
+      f.beta = P<float>(b[1].cast<uintptr_t>());
+      f.eps = b[2].cast<float>();
+      f.relu = b[3].cast<int>();
+      f.pool = b[4].cast<int>();
+      f.coef = P<float>(b[5].cast<uintptr_t>());
+      f.y = P<unsigned short>(b[6].cast<uintptr_t>());
+      f.P = b[7].cast<int>();
+      f.Q = b[8].cast<int>();
+      fp = &f;
+    }
+    int done = 0;
+    const int rc = ddp_conv_fwd_tr(&c, P<void>(x), P<void>(wc), P<float>(bias), P<void>(z),
+                                   P<float>(stats), P<float>(ws), ws_elems, fp, &done, S(st));
+    if (rc < 0) check(rc, "conv_fwd_tr");
+    if (rc >= 2) check(rc - 2, "conv_fwd_tr");
+    return rc == 1 ? 1 + done : 0;
+  }, py::arg("g"), py::arg("x"), py::arg("wc"), py::arg("bias"), py::arg("z"), py::arg("stats"),
+     py::arg("ws"), py::arg("ws_elems"), py::arg("st"), py::arg("bn") = py::none());
+  m.def("conv_tr_set", [](int mode, int M, int K, int C, int H, int bm, int bn, int splits,
+                          int stages) { ddp_conv_tr_set(mode, M, K, C, H, bm, bn, splits, stages); },
+        py::arg("mode"), py::arg("M"), py::arg("K"), py::arg("C"), py::arg("H"), py::arg("bm"),
+        py::arg("bn"), py::arg("splits"), py::arg("stages") = 0);
+  m.def("conv_tr_geometry", [](int BM, int N, int H, int W) {
+    int o[7];
+    ddp_conv_tr_geometry(BM, N, H, W, o);
+    return std::vector<int>(o, o + 7);
+  });
   // classifier-head dx + the preceding block's BN backward; bn = (z, coef, sums, pool, relu, Hz,
   // Wz), bna = (dz, dgamma, dbeta); True when launched (dx is then not computed)
   m.def("linear_dx_bn", [](uintptr_t dl, uintptr_t W, int B, int F, int J, uintptr_t g,

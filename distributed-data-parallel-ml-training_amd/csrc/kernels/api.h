@@ -123,6 +123,21 @@ int ddp_conv_fwd_bn(const ddp_amd::ConvGeom* g, const void* x, const void* wc, c
                     hipStream_t st);
 // classifier-head dx fused with the preceding block's whole BN backward (conv_igemm.hip
 // linear_dx_bnbwd_kernel): 1 launched, 0 not served, < 0 invalid, >= 2 HIP error (rc - 2)
+// split-K finish of a forward GEMM computed elsewhere (slabs [splits][M][K] -> z + statistics,
+// or the BatchNorm-fused finish with ``bn``); returns the HIP error code
+int ddp_conv_fwd_finish(const ddp_amd::ConvGeom* g, float* ws, int splits, const float* bias,
+                        void* z, float* stats, const ddp_amd::BnFwdFuse* bn, int* bn_done,
+                        hipStream_t st);
+// 3x3/s1/p1 forward through the tap-reuse kernel (conv_tr.hip): 1 served (*bn_done as
+// ddp_conv_fwd_bn), 0 not served (use ddp_conv_fwd[_bn]), < 0 invalid, >= 2 HIP error (rc - 2)
+int ddp_conv_fwd_tr(const ddp_amd::ConvGeom* g, const void* x, const void* wc, const float* bias,
+                    void* z, float* stats, float* ws, size_t ws_elems,
+                    const ddp_amd::BnFwdFuse* bn, int* bn_done, hipStream_t st);
+// tap-reuse policy: mode -1 clear table, 0/1 disable/enable (table entries), 4 enable with the
+// heuristic for untabled shapes, 2 table entry (M, K, C, H) ->
+// (bm, bn, splits, stages) (bm = 0: use the implicit-GEMM kernel), 3 force the same (sweeps)
+void ddp_conv_tr_set(int mode, int M, int K, int C, int H, int bm, int bn, int splits, int stages);
+int ddp_conv_tr_geometry(int BM, int N, int H, int W, int* out7);
 int ddp_linear_dx_bn(const float* dl, const float* W, int B, int F, int J, const float* gscale,
                      const ddp_amd::BnBwdFuse* bn, const ddp_amd::BnBwdApply* ba, hipStream_t st);
 // row limit of the BN-fused split-K finishes (default 128 or DDP_AMD_BN_FUSE_MAX_ROWS)

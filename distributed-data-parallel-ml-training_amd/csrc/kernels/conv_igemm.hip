@@ -2084,6 +2084,35 @@ extern "C" int ddp_conv_fwd_bn(const ConvGeom* g, const void* x, const void* wc,
   return e ? 2 + e : done;
 }
 
+// Split-K finish of a FWD GEMM computed elsewhere (conv_tr.hip's tap-reuse kernel): slabs
+// [splits][N*P*Q][K] -> bias + bf16 z + statistics, or with ``bn`` (small problems) the
+// BatchNorm-fused finish (*bn_done = 1). Returns the HIP error code.
+extern "C" int ddp_conv_fwd_finish(const ConvGeom* g, float* ws, int splits, const float* bias,
+                                   void* z, float* stats, const BnFwdFuse* bn, int* bn_done,
+                                   hipStream_t st) {
+  ConvArgs a{};
+  a.g = *g;
+  a.out = (unsigned short*)z;
+  a.ws = ws;
+  a.bias = bias;
+  a.stats = stats;
+  a.Mg = g->N * g->P * g->Q;
+  a.Ng = g->K;
+  a.Kg = g->R * g->S * g->C;
+  a.splits = splits;
+  a.fixup = 0;
+  static const bool bn_enabled = [] {
+    const char* e = std::getenv("DDP_AMD_BN_FWD_FUSE");
+    return !(e && e[0] == '0');
+  }();
+  if (bn && bn_enabled && a.Mg <= kBnFwdFuseMaxRows) {
+    a.bnfwd = bn;
+    a.bnfwd_done = bn_done;
+  }
+  launch_finish<MODE_FWD>(a, st);
+  return (int)hipGetLastError();
+}
+
 static int conv_dgrad_impl(const ConvGeom* g, const void* dy, const void* wc, void* dx,
                            float* ws, size_t ws_elems, int splits, int accumulate,
                            const BnBwdFuse* bn, const BnBwdApply* ba, int* bn_done,

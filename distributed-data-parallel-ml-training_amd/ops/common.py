@@ -51,7 +51,13 @@ def load_conv_tuning(n=None, path=None):
     for e in table.get("entries", []):
         n.conv_tune_set(int(e["mode"]), int(e["M"]), int(e["N"]), int(e["K"]), int(e["tile"]),
                         int(e["splits"]), int(e.get("stages", 0)))
-    return len(table.get("entries", []))
+    # tap-reuse 3x3 forward (conv_tr.hip, tools/conv_tune_tr.py): (M, K, C, H) -> (bm, bn,
+    # splits); bm = 0 keeps the implicit-GEMM kernel for that layer
+    n.conv_tr_set(-1, 0, 0, 0, 0, 0, 0, 0)
+    for e in table.get("tr_entries", []):
+        n.conv_tr_set(2, int(e["M"]), int(e["K"]), int(e["C"]), int(e["H"]), int(e["bm"]),
+                      int(e["bn"]), int(e["splits"]), int(e.get("stages", 0)))
+    return len(table.get("entries", [])) + len(table.get("tr_entries", []))
 
 
 def weight_krsc(w):

@@ -119,6 +119,13 @@ def conv_forward(spec, x, bias=None, stats=None, bn_fuse=None):
         # input layer (3 channels padded to 8): direct MFMA kernel, conv_smallk.hip
         return (z, False) if bn_fuse is not None else z
     ws = workspace(x.device)
+    if (CONV_TR and spec.R == 3 and spec.S == 3 and spec.stride == 1 and spec.pad == 1
+            and spec.C == spec.Cr and spec.C % 64 == 0 and spec.K % 64 == 0):
+        # 3x3 tap-reuse kernel (conv_tr.hip): input tile resident in LDS for all nine taps
+        r = native().conv_fwd_tr(g, ptr(x), ptr(spec.wc), ptr(bias), ptr(z), ptr(stats), ptr(ws),
+                                 ws.numel(), stream_handle(), bn_fuse)
+        if r:
+            return (z, r == 2) if bn_fuse is not None else z
     if bn_fuse is not None:
         fused = native().conv_fwd_bn(g, ptr(x), ptr(spec.wc), ptr(bias), ptr(z), ptr(stats),
                                      ptr(ws), ws.numel(), stream_handle(), bn_fuse)
@@ -157,6 +164,9 @@ class GradLink:
         return out
 
 
+# 3x3 stride-1 forward convolutions through the tap-reuse kernel (conv_tr.hip); =0 restores the
+# implicit-GEMM kernel for every layer (the native side also reads DDP_AMD_CONV_TR)
+CONV_TR = os.environ.get("DDP_AMD_CONV_TR", "1") != "0"
 # BatchNorm forward fused into the split-K finish of small conv GEMMs (conv_igemm.hip
 # splitk_finish_bnfwd_kernel; the native side also honours DDP_AMD_BN_FWD_FUSE=0)
 BN_FWD_FUSE = os.environ.get("DDP_AMD_BN_FWD_FUSE", "1") != "0"

@@ -500,63 +500,96 @@ def test_segmented_ddp_step_matches_single_graph(native_ext, split):
     m.close()
 
 
-def test_vgg11_20_step_trajectory_matches_cpu_fp32_oracle(native_ext):
-    """End-to-end numerics over time: 20 SGD steps (lr 0.01, momentum 0.9, wd 1e-4, batch 64)
-    of the fused bf16 GPU path vs the reference model + torch.optim.SGD in fp32 on the CPU
-    (reference loop: /root/reference/part1/main.py:65-77), on the same batches. Per-step losses
-    agree to a few percent, and the total parameter update points the same way."""
+def _plain_vgg_forward(model, x):
+    """The reference forward (/root/reference/part1/model.py:42-46) on ATen, any device, fp32."""
+    y = model.layers(x)
+    return model.fc1(y.view(y.size(0), -1))
+
+
+def test_vgg11_b256_trajectory_matches_bf16_emulated_oracle(native_ext):
+    """End-to-end numerics over time at the reference batch (256) and lr 0.01 (momentum 0.9,
+    wd 1e-4; reference loop /root/reference/part1/main.py:65-77): 12 SGD steps of the fused
+    bf16 GPU path against (a) the bf16-EMULATING oracle — the reference model on ATen in fp32
+    with bf16 rounding at exactly the points where the fused path stores bf16 (inputs, conv
+    outputs z, block outputs, weight copies; their gradients) + torch.optim.SGD — and (b) the
+    plain fp32 reference, all on the same batches.
+
+    Error model (what the thresholds are derived from, not fitted): the emulated oracle makes the
+    same roundings, so GPU-vs-emulated differs only by fp32 summation ORDER (BN-statistics
+    atomics, split-K, MFMA accumulation), which occasionally moves a stored bf16 value by one ulp
+    and, through ReLU / 2x2-max ties, re-routes a gradient. Two runs of the SAME GPU build on the
+    same data differ by exactly that mechanism (atomic order is not deterministic), so their
+    mutual distance is the noise floor: the GPU must stay as close to the emulated oracle as it
+    is to itself, within 3x that floor plus 0.5 % per-step loss for the few roundings the oracle
+    places differently (fp32 BN apply before the pool in the fused kernel vs ATen's order). A
+    wrong kernel (a missing BN gradient term, a wrong pool route, a stale weight copy) moves the
+    loss by far more than the order noise in the first steps and turns the update direction
+    (update cosine vs the emulated oracle >= 0.95 is required; fp32 oracle >= 0.9)."""
     from ddp_amd.models import VGG11
     from ddp_amd.engine import CrossEntropyLoss
     from ddp_amd.optim import FusedSGD
+    steps, B = 12, 256
     torch.manual_seed(2024)
-    cpu = VGG11()
-    gpu = copy.deepcopy(cpu).cuda()
-    p0 = torch.cat([p.detach().reshape(-1).clone() for p in cpu.parameters()])
-    oc = torch.optim.SGD(cpu.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
-    og = FusedSGD(gpu.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    base = VGG11()
+    p0 = torch.cat([p.detach().reshape(-1).clone() for p in base.parameters()]).double()
     crit = CrossEntropyLoss()
     g = torch.Generator().manual_seed(5)
-    # weakly class-dependent means: the loss falls steadily (no early collapse to ~0, where
-    # single-batch spikes make any two runs diverge)
     means = 0.25 * torch.randn(10, 3, 1, 1, generator=g)
-    losses_c, losses_g = [], []
-    for step in range(20):
-        y = torch.randint(0, 10, (64,), generator=g)
-        x = torch.randn(64, 3, 32, 32, generator=g) + means[y]
-        x = x.to(torch.bfloat16).float()  # the GPU consumes bf16 inputs: same values on both sides
-        oc.zero_grad()
-        lc = crit(cpu(x), y)
-        lc.backward()
-        oc.step()
-        og.zero_grad()
-        lg = crit(gpu(x.cuda()), y.cuda())
-        lg.backward()
-        og.step()
-        losses_c.append(float(lc))
-        losses_g.append(float(lg))
-    torch.cuda.synchronize()
-    print("cpu fp32:", [round(v, 3) for v in losses_c])
-    print("gpu bf16:", [round(v, 3) for v in losses_g])
-    # step by step while the trajectories are close; afterwards single-batch losses (< 0.7,
-    # memorising) amplify tiny weight differences, so compare 5-step window means there
-    rel = [abs(a - b) / abs(b) for a, b in zip(losses_g, losses_c)]
-    # (two GPU runs differ from each other by float-atomic ordering of the BN statistics, which
-    # grows to several % per step by step ~8; measured run to run on the box)
-    # (observed over 8 box runs: steps 0-2 within 3.4%, steps 0-4 within 4.5%, 5-step windows
-    # within 8%; the step-2 batch alone swings 1.5-3.3 % between runs of the same build)
-    assert max(rel[:3]) < 0.05 and max(rel[:5]) < 0.06, rel
-    for w in range(0, 20, 5):
-        mg, mc = sum(losses_g[w:w + 5]) / 5, sum(losses_c[w:w + 5]) / 5
-        assert abs(mg - mc) < 0.15 * mc + 0.02, (w, mg, mc)
-    assert max(abs(a - b) for a, b in zip(losses_g, losses_c)) < 0.3
-    assert losses_c[-1] < losses_c[0] and losses_g[-1] < losses_g[0]
-    pc = torch.cat([p.detach().reshape(-1) for p in cpu.parameters()]).double()
-    pg = torch.cat([p.detach().float().cpu().reshape(-1) for p in gpu.parameters()]).double()
-    p0 = p0.double()
-    dc, dg = pc - p0, pg - p0
-    cos_d = float(torch.dot(dc, dg) / (dc.norm() * dg.norm()))
-    cos_p = float(torch.dot(pc, pg) / (pc.norm() * pg.norm()))
-    print("update cosine", cos_d, "param cosine", cos_p)
-    # the total update after 20 steps is dominated by the memorising late steps, where single
-    # batches steer the weights (0.86 measured on the box); the parameters agree (0.9993)
-    assert cos_p > 0.995 and cos_d > 0.7
+    batches = []
+    for _ in range(steps):
+        y = torch.randint(0, 10, (B,), generator=g)
+        x = (torch.randn(B, 3, 32, 32, generator=g) + means[y]).to(torch.bfloat16).float()
+        batches.append((x.cuda(), y.cuda()))
+
+    def flat(m):
+        return torch.cat([p.detach().float().cpu().reshape(-1) for p in m.parameters()]).double()
+
+    def run_fused():
+        m = copy.deepcopy(base).cuda()
+        opt = FusedSGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+        ls = []
+        for x, y in batches:
+            opt.zero_grad()
+            loss = crit(m(x), y)
+            loss.backward()
+            opt.step()
+            ls.append(float(loss))
+        torch.cuda.synchronize()
+        return ls, flat(m) - p0
+
+    def run_aten(fwd):
+        m = copy.deepcopy(base).cuda()
+        opt = torch.optim.SGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+        ls = []
+        for x, y in batches:
+            opt.zero_grad()
+            loss = torch.nn.functional.cross_entropy(fwd(m, x), y)
+            loss.backward()
+            opt.step()
+            ls.append(float(loss))
+        torch.cuda.synchronize()
+        return ls, flat(m) - p0
+
+    lg, dg = run_fused()
+    lg2, dg2 = run_fused()  # same build, same data: the summation-order noise floor
+    le, de = run_aten(_emulated_vgg_forward)
+    lf, df = run_aten(_plain_vgg_forward)
+
+    def cos(a, b):
+        return float(torch.dot(a, b) / (a.norm() * b.norm()))
+
+    r_self = [abs(a - b) / abs(b) for a, b in zip(lg, lg2)]
+    r_emu = [abs(a - b) / abs(b) for a, b in zip(lg, le)]
+    r_f32 = [abs(a - b) / abs(b) for a, b in zip(lg, lf)]
+    print("fused  :", [round(v, 4) for v in lg])
+    print("fused2 :", [round(v, 4) for v in lg2])
+    print("emu    :", [round(v, 4) for v in le])
+    print("fp32   :", [round(v, 4) for v in lf])
+    print("update cosine vs self %.4f emu %.4f fp32 %.4f" % (cos(dg, dg2), cos(dg, de), cos(dg, df)))
+    floor = max(r_self)
+    for k in range(steps):
+        assert r_emu[k] <= 3.0 * floor + 0.005, (k, r_emu, r_self)
+    assert max(r_f32) < 0.05, r_f32  # bf16 vs fp32 storage: a few % at most
+    assert lg[-1] < lg[0] and le[-1] < le[0]
+    assert cos(dg, de) >= 0.95 and cos(dg, de) >= cos(dg, dg2) - 0.03
+    assert cos(dg, df) >= 0.9

@@ -212,3 +212,45 @@ def test_eager_ddp_overlaps_backward_on_comm_stream(native_ext):
     c = float(torch.dot(a, b) / (a.norm() * b.norm()))
     assert c > 0.98, c
     assert abs(float(b.norm()) / float(a.norm()) - 1) < 0.05
+
+
+@pytest.mark.parametrize("live", [False, True])
+def test_segmented_step_wait_timeout_skips_update_and_raises(native_ext, live):
+    """Failure path of the pipelined multi-GPU step (engine/step.py SegmentedDDPStep): a bucket
+    whose backward segment never signals — what a stuck peer or a lost launch looks like from
+    the comm stream — must not hang and must not apply unreduced gradients. The comm stream's
+    bounded device-side wait gives up after WAIT_TIMEOUT_S, records the error word, the bucket's
+    optimizer launch skips the update (parameters and momentum unchanged), and check_error()
+    raises. Reference: DDP's blocking bucket all-reduce (/root/reference/part3/main.py:174) has no
+    such bound; SURVEY.md §5.3."""
+    import time
+    from ddp_amd.models import VGG11
+    from ddp_amd.optim import FusedSGD
+    from ddp_amd.data import SyntheticCIFAR10, DeviceLoader
+    from ddp_amd.engine import SegmentedDDPStep, CrossEntropyLoss
+    from ddp_amd.parallel import DistributedDataParallel, RcclCommunicator
+    torch.manual_seed(11)
+    m = DistributedDataParallel(VGG11().cuda(), RcclCommunicator(0, 1, 0, self_comm=live),
+                                bucket_cap_mb=256.0, first_bucket_cap_mb=256.0)
+    opt = FusedSGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    ld = DeviceLoader(SyntheticCIFAR10(True, n=256), 32, "cuda")
+    st = SegmentedDDPStep(m, opt, CrossEntropyLoss(), ld, split=[3, 6])
+    st.WAIT_TIMEOUT_S = 0.5
+    torch.cuda.synchronize()
+    m.arena.grad.normal_()  # gradients an applied update would consume
+    p0, b0 = m.arena.data.clone(), opt.momentum_buffer.clone()
+    st.check_error()  # healthy before
+    t0 = time.monotonic()
+    for j in range(len(st.buckets)):
+        st._comm(j)  # every segment's signal is missing: each wait times out
+    torch.cuda.synchronize()
+    dt = time.monotonic() - t0
+    assert dt < 30.0, f"bounded waits took {dt:.1f}s"
+    assert dt >= 0.4, "the device-side wait must actually have waited for the signal"
+    assert torch.equal(m.arena.data, p0), "an update was applied without its bucket's all-reduce"
+    assert torch.equal(opt.momentum_buffer, b0)
+    with pytest.raises(RuntimeError, match="timed out"):
+        st.check_error()
+    with pytest.raises(RuntimeError, match="timed out"):
+        st.pop_loss()  # the training loop's per-window loss read surfaces it too
+    m.close()

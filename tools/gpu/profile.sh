@@ -9,7 +9,7 @@ mkdir -p gpurun_out/prof
 for B in $BATCHES; do
   N=${TAG}_${MODEL}_b$B
   D=$GRAFT_REPO_ROOT/gpurun_out/prof/$N
-  (cd /tmp && export TMPDIR=/tmp && export $ENVS && timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+  (cd /tmp && export TMPDIR=/tmp && { [ -z "$ENVS" ] || export $ENVS; } && timeout -k 10 300 rocprofv3 --kernel-trace --stats \
      --output-format csv -d "$D" -o p -- python3 "$GRAFT_REPO_ROOT/bench.py" --model $MODEL \
      --global-batch $B --steps $STEPS --warmup 5 --ref-window 0 > "$D.log" 2>&1) || { tail -5 "$D.log"; exit 1; }
   P=$(ls "$D"/*/p_kernel_stats.csv 2>/dev/null | head -1); P=${P%_kernel_stats.csv}

@@ -24,7 +24,8 @@ sys.path.insert(0, REPO)
 
 def build_model(name):
     import torch.nn as nn
-    from ddp_amd.models import VGG11, resnet50
+    from ddp_amd.models.vgg import VGG11
+    from ddp_amd.models.resnet import resnet50
 
     if name == "vgg11":
         m = VGG11()
