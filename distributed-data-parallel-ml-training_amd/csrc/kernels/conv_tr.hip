@@ -18,8 +18,9 @@
 // groups each mix two adjacent planes) then hits 16 distinct bank quads whenever the 16 rows are
 // 16 consecutive patch pixels — true for W >= 4 (rows of 16, 8 or 4 pixels are contiguous in the
 // patch); for W = 2 the per-image pitch `imgp` is chosen by the host so that four 2x2 images
-// land on distinct quads. The halo COLUMNS are not stored: taps s = 0 / 2 of an edge pixel read a
-// zero slot instead (one address select); halo ROWS are loaded (zeros at the image border).
+// land on distinct quads. The halo COLUMNS are not stored: for the s = 0 / 2 tap an edge lane
+// reads its own centre pixel (an address a neighbour lane reads anyway: no extra bank traffic)
+// and zeroes the fragment; halo ROWS are loaded (zeros at the image border).
 // The patch is loaded through registers (buffer_load_dwordx4, eight lanes per pixel = one
 // coalesced 128-B pixel row; out-of-range offsets read zero) and written to the planes by
 // ds_write_b128 (2-way bank conflicts); the weights stream by LDS-DMA (buffer_load ... lds).
@@ -172,12 +173,6 @@ __global__ __launch_bounds__(256) void conv_tr_fwd_kernel(Args a) {
     for (int u = 0; u < NL; ++u)
       if (adst[u] >= 0) *reinterpret_cast<v4i*>(dst + adst[u]) = areg[u];
   };
-  // the zero slot of every plane of both buffers (never written by the patch loads)
-  if (tid < 16) {
-    const int b = tid >> 3, c = tid & 7;
-    *reinterpret_cast<v4i*>(reinterpret_cast<char*>(abuf + b * aelems) +
-                            (plane_base(c, a.plane) + a.zslot) * 16) = (v4i){0, 0, 0, 0};
-  }
   // ---- B (weights) DMA: row (tid >> 3) + 32 i of the [col][k] tile, logical chunk lcB
   const int lcB = (tid & 7) ^ ((tid >> 4) & 7);
   unsigned boff[CB];
@@ -198,7 +193,6 @@ __global__ __launch_bounds__(256) void conv_tr_fwd_kernel(Args a) {
   // ---- fragment addresses (bytes within a patch buffer / B stage)
   int fa_base[TM];       // patch pixel of tap (r, s) = (0, 1) at chunk plane (lane >> 4), bytes
   unsigned col_ok[TM];   // bit 0: tap s = 0 valid, bit 1: s = 2 valid
-  const int za = (plane_base(lane >> 4, a.plane) + a.zslot) * 16;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = wm * WTM + i * 16 + (lane & 15);  // tile-local output row
@@ -224,16 +218,19 @@ __global__ __launch_bounds__(256) void conv_tr_fwd_kernel(Args a) {
     const char* Ab = reinterpret_cast<const char*>(abuf + abuf_i * aelems);
     const unsigned short* Bs = bring + slot * BTILE;
     const int r = t / 3, s = t - r * 3;
-    const int toff = (r * W + s - 1) * 16;
+    const int trow = r * W * 16, tcol = (s - 1) * 16;
 #pragma unroll
     for (int kk = 0; kk < 64; kk += 32) {
       bf16x8 fa[TM], fb[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        int off = fa_base[i] + toff;
-        if (s != 1) off = (col_ok[i] & (s == 0 ? 1u : 2u)) ? off : za;
-        off += kk ? kk_a : 0;
+        // an edge column's s = 0 / 2 tap is padding: the lane reads its own (centre) pixel —
+        // the address its neighbour lane reads for that tap, so no extra bank traffic — and
+        // zeroes the fragment
+        const bool ok = s == 1 || (col_ok[i] & (s == 0 ? 1u : 2u));
+        const int off = fa_base[i] + trow + (ok ? tcol : 0) + (kk ? kk_a : 0);
         fa[i] = *reinterpret_cast<const bf16x8*>(Ab + off);
+        if (s != 1 && !ok) fa[i] = (bf16x8){};
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j)
@@ -253,26 +250,32 @@ __global__ __launch_bounds__(256) void conv_tr_fwd_kernel(Args a) {
     if (s < nsteps) issue_b(s, s);
   store_a(0);  // (waits for the patch loads, not for the B DMAs issued after them)
 
-  // ---- main loop. Wait count at k-step j = vector-memory instructions issued after B(j): the
-  // B stages j+1 .. j+NST-2 still in flight, plus the next patch's loads when they were issued
-  // inside that window (at t == 0 of this channel block, i.e. t in [1, NST-2]); the
-  // compile-time cases are enumerated. LDS writes of the patch are drained before the barrier.
+  // ---- main loop: channel blocks x the nine taps (unrolled: tap offsets, the zero-column
+  // selects and the wait counts are compile-time). Wait count at k-step j = vector-memory
+  // instructions issued after B(j): the B stages j+1 .. j+NST-2 still in flight, plus the next
+  // patch's loads when they were issued inside that window (at t == 0 of this channel block,
+  // i.e. t in [1, NST-2]). The patch's LDS writes are drained before the first barrier of the
+  // channel block that reads them.
+  const int ncbl = cb1 - cb0;
   int slot = 0;
-  for (int j = 0; j < nsteps; ++j) {
-    const int cbl = j / 9, t = j - cbl * 9;
-    const int bafter = min(NST - 2, nsteps - 1 - j);
-    const bool anext = (t >= 1 && t <= NST - 2) && (cbl + 1 < cb1 - cb0);
-    if (t == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    wait_stage<NST - 2, CB, NL>(bafter, anext);
-    // every wave finished k-step j-1: ring slot (j-1) % NST is free
-    const bool more = cbl + 1 < cb1 - cb0;
-    if (t == 0 && more) load_a(cb0 + cbl + 1);
-    if (j + NST - 1 < nsteps) issue_b(j + NST - 1, slot == 0 ? NST - 1 : slot - 1);
-    compute(t, cbl & 1, slot);
-    // after the last tap of this channel block: the next patch goes to the other buffer (its
-    // readers, channel block cb-1, all passed this block's first barrier)
-    if (t == 8 && more) store_a((cbl + 1) & 1);
-    slot = slot + 1 == NST ? 0 : slot + 1;
+  for (int cbl = 0; cbl < ncbl; ++cbl) {
+    const bool more = cbl + 1 < ncbl;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int j = cbl * 9 + t;
+      const int bafter = min(NST - 2, nsteps - 1 - j);
+      const bool anext = (t >= 1 && t <= NST - 2) && more;
+      if (t == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      wait_stage<NST - 2, CB, NL>(bafter, anext);
+      // every wave finished k-step j-1: ring slot (j-1) % NST is free
+      if (t == 0 && more) load_a(cb0 + cbl + 1);
+      if (j + NST - 1 < nsteps) issue_b(j + NST - 1, slot == 0 ? NST - 1 : slot - 1);
+      compute(t, cbl & 1, slot);
+      // after the last tap: the next patch goes to the other buffer (its readers, channel
+      // block cb-1, all passed this block's first barrier)
+      if (t == 8 && more) store_a((cbl + 1) & 1);
+      slot = slot + 1 == NST ? 0 : slot + 1;
+    }
   }
 
   // ---- epilogue: acc[i][j][v] = D[row0 + wm*WTM + i*16 + (lane&15)][col0 + wn*WTN + j*16 + 4*(lane>>4) + v]

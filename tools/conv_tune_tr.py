@@ -53,6 +53,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, nargs="+", default=[256, 128, 64, 32])
     ap.add_argument("--write", action="store_true")
+    ap.add_argument("--out", default=None,
+                    help="write the merged table here instead of over ops/conv_tuning.json")
     ap.add_argument("--margin", type=float, default=0.03,
                     help="keep the implicit-GEMM kernel unless tap-reuse is this much faster")
     a = ap.parse_args()
@@ -116,9 +118,10 @@ def main():
         for e in entries:
             old[(e["M"], e["K"], e["C"], e["H"])] = e
         table["tr_entries"] = sorted(old.values(), key=lambda e: (e["H"], e["C"], e["M"]))
-        with open(path, "w") as f:
+        out = a.out or path
+        with open(out, "w") as f:
             json.dump(table, f, indent=1)
-        print(f"wrote {len(entries)} tap-reuse entries to {path}")
+        print(f"wrote {len(entries)} tap-reuse entries to {out}")
 
 
 if __name__ == "__main__":

@@ -1,8 +1,7 @@
-cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/trpmc && root=$GRAFT_REPO_ROOT
-i=0
-for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" \
-           "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVES"; do
-  i=$((i+1))
-  (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $set --output-format csv -d "$root/gpurun_out/trpmc/p$i" -o t -- python3 "$root/tools/probes/tr_probe.py" 32 512 512 2 64 64 1 3 > "$root/gpurun_out/trpmc/p$i.log" 2>&1) || { tail -5 gpurun_out/trpmc/p$i.log; exit 1; }
-done
-python3 tools/pmc_summary.py gpurun_out/trpmc
+cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/tr || exit 1
+timeout -k 10 900 python -u tools/conv_tune_tr.py --batch 256 128 64 32 --write --out gpurun_out/tr/conv_tuning.json > gpurun_out/tr/sweep_all.jsonl 2> gpurun_out/tr/sweep_all.err || { tail -5 gpurun_out/tr/sweep_all.err; exit 1; }
+tail -1 gpurun_out/tr/sweep_all.jsonl
+for B in 256 32 64 128; do for T in 1 0; do
+  DDP_AMD_CONV_TUNING_FILE=gpurun_out/tr/conv_tuning.json DDP_AMD_CONV_TR=$T timeout -k 10 200 python bench.py --global-batch $B --steps 60 --warmup 10 --ref-window 0 > gpurun_out/tr/bench_${B}_$T.log 2>&1 || { tail -5 gpurun_out/tr/bench_${B}_$T.log; exit 1; }
+  echo "B=$B TR=$T $(python -c "import json; d=json.loads(open('gpurun_out/tr/bench_${B}_$T.log').read().strip().splitlines()[-1]); print(d['ms_per_step'], d['train_loss_mean'])")"
+done; done
