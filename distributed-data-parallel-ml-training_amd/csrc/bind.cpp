@@ -110,7 +110,7 @@ PYBIND11_MODULE(_native, m) {
   // BatchNorm forward fused into its split-K finish (bn = conv_fwd_bn's tuple, or None)
   m.def("conv_fwd_tr", [](py::tuple g, uintptr_t x, uintptr_t wc, uintptr_t bias, uintptr_t z,
                           uintptr_t stats, uintptr_t ws, size_t ws_elems, uintptr_t st,
-                          py::object bn) {
+                          py::object bn, py::object fin) {
     auto c = geom(g);
     ddp_amd::BnFwdFuse f{};
     const ddp_amd::BnFwdFuse* fp = nullptr;
@@ -127,14 +127,36 @@ PYBIND11_MODULE(_native, m) {
       f.Q = b[8].cast<int>();
       fp = &f;
     }
+    // fused input (the preceding block's BN + ReLU [+ pool]): (z, stats, gamma, beta, eps,
+    // relu, pool, coef, y)
+    ddp_amd::TrFwdIn ti{};
+    const ddp_amd::TrFwdIn* tp = nullptr;
+    if (!fin.is_none()) {
+      py::tuple b = fin.cast<py::tuple>();
+      ti.z = P<unsigned short>(b[0].cast<uintptr_t>());
+      ti.stats = P<float>(b[1].cast<uintptr_t>());
+      ti.gamma = P<float>(b[2].cast<uintptr_t>());
+      ti.beta = P<float>(b[3].cast<uintptr_t>());
+      ti.eps = b[4].cast<float>();
+      ti.relu = b[5].cast<int>();
+      ti.pool = b[6].cast<int>();
+      ti.coef = P<float>(b[7].cast<uintptr_t>());
+      ti.y = P<unsigned short>(b[8].cast<uintptr_t>());
+      tp = &ti;
+    }
     int done = 0;
     const int rc = ddp_conv_fwd_tr(&c, P<void>(x), P<void>(wc), P<float>(bias), P<void>(z),
-                                   P<float>(stats), P<float>(ws), ws_elems, fp, &done, S(st));
+                                   P<float>(stats), P<float>(ws), ws_elems, fp, &done, tp, S(st));
     if (rc < 0) check(rc, "conv_fwd_tr");
     if (rc >= 2) check(rc - 2, "conv_fwd_tr");
     return rc == 1 ? 1 + done : 0;
   }, py::arg("g"), py::arg("x"), py::arg("wc"), py::arg("bias"), py::arg("z"), py::arg("stats"),
-     py::arg("ws"), py::arg("ws_elems"), py::arg("st"), py::arg("bn") = py::none());
+     py::arg("ws"), py::arg("ws_elems"), py::arg("st"), py::arg("bn") = py::none(),
+     py::arg("fin") = py::none());
+  m.def("conv_tr_would_serve", [](py::tuple g, size_t ws_elems, int in_mode) {
+    auto c = geom(g);
+    return ddp_conv_tr_would_serve(&c, ws_elems, in_mode) == 1;
+  });
   m.def("conv_tr_set", [](int mode, int M, int K, int C, int H, int bm, int bn, int splits,
                           int stages) { ddp_conv_tr_set(mode, M, K, C, H, bm, bn, splits, stages); },
         py::arg("mode"), py::arg("M"), py::arg("K"), py::arg("C"), py::arg("H"), py::arg("bm"),

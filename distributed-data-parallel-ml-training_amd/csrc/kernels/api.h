@@ -87,6 +87,21 @@ struct BnFwdFuse {
   int P, Q;                 // conv output spatial dims (pre-pool)
 };
 
+// Fused input of the tap-reuse 3x3 forward (conv_tr.hip): the conv input is
+// [2x2/s2 max-pool](ReLU(BatchNorm(z))) of the preceding block, computed while the input patch
+// is loaded (the preceding block's bn_act_fwd launch disappears). Training-mode batch
+// statistics only (no running statistics).
+struct TrFwdIn {
+  const unsigned short* z;  // preceding block's conv output [N][Hz][Wz][C] (Hz = 2H when pooled)
+  const float* stats;       // its statistics replicas [kStatRep][2][C]
+  const float* gamma;       // [C]
+  const float* beta;
+  float eps;
+  int relu, pool;
+  float* coef;              // [6][C] coefficient table written for its backward
+  unsigned short* y;        // materialised conv input [N][H][W][C] (the wgrad operand)
+};
+
 struct PackDesc {
   const float* p;          // fp32 master [K][Cr][R][S] (krsc == 0) or [K][R][S][Cr] (krsc == 1)
   unsigned short* wc;      // bf16 [K][R][S][C]   (may be null)
@@ -132,7 +147,9 @@ int ddp_conv_fwd_finish(const ddp_amd::ConvGeom* g, float* ws, int splits, const
 // ddp_conv_fwd_bn), 0 not served (use ddp_conv_fwd[_bn]), < 0 invalid, >= 2 HIP error (rc - 2)
 int ddp_conv_fwd_tr(const ddp_amd::ConvGeom* g, const void* x, const void* wc, const float* bias,
                     void* z, float* stats, float* ws, size_t ws_elems,
-                    const ddp_amd::BnFwdFuse* bn, int* bn_done, hipStream_t st);
+                    const ddp_amd::BnFwdFuse* bn, int* bn_done, const ddp_amd::TrFwdIn* in,
+                    hipStream_t st);
+int ddp_conv_tr_would_serve(const ddp_amd::ConvGeom* g, size_t ws_elems, int in_mode);
 // tap-reuse policy: mode -1 clear table, 0/1 disable/enable (table entries), 4 enable with the
 // heuristic for untabled shapes, 2 table entry (M, K, C, H) ->
 // (bm, bn, splits, stages) (bm = 0: use the implicit-GEMM kernel), 3 force the same (sweeps)

@@ -99,9 +99,24 @@ struct Args {
   int x_bytes, w_bytes;
   int tiles_m, tiles_n;
   int abuf_elems;            // bf16 elements of one patch buffer (16-B multiple)
+  // fused input (template IN = 1: BN + ReLU, IN = 2: BN + ReLU + 2x2/s2 max-pool): the conv
+  // input x = [pool](relu(scale * zin + shift)) is computed while the patch is loaded; zin is
+  // the preceding block's conv output [N][Hz][Wz][C] (Hz = 2H when pooled), its BatchNorm
+  // coefficients are folded here from the statistics replicas, block 0 writes the coefficient
+  // table the preceding block's backward reads, and the first column tile's blocks materialise
+  // x into y_out (the wgrad's operand)
+  const unsigned short* zin;
+  const float* in_stats;     // [kStatRep][2][C]
+  const float* in_gamma;
+  const float* in_beta;
+  float in_eps;
+  int in_relu;
+  float* in_coef;            // [6][C]: scale, shift, mean, invstd (written by block 0)
+  unsigned short* y_out;     // [N][H][W][C]
+  int z_bytes;
 };
 
-template <int BM, int BN, int NST, int NL>
+template <int BM, int BN, int NST, int NL, int IN>
 __global__ __launch_bounds__(256) void conv_tr_fwd_kernel(Args a) {
   constexpr int WTM = BM / 2, WTN = BN / 2, TM = WTM / 16, TN = WTN / 16;
   constexpr int CB = BN * 64 / 8 / 256;  // B DMA instructions per thread per k-step
@@ -112,6 +127,8 @@ __global__ __launch_bounds__(256) void conv_tr_fwd_kernel(Args a) {
   const int aelems = a.abuf_elems;                      // one patch buffer (bf16 elements)
   unsigned short* abuf = smem;                          // 2 patch buffers
   unsigned short* bring = smem + 2 * aelems;            // NST x BTILE
+  float* cf = reinterpret_cast<float*>(bring + NST * BTILE);  // IN: [2][C] scale | shift
+  constexpr int NP = IN == 2 ? 4 : 1;                   // source loads per patch item
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -132,13 +149,43 @@ __global__ __launch_bounds__(256) void conv_tr_fwd_kernel(Args a) {
   const int n0 = (tm / a.bands) * a.imgs;
   const int h0 = (tm % a.bands) * a.rows;  // first output row of the band
 
-  const __amdgpu_buffer_rsrc_t rsA = make_rsrc(a.x, a.x_bytes);
+  const __amdgpu_buffer_rsrc_t rsA = IN ? make_rsrc(a.zin, a.z_bytes) : make_rsrc(a.x, a.x_bytes);
+  if (IN) {
+    // BatchNorm finalize of the input channels (batch statistics of zin over N*Hz*Wz), as
+    // bn_act.hip fold_fwd_coeffs: every block reduces the replicas into LDS; block 0 also
+    // writes the coefficient table for the backward
+    const int Hz = IN == 2 ? 2 * H : H, Wz = IN == 2 ? 2 * W : W;
+    const float Mz = (float)a.N * Hz * Wz;
+    for (int c = tid; c < C; c += 256) {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int r = 0; r < kStatRep; ++r) {
+        s1 += a.in_stats[r * 2 * C + c];
+        s2 += a.in_stats[r * 2 * C + C + c];
+      }
+      const float mu = s1 / Mz;
+      const float var = fmaxf(s2 / Mz - mu * mu, 0.f);
+      const float is = rsqrtf(var + a.in_eps);
+      const float sc = a.in_gamma[c] * is, sh = a.in_beta[c] - mu * sc;
+      cf[c] = sc;
+      cf[C + c] = sh;
+      if (blockIdx.x == 0) {
+        a.in_coef[0 * C + c] = sc;
+        a.in_coef[1 * C + c] = sh;
+        a.in_coef[2 * C + c] = mu;
+        a.in_coef[3 * C + c] = is;
+      }
+    }
+    __syncthreads();
+  }
   const __amdgpu_buffer_rsrc_t rsB = make_rsrc(a.wc, a.w_bytes);
 
   // ---- A patch loads: item u*256 + tid = (stored pixel, chunk) with the chunk fastest (eight
   // lanes read one pixel's 128 B); destination = plane `chunk` at the pixel's patch index
   unsigned asrc[NL];
   int adst[NL];  // byte offset in a patch buffer, -1 = no item
+  int ydst[NL];  // IN: element offset of the item in y_out (channel block 0), -1 = not written
+  const bool write_y = IN && tn == 0;
   {
     const int pw = (a.rows + 2) * W;  // stored pixels per image
     const int npix = a.imgs * pw;
@@ -147,31 +194,81 @@ __global__ __launch_bounds__(256) void conv_tr_fwd_kernel(Args a) {
       const int it = u * 256 + tid;
       const int px = it >> 3, c = it & 7;
       unsigned off = kOOB;
-      int dst = -1;
+      int dst = -1, yd = -1;
       if (px < npix) {
         const int img = px / pw, loc = px - img * pw;
         const int hr = loc / W, wc = loc - hr * W;
         const int h = h0 + hr - 1;
-        if (h >= 0 && h < H) off = (unsigned)(2 * ((((n0 + img) * H + h) * W + wc) * C + c * 8));
+        if (h >= 0 && h < H) {
+          const int n = n0 + img;
+          if (IN == 2)  // top-left pixel of the 2x2 window in zin [N][2H][2W][C]
+            off = (unsigned)(2 * (((n * 2 * H + 2 * h) * 2 * W + 2 * wc) * C + c * 8));
+          else
+            off = (unsigned)(2 * (((n * H + h) * W + wc) * C + c * 8));
+          // the band's own rows (not its halo) are materialised by the first column tile
+          if (write_y && hr >= 1 && hr <= a.rows) yd = ((n * H + h) * W + wc) * C + c * 8;
+        }
         dst = (plane_base(c, a.plane) + img * a.imgp + loc) * 16;
       }
       asrc[u] = off;
       adst[u] = dst;
+      ydst[u] = yd;
     }
   }
   typedef int v4i __attribute__((ext_vector_type(4)));
-  v4i areg[NL];
+  v4i areg[NL][NP];
+  // (IN == 2) byte offsets of the window's other three pixels: (0, 1), (1, 0), (1, 1)
+  const unsigned pofs[4] = {0u, (unsigned)(2 * C), (unsigned)(2 * 2 * W * C),
+                            (unsigned)(2 * (2 * W * C + C))};
   auto load_a = [&](int cb) {
     const unsigned coff = (unsigned)(cb * 128);
 #pragma unroll
     for (int u = 0; u < NL; ++u)
-      areg[u] = __builtin_amdgcn_raw_buffer_load_b128(rsA, (int)(asrc[u] + coff), 0, 0);
-  };
-  auto store_a = [&](int buf) {
-    char* dst = reinterpret_cast<char*>(abuf + buf * aelems);
 #pragma unroll
-    for (int u = 0; u < NL; ++u)
-      if (adst[u] >= 0) *reinterpret_cast<v4i*>(dst + adst[u]) = areg[u];
+      for (int d = 0; d < NP; ++d)
+        areg[u][d] = __builtin_amdgcn_raw_buffer_load_b128(rsA, (int)(asrc[u] + coff + pofs[d]), 0, 0);
+  };
+  auto store_a = [&](int buf, int cb) {
+    char* dst = reinterpret_cast<char*>(abuf + buf * aelems);
+    float sc[8], sh[8];
+    if (IN) {  // this thread's eight channels (its chunk is the same for every item)
+      const int c0 = cb * 64 + (tid & 7) * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sc[e] = cf[c0 + e];
+        sh[e] = cf[C + c0 + e];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NL; ++u) {
+      if (adst[u] < 0) continue;
+      v4i v = areg[u][0];
+      if (IN) {
+        if (asrc[u] == kOOB) {
+          v = (v4i){0, 0, 0, 0};  // conv zero padding of the post-BN activation
+        } else {
+          float best[8];
+#pragma unroll
+          for (int d = 0; d < NP; ++d) {
+            const v4i q = areg[u][d];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const unsigned w32 = (unsigned)q[e >> 1];
+              const float zf = __uint_as_float((e & 1) ? (w32 & 0xffff0000u) : (w32 << 16));
+              float y = zf * sc[e] + sh[e];
+              if (a.in_relu) y = fmaxf(y, 0.f);
+              if (d == 0 || y > best[e] || y != y) best[e] = y;  // bn_act.hip's pool rule
+            }
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            v[e] = (int)((unsigned)f2bf(best[2 * e]) | ((unsigned)f2bf(best[2 * e + 1]) << 16));
+          if (ydst[u] >= 0)
+            *reinterpret_cast<v4i*>(a.y_out + ydst[u] + cb * 64) = v;
+        }
+      }
+      *reinterpret_cast<v4i*>(dst + adst[u]) = v;
+    }
   };
   // ---- B (weights) DMA: row (tid >> 3) + 32 i of the [col][k] tile, logical chunk lcB
   const int lcB = (tid & 7) ^ ((tid >> 4) & 7);
@@ -248,7 +345,7 @@ __global__ __launch_bounds__(256) void conv_tr_fwd_kernel(Args a) {
 #pragma unroll
   for (int s = 0; s < NST - 1; ++s)
     if (s < nsteps) issue_b(s, s);
-  store_a(0);  // (waits for the patch loads, not for the B DMAs issued after them)
+  store_a(0, cb0);  // (waits for the patch loads, not for the B DMAs issued after them)
 
   // ---- main loop: channel blocks x the nine taps (unrolled: tap offsets, the zero-column
   // selects and the wait counts are compile-time). Wait count at k-step j = vector-memory
@@ -266,14 +363,14 @@ __global__ __launch_bounds__(256) void conv_tr_fwd_kernel(Args a) {
       const int bafter = min(NST - 2, nsteps - 1 - j);
       const bool anext = (t >= 1 && t <= NST - 2) && more;
       if (t == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      wait_stage<NST - 2, CB, NL>(bafter, anext);
+      wait_stage<NST - 2, CB, NL * NP>(bafter, anext);
       // every wave finished k-step j-1: ring slot (j-1) % NST is free
       if (t == 0 && more) load_a(cb0 + cbl + 1);
       if (j + NST - 1 < nsteps) issue_b(j + NST - 1, slot == 0 ? NST - 1 : slot - 1);
       compute(t, cbl & 1, slot);
       // after the last tap: the next patch goes to the other buffer (its readers, channel
       // block cb-1, all passed this block's first barrier)
-      if (t == 8 && more) store_a((cbl + 1) & 1);
+      if (t == 8 && more) store_a((cbl + 1) & 1, cb0 + cbl + 1);
       slot = slot + 1 == NST ? 0 : slot + 1;
     }
   }
@@ -443,38 +540,44 @@ static Geo geometry(int BM, int N, int H, int W) {
   return g;
 }
 
-template <int BM, int BN, int NST, int NL>
+static size_t lds_bytes(const Args& a, int nst, int bn, int in) {
+  return 2 * (size_t)a.abuf_elems * 2 + (size_t)nst * bn * 64 * 2 + (in ? 2 * (size_t)a.C * 4 : 0);
+}
+
+template <int BM, int BN, int NST, int NL, int IN>
 static void launch_t(const Args& a, int items, hipStream_t st) {
-  const size_t lds = 2 * (size_t)a.abuf_elems * 2 + (size_t)NST * BN * 64 * 2;
+  const size_t lds = lds_bytes(a, NST, BN, IN);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv_tr_fwd_kernel<BM, BN, NST, NL>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv_tr_fwd_kernel<BM, BN, NST, NL, IN>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((conv_tr_fwd_kernel<BM, BN, NST, NL>), dim3(items), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((conv_tr_fwd_kernel<BM, BN, NST, NL, IN>), dim3(items), dim3(256), lds, st, a);
 }
 
-template <int BM, int BN, int NST>
+template <int BM, int BN, int NST, int IN>
 static bool launch_nl(const Args& a, int nl, int items, hipStream_t st) {
-  if (2 * (size_t)a.abuf_elems * 2 + (size_t)NST * BN * 64 * 2 > 160 * 1024) return false;
+  if (lds_bytes(a, NST, BN, IN) > 160 * 1024) return false;
   switch (nl) {
-    case 1: launch_t<BM, BN, NST, 1>(a, items, st); return true;
-    case 2: launch_t<BM, BN, NST, 2>(a, items, st); return true;
-    case 3: launch_t<BM, BN, NST, 3>(a, items, st); return true;
-    case 4: launch_t<BM, BN, NST, 4>(a, items, st); return true;
-    case 5: launch_t<BM, BN, NST, 5>(a, items, st); return true;
-    case 6: launch_t<BM, BN, NST, 6>(a, items, st); return true;
+    case 1: launch_t<BM, BN, NST, 1, IN>(a, items, st); return true;
+    case 2: launch_t<BM, BN, NST, 2, IN>(a, items, st); return true;
+    case 3: launch_t<BM, BN, NST, 3, IN>(a, items, st); return true;
+    case 4: launch_t<BM, BN, NST, 4, IN>(a, items, st); return true;
+    case 5: launch_t<BM, BN, NST, 5, IN>(a, items, st); return true;
+    case 6: launch_t<BM, BN, NST, 6, IN>(a, items, st); return true;
     default: return false;
   }
 }
 
 template <int BM, int BN>
-static bool launch_bmbn(int nst, const Args& a, int nl, int items, hipStream_t st) {
+static bool launch_bmbn(int nst, int in, const Args& a, int nl, int items, hipStream_t st) {
+  if (in == 1) return nst == 3 && launch_nl<BM, BN, 3, 1>(a, nl, items, st);
+  if (in == 2) return nst == 3 && launch_nl<BM, BN, 3, 2>(a, nl, items, st);
   switch (nst) {
-    case 3: return launch_nl<BM, BN, 3>(a, nl, items, st);
-    case 5: return launch_nl<BM, BN, 5>(a, nl, items, st);
-    case 8: return launch_nl<BM, BN, 8>(a, nl, items, st);
+    case 3: return launch_nl<BM, BN, 3, 0>(a, nl, items, st);
+    case 5: return launch_nl<BM, BN, 5, 0>(a, nl, items, st);
+    case 8: return launch_nl<BM, BN, 8, 0>(a, nl, items, st);
     default: return false;
   }
 }
@@ -485,20 +588,14 @@ struct Cfg {
   int bm, bn, splits, stages;  // stages: B ring depth (3, 5 or 8; 0 = policy)
 };
 
-static bool launch_stages(const Cfg& c, const Args& a, int nl, int items, hipStream_t st) {
-  // policy: the deepest ring of {8, 5, 3} that fits the 160 KiB LDS (LDS-DMA lands ~1 us after
-  // issue, MI355X_MICROARCH.md "ldsdma-fill": a k-step is latency-bound on the weight stage
-  // unless several are in flight)
-  const int want[3] = {8, 5, 3};
-  for (int i = 0; i < 3; ++i) {
-    const int n = c.stages ? c.stages : want[i];
-    bool ok = false;
-    if (c.bm == 128 && c.bn == 128) ok = launch_bmbn<128, 128>(n, a, nl, items, st);
-    else if (c.bm == 128 && c.bn == 64) ok = launch_bmbn<128, 64>(n, a, nl, items, st);
-    else if (c.bm == 64 && c.bn == 128) ok = launch_bmbn<64, 128>(n, a, nl, items, st);
-    else if (c.bm == 64 && c.bn == 64) ok = launch_bmbn<64, 64>(n, a, nl, items, st);
-    if (ok || c.stages) return ok;
-  }
+// B ring depth: the table's (3 was fastest for every VGG layer: deeper rings cost occupancy,
+// profiles/r3_conv_tr_sweep.jsonl); the fused-input modes are built with 3 only
+static bool launch_stages(const Cfg& c, int in, const Args& a, int nl, int items, hipStream_t st) {
+  const int n = in ? 3 : (c.stages ? c.stages : 3);
+  if (c.bm == 128 && c.bn == 128) return launch_bmbn<128, 128>(n, in, a, nl, items, st);
+  if (c.bm == 128 && c.bn == 64) return launch_bmbn<128, 64>(n, in, a, nl, items, st);
+  if (c.bm == 64 && c.bn == 128) return launch_bmbn<64, 128>(n, in, a, nl, items, st);
+  if (c.bm == 64 && c.bn == 64) return launch_bmbn<64, 64>(n, in, a, nl, items, st);
   return false;
 }
 static std::map<std::tuple<int, int, int, int>, Cfg> g_tr_tuned;
@@ -536,38 +633,43 @@ extern "C" void ddp_conv_tr_set(int mode, int M, int K, int C, int H, int bm, in
   if (mode == 3) tr::g_tr_force = tr::Cfg{bm, bn, splits, stages};
 }
 
-// 3x3 / stride 1 / pad 1 forward through the tap-reuse kernel. Returns 1 when served (z and the
-// statistics written; with ``bn`` and a split-K launch whose finish fused the BatchNorm forward
-// *bn_done = 1), 0 when the shape is not served (caller falls back to ddp_conv_fwd[_bn]),
-// < 0 invalid arguments, >= 2 HIP error (rc - 2).
-extern "C" int ddp_conv_fwd_tr(const ConvGeom* g, const void* x, const void* wc, const float* bias,
-                               void* z, float* stats, float* ws, size_t ws_elems,
-                               const BnFwdFuse* bn, int* bn_done, hipStream_t st) {
-  using namespace ddp_amd::tr;
-  if (bn_done) *bn_done = 0;
+namespace ddp_amd {
+namespace tr {
+struct Plan {
+  Cfg c;
+  Geo geo;
+  int splits, cbps;
+};
+
+// the launch decision shared by ddp_conv_fwd_tr and ddp_conv_tr_would_serve
+static bool plan(const ConvGeom* g, float* ws, size_t ws_elems, int in_mode, Plan* p) {
   if (g_tr_mode < 0) {
     // 0 off, 1 (default) table entries only, 2 also the heuristic for untabled shapes
     const char* e = std::getenv("DDP_AMD_CONV_TR");
     g_tr_mode = e ? std::max(0, std::min(2, std::atoi(e))) : 1;
   }
-  if (!g_tr_mode) return 0;
+  if (!g_tr_mode) return false;
   if (g->R != 3 || g->S != 3 || g->stride != 1 || g->pad != 1 || g->P != g->H || g->Q != g->W)
-    return 0;
-  if (g->C % 64 || g->K % 64 || g->Creal != g->C) return 0;
+    return false;
+  if (g->C % 64 || g->K % 64 || g->Creal != g->C) return false;
   const int N = g->N, H = g->H, W = g->W, C = g->C, K = g->K;
   const size_t M = (size_t)N * H * W;
-  const size_t xe = M * C, we = (size_t)K * 9 * C;
-  if (2 * xe >= kOOB || 2 * we >= kOOB || M * K >= kOOB) return 0;
+  const size_t xe = M * C * (in_mode == 2 ? 4 : 1), we = (size_t)K * 9 * C;
+  if (2 * xe >= kOOB || 2 * we >= kOOB || M * K >= kOOB) return false;
   Cfg c;
   auto it = g_tr_tuned.find(std::make_tuple((int)M, K, C, H));
   if (g_tr_force.bm) c = g_tr_force;
   else if (it != g_tr_tuned.end()) c = it->second;
   else if (g_tr_mode == 2) c = heuristic(N, H, W, C, K);
-  else return 0;  // default: only the layers the measured table assigns to this kernel
-  if (c.bm == 0) return 0;  // table entry "use the implicit-GEMM kernel"
-  if (K % c.bn || M % c.bm) return 0;
+  else return false;  // default: only the layers the measured table assigns to this kernel
+  if (c.bm == 0) return false;  // table entry "use the implicit-GEMM kernel"
+  if (K % c.bn || M % c.bm) return false;
   const Geo geo = geometry(c.bm, N, H, W);
-  if (!geo.ok || geo.nl < 1 || geo.nl > 6) return 0;
+  if (!geo.ok || geo.nl < 1 || geo.nl > 6) return false;
+  const int nst = in_mode ? 3 : (c.stages ? c.stages : 3);
+  const size_t lds = 2 * (size_t)geo.abuf * 2 + (size_t)nst * c.bn * 64 * 2 +
+                     (in_mode ? 2 * (size_t)C * 4 : 0);
+  if (lds > 160 * 1024) return false;
   const int ncb = C / 64;
   int splits = std::max(1, std::min(c.splits, ncb));
   int cbps = (ncb + splits - 1) / splits;
@@ -576,6 +678,35 @@ extern "C" int ddp_conv_fwd_tr(const ConvGeom* g, const void* x, const void* wc,
     splits = 1;
     cbps = ncb;
   }
+  p->c = c;
+  p->geo = geo;
+  p->splits = splits;
+  p->cbps = cbps;
+  return true;
+}
+}  // namespace tr
+}  // namespace ddp_amd
+
+// 3x3 / stride 1 / pad 1 forward through the tap-reuse kernel. ``in`` (optional): the input is
+// computed from the preceding block's conv output while the patch is loaded (TrFwdIn). Returns
+// 1 when served (z and the statistics written; with ``bn`` and a split-K launch whose finish
+// fused this block's BatchNorm forward *bn_done = 1), 0 when not served (caller falls back to
+// ddp_conv_fwd[_bn], after materialising a fused input itself), < 0 invalid arguments, >= 2 HIP
+// error (rc - 2).
+extern "C" int ddp_conv_fwd_tr(const ConvGeom* g, const void* x, const void* wc, const float* bias,
+                               void* z, float* stats, float* ws, size_t ws_elems,
+                               const BnFwdFuse* bn, int* bn_done, const TrFwdIn* in,
+                               hipStream_t st) {
+  using namespace ddp_amd::tr;
+  if (bn_done) *bn_done = 0;
+  const int in_mode = in ? (in->pool ? 2 : 1) : 0;
+  if (in && (!in->z || !in->stats || !in->gamma || !in->beta || !in->coef || !in->y)) return -1;
+  Plan pl;
+  if (!plan(g, ws, ws_elems, in_mode, &pl)) return 0;
+  const Cfg& c = pl.c;
+  const Geo& geo = pl.geo;
+  const int N = g->N, H = g->H, W = g->W, C = g->C, K = g->K;
+  const size_t M = (size_t)N * H * W;
   Args a{};
   a.N = N; a.H = H; a.W = W; a.C = C; a.K = K;
   a.x = (const unsigned short*)x;
@@ -584,26 +715,43 @@ extern "C" int ddp_conv_fwd_tr(const ConvGeom* g, const void* x, const void* wc,
   a.z = (unsigned short*)z;
   a.stats = stats;
   a.ws = ws;
-  a.splits = splits;
-  a.cbps = cbps;
+  a.splits = pl.splits;
+  a.cbps = pl.cbps;
   a.imgs = geo.imgs; a.rows = geo.rows; a.bands = geo.bands;
   a.imgp = geo.imgp; a.plane = geo.plane; a.zslot = geo.zslot;
-  a.x_bytes = (int)(2 * xe);
-  a.w_bytes = (int)(2 * we);
+  a.x_bytes = (int)(2 * M * C);
+  a.w_bytes = (int)(2 * (size_t)K * 9 * C);
   a.abuf_elems = geo.abuf;
   a.tiles_m = (int)(M / c.bm);
   a.tiles_n = K / c.bn;
-  const int items = a.tiles_m * a.tiles_n * splits;
-  bool ok = false;
-  ok = launch_stages(c, a, geo.nl, items, st);
-  if (!ok) return 0;
+  if (in) {
+    a.zin = (const unsigned short*)in->z;
+    a.in_stats = in->stats;
+    a.in_gamma = in->gamma;
+    a.in_beta = in->beta;
+    a.in_eps = in->eps;
+    a.in_relu = in->relu;
+    a.in_coef = in->coef;
+    a.y_out = (unsigned short*)in->y;
+    a.z_bytes = (int)(2 * M * C * (in->pool ? 4 : 1));
+  }
+  const int items = a.tiles_m * a.tiles_n * pl.splits;
+  if (!launch_stages(c, in_mode, a, geo.nl, items, st)) return 0;
   int e = (int)hipGetLastError();
   if (e) return 2 + e;
-  if (splits > 1) {
-    e = ddp_conv_fwd_finish(g, ws, splits, bias, z, stats, bn, bn_done, st);
+  if (pl.splits > 1) {
+    e = ddp_conv_fwd_finish(g, ws, pl.splits, bias, z, stats, bn, bn_done, st);
     if (e) return 2 + e;
   }
   return 1;
+}
+
+// would ddp_conv_fwd_tr serve this problem (with a fused input of mode in_mode: 0 none,
+// 1 BN+ReLU, 2 BN+ReLU+pool)? No launch.
+extern "C" int ddp_conv_tr_would_serve(const ConvGeom* g, size_t ws_elems, int in_mode) {
+  ddp_amd::tr::Plan pl;
+  float dummy;
+  return ddp_amd::tr::plan(g, ws_elems ? &dummy : nullptr, ws_elems, in_mode, &pl) ? 1 : 0;
 }
 
 // host-side geometry probe for tests: (ok, imgs, rows, bands, imgp, plane, na)

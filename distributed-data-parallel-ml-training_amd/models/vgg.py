@@ -73,6 +73,8 @@ class _VGG(nn.Module):
             # this block's dgrad produces the gradient at the previous block's output: it
             # accumulates that block's BatchNorm-backward sums (ops.layers, BnBwdFuse)
             spec.prev = stages[-1] if stages else None
+            if stages:
+                stages[-1].next = spec
             stages.append(spec)
             first = False
             i += 4 if pool else 3

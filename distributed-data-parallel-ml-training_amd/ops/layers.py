@@ -66,6 +66,11 @@ class ConvBNActSpec:
         # this block's input; this block's dgrad accumulates prev's BatchNorm-backward sums in
         # its epilogue and sets ``prev.sums_ready`` so prev's backward skips its reduce pass
         self.prev = None
+        self.next = None  # the block consuming this block's output (VGG chain)
+        # this forward's output y when its BN + ReLU (+ pool) is deferred into the next block's
+        # conv (conv_tr.hip fused input): (y, pool) — the next block's forward computes y while
+        # loading its input patch, or materialises it with bn_act_fwd if it cannot
+        self.deferred = None
         self.fwd_z = None
         self.sums_ready = False
         # set by the next block's backward when its dgrad finish completed this block's BN
@@ -99,14 +104,35 @@ class ConvBNActSpec:
                 wkrsc)
 
 
-def conv_forward(spec, x, bias=None, stats=None, bn_fuse=None):
+def _fin_args(prev, y):
+    """Fused-input tuple of conv_fwd_tr for the preceding block ``prev`` whose output is y."""
+    bn = prev.bn
+    return (ptr(prev.fwd_z), ptr(prev.stats), ptr(bn.weight), ptr(bn.bias), prev.eps,
+            int(prev.relu), int(prev.pool), ptr(prev.coef), ptr(y))
+
+
+def _bn_act_fwd_now(spec, z, y):
+    """The (deferred) BatchNorm + ReLU (+ pool) forward of ``spec`` as its own launch."""
+    N, P, Q, K = z.shape
+    bn = spec.bn
+    native().bn_act_fwd(N, P, Q, K, int(spec.pool), int(spec.relu), spec.eps, ptr(z), 0,
+                        ptr(spec.stats), ptr(bn.weight), ptr(bn.bias), ptr(y), stream_handle(),
+                        0, 0, float(bn.momentum if bn.momentum is not None else 0.1), 0,
+                        ptr(spec.coef))
+
+
+def conv_forward(spec, x, bias=None, stats=None, bn_fuse=None, fin=None):
     """z = conv(x) + bias (bf16 NHWC); stats[16][2][K] += per-channel sum / sumsq of z
     (accumulated into STAT_REPLICAS replicas; the consumer sums them).
 
     ``bn_fuse`` = (gamma, beta, eps, relu, pool, coef, y, P, Q) pointers/values: when the GEMM
     runs split-K and is small (the strong-scaling batches' deep layers), its finish kernel also
     computes the BatchNorm forward into y and the coefficient table (conv_igemm.hip
-    splitk_finish_bnfwd_kernel). Returns (z, fused) then; plain z otherwise."""
+    splitk_finish_bnfwd_kernel). Returns (z, fused) then; plain z otherwise.
+
+    ``fin`` = the preceding block whose BatchNorm + ReLU (+ pool) was deferred (x is its
+    unwritten output): the tap-reuse kernel computes x while loading its patch (and writes it);
+    when that kernel does not serve the shape, x is materialised first by bn_act_fwd."""
     N, H, W, C = x.shape
     check(x, BF16, name="conv input")
     if C != spec.C:
@@ -123,9 +149,12 @@ def conv_forward(spec, x, bias=None, stats=None, bn_fuse=None):
             and spec.C == spec.Cr and spec.C % 64 == 0 and spec.K % 64 == 0):
         # 3x3 tap-reuse kernel (conv_tr.hip): input tile resident in LDS for all nine taps
         r = native().conv_fwd_tr(g, ptr(x), ptr(spec.wc), ptr(bias), ptr(z), ptr(stats), ptr(ws),
-                                 ws.numel(), stream_handle(), bn_fuse)
+                                 ws.numel(), stream_handle(), bn_fuse,
+                                 _fin_args(fin, x) if fin is not None else None)
         if r:
             return (z, r == 2) if bn_fuse is not None else z
+    if fin is not None:
+        _bn_act_fwd_now(fin, fin.fwd_z, x)
     if bn_fuse is not None:
         fused = native().conv_fwd_bn(g, ptr(x), ptr(spec.wc), ptr(bias), ptr(z), ptr(stats),
                                      ptr(ws), ws.numel(), stream_handle(), bn_fuse)
@@ -167,6 +196,15 @@ class GradLink:
 # 3x3 stride-1 forward convolutions through the tap-reuse kernel (conv_tr.hip); =0 restores the
 # implicit-GEMM kernel for every layer (the native side also reads DDP_AMD_CONV_TR)
 CONV_TR = os.environ.get("DDP_AMD_CONV_TR", "1") != "0"
+# a block's BatchNorm + ReLU (+ 2x2 pool) forward computed by the NEXT block's tap-reuse conv
+# while it loads its input patch (conv_tr.hip fused input; no bn_act_fwd launch); =0 restores the
+# separate pass
+# (1 = every eligible block, 2 (default) = only blocks without a max-pool: a pooled block's
+# consumer loads four pre-pool values per input pixel, measured -1 % at 32 images per GPU but
+# +3 % at 256 (profiles/r3_fused_bn_input.md); DDP_AMD_FUSE_BN_IN_MAX_ROWS: only while the
+# consumer GEMM has at most this many rows)
+FUSE_BN_IN = int(os.environ.get("DDP_AMD_FUSE_BN_IN", "2"))
+FUSE_BN_IN_MAX_ROWS = int(os.environ.get("DDP_AMD_FUSE_BN_IN_MAX_ROWS", str(1 << 30)))
 # BatchNorm forward fused into the split-K finish of small conv GEMMs (conv_igemm.hip
 # splitk_finish_bnfwd_kernel; the native side also honours DDP_AMD_BN_FWD_FUSE=0)
 BN_FWD_FUSE = os.environ.get("DDP_AMD_BN_FWD_FUSE", "1") != "0"
@@ -248,15 +286,45 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=Non
     return (dx, bool(done)) if bna is not None else dx
 
 
+def _defer_bn(spec, residual, running_mean, N, Ho, Wo):
+    """Defer this block's BatchNorm + ReLU (+ pool) forward into the next block's conv: only on
+    a plain Conv->BN->ReLU(->pool) chain (no residual, batch statistics) whose next conv the
+    tap-reuse kernel serves with a fused input (conv_tr.hip)."""
+    nxt = spec.next
+    if (not FUSE_BN_IN or not CONV_TR or nxt is None or residual is not None
+            or running_mean is not None or nxt.C != spec.K or nxt.Cr != nxt.C
+            or nxt.R != 3 or nxt.stride != 1 or nxt.pad != 1):
+        return False
+    if (FUSE_BN_IN == 2 and spec.pool) or N * Ho * Wo > FUSE_BN_IN_MAX_ROWS:
+        return False
+    if spec.pool and (Ho * 2 != spec._out_p or Wo * 2 != spec._out_q):
+        return False
+    g = nxt.geom(N, Ho, Wo)
+    return bool(native().conv_tr_would_serve(g, workspace(nxt.wc.device).numel(),
+                                             2 if spec.pool else 1))
+
+
 class _ConvBNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, gamma, beta, residual, spec, in_link=None, res_link=None):
         spec.maybe_pack()
         spec.dz_fused = None  # a fused BN backward of an earlier pass must never be consumed
+        spec.deferred = None
+        # the preceding block deferred its BatchNorm forward into this conv (x = its unwritten
+        # output; a pipelined step's cut passes a detached view of the same storage)
+        prev = spec.prev
+        fin = None
+        if prev is not None and prev.deferred is not None:
+            if prev.deferred.data_ptr() == x.data_ptr():
+                fin = prev
+            else:  # not consumed by this block: materialise it where it is
+                _bn_act_fwd_now(prev, prev.fwd_z, prev.deferred)
+            prev.deferred = None
         N, H, W, _ = x.shape
         stats = spec.stats  # zeroed by the model's per-forward StepScratch.zero()
         P, Q = spec.out_hw(H, W)
         Ho, Wo = (P // 2, Q // 2) if spec.pool else (P, Q)
+        spec._out_p, spec._out_q = P, Q
         y = torch.empty(N, Ho, Wo, spec.K, dtype=BF16, device=x.device)
         if residual is not None:
             check(residual, BF16, (N, P, Q, spec.K), "residual")
@@ -271,10 +339,15 @@ class _ConvBNActFn(torch.autograd.Function):
             # batch-statistics BN without residual (VGG): may run inside the conv's split-K finish
             z, fused = conv_forward(spec, x, bias, stats,
                                     bn_fuse=(ptr(gamma), ptr(beta), spec.eps, int(spec.relu),
-                                             int(spec.pool), ptr(spec.coef), ptr(y), P, Q))
+                                             int(spec.pool), ptr(spec.coef), ptr(y), P, Q),
+                                    fin=fin)
         else:
-            z = conv_forward(spec, x, bias, stats)
-        if not fused:
+            z = conv_forward(spec, x, bias, stats, fin=fin)
+        spec.fwd_z = z
+        spec.last_deferred = not fused and _defer_bn(spec, residual, rm, N, Ho, Wo)
+        if spec.last_deferred:
+            spec.deferred = y  # computed by the next block's conv (conv_tr.hip fused input)
+        elif not fused:
             native().bn_act_fwd(N, P, Q, spec.K, int(spec.pool), int(spec.relu), spec.eps, ptr(z),
                                 ptr(residual), ptr(stats), ptr(gamma), ptr(beta), ptr(y),
                                 stream_handle(), ptr(rm), ptr(rv),
@@ -283,7 +356,6 @@ class _ConvBNActFn(torch.autograd.Function):
         ctx.spec = spec
         ctx.has_res = residual is not None
         ctx.in_link, ctx.res_link = in_link, res_link
-        spec.fwd_z = z
         # the preceding block's conv output of THIS forward (for the fused BN-backward sums)
         ctx.prev_z = spec.prev.fwd_z if spec.prev is not None else None
         ctx.save_for_backward(x, z, stats, weight, bias, gamma, beta, residual)

@@ -120,3 +120,95 @@ def test_conv_tr_default_policy_serves_vgg_layers(native_ext):
                 torch.cuda.synchronize()
                 ref = F.conv2d(x, conv.weight, conv.bias, 1, 1).permute(0, 2, 3, 1)
                 assert rel_err(z, ref) < 1e-2, (B, C, K, H)
+
+
+@pytest.mark.parametrize("N,C,Hz,K,pool,cfg", [
+    (8, 128, 16, 256, True, (64, 64, 1)),     # VGG 128 -> pool -> 8x8 conv 256
+    (8, 256, 8, 256, False, (128, 64, 1)),    # VGG 256 8x8 -> 8x8 conv (no pool)
+    (32, 512, 4, 512, True, (64, 64, 8)),     # 4x4 -> pool -> 2x2, split-K 8
+    (16, 256, 8, 512, True, (64, 128, 4)),    # 8x8 -> pool -> 4x4, split-K 4
+])
+def test_conv_tr_fused_bn_input(native_ext, N, C, Hz, K, pool, cfg):
+    """Fused input mode (api.h TrFwdIn): the conv computes its input x = [pool](relu(bn(z)))
+    from the preceding block's conv output while loading its patch, writes x (the wgrad operand)
+    and the preceding block's coefficient table. Against the separate bn_act_fwd pass + the same
+    conv on its output: x and the table bit-identical (same fold order, same formula), z equal."""
+    from ddp_amd.ops.common import ptr, stream_handle, workspace
+    nat = native_ext
+    H = Hz // 2 if pool else Hz
+    conv, spec, _, _ = _conv_setup(N, C, H, H, K, 3, 1, 1)
+    zin = (torch.randn(N, Hz, Hz, C, device=DEV) * 2 + 0.5).to(torch.bfloat16)
+    stats = torch.zeros(16, 2, C, device=DEV)
+    zf = zin.float().reshape(-1, C)
+    stats[3, 0] = zf.sum(0)  # one replica holds the sums (as the producer's atomics would)
+    stats[3, 1] = (zf * zf).sum(0)
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV) * 0.1
+    ws = workspace(torch.device(DEV))
+    s = stream_handle()
+    g = spec.geom(N, H, H)
+    # reference: bn_act_fwd then the conv on its output
+    x_ref = torch.empty(N, H, H, C, device=DEV, dtype=torch.bfloat16)
+    coef_ref = torch.zeros(6 * C, device=DEV)
+    nat.bn_act_fwd(N, Hz, Hz, C, int(pool), 1, 1e-5, ptr(zin), 0, ptr(stats), ptr(gamma),
+                   ptr(beta), ptr(x_ref), s, coef=ptr(coef_ref))
+    z_ref = torch.empty(N, H, H, K, device=DEV, dtype=torch.bfloat16)
+    st_ref = torch.zeros(16 * 2 * K, device=DEV)
+    _force(nat, *cfg)
+    try:
+        assert nat.conv_fwd_tr(g, ptr(x_ref), ptr(spec.wc), ptr(conv.bias), ptr(z_ref),
+                               ptr(st_ref), ptr(ws), ws.numel(), s) == 1
+        x = torch.full_like(x_ref, float("nan"))
+        coef = torch.zeros(6 * C, device=DEV)
+        z = torch.empty_like(z_ref)
+        st = torch.zeros_like(st_ref)
+        fin = (ptr(zin), ptr(stats), ptr(gamma), ptr(beta), 1e-5, 1, int(pool), ptr(coef), ptr(x))
+        r = nat.conv_fwd_tr(g, 0, ptr(spec.wc), ptr(conv.bias), ptr(z), ptr(st), ptr(ws),
+                            ws.numel(), s, None, fin)
+    finally:
+        _force(nat, 0, 0, 0)
+    torch.cuda.synchronize()
+    assert r == 1
+    assert torch.equal(x, x_ref), float((x.float() - x_ref.float()).abs().max())
+    assert torch.equal(coef[:4 * C], coef_ref[:4 * C])
+    assert rel_err(z, z_ref) < 1e-3
+    ref = F.conv2d(x_ref.float().permute(0, 3, 1, 2), conv.weight, conv.bias, 1, 1)
+    assert rel_err(z.permute(0, 3, 1, 2), ref) < 1e-2
+
+
+def test_vgg_forward_with_deferred_bn_matches_separate_passes(native_ext):
+    """Model level: with the BatchNorm forward of each block deferred into the next block's
+    tap-reuse conv (ops/layers.py _defer_bn) the VGG-11 forward and its gradients equal the
+    separate-pass forward (same kernels otherwise; only atomics order differs)."""
+    import copy
+    from ddp_amd.models import VGG11
+    from ddp_amd.engine import CrossEntropyLoss
+    from ddp_amd.ops import layers
+    torch.manual_seed(3)
+    base = VGG11().cuda()
+    x = torch.randn(32, 3, 32, 32, device=DEV)
+    y = torch.randint(0, 10, (32,), device=DEV)
+    out = {}
+    for fuse in (False, True):
+        layers.FUSE_BN_IN = fuse
+        try:
+            m = copy.deepcopy(base)
+            m._plan = None
+            loss = CrossEntropyLoss()(m(x), y)
+            loss.backward()
+            torch.cuda.synchronize()
+            ndef = sum(1 for sp in m.fused_plan() if getattr(sp, "last_deferred", False))
+            out[fuse] = (float(loss), torch.cat([p.grad.reshape(-1) for p in m.parameters()]))
+            if fuse:
+                deferred = ndef
+            else:
+                assert ndef == 0
+        finally:
+            layers.FUSE_BN_IN = True
+    # every block whose next conv the tap-reuse table serves (blocks 0-5 at 32 images; block 6's
+    # BatchNorm already runs inside its own split-K finish)
+    assert deferred >= 5, deferred
+    assert abs(out[True][0] - out[False][0]) < 1e-3 * abs(out[False][0])
+    a, b = out[True][1], out[False][1]
+    cos = float(torch.dot(a, b) / (a.norm() * b.norm()))
+    assert cos > 0.99, cos

@@ -304,15 +304,17 @@ def test_bn_fused_into_splitk_finishes_matches_unfused(native_ext):
     nat = native()
     taken = {"fwd": 0, "bwd": 0, "head": 0}
     orig = {k: getattr(nat, k) for k in ("conv_fwd_bn", "conv_bwd_pair", "conv_dgrad",
-                                         "linear_dx_bn")}
+                                         "linear_dx_bn", "conv_fwd_tr")}
 
-    def spy(name, key):
+    def spy(name, key, fused_value=None):
         def f(*args, **kw):
             r = orig[name](*args, **kw)
-            taken[key] += int(bool(r))
+            taken[key] += int(r == fused_value) if fused_value is not None else int(bool(r))
             return r
         return f
     nat.conv_fwd_bn = spy("conv_fwd_bn", "fwd")
+    # the tap-reuse conv's split-K finish fuses the BatchNorm forward the same way (returns 2)
+    nat.conv_fwd_tr = spy("conv_fwd_tr", "fwd", 2)
     nat.conv_bwd_pair = spy("conv_bwd_pair", "bwd")
     nat.conv_dgrad = spy("conv_dgrad", "bwd")
     nat.linear_dx_bn = spy("linear_dx_bn", "head")
