@@ -153,6 +153,14 @@ PYBIND11_MODULE(_native, m) {
   }, py::arg("g"), py::arg("x"), py::arg("wc"), py::arg("bias"), py::arg("z"), py::arg("stats"),
      py::arg("ws"), py::arg("ws_elems"), py::arg("st"), py::arg("bn") = py::none(),
      py::arg("fin") = py::none());
+  m.def("conv_dgrad_tr", [](py::tuple g, uintptr_t dz, uintptr_t wt, uintptr_t dx, uintptr_t ws,
+                            size_t ws_elems, uintptr_t st) {
+    auto c = geom(g);
+    const int rc = ddp_conv_dgrad_tr(&c, P<void>(dz), P<void>(wt), P<void>(dx), P<float>(ws),
+                                     ws_elems, S(st));
+    if (rc >= 2) check(rc - 2, "conv_dgrad_tr");
+    return rc == 1;
+  });
   m.def("conv_tr_would_serve", [](py::tuple g, size_t ws_elems, int in_mode) {
     auto c = geom(g);
     return ddp_conv_tr_would_serve(&c, ws_elems, in_mode) == 1;

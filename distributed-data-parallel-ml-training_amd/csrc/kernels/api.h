@@ -150,8 +150,12 @@ int ddp_conv_fwd_tr(const ddp_amd::ConvGeom* g, const void* x, const void* wc, c
                     const ddp_amd::BnFwdFuse* bn, int* bn_done, const ddp_amd::TrFwdIn* in,
                     hipStream_t st);
 int ddp_conv_tr_would_serve(const ddp_amd::ConvGeom* g, size_t ws_elems, int in_mode);
+// backward-data of a 3x3/s1/p1 conv through the tap-reuse kernel (wt = bf16 [C][3][3][K]);
+// g = the forward geometry; 1 served, 0 not served, >= 2 HIP error (rc - 2)
+int ddp_conv_dgrad_tr(const ddp_amd::ConvGeom* g, const void* dz, const void* wt, void* dx,
+                      float* ws, size_t ws_elems, hipStream_t st);
 // tap-reuse policy: mode -1 clear table, 0/1 disable/enable (table entries), 4 enable with the
-// heuristic for untabled shapes, 2 table entry (M, K, C, H) ->
+// heuristic for untabled shapes, 2 forward / 5 backward-data table entry (M, K, C, H) ->
 // (bm, bn, splits, stages) (bm = 0: use the implicit-GEMM kernel), 3 force the same (sweeps)
 void ddp_conv_tr_set(int mode, int M, int K, int C, int H, int bm, int bn, int splits, int stages);
 int ddp_conv_tr_geometry(int BM, int N, int H, int W, int* out7);

@@ -99,6 +99,8 @@ struct Args {
   int x_bytes, w_bytes;
   int tiles_m, tiles_n;
   int abuf_elems;            // bf16 elements of one patch buffer (16-B multiple)
+  int flip;                  // weights read at tap 8 - t (backward-data: dx = conv(dz, W
+                             // flipped + transposed), wc = the [C][3][3][K] copy)
   // fused input (template IN = 1: BN + ReLU, IN = 2: BN + ReLU + 2x2/s2 max-pool): the conv
   // input x = [pool](relu(scale * zin + shift)) is computed while the patch is loaded; zin is
   // the preceding block's conv output [N][Hz][Wz][C] (Hz = 2H when pooled), its BatchNorm
@@ -281,7 +283,8 @@ __global__ __launch_bounds__(256) void conv_tr_fwd_kernel(Args a) {
 
   auto issue_b = [&](int j, int slot) {
     const int cb = cb0 + j / 9, t = j - (j / 9) * 9;
-    const unsigned k0 = (unsigned)(2 * (t * C + cb * 64));
+    const int tw = a.flip ? 8 - t : t;
+    const unsigned k0 = (unsigned)(2 * (tw * C + cb * 64));
     unsigned short* dst = bring + slot * BTILE;
 #pragma unroll
     for (int i = 0; i < CB; ++i) dma(rsB, boff[i] + k0, dst + (wid * 64 + 256 * i) * 8);
@@ -598,7 +601,7 @@ static bool launch_stages(const Cfg& c, int in, const Args& a, int nl, int items
   if (c.bm == 64 && c.bn == 64) return launch_bmbn<64, 64>(n, in, a, nl, items, st);
   return false;
 }
-static std::map<std::tuple<int, int, int, int>, Cfg> g_tr_tuned;
+static std::map<std::tuple<int, int, int, int, int>, Cfg> g_tr_tuned;  // (op, M, K, C, H)
 static int g_tr_mode = -1;  // -1 unread; 0 off; 1 on (DDP_AMD_CONV_TR)
 static Cfg g_tr_force{0, 0, 0, 0};
 
@@ -629,7 +632,8 @@ extern "C" void ddp_conv_tr_set(int mode, int M, int K, int C, int H, int bm, in
   // mode: -1 clear table, 0/1 enable, 2 add table entry, 3 force (bm, bn, splits) for sweeps
   if (mode == -1) { tr::g_tr_tuned.clear(); return; }
   if (mode == 0 || mode == 1 || mode == 4) { tr::g_tr_mode = mode == 4 ? 2 : mode; return; }
-  if (mode == 2) { tr::g_tr_tuned[std::make_tuple(M, K, C, H)] = tr::Cfg{bm, bn, splits, stages}; return; }
+  if (mode == 2 || mode == 5)  // 2: forward entry, 5: backward-data entry (dgrad GEMM's K, C)
+    { tr::g_tr_tuned[std::make_tuple(mode == 5 ? 1 : 0, M, K, C, H)] = tr::Cfg{bm, bn, splits, stages}; return; }
   if (mode == 3) tr::g_tr_force = tr::Cfg{bm, bn, splits, stages};
 }
 
@@ -642,7 +646,8 @@ struct Plan {
 };
 
 // the launch decision shared by ddp_conv_fwd_tr and ddp_conv_tr_would_serve
-static bool plan(const ConvGeom* g, float* ws, size_t ws_elems, int in_mode, Plan* p) {
+static bool plan(const ConvGeom* g, float* ws, size_t ws_elems, int in_mode, Plan* p,
+                 int op = 0) {
   if (g_tr_mode < 0) {
     // 0 off, 1 (default) table entries only, 2 also the heuristic for untabled shapes
     const char* e = std::getenv("DDP_AMD_CONV_TR");
@@ -657,10 +662,10 @@ static bool plan(const ConvGeom* g, float* ws, size_t ws_elems, int in_mode, Pla
   const size_t xe = M * C * (in_mode == 2 ? 4 : 1), we = (size_t)K * 9 * C;
   if (2 * xe >= kOOB || 2 * we >= kOOB || M * K >= kOOB) return false;
   Cfg c;
-  auto it = g_tr_tuned.find(std::make_tuple((int)M, K, C, H));
+  auto it = g_tr_tuned.find(std::make_tuple(op, (int)M, K, C, H));
   if (g_tr_force.bm) c = g_tr_force;
   else if (it != g_tr_tuned.end()) c = it->second;
-  else if (g_tr_mode == 2) c = heuristic(N, H, W, C, K);
+  else if (g_tr_mode == 2 && op == 0) c = heuristic(N, H, W, C, K);
   else return false;  // default: only the layers the measured table assigns to this kernel
   if (c.bm == 0) return false;  // table entry "use the implicit-GEMM kernel"
   if (K % c.bn || M % c.bm) return false;
@@ -746,11 +751,65 @@ extern "C" int ddp_conv_fwd_tr(const ConvGeom* g, const void* x, const void* wc,
   return 1;
 }
 
+// Backward-data of a 3x3 / stride 1 / pad 1 conv through the tap-reuse kernel: dx = conv(dz,
+// flip(W)^T) — the same 3x3 problem with the channel roles swapped (input dz with K channels,
+// output dx with C channels) and the weights read from the transposed copy wt [C][3][3][K] at
+// tap 8 - t. g = the FORWARD geometry. Returns 1 served, 0 not served (use ddp_conv_dgrad /
+// the backward pair), >= 2 HIP error.
+extern "C" int ddp_conv_dgrad_tr(const ConvGeom* g, const void* dz, const void* wt, void* dx,
+                                 float* ws, size_t ws_elems, hipStream_t st) {
+  using namespace ddp_amd::tr;
+  ConvGeom t = *g;
+  t.C = g->K;
+  t.K = g->C;
+  t.Creal = g->K;
+  if (g->Creal != g->C) return 0;
+  Plan pl;
+  if (!plan(&t, ws, ws_elems, 0, &pl, 1)) return 0;
+  const Cfg& c = pl.c;
+  const Geo& geo = pl.geo;
+  const size_t M = (size_t)t.N * t.H * t.W;
+  Args a{};
+  a.N = t.N; a.H = t.H; a.W = t.W; a.C = t.C; a.K = t.K;
+  a.x = (const unsigned short*)dz;
+  a.wc = (const unsigned short*)wt;
+  a.z = (unsigned short*)dx;
+  a.ws = ws;
+  a.splits = pl.splits;
+  a.cbps = pl.cbps;
+  a.imgs = geo.imgs; a.rows = geo.rows; a.bands = geo.bands;
+  a.imgp = geo.imgp; a.plane = geo.plane; a.zslot = geo.zslot;
+  a.x_bytes = (int)(2 * M * t.C);
+  a.w_bytes = (int)(2 * (size_t)t.K * 9 * t.C);
+  a.abuf_elems = geo.abuf;
+  a.tiles_m = (int)(M / c.bm);
+  a.tiles_n = t.K / c.bn;
+  a.flip = 1;
+  const int items = a.tiles_m * a.tiles_n * pl.splits;
+  if (!launch_stages(c, 0, a, geo.nl, items, st)) return 0;
+  int e = (int)hipGetLastError();
+  if (e) return 2 + e;
+  if (pl.splits > 1) {
+    e = ddp_conv_fwd_finish(&t, ws, pl.splits, nullptr, dx, nullptr, nullptr, nullptr, st);
+    if (e) return 2 + e;
+  }
+  return 1;
+}
+
 // would ddp_conv_fwd_tr serve this problem (with a fused input of mode in_mode: 0 none,
 // 1 BN+ReLU, 2 BN+ReLU+pool)? No launch.
+// (in_mode -1: the backward-data problem of ddp_conv_dgrad_tr for the forward geometry g)
 extern "C" int ddp_conv_tr_would_serve(const ConvGeom* g, size_t ws_elems, int in_mode) {
   ddp_amd::tr::Plan pl;
   float dummy;
+  if (in_mode < 0) {
+    ConvGeom t = *g;
+    t.C = g->K;
+    t.K = g->C;
+    t.Creal = g->K;
+    if (g->Creal != g->C) return 0;
+    return ddp_amd::tr::plan(&t, ws_elems ? &dummy : nullptr, ws_elems, 0, &pl, 1) ? 1 : 0;
+  }
   return ddp_amd::tr::plan(g, ws_elems ? &dummy : nullptr, ws_elems, in_mode, &pl) ? 1 : 0;
 }
 

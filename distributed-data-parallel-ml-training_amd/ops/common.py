@@ -37,6 +37,10 @@ def native():
 TUNING_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "conv_tuning.json")
 
 
+# (forward K, forward C) of the 3x3 layers whose backward-data the tap-reuse table serves
+TR_DGRAD_SHAPES = set()
+
+
 def load_conv_tuning(n=None, path=None):
     """Load the measured conv tile / split-K table (tools/conv_tune.py) into the native launcher.
     DDP_AMD_CONV_TUNING=0 ignores it (cost-model choices only). Returns the number of entries."""
@@ -57,7 +61,16 @@ def load_conv_tuning(n=None, path=None):
     for e in table.get("tr_entries", []):
         n.conv_tr_set(2, int(e["M"]), int(e["K"]), int(e["C"]), int(e["H"]), int(e["bm"]),
                       int(e["bn"]), int(e["splits"]), int(e.get("stages", 0)))
-    return len(table.get("entries", [])) + len(table.get("tr_entries", []))
+    # backward-data entries: keyed by the dgrad problem (M, K = forward C, C = forward K, H);
+    # the layers with at least one served entry get a transposed weight copy (ops/layers.py)
+    TR_DGRAD_SHAPES.clear()
+    for e in table.get("tr_dgrad_entries", []):
+        if int(e["bm"]) > 0:
+            TR_DGRAD_SHAPES.add((int(e["C"]), int(e["K"])))  # (forward K, forward C)
+        n.conv_tr_set(5, int(e["M"]), int(e["K"]), int(e["C"]), int(e["H"]), int(e["bm"]),
+                      int(e["bn"]), int(e["splits"]), int(e.get("stages", 0)))
+    return (len(table.get("entries", [])) + len(table.get("tr_entries", []))
+            + len(table.get("tr_dgrad_entries", [])))
 
 
 def weight_krsc(w):

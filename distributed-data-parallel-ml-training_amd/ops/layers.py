@@ -46,8 +46,14 @@ class ConvBNActSpec:
         self.eps = float(bn.eps) if bn is not None else 1e-5
         dev = conv.weight.device
         self.wc = torch.empty(K, R, S, self.C, dtype=BF16, device=dev)
-        # (no transposed copy: the dgrad GEMM reads Wc k-major through transposing LDS reads)
+        # transposed copy [C][R][S][K] only for the tap-reuse backward-data kernel (conv_tr.hip
+        # ddp_conv_dgrad_tr); the implicit-GEMM dgrad reads Wc k-major through transposing LDS
+        # reads and needs none
         self.wt = None
+        if (DGRAD_TR and R == 3 and S == 3 and conv.stride[0] == 1 and conv.padding[0] == 1
+                and self.C == Cr and Cr % 64 == 0 and K % 64 == 0 and dev.type == "cuda"
+                and (DGRAD_TR == 2 or (K, Cr) in _common.TR_DGRAD_SHAPES)):
+            self.wt = torch.empty(self.C, R, S, K, dtype=BF16, device=dev)
         self._packed_version = None
         conv.weight._ddp_amd_pack = self.pack_desc  # the fused optimizer repacks after its step
         # per-step zeroed accumulators (StepScratch): BN statistics replicas + BN-backward sums
@@ -196,6 +202,14 @@ class GradLink:
 # 3x3 stride-1 forward convolutions through the tap-reuse kernel (conv_tr.hip); =0 restores the
 # implicit-GEMM kernel for every layer (the native side also reads DDP_AMD_CONV_TR)
 CONV_TR = os.environ.get("DDP_AMD_CONV_TR", "1") != "0"
+# backward-data of 3x3 stride-1 layers through the tap-reuse kernel where the measured table
+# says so (needs a transposed bf16 weight copy per eligible layer, repacked by the optimizer);
+# =0 (default) keeps the implicit-GEMM dgrad / backward pair everywhere. Opt-in: the kernel
+# wins per layer at 256 images (profiles/r3_conv_tr_dgrad_sweep.jsonl) but the transposed-copy
+# repack in the fused SGD costs more than it saves end to end (b256 0.8887 vs 0.8857 ms,
+# b32 0.4421 vs 0.4164 ms, same box; profiles/r3_conv_tr_dgrad.md)
+# (2: give every eligible layer the copy, e.g. for sweeps)
+DGRAD_TR = int(os.environ.get("DDP_AMD_DGRAD_TR", "0"))
 # a block's BatchNorm + ReLU (+ 2x2 pool) forward computed by the NEXT block's tap-reuse conv
 # while it loads its input patch (conv_tr.hip fused input; no bn_act_fwd launch); =0 restores the
 # separate pass
@@ -246,6 +260,17 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=Non
     g = spec.geom(N, H, W, weight_krsc(dweight))
     s = stream_handle()
     ws = workspace(x.device)
+    if (need_dx and link is None and bna is None and bnf is None and spec.wt is not None
+            and not _common.BWD_SIDE_STREAM
+            and native().conv_tr_would_serve(g, ws.numel(), -1)):
+        # tap-reuse backward-data (conv_tr.hip) + the weight gradient as its own launch
+        native().conv_wgrad(g, ptr(dz), ptr(x), ptr(dweight), ptr(ws), ws.numel(), 0, s)
+        if weight is not None:
+            grad_ready([weight])
+        dx = torch.empty_like(x)
+        if not native().conv_dgrad_tr(g, ptr(dz), ptr(spec.wt), ptr(dx), ptr(ws), ws.numel(), s):
+            raise RuntimeError("tap-reuse dgrad refused a shape it reported as served")
+        return dx
     if (need_dx and link is None and not _common.BWD_SIDE_STREAM and spec.stride == 1
             and spec.C == spec.Cr):
         # wgrad + dgrad of this layer as one grouped launch (+ one finish launch) when the
