@@ -169,13 +169,20 @@ def main():
                                         default_cuts(args.model, B) if world > 1 else "0")
     cuts = [int(v) for v in str(args.segmented).split(",") if int(v) > 0]
     segmented = bool(cuts) and args.strategy == "ddp" and not args.no_graph
+    # all-reduce bandwidth of THIS node, measured on the live communicator before the bucket
+    # plan is made (DDP_AMD_COMM_PROBE=0 falls back to comm_tuning.json)
+    comm_table = None
+    if world > 1 and os.environ.get("DDP_AMD_COMM_PROBE", "1") != "0":
+        from ddp_amd.parallel.bucket_plan import probe_table
+        comm_table = probe_table(comm, world, args.grad_comm, device=device)
+        beat()
     if args.strategy == "ddp":
         # captured step (``captured``): the reducer's collectives are inline in the graph (or
         # bypassed by the pipelined step) -> 'auto' plans one bucket = one collective
         model = DistributedDataParallel(model, comm, bucket_cap_mb=args.bucket_mb,
                                         first_bucket_cap_mb=args.first_bucket_mb,
                                         grad_comm_dtype=args.grad_comm,
-                                        captured=not args.no_graph)
+                                        captured=not args.no_graph, comm_table=comm_table)
     else:
         fn = STRATEGIES[args.strategy]
         sync = lambda m: fn(m, comm)  # noqa: E731
@@ -255,7 +262,7 @@ def main():
     consistent = True
     if world > 1:
         consistent = check_replicas(arena, world)
-    plan = comm_plan(args, world, step, model, cuts, segmented)
+    plan = comm_plan(args, world, step, model, cuts, segmented, comm_table)
     ms = elapsed / args.steps * 1000.0
     value = global_batch * args.steps / elapsed
     out = {
@@ -321,16 +328,20 @@ def _version_str(v):
     return f"{v // 10000}.{v // 100 % 100}.{v % 100}" if v else None
 
 
-def comm_plan(args, world, step, model, cuts, segmented):
+def comm_plan(args, world, step, model, cuts, segmented, comm_table=None):
     """Which gradient-communication plan this run used: collective granularity, bucket bytes
-    on the wire, wire dtype, and the all-reduce bandwidth table (parallel/comm_tuning.json,
-    "model" until tools/comm_bench.py --write-table measured a node) with its knee."""
-    from ddp_amd.parallel.bucket_plan import knee_bytes, load_table, rows_for
+    on the wire, wire dtype, and the all-reduce bandwidth table with its knee: measured on this
+    node's communicator at start-up (world > 1), else parallel/comm_tuning.json ("model" until
+    tools/comm_bench.py --write-table measured a node). With measured rows, the predicted
+    all-reduce time of every bucket is reported too."""
+    from ddp_amd.parallel.bucket_plan import knee_bytes, load_table, predict_us, rows_for
     wire = 2 if args.grad_comm == "bf16" else 4
-    rows, source = rows_for(load_table(), max(world, 2), args.grad_comm)
+    rows, source = rows_for(comm_table or load_table(), max(world, 2), args.grad_comm)
     out = {"wire": args.grad_comm, "comm_table": source,
            "comm_table_knee_bytes": knee_bytes(rows) if rows else None,
            "collectives_live": world > 1}
+    if comm_table is not None:
+        out["probe_busbw_GBps"] = {str(r["bytes"]): r["busbw_GBps"] for r in rows}
     if segmented:
         out.update(kind="pipelined segments (bucket all-reduce + its SGD under the earlier "
                         "layers' backward)", cuts=cuts,
@@ -345,6 +356,8 @@ def comm_plan(args, world, step, model, cuts, segmented):
         n = sum(1 for _ in model.parameters())
         out.update(kind=f"per-parameter {args.strategy} ({n} collectives)", cuts=[],
                    bucket_bytes=None)
+    if comm_table is not None and out.get("bucket_bytes"):
+        out["predicted_allreduce_us"] = [round(predict_us(rows, b), 1) for b in out["bucket_bytes"]]
     return out
 
 

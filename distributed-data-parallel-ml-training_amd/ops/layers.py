@@ -219,6 +219,10 @@ DGRAD_TR = int(os.environ.get("DDP_AMD_DGRAD_TR", "0"))
 # consumer GEMM has at most this many rows)
 FUSE_BN_IN = int(os.environ.get("DDP_AMD_FUSE_BN_IN", "2"))
 FUSE_BN_IN_MAX_ROWS = int(os.environ.get("DDP_AMD_FUSE_BN_IN_MAX_ROWS", str(1 << 30)))
+# mode 2 still fuses pooled blocks up to this many images per GPU: at 32 (the 8-GPU share) the
+# launch it removes outweighs the 4x patch bytes (b32 0.4132 vs 0.4178 ms; at 64 it loses,
+# 0.4933 vs 0.4870; profiles/r3_fused_bn_input.md)
+FUSE_BN_IN_POOL_MAX_BATCH = int(os.environ.get("DDP_AMD_FUSE_BN_IN_POOL_MAX_BATCH", "32"))
 # BatchNorm forward fused into the split-K finish of small conv GEMMs (conv_igemm.hip
 # splitk_finish_bnfwd_kernel; the native side also honours DDP_AMD_BN_FWD_FUSE=0)
 BN_FWD_FUSE = os.environ.get("DDP_AMD_BN_FWD_FUSE", "1") != "0"
@@ -320,7 +324,8 @@ def _defer_bn(spec, residual, running_mean, N, Ho, Wo):
             or running_mean is not None or nxt.C != spec.K or nxt.Cr != nxt.C
             or nxt.R != 3 or nxt.stride != 1 or nxt.pad != 1):
         return False
-    if (FUSE_BN_IN == 2 and spec.pool) or N * Ho * Wo > FUSE_BN_IN_MAX_ROWS:
+    if ((FUSE_BN_IN == 2 and spec.pool and N > FUSE_BN_IN_POOL_MAX_BATCH)
+            or N * Ho * Wo > FUSE_BN_IN_MAX_ROWS):
         return False
     if spec.pool and (Ho * 2 != spec._out_p or Wo * 2 != spec._out_q):
         return False

@@ -109,6 +109,32 @@ def model_rows(world, latency_us=12.0, link_GBps=153.0, links_used=1, sizes=None
     return rows
 
 
+def probe_table(comm, world, dtype="fp32", device="cuda", sizes=None, iters=10, warmup=3):
+    """Measure the all-reduce bus-bandwidth curve on the live communicator (every rank takes
+    part; per-size time = the max over ranks, so all ranks build the same table) and return it
+    in the comm_tuning.json layout with source "measured at start-up". ~50 ms on a node."""
+    import torch
+    from .commbench import allreduce_sweep
+    sizes = sizes or [1 << k for k in range(18, 27, 2)]  # 256 KiB .. 64 MiB
+    dt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    rows = allreduce_sweep(comm, sizes, dtype=dt, device=device, iters=iters, warmup=warmup)
+    if not all(r.get("correct", True) for r in rows):
+        raise RuntimeError("start-up all-reduce probe returned wrong sums")
+    rows = [{k: r[k] for k in ("bytes", "us", "algbw_GBps", "busbw_GBps")} for r in rows]
+    return {"worlds": {str(world): {"source": "measured at start-up", dtype: rows}}}
+
+
+def predict_us(rows, nbytes):
+    """All-reduce time of ``nbytes`` from bus-bandwidth rows (ring: bus = alg x 2(n-1)/n is
+    folded into the rows' own us where a row matches; interpolated otherwise)."""
+    for r in rows:
+        if r["bytes"] == nbytes:
+            return r["us"]
+    ref = rows[-1]
+    scale = ref["busbw_GBps"] / max(ref["algbw_GBps"], 1e-12)  # 2(n-1)/n
+    return nbytes * scale / (busbw_at(rows, nbytes) * 1e3)
+
+
 def merge_rows(path, world, dtype, rows, source="measured"):
     """Write measured comm_bench rows for (world, dtype) into the table at ``path``."""
     table = load_table(path) if os.path.exists(path) else {}

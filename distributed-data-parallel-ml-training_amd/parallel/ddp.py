@@ -213,7 +213,7 @@ class _PyReducer:
 class DistributedDataParallel(nn.Module):
     def __init__(self, module, comm, bucket_cap_mb=25.0, first_bucket_cap_mb=1.0,
                  broadcast_buffers=True, average=True, overlap=None, grad_comm_dtype="fp32",
-                 captured=False):
+                 captured=False, comm_table=None):
         super().__init__()
         self.module = module
         self.comm = comm
@@ -229,10 +229,12 @@ class DistributedDataParallel(nn.Module):
             from .bucket_plan import choose_bucket_caps
             wire = 2 if grad_comm_dtype == "bf16" else 4
             # ``captured``: the step will be captured into one hipGraph, whose bucket
-            # collectives are issued inline (no overlap to buy): one bucket
+            # collectives are issued inline (no overlap to buy): one bucket. ``comm_table``: a
+            # table measured by the caller on this very communicator (bench.py start-up probe)
+            # instead of comm_tuning.json
             cap_b, first_b, self.bucket_plan_reason = choose_bucket_caps(
                 comm.world, self.arena.total * wire, overlap=not captured,
-                dtype="bf16" if grad_comm_dtype == "bf16" else "fp32")
+                dtype="bf16" if grad_comm_dtype == "bf16" else "fp32", table=comm_table)
             # the planner counts fp32 arena bytes
             cap, cap_first = cap_b * 4 // wire, first_b * 4 // wire
         else:

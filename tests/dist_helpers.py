@@ -200,6 +200,29 @@ def commbench_worker(rank, world, port, q):
         q.put((rank, {"error": traceback.format_exc() + repr(e)}))
 
 
+def probe_worker(rank, world, port, q):
+    """bench.py's start-up probe (bucket_plan.probe_table) on Gloo, then DDP 'auto' bucket caps
+    planned from that table (overlapped reducer)."""
+    try:
+        _init(rank, world, port)
+        from ddp_amd.models import VGG11
+        from ddp_amd.parallel import TorchCommunicator, DistributedDataParallel
+        from ddp_amd.parallel import bucket_plan as bp
+        comm = TorchCommunicator()
+        t = bp.probe_table(comm, world, "fp32", device="cpu", sizes=[1 << 14, 1 << 16, 1 << 18],
+                           iters=2, warmup=1)
+        torch.manual_seed(0)
+        m = DistributedDataParallel(VGG11(), comm, bucket_cap_mb="auto", first_bucket_cap_mb="auto",
+                                    comm_table=t)
+        rows, src = bp.rows_for(t, world)
+        q.put((rank, {"table": t, "reason": m.bucket_plan_reason, "src": src,
+                      "pred": bp.predict_us(rows, 1 << 16), "pred_mid": bp.predict_us(rows, 1 << 17),
+                      "nb": len(m.buckets)}))
+    except Exception as e:  # pragma: no cover - surfaced by the parent
+        import traceback
+        q.put((rank, {"error": traceback.format_exc() + repr(e)}))
+
+
 class _Swapped(torch.nn.Module):
     """Parameters registered in the opposite order of their use: ``late`` is defined first but
     applied last, so its gradient is ready FIRST in backward while the reverse-parameter-order

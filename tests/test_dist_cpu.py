@@ -118,3 +118,20 @@ def test_allreduce_bandwidth_sweep():
         for row in v["rows"]:
             assert row["correct"] and row["us"] > 0 and row["busbw_GBps"] > 0
     assert out[0]["rows"] == out[1]["rows"]
+
+
+def test_startup_probe_table_plans_buckets():
+    """bench.py --gpus N>1 measures the all-reduce curve on its own communicator before planning
+    buckets (bucket_plan.probe_table): every rank gets the SAME table (max over ranks), marked
+    "measured at start-up", and DDP's 'auto' caps are planned from it."""
+    from dist_helpers import probe_worker
+    out = run_workers(probe_worker, WORLD)
+    for r, v in out.items():
+        assert "error" not in v, v.get("error")
+        assert v["src"].startswith("measured at start-up table (world 2")
+        assert "measured at start-up" in v["reason"]
+        rows = v["table"]["worlds"]["2"]["fp32"]
+        assert [row["bytes"] for row in rows] == [1 << 14, 1 << 16, 1 << 18]
+        assert v["pred"] == rows[1]["us"] and v["pred_mid"] > 0
+        assert v["nb"] >= 1
+    assert out[0]["table"] == out[1]["table"]
