@@ -328,6 +328,10 @@ PYBIND11_MODULE(_native, m) {
      py::arg("beta"), py::arg("dout"), py::arg("sums"), py::arg("dz"), py::arg("dres"),
      py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("stream"), py::arg("coef"),
      py::arg("counter") = 0, py::arg("sums_ready") = 0);
+  m.def("bn_bwd_local_ok", [](int N, int H, int W, int C, int pool) {
+    return ddp_bn_bwd_local_ok(N, H, W, C, pool) != 0;
+  });
+  m.def("bn_bwd_local_set", [](long long max_loads) { ddp_bn_bwd_local_set(max_loads); });
 
   m.def("linear_ce_fwd", [](uintptr_t x, uintptr_t W, uintptr_t b, uintptr_t labels, int B, int F,
                             int J, uintptr_t logits, uintptr_t dlogits, uintptr_t loss_sum,

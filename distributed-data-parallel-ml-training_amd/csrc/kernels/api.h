@@ -174,6 +174,11 @@ int ddp_conv_wgrad(const ddp_amd::ConvGeom* g, const void* dy, const void* x, fl
                    float* ws, size_t ws_elems, int splits, hipStream_t st);
 int ddp_bn_act_fwd(const ddp_amd::BnArgs* a, hipStream_t st);
 int ddp_bn_act_bwd(const ddp_amd::BnArgs* a, hipStream_t st);
+// small layers: the whole BatchNorm backward in one launch, one block per 8 channels
+// (bn_act_bwd_local_kernel); ok = this layer takes that path; set = its loads-per-thread
+// limit (0 = off)
+int ddp_bn_bwd_local_ok(int N, int H, int W, int C, int pool);
+void ddp_bn_bwd_local_set(long long max_loads);
 int ddp_linear_ce_fwd(const void* x, const float* W, const float* b, const long long* labels,
                       int B, int F, int J, float* logits, float* dlogits, float* loss_sum,
                       int* correct, float* loss_acc, hipStream_t st);

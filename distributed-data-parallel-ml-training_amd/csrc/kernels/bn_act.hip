@@ -435,6 +435,92 @@ __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(BnArgs a) {
   }
 }
 
+// ------------------------------- backward, one block per channel group -------------------------------
+// Small layers (the strong-scaling batches): ONE block owns 8 channels over EVERY (post-pool)
+// pixel. Its threads keep their items (dy, z [, res]) in registers, the block reduces S1 / S2
+// itself (wave shuffles + LDS: no atomics, no replicas), writes dgamma / dbeta / k1 / k2, and
+// applies from the same registers: the whole BatchNorm backward is ONE launch instead of three
+// dependent ones (reduce, finalize, apply ~ 4.5 us each in the captured b32 step), and dy / z are
+// read once instead of twice.
+template <bool POOL, int IPT, int NT>
+__global__ __launch_bounds__(NT) void bn_act_bwd_local_kernel(BnArgs a) {
+  constexpr int NP = POOL ? 4 : 1;
+  constexpr int NW = NT / kWave;
+  __shared__ float red[NW][16];
+  __shared__ float fin[16];
+  const int cg = blockIdx.x;
+  const int c0 = cg * 8;
+  const int Ho = POOL ? a.H / 2 : a.H, Wo = POOL ? a.W / 2 : a.W;
+  const size_t npix = (size_t)a.N * Ho * Wo;
+  BwdItems<POOL, IPT> L;
+  bwd_load<POOL, IPT>(a, L, threadIdx.x, NT, npix, cg, Ho, Wo);
+  float sc[8], sh[8], mu[8], is[8];
+  ld8f(a.coef + kSc * a.C + c0, sc);
+  ld8f(a.coef + kSh * a.C + c0, sh);
+  ld8f(a.coef + kMu * a.C + c0, mu);
+  ld8f(a.coef + kIs * a.C + c0, is);
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+#pragma unroll
+  for (int it = 0; it < IPT; ++it) {
+    if (!L.ok[it]) continue;
+    float xh[NP][8], dyb[NP][8];
+    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], sc, sh, mu, is, xh, dyb);
+#pragma unroll
+    for (int d = 0; d < NP; ++d)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s1[e] += dyb[d][e];
+        s2[e] += dyb[d][e] * xh[d][e];
+      }
+  }
+  const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float t1 = wave_sum(s1[e]), t2 = wave_sum(s2[e]);
+    if (lane == 0) { red[wave][e] = t1; red[wave][8 + e] = t2; }
+  }
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) t += red[w][threadIdx.x];
+    fin[threadIdx.x] = t;
+    const int e = threadIdx.x & 7;
+    const float inv_m = 1.f / ((float)a.N * a.H * a.W);
+    if (threadIdx.x < 8) {
+      a.coef[kK1 * a.C + c0 + e] = t * inv_m;
+      if (a.dbeta) a.dbeta[c0 + e] += t;  // one block per channel: plain accumulate
+    } else {
+      a.coef[kK2 * a.C + c0 + e] = t * inv_m;
+      if (a.dgamma) a.dgamma[c0 + e] += t;
+    }
+  }
+  __syncthreads();
+  const float inv_m = 1.f / ((float)a.N * a.H * a.W);
+  float k1[8], k2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { k1[e] = fin[e] * inv_m; k2[e] = fin[8 + e] * inv_m; }
+#pragma unroll
+  for (int it = 0; it < IPT; ++it) {
+    if (!L.ok[it]) continue;
+    float xh[NP][8], dyb[NP][8];
+    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], sc, sh, mu, is, xh, dyb);
+#pragma unroll
+    for (int d = 0; d < NP; ++d) {
+      u16x8 o, r;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        o[e] = f2bf(sc[e] * (dyb[d][e] - k1[e] - xh[d][e] * k2[e]));
+        r[e] = f2bf(dyb[d][e]);
+      }
+      st8(a.dz + L.off[it][d], o);
+      if (a.dres) st8(a.dres + L.off[it][d], r);
+    }
+  }
+}
+
 }  // namespace ddp_amd
 
 using namespace ddp_amd;
@@ -504,6 +590,59 @@ static void launch_bwd(const BnArgs& a, size_t npix, int Gb, int chunks, hipStre
   }
 }
 
+// One-block-per-channel-group backward (bn_act_bwd_local_kernel): items per thread for npix
+// (post-pool) pixels; false when the layer is too big for it. A block streams its 8-channel
+// column alone — every 16-byte load is its own cache line — so its time grows with the loads
+// per thread (measured, b64 step: 2 loads 5.1 us, 5 loads 9.6, 8 loads 9.5, 16-20 loads 22 us,
+// against 12-19 us for reduce + finalize + apply): served while ipt x (dy + z [+ res] vectors)
+// <= kLocalMaxLoads (DDP_AMD_BN_BWD_LOCAL_LOADS; 0 = never). Step A/B of the limit (0/5/8/10):
+// 8 is best at b32..b128 (b32 0.416 -> 0.405 ms, b64 -1.2 %, b128 -0.9 %), neutral at b256.
+static int kLocalMaxLoads = 8;
+constexpr int kLocalThreads = 256;
+static bool local_cfg(const BnArgs& a, int* ipt) {
+  static const bool init = [] {
+    if (const char* e = std::getenv("DDP_AMD_BN_BWD_LOCAL_LOADS")) kLocalMaxLoads = std::max(0, std::atoi(e));
+    return true;
+  }();
+  (void)init;
+  if (a.C % 8 || (a.pool && a.res)) return false;
+  const int Ho = a.pool ? a.H / 2 : a.H, Wo = a.pool ? a.W / 2 : a.W;
+  const size_t npix = (size_t)a.N * Ho * Wo;
+  const int per_item = 1 + (a.pool ? 4 : 1) + (a.res ? 1 : 0);
+  for (int i = 1; i <= 8; i *= 2) {
+    if ((size_t)kLocalThreads * i < npix) continue;
+    if (a.pool && i > 4) return false;  // register budget: 4 pre-pool vectors per item
+    if (i * per_item > kLocalMaxLoads) return false;
+    *ipt = i;
+    return true;
+  }
+  return false;
+}
+
+template <bool POOL>
+static void launch_local(const BnArgs& a, int ipt, hipStream_t st) {
+  const dim3 grid(a.C / 8), block(kLocalThreads);
+  if (ipt == 1) hipLaunchKernelGGL((bn_act_bwd_local_kernel<POOL, 1, kLocalThreads>), grid, block, 0, st, a);
+  else if (ipt == 2) hipLaunchKernelGGL((bn_act_bwd_local_kernel<POOL, 2, kLocalThreads>), grid, block, 0, st, a);
+  else if (ipt == 4) hipLaunchKernelGGL((bn_act_bwd_local_kernel<POOL, 4, kLocalThreads>), grid, block, 0, st, a);
+  else if constexpr (!POOL) hipLaunchKernelGGL((bn_act_bwd_local_kernel<POOL, 8, kLocalThreads>), grid, block, 0, st, a);
+}
+
+// tests / sweeps: the loads-per-thread limit of the one-launch backward (0 = off)
+extern "C" void ddp_bn_bwd_local_set(long long max_loads) {
+  BnArgs a{};
+  int ipt;
+  (void)local_cfg(a, &ipt);  // run the env init first so it cannot override this later
+  kLocalMaxLoads = (int)std::max(0LL, max_loads);
+}
+
+extern "C" int ddp_bn_bwd_local_ok(int N, int H, int W, int C, int pool) {
+  BnArgs a{};
+  a.N = N; a.H = H; a.W = W; a.C = C; a.pool = pool;
+  int ipt;
+  return local_cfg(a, &ipt) ? 1 : 0;
+}
+
 // a.coef must hold the table written by the matching forward; a.sums ([kStatRep][2][C]) must be
 // zero on entry (per-step scratch, zeroed once per forward).
 extern "C" int ddp_bn_act_bwd(const BnArgs* args, hipStream_t st) {
@@ -516,6 +655,16 @@ extern "C" int ddp_bn_act_bwd(const BnArgs* args, hipStream_t st) {
   BnArgs a = *args;
   if (a.C % 8 || a.coef == nullptr || a.sums == nullptr) return -1;
   if (a.pool && a.res) return -1;
+  {
+    // small layer: the whole backward in one launch (any sums the next layer's dgrad
+    // accumulated are simply not needed)
+    int ipt;
+    if (local_cfg(a, &ipt)) {
+      if (a.pool) launch_local<true>(a, ipt, st);
+      else launch_local<false>(a, ipt, st);
+      return (int)hipGetLastError();
+    }
+  }
   const int G = a.C / 8;
   const int Gb = G < 256 ? G : 256;
   if ((Gb < 256 && 256 % Gb) || (G > 256 && G % 256)) return -1;  // channel groups must tile 256 threads

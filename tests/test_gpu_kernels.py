@@ -173,16 +173,30 @@ def _bn_ref(z, gamma, beta, eps, relu, pool, res=None):
     return y
 
 
-@pytest.mark.parametrize("C,H,pool,res", [(64, 8, True, False), (128, 4, False, False),
-                                          (512, 2, True, False), (256, 8, False, True),
-                                          (2048, 2, False, True)])
-@pytest.mark.parametrize("last_block", [False, True])
-def test_bn_act_fwd_bwd(native_ext, C, H, pool, res, last_block):
-    """last_block: the reduce kernel's final block finalizes k1/k2/dgamma/dbeta (ticket counter,
-    agent release/acquire) instead of a separate finalize launch."""
+@pytest.mark.parametrize("N,C,H,pool,res", [(8, 64, 8, True, False), (8, 128, 4, False, False),
+                                            (8, 512, 2, True, False), (8, 256, 8, False, True),
+                                            (8, 2048, 2, False, True), (16, 128, 16, True, False),
+                                            (32, 256, 8, False, False), (16, 256, 8, False, True),
+                                            (32, 64, 8, True, False)])
+@pytest.mark.parametrize("mode", ["split", "last_block", "local"])
+def test_bn_act_fwd_bwd(native_ext, N, C, H, pool, res, mode):
+    """split: reduce -> finalize -> apply launches; last_block: the reduce kernel's final block
+    finalizes k1/k2/dgamma/dbeta (ticket counter) instead of a separate finalize launch; local:
+    one block per 8 channels does the whole backward in one launch (bn_act_bwd_local_kernel;
+    the shapes cover 1-8 items per thread, pooled, plain and residual)."""
     from ddp_amd.ops.common import ptr, stream_handle
     nat = native_ext
-    N = 8
+    last_block = mode == "last_block"
+    nat.bn_bwd_local_set(64 if mode == "local" else 0)  # local: any shape it can hold
+    try:
+        _bn_case(nat, N, C, H, pool, res, last_block, ptr, stream_handle)
+        if mode == "local":
+            assert nat.bn_bwd_local_ok(N, H, H, C, int(pool))
+    finally:
+        nat.bn_bwd_local_set(8)  # the shipped limit (bn_act.hip kLocalMaxLoads)
+
+
+def _bn_case(nat, N, C, H, pool, res, last_block, ptr, stream_handle):
     z = bf(torch.randn(N, C, H, H, device=DEV) * 2 + 0.5)
     r = bf(torch.randn(N, C, H, H, device=DEV)) if res else None
     gamma = torch.rand(C, device=DEV) + 0.5
