@@ -312,11 +312,12 @@ PYBIND11_MODULE(_native, m) {
                          uintptr_t res, uintptr_t stats, uintptr_t gamma, uintptr_t beta,
                          uintptr_t dout, uintptr_t sums, uintptr_t dz, uintptr_t dres,
                          uintptr_t dgamma, uintptr_t dbeta, uintptr_t dbias, uintptr_t st,
-                         uintptr_t coef, uintptr_t counter, int sums_ready) {
+                         uintptr_t coef, uintptr_t counter, int sums_ready, uintptr_t grid_sync) {
     ddp_amd::BnArgs a{};
     a.coef = P<float>(coef);
     a.counter = P<int>(counter);
     a.sums_ready = sums_ready;
+    a.grid_sync = P<int>(grid_sync);
     a.N = N; a.H = H; a.W = W; a.C = C; a.pool = pool; a.relu = relu; a.eps = eps;
     a.z = P<unsigned short>(z); a.res = P<unsigned short>(res); a.stats = P<float>(stats);
     a.gamma = P<float>(gamma); a.beta = P<float>(beta); a.dout = P<unsigned short>(dout);
@@ -327,7 +328,8 @@ PYBIND11_MODULE(_native, m) {
      py::arg("eps"), py::arg("z"), py::arg("res"), py::arg("stats"), py::arg("gamma"),
      py::arg("beta"), py::arg("dout"), py::arg("sums"), py::arg("dz"), py::arg("dres"),
      py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("stream"), py::arg("coef"),
-     py::arg("counter") = 0, py::arg("sums_ready") = 0);
+     py::arg("counter") = 0, py::arg("sums_ready") = 0, py::arg("grid_sync") = 0);
+  m.def("bn_bwd_cluster_set", [](int mode) { ddp_bn_bwd_cluster_set(mode); });
   m.def("bn_bwd_local_ok", [](int N, int H, int W, int C, int pool) {
     return ddp_bn_bwd_local_ok(N, H, W, C, pool) != 0;
   });

@@ -48,6 +48,8 @@ struct BnArgs {
                                 // block finalizes k1/k2, dgamma, dbeta (no finalize launch)
   int sums_ready;               // backward: sums already accumulated (BnBwdFuse in the next
                                 // layer's dgrad) -> finalize + apply only
+  int* grid_sync;               // backward: zeroed arrival counter of the one-launch clustered
+                                // backward (bn_act_bwd_cluster_kernel); null = not available
 };
 
 // BatchNorm-backward statistics fused into a conv dgrad: the dgrad output IS the gradient at the
@@ -179,6 +181,9 @@ int ddp_bn_act_bwd(const ddp_amd::BnArgs* a, hipStream_t st);
 // limit (0 = off)
 int ddp_bn_bwd_local_ok(int N, int H, int W, int C, int pool);
 void ddp_bn_bwd_local_set(long long max_loads);
+// mid-size layers: the same in one launch over up to kStatRep blocks per 64 channels that meet at
+// a bounded grid-wide counter (bn_act_bwd_cluster_kernel; needs BnArgs::grid_sync); 0 = off
+void ddp_bn_bwd_cluster_set(int mode);
 int ddp_linear_ce_fwd(const void* x, const float* W, const float* b, const long long* labels,
                       int B, int F, int J, float* logits, float* dlogits, float* loss_sum,
                       int* correct, float* loss_acc, hipStream_t st);

@@ -521,6 +521,119 @@ __global__ __launch_bounds__(NT) void bn_act_bwd_local_kernel(BnArgs a) {
   }
 }
 
+// ------------------------------- backward, clustered -------------------------------
+// Mid-size layers: the one-launch backward spread over K <= kStatRep blocks per 64-channel chunk
+// (block = 32 pixel rows x 8 channel groups: every 128-byte line is read whole). Each block
+// reduces its slice's S1 / S2, stores them (agent-scope stores: written past the XCD L2s) into
+// slot [slice][2][C] of the zeroed sums scratch, drains them (vmcnt), arrives on the grid
+// counter, waits until every block of the launch has arrived (the grid is at most a few hundred
+// blocks: all co-resident), sums the K slots of its chunk and applies from the items it still
+// holds in registers. One launch, dy / z read once, no float atomics. The wait is bounded: on
+// timeout the block poisons k1 (NaN -> the loss turns NaN) instead of hanging the GPU.
+constexpr int kClusterRows = 32;  // pixel rows per pass (256 threads = 32 x 8 groups)
+template <bool POOL, int IPT>
+__global__ __launch_bounds__(256) void bn_act_bwd_cluster_kernel(BnArgs a, int K, int P) {
+  constexpr int NP = POOL ? 4 : 1;
+  __shared__ float red[2][8][8 * kClusterRows];  // [s1|s2][e][thread]
+  __shared__ float fin[128];
+  __shared__ int timed_out;
+  const int chunk = blockIdx.x / K, slice = blockIdx.x % K;
+  const int tid = threadIdx.x, cgl = tid % 8, prow = tid / 8;
+  const int cg = chunk * 8 + cgl, c0 = cg * 8;
+  const int Ho = POOL ? a.H / 2 : a.H, Wo = POOL ? a.W / 2 : a.W;
+  const size_t npix = (size_t)a.N * Ho * Wo;
+  const size_t lo = (size_t)slice * P;
+  const size_t hi = lo + P < npix ? lo + P : npix;
+  BwdItems<POOL, IPT> L;
+  bwd_load<POOL, IPT>(a, L, lo + prow, kClusterRows, hi, cg, Ho, Wo);
+  float sc[8], sh[8], mu[8], is[8];
+  ld8f(a.coef + kSc * a.C + c0, sc);
+  ld8f(a.coef + kSh * a.C + c0, sh);
+  ld8f(a.coef + kMu * a.C + c0, mu);
+  ld8f(a.coef + kIs * a.C + c0, is);
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+#pragma unroll
+  for (int it = 0; it < IPT; ++it) {
+    if (!L.ok[it]) continue;
+    float xh[NP][8], dyb[NP][8];
+    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], sc, sh, mu, is, xh, dyb);
+#pragma unroll
+    for (int d = 0; d < NP; ++d)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s1[e] += dyb[d][e];
+        s2[e] += dyb[d][e] * xh[d][e];
+      }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[0][e][tid] = s1[e]; red[1][e][tid] = s2[e]; }
+  if (tid == 0) timed_out = 0;
+  __syncthreads();
+  // 128 partials of this block (2 sums x 64 channels): thread t < 128 adds its column
+  float* slot = a.sums + (size_t)slice * 2 * a.C;
+  if (tid < 128) {
+    const int k = tid / 64, ch = tid % 64, g = ch / 8, e = ch % 8;
+    float t = 0.f;
+    for (int r = 0; r < kClusterRows; ++r) t += red[k][e][r * 8 + g];
+    __hip_atomic_store(slot + k * a.C + chunk * 64 + ch, t, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const int nblk = gridDim.x;
+    __hip_atomic_fetch_add(a.grid_sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int spins = 0;
+    while (__hip_atomic_load(a.grid_sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nblk) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1 << 22)) { timed_out = 1; break; }
+    }
+  }
+  __syncthreads();
+  if (tid < 128) {
+    const int k = tid / 64, ch = tid % 64;
+    float t = 0.f;
+    for (int r = 0; r < K; ++r)
+      t += __hip_atomic_load(a.sums + (size_t)r * 2 * a.C + k * a.C + chunk * 64 + ch,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    fin[tid] = timed_out ? __builtin_nanf("") : t;
+    if (slice == 0) {
+      const float inv_m = 1.f / ((float)a.N * a.H * a.W);
+      const int c = chunk * 64 + ch;
+      a.coef[(k ? kK2 : kK1) * a.C + c] = fin[tid] * inv_m;
+      float* dst = k ? a.dgamma : a.dbeta;
+      if (dst) dst[c] += fin[tid];
+    }
+  }
+  __syncthreads();
+  const float inv_m = 1.f / ((float)a.N * a.H * a.W);
+  float k1[8], k2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    k1[e] = fin[cgl * 8 + e] * inv_m;
+    k2[e] = fin[64 + cgl * 8 + e] * inv_m;
+  }
+#pragma unroll
+  for (int it = 0; it < IPT; ++it) {
+    if (!L.ok[it]) continue;
+    float xh[NP][8], dyb[NP][8];
+    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], sc, sh, mu, is, xh, dyb);
+#pragma unroll
+    for (int d = 0; d < NP; ++d) {
+      u16x8 o, r;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        o[e] = f2bf(sc[e] * (dyb[d][e] - k1[e] - xh[d][e] * k2[e]));
+        r[e] = f2bf(dyb[d][e]);
+      }
+      st8(a.dz + L.off[it][d], o);
+      if (a.dres) st8(a.dres + L.off[it][d], r);
+    }
+  }
+}
+
 }  // namespace ddp_amd
 
 using namespace ddp_amd;
@@ -643,6 +756,50 @@ extern "C" int ddp_bn_bwd_local_ok(int N, int H, int W, int C, int pool) {
   return local_cfg(a, &ipt) ? 1 : 0;
 }
 
+// Clustered one-launch backward (bn_act_bwd_cluster_kernel) for layers too big for the local
+// kernel: K = ceil(npix / (32 x ipt)) <= kStatRep slices per 64-channel chunk, ipt <= 4 items
+// per thread; needs the arrival counter. OFF by default (DDP_AMD_BN_BWD_CLUSTER=1 enables):
+// measured slower than the three-launch chain it replaces — 12-23 us per layer against 10-15
+// (b32 step 0.404 -> 0.424 ms, b256 +1.2 %; profiles/r3_bn_bwd_one_launch.md): the arrival
+// counter and the agent-scope slot traffic cost more than the two launch boundaries.
+static int kClusterMode = 0;
+static bool cluster_cfg(const BnArgs& a, int* ipt, int* K, int* P) {
+  static const bool init = [] {
+    if (const char* e = std::getenv("DDP_AMD_BN_BWD_CLUSTER")) kClusterMode = std::atoi(e);
+    return true;
+  }();
+  (void)init;
+  if (!kClusterMode || !a.grid_sync || a.C % 64 || (a.pool && a.res)) return false;
+  const int Ho = a.pool ? a.H / 2 : a.H, Wo = a.pool ? a.W / 2 : a.W;
+  const size_t npix = (size_t)a.N * Ho * Wo;
+  for (int i = 1; i <= 4; i *= 2) {
+    const size_t per = (size_t)kClusterRows * i;
+    const size_t k = (npix + per - 1) / per;
+    if (k <= (size_t)kStatRep) {
+      *ipt = i;
+      *K = (int)k;
+      *P = (int)per;
+      return (size_t)(a.C / 64) * k <= 512;  // co-resident with room to spare
+    }
+  }
+  return false;
+}
+
+extern "C" void ddp_bn_bwd_cluster_set(int mode) {
+  BnArgs a{};
+  int i, k, p;
+  (void)cluster_cfg(a, &i, &k, &p);
+  kClusterMode = mode;
+}
+
+template <bool POOL>
+static void launch_cluster(const BnArgs& a, int ipt, int K, int P, hipStream_t st) {
+  const dim3 grid((a.C / 64) * K), block(256);
+  if (ipt == 1) hipLaunchKernelGGL((bn_act_bwd_cluster_kernel<POOL, 1>), grid, block, 0, st, a, K, P);
+  else if (ipt == 2) hipLaunchKernelGGL((bn_act_bwd_cluster_kernel<POOL, 2>), grid, block, 0, st, a, K, P);
+  else hipLaunchKernelGGL((bn_act_bwd_cluster_kernel<POOL, 4>), grid, block, 0, st, a, K, P);
+}
+
 // a.coef must hold the table written by the matching forward; a.sums ([kStatRep][2][C]) must be
 // zero on entry (per-step scratch, zeroed once per forward).
 extern "C" int ddp_bn_act_bwd(const BnArgs* args, hipStream_t st) {
@@ -662,6 +819,12 @@ extern "C" int ddp_bn_act_bwd(const BnArgs* args, hipStream_t st) {
     if (local_cfg(a, &ipt)) {
       if (a.pool) launch_local<true>(a, ipt, st);
       else launch_local<false>(a, ipt, st);
+      return (int)hipGetLastError();
+    }
+    int K, P;
+    if (cluster_cfg(a, &ipt, &K, &P)) {  // the sums scratch is overwritten (slots, not sums)
+      if (a.pool) launch_cluster<true>(a, ipt, K, P, st);
+      else launch_cluster<false>(a, ipt, K, P, st);
       return (int)hipGetLastError();
     }
   }

@@ -420,7 +420,10 @@ class _ConvBNActFn(torch.autograd.Function):
                                 ptr(sums), ptr(dz), ptr(dres), ptr(gg), ptr(gbt), ptr(gb),
                                 stream_handle(), ptr(spec.coef),
                                 ptr(spec.bwd_counter) if _common.BN_LAST_BLOCK else 0,
-                                sums_ready=int(sums_ready))
+                                sums_ready=int(sums_ready),
+                                # arrival counter of the clustered one-launch backward (zeroed
+                                # with the statistics every forward; bn_act.hip)
+                                grid_sync=0 if _common.BN_LAST_BLOCK else ptr(spec.bwd_counter))
         grad_ready([gamma, beta, bias])
         if ctx.res_link is not None and dres is not None:
             dres = ctx.res_link.offer(dres)

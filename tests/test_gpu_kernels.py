@@ -178,25 +178,32 @@ def _bn_ref(z, gamma, beta, eps, relu, pool, res=None):
                                             (8, 2048, 2, False, True), (16, 128, 16, True, False),
                                             (32, 256, 8, False, False), (16, 256, 8, False, True),
                                             (32, 64, 8, True, False)])
-@pytest.mark.parametrize("mode", ["split", "last_block", "local"])
+@pytest.mark.parametrize("mode", ["split", "last_block", "local", "cluster"])
 def test_bn_act_fwd_bwd(native_ext, N, C, H, pool, res, mode):
     """split: reduce -> finalize -> apply launches; last_block: the reduce kernel's final block
     finalizes k1/k2/dgamma/dbeta (ticket counter) instead of a separate finalize launch; local:
     one block per 8 channels does the whole backward in one launch (bn_act_bwd_local_kernel;
-    the shapes cover 1-8 items per thread, pooled, plain and residual)."""
+    the shapes cover 1-8 items per thread, pooled, plain and residual); cluster: up to 16
+    blocks per 64 channels meeting at a grid-wide arrival counter (bn_act_bwd_cluster_kernel)."""
     from ddp_amd.ops.common import ptr, stream_handle
     nat = native_ext
     last_block = mode == "last_block"
     nat.bn_bwd_local_set(64 if mode == "local" else 0)  # local: any shape it can hold
+    if mode == "cluster" and (C % 64 or N * H * H // (4 if pool else 1) > 16 * 32 * 4):
+        nat.bn_bwd_local_set(8)
+        pytest.skip("shape outside the clustered kernel's range")
+    nat.bn_bwd_cluster_set(1 if mode == "cluster" else 0)
     try:
-        _bn_case(nat, N, C, H, pool, res, last_block, ptr, stream_handle)
+        _bn_case(nat, N, C, H, pool, res, last_block, ptr, stream_handle,
+                 cluster=mode == "cluster")
         if mode == "local":
             assert nat.bn_bwd_local_ok(N, H, H, C, int(pool))
     finally:
-        nat.bn_bwd_local_set(8)  # the shipped limit (bn_act.hip kLocalMaxLoads)
+        nat.bn_bwd_local_set(8)  # the shipped limits (bn_act.hip kLocalMaxLoads, kClusterMode)
+        nat.bn_bwd_cluster_set(0)
 
 
-def _bn_case(nat, N, C, H, pool, res, last_block, ptr, stream_handle):
+def _bn_case(nat, N, C, H, pool, res, last_block, ptr, stream_handle, cluster=False):
     z = bf(torch.randn(N, C, H, H, device=DEV) * 2 + 0.5)
     r = bf(torch.randn(N, C, H, H, device=DEV)) if res else None
     gamma = torch.rand(C, device=DEV) + 0.5
@@ -228,10 +235,15 @@ def _bn_case(nat, N, C, H, pool, res, last_block, ptr, stream_handle):
     db = torch.zeros(C, device=DEV)
     dbias = torch.zeros(C, device=DEV)
     counter = torch.zeros(1, dtype=torch.int32, device=DEV) if last_block else None
+    sync = torch.zeros(1, dtype=torch.int32, device=DEV) if cluster else None
     nat.bn_act_bwd(N, H, H, C, int(pool), 1, 1e-5, ptr(zn), ptr(rn), ptr(stats), ptr(gamma),
                    ptr(beta), ptr(doutn), ptr(sums), ptr(dz), ptr(dres), ptr(dg), ptr(db),
-                   ptr(dbias), s, ptr(coef), ptr(counter))
+                   ptr(dbias), s, ptr(coef), ptr(counter), grid_sync=ptr(sync))
     torch.cuda.synchronize()
+    if cluster:  # every block of the launch arrived exactly once (grid as bn_act.hip cluster_cfg)
+        npix = N * H * H // (4 if pool else 1)
+        k = next(-(-npix // (32 * i)) for i in (1, 2, 4) if -(-npix // (32 * i)) <= 16)
+        assert int(sync.item()) == (C // 64) * k
     if last_block:
         assert int(counter.item()) == 0  # reset by the finalizing block
     assert rel_err(dz.permute(0, 3, 1, 2), zr.grad) < 2e-2
