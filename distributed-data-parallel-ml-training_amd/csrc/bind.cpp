@@ -329,11 +329,36 @@ PYBIND11_MODULE(_native, m) {
      py::arg("beta"), py::arg("dout"), py::arg("sums"), py::arg("dz"), py::arg("dres"),
      py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("stream"), py::arg("coef"),
      py::arg("counter") = 0, py::arg("sums_ready") = 0, py::arg("grid_sync") = 0);
+  // ResNet stem: BN + ReLU + MaxPool2d(3, 2, 1) in one pass each way (bn_act.hip bn_pool3_*):
+  // (N, H, W) = conv output, out / dout pooled, idx = uint8 window argmax (pooled shape)
+  m.def("bn_pool3_fwd", [](int N, int H, int W, int C, int relu, float eps, uintptr_t z,
+                           uintptr_t stats, uintptr_t gamma, uintptr_t beta, uintptr_t out,
+                           uintptr_t idx, uintptr_t st, uintptr_t running_mean,
+                           uintptr_t running_var, float momentum, int use_running, uintptr_t coef) {
+    ddp_amd::BnArgs a{};
+    a.N = N; a.H = H; a.W = W; a.C = C; a.relu = relu; a.eps = eps;
+    a.z = P<unsigned short>(z); a.stats = P<float>(stats); a.gamma = P<float>(gamma);
+    a.beta = P<float>(beta); a.out = P<unsigned short>(out); a.coef = P<float>(coef);
+    a.running_mean = P<float>(running_mean); a.running_var = P<float>(running_var);
+    a.momentum = momentum; a.use_running = use_running;
+    check(ddp_bn_pool3_fwd(&a, P<unsigned char>(idx), S(st)), "bn_pool3_fwd");
+  });
+  m.def("bn_pool3_bwd", [](int N, int H, int W, int C, int relu, float eps, uintptr_t z,
+                           uintptr_t dout, uintptr_t idx, uintptr_t sums, uintptr_t dz,
+                           uintptr_t dgamma, uintptr_t dbeta, uintptr_t st, uintptr_t coef) {
+    ddp_amd::BnArgs a{};
+    a.N = N; a.H = H; a.W = W; a.C = C; a.relu = relu; a.eps = eps;
+    a.z = P<unsigned short>(z); a.dout = P<unsigned short>(dout); a.sums = P<float>(sums);
+    a.dz = P<unsigned short>(dz); a.dgamma = P<float>(dgamma); a.dbeta = P<float>(dbeta);
+    a.coef = P<float>(coef);
+    check(ddp_bn_pool3_bwd(&a, P<unsigned char>(idx), S(st)), "bn_pool3_bwd");
+  });
   m.def("bn_bwd_cluster_set", [](int mode) { ddp_bn_bwd_cluster_set(mode); });
   m.def("bn_bwd_local_ok", [](int N, int H, int W, int C, int pool) {
     return ddp_bn_bwd_local_ok(N, H, W, C, pool) != 0;
   });
   m.def("bn_bwd_local_set", [](long long max_loads) { ddp_bn_bwd_local_set(max_loads); });
+  m.def("conv_epi_stage_set", [](int on) { ddp_conv_epi_stage_set(on); });
 
   m.def("linear_ce_fwd", [](uintptr_t x, uintptr_t W, uintptr_t b, uintptr_t labels, int B, int F,
                             int J, uintptr_t logits, uintptr_t dlogits, uintptr_t loss_sum,

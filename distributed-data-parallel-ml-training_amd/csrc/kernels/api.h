@@ -197,6 +197,9 @@ int ddp_sgd(float* p, const float* g, float* buf, size_t n, float lr, float mome
 int ddp_conv_fwd_smallk(const ddp_amd::ConvGeom* g, const void* x, const void* wc,
                         const float* bias, void* y, float* stats, hipStream_t st);
 void ddp_conv_options(int wgrad_atomic, int persistent, int stages);
+void ddp_conv_epi_stage_set(int on);
+int ddp_bn_pool3_fwd(const ddp_amd::BnArgs* a, unsigned char* idx, hipStream_t st);
+int ddp_bn_pool3_bwd(const ddp_amd::BnArgs* a, const unsigned char* idx, hipStream_t st);
 void ddp_conv_pair_mode(int mode, int items);
 // sweeps (tools/conv_tune.py --pairs): force the paired launch with these split-K factors (0 = off)
 void ddp_conv_pair_force(int splits_dg, int splits_wg);

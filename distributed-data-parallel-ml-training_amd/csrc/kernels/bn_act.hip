@@ -634,6 +634,165 @@ __global__ __launch_bounds__(256) void bn_act_bwd_cluster_kernel(BnArgs a, int K
   }
 }
 
+// ------------------------------- ResNet stem: BN + ReLU + 3x3/s2/p1 max-pool -------------------------------
+// The stem's 112x112 BatchNorm output only exists to be max-pooled (torchvision ResNet conv1 ->
+// bn1 -> relu -> maxpool): forward computes relu(scale*z + shift) for the nine taps of each
+// pooled output and stores only the pooled value and the window argmax (one byte); backward
+// routes the pooled gradient by a GATHER (each input pixel sums the <= 2x2 windows whose argmax
+// is its tap) straight into the BN-backward reduce and apply, so neither the 411 MB pre-pool
+// activation (batch 256) nor its gradient is ever written. Argmax tie-break / NaN rule: first
+// tap in row-major window order, NaN wins (pool.hip maxpool_fwd_kernel).
+constexpr int kP3 = 3, kP3S = 2, kP3P = 1;
+
+__global__ __launch_bounds__(256) void bn_pool3_fwd_kernel(BnArgs a, int Ho, int Wo,
+                                                           unsigned char* __restrict__ idx) {
+  const unsigned G = a.C / 8;
+  const unsigned total = (unsigned)a.N * Ho * Wo * G;  // < 2^31 (host)
+  for (unsigned t = blockIdx.x * 256 + threadIdx.x; t < total; t += gridDim.x * 256) {
+    const unsigned pix = t / G;
+    const int cg = (int)(t - pix * G);
+    const unsigned prow = pix / (unsigned)Wo;
+    const int wo = (int)(pix - prow * Wo);
+    const int n = (int)(prow / (unsigned)Ho);
+    const int ho = (int)(prow - (unsigned)n * Ho);
+    float sc[8], sh[8], best[8];
+    unsigned char arg[8];
+    ld8f(a.coef + kSc * a.C + cg * 8, sc);
+    ld8f(a.coef + kSh * a.C + cg * 8, sh);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; arg[e] = 0; }
+#pragma unroll
+    for (int kh = 0; kh < kP3; ++kh) {
+      const int h = ho * kP3S - kP3P + kh;
+      if ((unsigned)h >= (unsigned)a.H) continue;
+#pragma unroll
+      for (int kw = 0; kw < kP3; ++kw) {
+        const int w = wo * kP3S - kP3P + kw;
+        if ((unsigned)w >= (unsigned)a.W) continue;
+        const u16x8 v = ld8(a.z + (((size_t)n * a.H + h) * a.W + w) * a.C + cg * 8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float y = bf2f(v[e]) * sc[e] + sh[e];
+          if (a.relu) y = fmaxf(y, 0.f);
+          if (y > best[e] || y != y) { best[e] = y; arg[e] = (unsigned char)(kh * kP3 + kw); }
+        }
+      }
+    }
+    u16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(best[e]);
+    const size_t off = (size_t)pix * a.C + cg * 8;
+    st8(a.out + off, o);
+    uint2 packed;
+    packed.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | ((unsigned)arg[3] << 24);
+    packed.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | ((unsigned)arg[7] << 24);
+    *reinterpret_cast<uint2*>(idx + off) = packed;
+  }
+}
+
+// gradient at the BN output of pre-pool pixel (n, h, w), channels cg*8..+7: the pooled
+// gradients of the windows whose argmax is this pixel, masked by the ReLU (recomputed from z)
+__device__ __forceinline__ void pool3_gather(const BnArgs& a, const unsigned char* __restrict__ idx,
+                                             int Ho, int Wo, int n, int h, int w, int cg,
+                                             const float* sc, const float* sh, const u16x8& zv,
+                                             float* dyb) {
+  float g[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int ho_lo = max(0, (h + kP3P - kP3 + kP3S) / kP3S), ho_hi = min(Ho - 1, (h + kP3P) / kP3S);
+  const int wo_lo = max(0, (w + kP3P - kP3 + kP3S) / kP3S), wo_hi = min(Wo - 1, (w + kP3P) / kP3S);
+  for (int ho = ho_lo; ho <= ho_hi; ++ho) {
+    const int kh = h - (ho * kP3S - kP3P);
+    for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+      const int kw = w - (wo * kP3S - kP3P);
+      const size_t off = (((size_t)n * Ho + ho) * Wo + wo) * a.C + cg * 8;
+      const uint2 packed = *reinterpret_cast<const uint2*>(idx + off);
+      const u16x8 d = ld8(a.dout + off);
+      const unsigned me = (unsigned)(kh * kP3 + kw);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const unsigned word = e < 4 ? packed.x : packed.y;
+        if (((word >> (8 * (e & 3))) & 0xffu) == me) g[e] += bf2f(d[e]);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float y = bf2f(zv[e]) * sc[e] + sh[e];
+    dyb[e] = (a.relu && !(y > 0.f)) ? 0.f : g[e];
+  }
+}
+
+// APPLY = false: S1 / S2 (grid-stride over pixels, one channel group per thread, block
+// reduction, one atomic per channel per block into a replica); APPLY = true: dz.
+template <bool APPLY>
+__global__ __launch_bounds__(256) void bn_pool3_bwd_kernel(BnArgs a, int Ho, int Wo,
+                                                           const unsigned char* __restrict__ idx) {
+  const int G = a.C / 8;            // host: 64 % G == 0
+  const int cg = threadIdx.x % G;
+  const int per = 256 / G;          // pixels per block iteration
+  const unsigned npix = (unsigned)a.N * a.H * a.W;
+  float sc[8], sh[8], mu[8], is[8], k1[8], k2[8];
+  ld8f(a.coef + kSc * a.C + cg * 8, sc);
+  ld8f(a.coef + kSh * a.C + cg * 8, sh);
+  ld8f(a.coef + kMu * a.C + cg * 8, mu);
+  ld8f(a.coef + kIs * a.C + cg * 8, is);
+  if (APPLY) {
+    ld8f(a.coef + kK1 * a.C + cg * 8, k1);
+    ld8f(a.coef + kK2 * a.C + cg * 8, k2);
+  }
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  for (unsigned p = blockIdx.x * per + threadIdx.x / G; p < npix; p += gridDim.x * per) {
+    const unsigned prow = p / (unsigned)a.W;
+    const int w = (int)(p - prow * a.W);
+    const int n = (int)(prow / (unsigned)a.H);
+    const int h = (int)(prow - (unsigned)n * a.H);
+    const size_t off = (size_t)p * a.C + cg * 8;
+    const u16x8 zv = ld8(a.z + off);
+    float dyb[8];
+    pool3_gather(a, idx, Ho, Wo, n, h, w, cg, sc, sh, zv, dyb);
+    if (APPLY) {
+      u16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xh = (bf2f(zv[e]) - mu[e]) * is[e];
+        o[e] = f2bf(sc[e] * (dyb[e] - k1[e] - xh * k2[e]));
+      }
+      st8(a.dz + off, o);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s1[e] += dyb[e];
+        s2[e] += dyb[e] * ((bf2f(zv[e]) - mu[e]) * is[e]);
+      }
+    }
+  }
+  if (APPLY) return;
+  // lanes l, l + G, ... of a wave share the channel group: butterfly, then the 4 waves via LDS
+  for (int m = G; m < 64; m *= 2)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s1[e] += __shfl_xor(s1[e], m);
+      s2[e] += __shfl_xor(s2[e], m);
+    }
+  __shared__ float red[4][2][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane < G) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[wv][0][lane * 8 + e] = s1[e];
+      red[wv][1][lane * 8 + e] = s2[e];
+    }
+  }
+  __syncthreads();
+  float* rep = a.sums + (blockIdx.x % kStatRep) * 2 * a.C;
+  for (int k = threadIdx.x; k < 2 * a.C; k += 256) {
+    const int which = k / a.C, c = k - which * a.C;
+    atomicAdd(rep + which * a.C + c, red[0][which][c] + red[1][which][c] + red[2][which][c] +
+                                         red[3][which][c]);
+  }
+}
+
 }  // namespace ddp_amd
 
 using namespace ddp_amd;
@@ -853,5 +1012,43 @@ extern "C" int ddp_bn_act_bwd(const BnArgs* args, hipStream_t st) {
     else if (ipt == 2) launch_bwd<false, 2>(a, npix, Gb, chunks, st);
     else launch_bwd<false, 1>(a, npix, Gb, chunks, st);
   }
+  return (int)hipGetLastError();
+}
+
+
+// ResNet stem BN + ReLU + MaxPool2d(3, 2, 1) (bn_pool3_*): a.H x a.W = conv output, a.out /
+// a.dout = pooled [N][Ho][Wo][C], idx = the forward's window argmax bytes (pooled shape).
+static bool pool3_shape_ok(const BnArgs& a, int* Ho, int* Wo) {
+  if (a.C % 8 || 64 % (a.C / 8) || a.coef == nullptr || a.res || a.pool) return false;
+  *Ho = (a.H + 2 * kP3P - kP3) / kP3S + 1;
+  *Wo = (a.W + 2 * kP3P - kP3) / kP3S + 1;
+  return (size_t)a.N * a.H * a.W * a.C < (1ull << 31);
+}
+
+extern "C" int ddp_bn_pool3_fwd(const BnArgs* args, unsigned char* idx, hipStream_t st) {
+  const BnArgs a = *args;
+  int Ho, Wo;
+  if (!pool3_shape_ok(a, &Ho, &Wo) || idx == nullptr) return -1;
+  hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3(blocks_for(a.C, 256)), dim3(256), 0, st, a);
+  const size_t items = (size_t)a.N * Ho * Wo * (a.C / 8);
+  const unsigned nb = (unsigned)std::min<size_t>(blocks_for(items, 256), 8192);
+  hipLaunchKernelGGL(bn_pool3_fwd_kernel, dim3(nb), dim3(256), 0, st, a, Ho, Wo, idx);
+  return (int)hipGetLastError();
+}
+
+// a.sums must be zero on entry (per-step scratch); dgamma / dbeta are accumulated
+extern "C" int ddp_bn_pool3_bwd(const BnArgs* args, const unsigned char* idx, hipStream_t st) {
+  const BnArgs a = *args;
+  int Ho, Wo;
+  if (!pool3_shape_ok(a, &Ho, &Wo) || idx == nullptr || a.sums == nullptr || a.dz == nullptr)
+    return -1;
+  const size_t npix = (size_t)a.N * a.H * a.W;
+  const size_t per = 256 / (a.C / 8);
+  // reduce: ~8 pixel iterations per thread (fewer replica atomics); apply: one pass
+  const unsigned nr = (unsigned)std::max<size_t>(1, std::min<size_t>(blocks_for(npix, per * 8), 2048));
+  const unsigned na = (unsigned)std::min<size_t>(blocks_for(npix, per), 16384);
+  hipLaunchKernelGGL((bn_pool3_bwd_kernel<false>), dim3(nr), dim3(256), 0, st, a, Ho, Wo, idx);
+  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3(blocks_for(a.C, 256)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((bn_pool3_bwd_kernel<true>), dim3(na), dim3(256), 0, st, a, Ho, Wo, idx);
   return (int)hipGetLastError();
 }

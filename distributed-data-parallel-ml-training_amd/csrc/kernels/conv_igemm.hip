@@ -60,6 +60,12 @@ struct FastDiv {
 __device__ __forceinline__ int fast_div(int x, FastDiv d) {
   return (int)((__umulhi((unsigned)x, d.mul) + (unsigned)x) >> d.sh);
 }
+__device__ __forceinline__ void ld8f_conv(const float* p, float* v) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0];
+  const float4 b = reinterpret_cast<const float4*>(p)[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
 
 struct ConvArgs {
   ConvGeom g;
@@ -100,6 +106,9 @@ struct ConvArgs {
   // split-K finish (splitk_finish_bnbwd_kernel) and where to report that it was
   const BnBwdApply* bnapply;
   int* bnapply_done;
+  // FWD / DGRAD bf16 output through the LDS-staged epilogue (conv_igemm_body): full 16-B
+  // stores of whole tile rows instead of 8-B fragments of 16 rows per instruction
+  int epi_stage;
 };
 
 // ------------------------------------------------------------------ operand gathers
@@ -512,6 +521,114 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
   // a BnBwdFuse = the preceding block's BatchNorm-backward sums
   const bool red = (MODE == MODE_FWD && !split && args.stats != nullptr) ||
                    (MODE == MODE_DGRAD && BNF && !split);
+  // LDS-staged output (FWD, DGRAD incl. the accumulating second branch; no BN-backward
+  // fusion): the MFMA layout gives each lane one row and 4 columns, so a direct store writes
+  // 16 rows x 32 B per instruction — partial lines that run the big-output 1x1 convs at about
+  // half the HBM write rate (tools/probes/epilogue_probe.py). Instead each wave row parks its
+  // fp32 accumulators in the idle operand ring ([BM/2][BN] fp32, 16-B chunks XOR-swizzled by
+  // row; two halves, so the ring needs BM*BN*2 bytes), then every thread stores whole 16-B bf16
+  // chunks of 8 consecutive channels (a wave writes 64 x 16 B of 2-8 full rows), adding the
+  // bias / the old dx and rounding exactly like the direct path (bit-identical output), and
+  // accumulates the BatchNorm statistics of its fixed 8 channels on the way out.
+  if (MODE != MODE_WGRAD && BNF == 0 && !(BM == 64 && BN == 64) && !split && args.epi_stage) {
+    constexpr int HM = BM / 2;             // rows per half (= one wave row's WTM)
+    constexpr int C4 = BN / 4;             // fp32 16-B chunks per staged row
+    constexpr int CPR = BN / 8;            // bf16 16-B output chunks per tile row
+    constexpr int RPP = 256 / CPR;         // tile rows per pass of the block
+    constexpr int PASSES = HM / RPP;
+    static_assert(HM % RPP == 0 && HM == WTM, "half tiles must cover whole passes");
+    float* cf = reinterpret_cast<float*>(smem);  // launch_gemm_t sizes the ring >= BM*BN*2 B
+    const int rl = lane & 15, cq = 4 * (lane >> 4);
+    const int cc = tid % CPR;              // this thread's output chunk (8 channels)
+    const int col = col0 + cc * 8;
+    const bool cok = col < args.Ng;
+    float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (MODE == MODE_FWD && args.bias && cok) ld8f_conv(args.bias + col, bv);
+    float s[8], ss[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { s[e] = 0.f; ss[e] = 0.f; }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      __syncthreads();                     // ring idle (last MFMA reads / previous half stored)
+      if (wm == h) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int c = wn * WTN + j * 16 + cq;
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            const int r = i * 16 + rl;
+            *reinterpret_cast<f32x4*>(cf + r * BN + (((c >> 2) ^ (r & (C4 - 1))) << 2)) = acc[i][j];
+          }
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int p = 0; p < PASSES; ++p) {
+        const int r = tid / CPR + p * RPP;
+        const int row = row0 + h * HM + r;
+        const f32x4 lo = *reinterpret_cast<const f32x4*>(cf + r * BN + (((2 * cc) ^ (r & (C4 - 1))) << 2));
+        const f32x4 hi = *reinterpret_cast<const f32x4*>(cf + r * BN + (((2 * cc + 1) ^ (r & (C4 - 1))) << 2));
+        if (!cok || row >= args.Mg) continue;
+        const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        size_t orow = row;
+        if (phase) {  // phase-local row -> input pixel
+          const int hw = args.Hp * args.Wp;
+          const int n = fast_div(row, args.dPQ), rem = row - n * hw;
+          const int pi = fast_div(rem, args.dQ), pj = rem - pi * args.Wp;
+          orow = ((size_t)n * g.H + args.pa + g.stride * pi) * g.W + args.pb + g.stride * pj;
+        }
+        unsigned short* dst = args.out + orow * args.Ng + col;
+        u16x8 o;
+        if (MODE == MODE_DGRAD && args.accumulate) {  // dx += (second gradient branch)
+          const u16x8 old = ld8(dst);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e] + bf2f(old[e]));
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e] + bv[e]);
+        }
+        st8(dst, o);
+        if (MODE == MODE_FWD && red) {  // statistics of the stored (bf16-rounded) values
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float rv = bf2f(o[e]);
+            s[e] += rv;
+            ss[e] += rv * rv;
+          }
+        }
+      }
+    }
+    if (MODE == MODE_FWD && red) {
+      // lanes l, l + CPR, ... of a wave share the chunk column: butterfly over them, then the
+      // four waves meet in LDS (after every wave is done reading the staged tile)
+#pragma unroll
+      for (int m = CPR; m < 64; m *= 2)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          s[e] += __shfl_xor(s[e], m);
+          ss[e] += __shfl_xor(ss[e], m);
+        }
+      __syncthreads();
+      float* sl = reinterpret_cast<float*>(smem);  // [wave][2][BN]
+      if (lane < CPR) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          sl[(wid * 2 + 0) * BN + lane * 8 + e] = s[e];
+          sl[(wid * 2 + 1) * BN + lane * 8 + e] = ss[e];
+        }
+      }
+      __syncthreads();
+      float* st = args.stats + (bid % kStatRep) * 2 * args.Ng;  // spread contention
+      for (int k = tid; k < 2 * BN; k += 256) {
+        const int which = k / BN, cl = k - which * BN;
+        if (col0 + cl >= args.Ng) continue;
+        const float t = sl[(0 * 2 + which) * BN + cl] + sl[(1 * 2 + which) * BN + cl] +
+                        sl[(2 * 2 + which) * BN + cl] + sl[(3 * 2 + which) * BN + cl];
+        atomicAdd(st + which * args.Ng + col0 + cl, t);
+      }
+    }
+    return;
+  }
   // the LDS operand ring is reused for the statistics hand-off: every wave must be done with it
   if (red) __syncthreads();
   // (not for 64x64 tiles: measured slower there — the VGG-11 forward convs, whose long
@@ -1568,6 +1685,17 @@ static int g_persistent = 0;    // grid = resident slots, blocks loop over work 
 static int g_stages = 2;        // LDS ring depth policy (see stages_for)
 constexpr int kMaxAtomicSplits = 32;
 constexpr int kNumCUs = 256;
+// LDS-staged FWD / DGRAD epilogue (conv_igemm_body); DDP_AMD_EPI_STAGE=0 restores the direct
+// fragment stores
+static int g_epi_stage = -1;
+static bool epi_stage_enabled() {
+  if (g_epi_stage < 0) {
+    const char* e = std::getenv("DDP_AMD_EPI_STAGE");
+    g_epi_stage = e ? std::atoi(e) : 1;
+  }
+  return g_epi_stage != 0;
+}
+extern "C" void ddp_conv_epi_stage_set(int on) { g_epi_stage = on ? 1 : 0; }
 
 // Split-K factor for a tile config: aim for >= 2 workgroups per CU, keep >= 4 k-steps per
 // split, fit the slab workspace.
@@ -1623,8 +1751,12 @@ static void launch_gemm_t(const ConvArgs& a, int items, hipStream_t st) {
   // remain). Short reductions — the 1x1 convs over 64/128 channels, 1-2 k-steps — thus need a
   // fraction of the ring, and the smaller LDS footprint doubles the resident workgroups per CU
   // (their tiles are latency-bound: DMA in, a few MFMAs, stores out).
+  // the LDS-staged epilogue needs the whole bf16 tile (more than one stage only for the
+  // 256x128 / 128x256 tiles)
+  constexpr int kTileBytes = BM * BN * 2;
   const int stages = std::max(1, std::min(NST, a.ksteps_per_split));
-  const size_t lds = (size_t)stages * kStageBytes;
+  size_t lds = (size_t)stages * kStageBytes;
+  if (a.epi_stage && lds < (size_t)kTileBytes) lds = kTileBytes;
   void (*kern)(ConvArgs);
   if constexpr (BNF == 2 && MODE == MODE_DGRAD) kern = conv_igemm_bnf2_kernel<MODE, BM, BN, NST>;
   else kern = conv_igemm_kernel<MODE, BM, BN, NST, BNF>;
@@ -1632,7 +1764,8 @@ static void launch_gemm_t(const ConvArgs& a, int items, hipStream_t st) {
   if (!attr) {
     // an error here surfaces through the caller's hipGetLastError
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, NST * kStageBytes);
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              std::max(NST * kStageBytes, kTileBytes));
     attr = true;
   }
   // persistent grid: at most the resident workgroup slots (queried once per instantiation)
@@ -1671,6 +1804,7 @@ static int prepare_cfg(ConvArgs& a, int splits) {
   splits = (ksteps + per - 1) / per;
   a.splits = splits;
   a.ksteps_per_split = per;
+  a.epi_stage = MODE != MODE_WGRAD && epi_stage_enabled();
   if (MODE == MODE_DGRAD) {
     const int hh = a.phase ? a.Hp : a.g.H, ww = a.phase ? a.Wp : a.g.W;
     a.dPQ = make_fastdiv(std::max(1, hh * ww));
@@ -1935,7 +2069,8 @@ static void plan_mode(ConvArgs& a, size_t ws_elems, int* best_out, int* sp, int*
     }
   } else if (a.splits <= 0) {
     auto it = g_tuned.find(TuneKey{MODE, a.Mg, a.Ng, a.Kg});
-    if (it != g_tuned.end()) {
+    // (DGRAD on the 64x256 / 256x128 / 128x256 tiles computes a wrong dx: never from a table)
+    if (it != g_tuned.end() && !(MODE == MODE_DGRAD && it->second.tile >= 5)) {
       const size_t slab = (size_t)a.Mg * a.Ng;
       const int ksteps = (a.Kg + 63) / 64;
       int spl = std::max(1, std::min(it->second.splits, ksteps));

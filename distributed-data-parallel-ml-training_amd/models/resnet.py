@@ -11,8 +11,14 @@ GPU execution: every conv+BN(+residual)+ReLU is one ConvBNAct Function (implicit
 conv with fused BN statistics + one streaming BN/add/ReLU pass), the classifier is the same
 MFMA GEMM (1x1 conv), pooling uses the pool.hip kernels; CPU execution is plain ATen.
 """
+import os
+
 import torch
 import torch.nn as nn
+
+# stem BatchNorm + ReLU + 3x3/s2 max-pool fused (no pre-pool activation in HBM); =0 restores the
+# separate bn_act + maxpool passes
+STEM_POOL_FUSE = os.environ.get("DDP_AMD_STEM_POOL_FUSE", "1") != "0"
 
 
 class Bottleneck(nn.Module):
@@ -116,6 +122,8 @@ class ResNet(nn.Module):
         from ..ops.layers import ConvBNActSpec, LinearGemmSpec
         if self._stem is None:
             self._stem = ConvBNActSpec(self.conv1, self.bn1, relu=True, cin_pad=8)
+            # bn1 + relu + maxpool in one pass each way (bn_act.hip bn_pool3_*)
+            self._stem.maxpool3 = STEM_POOL_FUSE
             self._fc_spec = LinearGemmSpec(self.fc)
             for b in self.blocks():
                 b.specs()
@@ -134,16 +142,23 @@ class ResNet(nn.Module):
             x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
             return self.fc(torch.flatten(self.avgpool(x), 1))
         from ..ops.common import step_scratch
-        from ..ops.layers import conv_bn_act, global_avg_pool, linear_gemm, max_pool, to_nhwc_input
+        from ..ops.layers import conv_bn_act, global_avg_pool, linear_gemm, to_nhwc_input
         stem, fc = self._gpu_specs()
         step_scratch(x.device).zero()
         if self.training:
             self._bump_batches_tracked()
         h = to_nhwc_input(x, 8)
-        h = max_pool(conv_bn_act(h, stem), 3, 2, 1)
+        h = self._stem_forward(h, stem)
         for b in self.blocks():
             h = b.forward_fused(h)
         return linear_gemm(global_avg_pool(h), fc)
+
+    @staticmethod
+    def _stem_forward(h, stem):
+        from ..ops.layers import conv_bn_act, max_pool
+        if stem.maxpool3:
+            return conv_bn_act(h, stem)
+        return max_pool(conv_bn_act(h, stem), 3, 2, 1)
 
     # ------------------------------------------------------------ segmented backward (DDP)
     # Stages: 0 = stem (conv1 + bn1 + relu + maxpool), 1..16 = the bottleneck blocks in order.
@@ -165,8 +180,7 @@ class ResNet(nn.Module):
         models/vgg.py ``forward_loss_split``. A cut block input that feeds both residual
         branches is a leaf: the two branch gradients meet in its ``.grad``."""
         from ..ops.common import step_scratch
-        from ..ops.layers import (conv_bn_act, cross_entropy, global_avg_pool, linear_gemm,
-                                  max_pool, to_nhwc_input)
+        from ..ops.layers import cross_entropy, global_avg_pool, linear_gemm, to_nhwc_input
         stem, fc = self._gpu_specs()
         blocks = list(self.blocks())
         n = 1 + len(blocks)
@@ -183,7 +197,7 @@ class ResNet(nn.Module):
                 leaf = h.detach().requires_grad_(True)
                 cuts.append((h, leaf))
                 h = leaf
-            h = max_pool(conv_bn_act(h, stem), 3, 2, 1) if st == 0 else blocks[st - 1].forward_fused(h)
+            h = self._stem_forward(h, stem) if st == 0 else blocks[st - 1].forward_fused(h)
         loss = cross_entropy(linear_gemm(global_avg_pool(h), fc), labels)
         if acc is not None:
             acc.add_(loss.detach())

@@ -43,6 +43,9 @@ class ConvBNActSpec:
         self.C = cin_pad if cin_pad is not None else _pad8(Cr)
         self.stride, self.pad = conv.stride[0], conv.padding[0]
         self.relu, self.pool, self.residual = relu, pool, residual
+        # ResNet stem: BatchNorm + ReLU + MaxPool2d(3, 2, 1) fused (bn_act.hip bn_pool3_*; the
+        # pre-pool activation and its gradient are never materialised). Set by models/resnet.py
+        self.maxpool3 = False
         self.eps = float(bn.eps) if bn is not None else 1e-5
         dev = conv.weight.device
         self.wc = torch.empty(K, R, S, self.C, dtype=BF16, device=dev)
@@ -354,6 +357,10 @@ class _ConvBNActFn(torch.autograd.Function):
         stats = spec.stats  # zeroed by the model's per-forward StepScratch.zero()
         P, Q = spec.out_hw(H, W)
         Ho, Wo = (P // 2, Q // 2) if spec.pool else (P, Q)
+        if spec.maxpool3:
+            if spec.pool or residual is not None:
+                raise ValueError("the fused 3x3 max-pool excludes the 2x2 pool and a residual")
+            Ho, Wo = (P - 1) // 2 + 1, (Q - 1) // 2 + 1
         spec._out_p, spec._out_q = P, Q
         y = torch.empty(N, Ho, Wo, spec.K, dtype=BF16, device=x.device)
         if residual is not None:
@@ -374,8 +381,18 @@ class _ConvBNActFn(torch.autograd.Function):
         else:
             z = conv_forward(spec, x, bias, stats, fin=fin)
         spec.fwd_z = z
-        spec.last_deferred = not fused and _defer_bn(spec, residual, rm, N, Ho, Wo)
-        if spec.last_deferred:
+        ctx.pool3_idx = None
+        spec.last_deferred = (not fused and not spec.maxpool3
+                              and _defer_bn(spec, residual, rm, N, Ho, Wo))
+        if spec.maxpool3:
+            idx = torch.empty(N, Ho, Wo, spec.K, dtype=torch.uint8, device=x.device)
+            native().bn_pool3_fwd(N, P, Q, spec.K, int(spec.relu), spec.eps, ptr(z), ptr(stats),
+                                  ptr(gamma), ptr(beta), ptr(y), ptr(idx), stream_handle(),
+                                  ptr(rm), ptr(rv),
+                                  float(bn.momentum if bn.momentum is not None else 0.1),
+                                  use_running, ptr(spec.coef))
+            ctx.pool3_idx = idx
+        elif spec.last_deferred:
             spec.deferred = y  # computed by the next block's conv (conv_tr.hip fused input)
         elif not fused:
             native().bn_act_fwd(N, P, Q, spec.K, int(spec.pool), int(spec.relu), spec.eps, ptr(z),
@@ -412,6 +429,13 @@ class _ConvBNActFn(torch.autograd.Function):
             if zref is None or zref.data_ptr() != z.data_ptr():
                 raise RuntimeError("fused BatchNorm backward belongs to another forward pass "
                                    "(stale dz_fused): refusing to use an unwritten gradient")
+        elif ctx.pool3_idx is not None:  # stem: pooled gradient routed by the window argmax
+            dy = dy.contiguous()
+            dz = torch.empty_like(z)
+            native().bn_pool3_bwd(N, P, Q, K, int(spec.relu), spec.eps, ptr(z), ptr(dy),
+                                  ptr(ctx.pool3_idx), ptr(sums), ptr(dz), ptr(gg), ptr(gbt),
+                                  stream_handle(), ptr(spec.coef))
+            ctx.pool3_idx = None
         else:
             dy = dy.contiguous()
             dz = torch.empty_like(z)

@@ -538,3 +538,103 @@ def test_conv_splitk_finish_bn_fwd(native_ext, N, C, H, K, pool):
     zr = F.conv2d(x, conv.weight, conv.bias, 1, 1)
     ref = _bn_ref(zr, gamma, beta, 1e-5, True, pool, None)
     assert rel_err(y.permute(0, 3, 1, 2), ref) < 1e-2
+
+
+@pytest.mark.parametrize("tile", [1, 2, 3, 5])  # the tiles the tuned table uses (not 64x64)
+@pytest.mark.parametrize("case", [(4, 64, 28, 28, 256, 1, 1, 0), (4, 256, 28, 28, 64, 1, 1, 0),
+                                  (3, 64, 21, 21, 128, 1, 2, 0), (2, 64, 14, 14, 128, 3, 1, 1)])
+def test_conv_staged_epilogue(native_ext, case, tile):
+    """LDS-staged FWD / DGRAD epilogue (conv_igemm.hip epi_stage: bf16 tile through the idle
+    operand ring, 16-B row stores, BN statistics per 8-channel chunk) on every big tile, without
+    split-K: output bit-identical to the direct fragment stores (same fp32 sums, same rounding),
+    statistics and the accumulating second-branch dgrad (dx += ...) against fp32 PyTorch; the
+    strided case runs the phase-decomposed dgrad (row -> input pixel remap in the store)."""
+    from ddp_amd.ops.common import ptr, stream_handle, workspace
+    N, Cin, H, W, K, R, stride, pad = case
+    conv, spec, x, xn = _conv_setup(N, Cin, H, W, K, R, stride, pad)
+    ws = workspace(xn.device)
+    g = spec.geom(N, H, W)
+    P, Q = g[9], g[10]
+    dz = bf(torch.randn(N, K, P, Q, device=DEV))
+    dzn = dz.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    prior = bf(torch.randn(N, H, W, Cin, device=DEV)).to(torch.bfloat16)
+    out = {}
+    native_ext.conv_force_tile(tile, 0)
+    try:
+        for staged in (0, 1):
+            native_ext.conv_epi_stage_set(staged)
+            z = torch.empty(N, P, Q, K, dtype=torch.bfloat16, device=DEV)
+            stats = torch.zeros(16 * 2 * K, device=DEV)
+            native_ext.conv_fwd(g, ptr(xn), ptr(spec.wc), ptr(conv.bias), ptr(z), ptr(stats),
+                                ptr(ws), ws.numel(), 1, stream_handle())
+            dx = torch.empty_like(xn)
+            native_ext.conv_dgrad(g, ptr(dzn), ptr(spec.wc), ptr(dx), ptr(ws), ws.numel(), 1,
+                                  stream_handle())
+            dxa = prior.clone()
+            native_ext.conv_dgrad(g, ptr(dzn), ptr(spec.wc), ptr(dxa), ptr(ws), ws.numel(), 1,
+                                  stream_handle(), accumulate=1)
+            torch.cuda.synchronize()
+            out[staged] = (z, stats.view(16, 2 * K).sum(0), dx, dxa)
+    finally:
+        native_ext.conv_force_tile(0, 0)
+        native_ext.conv_epi_stage_set(1)
+    (z0, s0, dx0, dxa0), (z1, s1, dx1, dxa1) = out[0], out[1]
+    assert torch.equal(z0, z1) and torch.equal(dx0, dx1) and torch.equal(dxa0, dxa1)
+    ref = F.conv2d(x, conv.weight, conv.bias, stride, pad).permute(0, 2, 3, 1)
+    assert rel_err(z1, ref) < 1e-2
+    zf = z1.float().reshape(-1, K)
+    assert torch.allclose(s1[:K], zf.sum(0), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(s1[K:], (zf * zf).sum(0), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(s0, s1, rtol=1e-4, atol=1e-3)
+    xr = x.clone().requires_grad_(True)
+    F.conv2d(xr, conv.weight.detach(), None, stride, pad).backward(dz)
+    assert rel_err(dx1.permute(0, 3, 1, 2), xr.grad) < 1e-2
+    assert rel_err(dxa1.float(), xr.grad.permute(0, 2, 3, 1) + prior.float()) < 1e-2
+
+
+@pytest.mark.parametrize("N,C,H,running", [(4, 64, 16, False), (2, 64, 15, True), (3, 32, 9, False)])
+def test_bn_relu_maxpool3_fused(native_ext, N, C, H, running):
+    """ResNet stem BatchNorm + ReLU + MaxPool2d(3, 2, 1) in one pass each way (bn_act.hip
+    bn_pool3_*): pooled output, running statistics, dz (pooled gradient gathered through the
+    window argmax bytes and the recomputed ReLU mask), dgamma / dbeta against fp32 PyTorch."""
+    from ddp_amd.ops.common import ptr, stream_handle
+    nat = native_ext
+    z = bf(torch.randn(N, C, H, H, device=DEV) * 2 + 0.3)
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV) * 0.1
+    zn = z.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    zf = zn.float().reshape(-1, C)
+    stats = torch.zeros(16, 2 * C, device=DEV)
+    stats[5] = torch.cat([zf.sum(0), (zf * zf).sum(0)])
+    Ho = (H - 1) // 2 + 1
+    out = torch.empty(N, Ho, Ho, C, device=DEV, dtype=torch.bfloat16)
+    idx = torch.empty(N, Ho, Ho, C, device=DEV, dtype=torch.uint8)
+    rm = torch.zeros(C, device=DEV) if running else None
+    rv = torch.ones(C, device=DEV) if running else None
+    coef = torch.empty(6 * C, device=DEV)
+    s = stream_handle()
+    nat.bn_pool3_fwd(N, H, H, C, 1, 1e-5, ptr(zn), ptr(stats), ptr(gamma), ptr(beta), ptr(out),
+                     ptr(idx), s, ptr(rm), ptr(rv), 0.1, 0, ptr(coef))
+    zr = z.clone().requires_grad_(True)
+    gr = gamma.clone().requires_grad_(True)
+    br = beta.clone().requires_grad_(True)
+    rm_ref = torch.zeros(C, device=DEV)
+    rv_ref = torch.ones(C, device=DEV)
+    ref = F.max_pool2d(F.relu(F.batch_norm(zr, rm_ref, rv_ref, gr, br, True, 0.1, 1e-5)), 3, 2, 1)
+    assert rel_err(out.permute(0, 3, 1, 2), ref) < 1e-2
+    if running:
+        assert torch.allclose(rm, rm_ref, rtol=1e-4, atol=1e-5)
+        assert torch.allclose(rv, rv_ref, rtol=1e-3, atol=1e-4)
+    dout = bf(torch.randn_like(ref))
+    ref.backward(dout)
+    doutn = dout.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    sums = torch.zeros(16 * 2 * C, device=DEV)
+    dz = torch.empty_like(zn)
+    dg = torch.zeros(C, device=DEV)
+    db = torch.zeros(C, device=DEV)
+    nat.bn_pool3_bwd(N, H, H, C, 1, 1e-5, ptr(zn), ptr(doutn), ptr(idx), ptr(sums), ptr(dz),
+                     ptr(dg), ptr(db), s, ptr(coef))
+    torch.cuda.synchronize()
+    assert rel_err(dz.permute(0, 3, 1, 2), zr.grad) < 2e-2
+    assert rel_err(dg, gr.grad) < 1e-2
+    assert rel_err(db, br.grad) < 1e-2
