@@ -547,7 +547,7 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
     float s[8], ss[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) { s[e] = 0.f; ss[e] = 0.f; }
-#pragma unroll
+#pragma unroll 1
     for (int h = 0; h < 2; ++h) {
       __syncthreads();                     // ring idle (last MFMA reads / previous half stored)
       if (wm == h) {
@@ -636,8 +636,10 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
   // With a BnBwdFuse the preceding block's BatchNorm-backward sums ride along when that block
   // has no pool (its z has this output's shape: the same row offsets); pooled (VGG) fusions keep
   // the generic path, which routes through the window argmax.
+  // (BNF 0 takes the LDS-staged path above, or the generic one below when it is switched off:
+  // keeping this lean path out of those instantiations keeps them at 2 waves per SIMD)
   if (MODE != MODE_WGRAD && !(BM == 64 && BN == 64) && !split &&
-      !(MODE == MODE_DGRAD && args.accumulate) && BNF != 1) {
+      !(MODE == MODE_DGRAD && args.accumulate) && BNF == 2) {
     // Plain bf16 output (FWD, DGRAD overwriting dx). Short-reduction GEMMs (1x1 convs over
     // 64-128 channels: 1-2 k-steps) spend most of their VALU issue in the epilogue and the
     // gather setup, so: one row offset per (lane, i) computed up front (column groups are
@@ -993,8 +995,11 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
   }
 }
 
+// 2 waves per SIMD (<= 256 VGPR + AGPR per lane): left to itself the compiler gives the big
+// tiles 256 VGPRs + ~100 AGPRs (1 wave per SIMD), and these GEMMs are latency-bound
 template <int MODE, int BM, int BN, int NST, int BNF = 0>
-__global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs args) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+void conv_igemm_kernel(ConvArgs args) {
   // dynamic: the launcher sizes the ring to the stages a work item can use (launch_gemm_t)
   extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
   conv_igemm_body<MODE, BM, BN, NST, BNF>(args, smem, blockIdx.x, gridDim.x);

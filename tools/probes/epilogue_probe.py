@@ -61,6 +61,17 @@ def main():
         r["wgrad"] = timeit(lambda: conv_backward(spec, x, dz, dw, False))
         r["wgrad+dgrad"] = timeit(lambda: conv_backward(spec, x, dz, dw, True))
         r["copy(out)"] = timeit(lambda: big2.copy_(big))
+        r["fill(out)"] = timeit(lambda: big2.fill_(1.0))
+        if R == 1:  # the same GEMM through hipBLASLt (materialised A, no statistics)
+            a2 = x.view(-1, C)
+            w2 = torch.randn(C, K, device=dev).to(torch.bfloat16)
+            r["torch_mm"] = timeit(lambda: torch.mm(a2, w2))
+        native().conv_epi_stage_set(0)
+        r["fwd+stats(direct epi)"] = timeit(lambda: conv_forward(spec, x, None, stats))
+        native().conv_epi_stage_set(1)
+        native().conv_options(0, 1, 2)
+        r["fwd+stats(persistent)"] = timeit(lambda: conv_forward(spec, x, None, stats))
+        native().conv_options(0, 0, 2)
         # BN backward passes over the conv output (reduce -> finalize -> apply, no residual)
         z = conv_forward(spec, x, None, stats)
         y = torch.empty_like(z)
