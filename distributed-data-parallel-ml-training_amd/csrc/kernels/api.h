@@ -50,6 +50,9 @@ struct BnArgs {
                                 // layer's dgrad) -> finalize + apply only
   int* grid_sync;               // backward: zeroed arrival counter of the one-launch clustered
                                 // backward (bn_act_bwd_cluster_kernel); null = not available
+  unsigned char* rmask;         // optional, no pool: ReLU mask bits (y > 0), one byte per 8
+                                // channels — written by the forward, read by the backward
+                                // instead of re-reading the residual (ResNet bn3)
 };
 
 // BatchNorm-backward statistics fused into a conv dgrad: the dgrad output IS the gradient at the

@@ -201,6 +201,12 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnArgs a) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = f2bf(best[e]);
     st8(a.out + pix * a.C + cg * 8, o);
+    if (!POOL && a.rmask) {  // ReLU mask for the backward (replaces re-reading the residual)
+      unsigned bits = 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bits |= (best[e] > 0.f ? 1u : 0u) << e;
+      a.rmask[pix * G + cg] = (unsigned char)bits;
+    }
   }
 }
 
@@ -213,6 +219,7 @@ struct BwdItems {
   u16x8 dv[IPT];
   u16x8 zv[IPT][NP];
   u16x8 rv[IPT][POOL ? 1 : NP];  // residual: only without pooling (host rejects pool + res)
+  unsigned mk[IPT];               // ReLU mask byte of the item's 8 channels (BnArgs::rmask)
   size_t off[IPT][NP];
   bool ok[IPT];
 };
@@ -236,7 +243,8 @@ __device__ __forceinline__ void bwd_load(const BnArgs& a, BwdItems<POOL, IPT>& L
       const size_t off = (((size_t)n * a.H + h) * a.W + w) * a.C + cg * 8;
       L.off[it][d] = off;
       L.zv[it][d] = ld8(a.z + off);
-      if (!POOL && a.res) L.rv[it][POOL ? 0 : d] = ld8(a.res + off);
+      if (!POOL && a.rmask) L.mk[it] = a.rmask[off >> 3];  // 1 byte instead of 16 (residual)
+      else if (!POOL && a.res) L.rv[it][POOL ? 0 : d] = ld8(a.res + off);
     }
   }
 }
@@ -244,7 +252,7 @@ __device__ __forceinline__ void bwd_load(const BnArgs& a, BwdItems<POOL, IPT>& L
 // dy_bn (gradient at the BN output, after ReLU mask and pool routing) and xhat for one item
 template <bool POOL>
 __device__ __forceinline__ void bwd_compute(const BnArgs& a, const u16x8& dv, const u16x8* zv,
-                                            const u16x8* rv, const float* sc, const float* sh,
+                                            const u16x8* rv, unsigned mk, const float* sc, const float* sh,
                                             const float* mu, const float* is, float (*xh)[8],
                                             float (*dyb)[8]) {
   constexpr int NP = POOL ? 4 : 1;
@@ -258,7 +266,8 @@ __device__ __forceinline__ void bwd_compute(const BnArgs& a, const u16x8& dv, co
     for (int e = 0; e < 8; ++e) {
       const float zf = bf2f(zv[d][e]);
       float y = zf * sc[e] + sh[e];
-      if (!POOL && a.res) y += bf2f(rv[POOL ? 0 : d][e]);
+      if (!POOL && a.rmask) y = ((mk >> e) & 1u) ? 1.f : 0.f;  // only its sign is used below
+      else if (!POOL && a.res) y += bf2f(rv[POOL ? 0 : d][e]);
       xh[d][e] = (zf - mu[e]) * is[e];
       yv[d][e] = y;
       if (POOL) {
@@ -307,7 +316,7 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
   for (int it = 0; it < IPT; ++it) {
     if (!L.ok[it]) continue;
     float xh[NP][8], dyb[NP][8];
-    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], sc, sh, mu, is, xh, dyb);
+    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], L.mk[it], sc, sh, mu, is, xh, dyb);
 #pragma unroll
     for (int d = 0; d < NP; ++d)
 #pragma unroll
@@ -420,7 +429,7 @@ __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(BnArgs a) {
   for (int it = 0; it < IPT; ++it) {
     if (!L.ok[it]) continue;
     float xh[NP][8], dyb[NP][8];
-    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], sc, sh, mu, is, xh, dyb);
+    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], L.mk[it], sc, sh, mu, is, xh, dyb);
 #pragma unroll
     for (int d = 0; d < NP; ++d) {
       u16x8 o, r;
@@ -466,7 +475,7 @@ __global__ __launch_bounds__(NT) void bn_act_bwd_local_kernel(BnArgs a) {
   for (int it = 0; it < IPT; ++it) {
     if (!L.ok[it]) continue;
     float xh[NP][8], dyb[NP][8];
-    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], sc, sh, mu, is, xh, dyb);
+    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], L.mk[it], sc, sh, mu, is, xh, dyb);
 #pragma unroll
     for (int d = 0; d < NP; ++d)
 #pragma unroll
@@ -506,7 +515,7 @@ __global__ __launch_bounds__(NT) void bn_act_bwd_local_kernel(BnArgs a) {
   for (int it = 0; it < IPT; ++it) {
     if (!L.ok[it]) continue;
     float xh[NP][8], dyb[NP][8];
-    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], sc, sh, mu, is, xh, dyb);
+    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], L.mk[it], sc, sh, mu, is, xh, dyb);
 #pragma unroll
     for (int d = 0; d < NP; ++d) {
       u16x8 o, r;
@@ -558,7 +567,7 @@ __global__ __launch_bounds__(256) void bn_act_bwd_cluster_kernel(BnArgs a, int K
   for (int it = 0; it < IPT; ++it) {
     if (!L.ok[it]) continue;
     float xh[NP][8], dyb[NP][8];
-    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], sc, sh, mu, is, xh, dyb);
+    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], L.mk[it], sc, sh, mu, is, xh, dyb);
 #pragma unroll
     for (int d = 0; d < NP; ++d)
 #pragma unroll
@@ -619,7 +628,7 @@ __global__ __launch_bounds__(256) void bn_act_bwd_cluster_kernel(BnArgs a, int K
   for (int it = 0; it < IPT; ++it) {
     if (!L.ok[it]) continue;
     float xh[NP][8], dyb[NP][8];
-    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], sc, sh, mu, is, xh, dyb);
+    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], L.mk[it], sc, sh, mu, is, xh, dyb);
 #pragma unroll
     for (int d = 0; d < NP; ++d) {
       u16x8 o, r;
@@ -828,6 +837,7 @@ extern "C" int ddp_bn_act_fwd(const BnArgs* args, hipStream_t st) {
   BnArgs a = *args;
   if (a.C % 8 || a.coef == nullptr) return -1;
   if (a.pool && a.res) return -1;  // residual add is only fused without pooling
+  if (a.pool && a.rmask) return -1;
   const int Ho = a.pool ? a.H / 2 : a.H, Wo = a.pool ? a.W / 2 : a.W;
   const size_t items = (size_t)a.N * Ho * Wo * (a.C / 8);
   // 1 item per thread for small layers; 2 (pooled) / 4 (plain) when there are enough to keep
@@ -970,7 +980,7 @@ extern "C" int ddp_bn_act_bwd(const BnArgs* args, hipStream_t st) {
   (void)init;
   BnArgs a = *args;
   if (a.C % 8 || a.coef == nullptr || a.sums == nullptr) return -1;
-  if (a.pool && a.res) return -1;
+  if (a.pool && (a.res || a.rmask)) return -1;
   {
     // small layer: the whole backward in one launch (any sums the next layer's dgrad
     // accumulated are simply not needed)

@@ -235,6 +235,11 @@ BN_BWD_APPLY_FUSE = os.environ.get("DDP_AMD_BN_BWD_APPLY_FUSE", "1") != "0"
 # ... and into the classifier head's dx (linear_dx_bnbwd_kernel; needs BN_BWD_APPLY_FUSE too)
 HEAD_BN_FUSE = os.environ.get("DDP_AMD_HEAD_BN_FUSE", "1") != "0"
 BN_BWD_FUSE_MAX_HW = int(os.environ.get("DDP_AMD_BN_BWD_FUSE_MAX_HW", "16"))
+# residual blocks (ResNet bn3): the forward stores the ReLU mask as bits and the backward reads
+# those instead of the residual tensor (two fewer full-tensor reads per block). Opt-in (=1):
+# measured neutral on ResNet-50 b256 (26.95 / 27.01 vs 26.98 / 27.00 ms, same box) — the byte
+# loads cost about what the 16-B residual loads did
+RELU_MASK = os.environ.get("DDP_AMD_RELU_MASK", "0") == "1"
 # preceding block without a max-pool (ResNet's conv1 -> conv2 -> conv3 chain): one z load per
 # dgrad output element in the epilogue would replace a whole dy + z pass of the reduce kernel,
 # but measured on ResNet-50 b256 the BNF epilogue makes the big dgrad GEMMs slower than the pass
@@ -382,6 +387,7 @@ class _ConvBNActFn(torch.autograd.Function):
             z = conv_forward(spec, x, bias, stats, fin=fin)
         spec.fwd_z = z
         ctx.pool3_idx = None
+        ctx.rmask = None
         spec.last_deferred = (not fused and not spec.maxpool3
                               and _defer_bn(spec, residual, rm, N, Ho, Wo))
         if spec.maxpool3:
@@ -395,11 +401,16 @@ class _ConvBNActFn(torch.autograd.Function):
         elif spec.last_deferred:
             spec.deferred = y  # computed by the next block's conv (conv_tr.hip fused input)
         elif not fused:
+            if residual is not None and spec.relu and RELU_MASK and torch.is_grad_enabled():
+                # ReLU mask bits for the backward instead of re-reading the residual (bn_act.hip
+                # BnArgs::rmask: 1 byte per 8 channels vs 16)
+                ctx.rmask = torch.empty(N * P * Q * spec.K // 8, dtype=torch.uint8,
+                                        device=x.device)
             native().bn_act_fwd(N, P, Q, spec.K, int(spec.pool), int(spec.relu), spec.eps, ptr(z),
                                 ptr(residual), ptr(stats), ptr(gamma), ptr(beta), ptr(y),
                                 stream_handle(), ptr(rm), ptr(rv),
                                 float(bn.momentum if bn.momentum is not None else 0.1),
-                                use_running, ptr(spec.coef))
+                                use_running, ptr(spec.coef), rmask=ptr(ctx.rmask))
         ctx.spec = spec
         ctx.has_res = residual is not None
         ctx.in_link, ctx.res_link = in_link, res_link
@@ -447,7 +458,9 @@ class _ConvBNActFn(torch.autograd.Function):
                                 sums_ready=int(sums_ready),
                                 # arrival counter of the clustered one-launch backward (zeroed
                                 # with the statistics every forward; bn_act.hip)
-                                grid_sync=0 if _common.BN_LAST_BLOCK else ptr(spec.bwd_counter))
+                                grid_sync=0 if _common.BN_LAST_BLOCK else ptr(spec.bwd_counter),
+                                rmask=ptr(ctx.rmask))
+            ctx.rmask = None
         grad_ready([gamma, beta, bias])
         if ctx.res_link is not None and dres is not None:
             dres = ctx.res_link.offer(dres)

@@ -638,3 +638,53 @@ def test_bn_relu_maxpool3_fused(native_ext, N, C, H, running):
     assert rel_err(dz.permute(0, 3, 1, 2), zr.grad) < 2e-2
     assert rel_err(dg, gr.grad) < 1e-2
     assert rel_err(db, br.grad) < 1e-2
+
+
+@pytest.mark.parametrize("N,C,H", [(8, 256, 8), (4, 64, 28), (16, 256, 8)])
+@pytest.mark.parametrize("local", [False, True])
+def test_bn_relu_mask_replaces_residual(native_ext, N, C, H, local):
+    """Residual BatchNorm + ReLU (ResNet bn3) with the ReLU mask bits written by the forward
+    (BnArgs::rmask): the backward that reads the mask instead of the residual gives the same
+    dz / d_res / dgamma / dbeta bits as the residual re-read, and the mask is relu(y) > 0."""
+    from ddp_amd.ops.common import ptr, stream_handle
+    nat = native_ext
+    z = bf(torch.randn(N, H, H, C, device=DEV) * 2 + 0.5).to(torch.bfloat16)
+    r = bf(torch.randn(N, H, H, C, device=DEV)).to(torch.bfloat16)
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV) * 0.1
+    zf = z.float().reshape(-1, C)
+    stats = torch.zeros(16, 2 * C, device=DEV)
+    stats[0] = torch.cat([zf.sum(0), (zf * zf).sum(0)])
+    s = stream_handle()
+    out = torch.empty_like(z)
+    mask = torch.empty(N * H * H * C // 8, dtype=torch.uint8, device=DEV)
+    coef = torch.empty(6 * C, device=DEV)
+    nat.bn_act_fwd(N, H, H, C, 0, 1, 1e-5, ptr(z), ptr(r), ptr(stats), ptr(gamma), ptr(beta),
+                   ptr(out), s, coef=ptr(coef), rmask=ptr(mask))
+    bits = (out.reshape(-1, 8) > 0).to(torch.int32)
+    ref_mask = (bits << torch.arange(8, device=DEV, dtype=torch.int32)).sum(1)
+    assert torch.equal(mask.to(torch.int32), ref_mask)
+    dout = bf(torch.randn(N, H, H, C, device=DEV)).to(torch.bfloat16)
+    nat.bn_bwd_local_set(64 if local else 0)
+    res = []
+    try:
+        for use_mask in (False, True):
+            sums = torch.zeros(16 * 2 * C, device=DEV)
+            dz = torch.empty_like(z)
+            dres = torch.empty_like(z)
+            dg = torch.zeros(C, device=DEV)
+            db = torch.zeros(C, device=DEV)
+            nat.bn_act_bwd(N, H, H, C, 0, 1, 1e-5, ptr(z), ptr(r), ptr(stats), ptr(gamma),
+                           ptr(beta), ptr(dout), ptr(sums), ptr(dz), ptr(dres), ptr(dg), ptr(db),
+                           0, s, ptr(coef), rmask=ptr(mask) if use_mask else 0)
+            torch.cuda.synchronize()
+            res.append((dz, dres, dg, db))
+        exact = local and nat.bn_bwd_local_ok(N, H, H, C, 0)  # else the split path ran
+    finally:
+        nat.bn_bwd_local_set(8)
+    assert torch.equal(res[0][1], res[1][1])  # d_res = the masked gradient itself
+    # (split mode: S1 / S2 come from float atomics in arrival order, so k1 / k2 may differ in
+    # the last bit between the two runs)
+    assert torch.equal(res[0][0], res[1][0]) if exact else rel_err(res[1][0], res[0][0]) < 1e-3
+    assert torch.allclose(res[0][2], res[1][2], rtol=1e-5, atol=1e-5)
+    assert torch.allclose(res[0][3], res[1][3], rtol=1e-5, atol=1e-5)
