@@ -699,46 +699,74 @@ __global__ __launch_bounds__(256) void bn_pool3_fwd_kernel(BnArgs a, int Ho, int
   }
 }
 
-// gradient at the BN output of pre-pool pixel (n, h, w), channels cg*8..+7: the pooled
-// gradients of the windows whose argmax is this pixel, masked by the ReLU (recomputed from z)
-__device__ __forceinline__ void pool3_gather(const BnArgs& a, const unsigned char* __restrict__ idx,
-                                             int Ho, int Wo, int n, int h, int w, int cg,
-                                             const float* sc, const float* sh, const u16x8& zv,
-                                             float* dyb) {
-  float g[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const int ho_lo = max(0, (h + kP3P - kP3 + kP3S) / kP3S), ho_hi = min(Ho - 1, (h + kP3P) / kP3S);
-  const int wo_lo = max(0, (w + kP3P - kP3 + kP3S) / kP3S), wo_hi = min(Wo - 1, (w + kP3P) / kP3S);
-  for (int ho = ho_lo; ho <= ho_hi; ++ho) {
-    const int kh = h - (ho * kP3S - kP3P);
-    for (int wo = wo_lo; wo <= wo_hi; ++wo) {
-      const int kw = w - (wo * kP3S - kP3P);
-      const size_t off = (((size_t)n * Ho + ho) * Wo + wo) * a.C + cg * 8;
-      const uint2 packed = *reinterpret_cast<const uint2*>(idx + off);
-      const u16x8 d = ld8(a.dout + off);
-      const unsigned me = (unsigned)(kh * kP3 + kw);
+// Backward item = the 2x2 pre-pool pixels (2i+a, 2j+b) of pooled position (i, j), 8 channels.
+// With k3 / s2 / p1 a pre-pool row 2i is covered only by window row i (tap row 1), row 2i+1 by
+// window rows i (tap 2) and i+1 (tap 0) — same for columns — so the four windows (i..i+1,
+// j..j+1) serve all four pixels: 4 argmax + 4 gradient loads instead of 9 of each, and 4
+// independent z loads per thread.
+struct Pool3Quad {
+  u16x8 z[4];      // pixel (a, b) -> z[2a + b]
+  float dyb[4][8]; // gradient at the BN output (window-routed, ReLU-masked)
+  bool ok[4];
+  size_t off[4];
+};
+
+__device__ __forceinline__ void pool3_quad(const BnArgs& a, const unsigned char* __restrict__ idx,
+                                           int Ho, int Wo, int n, int i, int j, int cg,
+                                           const float* sc, const float* sh, Pool3Quad& q) {
+  u16x8 d[4];
+  uint2 am[4];
+  bool wok[4];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const unsigned word = e < 4 ? packed.x : packed.y;
-        if (((word >> (8 * (e & 3))) & 0xffu) == me) g[e] += bf2f(d[e]);
-      }
-    }
+  for (int t = 0; t < 4; ++t) {  // window (i + (t >> 1), j + (t & 1))
+    const int ho = i + (t >> 1), wo = j + (t & 1);
+    wok[t] = ho < Ho && wo < Wo;
+    const size_t off = (((size_t)n * Ho + (wok[t] ? ho : i)) * Wo + (wok[t] ? wo : j)) * a.C + cg * 8;
+    am[t] = *reinterpret_cast<const uint2*>(idx + off);
+    d[t] = ld8(a.dout + off);
   }
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const float y = bf2f(zv[e]) * sc[e] + sh[e];
-    dyb[e] = (a.relu && !(y > 0.f)) ? 0.f : g[e];
+  for (int p = 0; p < 4; ++p) {  // pre-pool pixel (2i + (p >> 1), 2j + (p & 1))
+    const int h = 2 * i + (p >> 1), w = 2 * j + (p & 1);
+    q.ok[p] = h < a.H && w < a.W;
+    q.off[p] = ((((size_t)n * a.H + (q.ok[p] ? h : 2 * i)) * a.W) + (q.ok[p] ? w : 2 * j)) * a.C + cg * 8;
+    q.z[p] = ld8(a.z + q.off[p]);
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int pa = p >> 1, pb = p & 1;
+    float g[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int da = t >> 1, db = t & 1;
+      if (pa == 0 && da == 1) continue;  // row 2i: only window row i
+      if (pb == 0 && db == 1) continue;
+      const int kh = pa == 0 ? 1 : (da == 0 ? 2 : 0), kw = pb == 0 ? 1 : (db == 0 ? 2 : 0);
+      const unsigned me = (unsigned)(kh * kP3 + kw);
+      if (!wok[t]) continue;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const unsigned word = e < 4 ? am[t].x : am[t].y;
+        if (((word >> (8 * (e & 3))) & 0xffu) == me) g[e] += bf2f(d[t][e]);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float y = bf2f(q.z[p][e]) * sc[e] + sh[e];
+      q.dyb[p][e] = (a.relu && !(y > 0.f)) ? 0.f : g[e];
+    }
   }
 }
 
-// APPLY = false: S1 / S2 (grid-stride over pixels, one channel group per thread, block
+// APPLY = false: S1 / S2 (grid-stride over the 2x2 quads, one channel group per thread, block
 // reduction, one atomic per channel per block into a replica); APPLY = true: dz.
 template <bool APPLY>
 __global__ __launch_bounds__(256) void bn_pool3_bwd_kernel(BnArgs a, int Ho, int Wo,
                                                            const unsigned char* __restrict__ idx) {
   const int G = a.C / 8;            // host: 64 % G == 0
   const int cg = threadIdx.x % G;
-  const int per = 256 / G;          // pixels per block iteration
-  const unsigned npix = (unsigned)a.N * a.H * a.W;
+  const int per = 256 / G;          // quads per block iteration
+  const unsigned nq = (unsigned)a.N * Ho * Wo;
   float sc[8], sh[8], mu[8], is[8], k1[8], k2[8];
   ld8f(a.coef + kSc * a.C + cg * 8, sc);
   ld8f(a.coef + kSh * a.C + cg * 8, sh);
@@ -751,28 +779,30 @@ __global__ __launch_bounds__(256) void bn_pool3_bwd_kernel(BnArgs a, int Ho, int
   float s1[8], s2[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
-  for (unsigned p = blockIdx.x * per + threadIdx.x / G; p < npix; p += gridDim.x * per) {
-    const unsigned prow = p / (unsigned)a.W;
-    const int w = (int)(p - prow * a.W);
-    const int n = (int)(prow / (unsigned)a.H);
-    const int h = (int)(prow - (unsigned)n * a.H);
-    const size_t off = (size_t)p * a.C + cg * 8;
-    const u16x8 zv = ld8(a.z + off);
-    float dyb[8];
-    pool3_gather(a, idx, Ho, Wo, n, h, w, cg, sc, sh, zv, dyb);
-    if (APPLY) {
-      u16x8 o;
+  for (unsigned qi = blockIdx.x * per + threadIdx.x / G; qi < nq; qi += gridDim.x * per) {
+    const unsigned prow = qi / (unsigned)Wo;
+    const int j = (int)(qi - prow * Wo);
+    const int n = (int)(prow / (unsigned)Ho);
+    const int i = (int)(prow - (unsigned)n * Ho);
+    Pool3Quad q;
+    pool3_quad(a, idx, Ho, Wo, n, i, j, cg, sc, sh, q);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float xh = (bf2f(zv[e]) - mu[e]) * is[e];
-        o[e] = f2bf(sc[e] * (dyb[e] - k1[e] - xh * k2[e]));
-      }
-      st8(a.dz + off, o);
-    } else {
+    for (int p = 0; p < 4; ++p) {
+      if (!q.ok[p]) continue;
+      if (APPLY) {
+        u16x8 o;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        s1[e] += dyb[e];
-        s2[e] += dyb[e] * ((bf2f(zv[e]) - mu[e]) * is[e]);
+        for (int e = 0; e < 8; ++e) {
+          const float xh = (bf2f(q.z[p][e]) - mu[e]) * is[e];
+          o[e] = f2bf(sc[e] * (q.dyb[p][e] - k1[e] - xh * k2[e]));
+        }
+        st8(a.dz + q.off[p], o);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          s1[e] += q.dyb[p][e];
+          s2[e] += q.dyb[p][e] * ((bf2f(q.z[p][e]) - mu[e]) * is[e]);
+        }
       }
     }
   }
@@ -1052,11 +1082,11 @@ extern "C" int ddp_bn_pool3_bwd(const BnArgs* args, const unsigned char* idx, hi
   int Ho, Wo;
   if (!pool3_shape_ok(a, &Ho, &Wo) || idx == nullptr || a.sums == nullptr || a.dz == nullptr)
     return -1;
-  const size_t npix = (size_t)a.N * a.H * a.W;
+  const size_t nq = (size_t)a.N * Ho * Wo;  // 2x2 pre-pool quads
   const size_t per = 256 / (a.C / 8);
-  // reduce: ~8 pixel iterations per thread (fewer replica atomics); apply: one pass
-  const unsigned nr = (unsigned)std::max<size_t>(1, std::min<size_t>(blocks_for(npix, per * 8), 2048));
-  const unsigned na = (unsigned)std::min<size_t>(blocks_for(npix, per), 16384);
+  // reduce: ~4 quad iterations per thread (fewer replica atomics); apply: one pass
+  const unsigned nr = (unsigned)std::max<size_t>(1, std::min<size_t>(blocks_for(nq, per * 4), 4096));
+  const unsigned na = (unsigned)std::min<size_t>(blocks_for(nq, per), 16384);
   hipLaunchKernelGGL((bn_pool3_bwd_kernel<false>), dim3(nr), dim3(256), 0, st, a, Ho, Wo, idx);
   hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3(blocks_for(a.C, 256)), dim3(256), 0, st, a);
   hipLaunchKernelGGL((bn_pool3_bwd_kernel<true>), dim3(na), dim3(256), 0, st, a, Ho, Wo, idx);
