@@ -172,15 +172,17 @@ def main():
                     entries.append({"mode": mode, "M": M, "N": Nn, "K": Kk, "tile": t,
                                     "splits": s, "stages": nst, "us": round(us, 2), "auto_us": round(auto_us, 2),
                                     "shape": label})
+    table = {}
     if args.merge and os.path.exists(args.merge):
         with open(args.merge) as f:
-            old = json.load(f)["entries"]
+            table = json.load(f)  # other sections (tap-reuse tables) are kept as they are
+        old = table.get("entries", [])
         have = {(e["mode"], e["M"], e["N"], e["K"]) for e in entries}
         entries = [e for e in old if (e["mode"], e["M"], e["N"], e["K"]) not in have] + entries
     out = args.out or TUNING_FILE
+    table.update({"device": torch.cuda.get_device_name(0), "reps": args.reps, "entries": entries})
     with open(out, "w") as f:
-        json.dump({"device": torch.cuda.get_device_name(0), "reps": args.reps,
-                   "entries": entries}, f, indent=1)
+        json.dump(table, f, indent=1)
     print(f"wrote {len(entries)} entries to {out}; summed per-op saving {saved_total:.1f} us")
 
 
@@ -286,16 +288,17 @@ def tune_pairs(args):
                             "stages": sw, "us": round(us, 2), "auto_us": round(pol, 2),
                             "shape": label + " bwd pair"})
     src = args.merge or TUNING_FILE
-    old = []
+    table = {}
     if os.path.exists(src):
         with open(src) as f:
-            old = json.load(f)["entries"]
+            table = json.load(f)  # other sections (tap-reuse tables) are kept as they are
+    old = table.get("entries", [])
     have = {(e["mode"], e["M"], e["N"], e["K"]) for e in entries}
     entries = [e for e in old if (e["mode"], e["M"], e["N"], e["K"]) not in have] + entries
     out = args.out or TUNING_FILE
+    table.update({"device": torch.cuda.get_device_name(0), "reps": args.reps, "entries": entries})
     with open(out, "w") as f:
-        json.dump({"device": torch.cuda.get_device_name(0), "reps": args.reps,
-                   "entries": entries}, f, indent=1)
+        json.dump(table, f, indent=1)
     print(f"wrote {len(entries)} entries to {out}; pair saving vs policy {saved:.1f} us")
 
 
