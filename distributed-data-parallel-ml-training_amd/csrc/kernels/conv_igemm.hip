@@ -997,8 +997,12 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
 
 // 2 waves per SIMD (<= 256 VGPR + AGPR per lane): left to itself the compiler gives the big
 // tiles 256 VGPRs + ~100 AGPRs (1 wave per SIMD), and these GEMMs are latency-bound
+// (-DDDP_CONV_WAVES_PER_EU=1 builds the unconstrained variant for A/B runs)
+#ifndef DDP_CONV_WAVES_PER_EU
+#define DDP_CONV_WAVES_PER_EU 2
+#endif
 template <int MODE, int BM, int BN, int NST, int BNF = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DDP_CONV_WAVES_PER_EU)))
 void conv_igemm_kernel(ConvArgs args) {
   // dynamic: the launcher sizes the ring to the stages a work item can use (launch_gemm_t)
   extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
