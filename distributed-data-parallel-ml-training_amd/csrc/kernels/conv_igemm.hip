@@ -60,6 +60,12 @@ struct FastDiv {
 __device__ __forceinline__ int fast_div(int x, FastDiv d) {
   return (int)((__umulhi((unsigned)x, d.mul) + (unsigned)x) >> d.sh);
 }
+// zero n16 16-byte chunks (the strided dgrad's untouched phases; see conv_dgrad_impl)
+__global__ __launch_bounds__(256) void zero16_kernel(uint4* __restrict__ p, size_t n16) {
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256)
+    p[i] = (uint4){0u, 0u, 0u, 0u};
+}
+
 __device__ __forceinline__ void ld8f_conv(const float* p, float* v) {
   const float4 a = reinterpret_cast<const float4*>(p)[0];
   const float4 b = reinterpret_cast<const float4*>(p)[1];
@@ -2300,8 +2306,14 @@ static int conv_dgrad_impl(const ConvGeom* g, const void* dy, const void* wc, vo
       if ((r0 >= g->R || s0 >= g->S) && pa < g->H && pb < g->W) zero_fill = true;
     }
   if (zero_fill && !accumulate) {  // (accumulating: untouched phases keep their values)
-    const hipError_t e = hipMemsetAsync(dx, 0, (size_t)g->N * g->H * g->W * g->C * 2, st);
-    if (e != hipSuccess) return (int)e;
+    // a kernel, not hipMemsetAsync: captured into a hipGraph, the memset node was measured to
+    // leave dx unwritten before the phase GEMM / the second branch's accumulating dgrad read it
+    // (sporadic NaN gradients in replayed ResNet-50 steps, never in eager ones;
+    // tools/probes/resnet_graph_probe.py)
+    const size_t n16 = (size_t)g->N * g->H * g->W * g->C / 8;  // C % 8 == 0: 16-B chunks
+    const unsigned nb = (unsigned)std::min<size_t>((n16 + 255) / 256, 8192);
+    hipLaunchKernelGGL(zero16_kernel, dim3(std::max(1u, nb)), dim3(256), 0, st,
+                       reinterpret_cast<uint4*>(dx), n16);
   }
   for (int pa = 0; pa < sd; ++pa) {
     for (int pb = 0; pb < sd; ++pb) {

@@ -243,3 +243,35 @@ def test_resnet50_trajectory_tracks_fp32_reference(native_ext):
     # batch 32 on a fresh box: one early step at 3.1 %, mean 0.9 %, parameter cosine 0.9975)
     assert max(rel[:6]) < 0.05 and sum(rel) / len(rel) < 0.03 and max(rel) < 0.1, rel
     assert cos_p > 0.99, cos_p
+
+
+@pytest.mark.parametrize("batch", [64])
+def test_resnet50_graph_replay_matches_eager_steps(native_ext, batch):
+    """Replayed ResNet-50 training steps (hipGraph) at lr 0 give the eager steps' loss for the
+    same batch and leave every parameter finite. Regression: the strided 1x1 dgrad cleared its
+    untouched phases with hipMemsetAsync; captured, that node did not order before the readers,
+    and replays sporadically fed NaN gradients into stem..layer2 (tools/probes/resnet_graph_probe.py)."""
+    import ddp_amd
+    from ddp_amd.models import build
+    from ddp_amd.engine import CrossEntropyLoss
+    from ddp_amd.engine.step import TrainStep
+    from ddp_amd.optim import FusedSGD
+    from ddp_amd.data import SyntheticImageNet, DeviceLoader
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(ddp_amd.SEED)
+    loader = DeviceLoader(SyntheticImageNet(True, n=4 * batch), batch, dev, 1, 0, train=True, cpad=8)
+    model = build("resnet50").to(dev)
+    opt = FusedSGD(model.parameters(), lr=0.0, momentum=0.9, weight_decay=1e-4)
+    step = TrainStep(model, opt, CrossEntropyLoss(), loader, use_graph=True)
+    eager = []
+    for _ in range(4):  # one pass over the 4 batches of the dataset
+        step.warmup(1)
+        eager.append(step.pop_loss())
+    step.capture()
+    step.pop_loss()
+    for i in range(8):  # two more passes, replayed
+        step.step()
+        v = step.pop_loss()
+        assert v == v and abs(v - eager[i % 4]) < 2e-2 * abs(eager[i % 4]), (i, v, eager)
+    assert bool(torch.isfinite(opt.arena.data).all())
+    assert bool(torch.isfinite(opt.momentum_buffer).all())

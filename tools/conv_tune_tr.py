@@ -21,6 +21,8 @@ sys.path.insert(0, REPO)
 
 LAYERS = [(64, 128, 16), (128, 256, 8), (256, 256, 8), (256, 512, 4), (512, 512, 4),
           (512, 512, 2)]
+# ResNet-50's stride-1 3x3 convolutions (conv2 of every non-first bottleneck): (C, K, H)
+RESNET_LAYERS = [(64, 64, 56), (128, 128, 28), (256, 256, 14), (512, 512, 7)]
 CANDS = [(bm, bn, s, n) for bm in (64, 128) for bn in (64, 128) for s in (1, 2, 4, 8)
          for n in (3, 5, 8)]
 
@@ -113,6 +115,8 @@ def main():
                     help="sweep the backward-data kernel instead (tr_dgrad_entries)")
     ap.add_argument("--out", default=None,
                     help="write the merged table here instead of over ops/conv_tuning.json")
+    ap.add_argument("--model", default="vgg11", choices=["vgg11", "resnet50"],
+                    help="layer set of the forward sweep (resnet50: the stride-1 3x3 convs)")
     ap.add_argument("--margin", type=float, default=0.03,
                     help="keep the implicit-GEMM kernel unless tap-reuse is this much faster")
     a = ap.parse_args()
@@ -136,7 +140,7 @@ def main():
             print(f"wrote {len(entries)} backward-data entries to {a.out or path}")
         return
     for B in a.batch:
-        for C, K, H in LAYERS:
+        for C, K, H in (RESNET_LAYERS if a.model == "resnet50" else LAYERS):
             conv = torch.nn.Conv2d(C, K, 3, 1, 1).to(dev)
             conv.weight.data = conv.weight.data.contiguous(memory_format=torch.channels_last)
             spec = ConvBNActSpec(conv, None)
@@ -176,7 +180,7 @@ def main():
             ent = {"M": M, "K": K, "C": C, "H": H, "bm": best[1][0], "bn": best[1][1],
                    "splits": best[1][2], "stages": best[1][3], "us": round(best[0], 2),
                    "igemm_us": round(base, 2),
-                   "shape": f"vgg11 N{B} {C}->{K} {H}x{H}"}
+                   "shape": f"{a.model} N{B} {C}->{K} {H}x{H}"}
             entries.append(ent)
             print(json.dumps(dict(ent, candidates=res)), flush=True)
     if a.write:
