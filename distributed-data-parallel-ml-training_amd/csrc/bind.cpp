@@ -193,6 +193,27 @@ PYBIND11_MODULE(_native, m) {
     if (rc >= 2) check(rc - 2, "linear_dx_bn");
     return rc == 1;
   });
+  // the whole head backward (dx fused with the preceding block's BatchNorm backward + dW / db)
+  // in one launch; returns False when not served (nothing launched)
+  m.def("linear_head_bwd_bn", [](uintptr_t dl, uintptr_t W, uintptr_t x, int B, int F, int J,
+                                 uintptr_t g, py::tuple bn, py::tuple bna, uintptr_t dW,
+                                 uintptr_t db, uintptr_t st) {
+    ddp_amd::BnBwdFuse f{};
+    f.z = P<unsigned short>(bn[0].cast<uintptr_t>());
+    f.coef = P<float>(bn[1].cast<uintptr_t>());
+    f.sums = P<float>(bn[2].cast<uintptr_t>());
+    f.pool = bn[3].cast<int>();
+    f.relu = bn[4].cast<int>();
+    f.Hz = bn[5].cast<int>();
+    f.Wz = bn[6].cast<int>();
+    ddp_amd::BnBwdApply ap{};
+    bn_apply(bna, &ap);
+    const int rc = ddp_linear_head_bwd_bn(P<float>(dl), P<float>(W), P<void>(x), B, F, J,
+                                          P<float>(g), &f, &ap, P<float>(dW), P<float>(db), S(st));
+    if (rc < 0) check(rc, "linear_head_bwd_bn");
+    if (rc >= 2) check(rc - 2, "linear_head_bwd_bn");
+    return rc == 1;
+  });
   // direct MFMA conv for C = 8 input layers; returns False when the shape is not served
   m.def("conv_fwd_smallk", [](py::tuple g, uintptr_t x, uintptr_t wc, uintptr_t bias, uintptr_t y,
                               uintptr_t stats, uintptr_t st) {

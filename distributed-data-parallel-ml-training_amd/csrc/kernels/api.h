@@ -166,6 +166,9 @@ void ddp_conv_tr_set(int mode, int M, int K, int C, int H, int bm, int bn, int s
 int ddp_conv_tr_geometry(int BM, int N, int H, int W, int* out7);
 int ddp_linear_dx_bn(const float* dl, const float* W, int B, int F, int J, const float* gscale,
                      const ddp_amd::BnBwdFuse* bn, const ddp_amd::BnBwdApply* ba, hipStream_t st);
+int ddp_linear_head_bwd_bn(const float* dl, const float* W, const void* x, int B, int F, int J,
+                           const float* gscale, const ddp_amd::BnBwdFuse* bn,
+                           const ddp_amd::BnBwdApply* ba, float* dW, float* db, hipStream_t st);
 // row limit of the BN-fused split-K finishes (default 128 or DDP_AMD_BN_FUSE_MAX_ROWS)
 void ddp_conv_bn_fuse_rows(int rows);
 int ddp_conv_dgrad(const ddp_amd::ConvGeom* g, const void* dy, const void* wt, void* dx,

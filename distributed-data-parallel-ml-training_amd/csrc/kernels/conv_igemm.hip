@@ -40,6 +40,7 @@
 //     statistics of the rounded output (sum, sum of squares) — BN needs no separate stats pass.
 #include "common.h"
 #include "api.h"
+#include "linear_blocks.h"
 #include <algorithm>
 #include <map>
 #include <cstdlib>
@@ -1520,13 +1521,13 @@ __global__ __launch_bounds__(256) void splitk_finish_bnbwd_kernel(FinishArgs fa,
 // per-block BN backward as the small dgrad finishes. Replaces the head's dx pass and that
 // block's reduce + finalize + apply launches (linear_bwd then only computes dW / db).
 template <int RPT>
-__global__ __launch_bounds__(256) void linear_dx_bnbwd_kernel(const float* __restrict__ dl,
-                                                              const float* __restrict__ Wt, int B,
-                                                              int F, int J, const float* gscale,
-                                                              BnBwdFuse bn, BnBwdApply ba) {
+__device__ __forceinline__ void linear_dx_bnbwd_body(const float* __restrict__ dl,
+                                                     const float* __restrict__ Wt, int B, int F,
+                                                     int J, const float* gscale, BnBwdFuse bn,
+                                                     BnBwdApply ba, int bx) {
   __shared__ float wred[4][2][8];
   const int half = threadIdx.x >> 7, lane = threadIdx.x & 127;
-  const int c0 = blockIdx.x * 16 + half * 8;
+  const int c0 = bx * 16 + half * 8;
   const float g = gscale ? *gscale : 1.f;
   float w[16][8];
 #pragma unroll
@@ -1556,6 +1557,33 @@ __global__ __launch_bounds__(256) void linear_dx_bnbwd_kernel(const float* __res
     }
   }
   bnbwd_from_dx<RPT, true>(bn, ba, B, F, 1, 1, v, wred, half, lane, c0);
+}
+
+template <int RPT>
+__global__ __launch_bounds__(256) void linear_dx_bnbwd_kernel(const float* __restrict__ dl,
+                                                              const float* __restrict__ Wt, int B,
+                                                              int F, int J, const float* gscale,
+                                                              BnBwdFuse bn, BnBwdApply ba) {
+  linear_dx_bnbwd_body<RPT>(dl, Wt, B, F, J, gscale, bn, ba, blockIdx.x);
+}
+
+// The whole head backward in ONE launch: blocks [0, F/16) run the fused dx + BatchNorm backward
+// above, the rest the weight / bias gradient (linear_blocks.h linear_dw_block) — one dispatch
+// instead of two on the strong-scaling step's critical chain.
+template <int RPT>
+__global__ __launch_bounds__(256) void linear_head_bwd_kernel(const float* __restrict__ dl,
+                                                              const float* __restrict__ Wt,
+                                                              const unsigned short* __restrict__ x,
+                                                              int B, int F, int J,
+                                                              const float* gscale, BnBwdFuse bn,
+                                                              BnBwdApply ba, float* dW, float* db,
+                                                              int ndx, int nfx) {
+  if ((int)blockIdx.x < ndx) {
+    linear_dx_bnbwd_body<RPT>(dl, Wt, B, F, J, gscale, bn, ba, blockIdx.x);
+  } else {
+    const int t = blockIdx.x - ndx;
+    linear_dw_block(dl, x, B, F, J, gscale, dW, db, t % nfx, t / nfx);
+  }
 }
 
 // Split-K finish for WGRAD: dW[k][c][r][s] += sum_z slab[z][k][(r,s,c)].
@@ -2184,6 +2212,24 @@ extern "C" int ddp_conv_fwd(const ConvGeom* g, const void* x, const void* wc, co
 // 1: launched (dx NOT written; dz / dgamma / dbeta of the block before the head written),
 // 0: shape not served (caller runs linear_bwd with dx + that block's BN backward), < 0 invalid,
 // >= 2: HIP error (rc - 2)
+// dx fused with the BatchNorm backward AND dW / db in one launch; same return codes as
+// ddp_linear_dx_bn (0: not served — nothing was launched)
+extern "C" int ddp_linear_head_bwd_bn(const float* dl, const float* W, const void* x, int B,
+                                      int F, int J, const float* gscale, const BnBwdFuse* bn,
+                                      const BnBwdApply* ba, float* dW, float* db, hipStream_t st) {
+  if (!bn || !ba || !dl || !W || !x || !dW) return -1;
+  if (J < 1 || J > 16 || F % 16 || B < 1 || B > 512 || !bn->pool || bn->Hz != 2 || bn->Wz != 2)
+    return 0;
+  const int ndx = F / 16, nfx = (F + 63) / 64, nry = (B + kDwRows - 1) / kDwRows;
+  const dim3 grid(ndx + nfx * nry);
+  const unsigned short* xb = (const unsigned short*)x;
+  if (B <= 128) hipLaunchKernelGGL(linear_head_bwd_kernel<1>, grid, dim3(256), 0, st, dl, W, xb, B, F, J, gscale, *bn, *ba, dW, db, ndx, nfx);
+  else if (B <= 256) hipLaunchKernelGGL(linear_head_bwd_kernel<2>, grid, dim3(256), 0, st, dl, W, xb, B, F, J, gscale, *bn, *ba, dW, db, ndx, nfx);
+  else hipLaunchKernelGGL(linear_head_bwd_kernel<4>, grid, dim3(256), 0, st, dl, W, xb, B, F, J, gscale, *bn, *ba, dW, db, ndx, nfx);
+  const int e = (int)hipGetLastError();
+  return e ? 2 + e : 1;
+}
+
 extern "C" int ddp_linear_dx_bn(const float* dl, const float* W, int B, int F, int J,
                                 const float* gscale, const BnBwdFuse* bn, const BnBwdApply* ba,
                                 hipStream_t st) {

@@ -234,6 +234,8 @@ BN_FWD_FUSE = os.environ.get("DDP_AMD_BN_FWD_FUSE", "1") != "0"
 BN_BWD_APPLY_FUSE = os.environ.get("DDP_AMD_BN_BWD_APPLY_FUSE", "1") != "0"
 # ... and into the classifier head's dx (linear_dx_bnbwd_kernel; needs BN_BWD_APPLY_FUSE too)
 HEAD_BN_FUSE = os.environ.get("DDP_AMD_HEAD_BN_FUSE", "1") != "0"
+# ... with the head's dW / db in the same launch (=0: a separate linear_bwd launch)
+HEAD_ONE_LAUNCH = os.environ.get("DDP_AMD_HEAD_ONE_LAUNCH", "1") != "0"
 BN_BWD_FUSE_MAX_HW = int(os.environ.get("DDP_AMD_BN_BWD_FUSE_MAX_HW", "16"))
 # residual blocks (ResNet bn3): the forward stores the ReLU mask as bits and the backward reads
 # those instead of the residual tensor (two fewer full-tensor reads per block). Opt-in (=1):
@@ -571,14 +573,19 @@ class _LinearCEFn(torch.autograd.Function):
                 and _common.BN_BWD_FUSE and prev.pool and not prev.residual
                 and pz.shape[1] == 2 and pz.shape[2] == 2 and prev.K == F):
             dz_prev = torch.empty_like(pz)
-            done = native().linear_dx_bn(
-                ptr(dl), ptr(weight), B, F, J, ptr(g),
-                (ptr(pz), ptr(prev.coef), ptr(prev.sums), 1, int(prev.relu), 2, 2),
-                (ptr(dz_prev), ptr(ensure_grad(prev.bn.weight)), ptr(ensure_grad(prev.bn.bias))),
-                stream_handle())
+            bnf = (ptr(pz), ptr(prev.coef), ptr(prev.sums), 1, int(prev.relu), 2, 2)
+            bna = (ptr(dz_prev), ptr(ensure_grad(prev.bn.weight)), ptr(ensure_grad(prev.bn.bias)))
+            if HEAD_ONE_LAUNCH:
+                # dx + the block's whole BN backward + dW / db: one launch (linear_head_bwd_kernel)
+                done = native().linear_head_bwd_bn(ptr(dl), ptr(weight), ptr(x), B, F, J, ptr(g),
+                                                   bnf, bna, ptr(gw), ptr(gb), stream_handle())
+            else:
+                done = native().linear_dx_bn(ptr(dl), ptr(weight), B, F, J, ptr(g), bnf, bna,
+                                             stream_handle())
+                if done:
+                    native().linear_bwd(ptr(dl), ptr(x), ptr(weight), B, F, J, ptr(g), 0,
+                                        ptr(gw), ptr(gb), stream_handle())
             if done:  # dx never materialised: the block's backward takes dz_prev
-                native().linear_bwd(ptr(dl), ptr(x), ptr(weight), B, F, J, ptr(g), 0, ptr(gw),
-                                    ptr(gb), stream_handle())
                 prev.dz_fused = (dz_prev, pz)
                 grad_ready([weight, bias])
                 return torch.empty_like(x), None, None, None, None, None, None

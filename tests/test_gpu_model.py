@@ -304,7 +304,7 @@ def test_bn_fused_into_splitk_finishes_matches_unfused(native_ext):
     nat = native()
     taken = {"fwd": 0, "bwd": 0, "head": 0}
     orig = {k: getattr(nat, k) for k in ("conv_fwd_bn", "conv_bwd_pair", "conv_dgrad",
-                                         "linear_dx_bn", "conv_fwd_tr")}
+                                         "linear_head_bwd_bn", "conv_fwd_tr")}
 
     def spy(name, key, fused_value=None):
         def f(*args, **kw):
@@ -317,7 +317,7 @@ def test_bn_fused_into_splitk_finishes_matches_unfused(native_ext):
     nat.conv_fwd_tr = spy("conv_fwd_tr", "fwd", 2)
     nat.conv_bwd_pair = spy("conv_bwd_pair", "bwd")
     nat.conv_dgrad = spy("conv_dgrad", "bwd")
-    nat.linear_dx_bn = spy("linear_dx_bn", "head")
+    nat.linear_head_bwd_bn = spy("linear_head_bwd_bn", "head")
     losses, grads = [], []
     saved = (layers.BN_FWD_FUSE, layers.BN_BWD_APPLY_FUSE)
     try:
