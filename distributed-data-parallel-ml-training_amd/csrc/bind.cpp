@@ -385,6 +385,7 @@ PYBIND11_MODULE(_native, m) {
   });
   m.def("bn_bwd_local_set", [](long long max_loads) { ddp_bn_bwd_local_set(max_loads); });
   m.def("conv_epi_stage_set", [](int on) { ddp_conv_epi_stage_set(on); });
+  m.def("bn_bwd_local_wide_set", [](int on) { ddp_bn_bwd_local_wide_set(on); });
 
   m.def("linear_ce_fwd", [](uintptr_t x, uintptr_t W, uintptr_t b, uintptr_t labels, int B, int F,
                             int J, uintptr_t logits, uintptr_t dlogits, uintptr_t loss_sum,

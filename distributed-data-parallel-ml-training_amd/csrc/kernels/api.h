@@ -204,6 +204,7 @@ int ddp_conv_fwd_smallk(const ddp_amd::ConvGeom* g, const void* x, const void* w
                         const float* bias, void* y, float* stats, hipStream_t st);
 void ddp_conv_options(int wgrad_atomic, int persistent, int stages);
 void ddp_conv_epi_stage_set(int on);
+void ddp_bn_bwd_local_wide_set(int on);
 int ddp_bn_pool3_fwd(const ddp_amd::BnArgs* a, unsigned char* idx, hipStream_t st);
 int ddp_bn_pool3_bwd(const ddp_amd::BnArgs* a, const unsigned char* idx, hipStream_t st);
 void ddp_conv_pair_mode(int mode, int items);

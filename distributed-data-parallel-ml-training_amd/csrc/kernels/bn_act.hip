@@ -911,7 +911,41 @@ static void launch_bwd(const BnArgs& a, size_t npix, int Gb, int chunks, hipStre
 // 8 is best at b32..b128 (b32 0.416 -> 0.405 ms, b64 -1.2 %, b128 -0.9 %), neutral at b256.
 static int kLocalMaxLoads = 8;
 constexpr int kLocalThreads = 256;
+// Layers too big for 256 threads may still fit ONE 1024-thread block per channel group (4x the
+// threads, a quarter of the loads each; <= 2 items per thread keeps the kernel within the 128
+// VGPRs a 1024-thread block allows): e.g. the b32 step's 8x8x256 layer (2048 pixels) would drop
+// its reduce -> finalize -> apply chain. OFF by default (DDP_AMD_BN_BWD_LOCAL_WIDE=1 enables):
+// measured slower — b32 0.3997 -> 0.4056 ms, b64 0.477 -> 0.488, b256 0.876 -> 0.890 (same box;
+// profiles/r3_conv_occupancy.md): C/8 blocks of 1024 threads stream from too few CUs.
+static int kLocalWide = -1;
+static bool local_cfg_256(const BnArgs& a, int* ipt);
+static bool local_cfg_nt(const BnArgs& a, int* ipt, int* nt);
 static bool local_cfg(const BnArgs& a, int* ipt) {
+  int nt;
+  return local_cfg_nt(a, ipt, &nt) && nt == kLocalThreads;
+}
+static bool local_cfg_nt(const BnArgs& a, int* ipt, int* nt) {
+  if (kLocalWide < 0) {
+    const char* e = std::getenv("DDP_AMD_BN_BWD_LOCAL_WIDE");
+    kLocalWide = e ? std::atoi(e) : 0;
+  }
+  *nt = kLocalThreads;
+  int i256;
+  if (local_cfg_256(a, &i256)) { *ipt = i256; return true; }
+  if (!kLocalWide || kLocalMaxLoads == 0 || a.C % 8 || (a.pool && a.res)) return false;
+  const int Ho = a.pool ? a.H / 2 : a.H, Wo = a.pool ? a.W / 2 : a.W;
+  const size_t npix = (size_t)a.N * Ho * Wo;
+  const int per_item = 1 + (a.pool ? 4 : 1) + (a.res ? 1 : 0);
+  for (int i = 1; i <= (a.pool ? 1 : 2); i *= 2) {
+    if ((size_t)1024 * i < npix) continue;
+    if (i * per_item > kLocalMaxLoads) return false;
+    *ipt = i;
+    *nt = 1024;
+    return true;
+  }
+  return false;
+}
+static bool local_cfg_256(const BnArgs& a, int* ipt) {
   static const bool init = [] {
     if (const char* e = std::getenv("DDP_AMD_BN_BWD_LOCAL_LOADS")) kLocalMaxLoads = std::max(0, std::atoi(e));
     return true;
@@ -932,8 +966,13 @@ static bool local_cfg(const BnArgs& a, int* ipt) {
 }
 
 template <bool POOL>
-static void launch_local(const BnArgs& a, int ipt, hipStream_t st) {
+static void launch_local(const BnArgs& a, int ipt, hipStream_t st, int nt = kLocalThreads) {
   const dim3 grid(a.C / 8), block(kLocalThreads);
+  if (nt == 1024) {
+    if (ipt == 1) hipLaunchKernelGGL((bn_act_bwd_local_kernel<POOL, 1, 1024>), grid, dim3(1024), 0, st, a);
+    else if constexpr (!POOL) hipLaunchKernelGGL((bn_act_bwd_local_kernel<POOL, 2, 1024>), grid, dim3(1024), 0, st, a);
+    return;
+  }
   if (ipt == 1) hipLaunchKernelGGL((bn_act_bwd_local_kernel<POOL, 1, kLocalThreads>), grid, block, 0, st, a);
   else if (ipt == 2) hipLaunchKernelGGL((bn_act_bwd_local_kernel<POOL, 2, kLocalThreads>), grid, block, 0, st, a);
   else if (ipt == 4) hipLaunchKernelGGL((bn_act_bwd_local_kernel<POOL, 4, kLocalThreads>), grid, block, 0, st, a);
@@ -948,11 +987,13 @@ extern "C" void ddp_bn_bwd_local_set(long long max_loads) {
   kLocalMaxLoads = (int)std::max(0LL, max_loads);
 }
 
+extern "C" void ddp_bn_bwd_local_wide_set(int on) { kLocalWide = on ? 1 : 0; }
+
 extern "C" int ddp_bn_bwd_local_ok(int N, int H, int W, int C, int pool) {
   BnArgs a{};
   a.N = N; a.H = H; a.W = W; a.C = C; a.pool = pool;
-  int ipt;
-  return local_cfg(a, &ipt) ? 1 : 0;
+  int ipt, nt;
+  return local_cfg_nt(a, &ipt, &nt) ? 1 : 0;
 }
 
 // Clustered one-launch backward (bn_act_bwd_cluster_kernel) for layers too big for the local
@@ -1014,10 +1055,10 @@ extern "C" int ddp_bn_act_bwd(const BnArgs* args, hipStream_t st) {
   {
     // small layer: the whole backward in one launch (any sums the next layer's dgrad
     // accumulated are simply not needed)
-    int ipt;
-    if (local_cfg(a, &ipt)) {
-      if (a.pool) launch_local<true>(a, ipt, st);
-      else launch_local<false>(a, ipt, st);
+    int ipt, nt;
+    if (local_cfg_nt(a, &ipt, &nt)) {
+      if (a.pool) launch_local<true>(a, ipt, st, nt);
+      else launch_local<false>(a, ipt, st, nt);
       return (int)hipGetLastError();
     }
     int K, P;

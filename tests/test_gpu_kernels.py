@@ -688,3 +688,20 @@ def test_bn_relu_mask_replaces_residual(native_ext, N, C, H, local):
     assert torch.equal(res[0][0], res[1][0]) if exact else rel_err(res[1][0], res[0][0]) < 1e-3
     assert torch.allclose(res[0][2], res[1][2], rtol=1e-5, atol=1e-5)
     assert torch.allclose(res[0][3], res[1][3], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("N,C,H,pool,res", [(32, 256, 8, False, False), (16, 128, 16, True, False),
+                                            (16, 256, 8, False, True)])
+def test_bn_act_bwd_wide_local(native_ext, N, C, H, pool, res):
+    """One-launch BatchNorm backward with ONE 1024-thread block per 8 channels (bn_act.hip
+    local_cfg_nt: layers past the 256-thread block's load limit, e.g. the b32 step's 8x8x256
+    layer) against fp32 PyTorch, at the shipped load limit."""
+    from ddp_amd.ops.common import ptr, stream_handle
+    nat = native_ext
+    nat.bn_bwd_local_set(8)
+    nat.bn_bwd_local_wide_set(1)  # opt-in (measured slower end to end)
+    try:
+        assert nat.bn_bwd_local_ok(N, H, H, C, int(pool))
+        _bn_case(nat, N, C, H, pool, res, False, ptr, stream_handle)
+    finally:
+        nat.bn_bwd_local_wide_set(0)
