@@ -119,7 +119,11 @@ struct Args {
 };
 
 template <int BM, int BN, int NST, int NL, int IN>
-__global__ __launch_bounds__(256) void conv_tr_fwd_kernel(Args a) {
+#ifndef DDP_TR_WAVES_PER_EU
+#define DDP_TR_WAVES_PER_EU 1  // (A/B knob: -DDDP_TR_WAVES_PER_EU=3 asks for 3 waves per SIMD)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DDP_TR_WAVES_PER_EU)))
+void conv_tr_fwd_kernel(Args a) {
   constexpr int WTM = BM / 2, WTN = BN / 2, TM = WTM / 16, TN = WTN / 16;
   constexpr int CB = BN * 64 / 8 / 256;  // B DMA instructions per thread per k-step
   constexpr int BTILE = BN * 64;         // bf16 elements per B stage
