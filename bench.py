@@ -164,6 +164,10 @@ def main():
     # on the comm stream while the earlier layers' backward runs (one-GPU study with an
     # 8-GPU-sized stand-in collective: profiles/r2_pipelined_ddp.md); one GPU has no collective
     # to hide -> one graph.
+    # On > 1 GPUs without --segmented / DDP_AMD_SEGMENTED the cuts are chosen on the node below
+    # (parallel/cut_plan.py: measured stage backward times x the start-up all-reduce probe)
+    cut_source = "cli" if args.segmented is not None else (
+        "env" if "DDP_AMD_SEGMENTED" in os.environ else "default")
     if args.segmented is None:
         args.segmented = os.environ.get("DDP_AMD_SEGMENTED",
                                         default_cuts(args.model, B) if world > 1 else "0")
@@ -188,6 +192,15 @@ def main():
         sync = lambda m: fn(m, comm)  # noqa: E731
     lr = args.lr if args.lr is not None else (0.01 if resnet else 0.1)
     opt = FusedSGD(model.parameters(), lr=lr, momentum=0.9, weight_decay=1e-4)
+    cut_plan = None
+    if (segmented and cut_source == "default" and world > 1
+            and os.environ.get("DDP_AMD_CUT_PLAN", "1") != "0"):
+        cut_plan = choose_cuts_on_node(model, opt, criterion, loader, args, world, comm_table)
+        beat()
+        if cut_plan.get("cuts"):
+            cuts = cut_plan["cuts"]
+            args.segmented = ",".join(str(c) for c in cuts)
+            cut_source = cut_plan["source"]
     if segmented:
         step = SegmentedDDPStep(model, opt, criterion, loader, split=cuts,
                                 emulate=int(os.environ.get("DDP_AMD_EMULATE_COMM", "0")),
@@ -263,6 +276,9 @@ def main():
     if world > 1:
         consistent = check_replicas(arena, world)
     plan = comm_plan(args, world, step, model, cuts, segmented, comm_table)
+    plan["cut_source"] = cut_source if segmented else None
+    if cut_plan is not None:
+        plan["cut_plan"] = cut_plan
     ms = elapsed / args.steps * 1000.0
     value = global_batch * args.steps / elapsed
     out = {
@@ -316,6 +332,49 @@ def main():
         watchdog.stop()
     if world > 1:
         dist.destroy_process_group()
+
+
+def choose_cuts_on_node(model, opt, criterion, loader, args, world, comm_table):
+    """Pipelined-step cuts from THIS node's measurements (parallel/cut_plan.py): every fused
+    stage's backward time at this per-GPU batch (device events on a cut-everywhere step,
+    engine/step.py profile_stage_times; state rolled back) and the all-reduce curve of the
+    start-up probe (or comm_tuning.json). The stage times are maxed over ranks so every rank
+    picks the same cuts. Any failure keeps the fallback cuts and says why."""
+    import torch
+    import torch.distributed as dist
+    from ddp_amd.engine.step import profile_stage_times
+    from ddp_amd.parallel.bucket_plan import load_table, rows_for
+    from ddp_amd.parallel.cut_plan import plan_cuts
+    inner = model.module
+    n = inner.n_stages()
+    arena = model.arena
+    pidx = {id(p): i for i, p in enumerate(arena.params)}
+    first = [pidx[id(inner.first_param_of_stage(i))] for i in range(n)] + [len(arena.params)]
+    off = list(arena.offsets) + [arena.total]
+    pbytes = [4 * (off[first[i + 1]] - off[first[i]]) for i in range(n)]
+    ok = 1
+    try:
+        stage_us = profile_stage_times(model, opt, criterion, loader, n)
+    except Exception as e:  # keep the fallback cuts, loudly (on every rank: see below)
+        print(f"[bench] stage profiling failed ({e!r}); fallback cuts", file=sys.stderr)
+        ok, stage_us = 0, [0.0] * n
+    # collective decision: every rank takes part in both reductions whatever happened locally
+    flag = torch.tensor([ok], dtype=torch.int64)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    t = torch.tensor(stage_us, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if int(flag.item()) == 0:
+        return {"source": "fallback (stage profiling failed on a rank)", "cuts": None}
+    stage_us = [float(v) for v in t]
+    rows, table_src = rows_for(comm_table or load_table(), world, args.grad_comm)
+    wire = 0.5 if args.grad_comm == "bf16" else 1.0
+    best, ranked = plan_cuts(stage_us, pbytes, rows, wire_scale=wire)
+    return {"source": "probe" if comm_table is not None else "table", "comm_table": table_src,
+            "cuts": best["cuts"], "stage_us": [round(v, 1) for v in stage_us],
+            "stage_param_bytes": pbytes, "bucket_bytes": best["bucket_bytes"],
+            "predicted_allreduce_us": [round(v, 1) for v in best["allreduce_us"]],
+            "predicted_step_us": round(best["step_us"], 1),
+            "predicted_exposed_us": round(best["exposed_us"], 1), "top5": ranked[:5]}
 
 
 def native_version():

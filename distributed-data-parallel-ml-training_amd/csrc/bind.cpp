@@ -52,6 +52,32 @@ struct StreamLink {
   void wait(uintptr_t s) { check((int)hipStreamWaitEvent(S(s), ev, 0), "hipStreamWaitEvent"); }
 };
 
+// (z, coef, sums, pool, relu, Hz, Wz) -> BnBwdFuse (None -> nullptr)
+static const ddp_amd::BnBwdFuse* bn_fuse(py::object o, ddp_amd::BnBwdFuse* f) {
+  if (o.is_none()) return nullptr;
+  auto t = o.cast<py::tuple>();
+  f->z = P<unsigned short>(t[0].cast<uintptr_t>());
+  f->coef = P<float>(t[1].cast<uintptr_t>());
+  f->sums = P<float>(t[2].cast<uintptr_t>());
+  f->pool = t[3].cast<int>();
+  f->relu = t[4].cast<int>();
+  f->Hz = t[5].cast<int>();
+  f->Wz = t[6].cast<int>();
+  return f;
+}
+
+// (z, g, coef, C[, mask]) -> BnBwdXf (None -> nullptr)
+static const ddp_amd::BnBwdXf* xf_args(py::object o, ddp_amd::BnBwdXf* x) {
+  if (o.is_none()) return nullptr;
+  auto t = o.cast<py::tuple>();
+  x->z = P<void>(t[0].cast<uintptr_t>());
+  x->g = P<void>(t[1].cast<uintptr_t>());
+  x->coef = P<float>(t[2].cast<uintptr_t>());
+  x->C = t[3].cast<int>();
+  x->mask = t.size() > 4 ? t[4].cast<int>() : 0;
+  return x;
+}
+
 // (dz, dgamma, dbeta) -> BnBwdApply (None -> nullptr)
 static const ddp_amd::BnBwdApply* bn_apply(py::object o, ddp_amd::BnBwdApply* out) {
   if (o.is_none()) return nullptr;
@@ -227,10 +253,29 @@ PYBIND11_MODULE(_native, m) {
   // block whose BatchNorm-backward sums the dgrad epilogue accumulates (api.h BnBwdFuse)
   // bna: optional (dz, dgamma, dbeta) — complete that block's BN backward in the split-K finish
   // when possible (api.h BnBwdApply); returns True when it did (dx is then NOT written)
+  // xf: optional (z, g, coef, C) — the BatchNorm-backward apply computed on the A operand of
+  // the backward GEMMs (api.h BnBwdXf; dy is then ignored: the operand is dz = A g + B z + C)
+  m.def("conv_xf_ok", [](py::tuple g, int need_dx) {
+    auto c = geom(g);
+    return ddp_conv_xf_ok(&c, need_dx) != 0;
+  });
   m.def("conv_dgrad", [](py::tuple g, uintptr_t dy, uintptr_t wt, uintptr_t dx, uintptr_t ws,
                          size_t ws_elems, int splits, uintptr_t st, int accumulate, py::object bn,
-                         py::object bna) {
+                         py::object bna, py::object xf) {
     auto c = geom(g);
+    ddp_amd::BnBwdXf xv{};
+    const ddp_amd::BnBwdXf* xp = xf_args(xf, &xv);
+    if (xp) {
+      ddp_amd::BnBwdFuse f{};
+      const ddp_amd::BnBwdFuse* fp = bn_fuse(bn, &f);
+      ddp_amd::BnBwdApply ap{};
+      const ddp_amd::BnBwdApply* app = fp ? bn_apply(bna, &ap) : nullptr;
+      int done = 0;
+      if (accumulate) check(-4, "conv_dgrad (xf cannot accumulate)");
+      check(ddp_conv_dgrad_xf(&c, P<void>(wt), P<void>(dx), P<float>(ws), ws_elems, fp, app,
+                              &done, xp, S(st)), "conv_dgrad_xf");
+      return done == 1;
+    }
     if (bn.is_none()) {
       check(ddp_conv_dgrad(&c, P<void>(dy), P<void>(wt), P<void>(dx), P<float>(ws), ws_elems,
                            splits, accumulate, S(st)), "conv_dgrad");
@@ -253,12 +298,14 @@ PYBIND11_MODULE(_native, m) {
     return done == 1;
   }, py::arg("g"), py::arg("dy"), py::arg("wt"), py::arg("dx"), py::arg("ws"),
      py::arg("ws_elems"), py::arg("splits"), py::arg("stream"), py::arg("accumulate") = 0,
-     py::arg("bn") = py::none(), py::arg("bna") = py::none());
+     py::arg("bn") = py::none(), py::arg("bna") = py::none(), py::arg("xf") = py::none());
   // one layer's backward: WGRAD (dw += ...) and stride-1 DGRAD (dx = ..., optional BN-backward
   // sums) as one grouped launch when the policy allows (ddp_conv_bwd_pair), else two
   m.def("conv_bwd_pair", [](py::tuple g, uintptr_t dy, uintptr_t wc, uintptr_t dx, uintptr_t x,
                             uintptr_t dw, uintptr_t ws, size_t ws_elems, uintptr_t st,
-                            py::object bn, py::object bna) {
+                            py::object bn, py::object bna, py::object xf) {
+    ddp_amd::BnBwdXf xv{};
+    const ddp_amd::BnBwdXf* xp = xf_args(xf, &xv);
     auto c = geom(g);
     ddp_amd::BnBwdApply ap{};
     const ddp_amd::BnBwdApply* app = bn_apply(bna, &ap);
@@ -277,30 +324,31 @@ PYBIND11_MODULE(_native, m) {
       fp = &f;
     }
     check(ddp_conv_bwd_pair(&c, P<void>(dy), P<void>(wc), P<void>(dx), P<void>(x), P<float>(dw),
-                            P<float>(ws), ws_elems, fp, app, &done, S(st)), "conv_bwd_pair");
+                            P<float>(ws), ws_elems, fp, app, &done, S(st), xp), "conv_bwd_pair");
     return done == 1;
   }, py::arg("g"), py::arg("dy"), py::arg("wc"), py::arg("dx"), py::arg("x"), py::arg("dw"),
      py::arg("ws"), py::arg("ws_elems"), py::arg("stream"), py::arg("bn") = py::none(),
-     py::arg("bna") = py::none());
+     py::arg("bna") = py::none(), py::arg("xf") = py::none());
   m.def("conv_pair_mode", [](int mode, int items) { ddp_conv_pair_mode(mode, items); },
         py::arg("mode"), py::arg("items") = 0);
   m.def("conv_pair_force", [](int sd, int sw) { ddp_conv_pair_force(sd, sw); },
         py::arg("splits_dg"), py::arg("splits_wg"));
   m.def("conv_wgrad", [](py::tuple g, uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws,
-                         size_t ws_elems, int splits, uintptr_t st) {
+                         size_t ws_elems, int splits, uintptr_t st, py::object xf) {
     auto c = geom(g);
-    check(ddp_conv_wgrad(&c, P<void>(dy), P<void>(x), P<float>(dw), P<float>(ws), ws_elems,
-                         splits, S(st)), "conv_wgrad");
-  });
+    ddp_amd::BnBwdXf xv{};
+    const ddp_amd::BnBwdXf* xp = xf_args(xf, &xv);
+    check(ddp_conv_wgrad_xf(&c, P<void>(dy), P<void>(x), P<float>(dw), P<float>(ws), ws_elems,
+                            splits, xp, S(st)), "conv_wgrad");
+  }, py::arg("g"), py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("ws"), py::arg("ws_elems"),
+     py::arg("splits"), py::arg("stream"), py::arg("xf") = py::none());
 
   m.def("bn_act_fwd", [](int N, int H, int W, int C, int pool, int relu, float eps, uintptr_t z,
                          uintptr_t res, uintptr_t stats, uintptr_t gamma, uintptr_t beta,
                          uintptr_t out, uintptr_t st, uintptr_t running_mean,
-                         uintptr_t running_var, float momentum, int use_running, uintptr_t coef,
-                         uintptr_t rmask) {
+                         uintptr_t running_var, float momentum, int use_running, uintptr_t coef) {
     ddp_amd::BnArgs a{};
     a.coef = P<float>(coef);
-    a.rmask = P<unsigned char>(rmask);
     a.N = N; a.H = H; a.W = W; a.C = C; a.pool = pool; a.relu = relu; a.eps = eps;
     a.z = P<unsigned short>(z); a.res = P<unsigned short>(res); a.stats = P<float>(stats);
     a.gamma = P<float>(gamma); a.beta = P<float>(beta); a.out = P<unsigned short>(out);
@@ -311,7 +359,7 @@ PYBIND11_MODULE(_native, m) {
      py::arg("eps"), py::arg("z"), py::arg("res"), py::arg("stats"), py::arg("gamma"),
      py::arg("beta"), py::arg("out"), py::arg("stream"), py::arg("running_mean") = 0,
      py::arg("running_var") = 0, py::arg("momentum") = 0.1f, py::arg("use_running") = 0,
-     py::arg("coef") = 0, py::arg("rmask") = 0);
+     py::arg("coef") = 0);
   m.def("maxpool_fwd", [](uintptr_t x, int N, int H, int W, int C, int KH, int KW, int stride,
                           int pad, int Ho, int Wo, uintptr_t y, uintptr_t idx, uintptr_t st) {
     check(ddp_maxpool_fwd(P<void>(x), N, H, W, C, KH, KW, stride, pad, Ho, Wo, P<void>(y),
@@ -335,14 +383,10 @@ PYBIND11_MODULE(_native, m) {
                          uintptr_t res, uintptr_t stats, uintptr_t gamma, uintptr_t beta,
                          uintptr_t dout, uintptr_t sums, uintptr_t dz, uintptr_t dres,
                          uintptr_t dgamma, uintptr_t dbeta, uintptr_t dbias, uintptr_t st,
-                         uintptr_t coef, uintptr_t counter, int sums_ready, uintptr_t grid_sync,
-                         uintptr_t rmask) {
+                         uintptr_t coef, int sums_ready) {
     ddp_amd::BnArgs a{};
-    a.rmask = P<unsigned char>(rmask);
     a.coef = P<float>(coef);
-    a.counter = P<int>(counter);
     a.sums_ready = sums_ready;
-    a.grid_sync = P<int>(grid_sync);
     a.N = N; a.H = H; a.W = W; a.C = C; a.pool = pool; a.relu = relu; a.eps = eps;
     a.z = P<unsigned short>(z); a.res = P<unsigned short>(res); a.stats = P<float>(stats);
     a.gamma = P<float>(gamma); a.beta = P<float>(beta); a.dout = P<unsigned short>(dout);
@@ -353,8 +397,23 @@ PYBIND11_MODULE(_native, m) {
      py::arg("eps"), py::arg("z"), py::arg("res"), py::arg("stats"), py::arg("gamma"),
      py::arg("beta"), py::arg("dout"), py::arg("sums"), py::arg("dz"), py::arg("dres"),
      py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("stream"), py::arg("coef"),
-     py::arg("counter") = 0, py::arg("sums_ready") = 0, py::arg("grid_sync") = 0,
-     py::arg("rmask") = 0);
+     py::arg("sums_ready") = 0);
+  // BatchNorm backward without its apply pass: reduce (+ dy_bn stored to dyb) + finalize into
+  // xcoef; the conv backward then takes xf = (z, dyb, xcoef, C) (bn_act.hip ddp_bn_bwd_xf)
+  m.def("bn_bwd_xf_ok", [](int N, int H, int W, int C, int pool, int res, int sums_ready) {
+    return ddp_bn_bwd_xf_ok(N, H, W, C, pool, res, sums_ready) != 0;
+  });
+  m.def("bn_bwd_xf", [](int N, int H, int W, int C, int pool, int relu, float eps, uintptr_t z,
+                        uintptr_t res, uintptr_t dout, uintptr_t sums, uintptr_t dyb,
+                        uintptr_t xcoef, uintptr_t dgamma, uintptr_t dbeta, uintptr_t coef,
+                        uintptr_t st) {
+    ddp_amd::BnArgs a{};
+    a.N = N; a.H = H; a.W = W; a.C = C; a.pool = pool; a.relu = relu; a.eps = eps;
+    a.z = P<unsigned short>(z); a.res = P<unsigned short>(res); a.dout = P<unsigned short>(dout);
+    a.sums = P<float>(sums); a.dyb = P<unsigned short>(dyb); a.xcoef = P<float>(xcoef);
+    a.dgamma = P<float>(dgamma); a.dbeta = P<float>(dbeta); a.coef = P<float>(coef);
+    check(ddp_bn_bwd_xf(&a, S(st)), "bn_bwd_xf");
+  });
   // ResNet stem: BN + ReLU + MaxPool2d(3, 2, 1) in one pass each way (bn_act.hip bn_pool3_*):
   // (N, H, W) = conv output, out / dout pooled, idx = uint8 window argmax (pooled shape)
   m.def("bn_pool3_fwd", [](int N, int H, int W, int C, int relu, float eps, uintptr_t z,
@@ -379,13 +438,11 @@ PYBIND11_MODULE(_native, m) {
     a.coef = P<float>(coef);
     check(ddp_bn_pool3_bwd(&a, P<unsigned char>(idx), S(st)), "bn_pool3_bwd");
   });
-  m.def("bn_bwd_cluster_set", [](int mode) { ddp_bn_bwd_cluster_set(mode); });
   m.def("bn_bwd_local_ok", [](int N, int H, int W, int C, int pool) {
     return ddp_bn_bwd_local_ok(N, H, W, C, pool) != 0;
   });
   m.def("bn_bwd_local_set", [](long long max_loads) { ddp_bn_bwd_local_set(max_loads); });
   m.def("conv_epi_stage_set", [](int on) { ddp_conv_epi_stage_set(on); });
-  m.def("bn_bwd_local_wide_set", [](int on) { ddp_bn_bwd_local_wide_set(on); });
 
   m.def("linear_ce_fwd", [](uintptr_t x, uintptr_t W, uintptr_t b, uintptr_t labels, int B, int F,
                             int J, uintptr_t logits, uintptr_t dlogits, uintptr_t loss_sum,
@@ -414,13 +471,9 @@ PYBIND11_MODULE(_native, m) {
     check(ddp_sgd(P<float>(p), P<float>(g), P<float>(buf), n, lr, momentum, wd, grad_scale,
                   nesterov, S(st)), "sgd");
   });
-  m.def("conv_fixup", [](uintptr_t facc, size_t n, uintptr_t tickets, size_t nt, int mode,
-                         size_t max_bytes) {
-    ddp_conv_fixup(P<float>(facc), n, P<unsigned>(tickets), nt, mode, max_bytes);
-  });
-  m.def("conv_options", [](int wgrad_atomic, int persistent, int stages) {
-    ddp_conv_options(wgrad_atomic, persistent, stages);
-  }, py::arg("wgrad_atomic") = 0, py::arg("persistent") = 0, py::arg("stages") = 2);
+  m.def("conv_options", [](int persistent, int stages) {
+    ddp_conv_options(persistent, stages);
+  }, py::arg("persistent") = 0, py::arg("stages") = 2);
   // measured tile/split table (mode 0 fwd, 1 dgrad, 2 wgrad; GEMM dims M, N, K; tile 0..3 =
   // 128x128, 128x64, 64x128, 64x64) and the forced-tile switch used by tools/conv_tune.py
   m.def("conv_tune_set", [](int mode, int M, int N, int K, int tile, int splits, int stages) {
@@ -586,6 +639,7 @@ PYBIND11_MODULE(_native, m) {
       .def("recv", [](RcclComm& c, uintptr_t b, size_t n, int dt, int peer, uintptr_t st) {
         c.recv(P<void>(b), n, dt, peer, S(st));
       })
+      .def("reserve_stage", &RcclComm::reserve_stage)
       .def("async_error", &RcclComm::async_error)
       .def("abort", &RcclComm::abort);
 

@@ -44,15 +44,12 @@ struct BnArgs {
   int use_running;              // eval with running statistics instead of batch statistics
   float* coef;                  // [6][C] scale, shift, mean, invstd (fwd) and k1, k2 (bwd); the
                                 // backward reads the table its forward wrote
-  int* counter;                 // backward: zeroed ticket counter -> the reduce kernel's last
-                                // block finalizes k1/k2, dgamma, dbeta (no finalize launch)
   int sums_ready;               // backward: sums already accumulated (BnBwdFuse in the next
                                 // layer's dgrad) -> finalize + apply only
-  int* grid_sync;               // backward: zeroed arrival counter of the one-launch clustered
-                                // backward (bn_act_bwd_cluster_kernel); null = not available
-  unsigned char* rmask;         // optional, no pool: ReLU mask bits (y > 0), one byte per 8
-                                // channels — written by the forward, read by the backward
-                                // instead of re-reading the residual (ResNet bn3)
+  unsigned short* dyb;          // backward without apply (ddp_bn_bwd_xf): dy_bn, the routed /
+                                // masked gradient at the BN output (z's shape; = d residual)
+  float* xcoef;                 // ... and the [C/8][3|5][8] table of dz = A dy_bn + B z + C
+                                // (+ scale, shift when the consumer masks: dyb == nullptr)
 };
 
 // BatchNorm-backward statistics fused into a conv dgrad: the dgrad output IS the gradient at the
@@ -105,6 +102,18 @@ struct TrFwdIn {
   int relu, pool;
   float* coef;              // [6][C] coefficient table written for its backward
   unsigned short* y;        // materialised conv input [N][H][W][C] (the wgrad operand)
+};
+
+// BatchNorm-backward apply fused into the A-operand staging of the producing conv's backward
+// GEMMs (conv_igemm.hip XF): dz = A[c] * g + B[c] * z + C[c] is computed in LDS; dz never exists.
+struct BnBwdXf {
+  const void* z;        // the conv output the BatchNorm normalised [N][P][Q][C] (bf16)
+  const void* g;        // mask = 0: gradient at the BN output after ReLU mask / pool routing
+                        // (dy_bn); mask = 1 (no pool, no residual): the raw gradient at the
+                        // block output — the consumer applies the ReLU mask itself
+  const float* coef;    // [C/8][3 or 5][8]: A | B | C (| scale | shift) of 8 channels
+  int C;
+  int mask;
 };
 
 struct PackDesc {
@@ -178,18 +187,25 @@ int ddp_conv_dgrad(const ddp_amd::ConvGeom* g, const void* dy, const void* wt, v
 int ddp_conv_dgrad_bn(const ddp_amd::ConvGeom* g, const void* dy, const void* wt, void* dx,
                       float* ws, size_t ws_elems, int splits, const ddp_amd::BnBwdFuse* bn,
                       const ddp_amd::BnBwdApply* ba, int* bn_done, hipStream_t st);
+int ddp_conv_xf_ok(const ddp_amd::ConvGeom* g, int need_dx);
+int ddp_conv_dgrad_xf(const ddp_amd::ConvGeom* g, const void* wc, void* dx, float* ws,
+                      size_t ws_elems, const ddp_amd::BnBwdFuse* bn, const ddp_amd::BnBwdApply* ba,
+                      int* bn_done, const ddp_amd::BnBwdXf* xf, hipStream_t st);
+int ddp_conv_wgrad_xf(const ddp_amd::ConvGeom* g, const void* dy, const void* x, float* dw,
+                      float* ws, size_t ws_elems, int splits, const ddp_amd::BnBwdXf* xf,
+                      hipStream_t st);
 int ddp_conv_wgrad(const ddp_amd::ConvGeom* g, const void* dy, const void* x, float* dw,
                    float* ws, size_t ws_elems, int splits, hipStream_t st);
 int ddp_bn_act_fwd(const ddp_amd::BnArgs* a, hipStream_t st);
 int ddp_bn_act_bwd(const ddp_amd::BnArgs* a, hipStream_t st);
+int ddp_bn_bwd_xf_ok(int N, int H, int W, int C, int pool, int res, int sums_ready);
+int ddp_bn_bwd_xf(const ddp_amd::BnArgs* a, hipStream_t st);
 // small layers: the whole BatchNorm backward in one launch, one block per 8 channels
 // (bn_act_bwd_local_kernel); ok = this layer takes that path; set = its loads-per-thread
 // limit (0 = off)
 int ddp_bn_bwd_local_ok(int N, int H, int W, int C, int pool);
 void ddp_bn_bwd_local_set(long long max_loads);
 // mid-size layers: the same in one launch over up to kStatRep blocks per 64 channels that meet at
-// a bounded grid-wide counter (bn_act_bwd_cluster_kernel; needs BnArgs::grid_sync); 0 = off
-void ddp_bn_bwd_cluster_set(int mode);
 int ddp_linear_ce_fwd(const void* x, const float* W, const float* b, const long long* labels,
                       int B, int F, int J, float* logits, float* dlogits, float* loss_sum,
                       int* correct, float* loss_acc, hipStream_t st);
@@ -202,9 +218,8 @@ int ddp_sgd(float* p, const float* g, float* buf, size_t n, float lr, float mome
             float grad_scale, int nesterov, hipStream_t st);
 int ddp_conv_fwd_smallk(const ddp_amd::ConvGeom* g, const void* x, const void* wc,
                         const float* bias, void* y, float* stats, hipStream_t st);
-void ddp_conv_options(int wgrad_atomic, int persistent, int stages);
+void ddp_conv_options(int persistent, int stages);
 void ddp_conv_epi_stage_set(int on);
-void ddp_bn_bwd_local_wide_set(int on);
 int ddp_bn_pool3_fwd(const ddp_amd::BnArgs* a, unsigned char* idx, hipStream_t st);
 int ddp_bn_pool3_bwd(const ddp_amd::BnArgs* a, const unsigned char* idx, hipStream_t st);
 void ddp_conv_pair_mode(int mode, int items);
@@ -213,9 +228,7 @@ void ddp_conv_pair_force(int splits_dg, int splits_wg);
 int ddp_conv_bwd_pair(const ddp_amd::ConvGeom* g, const void* dy, const void* wc, void* dx,
                       const void* x, float* dw, float* ws, size_t ws_elems,
                       const ddp_amd::BnBwdFuse* bn, const ddp_amd::BnBwdApply* ba, int* bn_done,
-                      hipStream_t st);
-void ddp_conv_fixup(float* facc, size_t facc_elems, unsigned* tickets, size_t n_tickets, int mode,
-                    size_t max_bytes);
+                      hipStream_t st, const ddp_amd::BnBwdXf* xf);
 void ddp_conv_tune_set(int mode, int M, int N, int K, int tile, int splits, int stages);
 void ddp_conv_tune_clear();
 void ddp_conv_force_tile(int tile_plus_one, int stages);
@@ -239,6 +252,9 @@ int ddp_avgpool_bwd(const void* dy, int N, int HW, int C, void* dx, hipStream_t 
 int ddp_colsum(const void* dl, int B, int J, float* db, hipStream_t st);
 int ddp_mean_ws(const float* in, size_t n, int ws, float* out, hipStream_t st);
 int ddp_scale(float* x, size_t n, float s, hipStream_t st);
+// kernel copy / byte fill (graph-capture-safe stand-ins for hipMemcpyAsync / hipMemsetAsync)
+int ddp_copy_bytes(void* dst, const void* src, size_t n, hipStream_t st);
+int ddp_fill_bytes(void* dst, int value, size_t n, hipStream_t st);
 int ddp_comm_standin(float* x, size_t n, int blocks, float usec, float scale, hipStream_t st);
 int ddp_flag_signal(unsigned* flag, hipStream_t st);
 int ddp_flag_wait(const unsigned* flag, unsigned* expected, unsigned* err, float timeout_s,

@@ -16,10 +16,15 @@
 //         finalize  — one thread per channel: k1 = S1/M, k2 = S2/M; dgamma += S2, dbeta += S1
 //         apply     — dz = scale * (dy_bn - k1 - xhat * k2);  d_res = dy_bn (residual branch)
 // The coefficient table is built ONCE per layer (a table rebuilt by every block would re-read
-// 16 replicas x C channels per block: ~800 MB per ResNet-50 BN layer). For small layers
+// 16 replicas x C channels per block: ~800 MB per ResNet-50 BN layer). For small forward layers
 // (blocks x channels x replicas below kFoldBytes) the finalize step is FOLDED into the apply
 // kernel instead: every block reduces the replicas it needs into LDS, saving a launch (each
 // dispatch costs ~4-5 us of the captured step).
+// Backward without an apply pass (ddp_bn_bwd_xf): the reduce kernel also stores dy_bn (the
+// routed, masked gradient at the BN output — also the residual branch's gradient), and the
+// finalize writes dz = A * dy_bn + B * z + C per channel (A = scale, B = -scale * invstd * k2,
+// C = scale * (invstd * k2 * mean - k1)) for the conv backward GEMMs, which compute dz while
+// staging their A operand (conv_igemm.hip XF): dz is never written or re-read.
 // Every apply/reduce thread owns 8 contiguous channels (one 16-byte vector) of an output pixel
 // and reads its coefficients straight from the (L2-resident) table: no LDS, no barrier before
 // the streaming loads.
@@ -201,12 +206,6 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnArgs a) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = f2bf(best[e]);
     st8(a.out + pix * a.C + cg * 8, o);
-    if (!POOL && a.rmask) {  // ReLU mask for the backward (replaces re-reading the residual)
-      unsigned bits = 0;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) bits |= (best[e] > 0.f ? 1u : 0u) << e;
-      a.rmask[pix * G + cg] = (unsigned char)bits;
-    }
   }
 }
 
@@ -219,7 +218,6 @@ struct BwdItems {
   u16x8 dv[IPT];
   u16x8 zv[IPT][NP];
   u16x8 rv[IPT][POOL ? 1 : NP];  // residual: only without pooling (host rejects pool + res)
-  unsigned mk[IPT];               // ReLU mask byte of the item's 8 channels (BnArgs::rmask)
   size_t off[IPT][NP];
   bool ok[IPT];
 };
@@ -243,8 +241,7 @@ __device__ __forceinline__ void bwd_load(const BnArgs& a, BwdItems<POOL, IPT>& L
       const size_t off = (((size_t)n * a.H + h) * a.W + w) * a.C + cg * 8;
       L.off[it][d] = off;
       L.zv[it][d] = ld8(a.z + off);
-      if (!POOL && a.rmask) L.mk[it] = a.rmask[off >> 3];  // 1 byte instead of 16 (residual)
-      else if (!POOL && a.res) L.rv[it][POOL ? 0 : d] = ld8(a.res + off);
+      if (!POOL && a.res) L.rv[it][POOL ? 0 : d] = ld8(a.res + off);
     }
   }
 }
@@ -252,7 +249,7 @@ __device__ __forceinline__ void bwd_load(const BnArgs& a, BwdItems<POOL, IPT>& L
 // dy_bn (gradient at the BN output, after ReLU mask and pool routing) and xhat for one item
 template <bool POOL>
 __device__ __forceinline__ void bwd_compute(const BnArgs& a, const u16x8& dv, const u16x8* zv,
-                                            const u16x8* rv, unsigned mk, const float* sc, const float* sh,
+                                            const u16x8* rv, const float* sc, const float* sh,
                                             const float* mu, const float* is, float (*xh)[8],
                                             float (*dyb)[8]) {
   constexpr int NP = POOL ? 4 : 1;
@@ -266,8 +263,7 @@ __device__ __forceinline__ void bwd_compute(const BnArgs& a, const u16x8& dv, co
     for (int e = 0; e < 8; ++e) {
       const float zf = bf2f(zv[d][e]);
       float y = zf * sc[e] + sh[e];
-      if (!POOL && a.rmask) y = ((mk >> e) & 1u) ? 1.f : 0.f;  // only its sign is used below
-      else if (!POOL && a.res) y += bf2f(rv[POOL ? 0 : d][e]);
+      if (!POOL && a.res) y += bf2f(rv[POOL ? 0 : d][e]);
       xh[d][e] = (zf - mu[e]) * is[e];
       yv[d][e] = y;
       if (POOL) {
@@ -316,14 +312,21 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
   for (int it = 0; it < IPT; ++it) {
     if (!L.ok[it]) continue;
     float xh[NP][8], dyb[NP][8];
-    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], L.mk[it], sc, sh, mu, is, xh, dyb);
+    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], sc, sh, mu, is, xh, dyb);
 #pragma unroll
-    for (int d = 0; d < NP; ++d)
+    for (int d = 0; d < NP; ++d) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         acc[0][e] += dyb[d][e];
         acc[1][e] += dyb[d][e] * xh[d][e];
       }
+      if (a.dyb) {  // (ddp_bn_bwd_xf) dy_bn for the consumer GEMMs' A-operand transform
+        u16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = f2bf(dyb[d][e]);  // exact: a routed / masked bf16 value
+        st8(a.dyb + L.off[it][d], o);
+      }
+    }
   }
   // block reduction over the 256/Gb threads sharing each channel group, then one atomic per
   // channel per block into this block's replica
@@ -342,40 +345,42 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
       atomicAdd(rep + k * a.C + (cg_base + g) * 8 + e, s);
     }
   }
-  if (a.counter == nullptr) return;
-  // In-launch finalize (cdna_hip_programming.md §6 Guideline 16, counter form with sc1 hand-off):
-  // the replica sums are written by device-scope atomics (performed past the XCD L2s), so no
-  // release fence is needed — every wave drains its atomics (vmcnt), a barrier, then one ticket
-  // per block; the block that draws the last ticket reads the replicas with sc1 loads and turns
-  // them into k1 / k2 and the dgamma / dbeta contributions (no separate finalize launch).
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int* flag = reinterpret_cast<int*>(red);
-  if (tid == 0) {
-    const int nblk = gridDim.x * gridDim.y;
-    const int t = __hip_atomic_fetch_add(a.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flag[0] = (t == nblk - 1);
-    if (t == nblk - 1) *a.counter = 0;  // ready for the next backward (scratch fill zeroes it too)
-  }
-  __syncthreads();
-  if (!flag[0]) return;
-  const float inv_m = 1.f / ((float)a.N * a.H * a.W);
-  for (int c = tid; c < a.C; c += 256) {
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int r = 0; r < kStatRep; ++r) {
-      s1 += __hip_atomic_load(a.sums + r * 2 * a.C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s2 += __hip_atomic_load(a.sums + r * 2 * a.C + a.C + c, __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_AGENT);
-    }
-    a.coef[kK1 * a.C + c] = s1 * inv_m;
-    a.coef[kK2 * a.C + c] = s2 * inv_m;
-    if (a.dgamma) a.dgamma[c] += s2;
-    if (a.dbeta) a.dbeta[c] += s1;
-  }
 }
 
-template <bool POOL, int IPT, bool FOLD>
+// (ddp_bn_bwd_xf) k1 / k2 -> the per-channel affine form of the BN-backward apply, for the conv
+// backward GEMMs' A-operand transform: xcoef[c / 8][rows][8] = A | B | C (| scale | shift) with
+// dz = A * dy_bn + B * z + C (the apply kernel's scale * (dy_bn - k1 - xhat * k2) expanded);
+// rows = 5 when the consumer applies the ReLU mask itself (a.dyb == nullptr with ReLU, no pool,
+// no residual: dy_bn = [scale * z + shift > 0] * dout needs nothing stored). dgamma += S2,
+// dbeta += S1 as in bn_finalize_bwd_kernel.
+__global__ __launch_bounds__(256) void bn_finalize_bwd_xf_kernel(BnArgs a) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.C) return;
+  const float inv_m = 1.f / ((float)a.N * a.H * a.W);
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int r = 0; r < kStatRep; ++r) {
+    s1 += a.sums[r * 2 * a.C + c];
+    s2 += a.sums[r * 2 * a.C + a.C + c];
+  }
+  const float k1 = s1 * inv_m, k2 = s2 * inv_m;
+  const float sc = a.coef[kSc * a.C + c], mu = a.coef[kMu * a.C + c], is = a.coef[kIs * a.C + c];
+  a.coef[kK1 * a.C + c] = k1;
+  a.coef[kK2 * a.C + c] = k2;
+  const bool mask = a.dyb == nullptr && a.relu;  // (no ReLU: dy_bn = dout, nothing to mask)
+  float* x = a.xcoef + (c >> 3) * (mask ? 40 : 24) + (c & 7);
+  x[0] = sc;
+  x[8] = -sc * is * k2;
+  x[16] = sc * (is * k2 * mu - k1);
+  if (mask) {
+    x[24] = sc;
+    x[32] = a.coef[kSh * a.C + c];
+  }
+  if (a.dgamma) a.dgamma[c] += s2;
+  if (a.dbeta) a.dbeta[c] += s1;
+}
+
+template <bool POOL, int IPT>
 __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(BnArgs a) {
   constexpr int NP = POOL ? 4 : 1;
   const int G = a.C / 8;
@@ -394,42 +399,13 @@ __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(BnArgs a) {
   ld8f(a.coef + kSh * a.C + c0, sh);
   ld8f(a.coef + kMu * a.C + c0, mu);
   ld8f(a.coef + kIs * a.C + c0, is);
-  if (!FOLD) {
-    ld8f(a.coef + kK1 * a.C + c0, k1);
-    ld8f(a.coef + kK2 * a.C + c0, k2);
-  } else {
-    // replica reduction of this block's channel chunk (small layers: no finalize launch);
-    // block row 0 owns the dgamma / dbeta accumulation
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int nch = Gb * 8;
-    const float inv_m = 1.f / ((float)a.N * a.H * a.W);
-    for (int i = threadIdx.x; i < nch; i += blockDim.x) {
-      const int c = cg_base * 8 + i;
-      float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int r = 0; r < kStatRep; ++r) {
-        s1 += a.sums[r * 2 * a.C + c];
-        s2 += a.sums[r * 2 * a.C + a.C + c];
-      }
-      lds[i] = s1 * inv_m;
-      lds[nch + i] = s2 * inv_m;
-      if (blockIdx.x == 0) {
-        if (a.dgamma) a.dgamma[c] += s2;
-        if (a.dbeta) a.dbeta[c] += s1;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      k1[e] = lds[cgl * 8 + e];
-      k2[e] = lds[nch + cgl * 8 + e];
-    }
-  }
+  ld8f(a.coef + kK1 * a.C + c0, k1);
+  ld8f(a.coef + kK2 * a.C + c0, k2);
 #pragma unroll
   for (int it = 0; it < IPT; ++it) {
     if (!L.ok[it]) continue;
     float xh[NP][8], dyb[NP][8];
-    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], L.mk[it], sc, sh, mu, is, xh, dyb);
+    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], sc, sh, mu, is, xh, dyb);
 #pragma unroll
     for (int d = 0; d < NP; ++d) {
       u16x8 o, r;
@@ -475,7 +451,7 @@ __global__ __launch_bounds__(NT) void bn_act_bwd_local_kernel(BnArgs a) {
   for (int it = 0; it < IPT; ++it) {
     if (!L.ok[it]) continue;
     float xh[NP][8], dyb[NP][8];
-    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], L.mk[it], sc, sh, mu, is, xh, dyb);
+    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], sc, sh, mu, is, xh, dyb);
 #pragma unroll
     for (int d = 0; d < NP; ++d)
 #pragma unroll
@@ -515,120 +491,7 @@ __global__ __launch_bounds__(NT) void bn_act_bwd_local_kernel(BnArgs a) {
   for (int it = 0; it < IPT; ++it) {
     if (!L.ok[it]) continue;
     float xh[NP][8], dyb[NP][8];
-    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], L.mk[it], sc, sh, mu, is, xh, dyb);
-#pragma unroll
-    for (int d = 0; d < NP; ++d) {
-      u16x8 o, r;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        o[e] = f2bf(sc[e] * (dyb[d][e] - k1[e] - xh[d][e] * k2[e]));
-        r[e] = f2bf(dyb[d][e]);
-      }
-      st8(a.dz + L.off[it][d], o);
-      if (a.dres) st8(a.dres + L.off[it][d], r);
-    }
-  }
-}
-
-// ------------------------------- backward, clustered -------------------------------
-// Mid-size layers: the one-launch backward spread over K <= kStatRep blocks per 64-channel chunk
-// (block = 32 pixel rows x 8 channel groups: every 128-byte line is read whole). Each block
-// reduces its slice's S1 / S2, stores them (agent-scope stores: written past the XCD L2s) into
-// slot [slice][2][C] of the zeroed sums scratch, drains them (vmcnt), arrives on the grid
-// counter, waits until every block of the launch has arrived (the grid is at most a few hundred
-// blocks: all co-resident), sums the K slots of its chunk and applies from the items it still
-// holds in registers. One launch, dy / z read once, no float atomics. The wait is bounded: on
-// timeout the block poisons k1 (NaN -> the loss turns NaN) instead of hanging the GPU.
-constexpr int kClusterRows = 32;  // pixel rows per pass (256 threads = 32 x 8 groups)
-template <bool POOL, int IPT>
-__global__ __launch_bounds__(256) void bn_act_bwd_cluster_kernel(BnArgs a, int K, int P) {
-  constexpr int NP = POOL ? 4 : 1;
-  __shared__ float red[2][8][8 * kClusterRows];  // [s1|s2][e][thread]
-  __shared__ float fin[128];
-  __shared__ int timed_out;
-  const int chunk = blockIdx.x / K, slice = blockIdx.x % K;
-  const int tid = threadIdx.x, cgl = tid % 8, prow = tid / 8;
-  const int cg = chunk * 8 + cgl, c0 = cg * 8;
-  const int Ho = POOL ? a.H / 2 : a.H, Wo = POOL ? a.W / 2 : a.W;
-  const size_t npix = (size_t)a.N * Ho * Wo;
-  const size_t lo = (size_t)slice * P;
-  const size_t hi = lo + P < npix ? lo + P : npix;
-  BwdItems<POOL, IPT> L;
-  bwd_load<POOL, IPT>(a, L, lo + prow, kClusterRows, hi, cg, Ho, Wo);
-  float sc[8], sh[8], mu[8], is[8];
-  ld8f(a.coef + kSc * a.C + c0, sc);
-  ld8f(a.coef + kSh * a.C + c0, sh);
-  ld8f(a.coef + kMu * a.C + c0, mu);
-  ld8f(a.coef + kIs * a.C + c0, is);
-  float s1[8], s2[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
-#pragma unroll
-  for (int it = 0; it < IPT; ++it) {
-    if (!L.ok[it]) continue;
-    float xh[NP][8], dyb[NP][8];
-    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], L.mk[it], sc, sh, mu, is, xh, dyb);
-#pragma unroll
-    for (int d = 0; d < NP; ++d)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        s1[e] += dyb[d][e];
-        s2[e] += dyb[d][e] * xh[d][e];
-      }
-  }
-#pragma unroll
-  for (int e = 0; e < 8; ++e) { red[0][e][tid] = s1[e]; red[1][e][tid] = s2[e]; }
-  if (tid == 0) timed_out = 0;
-  __syncthreads();
-  // 128 partials of this block (2 sums x 64 channels): thread t < 128 adds its column
-  float* slot = a.sums + (size_t)slice * 2 * a.C;
-  if (tid < 128) {
-    const int k = tid / 64, ch = tid % 64, g = ch / 8, e = ch % 8;
-    float t = 0.f;
-    for (int r = 0; r < kClusterRows; ++r) t += red[k][e][r * 8 + g];
-    __hip_atomic_store(slot + k * a.C + chunk * 64 + ch, t, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    const int nblk = gridDim.x;
-    __hip_atomic_fetch_add(a.grid_sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int spins = 0;
-    while (__hip_atomic_load(a.grid_sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nblk) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1 << 22)) { timed_out = 1; break; }
-    }
-  }
-  __syncthreads();
-  if (tid < 128) {
-    const int k = tid / 64, ch = tid % 64;
-    float t = 0.f;
-    for (int r = 0; r < K; ++r)
-      t += __hip_atomic_load(a.sums + (size_t)r * 2 * a.C + k * a.C + chunk * 64 + ch,
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    fin[tid] = timed_out ? __builtin_nanf("") : t;
-    if (slice == 0) {
-      const float inv_m = 1.f / ((float)a.N * a.H * a.W);
-      const int c = chunk * 64 + ch;
-      a.coef[(k ? kK2 : kK1) * a.C + c] = fin[tid] * inv_m;
-      float* dst = k ? a.dgamma : a.dbeta;
-      if (dst) dst[c] += fin[tid];
-    }
-  }
-  __syncthreads();
-  const float inv_m = 1.f / ((float)a.N * a.H * a.W);
-  float k1[8], k2[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    k1[e] = fin[cgl * 8 + e] * inv_m;
-    k2[e] = fin[64 + cgl * 8 + e] * inv_m;
-  }
-#pragma unroll
-  for (int it = 0; it < IPT; ++it) {
-    if (!L.ok[it]) continue;
-    float xh[NP][8], dyb[NP][8];
-    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], L.mk[it], sc, sh, mu, is, xh, dyb);
+    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], sc, sh, mu, is, xh, dyb);
 #pragma unroll
     for (int d = 0; d < NP; ++d) {
       u16x8 o, r;
@@ -844,13 +707,6 @@ static unsigned blocks_for(size_t items, size_t per_block) {
 // Folding the finalize into the apply kernel costs every block a replica reduction of its
 // channels; worth it (one launch fewer) while that re-read traffic stays small.
 constexpr size_t kFoldBytes = 24u << 20;
-// Backward fold threshold (replica bytes re-read by all apply blocks): measured 3-4x slower
-// applies when folding the big layers (>= 16 MB re-read at batch 256); at the strong-scaling
-// batches folding was measured slower as well (b32 step +50 us: each apply block re-reduces the
-// 16 replicas serially, profiles/r2_launch_reduction_ab.md) -> never by default.
-static size_t kFoldBwdBytes = 0;  // DDP_AMD_BN_FOLD_BWD_KB overrides (0 = never fold)
-static size_t kBwdBlocks = 1024;  // target reduce-grid size (DDP_AMD_BN_BWD_BLOCKS overrides)
-
 template <bool POOL, int IPT>
 static void launch_fwd(const BnArgs& a, size_t items, hipStream_t st) {
   const unsigned nb = blocks_for(items, 256 * IPT);
@@ -867,7 +723,6 @@ extern "C" int ddp_bn_act_fwd(const BnArgs* args, hipStream_t st) {
   BnArgs a = *args;
   if (a.C % 8 || a.coef == nullptr) return -1;
   if (a.pool && a.res) return -1;  // residual add is only fused without pooling
-  if (a.pool && a.rmask) return -1;
   const int Ho = a.pool ? a.H / 2 : a.H, Wo = a.pool ? a.W / 2 : a.W;
   const size_t items = (size_t)a.N * Ho * Wo * (a.C / 8);
   // 1 item per thread for small layers; 2 (pooled) / 4 (plain) when there are enough to keep
@@ -882,23 +737,23 @@ extern "C" int ddp_bn_act_fwd(const BnArgs* args, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-template <bool POOL, int IPT>
+// Target reduce-grid size (DDP_AMD_BN_BWD_BLOCKS overrides).
+static size_t kBwdBlocks = 1024;
+
+template <bool POOL, int IPT, bool APPLY>
 static void launch_bwd(const BnArgs& a, size_t npix, int Gb, int chunks, hipStream_t st) {
   const unsigned bx = blocks_for(npix, (size_t)(256 / Gb) * IPT);
   if (!a.sums_ready)  // (else: accumulated by the next layer's dgrad epilogue, BnBwdFuse)
     hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<POOL, IPT>), dim3(bx, chunks), dim3(256), 0, st, a);
-  // (measured: folding the backward finalize made the apply 3-4x slower — the replicated sums
-  // were just written by memory-side atomics and every block re-reads them uncached — so the
-  // backward keeps its separate finalize launch)
-  const size_t nch = (size_t)Gb * 8;
-  if (a.counter && !a.sums_ready) {  // finalized by the reduce kernel's last block
-    hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT, false>), dim3(bx, chunks), dim3(256), 0, st, a);
-  } else if ((size_t)bx * chunks * nch * 2 * kStatRep * sizeof(float) <= kFoldBwdBytes) {
-    hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT, true>), dim3(bx, chunks), dim3(256),
-                       2 * nch * sizeof(float), st, a);
-  } else {
+  // The finalize stays its own launch: folding it into the apply (every block re-reducing the 16
+  // replicas the reduce just wrote with memory-side atomics) measured 3-4x slower applies at
+  // batch 256 and +50 us per b32 step; the reduce's last-arriving block doing it measured slower
+  // than the launch boundary too (profiles/r2_launch_reduction_ab.md, r3_bn_bwd_one_launch.md).
+  if (APPLY) {
     hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3(blocks_for(a.C, 256)), dim3(256), 0, st, a);
-    hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT, false>), dim3(bx, chunks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT>), dim3(bx, chunks), dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL(bn_finalize_bwd_xf_kernel, dim3(blocks_for(a.C, 256)), dim3(256), 0, st, a);
   }
 }
 
@@ -909,43 +764,11 @@ static void launch_bwd(const BnArgs& a, size_t npix, int Gb, int chunks, hipStre
 // against 12-19 us for reduce + finalize + apply): served while ipt x (dy + z [+ res] vectors)
 // <= kLocalMaxLoads (DDP_AMD_BN_BWD_LOCAL_LOADS; 0 = never). Step A/B of the limit (0/5/8/10):
 // 8 is best at b32..b128 (b32 0.416 -> 0.405 ms, b64 -1.2 %, b128 -0.9 %), neutral at b256.
+// (1024-thread blocks for the next-bigger layers and a clustered grid-synchronised variant were
+// measured slower and removed in round 4: profiles/r3_conv_occupancy.md, r3_bn_bwd_one_launch.md)
 static int kLocalMaxLoads = 8;
 constexpr int kLocalThreads = 256;
-// Layers too big for 256 threads may still fit ONE 1024-thread block per channel group (4x the
-// threads, a quarter of the loads each; <= 2 items per thread keeps the kernel within the 128
-// VGPRs a 1024-thread block allows): e.g. the b32 step's 8x8x256 layer (2048 pixels) would drop
-// its reduce -> finalize -> apply chain. OFF by default (DDP_AMD_BN_BWD_LOCAL_WIDE=1 enables):
-// measured slower — b32 0.3997 -> 0.4056 ms, b64 0.477 -> 0.488, b256 0.876 -> 0.890 (same box;
-// profiles/r3_conv_occupancy.md): C/8 blocks of 1024 threads stream from too few CUs.
-static int kLocalWide = -1;
-static bool local_cfg_256(const BnArgs& a, int* ipt);
-static bool local_cfg_nt(const BnArgs& a, int* ipt, int* nt);
 static bool local_cfg(const BnArgs& a, int* ipt) {
-  int nt;
-  return local_cfg_nt(a, ipt, &nt) && nt == kLocalThreads;
-}
-static bool local_cfg_nt(const BnArgs& a, int* ipt, int* nt) {
-  if (kLocalWide < 0) {
-    const char* e = std::getenv("DDP_AMD_BN_BWD_LOCAL_WIDE");
-    kLocalWide = e ? std::atoi(e) : 0;
-  }
-  *nt = kLocalThreads;
-  int i256;
-  if (local_cfg_256(a, &i256)) { *ipt = i256; return true; }
-  if (!kLocalWide || kLocalMaxLoads == 0 || a.C % 8 || (a.pool && a.res)) return false;
-  const int Ho = a.pool ? a.H / 2 : a.H, Wo = a.pool ? a.W / 2 : a.W;
-  const size_t npix = (size_t)a.N * Ho * Wo;
-  const int per_item = 1 + (a.pool ? 4 : 1) + (a.res ? 1 : 0);
-  for (int i = 1; i <= (a.pool ? 1 : 2); i *= 2) {
-    if ((size_t)1024 * i < npix) continue;
-    if (i * per_item > kLocalMaxLoads) return false;
-    *ipt = i;
-    *nt = 1024;
-    return true;
-  }
-  return false;
-}
-static bool local_cfg_256(const BnArgs& a, int* ipt) {
   static const bool init = [] {
     if (const char* e = std::getenv("DDP_AMD_BN_BWD_LOCAL_LOADS")) kLocalMaxLoads = std::max(0, std::atoi(e));
     return true;
@@ -966,13 +789,8 @@ static bool local_cfg_256(const BnArgs& a, int* ipt) {
 }
 
 template <bool POOL>
-static void launch_local(const BnArgs& a, int ipt, hipStream_t st, int nt = kLocalThreads) {
+static void launch_local(const BnArgs& a, int ipt, hipStream_t st) {
   const dim3 grid(a.C / 8), block(kLocalThreads);
-  if (nt == 1024) {
-    if (ipt == 1) hipLaunchKernelGGL((bn_act_bwd_local_kernel<POOL, 1, 1024>), grid, dim3(1024), 0, st, a);
-    else if constexpr (!POOL) hipLaunchKernelGGL((bn_act_bwd_local_kernel<POOL, 2, 1024>), grid, dim3(1024), 0, st, a);
-    return;
-  }
   if (ipt == 1) hipLaunchKernelGGL((bn_act_bwd_local_kernel<POOL, 1, kLocalThreads>), grid, block, 0, st, a);
   else if (ipt == 2) hipLaunchKernelGGL((bn_act_bwd_local_kernel<POOL, 2, kLocalThreads>), grid, block, 0, st, a);
   else if (ipt == 4) hipLaunchKernelGGL((bn_act_bwd_local_kernel<POOL, 4, kLocalThreads>), grid, block, 0, st, a);
@@ -987,87 +805,21 @@ extern "C" void ddp_bn_bwd_local_set(long long max_loads) {
   kLocalMaxLoads = (int)std::max(0LL, max_loads);
 }
 
-extern "C" void ddp_bn_bwd_local_wide_set(int on) { kLocalWide = on ? 1 : 0; }
-
 extern "C" int ddp_bn_bwd_local_ok(int N, int H, int W, int C, int pool) {
   BnArgs a{};
   a.N = N; a.H = H; a.W = W; a.C = C; a.pool = pool;
-  int ipt, nt;
-  return local_cfg_nt(a, &ipt, &nt) ? 1 : 0;
+  int ipt;
+  return local_cfg(a, &ipt) ? 1 : 0;
 }
 
-// Clustered one-launch backward (bn_act_bwd_cluster_kernel) for layers too big for the local
-// kernel: K = ceil(npix / (32 x ipt)) <= kStatRep slices per 64-channel chunk, ipt <= 4 items
-// per thread; needs the arrival counter. OFF by default (DDP_AMD_BN_BWD_CLUSTER=1 enables):
-// measured slower than the three-launch chain it replaces — 12-23 us per layer against 10-15
-// (b32 step 0.404 -> 0.424 ms, b256 +1.2 %; profiles/r3_bn_bwd_one_launch.md): the arrival
-// counter and the agent-scope slot traffic cost more than the two launch boundaries.
-static int kClusterMode = 0;
-static bool cluster_cfg(const BnArgs& a, int* ipt, int* K, int* P) {
-  static const bool init = [] {
-    if (const char* e = std::getenv("DDP_AMD_BN_BWD_CLUSTER")) kClusterMode = std::atoi(e);
-    return true;
-  }();
-  (void)init;
-  if (!kClusterMode || !a.grid_sync || a.C % 64 || (a.pool && a.res)) return false;
-  const int Ho = a.pool ? a.H / 2 : a.H, Wo = a.pool ? a.W / 2 : a.W;
-  const size_t npix = (size_t)a.N * Ho * Wo;
-  for (int i = 1; i <= 4; i *= 2) {
-    const size_t per = (size_t)kClusterRows * i;
-    const size_t k = (npix + per - 1) / per;
-    if (k <= (size_t)kStatRep) {
-      *ipt = i;
-      *K = (int)k;
-      *P = (int)per;
-      return (size_t)(a.C / 64) * k <= 512;  // co-resident with room to spare
-    }
-  }
-  return false;
-}
-
-extern "C" void ddp_bn_bwd_cluster_set(int mode) {
-  BnArgs a{};
-  int i, k, p;
-  (void)cluster_cfg(a, &i, &k, &p);
-  kClusterMode = mode;
-}
-
-template <bool POOL>
-static void launch_cluster(const BnArgs& a, int ipt, int K, int P, hipStream_t st) {
-  const dim3 grid((a.C / 64) * K), block(256);
-  if (ipt == 1) hipLaunchKernelGGL((bn_act_bwd_cluster_kernel<POOL, 1>), grid, block, 0, st, a, K, P);
-  else if (ipt == 2) hipLaunchKernelGGL((bn_act_bwd_cluster_kernel<POOL, 2>), grid, block, 0, st, a, K, P);
-  else hipLaunchKernelGGL((bn_act_bwd_cluster_kernel<POOL, 4>), grid, block, 0, st, a, K, P);
-}
-
-// a.coef must hold the table written by the matching forward; a.sums ([kStatRep][2][C]) must be
-// zero on entry (per-step scratch, zeroed once per forward).
-extern "C" int ddp_bn_act_bwd(const BnArgs* args, hipStream_t st) {
+// reduce(+finalize, +apply) grid shape shared by ddp_bn_act_bwd and ddp_bn_bwd_xf
+template <bool APPLY>
+static int launch_reduce_chain(const BnArgs& a, hipStream_t st) {
   static const bool init = [] {
     if (const char* e = std::getenv("DDP_AMD_BN_BWD_BLOCKS")) kBwdBlocks = std::max(1, std::atoi(e));
-    if (const char* e = std::getenv("DDP_AMD_BN_FOLD_BWD_KB")) kFoldBwdBytes = (size_t)std::max(0, std::atoi(e)) << 10;
     return true;
   }();
   (void)init;
-  BnArgs a = *args;
-  if (a.C % 8 || a.coef == nullptr || a.sums == nullptr) return -1;
-  if (a.pool && (a.res || a.rmask)) return -1;
-  {
-    // small layer: the whole backward in one launch (any sums the next layer's dgrad
-    // accumulated are simply not needed)
-    int ipt, nt;
-    if (local_cfg_nt(a, &ipt, &nt)) {
-      if (a.pool) launch_local<true>(a, ipt, st, nt);
-      else launch_local<false>(a, ipt, st, nt);
-      return (int)hipGetLastError();
-    }
-    int K, P;
-    if (cluster_cfg(a, &ipt, &K, &P)) {  // the sums scratch is overwritten (slots, not sums)
-      if (a.pool) launch_cluster<true>(a, ipt, K, P, st);
-      else launch_cluster<false>(a, ipt, K, P, st);
-      return (int)hipGetLastError();
-    }
-  }
   const int G = a.C / 8;
   const int Gb = G < 256 ? G : 256;
   if ((Gb < 256 && 256 % Gb) || (G > 256 && G % 256)) return -1;  // channel groups must tile 256 threads
@@ -1085,15 +837,60 @@ extern "C" int ddp_bn_act_bwd(const BnArgs* args, hipStream_t st) {
   if (blocks1 > 2 * kBwdBlocks)
     while (ipt < 4 && blocks1 / ipt > kBwdBlocks) ipt *= 2;
   if (a.pool) {
-    if (ipt >= 4) launch_bwd<true, 4>(a, npix, Gb, chunks, st);
-    else if (ipt == 2) launch_bwd<true, 2>(a, npix, Gb, chunks, st);
-    else launch_bwd<true, 1>(a, npix, Gb, chunks, st);
+    if (ipt >= 4) launch_bwd<true, 4, APPLY>(a, npix, Gb, chunks, st);
+    else if (ipt == 2) launch_bwd<true, 2, APPLY>(a, npix, Gb, chunks, st);
+    else launch_bwd<true, 1, APPLY>(a, npix, Gb, chunks, st);
   } else {
-    if (ipt >= 4) launch_bwd<false, 4>(a, npix, Gb, chunks, st);
-    else if (ipt == 2) launch_bwd<false, 2>(a, npix, Gb, chunks, st);
-    else launch_bwd<false, 1>(a, npix, Gb, chunks, st);
+    if (ipt >= 4) launch_bwd<false, 4, APPLY>(a, npix, Gb, chunks, st);
+    else if (ipt == 2) launch_bwd<false, 2, APPLY>(a, npix, Gb, chunks, st);
+    else launch_bwd<false, 1, APPLY>(a, npix, Gb, chunks, st);
   }
   return (int)hipGetLastError();
+}
+
+// a.coef must hold the table written by the matching forward; a.sums ([kStatRep][2][C]) must be
+// zero on entry (per-step scratch, zeroed once per forward).
+extern "C" int ddp_bn_act_bwd(const BnArgs* args, hipStream_t st) {
+  BnArgs a = *args;
+  a.dyb = nullptr;
+  if (a.C % 8 || a.coef == nullptr || a.sums == nullptr) return -1;
+  if (a.pool && a.res) return -1;
+  int ipt;
+  if (local_cfg(a, &ipt)) {
+    // small layer: the whole backward in one launch (any sums the next layer's dgrad
+    // accumulated are simply not needed)
+    if (a.pool) launch_local<true>(a, ipt, st);
+    else launch_local<false>(a, ipt, st);
+    return (int)hipGetLastError();
+  }
+  return launch_reduce_chain<true>(a, st);
+}
+
+// Is the apply-free backward (ddp_bn_bwd_xf) the one to run for this layer? Not for layers the
+// one-launch local kernel serves (one launch beats reduce + finalize), nor when the sums came
+// from the next layer's dgrad epilogue (sums_ready: no reduce pass to store dy_bn in).
+extern "C" int ddp_bn_bwd_xf_ok(int N, int H, int W, int C, int pool, int res, int sums_ready) {
+  BnArgs a{};
+  a.N = N; a.H = H; a.W = W; a.C = C; a.pool = pool;
+  a.res = res ? reinterpret_cast<const unsigned short*>(16) : nullptr;
+  int ipt;
+  if (C % 8 || (pool && res) || sums_ready || local_cfg(a, &ipt)) return 0;
+  const int G = C / 8, Gb = G < 256 ? G : 256;
+  return ((Gb < 256 && 256 % Gb) || (G > 256 && G % 256)) ? 0 : 1;
+}
+
+// BatchNorm backward WITHOUT the apply pass: reduce (S1 / S2, and dy_bn stored to a.dyb) +
+// finalize into a.xcoef ([C/8][3][8] = A | B | C of dz = A * dy_bn + B * z + C) and dgamma /
+// dbeta. The conv backward GEMMs then take (z, dy_bn, xcoef) as their A operand (BnBwdXf).
+// a.dyb doubles as the residual-branch gradient. Without pool and residual a.dyb may be null:
+// the table then carries scale / shift too and the GEMMs mask the raw dout themselves
+// (BnBwdXf::mask). Requires ddp_bn_bwd_xf_ok.
+extern "C" int ddp_bn_bwd_xf(const BnArgs* args, hipStream_t st) {
+  BnArgs a = *args;
+  if (a.C % 8 || a.coef == nullptr || a.sums == nullptr || a.xcoef == nullptr ||
+      a.sums_ready || (a.pool && a.res) || (a.dyb == nullptr && (a.pool || a.res)))
+    return -1;
+  return launch_reduce_chain<false>(a, st);
 }
 
 

@@ -75,6 +75,40 @@ __global__ __launch_bounds__(64) void flag_wait_kernel(const unsigned* flag, uns
   }
 }
 
+// copy / fill used by the communicator instead of hipMemcpyAsync / hipMemsetAsync: inside a
+// captured step those become memcpy / memset graph nodes, and a captured memset node was seen
+// not to order before its readers on ROCm 7 (profiles/r3_conv_occupancy.md section 6) — a
+// kernel node is ordered like every other kernel of the stream
+__global__ __launch_bounds__(256) void copy_bytes_kernel(unsigned char* __restrict__ dst,
+                                                         const unsigned char* __restrict__ src,
+                                                         size_t n, int vec) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  const size_t i0 = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  size_t head = 0;
+  if (vec) {
+    const size_t n16 = n / 16;
+    for (size_t i = i0; i < n16; i += stride)
+      reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+    head = n16 * 16;
+  }
+  for (size_t i = head + i0; i < n; i += stride) dst[i] = src[i];
+}
+
+__global__ __launch_bounds__(256) void fill_bytes_kernel(unsigned char* __restrict__ dst,
+                                                         unsigned v, size_t n, int vec) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  const size_t i0 = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  size_t head = 0;
+  if (vec) {
+    const unsigned w = v * 0x01010101u;
+    const size_t n16 = n / 16;
+    for (size_t i = i0; i < n16; i += stride)
+      reinterpret_cast<uint4*>(dst)[i] = (uint4){w, w, w, w};
+    head = n16 * 16;
+  }
+  for (size_t i = head + i0; i < n; i += stride) dst[i] = (unsigned char)v;
+}
+
 __global__ __launch_bounds__(256) void pack_bf16_kernel(const float* __restrict__ x, size_t n,
                                                         unsigned short* __restrict__ y) {
   const size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -129,6 +163,22 @@ static int wall_khz() {
 
 extern "C" int ddp_mean_ws(const float* in, size_t n, int ws, float* out, hipStream_t st) {
   hipLaunchKernelGGL(mean_ws_kernel, dim3(blocks_for(n)), dim3(256), 0, st, in, n, ws, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int ddp_copy_bytes(void* dst, const void* src, size_t n, hipStream_t st) {
+  if (n == 0 || dst == src) return 0;
+  const int vec = ((uintptr_t)dst % 16 == 0 && (uintptr_t)src % 16 == 0) ? 1 : 0;
+  hipLaunchKernelGGL(copy_bytes_kernel, dim3(blocks_for(vec ? n / 16 + 1 : n)), dim3(256), 0, st,
+                     (unsigned char*)dst, (const unsigned char*)src, n, vec);
+  return (int)hipGetLastError();
+}
+
+extern "C" int ddp_fill_bytes(void* dst, int value, size_t n, hipStream_t st) {
+  if (n == 0) return 0;
+  const int vec = (uintptr_t)dst % 16 == 0 ? 1 : 0;
+  hipLaunchKernelGGL(fill_bytes_kernel, dim3(blocks_for(vec ? n / 16 + 1 : n)), dim3(256), 0, st,
+                     (unsigned char*)dst, (unsigned)(value & 0xff), n, vec);
   return (int)hipGetLastError();
 }
 

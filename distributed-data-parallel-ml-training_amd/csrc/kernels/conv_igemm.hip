@@ -32,10 +32,9 @@
 //   * MFMA operands are swapped (D^T = B^T A^T) so each lane owns one output row and four
 //     consecutive columns: 8-B bf16 / 16-B fp32 stores in the epilogue;
 //   * XCD-aware bijective tile order (T1); split-K writes plain fp32 slabs [split][M][N] that a
-//     finish kernel reduces in a fixed order, or — for the small problems of strong-scaling
-//     batches, where the finish launch costs more than the reduction — accumulates with fp32
-//     atomics and lets the tile's last-arriving split block run the epilogue ("fixup"; WGRAD
-//     atomics go straight into the fp32 weight gradient);
+//     finish kernel reduces in a fixed order (deterministic; fp32-atomic variants — a "ticket
+//     fixup" and WGRAD atomics into dW — measured 3-5x slower on MI355X and were removed in
+//     round 4: profiles/r2_launch_reduction_ab.md);
 //   * FWD epilogue adds the bias, rounds to bf16 and accumulates the per-channel BatchNorm
 //     statistics of the rounded output (sum, sum of squares) — BN needs no separate stats pass.
 #include "common.h"
@@ -86,7 +85,6 @@ struct ConvArgs {
   int Mg, Ng, Kg;            // GEMM dims
   int splits;
   int ksteps_per_split;
-  int wg_atomic;             // WGRAD split-K: fp32 atomics into dw instead of slabs + finish
   // DGRAD of a strided conv, one output phase (pa, pb): GEMM rows are the input pixels
   // h = pa + stride*i, w = pb + stride*j (i < Hp, j < Wp); the only taps that reach them are
   // r = r0 + stride*t (t < Rt), s = s0 + stride*u (u < St), read from dy at (i + qa - t,
@@ -98,13 +96,6 @@ struct ConvArgs {
   FastDiv dPQ, dQ;           // row -> pixel: FWD / WGRAD P*Q, Q; DGRAD H*W, W (phase: Hp*Wp, Wp)
   int has_bnf;               // DGRAD (stride 1, no accumulate): accumulate the preceding
   BnBwdFuse bnf;             //   block's BatchNorm-backward sums in the epilogue (api.h)
-  // split-K "ticket" fixup (FWD/DGRAD, small problems): every split adds its partial tile into
-  // facc [Mg][Ng] fp32 with device-scope atomics; the LAST split block of a tile (per-tile
-  // arrival ticket) reads the total back, clears it and runs the normal epilogue — no slab
-  // workspace, no finish launch. facc / tickets are zero on entry and left zero.
-  int fixup;
-  float* facc;
-  unsigned* tickets;
   // FWD (host-side only, never read by a kernel): BatchNorm forward to fuse into the split-K
   // finish (splitk_finish_bnfwd_kernel) and where to report that it was fused
   const BnFwdFuse* bnfwd;
@@ -116,7 +107,25 @@ struct ConvArgs {
   // FWD / DGRAD bf16 output through the LDS-staged epilogue (conv_igemm_body): full 16-B
   // stores of whole tile rows instead of 8-B fragments of 16 rows per instruction
   int epi_stage;
+  // DGRAD / WGRAD A-operand transform (XF instantiations): the A operand is the gradient at a
+  // training-mode BatchNorm's input, dz = xA[c] * g + xB[c] * z + xC[c], computed while the tile
+  // sits in LDS — its BN-backward "apply" pass never runs and dz is never stored. ``a`` = z
+  // (the conv output the BN normalised), ``xg`` = g (the gradient at the BN output after the
+  // ReLU mask and pool routing: bn_act.hip reduce kernel's dyb, same [pixel][channel] layout),
+  // ``xcoef`` = [xc / 8][rows][8] fp32 (xA | xB | xC [| scale | shift] of 8 channels).
+  // xmask: g is the RAW gradient at the BN output of a block without pool / residual, and the
+  // ReLU mask is applied here (scale * z + shift > 0; rows = 5) — the BN reduce then stores
+  // nothing; otherwise g = dy_bn, already routed and masked (rows = 3).
+  const unsigned short* xg;
+  const float* xcoef;
+  int xc;
+  int xmask;
 };
+
+// LDS elements (u16) of the XF coefficient table in front of the operand ring (64-aligned)
+__host__ __device__ inline int xf_table_elems(int xc, int xmask) {
+  return (xc * (xmask ? 10 : 6) + 63) / 64 * 64;
+}
 
 // ------------------------------------------------------------------ operand gathers
 // Index math is hoisted: the pixel decomposition of a GEMM row is computed once per kernel
@@ -184,6 +193,15 @@ __device__ __forceinline__ int mc_swz(int m) {
   if (NCOL >= 128) return (((m & 3) | (((m >> 3) & 1) << 2)) << 1) & (NCOL / 8 - 1);
   return ((((m >> 1) & 1) | (((m >> 3) & 1) << 1)) << 1);  // 8 chunks: row parity splits banks
 }
+// Logical-chunk correction of DMA chunk i relative to chunk 0 of the same thread in an [m][NCOL]
+// tile: chunk i sits 2048 / NCOL rows further down. For NCOL <= 128 that step (>= 16 rows) keeps
+// every bit mc_swz reads; at NCOL = 256 it is 8 rows, which flips bit 3 of m on odd i -> the
+// swizzle flips chunk bit 3. (The WGRAD B' gather keeps one tap decomposition per thread and so
+// still requires NCOL <= 128: WGRAD BN = 256 tiles are refused by the launcher.)
+template <int NCOL>
+__device__ __forceinline__ int swz_row_step(int i) {
+  return NCOL >= 256 ? ((i & 1) << 3) : 0;
+}
 template <int NCOL>
 __device__ __forceinline__ int mc_off(int m, int col) {
   return m * NCOL + (((col >> 3) ^ mc_swz<NCOL>(m)) << 3) + (col & 7);
@@ -223,10 +241,13 @@ struct ConvSmem {
 // The GEMM body. ``bid`` / ``nblk`` stand for blockIdx.x / gridDim.x, so a grouped launch
 // (conv_bwd_pair_kernel: the DGRAD and WGRAD GEMMs of one layer in ONE launch) can hand each
 // problem its own block range. ``smem`` = the launching kernel's single LDS array.
-template <int MODE, int BM, int BN, int NST, int BNF = 0>
-__device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned short* smem,
+template <int MODE, int BM, int BN, int NST, int BNF = 0, int XF = 0>
+__device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned short* smem_base,
                                                 const int bid, const int nblk) {
   constexpr int BK = 64;
+  static_assert(!XF || (MODE != MODE_FWD && BM <= 128 && BN <= 128), "XF: DGRAD/WGRAD, BM <= 128");
+  // XF: the coefficient table occupies the front of the LDS array, the ring follows
+  unsigned short* const smem = smem_base + (XF ? xf_table_elems(args.xc, args.xmask) : 0);
   constexpr int WTM = BM / 2, WTN = BN / 2;
   // BNF: 0 none, 1 = the preceding block is pooled (generic epilogue, window-argmax routing),
   // 2 = no pool (lean epilogue, same row offsets as the output). The generic epilogue also
@@ -236,6 +257,8 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
   constexpr int CA = BM * BK / 8 / 256;  // 16-B chunks per thread per tile
   constexpr int CB = BN * BK / 8 / 256;
   constexpr int TILE_A = BM * BK, TILE_B = BN * BK;
+  constexpr int TILE_G = XF ? TILE_A : 0;        // XF: the g operand, staged beside z
+  constexpr int STAGE = TILE_A + TILE_B + TILE_G;
   static_assert(CA >= 1 && CB >= 1, "tile too small for 256 threads");
   static_assert(NST >= 2 && NST <= 4, "2..4 LDS stages");
 
@@ -289,6 +312,8 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
   const int lcB = !BKM ? lcA : ((tid % (BN / 8)) ^ mc_swz<BN>(tid / (BN / 8)));
   const __amdgpu_buffer_rsrc_t rsA = make_rsrc(args.a, args.a_bytes);
   const __amdgpu_buffer_rsrc_t rsB = make_rsrc(args.b, args.b_bytes);
+  // XF: g has z's layout and size (a_bytes)
+  const __amdgpu_buffer_rsrc_t rsG = make_rsrc(XF ? args.xg : args.a, args.a_bytes);
 
   auto setup = [&](int item) {
     zsplit = item / tiles;
@@ -316,11 +341,14 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
           b_off[i] = col < args.Ng ? 2 * (col * args.Kg + lcB * 8) : (int)kOOB;
         }
       } else {  // DGRAD: row m of the k-step = output channel kc + m, columns = input channels
-        const int col = col0 + lcB * 8;
 #pragma unroll
-        for (int i = 0; i < CB; ++i)
+        for (int i = 0; i < CB; ++i) {
+          // chunk i lands on row m + (256 / (BN/8)) i; at BN = 256 that is m + 8 i, whose swizzle
+          // differs from row m's in bit 3 (mc_swz): the logical chunk follows the row
+          const int col = col0 + (lcB ^ swz_row_step<BN>(i)) * 8;
           b_off[i] = col < args.Ng ? 2 * (((tid + i * 256) / (BN / 8)) * gg.R * gg.S * gg.C + col)
                                    : (int)kOOB;
+        }
       }
       // decomposition of the first reduction index (fast: of the k-step; slow: of the chunk)
       const int kk = ks_begin * BK + (fast ? 0 : lcA * 8);
@@ -330,10 +358,11 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
       ks_ = rs - kr * Sdec;
     } else {
       constexpr int NCA = BM / 8;
-      const int kout = row0 + lcA * 8;
 #pragma unroll
-      for (int i = 0; i < CA; ++i)
+      for (int i = 0; i < CA; ++i) {
+        const int kout = row0 + (lcA ^ swz_row_step<BM>(i)) * 8;  // (BM = 256: see DGRAD's B)
         a_off[i] = kout < args.Mg ? 2 * (((tid + i * 256) / NCA) * gg.K + kout) : (int)kOOB;
+      }
       const int j = col0 + lcB * 8;
       const int rs = j / gg.C;
       xk.c = j - rs * gg.C;
@@ -347,8 +376,9 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
 
   // issue the LDS-DMA of k-step ks into buffer buf (and advance the incremental k state)
   auto issue = [&](int ks, int buf) {
-    unsigned short* As = smem + buf * (TILE_A + TILE_B);
+    unsigned short* As = smem + buf * STAGE;
     unsigned short* Bs = As + TILE_A;
+    unsigned short* Gs = Bs + TILE_B;
     const int k0 = ks * BK;
     if (MODE != MODE_WGRAD) {
       const int W_ = MODE == MODE_FWD ? gg.W : gg.Q;
@@ -363,6 +393,7 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
           else
             ok = (unsigned)(a_h0[i] - kr) < (unsigned)gg.P && (unsigned)(a_w0[i] - ks_) < (unsigned)gg.Q;
           dma_buf(rsA, ok ? a_off[i] + tap : (int)kOOB, As + (wid * 64 + 256 * i) * 8);
+          if (XF) dma_buf(rsG, ok ? a_off[i] + tap : (int)kOOB, Gs + (wid * 64 + 256 * i) * 8);
         }
         int boff;
         if (MODE == MODE_FWD) {
@@ -420,8 +451,10 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
       constexpr int NCB = BN / 8;
       const int ka = 2 * k0 * gg.K;
 #pragma unroll
-      for (int i = 0; i < CA; ++i)  // dy[m][kout]; m >= Kg lands past the buffer -> zeros
+      for (int i = 0; i < CA; ++i) {  // dy[m][kout]; m >= Kg lands past the buffer -> zeros
         dma_buf(rsA, a_off[i] + ka, As + (wid * 64 + 256 * i) * 8);
+        if (XF) dma_buf(rsG, a_off[i] + ka, Gs + (wid * 64 + 256 * i) * 8);
+      }
       // "same" convolution (stride 1, P == H, Q == W): the input pixel of output pixel m at tap
       // (r, s) is m + (r - pad) * W + (s - pad), so the offset is linear in m; only the border
       // test needs (p, q)
@@ -469,7 +502,7 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
   }
 
   auto compute = [&](int buf) {
-    const unsigned short* As = smem + buf * (TILE_A + TILE_B);
+    const unsigned short* As = smem + buf * STAGE;
     const unsigned short* Bs = As + TILE_A;
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 32) {
@@ -513,6 +546,76 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
           // operands swapped (D^T = B^T A^T): each lane ends up owning ONE output row and FOUR
           // consecutive output columns, so the epilogue stores 8 B (bf16) / 16 B (fp32) per lane
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  // ---------------- XF: BatchNorm-backward apply on the staged A operand ----------------
+  // Each thread rewrites exactly the A chunks its own DMAs filled (z at As, g at Gs, same slot):
+  // dz = xA * g + xB * z + xC for its 8 channels, zero for a padding / out-of-range chunk (its
+  // DMAs read zeros, but dz there is 0, not xC). Called once the stage's DMAs are retired by
+  // vmcnt + a barrier; a barrier after it publishes the rewritten chunks to the other waves.
+  // The coefficient table sits in front of the ring (loaded once per block).
+  auto xform = [&](int ks, int buf) {
+    unsigned short* As = smem + buf * STAGE;
+    const unsigned short* Gs = As + TILE_A + TILE_B;
+    const float* xct = reinterpret_cast<const float*>(smem_base);
+    int c0;
+    bool ok[CA];
+    if (MODE == MODE_DGRAD) {  // fast path only (host: K % 64 == 0, stride 1): uniform tap
+      const int k0 = ks * BK;
+      const int rs = k0 / gg.K;
+      const int kr_ = rs / gg.S, ks2 = rs - kr_ * gg.S;
+      c0 = k0 - rs * gg.K + lcA * 8;
+#pragma unroll
+      for (int i = 0; i < CA; ++i)
+        ok[i] = (unsigned)(a_h0[i] - kr_) < (unsigned)gg.P && (unsigned)(a_w0[i] - ks2) < (unsigned)gg.Q;
+    } else {  // WGRAD: rows = pixels ks*64 + m, columns = output channels (BM <= 128: one kout)
+      constexpr int NCA = BM / 8;
+      c0 = row0 + lcA * 8;
+#pragma unroll
+      for (int i = 0; i < CA; ++i)
+        ok[i] = c0 < args.Mg && ks * BK + (tid + i * 256) / NCA < args.Kg;
+    }
+    const bool xm = args.xmask;  // uniform
+    const float* cp = xct + (c0 >> 3) * (xm ? 40 : 24);
+    float xa[8], xb[8], xc8[8], xs[8], xh[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(cp + 4 * h);
+      const f32x4 b = *reinterpret_cast<const f32x4*>(cp + 8 + 4 * h);
+      const f32x4 d = *reinterpret_cast<const f32x4*>(cp + 16 + 4 * h);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { xa[4 * h + e] = a[e]; xb[4 * h + e] = b[e]; xc8[4 * h + e] = d[e]; }
+    }
+    if (xm) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(cp + 24 + 4 * h);
+        const f32x4 b = *reinterpret_cast<const f32x4*>(cp + 32 + 4 * h);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { xs[4 * h + e] = a[e]; xh[4 * h + e] = b[e]; }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < CA; ++i) {
+      unsigned short* slot = As + (tid + 256 * i) * 8;
+      u16x8 o;
+      if (ok[i]) {
+        const u16x8 zv = *reinterpret_cast<const u16x8*>(slot);
+        const u16x8 gv = *reinterpret_cast<const u16x8*>(Gs + (tid + 256 * i) * 8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float zf = bf2f(zv[e]);
+          float gf = bf2f(gv[e]);
+          // (the forward's ReLU input: bf16 z times the same fp32 scale / shift, bn_act.hip)
+          if (xm && !(zf * xs[e] + xh[e] > 0.f)) gf = 0.f;
+          o[e] = f2bf(fmaf(xa[e], gf, fmaf(xb[e], zf, xc8[e])));
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = 0;
+      }
+      *reinterpret_cast<u16x8*>(slot) = o;
     }
   };
 
@@ -779,25 +882,19 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
       const int row = row0 + wm * WTM + i * 16 + rl;
       if (!cok || row >= args.Mg) continue;
       const f32x4 v = acc[i][j];
-      if (MODE == MODE_WGRAD && (!split || args.wg_atomic)) {
+      if (MODE == MODE_WGRAD && !split) {
         if (g.wkrsc && g.Creal == g.C) {
           float* d = args.dw + ((size_t)row * g.R * g.S + wrs) * g.C + wc;
-          if (split) {
-#pragma unroll
-            for (int t = 0; t < 4; ++t) unsafeAtomicAdd(d + t, v[t]);
-          } else {
-            float4 o = *reinterpret_cast<float4*>(d);
-            o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
-            *reinterpret_cast<float4*>(d) = o;
-          }
+          float4 o = *reinterpret_cast<float4*>(d);
+          o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
+          *reinterpret_cast<float4*>(d) = o;
         } else {
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
             if (wc + t >= g.Creal) break;
             const size_t di = g.wkrsc ? ((size_t)row * g.R * g.S + wrs) * g.Creal + wc + t
                                       : ((size_t)row * g.Creal + wc + t) * g.R * g.S + wrs;
-            if (split) unsafeAtomicAdd(args.dw + di, v[t]);
-            else args.dw[di] += v[t];
+            args.dw[di] += v[t];
           }
         }
       } else if (split) {
@@ -912,62 +1009,13 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
   }
   };
 
-  // Split-K ticket fixup (FWD/DGRAD): add this split's partial tile into facc with device-scope
-  // (sc1) float atomics, drain them (vmcnt), then one arrival ticket per block. Only the block
-  // drawing the tile's last ticket continues: it reads the totals back with device-scope loads
-  // (coherent across the XCD L2s), clears facc and the ticket for the next launch, and leaves
-  // the totals in acc[][] for the plain (non-split) epilogue. No release fence is needed: the
-  // atomics are performed past the L2 before the ticket (cdna_hip_programming.md Guideline 16).
-  // (the arrival flag travels through the first word of the idle operand ring: every wave is
-  // past its last MFMA read at the barrier below, and reads the flag before the barrier that
-  // precedes the next item's DMA)
-  int* fix_last = reinterpret_cast<int*>(smem);
-  auto fixup = [&]() -> bool {
-    const int rl = lane & 15, cq = 4 * (lane >> 4);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = col0 + wn * WTN + j * 16 + cq;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = row0 + wm * WTM + i * 16 + rl;
-        if (col >= args.Ng || row >= args.Mg) continue;
-        float* d = args.facc + (size_t)row * args.Ng + col;
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-          __hip_atomic_fetch_add(d + t, acc[i][j][t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      const unsigned t = __hip_atomic_fetch_add(args.tickets + cur_tile, 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-      const bool last = t == (unsigned)(args.splits - 1);
-      if (last) __hip_atomic_store(args.tickets + cur_tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *fix_last = last ? 1 : 0;
-    }
-    __syncthreads();
-    if (!*fix_last) return false;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = col0 + wn * WTN + j * 16 + cq;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = row0 + wm * WTM + i * 16 + rl;
-        if (col >= args.Ng || row >= args.Mg) continue;
-        float* d = args.facc + (size_t)row * args.Ng + col;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          acc[i][j][t] = __hip_atomic_load(d + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(d + t, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-    }
-    return true;
-  };
-
   // NST-stage LDS ring: the DMAs of up to NST-1 k-steps are in flight while one is computed.
-  constexpr int DMA = CA + CB;  // vector-memory instructions per thread per stage
+  constexpr int DMA = CA + CB + (XF ? CA : 0);  // vector-memory instructions per thread per stage
+  if (XF) {  // the block's coefficient table (before any DMA is in flight)
+    float* xct = reinterpret_cast<float*>(smem_base);
+    for (int i = tid; i < args.xc * (args.xmask ? 5 : 3); i += 256) xct[i] = args.xcoef[i];
+    __syncthreads();
+  }
   for (int item = bid; item < nitems; item += nblk) {
     setup(item);
 #pragma unroll
@@ -978,23 +1026,38 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
 #pragma unroll
     for (int s = 0; s < NST - 1; ++s)
       if (kb + s < ke) issue(kb + s, s);
+    if (XF) {  // stage kb: retire its DMAs (all but the ones issued after it), barrier, rewrite
+      const int after = min(NST - 2, ke - 1 - kb);
+      if (NST >= 4 && after >= 2) wait_dma_barrier<(NST >= 4 ? 2 : 0) * DMA>();
+      else if (NST >= 3 && after >= 1) wait_dma_barrier<(NST >= 3 ? 1 : 0) * DMA>();
+      else wait_dma_barrier<0>();
+      xform(kb, 0);
+    }
     int stage = 0;
     for (int ks = kb; ks < ke; ++ks) {
       // stages issued after ks and still allowed in flight: min(NST-2, ke-1-ks)
       const int ahead = ke - 1 - ks;
+      if (XF) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the xform's LDS writes
       if (NST >= 4 && ahead >= 2) wait_dma_barrier<(NST >= 4 ? 2 : 0) * DMA>();
       else if (NST >= 3 && ahead >= 1) wait_dma_barrier<(NST >= 3 ? 1 : 0) * DMA>();
       else wait_dma_barrier<0>();
       // every wave finished computing ks-1: its buffer takes k-step ks+NST-1
       if (ks + NST - 1 < ke) issue(ks + NST - 1, stage == 0 ? NST - 1 : stage - 1);
       compute(stage);
-      stage = stage + 1 == NST ? 0 : stage + 1;
+      const int next = stage + 1 == NST ? 0 : stage + 1;
+      if (XF && ks + 1 < ke) {
+        // k-step ks+1: its DMAs were issued before the ones of ks+2.. (at most NST-2 stages,
+        // min(NST-2, ke-ks-2) of them real); retire it, barrier (LDS-DMA data is visible to a
+        // ds_read only after the issuing wave's vmcnt AND a barrier), rewrite the A chunks
+        const int after = ke - 2 - ks;
+        if (NST >= 4 && after >= 2) wait_dma_barrier<(NST >= 4 ? 2 : 0) * DMA>();
+        else if (NST >= 3 && after >= 1) wait_dma_barrier<(NST >= 3 ? 1 : 0) * DMA>();
+        else wait_dma_barrier<0>();
+        xform(ks + 1, next);
+      }
+      stage = next;
     }
-    if (MODE != MODE_WGRAD && args.splits > 1 && args.fixup) {
-      if (fixup()) epilogue(row0, col0, zsplit, false);
-    } else {
-      epilogue(row0, col0, zsplit, args.splits > 1);
-    }
+    epilogue(row0, col0, zsplit, args.splits > 1);
     // all reads of the ring done before the next item's prologue DMA. Not after the last item:
     // vmcnt also counts the epilogue's stores, and waiting for their acknowledgement would hold
     // the workgroup slot (and its registers) for a full memory round trip after the last MFMA
@@ -1008,21 +1071,21 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
 #ifndef DDP_CONV_WAVES_PER_EU
 #define DDP_CONV_WAVES_PER_EU 2
 #endif
-template <int MODE, int BM, int BN, int NST, int BNF = 0>
+template <int MODE, int BM, int BN, int NST, int BNF = 0, int XF = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DDP_CONV_WAVES_PER_EU)))
 void conv_igemm_kernel(ConvArgs args) {
   // dynamic: the launcher sizes the ring to the stages a work item can use (launch_gemm_t)
   extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
-  conv_igemm_body<MODE, BM, BN, NST, BNF>(args, smem, blockIdx.x, gridDim.x);
+  conv_igemm_body<MODE, BM, BN, NST, BNF, XF>(args, smem, blockIdx.x, gridDim.x);
 }
 
 // BNF 2 (no-pool BN-backward sums in the lean epilogue): the extra per-column coefficients push
 // the big tiles past 256 registers (1 wave per SIMD); ask the register allocator for 2 waves.
-template <int MODE, int BM, int BN, int NST>
+template <int MODE, int BM, int BN, int NST, int XF = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 void conv_igemm_bnf2_kernel(ConvArgs args) {
   extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
-  conv_igemm_body<MODE, BM, BN, NST, 2>(args, smem, blockIdx.x, gridDim.x);
+  conv_igemm_body<MODE, BM, BN, NST, 2, XF>(args, smem, blockIdx.x, gridDim.x);
 }
 
 // One layer's backward GEMMs in ONE launch: blocks [0, n_dg) run the DGRAD problem, the rest
@@ -1036,6 +1099,16 @@ __global__ __launch_bounds__(256) void conv_bwd_pair_kernel(ConvArgs dg, ConvArg
     conv_igemm_body<MODE_DGRAD, BM, BN, NST, BNF>(dg, smem, blockIdx.x, n_dg);
   else
     conv_igemm_body<MODE_WGRAD, BM, BN, NST, 0>(wg, smem, blockIdx.x - n_dg, gridDim.x - n_dg);
+}
+// The same with the BatchNorm-backward apply on both halves' A operand (XF): both GEMMs read dz
+// of this layer's BN backward, computed in LDS from z and g (dynamic LDS: table + XF ring)
+template <int BM, int BN, int NST, int BNF>
+__global__ __launch_bounds__(256) void conv_bwd_pair_xf_kernel(ConvArgs dg, ConvArgs wg, int n_dg) {
+  extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
+  if ((int)blockIdx.x < n_dg)
+    conv_igemm_body<MODE_DGRAD, BM, BN, NST, BNF, 1>(dg, smem, blockIdx.x, n_dg);
+  else
+    conv_igemm_body<MODE_WGRAD, BM, BN, NST, 0, 1>(wg, smem, blockIdx.x - n_dg, gridDim.x - n_dg);
 }
 
 // Split-K finish for FWD/DGRAD: sum the slabs in split order -> (+bias) bf16 output
@@ -1715,18 +1788,8 @@ static FastDiv make_fastdiv(int d) {
 
 static bool fits_buffer(size_t elems) { return elems * 2 < (size_t)kOOB; }
 
-static int g_wgrad_atomic = 0;  // WGRAD split-K through fp32 atomics: 0 never, 1 always, 2 small
-// split-K ticket fixup (FWD/DGRAD): 0 never, 1 always (when the buffers fit), 2 when the
-// atomic traffic splits x M x N x 4 B is at most g_fixup_bytes (small, launch-bound problems)
-static int g_fixup = 0;
-static size_t g_fixup_bytes = 8u << 20;
-static float* g_facc = nullptr;       // fp32 accumulation buffer (zero between launches)
-static size_t g_facc_elems = 0;
-static unsigned* g_tickets = nullptr;  // per-tile arrival tickets (zero between launches)
-static size_t g_tickets_n = 0;
 static int g_persistent = 0;    // grid = resident slots, blocks loop over work items
 static int g_stages = 2;        // LDS ring depth policy (see stages_for)
-constexpr int kMaxAtomicSplits = 32;
 constexpr int kNumCUs = 256;
 // LDS-staged FWD / DGRAD epilogue (conv_igemm_body); DDP_AMD_EPI_STAGE=0 restores the direct
 // fragment stores
@@ -1768,12 +1831,9 @@ static double tile_cost(int BM, int BN, const ConvArgs& a, size_t ws_elems, int*
   // padded work actually issued
   const double work = (double)tiles * BM * BN * ksteps * 64.0;
   const double t_mfma = work / (eff * fill) / 1.0e15 * 2.0;
-  // slab write + read at ~4 TB/s plus the finish launch (~3 us); atomics: one RMW per element
-  // per split, no finish pass
+  // slab write + read at ~4 TB/s plus the finish launch (~3 us)
   double t_split = 0.0;
-  if (splits > 1)
-    t_split = (a.wg_atomic && splits <= kMaxAtomicSplits) ? 4.0 * splits * (double)slab / 1.3e12
-                          : 8.0 * splits * (double)slab / 4.0e12 + 3.0e-6;
+  if (splits > 1) t_split = 8.0 * splits * (double)slab / 4.0e12 + 3.0e-6;
   return t_mfma + t_split;
 }
 
@@ -1786,9 +1846,9 @@ static int stages_for(int BM, int BN) {
   return 3;
 }
 
-template <int MODE, int BM, int BN, int NST, int BNF>
+template <int MODE, int BM, int BN, int NST, int BNF, int XF = 0>
 static void launch_gemm_t(const ConvArgs& a, int items, hipStream_t st) {
-  constexpr int kStageBytes = (BM + BN) * 64 * 2;
+  constexpr int kStageBytes = (BM + BN + (XF ? BM : 0)) * 64 * 2;
   // A work item of k k-steps touches min(NST, k) ring stages (the prologue issues k-steps
   // 0..NST-2, the loop refills the stage freed by the previous k-step only while k-steps
   // remain). Short reductions — the 1x1 convs over 64/128 channels, 1-2 k-steps — thus need a
@@ -1800,15 +1860,16 @@ static void launch_gemm_t(const ConvArgs& a, int items, hipStream_t st) {
   const int stages = std::max(1, std::min(NST, a.ksteps_per_split));
   size_t lds = (size_t)stages * kStageBytes;
   if (a.epi_stage && lds < (size_t)kTileBytes) lds = kTileBytes;
+  if (XF) lds += 2 * (size_t)xf_table_elems(a.xc, a.xmask);  // coefficient table, then the ring
   void (*kern)(ConvArgs);
-  if constexpr (BNF == 2 && MODE == MODE_DGRAD) kern = conv_igemm_bnf2_kernel<MODE, BM, BN, NST>;
-  else kern = conv_igemm_kernel<MODE, BM, BN, NST, BNF>;
+  if constexpr (BNF == 2 && MODE == MODE_DGRAD) kern = conv_igemm_bnf2_kernel<MODE, BM, BN, NST, XF>;
+  else kern = conv_igemm_kernel<MODE, BM, BN, NST, BNF, XF>;
   static bool attr = false;
   if (!attr) {
     // an error here surfaces through the caller's hipGetLastError
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                              std::max(NST * kStageBytes, kTileBytes));
+                              XF ? 160 * 1024 : std::max(NST * kStageBytes, kTileBytes));
     attr = true;
   }
   // persistent grid: at most the resident workgroup slots (queried once per instantiation)
@@ -1826,18 +1887,27 @@ static void launch_gemm_t(const ConvArgs& a, int items, hipStream_t st) {
 
 template <int MODE, int BM, int BN, int NST>
 static void launch_gemm(const ConvArgs& a, int items, hipStream_t st) {
+  if constexpr (MODE != MODE_FWD && BM <= 128 && BN <= 128 && NST <= 3) {
+    if (a.xg) {  // BatchNorm-backward apply on the A operand (xf_ok / launch_cfg checked it)
+      if constexpr (MODE == MODE_DGRAD) {
+        if (a.has_bnf && a.splits <= 1)
+          return a.bnf.pool ? launch_gemm_t<MODE, BM, BN, NST, 1, 1>(a, items, st)
+                            : launch_gemm_t<MODE, BM, BN, NST, 2, 1>(a, items, st);
+      }
+      return launch_gemm_t<MODE, BM, BN, NST, 0, 1>(a, items, st);
+    }
+  }
   if constexpr (MODE == MODE_DGRAD) {
-    // the BN-backward sums are reduced in the non-split epilogue: a single split, or the
-    // ticket fixup's last-arriving split block
-    if (a.has_bnf && (a.splits <= 1 || a.fixup))
+    // the BN-backward sums are reduced in the non-split epilogue: a single split only (split
+    // GEMMs reduce them in the finish kernel)
+    if (a.has_bnf && a.splits <= 1)
       return a.bnf.pool ? launch_gemm_t<MODE, BM, BN, NST, 1>(a, items, st)
                         : launch_gemm_t<MODE, BM, BN, NST, 2>(a, items, st);
   }
   launch_gemm_t<MODE, BM, BN, NST, 0>(a, items, st);
 }
 
-// Normalise the split count (no empty split), decide WGRAD atomics / FWD-DGRAD fixup; returns
-// the number of work items (tiles x splits).
+// Normalise the split count (no empty split); returns the number of work items (tiles x splits).
 template <int MODE, int BM, int BN>
 static int prepare_cfg(ConvArgs& a, int splits) {
   constexpr int BK = 64;
@@ -1856,28 +1926,13 @@ static int prepare_cfg(ConvArgs& a, int splits) {
     a.dPQ = make_fastdiv(std::max(1, a.g.P * a.g.Q));
     a.dQ = make_fastdiv(std::max(1, a.g.Q));
   }
-  // same-address fp32 atomics serialise: beyond kMaxAtomicSplits partial sums per element the
-  // slab + grouped-finish reduction is cheaper
-  const size_t atomic_bytes = 4ull * (size_t)splits * a.Mg * a.Ng;
-  if (a.wg_atomic == 2) a.wg_atomic = atomic_bytes <= g_fixup_bytes ? 1 : 0;
-  if (a.wg_atomic && splits > kMaxAtomicSplits) a.wg_atomic = 0;
-  if (MODE != MODE_WGRAD && splits > 1 && a.fixup >= 0 && g_facc != nullptr &&
-      (size_t)a.Mg * a.Ng <= g_facc_elems && (size_t)tiles <= g_tickets_n &&
-      (a.fixup == 1 || (g_fixup == 1) || (g_fixup == 2 && atomic_bytes <= g_fixup_bytes))) {
-    a.fixup = 1;
-    a.facc = g_facc;
-    a.tickets = g_tickets;
-  } else {
-    a.fixup = 0;
-  }
   return tiles * splits;
 }
 
 // split-K finish geometry / arguments of a prepared problem
 static bool needs_finish(int mode, const ConvArgs& a) {
-  if (a.splits <= 1) return false;
-  if (mode == MODE_WGRAD) return !a.wg_atomic;
-  return !a.fixup;
+  (void)mode;
+  return a.splits > 1;
 }
 
 // Rows per thread of the FWD / DGRAD split-K finish: 1 for small grids (<= 128 blocks at one
@@ -1947,7 +2002,7 @@ static int bn_bwd_fuse_max_rows() {
 }
 
 static bool bnbwd_fusable(const ConvArgs& a) {
-  return a.has_bnf && a.bnapply && a.splits > 1 && !a.fixup && !a.phase && !a.accumulate &&
+  return a.has_bnf && a.bnapply && a.splits > 1 && !a.phase && !a.accumulate &&
          a.Mg <= bn_bwd_fuse_max_rows() && a.Mg <= kBnBwdFuseMaxRows && a.Ng % 16 == 0 &&
          a.g.stride == 1 &&
          (!a.bnf.pool || (a.bnf.Hz == 2 * a.g.H && a.bnf.Wz == 2 * a.g.W)) &&
@@ -2057,6 +2112,7 @@ static void launch_cfg(ConvArgs& a, int splits, hipStream_t st, int nst_req = 0)
   constexpr int kMaxStages = kStageBytes * 4 <= 163840 ? 4 : (kStageBytes * 3 <= 163840 ? 3 : 2);
   int nst = nst_req >= 2 && nst_req <= 4 ? nst_req : stages_for(BM, BN);
   nst = std::min(nst, kMaxStages);
+  if (a.xg) nst = std::min(nst, (BM == 128 && BN == 128) ? 2 : 3);  // XF: g doubles the A bytes
   if constexpr (kMaxStages >= 4) {
     if (nst == 4) { launch_gemm<MODE, BM, BN, 4>(a, items, st); goto launched; }
   }
@@ -2096,7 +2152,19 @@ static int g_force_stages = 0;              // 2..4 (sweeps), 0 = policy
 // L2 -> LDS traffic per MFMA, fewer tiles)
 constexpr int kNumTiles = 8;
 
+// Tiles a mode may run. WGRAD keeps one tap decomposition of its B' (x) gather per thread, which
+// needs BN <= 128 (swz_row_step): 64x256 / 128x256 are never launched for WGRAD. (Before round 4
+// the 256-wide k-major tiles put odd DMA chunks in the wrong swizzled LDS slot — DGRAD 64x256 /
+// 128x256 computed a wrong dx, WGRAD 256x64 / 256x128 a wrong dW; tests/test_gpu_kernels.py
+// ::test_conv_every_tile now checks every tile in every mode.)
+template <int MODE>
+static bool tile_ok(int tile) {
+  if (MODE == MODE_WGRAD && (tile == 5 || tile == 7)) return false;
+  return tile >= 0 && tile < kNumTiles;
+}
+
 // tile / split-K / LDS-stage choice for a problem: the measured table, else the cost model
+// (a forced or tabulated tile the mode may not run falls back to the cost model's choice)
 template <int MODE>
 static void plan_mode(ConvArgs& a, size_t ws_elems, int* best_out, int* sp, int* nst_out) {
   const double c[4] = {tile_cost(128, 128, a, ws_elems, &sp[0]), tile_cost(128, 64, a, ws_elems, &sp[1]),
@@ -2104,7 +2172,7 @@ static void plan_mode(ConvArgs& a, size_t ws_elems, int* best_out, int* sp, int*
   int best = 0, nst = g_force_stages;
   for (int i = 1; i < 4; ++i)
     if (c[i] < c[best]) best = i;
-  if (g_force_tile >= 1 && g_force_tile <= kNumTiles) {
+  if (g_force_tile >= 1 && g_force_tile <= kNumTiles && tile_ok<MODE>(g_force_tile - 1)) {
     best = g_force_tile - 1;
     if (best >= 4) {
       static const int bmn[4][2] = {{256, 64}, {64, 256}, {256, 128}, {128, 256}};
@@ -2112,8 +2180,7 @@ static void plan_mode(ConvArgs& a, size_t ws_elems, int* best_out, int* sp, int*
     }
   } else if (a.splits <= 0) {
     auto it = g_tuned.find(TuneKey{MODE, a.Mg, a.Ng, a.Kg});
-    // (DGRAD on the 64x256 / 256x128 / 128x256 tiles computes a wrong dx: never from a table)
-    if (it != g_tuned.end() && !(MODE == MODE_DGRAD && it->second.tile >= 5)) {
+    if (it != g_tuned.end() && tile_ok<MODE>(it->second.tile)) {
       const size_t slab = (size_t)a.Mg * a.Ng;
       const int ksteps = (a.Kg + 63) / 64;
       int spl = std::max(1, std::min(it->second.splits, ksteps));
@@ -2123,6 +2190,11 @@ static void plan_mode(ConvArgs& a, size_t ws_elems, int* best_out, int* sp, int*
       sp[best] = spl;
       nst = it->second.stages;
     }
+  }
+  if (a.xg && best > 3) {  // XF kernels exist for the 128/64 tiles only
+    best = 0;
+    for (int i = 1; i < 4; ++i)
+      if (c[i] < c[best]) best = i;
   }
   *best_out = best;
   *nst_out = nst;
@@ -2138,28 +2210,19 @@ static void launch_mode(ConvArgs& a, size_t ws_elems, hipStream_t st) {
     case 2: launch_cfg<MODE, 64, 128>(a, sp[2], st, nst); break;
     case 3: launch_cfg<MODE, 64, 64>(a, sp[3], st, nst); break;
     case 4: launch_cfg<MODE, 256, 64>(a, sp[4], st, nst); break;
-    case 5: launch_cfg<MODE, 64, 256>(a, sp[5], st, nst); break;
     case 6: launch_cfg<MODE, 256, 128>(a, sp[6], st, nst); break;
-    default: launch_cfg<MODE, 128, 256>(a, sp[7], st, nst); break;
+    default:
+      if constexpr (MODE != MODE_WGRAD) {  // BN = 256 (tile_ok keeps WGRAD off them)
+        if (best == 5) launch_cfg<MODE, 64, 256>(a, sp[5], st, nst);
+        else launch_cfg<MODE, 128, 256>(a, sp[7], st, nst);
+      }
+      break;
   }
 }
 
-extern "C" void ddp_conv_options(int wgrad_atomic, int persistent, int stages) {
-  g_wgrad_atomic = wgrad_atomic;
+extern "C" void ddp_conv_options(int persistent, int stages) {
   g_persistent = persistent;
   g_stages = stages;
-}
-
-// Split-K ticket fixup: the zeroed accumulation / ticket buffers (allocated once per device by
-// ops/common.py, before any graph capture) and the policy (mode 0/1/2, byte threshold).
-extern "C" void ddp_conv_fixup(float* facc, size_t facc_elems, unsigned* tickets, size_t n_tickets,
-                               int mode, size_t max_bytes) {
-  g_facc = facc;
-  g_facc_elems = facc ? facc_elems : 0;
-  g_tickets = tickets;
-  g_tickets_n = tickets ? n_tickets : 0;
-  g_fixup = mode;
-  g_fixup_bytes = max_bytes;
 }
 
 // tile: index into the launch_mode table (0..kNumTiles-1)
@@ -2273,7 +2336,6 @@ extern "C" int ddp_conv_fwd_bn(const ConvGeom* g, const void* x, const void* wc,
   if (enabled && bn && a.Mg <= kBnFwdFuseMaxRows) {
     a.bnfwd = bn;
     a.bnfwd_done = &done;
-    a.fixup = -1;  // (the fused finish needs the slabs)
   }
   launch_mode<MODE_FWD>(a, ws_elems, st);
   const int e = (int)hipGetLastError();
@@ -2296,7 +2358,6 @@ extern "C" int ddp_conv_fwd_finish(const ConvGeom* g, float* ws, int splits, con
   a.Ng = g->K;
   a.Kg = g->R * g->S * g->C;
   a.splits = splits;
-  a.fixup = 0;
   static const bool bn_enabled = [] {
     const char* e = std::getenv("DDP_AMD_BN_FWD_FUSE");
     return !(e && e[0] == '0');
@@ -2309,13 +2370,29 @@ extern "C" int ddp_conv_fwd_finish(const ConvGeom* g, float* ws, int splits, con
   return (int)hipGetLastError();
 }
 
+// XF (BatchNorm-backward apply on the A operand) is available for: WGRAD always; DGRAD of a
+// stride-1 conv with K % 64 == 0 (the uniform-tap fast path), not accumulating into dx
+static bool xf_dgrad_ok(const ConvGeom* g) { return g->stride == 1 && g->K % 64 == 0; }
+static void set_xf(ConvArgs& a, const BnBwdXf* xf) {
+  if (!xf) return;
+  a.a = (const unsigned short*)xf->z;
+  a.xg = (const unsigned short*)xf->g;
+  a.xcoef = xf->coef;
+  a.xc = xf->C;
+  a.xmask = xf->mask;
+}
+extern "C" int ddp_conv_xf_ok(const ConvGeom* g, int need_dx) {
+  return (g->K % 8 == 0 && g->C % 8 == 0 && (!need_dx || xf_dgrad_ok(g))) ? 1 : 0;
+}
+
 static int conv_dgrad_impl(const ConvGeom* g, const void* dy, const void* wc, void* dx,
                            float* ws, size_t ws_elems, int splits, int accumulate,
                            const BnBwdFuse* bn, const BnBwdApply* ba, int* bn_done,
-                           hipStream_t st) {
+                           hipStream_t st, const BnBwdXf* xf = nullptr) {
   if (bn_done) *bn_done = 0;
   if (g->C % 8 || g->K % 8) return -1;
   if (bn && (accumulate || g->stride != 1)) return -3;  // fused BN sums: plain stride-1 dgrad only
+  if (xf && (accumulate || !xf_dgrad_ok(g) || xf->C != g->K)) return -4;
   ConvArgs a{};
   a.accumulate = accumulate;
   if (bn) {
@@ -2337,6 +2414,7 @@ static int conv_dgrad_impl(const ConvGeom* g, const void* dy, const void* wc, vo
     return -2;
   a.a_bytes = (int)(2 * dya);
   a.b_bytes = (int)(2 * wb);
+  set_xf(a, xf);
   if (g->stride == 1) {
     a.Mg = g->N * g->H * g->W;
     a.Kg = g->R * g->S * g->K;
@@ -2397,16 +2475,32 @@ extern "C" int ddp_conv_dgrad_bn(const ConvGeom* g, const void* dy, const void* 
   return conv_dgrad_impl(g, dy, wc, dx, ws, ws_elems, splits, 0, bn, ba, bn_done, st);
 }
 
+extern "C" int ddp_conv_wgrad_xf(const ConvGeom* g, const void* dy, const void* x, float* dw,
+                                 float* ws, size_t ws_elems, int splits, const BnBwdXf* xf,
+                                 hipStream_t st);
 extern "C" int ddp_conv_wgrad(const ConvGeom* g, const void* dy, const void* x, float* dw,
                               float* ws, size_t ws_elems, int splits, hipStream_t st) {
+  return ddp_conv_wgrad_xf(g, dy, x, dw, ws, ws_elems, splits, nullptr, st);
+}
+
+extern "C" int ddp_conv_dgrad_xf(const ConvGeom* g, const void* wc, void* dx, float* ws,
+                                 size_t ws_elems, const BnBwdFuse* bn, const BnBwdApply* ba,
+                                 int* bn_done, const BnBwdXf* xf, hipStream_t st) {
+  if (!xf) return -1;
+  return conv_dgrad_impl(g, nullptr, wc, dx, ws, ws_elems, 0, 0, bn, ba, bn_done, st, xf);
+}
+
+extern "C" int ddp_conv_wgrad_xf(const ConvGeom* g, const void* dy, const void* x, float* dw,
+                                 float* ws, size_t ws_elems, int splits, const BnBwdXf* xf,
+                                 hipStream_t st) {
   if (g->C % 8 || g->K % 8) return -1;
+  if (xf && xf->C != g->K) return -4;
   ConvArgs a{};
   a.g = *g;
   a.a = (const unsigned short*)dy;
   a.b = (const unsigned short*)x;
   a.dw = dw;
   a.ws = ws;
-  a.wg_atomic = g_wgrad_atomic;
   if (g->R * g->S == 1) a.g.wkrsc = 1;  // 1x1: [K][C][1][1] == [K][1][1][C]
   a.Mg = g->K;
   a.Ng = g->R * g->S * g->C;
@@ -2418,6 +2512,7 @@ extern "C" int ddp_conv_wgrad(const ConvGeom* g, const void* dy, const void* x, 
   a.b_bytes = (int)(2 * xb);
   a.dPQ = make_fastdiv(g->P * g->Q);
   a.dQ = make_fastdiv(g->Q);
+  set_xf(a, xf);
   launch_mode<MODE_WGRAD>(a, ws_elems, st);
   return (int)hipGetLastError();
 }
@@ -2442,13 +2537,14 @@ extern "C" void ddp_conv_pair_mode(int m, int items) {
 extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* wc, void* dx,
                                  const void* x, float* dw, float* ws, size_t ws_elems,
                                  const BnBwdFuse* bn, const BnBwdApply* ba, int* bn_done,
-                                 hipStream_t st) {
+                                 hipStream_t st, const BnBwdXf* xf) {
   if (bn_done) *bn_done = 0;
   if (!bn) ba = nullptr;
+  if (xf && (!xf_dgrad_ok(g) || xf->C != g->K)) return -4;
   auto separate = [&]() -> int {
-    const int r = ddp_conv_wgrad(g, dy, x, dw, ws, ws_elems, 0, st);
+    const int r = ddp_conv_wgrad_xf(g, dy, x, dw, ws, ws_elems, 0, xf, st);
     if (r) return r;
-    return conv_dgrad_impl(g, dy, wc, dx, ws, ws_elems, 0, 0, bn, ba, bn_done, st);
+    return conv_dgrad_impl(g, dy, wc, dx, ws, ws_elems, 0, 0, bn, ba, bn_done, st, xf);
   };
   if (g_pair_mode == 0 || g->stride != 1 || g->C % 8 || g->K % 8 || g->Creal != g->C)
     return separate();
@@ -2479,7 +2575,6 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
   w.b = (const unsigned short*)x;
   w.dw = dw;
   w.ws = ws;
-  w.wg_atomic = g_wgrad_atomic;
   w.Mg = g->K;
   w.Ng = g->R * g->S * g->C;
   w.Kg = g->N * g->P * g->Q;
@@ -2487,6 +2582,8 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
   w.b_bytes = (int)(2 * xb);
   w.dPQ = make_fastdiv(g->P * g->Q);
   w.dQ = make_fastdiv(g->Q);
+  set_xf(d, xf);
+  set_xf(w, xf);
   // measured pair entry (tools/conv_tune.py --pairs) or forced splits (its sweep) first
   bool tuned = false;
   int sd = 1, sw = 1;
@@ -2528,12 +2625,30 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
   const size_t wneed = needs_finish(MODE_WGRAD, w) ? (size_t)w.splits * w.Mg * w.Ng : 0;
   if (dneed + wneed > ws_elems) return separate();
   if (g_pair_mode == 3 && !both64 && itd + itw > g_pair_items) return separate();
-  if (d.has_bnf && (d.splits <= 1 || d.fixup))
+  const bool bnf1 = d.has_bnf && d.splits <= 1;
+  if (xf) {
+    static const bool attr = [] {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv_bwd_pair_xf_kernel<64, 64, 3, 0>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv_bwd_pair_xf_kernel<64, 64, 3, 1>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      return true;
+    }();
+    (void)attr;
+    const size_t lds = 2 * (size_t)xf_table_elems(xf->C, xf->mask) + 3 * (size_t)(64 + 64 + 64) * 64 * 2;
+    if (bnf1)
+      hipLaunchKernelGGL((conv_bwd_pair_xf_kernel<64, 64, 3, 1>), dim3(itd + itw), dim3(256), lds,
+                         st, d, w, itd);
+    else
+      hipLaunchKernelGGL((conv_bwd_pair_xf_kernel<64, 64, 3, 0>), dim3(itd + itw), dim3(256), lds,
+                         st, d, w, itd);
+  } else if (bnf1) {
     hipLaunchKernelGGL((conv_bwd_pair_kernel<64, 64, 3, 1>), dim3(itd + itw), dim3(256), 0, st,
                        d, w, itd);
-  else
+  } else {
     hipLaunchKernelGGL((conv_bwd_pair_kernel<64, 64, 3, 0>), dim3(itd + itw), dim3(256), 0, st,
                        d, w, itd);
+  }
   const bool fd = needs_finish(MODE_DGRAD, d), fw = needs_finish(MODE_WGRAD, w);
   if (fd && fw && w.g.wkrsc && bnbwd_fusable(d)) {
     const WgFinishArgs wa = wg_finish_args(w);

@@ -17,6 +17,14 @@ namespace ddp_amd {
                                " at " __FILE__ ":" + std::to_string(__LINE__));          \
   } while (0)
 
+#define KERNEL_OK(x)                                                                     \
+  do {                                                                                   \
+    const int k_ = (x);                                                                  \
+    if (k_ != 0)                                                                         \
+      throw std::runtime_error(std::string("kernel launch failed (") + std::to_string(k_) + \
+                               ") at " __FILE__ ":" + std::to_string(__LINE__));         \
+  } while (0)
+
 #define NCCL_OK(x)                                                                       \
   do {                                                                                   \
     ncclResult_t r_ = (x);                                                               \
@@ -106,7 +114,7 @@ void RcclComm::broadcast(void* buf, size_t count, int dtype, int root, hipStream
 
 void RcclComm::all_gather(const void* send, void* recv, size_t count, int dtype, hipStream_t st) {
   if (comm_ == nullptr) {
-    if (send != recv) HIP_OK(hipMemcpyAsync(recv, send, count * dtype_bytes(dtype), hipMemcpyDeviceToDevice, st));
+    if (send != recv) KERNEL_OK(ddp_copy_bytes(recv, send, count * dtype_bytes(dtype), st));
     return;
   }
   NCCL_OK(ncclAllGather(send, recv, count, to_nccl(dtype), comm_, st));
@@ -115,7 +123,7 @@ void RcclComm::all_gather(const void* send, void* recv, size_t count, int dtype,
 void RcclComm::reduce_scatter(const void* send, void* recv, size_t count, int dtype, int op,
                               hipStream_t st) {
   if (comm_ == nullptr) {
-    if (send != recv) HIP_OK(hipMemcpyAsync(recv, send, count * dtype_bytes(dtype), hipMemcpyDeviceToDevice, st));
+    if (send != recv) KERNEL_OK(ddp_copy_bytes(recv, send, count * dtype_bytes(dtype), st));
     return;
   }
   NCCL_OK(ncclReduceScatter(send, recv, count, to_nccl(dtype), to_op(op), comm_, st));
@@ -134,12 +142,14 @@ void RcclComm::gather(const void* send, void* recv, size_t count, int dtype, int
       NCCL_OK(ncclRecv((char*)recv + (size_t)root * bytes, count, dt, rank_, comm_, st));
       NCCL_OK(ncclGroupEnd());
     } else if ((const char*)recv + (size_t)root * bytes != send) {
-      HIP_OK(hipMemcpyAsync((char*)recv + (size_t)root * bytes, send, bytes, hipMemcpyDeviceToDevice, st));
+      KERNEL_OK(ddp_copy_bytes((char*)recv + (size_t)root * bytes, send, bytes, st));
     }
     return;
   }
+  // the root's own slot: a copy KERNEL, not hipMemcpyAsync (a captured step must stay a graph of
+  // kernel nodes; see ddp_copy_bytes)
   if (rank_ == root)
-    HIP_OK(hipMemcpyAsync((char*)recv + (size_t)root * bytes, send, bytes, hipMemcpyDeviceToDevice, st));
+    KERNEL_OK(ddp_copy_bytes((char*)recv + (size_t)root * bytes, send, bytes, st));
   NCCL_OK(ncclGroupStart());
   if (rank_ == root) {
     for (int r = 0; r < world_; ++r)
@@ -161,12 +171,12 @@ void RcclComm::scatter(const void* send, void* recv, size_t count, int dtype, in
       NCCL_OK(ncclRecv(recv, count, dt, rank_, comm_, st));
       NCCL_OK(ncclGroupEnd());
     } else if ((const char*)send + (size_t)root * bytes != recv) {
-      HIP_OK(hipMemcpyAsync(recv, (const char*)send + (size_t)root * bytes, bytes, hipMemcpyDeviceToDevice, st));
+      KERNEL_OK(ddp_copy_bytes(recv, (const char*)send + (size_t)root * bytes, bytes, st));
     }
     return;
   }
   if (rank_ == root && (const char*)send + (size_t)root * bytes != recv)
-    HIP_OK(hipMemcpyAsync(recv, (const char*)send + (size_t)root * bytes, bytes, hipMemcpyDeviceToDevice, st));
+    KERNEL_OK(ddp_copy_bytes(recv, (const char*)send + (size_t)root * bytes, bytes, st));
   NCCL_OK(ncclGroupStart());
   if (rank_ == root) {
     for (int r = 0; r < world_; ++r)
@@ -188,16 +198,22 @@ void RcclComm::scatter_replicated(void* buf, size_t count, int dtype, int root, 
     // and a receive that wrote nothing shows up as NaN in buf (tests/test_gpu_rccl_self.py)
     const size_t bytes = count * dtype_bytes(dtype);
     if (bytes > stage_bytes_) {
-      if (stage_) HIP_OK(hipFree(stage_));
-      HIP_OK(hipMalloc(&stage_, bytes));
-      stage_bytes_ = bytes;
+      // growing the staging buffer is a hipMalloc / hipFree: illegal inside a stream capture.
+      // Callers reserve the largest size before capturing (reserve_stage); refuse otherwise
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      HIP_OK(hipStreamIsCapturing(st, &cs));
+      if (cs != hipStreamCaptureStatusNone)
+        throw std::runtime_error("scatter_replicated: staging buffer must be reserved before "
+                                 "graph capture (RcclComm::reserve_stage)");
+      reserve_stage(bytes);
     }
-    HIP_OK(hipMemsetAsync(stage_, 0xff, bytes, st));
+    // fill + copy-back are kernels (a captured memset node did not order before its readers)
+    KERNEL_OK(ddp_fill_bytes(stage_, 0xff, bytes, st));
     NCCL_OK(ncclGroupStart());
     NCCL_OK(ncclSend(buf, count, dt, rank_, comm_, st));
     NCCL_OK(ncclRecv(stage_, count, dt, rank_, comm_, st));
     NCCL_OK(ncclGroupEnd());
-    HIP_OK(hipMemcpyAsync(buf, stage_, bytes, hipMemcpyDeviceToDevice, st));
+    KERNEL_OK(ddp_copy_bytes(buf, stage_, bytes, st));
     return;
   }
   NCCL_OK(ncclGroupStart());
@@ -208,6 +224,17 @@ void RcclComm::scatter_replicated(void* buf, size_t count, int dtype, int root, 
     NCCL_OK(ncclRecv(buf, count, dt, root, comm_, st));
   }
   NCCL_OK(ncclGroupEnd());
+}
+
+void RcclComm::reserve_stage(size_t bytes) {
+  if (bytes <= stage_bytes_) return;
+  if (stage_) {
+    HIP_OK(hipDeviceSynchronize());  // the old buffer may still be read by queued work
+    HIP_OK(hipFree(stage_));
+    stage_ = nullptr;
+  }
+  HIP_OK(hipMalloc(&stage_, bytes));
+  stage_bytes_ = bytes;
 }
 
 void RcclComm::send(const void* buf, size_t count, int dtype, int peer, hipStream_t st) {

@@ -51,6 +51,9 @@ class RcclComm {
   // scatter of `world` identical copies (reference 2A: dist.scatter(grad, [mean]*ws, src=0)):
   // root sends the same buffer to every peer over its own xGMI link; peers receive into buf.
   void scatter_replicated(void* buf, size_t count, int dtype, int root, hipStream_t st);
+  // world 1 with a live communicator: size the scatter_replicated receive staging buffer ahead
+  // of a graph capture (growing it during a capture would be a hipMalloc inside the capture)
+  void reserve_stage(size_t bytes);
   void send(const void* buf, size_t count, int dtype, int peer, hipStream_t st);
   void recv(void* buf, size_t count, int dtype, int peer, hipStream_t st);
   // Returns the RCCL async error code (0 == ncclSuccess).

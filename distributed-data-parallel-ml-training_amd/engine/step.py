@@ -221,7 +221,7 @@ class SegmentedDDPStep(TrainStep):
     WAIT_TIMEOUT_S = 100.0  # a device-side wait that exceeds this records an error and returns
 
     def __init__(self, ddp, optimizer, criterion, loader, split=4, emulate=0, emulate_gbps=0.0,
-                 emulate_scale=1.0, grad_comm="fp32", zero=False):
+                 emulate_scale=1.0, grad_comm="fp32", zero=False, collectives=True):
         super().__init__(ddp, optimizer, criterion, loader, sync=None, use_graph=True)
         inner = getattr(ddp, "module", None)
         if inner is None or not hasattr(inner, "forward_loss_split") or not self.fold_opt:
@@ -256,7 +256,9 @@ class SegmentedDDPStep(TrainStep):
         prio = os.environ.get("DDP_AMD_COMM_PRIORITY", "high")
         self.comm_stream = torch.cuda.Stream(priority=-1 if prio == "high" else 0)
         self.comm_a = None
-        if is_live(ddp.comm):
+        # collectives=False: no bucket all-reduce at all (profile_stage_times: per-segment
+        # compute times of a cut-everywhere step on a multi-rank job, state rolled back after)
+        if collectives and is_live(ddp.comm):
             from ..parallel.comm import RcclCommunicator
             self.comm_a = RcclCommunicator(ddp.comm.rank, ddp.comm.world, ddp.comm.device,
                                            key="ddp_amd/rccl_uid_overlap", self_comm=True)
@@ -405,12 +407,18 @@ class SegmentedDDPStep(TrainStep):
         self.graphs = graphs
         self.graph = graphs[0]  # "captured" marker for the shared helpers
 
-    def step(self):
+    def step(self, seg_events=None):
+        """One replayed step. ``seg_events``: list receiving a timing event recorded on the main
+        stream before the first and after every segment graph (profile_stage_times)."""
         if self.graph is None:  # never captured, or validate_distributed fell back to eager
             self._body()
             return
+        if seg_events is not None:
+            seg_events.append(self._probe_event(torch.cuda.current_stream()))
         for j, g in enumerate(self.graphs):
             g.replay()
+            if seg_events is not None:
+                seg_events.append(self._probe_event(torch.cuda.current_stream()))
             self._comm(j)
 
     def check_error(self):
@@ -428,3 +436,41 @@ class SegmentedDDPStep(TrainStep):
         v = super().pop_loss()
         self.check_error()
         return v
+
+
+def profile_stage_times(ddp, optimizer, criterion, loader, n_stages, reps=4):
+    """Backward time of every fused stage at this per-GPU batch, measured on the device: a
+    pipelined step cut before EVERY stage and without collectives is captured and replayed
+    ``reps`` times with timing events between its segment graphs (the comm stream still runs
+    each bucket's SGD, as in the real step). Segment j of that step is stage n_stages-1-j;
+    stage n_stages-1's time also holds the forward, the classifier head and the data step.
+    Parameters, momentum and the data cursor are rolled back afterwards (without collectives
+    the replicas' updates would differ), so training continues from the same state on every
+    rank. Returns a list of n_stages floats (us, median over reps). Feeds
+    parallel/cut_plan.plan_cuts."""
+    arena = ddp.arena
+    snap = (arena.data.clone(), optimizer.momentum_buffer.clone(), loader.cursor.clone())
+    st = SegmentedDDPStep(ddp, optimizer, criterion, loader, split=list(range(1, n_stages)),
+                          collectives=False)
+    try:
+        st.warmup(1)
+        st.capture()
+        runs = []
+        for r in range(reps + 1):
+            evs = []
+            st.step(seg_events=evs)
+            torch.cuda.synchronize()
+            if r:  # the first replay warms the graphs up
+                runs.append([evs[i].elapsed_time(evs[i + 1]) * 1000.0 for i in range(len(evs) - 1)])
+        st.check_error()
+    finally:
+        torch.cuda.synchronize()
+        st.graphs = st.graph = None
+        arena.data.copy_(snap[0])
+        optimizer.momentum_buffer.copy_(snap[1])
+        loader.cursor.copy_(snap[2])
+        arena.grad.zero_()
+        optimizer.repack()
+        torch.cuda.synchronize()
+    per_seg = [sorted(col)[len(col) // 2] for col in zip(*runs)]
+    return per_seg[::-1]  # segment j = stage n_stages-1-j

@@ -13,17 +13,13 @@ def native():
     global _NATIVE
     if _NATIVE is None:
         _NATIVE = _load()
-        # DDP_AMD_WGRAD_ATOMIC=1: split-K weight gradients accumulate with fp32 atomics (no
-        # finish pass, but memory-side atomics run at ~1.3 TB/s vs ~6 TB/s for slab stores);
-        # default 0 = slab + grouped finish reduction
         # DDP_AMD_CONV_PERSISTENT=1: conv grids sized to the resident slots, blocks loop over
-        # tiles and prefetch the next tile's first k-step (default 0: one tile per workgroup)
+        # tiles (default 0: one tile per workgroup)
         # DDP_AMD_CONV_STAGES: LDS ring depth policy of the conv GEMMs (2 = double buffering)
-        # DDP_AMD_WGRAD_ATOMIC: 0 (default) = slabs + finish, 1 = atomics, 2 = atomics for
-        # small problems (split x M x N x 4 B <= DDP_AMD_FIXUP_KB), slabs for large ones
-        # (2 measured 6-60% slower steps, profiles/r2_launch_reduction_ab.md)
-        _NATIVE.conv_options(int(os.environ.get("DDP_AMD_WGRAD_ATOMIC", "0")),
-                             int(os.environ.get("DDP_AMD_CONV_PERSISTENT", "0")),
+        # (split-K always goes through fp32 slabs + a deterministic finish: the fp32-atomic
+        # variants measured 6-60 % slower steps, profiles/r2_launch_reduction_ab.md, and were
+        # removed in round 4)
+        _NATIVE.conv_options(int(os.environ.get("DDP_AMD_CONV_PERSISTENT", "0")),
                              int(os.environ.get("DDP_AMD_CONV_STAGES", str(CONV_STAGES))))
         # DDP_AMD_BWD_PAIR: one layer's wgrad + dgrad as ONE grouped launch — 0 never,
         # 1 when both problems pick the 64x64 tile, 2 always (stride-1 layers), 3 (default)
@@ -111,32 +107,12 @@ def check(t, dtype=None, shape=None, name="tensor"):
 WORKSPACE_ELEMS = 32 << 20  # 128 MiB of the 288 GB HBM
 _WS = {}
 
-# Split-K ticket fixup (conv_igemm.hip): small split-K problems (the strong-scaling batches: 32
-# images per GPU at 8 GPUs) accumulate their partial tiles with fp32 atomics and the last split
-# block of each tile runs the epilogue — no slab pass, no finish launch. One zeroed accumulation
-# buffer + one ticket array per process (the kernels leave both zero). Policy:
-# DDP_AMD_FIXUP=0 (default) never / 1 always / 2 when splits x M x N x 4 B <= DDP_AMD_FIXUP_KB.
-# OFF by default: measured on MI355X the device-scope atomics (they bypass the per-XCD L2s) make
-# the fixed-up GEMMs 3-5x slower than slab + finish (b32 step 0.884 vs 0.548 ms,
-# profiles/r2_launch_reduction_ab.md).
-FIXUP_ELEMS = 4 << 20
-FIXUP_TICKETS = 1 << 16
-FIXUP_MODE = int(os.environ.get("DDP_AMD_FIXUP", "0"))
-FIXUP_KB = int(os.environ.get("DDP_AMD_FIXUP_KB", "8192"))
-
-
 def workspace(device):
     key = str(device)
     ws = _WS.get(key)
     if ws is None:
         ws = torch.empty(WORKSPACE_ELEMS, dtype=torch.float32, device=device)
         _WS[key] = ws
-        if not _WS.get("_fixup"):
-            facc = torch.zeros(FIXUP_ELEMS, dtype=torch.float32, device=device)
-            tickets = torch.zeros(FIXUP_TICKETS, dtype=torch.int32, device=device)
-            _WS["_fixup"] = (facc, tickets)
-            native().conv_fixup(facc.data_ptr(), FIXUP_ELEMS, tickets.data_ptr(), FIXUP_TICKETS,
-                                FIXUP_MODE, FIXUP_KB << 10)
     return ws
 
 
@@ -197,13 +173,12 @@ def join_side_streams():
         st.join()
 
 
-# BatchNorm backward: DDP_AMD_BN_LAST_BLOCK=1 lets the reduce kernel's last block (ticket
-# counter) finalize the coefficients instead of a separate one-block launch. OFF by default:
-# measured slower on MI355X (VGG-11 b256 1.020 vs 0.965 ms/step, ResNet-50 b64 11.81 vs 10.07;
-# with an agent release fence per block 1.044 / 15.29) — every block must drain its memory-side
-# atomics before its ticket, and the single ticket address serialises thousands of blocks,
-# which costs more than the ~5 us launch it saves.
-BN_LAST_BLOCK = os.environ.get("DDP_AMD_BN_LAST_BLOCK", "0") == "1"
+# BatchNorm backward without its apply pass (bn_act.hip ddp_bn_bwd_xf + conv_igemm.hip XF): the
+# reduce kernel stores dy_bn, the finalize writes the per-channel affine form of dz, and the
+# producing conv's backward GEMMs compute dz = A dy_bn + B z + C while staging their A operand —
+# dz is never written and never re-read. Layers the one-launch local BN backward serves keep it.
+# DDP_AMD_BN_BWD_XF=0 restores reduce -> finalize -> apply -> GEMMs on dz.
+BN_BWD_XF = os.environ.get("DDP_AMD_BN_BWD_XF", "1") != "0"
 
 
 # BatchNorm-backward sums of a Conv->BN->ReLU(->pool) block accumulated by the NEXT block's

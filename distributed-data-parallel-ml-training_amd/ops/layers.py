@@ -65,12 +65,12 @@ class ConvBNActSpec:
         self.stats = sc.take(STAT_REPLICAS * 2 * K)[:STAT_REPLICAS * 2 * K]
         sums = sc.take(STAT_REPLICAS * 2 * K + 64)
         self.sums = sums[:STAT_REPLICAS * 2 * K]
-        # ticket counter of the BN-backward reduce kernel's in-launch finalize (zeroed with the
-        # rest of the scratch each forward, and reset by the finalizing block)
-        self.bwd_counter = sums[STAT_REPLICAS * 2 * K:STAT_REPLICAS * 2 * K + 1]
         # per-layer BN coefficient table [6][K] (scale, shift, mean, invstd | k1, k2): written
         # by the forward's finalize kernel, read by the backward (one use per step per layer)
         self.coef = torch.empty(6 * K, dtype=F32, device=dev)
+        # apply-free BN backward (BN_BWD_XF): [K/8][3 or 5][8] affine form of dz (+ the ReLU
+        # mask's scale / shift) for the conv GEMMs
+        self.xcoef = torch.empty(5 * K, dtype=F32, device=dev)
         # BnBwdFuse chaining (VGG): ``prev`` is the Conv->BN->ReLU(->pool) block that produces
         # this block's input; this block's dgrad accumulates prev's BatchNorm-backward sums in
         # its epilogue and sets ``prev.sums_ready`` so prev's backward skips its reduce pass
@@ -237,11 +237,6 @@ HEAD_BN_FUSE = os.environ.get("DDP_AMD_HEAD_BN_FUSE", "1") != "0"
 # ... with the head's dW / db in the same launch (=0: a separate linear_bwd launch)
 HEAD_ONE_LAUNCH = os.environ.get("DDP_AMD_HEAD_ONE_LAUNCH", "1") != "0"
 BN_BWD_FUSE_MAX_HW = int(os.environ.get("DDP_AMD_BN_BWD_FUSE_MAX_HW", "16"))
-# residual blocks (ResNet bn3): the forward stores the ReLU mask as bits and the backward reads
-# those instead of the residual tensor (two fewer full-tensor reads per block). Opt-in (=1):
-# measured neutral on ResNet-50 b256 (26.95 / 27.01 vs 26.98 / 27.00 ms, same box) — the byte
-# loads cost about what the 16-B residual loads did
-RELU_MASK = os.environ.get("DDP_AMD_RELU_MASK", "0") == "1"
 # preceding block without a max-pool (ResNet's conv1 -> conv2 -> conv3 chain): one z load per
 # dgrad output element in the epilogue would replace a whole dy + z pass of the reduce kernel,
 # but measured on ResNet-50 b256 the BNF epilogue makes the big dgrad GEMMs slower than the pass
@@ -262,20 +257,39 @@ def bn_bwd_fuse_pays(H, W, pool=True):
     return H * W <= BN_BWD_FUSE_MAX_HW
 
 
-def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=None, bna=None):
+def conv_xf_ok(spec, x, need_dx, link=None):
+    """Can this layer's backward GEMMs take the BatchNorm-backward apply on their A operand
+    (conv_igemm.hip XF)? Not for an accumulating second-branch dgrad (ResNet GradLink) nor for
+    the opt-in tap-reuse dgrad."""
+    if need_dx and ((link is not None and link.buf is not None) or spec.wt is not None):
+        return False
+    N, H, W, _ = x.shape
+    return bool(native().conv_xf_ok(spec.geom(N, H, W), int(bool(need_dx))))
+
+
+def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=None, bna=None,
+                  xf=None):
     """dW += wgrad(dz, x); returns dx (or None). With ``weight`` (the parameter whose gradient
     is dweight) and the backward side stream enabled, the wgrad runs on the side stream and the
     parameter is announced ready there (common.side_stream); otherwise everything is stream-
     ordered on the current stream and the caller announces the gradient.
     ``bna`` = (dz_prev, dgamma_prev, dbeta_prev) pointers (with ``bnf``): the preceding block's
     whole BatchNorm backward may be completed in the dgrad's split-K finish; the return value is
-    then (dx, done) — when done, dx was NOT written and dz_prev / dgamma / dbeta were."""
+    then (dx, done) — when done, dx was NOT written and dz_prev / dgamma / dbeta were.
+    ``xf`` = (z, dy_bn, xcoef, K) pointers: dz is not a tensor — both GEMMs compute it from the
+    BatchNorm's input z and output gradient dy_bn while staging their A operand (``dz`` is then
+    None; conv_xf_ok must have said yes)."""
     N, H, W, C = x.shape
     g = spec.geom(N, H, W, weight_krsc(dweight))
     s = stream_handle()
     ws = workspace(x.device)
-    if (need_dx and link is None and bna is None and bnf is None and spec.wt is not None
-            and not _common.BWD_SIDE_STREAM
+    if xf is not None:
+        if dz is not None:
+            raise ValueError("conv_backward: pass either dz or xf")
+        if need_dx and ((link is not None and link.buf is not None) or spec.wt is not None):
+            raise ValueError("conv_backward: xf cannot serve an accumulating / tap-reuse dgrad")
+    if (xf is None and need_dx and link is None and bna is None and bnf is None
+            and spec.wt is not None and not _common.BWD_SIDE_STREAM
             and native().conv_tr_would_serve(g, ws.numel(), -1)):
         # tap-reuse backward-data (conv_tr.hip) + the weight gradient as its own launch
         native().conv_wgrad(g, ptr(dz), ptr(x), ptr(dweight), ptr(ws), ws.numel(), 0, s)
@@ -291,7 +305,7 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=Non
         # kernel policy allows it (conv_igemm.hip ddp_conv_bwd_pair), else the two launches
         dx = torch.empty_like(x)
         done = native().conv_bwd_pair(g, ptr(dz), ptr(spec.wc), ptr(dx), ptr(x), ptr(dweight),
-                                      ptr(ws), ws.numel(), s, bn=bnf, bna=bna)
+                                      ptr(ws), ws.numel(), s, bn=bnf, bna=bna, xf=xf)
         if weight is not None:
             grad_ready([weight])
         return (dx, bool(done)) if bna is not None else dx
@@ -299,10 +313,10 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=Non
         side = side_stream(x.device, x, dz)
         with torch.cuda.stream(side.stream):
             native().conv_wgrad(g, ptr(dz), ptr(x), ptr(dweight), ptr(side.ws), side.ws.numel(), 0,
-                                side.stream.cuda_stream)
+                                side.stream.cuda_stream, xf=xf)
             grad_ready([weight])
     else:
-        native().conv_wgrad(g, ptr(dz), ptr(x), ptr(dweight), ptr(ws), ws.numel(), 0, s)
+        native().conv_wgrad(g, ptr(dz), ptr(x), ptr(dweight), ptr(ws), ws.numel(), 0, s, xf=xf)
         if weight is not None:
             grad_ready([weight])
     if not need_dx:
@@ -317,7 +331,7 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=Non
         return link.result()
     dx = torch.empty_like(x)
     done = native().conv_dgrad(g, ptr(dz), ptr(spec.wc), ptr(dx), ptr(ws), ws.numel(), 0, s,
-                               bn=bnf, bna=bna)
+                               bn=bnf, bna=bna, xf=xf)
     if link is not None:
         link.seen += 1
         link.buf = dx
@@ -389,7 +403,6 @@ class _ConvBNActFn(torch.autograd.Function):
             z = conv_forward(spec, x, bias, stats, fin=fin)
         spec.fwd_z = z
         ctx.pool3_idx = None
-        ctx.rmask = None
         spec.last_deferred = (not fused and not spec.maxpool3
                               and _defer_bn(spec, residual, rm, N, Ho, Wo))
         if spec.maxpool3:
@@ -403,16 +416,11 @@ class _ConvBNActFn(torch.autograd.Function):
         elif spec.last_deferred:
             spec.deferred = y  # computed by the next block's conv (conv_tr.hip fused input)
         elif not fused:
-            if residual is not None and spec.relu and RELU_MASK and torch.is_grad_enabled():
-                # ReLU mask bits for the backward instead of re-reading the residual (bn_act.hip
-                # BnArgs::rmask: 1 byte per 8 channels vs 16)
-                ctx.rmask = torch.empty(N * P * Q * spec.K // 8, dtype=torch.uint8,
-                                        device=x.device)
             native().bn_act_fwd(N, P, Q, spec.K, int(spec.pool), int(spec.relu), spec.eps, ptr(z),
                                 ptr(residual), ptr(stats), ptr(gamma), ptr(beta), ptr(y),
                                 stream_handle(), ptr(rm), ptr(rv),
                                 float(bn.momentum if bn.momentum is not None else 0.1),
-                                use_running, ptr(spec.coef), rmask=ptr(ctx.rmask))
+                                use_running, ptr(spec.coef))
         ctx.spec = spec
         ctx.has_res = residual is not None
         ctx.in_link, ctx.res_link = in_link, res_link
@@ -435,7 +443,27 @@ class _ConvBNActFn(torch.autograd.Function):
         sums_ready, spec.sums_ready = spec.sums_ready, False
         dz_done, spec.dz_fused = spec.dz_fused, None
         spec.fwd_z = None
-        if dz_done is not None:
+        xf = None
+        need_dx = ctx.needs_input_grad[0]
+        if (_common.BN_BWD_XF and dz_done is None and ctx.pool3_idx is None and not sums_ready
+                and native().bn_bwd_xf_ok(N, P, Q, K, int(spec.pool), int(ctx.has_res), 0)
+                and conv_xf_ok(spec, x, need_dx, ctx.in_link)):
+            # apply-free BatchNorm backward: reduce (+ dy_bn) and finalize here, dz computed by
+            # the conv backward GEMMs below from (z, dy_bn) — never stored (conv_igemm.hip XF)
+            dy = dy.contiguous()
+            # pooled / residual blocks: the reduce stores dy_bn (routed, masked; also the
+            # residual gradient); plain blocks: the GEMMs mask the raw dy themselves
+            plain = not spec.pool and not ctx.has_res
+            dyb = None if plain else torch.empty_like(z)
+            native().bn_bwd_xf(N, P, Q, K, int(spec.pool), int(spec.relu), spec.eps, ptr(z),
+                               ptr(residual), ptr(dy), ptr(sums), ptr(dyb), ptr(spec.xcoef),
+                               ptr(gg), ptr(gbt), ptr(spec.coef), stream_handle())
+            xf = (ptr(z), ptr(dy) if plain else ptr(dyb), ptr(spec.xcoef), K,
+                  int(plain and spec.relu))
+            dz = None
+            if dres is not None:
+                dres = dyb  # the residual branch's gradient IS dy_bn
+        elif dz_done is not None:
             # the next block's dgrad finish already ran this block's whole BN backward (dz,
             # dgamma, dbeta; conv_igemm.hip splitk_finish_bnbwd_kernel): dy was never written
             dz, zref = dz_done
@@ -455,14 +483,7 @@ class _ConvBNActFn(torch.autograd.Function):
             native().bn_act_bwd(N, P, Q, K, int(spec.pool), int(spec.relu), spec.eps, ptr(z),
                                 ptr(residual), ptr(stats), ptr(gamma), ptr(beta), ptr(dy),
                                 ptr(sums), ptr(dz), ptr(dres), ptr(gg), ptr(gbt), ptr(gb),
-                                stream_handle(), ptr(spec.coef),
-                                ptr(spec.bwd_counter) if _common.BN_LAST_BLOCK else 0,
-                                sums_ready=int(sums_ready),
-                                # arrival counter of the clustered one-launch backward (zeroed
-                                # with the statistics every forward; bn_act.hip)
-                                grid_sync=0 if _common.BN_LAST_BLOCK else ptr(spec.bwd_counter),
-                                rmask=ptr(ctx.rmask))
-            ctx.rmask = None
+                                stream_handle(), ptr(spec.coef), sums_ready=int(sums_ready))
         grad_ready([gamma, beta, bias])
         if ctx.res_link is not None and dres is not None:
             dres = ctx.res_link.offer(dres)
@@ -481,7 +502,7 @@ class _ConvBNActFn(torch.autograd.Function):
                        ptr(ensure_grad(prev.bn.bias)))
         if bna is not None:
             dx, done = conv_backward(spec, x, dz, gw, ctx.needs_input_grad[0], ctx.in_link,
-                                     weight=weight, bnf=bnf, bna=bna)
+                                     weight=weight, bnf=bnf, bna=bna, xf=xf)
             if done:  # prev's backward skips its BN backward; dx was not written
                 prev.dz_fused = (dz_prev, ctx.prev_z)
             else:
@@ -490,7 +511,7 @@ class _ConvBNActFn(torch.autograd.Function):
             if bnf is not None:
                 prev.sums_ready = True
             dx = conv_backward(spec, x, dz, gw, ctx.needs_input_grad[0], ctx.in_link,
-                               weight=weight, bnf=bnf)
+                               weight=weight, bnf=bnf, xf=xf)
         ctx.prev_z = None
         return dx, None, None, None, None, dres, None, None, None
 

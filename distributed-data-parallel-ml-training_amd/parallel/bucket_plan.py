@@ -118,8 +118,16 @@ def probe_table(comm, world, dtype="fp32", device="cuda", sizes=None, iters=10, 
     sizes = sizes or [1 << k for k in range(18, 27, 2)]  # 256 KiB .. 64 MiB
     dt = torch.bfloat16 if dtype == "bf16" else torch.float32
     rows = allreduce_sweep(comm, sizes, dtype=dt, device=device, iters=iters, warmup=warmup)
-    if not all(r.get("correct", True) for r in rows):
-        raise RuntimeError("start-up all-reduce probe returned wrong sums")
+    ok = all(r.get("correct", True) for r in rows)
+    # decide together: a rank that raised alone would leave its peers blocked in the next
+    # collective (a late watchdog failure instead of this clear error)
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int64)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        ok = bool(flag.item())
+    if not ok:
+        raise RuntimeError("start-up all-reduce probe returned wrong sums (on at least one rank)")
     rows = [{k: r[k] for k in ("bytes", "us", "algbw_GBps", "busbw_GBps")} for r in rows]
     return {"worlds": {str(world): {"source": "measured at start-up", dtype: rows}}}
 

@@ -212,6 +212,13 @@ class RcclCommunicator:
         self.comm.gather(t.data_ptr(), buf.data_ptr() if buf is not None else 0, t.numel(),
                          _DT[t.dtype], dst, self._s())
 
+    def reserve_staging(self, nbytes):
+        """Pre-size the single-rank scatter staging buffer (before any graph capture; during a
+        capture this is a no-op and scatter_replicated refuses to grow the buffer)."""
+        if torch.cuda.is_current_stream_capturing():
+            return
+        self.comm.reserve_stage(int(nbytes))
+
     def scatter_replicated(self, t, src=0):
         self.comm.scatter_replicated(t.data_ptr(), t.numel(), _DT[t.dtype], src, self._s())
 

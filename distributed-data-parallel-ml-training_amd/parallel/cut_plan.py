@@ -1,0 +1,131 @@
+"""Backward cut points of the pipelined multi-GPU DDP step, chosen on the node.
+
+The pipelined step (engine/step.py SegmentedDDPStep) cuts the captured backward before some
+fused stages; after each segment the comm stream all-reduces that segment's gradient bucket and
+runs its share of the SGD while the earlier layers are still back-propagating. Which cuts are
+best depends on two measured curves of the machine it runs on:
+
+* how long each fused stage's backward takes at this per-GPU batch (``stage_us``, timed with
+  device events on segment graphs cut at EVERY stage: engine/step.py ``profile_stage_times``),
+  and
+* how long an all-reduce of a bucket takes (the start-up probe's bus-bandwidth rows,
+  ``bucket_plan.probe_table``, or ``comm_tuning.json``).
+
+``plan_cuts`` replays the step's two-stream schedule for every candidate cut set and keeps the
+one with the earliest finish: the main stream runs segment j, then the comm stream (in bucket
+order, one stream) waits for it and runs bucket j's all-reduce + its SGD; every extra cut costs a
+graph boundary plus a flag signal / wait (``seg_overhead_us``). The step ends when both the last
+segment and the last bucket's update are done; "exposed" = the part of the communication that is
+not hidden under the backward.
+
+Reference: torch DDP's fixed 25 MB buckets, rebuilt after iteration 0
+(/root/reference/part3/main.py:174); SURVEY.md §5.8 (bucket sizing for 7 xGMI links).
+"""
+import itertools
+
+from .bucket_plan import predict_us
+
+# measured on one MI355X (profiles/r2_pipelined_ddp.md, "World 1" section): each extra segment
+# boundary (graph launch gap + flag signal + flag wait) costs ~4.5-5 us
+SEG_OVERHEAD_US = 5.0
+# fused SGD + bf16 re-pack per fp32 parameter byte (sgd_pack_kernel: 42 us for VGG-11's 36.9 MB)
+SGD_US_PER_BYTE = 42.4 / 36.9e6
+# the comm stream's flag wait + RCCL launch, per bucket
+COMM_OVERHEAD_US = 4.0
+# a collective occupies CUs (RCCL channels / the stand-in's 32 workgroups): the backward that runs
+# under it is slowed by about this fraction of the overlap
+CONTENTION = 0.15
+
+
+def _overlap(a, b, spans):
+    return sum(max(0.0, min(b, e) - max(a, s)) for s, e in spans)
+
+
+def schedule(stage_us, param_bytes, cuts, rows, wire_scale=1.0, head_bytes=0,
+             seg_overhead_us=SEG_OVERHEAD_US, sgd_us=None, comm_overhead_us=COMM_OVERHEAD_US,
+             contention=CONTENTION):
+    """Replay one pipelined step with cuts before the stages in ``cuts``.
+
+    stage_us[i]: backward time of fused stage i (stage S-1's entry also carries the forward and
+    the classifier head: every candidate's first segment contains it). param_bytes[i]: fp32
+    bytes of stage i's parameters (head_bytes: the classifier's, in the first bucket).
+    wire_scale: wire bytes per fp32 byte (0.5 for a bf16 wire). sgd_us(bytes) -> update time
+    (default: SGD_US_PER_BYTE). Returns a dict with the step time, the per-bucket wire bytes, the
+    predicted all-reduce time per bucket and the exposed communication time."""
+    S = len(stage_us)
+    cuts = sorted(set(int(c) for c in cuts))
+    if any(not 0 < c < S for c in cuts):
+        raise ValueError(f"cuts must lie in 1..{S - 1}")
+    sgd = sgd_us or (lambda b: b * SGD_US_PER_BYTE)
+    bounds = [S] + cuts[::-1] + [0]
+    t_main = 0.0
+    free = 0.0
+    buckets, ar, busy = [], [], []
+    free_before_last = 0.0
+    for j in range(len(bounds) - 1):
+        if j == len(bounds) - 2:
+            free_before_last = free
+        lo, hi = bounds[j + 1], bounds[j]
+        seg = sum(stage_us[lo:hi]) + (seg_overhead_us if j > 0 else 0.0)
+        # (one pass: the buckets launched so far slow this segment by their overlap with it)
+        t_main += seg + contention * _overlap(t_main, t_main + seg, busy)
+        pb = sum(param_bytes[lo:hi]) + (head_bytes if j == 0 else 0)
+        wire = int(pb * wire_scale)
+        t_ar = predict_us(rows, wire) if rows else 0.0
+        start = max(t_main, free) + comm_overhead_us
+        free = start + t_ar + sgd(pb)
+        busy.append((start, start + t_ar))
+        buckets.append(wire)
+        ar.append(t_ar)
+    end = max(t_main, free)
+    # slack: how long before the end of the backward the earlier buckets are all done (a plan
+    # that finishes them with margin tolerates a slower collective than the probe measured)
+    return {"cuts": cuts, "step_us": end, "backward_us": t_main, "exposed_us": end - t_main,
+            "slack_us": t_main - free_before_last, "bucket_bytes": buckets, "allreduce_us": ar}
+
+
+def schedule_inline(stage_us, param_bytes, rows, wire_scale=1.0, head_bytes=0, sgd_us=None):
+    """One graph, one bucket all-reduced inline after the whole backward (cuts = [])."""
+    sgd = sgd_us or (lambda b: b * SGD_US_PER_BYTE)
+    pb = sum(param_bytes) + head_bytes
+    wire = int(pb * wire_scale)
+    t_ar = predict_us(rows, wire) if rows else 0.0
+    t = sum(stage_us)
+    return {"cuts": [], "step_us": t + t_ar + sgd(pb), "backward_us": t,
+            "exposed_us": t_ar + sgd(pb), "bucket_bytes": [wire], "allreduce_us": [t_ar]}
+
+
+def plan_cuts(stage_us, param_bytes, rows, wire_scale=1.0, head_bytes=0, max_cuts=3,
+              seg_overhead_us=SEG_OVERHEAD_US, sgd_us=None, comm_overhead_us=COMM_OVERHEAD_US,
+              tie_us=1.0, candidates=None, contention=CONTENTION):
+    """Best cut set and the predicted schedules of the candidates: (best_schedule, ranked list
+    of (step_us, cuts)). Among the sets within ``tie_us`` of the fastest: the fewest cuts, then
+    the most slack (the earlier buckets finish furthest ahead of the end of the backward).
+    ``candidates``: restrict the search to these cut sets (default: every set of 1..max_cuts)."""
+    S = len(stage_us)
+    if S < 2:
+        raise ValueError("need at least two stages")
+    if candidates is None:
+        candidates = [c for k in range(1, min(max_cuts, S - 1) + 1)
+                      for c in itertools.combinations(range(1, S), k)]
+    cands = []
+    for c in candidates:
+        c = tuple(sorted(c))
+        r = schedule(stage_us, param_bytes, c, rows, wire_scale, head_bytes,
+                     seg_overhead_us, sgd_us, comm_overhead_us, contention)
+        cands.append((r["step_us"], len(c), c, r))
+    fastest = min(t for t, _, _, _ in cands)
+    near = [x for x in cands if x[0] <= fastest + tie_us]
+    near.sort(key=lambda x: (x[1], -x[3]["slack_us"], x[0]))
+    best = near[0][3]
+    ranked = sorted(((round(t, 1), list(c)) for t, _, c, _ in cands))
+    return best, ranked
+
+
+def stand_in_rows(world, algbw_GBps, sizes=None):
+    """Bus-bandwidth rows of a fixed-algorithm-bandwidth collective (the one-GPU timed stand-in of
+    profiles/r2_pipelined_ddp.md: bytes / algbw), in the comm_tuning.json row format."""
+    sizes = sizes or [1 << k for k in range(12, 27)]
+    f = 2 * (world - 1) / world
+    return [{"bytes": s, "us": s / (algbw_GBps * 1e3), "algbw_GBps": algbw_GBps,
+             "busbw_GBps": algbw_GBps * f} for s in sizes]

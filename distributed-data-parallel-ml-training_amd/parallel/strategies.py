@@ -37,6 +37,10 @@ def sync_gradients_gather_scatter(model, comm, root=0):
     staging = None
     if comm.rank == root:
         staging = _staging(params[0].grad.device, comm.world, maxn)
+    if comm.world == 1 and hasattr(comm, "reserve_staging"):
+        # single-rank RCCL: the self send/recv of the scatter lands in a staging buffer that
+        # must exist before a capture (no allocation inside a captured step)
+        comm.reserve_staging(maxn * params[0].grad.element_size())
     s = stream_handle()
     for p in params:
         g = p.grad

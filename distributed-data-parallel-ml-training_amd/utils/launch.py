@@ -15,8 +15,13 @@ use this module when no launcher set ``WORLD_SIZE``:
   stdout goes to stderr;
 * every child runs in its own session: on a child failure (after a grace period for its
   peers to notice) or on the overall timeout the parent kills every child's process group and
-  returns non-zero (the failing rank's code, or 124 on timeout).
+  returns non-zero (the failing rank's code, or 124 on timeout);
+* the ranks never outlive the launcher: SIGTERM / SIGHUP / SIGINT to the parent kill every
+  rank's process group before the parent exits with 128 + signal, and each child also carries
+  a parent-death signal (``prctl(PR_SET_PDEATHSIG, SIGKILL)``), which covers a parent killed
+  with SIGKILL — the ranks would otherwise keep their GPUs and RCCL communicators.
 """
+import ctypes
 import os
 import signal
 import socket
@@ -59,6 +64,46 @@ def rank_env(rank, world, port, addr="127.0.0.1", base=None):
     return env
 
 
+_PR_SET_PDEATHSIG = 1
+
+
+def _child_setup():
+    """preexec_fn of every rank (runs in the forked child before exec): SIGKILL when the
+    launcher dies, whatever kills it."""
+    try:
+        libc = ctypes.CDLL(None, use_errno=True)
+        libc.prctl(_PR_SET_PDEATHSIG, signal.SIGKILL, 0, 0, 0)
+    except (OSError, AttributeError):
+        pass
+
+
+class _SignalGuard:
+    """Within the ``with`` block, SIGTERM / SIGHUP / SIGINT kill the ranks, then exit the parent
+    with 128 + signal (only installable from the main thread; a no-op elsewhere)."""
+
+    SIGNALS = (signal.SIGTERM, signal.SIGHUP, signal.SIGINT)
+
+    def __init__(self, procs, log):
+        self.procs, self.log, self.old = procs, log, {}
+
+    def _handler(self, signum, frame):
+        self.log(f"launcher got signal {signum}: killing {len(self.procs)} ranks")
+        _kill_all(self.procs)
+        os._exit(128 + signum)
+
+    def __enter__(self):
+        import threading
+        if threading.current_thread() is threading.main_thread():
+            for s in self.SIGNALS:
+                self.old[s] = signal.signal(s, self._handler)
+        return self
+
+    def __exit__(self, *exc):
+        for s, h in self.old.items():
+            signal.signal(s, h)
+        return False
+
+
 def spawn(cmd, nprocs, timeout_s=None, addr="127.0.0.1", port=None, grace_s=15.0, poll_s=0.05,
           log=None):
     """Run ``cmd`` (argv list) as ``nprocs`` ranks; return 0 when every rank exits 0, else the
@@ -68,11 +113,13 @@ def spawn(cmd, nprocs, timeout_s=None, addr="127.0.0.1", port=None, grace_s=15.0
     check_no_gpu_init()
     port = port or free_port(addr)
     procs = []
+    guard = _SignalGuard(procs, log)
     try:
+        guard.__enter__()
         for r in range(nprocs):
             out = None if r == 0 else sys.stderr
             procs.append(subprocess.Popen(cmd, env=rank_env(r, nprocs, port, addr), stdout=out,
-                                          start_new_session=True))
+                                          start_new_session=True, preexec_fn=_child_setup))
         t0 = time.monotonic()
         failed_at, rc_fail = None, 0
         while True:
@@ -99,6 +146,8 @@ def spawn(cmd, nprocs, timeout_s=None, addr="127.0.0.1", port=None, grace_s=15.0
     except BaseException:
         _kill_all(procs)
         raise
+    finally:
+        guard.__exit__()
 
 
 def _kill_all(procs):

@@ -595,3 +595,91 @@ def test_vgg11_b256_trajectory_matches_bf16_emulated_oracle(native_ext):
     assert lg[-1] < lg[0] and le[-1] < le[0]
     assert cos(dg, de) >= 0.95 and cos(dg, de) >= cos(dg, dg2) - 0.03
     assert cos(dg, df) >= 0.9
+
+
+def test_vgg11_lr01_headline_regime_tracks_fp32_family(native_ext):
+    """Numerics in the HEADLINE regime: the bench's own synthetic batches (on-device crop / flip /
+    normalise, 256 images) at the reference's lr 0.1, momentum 0.9, wd 1e-4
+    (/root/reference/part1/main.py:124-125), 20 SGD steps. At lr 0.1 a random-init VGG-11 is
+    chaotic for the first steps (the loss spikes well above ln 10), so per-step agreement is only
+    meaningful while the trajectories have not separated; after that the fused path must stay in
+    the family of fp32 runs whose initial weights differ by bf16 rounding noise.
+
+    Runs (all on the same batches): fused bf16 GPU path x2 (its own noise floor), the
+    bf16-emulating oracle, plain fp32 ATen, and two fp32 runs from weights perturbed by a
+    relative 2^-9 (half a bf16 ulp) — the fp32 model's own sensitivity to bf16-sized noise.
+    Requirements (derived from that family, not fitted to the fused path):
+      * the spike is the model's: fp32's peak and the fused peak are both above 2 ln 10 or
+        both below;
+      * while the fp32 family agrees within 2 % (k < k0), fused tracks the emulated oracle within
+        3x its self-noise + 1 %;
+      * the fused mean loss over steps 10..19 (the bench's timed window after warm-up) lies in
+        the family's range widened by 25 %, and the fused final loss is below its peak."""
+    import math
+    from ddp_amd.models import VGG11
+    from ddp_amd.optim import FusedSGD
+    from ddp_amd.data import SyntheticCIFAR10, DeviceLoader
+    from ddp_amd.ops.layers import to_nhwc_input  # noqa: F401  (import check of the fused ops)
+    steps, B, lr = 20, 256, 0.1
+    torch.manual_seed(89395)
+    base = VGG11()
+    ld = DeviceLoader(SyntheticCIFAR10(True, n=B * steps), B, "cuda", cpad=8)
+    batches = []
+    for _ in range(steps):
+        x, y = ld.fill(advance=True)
+        batches.append((x[..., :3].permute(0, 3, 1, 2).float().contiguous(), y.clone().long()))
+    torch.cuda.synchronize()
+
+    def run_fused():
+        m = copy.deepcopy(base).cuda()
+        opt = FusedSGD(m.parameters(), lr=lr, momentum=0.9, weight_decay=1e-4)
+        ls = []
+        for x, y in batches:
+            opt.zero_grad()
+            loss = torch.nn.functional.cross_entropy(m(x), y)
+            loss.backward()
+            opt.step()
+            ls.append(float(loss))
+        return ls
+
+    def run_aten(fwd, perturb_seed=None):
+        m = copy.deepcopy(base).cuda()
+        if perturb_seed is not None:
+            g = torch.Generator(device="cuda").manual_seed(perturb_seed)
+            with torch.no_grad():
+                for p in m.parameters():
+                    p.mul_(1 + (2.0 ** -9) * torch.randn(p.shape, generator=g, device="cuda"))
+        opt = torch.optim.SGD(m.parameters(), lr=lr, momentum=0.9, weight_decay=1e-4)
+        ls = []
+        for x, y in batches:
+            opt.zero_grad()
+            loss = torch.nn.functional.cross_entropy(fwd(m, x), y)
+            loss.backward()
+            opt.step()
+            ls.append(float(loss))
+        return ls
+
+    lg, lg2 = run_fused(), run_fused()
+    le = run_aten(_emulated_vgg_forward)
+    lf = run_aten(_plain_vgg_forward)
+    lp = [run_aten(_plain_vgg_forward, s) for s in (1, 2)]
+    for name, ls in (("fused", lg), ("fused2", lg2), ("emu", le), ("fp32", lf), ("fp32~1", lp[0]),
+                     ("fp32~2", lp[1])):
+        print(f"{name:7s}", [round(v, 3) for v in ls])
+    fam = [lf, le] + lp
+    assert all(math.isfinite(v) for v in lg + lg2)
+    spike = 2 * math.log(10)
+    assert (max(lf) > spike) == (max(lg) > spike), (max(lf), max(lg))
+    # steps where the fp32 family still agrees within 2 %
+    k0 = 0
+    while k0 < steps and max(abs(f[k0] - lf[k0]) / abs(lf[k0]) for f in fam) < 0.02:
+        k0 += 1
+    floor = max([abs(a - b) / abs(b) for a, b in zip(lg[:k0], lg2[:k0])] + [0.0])
+    for k in range(k0):
+        assert abs(lg[k] - le[k]) / abs(le[k]) <= 3 * floor + 0.01, (k, lg[k], le[k], floor)
+    w = slice(10, steps)
+    means = [sum(f[w]) / len(f[w]) for f in fam]
+    mg = sum(lg[w]) / len(lg[w])
+    print("k0", k0, "window means: fused %.3f family %s" % (mg, [round(v, 3) for v in means]))
+    assert min(means) / 1.25 <= mg <= max(means) * 1.25, (mg, means)
+    assert lg[-1] < max(lg)

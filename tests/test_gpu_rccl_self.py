@@ -254,3 +254,97 @@ def test_segmented_step_wait_timeout_skips_update_and_raises(native_ext, live):
     with pytest.raises(RuntimeError, match="timed out"):
         st.pop_loss()  # the training loop's per-window loss read surfaces it too
     m.close()
+
+
+@pytest.mark.parametrize("strategy", ["gather_scatter", "gather_broadcast", "allreduce"])
+def test_captured_strategy_step_with_live_rccl(native_ext, strategy):
+    """2A / 2B inside a CAPTURED whole step (TrainStep(sync=...)) on a live one-rank
+    communicator: the grouped self send/recv, the root-slot copy and the scatter staging fill /
+    copy-back are all kernel or RCCL nodes of the graph (no hipMemcpyAsync / hipMemsetAsync
+    nodes, csrc/runtime/comm.cpp). With the 2A staging buffer NaN-filled before every run, the
+    replayed step must apply the same update as an eager step without any sync (a one-rank mean
+    is the identity) and leave no NaN. Reference: part2/part2a/main.py:97-115,
+    part2/part2b/main.py:97-103."""
+    from ddp_amd.models import VGG11
+    from ddp_amd.optim import FusedSGD
+    from ddp_amd.data import SyntheticCIFAR10, DeviceLoader
+    from ddp_amd.engine import TrainStep, CrossEntropyLoss
+    from ddp_amd.parallel import RcclCommunicator, STRATEGIES
+    from ddp_amd.parallel import strategies as strat
+    from ddp_amd.engine.step import capture_mode
+    torch.manual_seed(13)
+    c = RcclCommunicator(0, 1, 0, self_comm=True)
+    assert capture_mode() == "thread_local"
+    m = VGG11().cuda()
+    opt = FusedSGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    ld = DeviceLoader(SyntheticCIFAR10(True, n=256), 32, "cuda")
+    ref_step = TrainStep(m, opt, CrossEntropyLoss(), ld, sync=None)
+    st = TrainStep(m, opt, CrossEntropyLoss(), ld, sync=lambda mod: STRATEGIES[strategy](mod, c))
+    arena = opt.arena
+    snap = (arena.data.clone(), opt.momentum_buffer.clone(), ld.cursor.clone())
+
+    def run(fn):
+        arena.data.copy_(snap[0])
+        opt.momentum_buffer.copy_(snap[1])
+        ld.cursor.copy_(snap[2])
+        arena.grad.zero_()
+        for sp in m.fused_plan():
+            sp._packed_version = None
+            sp.maybe_pack()
+        for buf in strat._STAGING.values():
+            buf.fill_(float("nan"))
+        torch.cuda.synchronize()
+        fn()
+        torch.cuda.synchronize()
+        return arena.data - snap[0]
+
+    e_ref = [run(ref_step._body), run(ref_step._body)]
+    e_sync = run(st._body)
+    st.warmup(1)
+    st.capture()
+    assert st.graph is not None
+    replays = [run(st.step), run(st.step)]
+    tol = min(0.99, _cos(e_ref[0], e_ref[1]) - 0.005)
+    assert float(e_ref[0].norm()) > 0
+    for d in [e_sync] + replays:
+        assert not torch.isnan(d).any()
+        assert _cos(e_ref[0], d) > tol, (_cos(e_ref[0], d), tol)
+        assert abs(float(d.norm()) / float(e_ref[0].norm()) - 1) < 0.02
+    assert c.comm.async_error() == 0
+
+
+def test_profile_stage_times_rolls_back_and_feeds_cut_plan(native_ext):
+    """Start-up stage profiling of the pipelined step (engine/step.py profile_stage_times): a
+    cut-everywhere, collective-free segmented step is captured and replayed with device events
+    between its segment graphs. Every stage gets a positive time, the training state (weights,
+    momentum, data cursor) is exactly what it was before, and the times drive
+    parallel/cut_plan.plan_cuts to a valid cut set (reference DDP buckets:
+    /root/reference/part3/main.py:174)."""
+    from ddp_amd.models import VGG11
+    from ddp_amd.optim import FusedSGD
+    from ddp_amd.data import SyntheticCIFAR10, DeviceLoader
+    from ddp_amd.engine import CrossEntropyLoss
+    from ddp_amd.engine.step import profile_stage_times
+    from ddp_amd.parallel import DistributedDataParallel, RcclCommunicator
+    from ddp_amd.parallel.cut_plan import plan_cuts, stand_in_rows
+    torch.manual_seed(17)
+    m = DistributedDataParallel(VGG11().cuda(), RcclCommunicator(0, 1, 0, self_comm=False),
+                                bucket_cap_mb=256.0, first_bucket_cap_mb=256.0)
+    opt = FusedSGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    ld = DeviceLoader(SyntheticCIFAR10(True, n=512), 32, "cuda")
+    opt.momentum_buffer.normal_()
+    torch.cuda.synchronize()
+    snap = (m.arena.data.clone(), opt.momentum_buffer.clone(), ld.cursor.clone())
+    n = m.module.n_stages()
+    us = profile_stage_times(m, opt, CrossEntropyLoss(), ld, n, reps=3)
+    assert len(us) == n and all(v > 0 for v in us), us
+    assert us[-1] > max(us[:-1]) * 0.5  # the last stage's segment also holds the forward
+    assert torch.equal(m.arena.data, snap[0])
+    assert torch.equal(opt.momentum_buffer, snap[1])
+    assert torch.equal(ld.cursor, snap[2])
+    pbytes = [4 * sum(p.numel() for p in (sp.conv.weight, sp.conv.bias, sp.bn.weight, sp.bn.bias))
+              for sp in m.module.fused_plan()]
+    best, ranked = plan_cuts(us, pbytes, stand_in_rows(8, 171.0), head_bytes=4 * 5130)
+    assert best["cuts"] and all(0 < c < n for c in best["cuts"])
+    assert best["step_us"] >= sum(us)
+    m.close()

@@ -139,3 +139,42 @@ def test_comm_bench_through_launcher_writes_table(tmp_path):
     assert src.startswith("measured-gloo-cpu table (world 2")
     cap, first, why = choose_bucket_caps(2, 40 << 20, overlap=True, table=t)
     assert cap >= 7 * 512 * 1024 and "measured-gloo-cpu" in why
+
+
+def _alive(pid):
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().split()[2] != "Z"
+    except OSError:
+        return False
+
+
+@pytest.mark.parametrize("sig", ["SIGTERM", "SIGHUP", "SIGKILL"])
+def test_parent_signal_leaves_no_rank_behind(stub, tmp_path, sig):
+    """A launcher that is terminated (scheduler timeout, closed terminal: SIGTERM / SIGHUP) or
+    killed outright (SIGKILL) must not orphan its ranks: they live in their own sessions, so the
+    signal never reaches them by itself (utils/launch.py _SignalGuard + PR_SET_PDEATHSIG)."""
+    import signal as _signal
+    code = ("import sys; sys.path.insert(0, %r); from ddp_amd.utils import launch; "
+            "sys.exit(launch.spawn([sys.executable, %r, %r, 'hang'], 3, timeout_s=300))"
+            % (REPO, stub, str(tmp_path)))
+    parent = subprocess.Popen([sys.executable, "-c", code], env=_clean_env(),
+                              stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    try:
+        deadline = time.monotonic() + 120
+        while time.monotonic() < deadline and not all(
+                (tmp_path / f"rank{r}.json").exists() for r in range(3)):
+            time.sleep(0.1)
+        pids = [json.loads((tmp_path / f"rank{r}.json").read_text())["pid"] for r in range(3)]
+        assert all(_alive(p) for p in pids)
+        parent.send_signal(getattr(_signal, sig))
+        rc = parent.wait(timeout=60)
+        if sig != "SIGKILL":
+            assert rc == 128 + int(getattr(_signal, sig)), rc
+        deadline = time.monotonic() + 20
+        while time.monotonic() < deadline and any(_alive(p) for p in pids):
+            time.sleep(0.1)
+        assert not any(_alive(p) for p in pids), "a rank outlived its launcher"
+    finally:
+        if parent.poll() is None:
+            parent.kill()

@@ -69,9 +69,9 @@ def main():
         native().conv_epi_stage_set(0)
         r["fwd+stats(direct epi)"] = timeit(lambda: conv_forward(spec, x, None, stats))
         native().conv_epi_stage_set(1)
-        native().conv_options(0, 1, 2)
+        native().conv_options(1, 2)
         r["fwd+stats(persistent)"] = timeit(lambda: conv_forward(spec, x, None, stats))
-        native().conv_options(0, 0, 2)
+        native().conv_options(0, 2)
         # BN backward passes over the conv output (reduce -> finalize -> apply, no residual)
         z = conv_forward(spec, x, None, stats)
         y = torch.empty_like(z)
@@ -91,7 +91,7 @@ def main():
             sums.zero_()
             native().bn_act_bwd(N_, P, Q, Kc, 0, 1, 1e-5, ptr(z), 0, ptr(stats), ptr(g), ptr(b_),
                                 ptr(dz), ptr(sums), ptr(dzz), 0, ptr(gg), ptr(gb), 0,
-                                stream_handle(), ptr(spec.coef), 0, sums_ready=0, grid_sync=0)
+                                stream_handle(), ptr(spec.coef), sums_ready=0)
         r["bn_bwd(zero+reduce+fin+apply)"] = timeit(bwd)
         r["zero"] = timeit(lambda: sums.zero_())
         line = {k: round(v, 1) for k, v in r.items()}
