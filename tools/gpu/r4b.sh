@@ -14,3 +14,5 @@ for B in 256 32 64 128; do
   echo "b$B noxf $(python -c "import json; d=json.loads(open('$O/bench_b${B}_noxf.log').read().strip().splitlines()[-1]); print(d['ms_per_step'], d['train_loss_mean'])")"
 done
 TAG=r4b BATCHES="256 32" bash tools/gpu/profile.sh
+timeout -k 10 300 python -u tools/probes/roofline.py --batch 256 32 --json $O/roofline.json > $O/roofline.log 2>&1 || { tail -5 $O/roofline.log; exit 1; }
+grep totals $O/roofline.log
