@@ -107,6 +107,7 @@ struct ConvArgs {
   // FWD / DGRAD bf16 output through the LDS-staged epilogue (conv_igemm_body): full 16-B
   // stores of whole tile rows instead of 8-B fragments of 16 rows per instruction
   int epi_stage;
+  int nmajor;                // tile order (common.h tile_order_n): 1 = row tiles fastest
   // DGRAD / WGRAD A-operand transform (XF instantiations): the A operand is the gradient at a
   // training-mode BatchNorm's input, dz = xA[c] * g + xB[c] * z + xC[c], computed while the tile
   // sits in LDS — its BN-backward "apply" pass never runs and dz is never stored. ``a`` = z
@@ -319,7 +320,8 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
     zsplit = item / tiles;
     const int tile = xcd_remap(item - zsplit * tiles, tiles);
     cur_tile = tile;
-    const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+    const int tm = args.nmajor ? tile % tiles_m : tile / tiles_n;
+    const int tn = args.nmajor ? tile / tiles_m : tile - tm * tiles_n;
     row0 = tm * BM;
     col0 = tn * BN;
     ks_begin = zsplit * args.ksteps_per_split;
@@ -1918,6 +1920,7 @@ static int prepare_cfg(ConvArgs& a, int splits) {
   a.splits = splits;
   a.ksteps_per_split = per;
   a.epi_stage = MODE != MODE_WGRAD && epi_stage_enabled();
+  a.nmajor = tile_order_n();
   if (MODE == MODE_DGRAD) {
     const int hh = a.phase ? a.Hp : a.g.H, ww = a.phase ? a.Wp : a.g.W;
     a.dPQ = make_fastdiv(std::max(1, hh * ww));

@@ -98,6 +98,8 @@ struct Args {
   int imgp, plane, zslot;    // patch pitch per image, pixels per chunk plane, zero pixel
   int x_bytes, w_bytes;
   int tiles_m, tiles_n;
+  int nmajor;                // tile order: 0 = column tiles fastest, 1 = row tiles fastest (each
+                             // XCD's run of consecutive tiles then shares one weight slice)
   int abuf_elems;            // bf16 elements of one patch buffer (16-B multiple)
   int flip;                  // weights read at tap 8 - t (backward-data: dx = conv(dz, W
                              // flipped + transposed), wc = the [C][3][3][K] copy)
@@ -147,7 +149,8 @@ void conv_tr_fwd_kernel(Args a) {
   const int item = blockIdx.x;
   const int sp = item / tiles;
   const int tile = xcd_remap(item - sp * tiles, tiles);
-  const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
+  const int tm = a.nmajor ? tile % a.tiles_m : tile / a.tiles_n;
+  const int tn = a.nmajor ? tile / a.tiles_m : tile - tm * a.tiles_n;
   const int row0 = tm * BM, col0 = tn * BN;
   const int cb0 = sp * a.cbps, cb1 = min(ncb, cb0 + a.cbps);
   const int nsteps = (cb1 - cb0) * 9;
@@ -733,6 +736,7 @@ extern "C" int ddp_conv_fwd_tr(const ConvGeom* g, const void* x, const void* wc,
   a.abuf_elems = geo.abuf;
   a.tiles_m = (int)(M / c.bm);
   a.tiles_n = K / c.bn;
+  a.nmajor = tile_order_n();
   if (in) {
     a.zin = (const unsigned short*)in->z;
     a.in_stats = in->stats;
@@ -788,6 +792,7 @@ extern "C" int ddp_conv_dgrad_tr(const ConvGeom* g, const void* dz, const void* 
   a.abuf_elems = geo.abuf;
   a.tiles_m = (int)(M / c.bm);
   a.tiles_n = t.K / c.bn;
+  a.nmajor = tile_order_n();
   a.flip = 1;
   const int items = a.tiles_m * a.tiles_n * pl.splits;
   if (!launch_stages(c, 0, a, geo.nl, items, st)) return 0;

@@ -13,9 +13,9 @@ from collections import defaultdict
 def main(root, flt=""):
     disp = defaultdict(dict)
     names, dur = {}, {}
-    for f in sorted(glob.glob(os.path.join(root, "p*", "*counter_collection.csv"))):
+    for f in sorted(glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True)):
         for r in csv.DictReader(open(f)):
-            key = (os.path.basename(os.path.dirname(f)), int(r["Dispatch_Id"]))
+            key = (os.path.relpath(f, root).split(os.sep)[0], int(r["Dispatch_Id"]))
             disp[key][r["Counter_Name"]] = float(r["Counter_Value"])
             names[key] = r["Kernel_Name"]
             dur[key] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0
@@ -25,8 +25,10 @@ def main(root, flt=""):
         merged[d].update(v)
         merged[d]["_name"] = names[(p, d)]
         merged[d].setdefault("_us", dur[(p, d)])
-    print("| id | us | kernel | MFMA busy/wave-cyc | VALU/MFMA | LDS-conflict/LDS | wait-LDS % | wait-any % | L2 hit % |")
-    print("|---|---|---|---|---|---|---|---|---|")
+    # MFMA util = MFMA-busy cycles / (effective clock cycles x 1024 SIMDs); effective clock =
+    # GRBM_GUI_ACTIVE / 8 XCDs / wall (MI355X_MICROARCH.md 'DVFS give-back'; reads high < 0.3 ms)
+    print("| id | us | kernel | MFMA util % | clk GHz | VALU/MFMA | LDS-conflict/LDS | wait-LDS % | wait-any % | L2 hit % |")
+    print("|---|---|---|---|---|---|---|---|---|---|")
     for d in sorted(merged):
         v = merged[d]
         n = v["_name"]
@@ -36,8 +38,10 @@ def main(root, flt=""):
         wc = g("SQ_WAVE_CYCLES")
         mf = g("SQ_INSTS_MFMA")
         hit, miss = g("TCC_HIT_sum"), g("TCC_MISS_sum")
+        cyc = g("GRBM_GUI_ACTIVE") / 8.0
         print(f"| {d} | {v['_us']:.1f} | `{n.split('(')[0][-48:]}` | "
-              f"{g('SQ_VALU_MFMA_BUSY_CYCLES') / max(g('SQ_BUSY_CYCLES'), 1):.2f} | "
+              f"{100 * g('SQ_VALU_MFMA_BUSY_CYCLES') / max(cyc * 1024, 1):.1f} | "
+              f"{cyc / max(v['_us'], 1e-3) / 1000:.2f} | "
               f"{g('SQ_INSTS_VALU') / max(mf, 1):.1f} | {g('SQ_LDS_BANK_CONFLICT') / max(g('SQ_INSTS_LDS'), 1):.2f} | "
               f"{100 * g('SQ_WAIT_INST_LDS') / max(wc, 1):.1f} | {100 * g('SQ_WAIT_ANY') / max(wc, 1):.1f} | "
               f"{100 * hit / max(hit + miss, 1):.1f} |")
