@@ -12,3 +12,5 @@ TAG=r4c BATCHES="128 64" bash tools/gpu/profile.sh || exit 1
 bash tools/gpu/pmc.sh > $O/pmc.log 2>&1 || { tail -5 $O/pmc.log; exit 1; }
 python tools/pmc_summary.py gpurun_out/pmc > $O/pmc_b256.md && grep -c conv $O/pmc_b256.md
 NOTEST=1 VARIANTS="m: n:DDP_AMD_TILE_ORDER=n" CFGS="vgg11:256 vgg11:32 resnet50:256" bash tools/gpu/ab_env.sh
+timeout -k 10 180 tools/probes/gemm_struct.bin 50 > $O/gemm_struct.jsonl 2>&1 || { tail -5 $O/gemm_struct.jsonl; exit 1; }
+timeout -k 10 300 python -u tools/probes/resnet_1x1_table.py --batch 256 --json $O/resnet_1x1.json > $O/resnet_1x1.log 2>&1 || { tail -5 $O/resnet_1x1.log; exit 1; }
