@@ -329,19 +329,48 @@ PYBIND11_MODULE(_native, m) {
   }, py::arg("g"), py::arg("dy"), py::arg("wc"), py::arg("dx"), py::arg("x"), py::arg("dw"),
      py::arg("ws"), py::arg("ws_elems"), py::arg("stream"), py::arg("bn") = py::none(),
      py::arg("bna") = py::none(), py::arg("xf") = py::none());
+  // SGD in the backward (world 1): register a conv weight's gradient view with its update
+  // (p, momentum buffer, bf16 copy, lr, momentum, wd, grad_scale, nesterov); dw = 0 with
+  // clear = 1 switches it off. sgd_fuse_taken: gradient views whose WGRAD finish applied it
+  // since sgd_fuse_begin.
+  m.def("sgd_fuse_register", [](uintptr_t dw, uintptr_t p, uintptr_t buf, uintptr_t wc, float lr,
+                                float momentum, float wd, float grad_scale, int nesterov,
+                                int clear) {
+    ddp_amd::SgdFuse f{P<float>(p), P<float>(buf), P<unsigned short>(wc), lr, momentum, wd,
+                       grad_scale, nesterov};
+    ddp_sgd_fuse_register(P<float>(dw), dw ? &f : nullptr, clear);
+  }, py::arg("dw"), py::arg("p") = 0, py::arg("buf") = 0, py::arg("wc") = 0, py::arg("lr") = 0.f,
+     py::arg("momentum") = 0.f, py::arg("wd") = 0.f, py::arg("grad_scale") = 1.f,
+     py::arg("nesterov") = 0, py::arg("clear") = 0);
+  m.def("sgd_fuse_begin", []() { ddp_sgd_fuse_begin(); });
+  m.def("sgd_fuse_taken", []() {
+    std::vector<uintptr_t> v(256);
+    int n = ddp_sgd_fuse_taken(v.data(), (int)v.size());
+    if (n > (int)v.size()) {
+      v.resize(n);
+      n = ddp_sgd_fuse_taken(v.data(), n);
+    }
+    v.resize(n);
+    return v;
+  });
   m.def("conv_pair_mode", [](int mode, int items) { ddp_conv_pair_mode(mode, items); },
         py::arg("mode"), py::arg("items") = 0);
   m.def("conv_pair_force", [](int sd, int sw) { ddp_conv_pair_force(sd, sw); },
         py::arg("splits_dg"), py::arg("splits_wg"));
+  // final = 1: no DGRAD of this layer follows (its finish may apply a registered SGD step)
   m.def("conv_wgrad", [](py::tuple g, uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws,
-                         size_t ws_elems, int splits, uintptr_t st, py::object xf) {
+                         size_t ws_elems, int splits, uintptr_t st, py::object xf, int final_) {
     auto c = geom(g);
     ddp_amd::BnBwdXf xv{};
     const ddp_amd::BnBwdXf* xp = xf_args(xf, &xv);
-    check(ddp_conv_wgrad_xf(&c, P<void>(dy), P<void>(x), P<float>(dw), P<float>(ws), ws_elems,
-                            splits, xp, S(st)), "conv_wgrad");
+    if (final_)
+      check(ddp_conv_wgrad_final(&c, P<void>(dy), P<void>(x), P<float>(dw), P<float>(ws),
+                                 ws_elems, splits, xp, S(st)), "conv_wgrad");
+    else
+      check(ddp_conv_wgrad_xf(&c, P<void>(dy), P<void>(x), P<float>(dw), P<float>(ws), ws_elems,
+                              splits, xp, S(st)), "conv_wgrad");
   }, py::arg("g"), py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("ws"), py::arg("ws_elems"),
-     py::arg("splits"), py::arg("stream"), py::arg("xf") = py::none());
+     py::arg("splits"), py::arg("stream"), py::arg("xf") = py::none(), py::arg("final") = 0);
 
   m.def("bn_act_fwd", [](int N, int H, int W, int C, int pool, int relu, float eps, uintptr_t z,
                          uintptr_t res, uintptr_t stats, uintptr_t gamma, uintptr_t beta,

@@ -116,6 +116,18 @@ struct BnBwdXf {
   int mask;
 };
 
+// SGD in the backward (conv_igemm.hip wgrad_finish_krsc_body): the optimizer step of one conv
+// weight, applied by the WGRAD split-K finish that produces its complete gradient
+// (torch.optim.SGD, dampening 0: d = g * grad_scale + wd * p; buf = momentum * buf + d;
+// d = nesterov ? d + momentum * buf : buf; p -= lr * d) + the bf16 forward operand copy.
+struct SgdFuse {
+  float* p;             // fp32 master weight, same [K][R][S][Cr] index order as the gradient
+  float* buf;           // its momentum buffer
+  unsigned short* wc;   // bf16 forward operand [K][R][S][C] (C >= Cr, pad channels untouched)
+  float lr, momentum, wd, grad_scale;
+  int nesterov;
+};
+
 struct PackDesc {
   const float* p;          // fp32 master [K][Cr][R][S] (krsc == 0) or [K][R][S][Cr] (krsc == 1)
   unsigned short* wc;      // bf16 [K][R][S][C]   (may be null)
@@ -223,6 +235,12 @@ void ddp_conv_epi_stage_set(int on);
 int ddp_bn_pool3_fwd(const ddp_amd::BnArgs* a, unsigned char* idx, hipStream_t st);
 int ddp_bn_pool3_bwd(const ddp_amd::BnArgs* a, const unsigned char* idx, hipStream_t st);
 void ddp_conv_pair_mode(int mode, int items);
+void ddp_sgd_fuse_register(float* dw, const ddp_amd::SgdFuse* f, int clear);
+void ddp_sgd_fuse_begin();
+int ddp_conv_wgrad_final(const ddp_amd::ConvGeom* g, const void* dy, const void* x, float* dw,
+                         float* ws, size_t ws_elems, int splits, const ddp_amd::BnBwdXf* xf,
+                         hipStream_t st);
+int ddp_sgd_fuse_taken(uintptr_t* out, int cap);
 // sweeps (tools/conv_tune.py --pairs): force the paired launch with these split-K factors (0 = off)
 void ddp_conv_pair_force(int splits_dg, int splits_wg);
 int ddp_conv_bwd_pair(const ddp_amd::ConvGeom* g, const void* dy, const void* wc, void* dx,

@@ -42,6 +42,7 @@
 #include "linear_blocks.h"
 #include <algorithm>
 #include <map>
+#include <set>
 #include <cstdlib>
 
 namespace ddp_amd {
@@ -1697,15 +1698,29 @@ __global__ __launch_bounds__(256) void wgrad_finish_kernel(const float* ws, int 
 // Split-K finish for WGRAD into a [K][R][S][Cr] gradient: the GEMM row IS the gradient row, so
 // this is a vectorised sum of the slabs — no transpose. blockIdx.y = group of kWgFinishGroupKrsc
 // slabs (fixed order inside a group); several groups combine with atomics.
+__device__ __forceinline__ float sgd_step1(float p, float g, float& b, const SgdFuse& h) {
+  float d = g * h.grad_scale + h.wd * p;
+  if (h.momentum != 0.f) {
+    b = h.momentum * b + d;
+    d = h.nesterov ? d + h.momentum * b : b;
+  }
+  return p - h.lr * d;
+}
+
+// With ``sg.p`` (SGD in the backward, api.h SgdFuse; single group only: the sum is the final
+// gradient) the finish applies the optimizer step to the layer's weights instead of storing the
+// gradient: p -= lr * (momentum buffer update of g + wd * p), plus the bf16 forward operand copy
+// — the gradient never reaches memory and the step's separate SGD pass skips this tensor.
 constexpr int kWgFinishGroupKrsc = 16;
 __device__ __forceinline__ void wgrad_finish_krsc_body(const float* __restrict__ ws, int splits,
                                                        int K, int RS, int C, int Creal,
                                                        float* __restrict__ dw, int bx, int by,
-                                                       int gx, int gy) {
+                                                       int gx, int gy, const SgdFuse& sg) {
   const size_t slab = (size_t)K * RS * C;
   const size_t n4 = slab / 4;
   const int z0 = by * kWgFinishGroupKrsc, z1 = min(splits, z0 + kWgFinishGroupKrsc);
   const bool single = gy == 1;
+  const bool opt = single && sg.p != nullptr;
   for (size_t i = bx * (size_t)blockDim.x + threadIdx.x; i < n4;
        i += (size_t)gx * blockDim.x) {
     float4 v = reinterpret_cast<const float4*>(ws + z0 * slab)[i];
@@ -1720,6 +1735,37 @@ __device__ __forceinline__ void wgrad_finish_krsc_body(const float* __restrict__
         if (zb + u < z1) { v.x += a[u].x; v.y += a[u].y; v.z += a[u].z; v.w += a[u].w; }
     }
     const float vv[4] = {v.x, v.y, v.z, v.w};
+    if (opt) {
+      if (Creal == C) {
+        float4 pv = reinterpret_cast<float4*>(sg.p)[i];
+        float4 bv = reinterpret_cast<float4*>(sg.buf)[i];
+        pv.x = sgd_step1(pv.x, v.x, bv.x, sg);
+        pv.y = sgd_step1(pv.y, v.y, bv.y, sg);
+        pv.z = sgd_step1(pv.z, v.z, bv.z, sg);
+        pv.w = sgd_step1(pv.w, v.w, bv.w, sg);
+        reinterpret_cast<float4*>(sg.p)[i] = pv;
+        reinterpret_cast<float4*>(sg.buf)[i] = bv;
+        uint2 pk;
+        pk.x = (unsigned)f2bf(pv.x) | ((unsigned)f2bf(pv.y) << 16);
+        pk.y = (unsigned)f2bf(pv.z) | ((unsigned)f2bf(pv.w) << 16);
+        *reinterpret_cast<uint2*>(sg.wc + i * 4) = pk;
+      } else {  // channel-padded input layer: master [K][R][S][Creal], copy [K][R][S][C]
+        const size_t e = i * 4;
+        const int c = (int)(e % C);
+        const size_t krs = e / C;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          if (c + t >= Creal) continue;
+          const size_t mi = krs * Creal + c + t;
+          float b = sg.buf[mi];
+          const float np = sgd_step1(sg.p[mi], vv[t], b, sg);
+          sg.p[mi] = np;
+          sg.buf[mi] = b;
+          sg.wc[e + t] = f2bf(np);
+        }
+      }
+      continue;
+    }
     if (Creal == C) {
       if (single) {
         float4* o = reinterpret_cast<float4*>(dw) + i;
@@ -1746,9 +1792,10 @@ __device__ __forceinline__ void wgrad_finish_krsc_body(const float* __restrict__
 
 __global__ __launch_bounds__(256) void wgrad_finish_krsc_kernel(const float* __restrict__ ws,
                                                                 int splits, int K, int RS, int C,
-                                                                int Creal, float* __restrict__ dw) {
+                                                                int Creal, float* __restrict__ dw,
+                                                                SgdFuse sg) {
   wgrad_finish_krsc_body(ws, splits, K, RS, C, Creal, dw, blockIdx.x, blockIdx.y, gridDim.x,
-                         gridDim.y);
+                         gridDim.y, sg);
 }
 
 struct WgFinishArgs {
@@ -1756,6 +1803,7 @@ struct WgFinishArgs {
   int splits, K, RS, C, Creal;
   float* dw;
   int gx, gy;  // its own grid (0 x 0 = no WGRAD finish in this launch)
+  SgdFuse sgd;  // SGD in the backward (sgd.p == nullptr: store the gradient)
 };
 
 // The split-K finishes of one layer's backward pair in ONE launch: blocks [0, dgx*dgy) reduce
@@ -1770,7 +1818,7 @@ __global__ __launch_bounds__(256) void bwd_pair_finish_kernel(FinishArgs fa, int
   } else {
     const int w = b - dgx * dgy;
     wgrad_finish_krsc_body(wa.ws, wa.splits, wa.K, wa.RS, wa.C, wa.Creal, wa.dw, w % wa.gx,
-                           w / wa.gx, wa.gx, wa.gy);
+                           w / wa.gx, wa.gx, wa.gy, wa.sgd);
   }
 }
 
@@ -1971,11 +2019,29 @@ static FinishArgs finish_args(int mode, const ConvArgs& a) {
                     a.Mg, a.Ng, rm, a.accumulate, a.bnf, a.g.H, a.g.W};
 }
 
+// ---- SGD in the backward (world 1, engine/step.py TrainStep): registered weights whose WGRAD
+// finish reduces every slab in one group take the optimizer step in that finish (SgdFuse);
+// ddp_sgd_fuse_taken reports which did, and the step's SGD launch skips exactly those.
+// Only where nothing reads the layer's weights after its WGRAD finish within the backward: the
+// grouped pair launch (its DGRAD half ran before the finish), a separate DGRAD issued first, or
+// a layer without a DGRAD (g_sgd_allow is raised around exactly those finishes).
+static std::map<const float*, SgdFuse> g_sgd_reg;  // gradient view -> its fused update
+static std::set<const float*> g_sgd_taken;
+static bool g_sgd_allow = false;
+static SgdFuse sgd_fuse_for(const float* dw, int groups) {
+  if (!g_sgd_allow || groups != 1 || g_sgd_reg.empty()) return SgdFuse{};
+  auto it = g_sgd_reg.find(dw);
+  if (it == g_sgd_reg.end()) return SgdFuse{};
+  g_sgd_taken.insert(dw);
+  return it->second;
+}
+
 static WgFinishArgs wg_finish_args(const ConvArgs& a) {
   const size_t n4 = (size_t)a.Mg * a.Ng / 4;
   const int groups = (a.splits + kWgFinishGroupKrsc - 1) / kWgFinishGroupKrsc;
   const int bx = (int)std::min<size_t>((n4 + 255) / 256, std::max(1, 2048 / groups));
-  return WgFinishArgs{a.ws, a.splits, a.g.K, a.g.R * a.g.S, a.g.C, a.g.Creal, a.dw, bx, groups};
+  return WgFinishArgs{a.ws, a.splits, a.g.K, a.g.R * a.g.S, a.g.C, a.g.Creal, a.dw, bx, groups,
+                      sgd_fuse_for(a.dw, groups)};
 }
 
 // DGRAD split-K finish with the preceding block's complete BatchNorm backward (small stride-1
@@ -2022,7 +2088,7 @@ __global__ __launch_bounds__(256) void bwd_pair_finish_bnbwd_kernel(FinishArgs f
   } else {
     const int w = b - dgx;
     wgrad_finish_krsc_body(wa.ws, wa.splits, wa.K, wa.RS, wa.C, wa.Creal, wa.dw, w % wa.gx,
-                           w / wa.gx, wa.gx, wa.gy);
+                           w / wa.gx, wa.gx, wa.gy, wa.sgd);
   }
 }
 
@@ -2088,7 +2154,7 @@ static void launch_finish(const ConvArgs& a, hipStream_t st) {
   if (MODE == MODE_WGRAD && a.g.wkrsc) {
     const WgFinishArgs w = wg_finish_args(a);
     hipLaunchKernelGGL(wgrad_finish_krsc_kernel, dim3(w.gx, w.gy), dim3(256), 0, st, a.ws,
-                       a.splits, a.g.K, a.g.R * a.g.S, a.g.C, a.g.Creal, a.dw);
+                       a.splits, a.g.K, a.g.R * a.g.S, a.g.C, a.g.Creal, a.dw, w.sgd);
   } else if (MODE == MODE_WGRAD) {
     const int groups = (a.splits + kWgFinishGroup - 1) / kWgFinishGroup;
     const size_t lds = sizeof(float) * a.g.R * a.g.S * a.g.C;
@@ -2545,9 +2611,13 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
   if (!bn) ba = nullptr;
   if (xf && (!xf_dgrad_ok(g) || xf->C != g->K)) return -4;
   auto separate = [&]() -> int {
-    const int r = ddp_conv_wgrad_xf(g, dy, x, dw, ws, ws_elems, 0, xf, st);
+    // DGRAD first: the WGRAD finish may then apply the layer's SGD step (g_sgd_allow)
+    const int r = conv_dgrad_impl(g, dy, wc, dx, ws, ws_elems, 0, 0, bn, ba, bn_done, st, xf);
     if (r) return r;
-    return conv_dgrad_impl(g, dy, wc, dx, ws, ws_elems, 0, 0, bn, ba, bn_done, st, xf);
+    g_sgd_allow = true;
+    const int rw = ddp_conv_wgrad_xf(g, dy, x, dw, ws, ws_elems, 0, xf, st);
+    g_sgd_allow = false;
+    return rw;
   };
   if (g_pair_mode == 0 || g->stride != 1 || g->C % 8 || g->K % 8 || g->Creal != g->C)
     return separate();
@@ -2653,6 +2723,10 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
                        d, w, itd);
   }
   const bool fd = needs_finish(MODE_DGRAD, d), fw = needs_finish(MODE_WGRAD, w);
+  struct Allow {  // the finishes below run after both GEMMs of the pair
+    Allow() { g_sgd_allow = true; }
+    ~Allow() { g_sgd_allow = false; }
+  } allow;
   if (fd && fw && w.g.wkrsc && bnbwd_fusable(d)) {
     const WgFinishArgs wa = wg_finish_args(w);
     launch_finish_bnbwd(d, st, &wa);
@@ -2671,4 +2745,29 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
     launch_finish<MODE_WGRAD>(w, st);
   }
   return (int)hipGetLastError();
+}
+
+// SGD in the backward: register (dw -> update) pairs (clear = 1 drops the registry first),
+// reset / read the set of gradients whose finish took the update since the last begin.
+extern "C" void ddp_sgd_fuse_register(float* dw, const SgdFuse* f, int clear) {
+  if (clear) g_sgd_reg.clear();
+  if (dw && f) g_sgd_reg[dw] = *f;
+}
+extern "C" void ddp_sgd_fuse_begin() { g_sgd_taken.clear(); }
+// a WGRAD whose layer runs no DGRAD (the input layer): its finish may apply the SGD step
+extern "C" int ddp_conv_wgrad_final(const ConvGeom* g, const void* dy, const void* x, float* dw,
+                                    float* ws, size_t ws_elems, int splits, const BnBwdXf* xf,
+                                    hipStream_t st) {
+  g_sgd_allow = true;
+  const int r = ddp_conv_wgrad_xf(g, dy, x, dw, ws, ws_elems, splits, xf, st);
+  g_sgd_allow = false;
+  return r;
+}
+extern "C" int ddp_sgd_fuse_taken(uintptr_t* out, int cap) {
+  int n = 0;
+  for (const float* p : g_sgd_taken) {
+    if (n < cap) out[n] = reinterpret_cast<uintptr_t>(p);
+    ++n;
+  }
+  return n;
 }

@@ -38,6 +38,19 @@ def default_cuts(model_name, per_gpu_batch):
     return "3,6" if per_gpu_batch <= 128 else "2,5"
 
 
+def sgd_in_backward_ok(model):
+    """May the optimizer step run inside the backward (TrainStep.opt_in_bwd)? Only when no
+    gradient collective or stand-in reads the gradients: no live communicator, no emulated
+    collective, and not switched off (DDP_AMD_SGD_IN_BWD=0)."""
+    if os.environ.get("DDP_AMD_SGD_IN_BWD", "1") == "0":
+        return False
+    if int(os.environ.get("DDP_AMD_EMULATE_COMM", "0")) > 0 or \
+            float(os.environ.get("DDP_AMD_EMULATE_COMM_GBPS", "0")) > 0:
+        return False
+    comm = getattr(model, "comm", None)
+    return comm is None or not is_live(comm)
+
+
 class TrainStep:
     def __init__(self, model, optimizer, criterion, loader, sync=None, use_graph=True):
         self.model, self.optimizer, self.criterion, self.loader = model, optimizer, criterion, loader
@@ -54,6 +67,12 @@ class TrainStep:
         self.fold_opt = bool(getattr(optimizer, "_fused", False)) and hasattr(loader, "cursor_advance")
         if self.fold_opt:
             optimizer.zero_grad()  # later steps get clean gradients from the previous step's launch
+        # SGD in the backward: one GPU, no gradient collective (nothing reads a gradient between
+        # its WGRAD finish and the update) -> each conv weight's update runs in the split-K
+        # finish that completes its gradient; the step's SGD launch covers only the rest
+        # (optim/sgd.py register_in_backward). DDP_AMD_SGD_IN_BWD=0 keeps the separate pass.
+        self.opt_in_bwd = (self.fold_opt and sync is None and sgd_in_backward_ok(model)
+                           and hasattr(optimizer, "register_in_backward"))
 
     def _fused_loss(self):
         """Use the model's fused classifier+loss when the criterion is the plain mean CE."""
@@ -65,6 +84,8 @@ class TrainStep:
     def _body(self):
         if not self.fold_opt:
             self.optimizer.zero_grad()
+        if self.opt_in_bwd:
+            self.optimizer.register_in_backward()
         with trace_range("data"):
             x, y = self.loader.fill(advance=not self.fold_opt)
         with trace_range("forward"):
@@ -82,9 +103,12 @@ class TrainStep:
             if self.fold_opt:
                 # the optimizer launch also clears the gradients for the next step and advances
                 # the data cursor: no zero_grad fill, no counter kernel
-                self.optimizer.step(zero_grad=True, counter=self.loader.cursor_advance())
+                self.optimizer.step(zero_grad=True, counter=self.loader.cursor_advance(),
+                                    fused_taken=self.opt_in_bwd)
             else:
                 self.optimizer.step()
+        if self.opt_in_bwd:
+            self.optimizer.unregister_in_backward()
         if not self.fused:
             self.loss_sum.add_(loss.detach())
 
@@ -125,6 +149,8 @@ class TrainStep:
         replays. Gradients are clear on entry when the optimizer launch clears them."""
         if not self.fold_opt:
             self.optimizer.zero_grad()
+        if self.opt_in_bwd:
+            self.optimizer.register_in_backward()
         if self.fused:
             loss = self.model.forward_loss(x, y, acc=self.loss_sum)
         else:
@@ -134,9 +160,11 @@ class TrainStep:
         if self.sync is not None:
             self.sync(self.model)
         if self.fold_opt:
-            self.optimizer.step(zero_grad=True)
+            self.optimizer.step(zero_grad=True, fused_taken=self.opt_in_bwd)
         else:
             self.optimizer.step()
+        if self.opt_in_bwd:
+            self.optimizer.unregister_in_backward()
 
     def wait(self, timeout_s=None, poll_s=0.001):
         """Synchronise with the device, optionally bounded: returns False on timeout instead of

@@ -316,7 +316,9 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=Non
                                 side.stream.cuda_stream, xf=xf)
             grad_ready([weight])
     else:
-        native().conv_wgrad(g, ptr(dz), ptr(x), ptr(dweight), ptr(ws), ws.numel(), 0, s, xf=xf)
+        # final: no dgrad of this layer follows, so its finish may apply a registered SGD step
+        native().conv_wgrad(g, ptr(dz), ptr(x), ptr(dweight), ptr(ws), ws.numel(), 0, s, xf=xf,
+                            final=int(not need_dx))
         if weight is not None:
             grad_ready([weight])
     if not need_dx:

@@ -43,11 +43,48 @@ class FusedSGD(torch.optim.SGD):
             from ..ops.common import native, stream_handle
             native().pack_conv_weights(descs, stream_handle())
 
-    def _work_table(self, prange=None):
+    def register_in_backward(self):
+        """SGD in the backward (engine/step.py TrainStep, one GPU): hand every conv weight whose
+        bf16 copy has the master's index order to the kernel library, which applies its update
+        in the WGRAD split-K finish that completes its gradient (conv_igemm.hip SgdFuse). Active
+        until unregister_in_backward(); ``step(fused_taken=True)`` then skips the tensors whose
+        finish took it (native sgd_fuse_taken)."""
+        from ..ops.common import native
+        a, g = self.arena, self.param_groups[0]
+        nat = native()
+        nat.sgd_fuse_register(0, clear=1)
+        self._bwd_index = {}
+        base_g, base_p = a.grad.data_ptr(), a.data.data_ptr()
+        base_b = self.momentum_buffer.data_ptr()
+        for i, p in enumerate(a.params):
+            if not hasattr(p, "_ddp_amd_pack"):
+                continue
+            pp, wc, wt, K, Cr, C, R, S, krsc = p._ddp_amd_pack()
+            if wt or not wc or not (krsc or R * S == 1) or pp != base_p + 4 * a.offsets[i]:
+                continue
+            dw = base_g + 4 * a.offsets[i]
+            nat.sgd_fuse_register(dw, pp, base_b + 4 * a.offsets[i], wc, float(g["lr"]),
+                                  float(g["momentum"]), float(g["weight_decay"]),
+                                  float(self._grad_scale_factor), int(bool(g["nesterov"])))
+            self._bwd_index[dw] = i
+        nat.sgd_fuse_begin()
+
+    def unregister_in_backward(self):
+        from ..ops.common import native
+        native().sgd_fuse_register(0, clear=1)
+
+    def _fused_in_backward(self):
+        """Parameter indices whose update a WGRAD finish applied since register_in_backward."""
+        from ..ops.common import native
+        idx = getattr(self, "_bwd_index", {})
+        return frozenset(idx[d] for d in native().sgd_fuse_taken() if d in idx)
+
+    def _work_table(self, prange=None, exclude=frozenset()):
         """Device work-item table of the fused SGD + re-pack kernel (rebuilt when the set of
         packed conv weights changes, e.g. after the model's fused plan is first built).
         ``prange = (i0, i1)`` restricts it to parameters i0 <= i < i1 (one DDP bucket: the
-        pipelined step updates each bucket as soon as its all-reduce is done)."""
+        pipelined step updates each bucket as soon as its all-reduce is done); ``exclude`` =
+        parameter indices updated elsewhere (SGD in the backward)."""
         from ..ops.common import native
         a = self.arena
         key = tuple(self._packs())
@@ -84,16 +121,18 @@ class FusedSGD(torch.optim.SGD):
             dev = a.data.device
             self._descs = torch.tensor(descs if descs else [[0] * 12], dtype=torch.int64, device=dev)
         rng = tuple(prange) if prange is not None else (0, len(a.params))
-        t = self._tables.get(rng)
+        t = self._tables.get((rng, exclude))
         if t is None:
+            keep = [i for i in range(*rng) if i not in exclude]
             # conv re-pack items first (the heavier tiles start early), then elementwise items
-            sel = [it for i in range(*rng) for it in self._per_param[i] if it[0] != 0] + \
-                  [it for i in range(*rng) for it in self._per_param[i] if it[0] == 0]
-            if not sel:
+            sel = [it for i in keep for it in self._per_param[i] if it[0] != 0] + \
+                  [it for i in keep for it in self._per_param[i] if it[0] == 0]
+            if not sel and not exclude:
                 raise ValueError(f"no parameters in range {rng}")
-            items = torch.tensor(sel, dtype=torch.int32, device=a.data.device)
+            items = (torch.tensor(sel, dtype=torch.int32, device=a.data.device) if sel
+                     else None)
             t = (items, len(sel))
-            self._tables[rng] = t
+            self._tables[(rng, exclude)] = t
         return t[0], t[1], self._descs
 
     def _elem_table(self, lo, hi):
@@ -166,12 +205,14 @@ class FusedSGD(torch.optim.SGD):
 
     @torch.no_grad()
     def step(self, closure=None, zero_grad=False, counter=None, skip=None, params=None,
-             stream=None):
+             stream=None, fused_taken=False):
         """One fused launch. ``params = (i0, i1)``: only parameters i0 <= i < i1 (arena order);
         ``stream``: launch on this torch stream instead of the current one. ``zero_grad=True`` also clears every gradient after its use (the
         next step then needs no zero_grad fill); ``counter=(int32 device ptr, delta)`` is
         advanced by the same launch (the on-device data cursor of engine/step.py); ``skip`` =
-        device pointer of a uint32 error word: the update is skipped when it is non-zero."""
+        device pointer of a uint32 error word: the update is skipped when it is non-zero.
+        ``fused_taken=True``: skip the parameters whose update the backward already applied
+        (register_in_backward)."""
         if not self._fused:
             out = super().step(closure)
             if zero_grad:
@@ -181,7 +222,12 @@ class FusedSGD(torch.optim.SGD):
         g = self.param_groups[0]
         s = stream.cuda_stream if stream is not None else stream_handle()
         a = self.arena
-        items, n_items, descs = self._work_table(params)
+        exclude = self._fused_in_backward() if fused_taken else frozenset()
+        items, n_items, descs = self._work_table(params, exclude)
+        if n_items == 0:  # every tensor was updated in the backward: only the data cursor
+            if counter:
+                native().counter_add(int(counter[0]), int(counter[1]), s)
+            return None
         # one launch: SGD over every tensor + bf16 re-pack of every conv weight
         native().sgd_pack(items.data_ptr(), n_items, descs.data_ptr(), a.data.data_ptr(),
                           a.grad.data_ptr(), self.momentum_buffer.data_ptr(), float(g["lr"]),

@@ -751,3 +751,63 @@ def test_conv_bwd_xf(native_ext, case, pair_mode):
         assert rel_err(res[True][0], res[False][0]) < 1e-2
     assert torch.allclose(res[True][2], res[False][2], rtol=1e-4, atol=1e-4)
     assert torch.allclose(res[True][3], res[False][3], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("path", ["pair", "separate", "layer0"])
+def test_sgd_in_backward_finish(native_ext, path):
+    """SGD in the backward (conv_igemm.hip SgdFuse): a registered weight's WGRAD split-K finish
+    applies torch.optim.SGD's update (momentum 0.9, wd 1e-4) to the fp32 master and its momentum
+    buffer and rewrites the bf16 forward copy, instead of storing the gradient. Checked against
+    the unfused backward's gradient + the SGD formula in fp32 PyTorch; dx must be unchanged
+    (the DGRAD reads the weights before the update: grouped pair, or DGRAD issued first)."""
+    from ddp_amd.ops.layers import conv_backward
+    nat = native_ext
+    if path == "layer0":
+        N, Cin, H, K, Creal, need_dx = 8, 8, 32, 64, 3, False
+    else:
+        N, Cin, H, K, Creal, need_dx = 8, 64, 16, 128, 64, True
+    conv, spec, x, xn = _conv_setup(N, Cin, H, H, K, 3, 1, 1, Creal=Creal)
+    dz = bf(torch.randn(N, K, H, H, device=DEV))
+    dzn = dz.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    lr, mom, wd = 0.1, 0.9, 1e-4
+    mode = {"pair": 2, "separate": 0, "layer0": 3}[path]
+    nat.conv_pair_mode(mode)
+    if path == "pair":
+        nat.conv_pair_force(1, 4)  # WGRAD split 4 ways: a single-group finish
+    try:
+        dw_ref = torch.zeros_like(conv.weight, memory_format=torch.channels_last)
+        dx_ref = conv_backward(spec, xn, dzn, dw_ref, need_dx)
+        torch.cuda.synchronize()
+        p = conv.weight.detach().clone().contiguous(memory_format=torch.channels_last)
+        buf = (torch.randn_like(p) * 1e-3).contiguous(memory_format=torch.channels_last)
+        p0, buf0 = p.clone(), buf.clone()
+        dw = torch.zeros_like(p)
+        nat.sgd_fuse_register(dw.data_ptr(), p.data_ptr(), buf.data_ptr(), spec.wc.data_ptr(),
+                              lr, mom, wd, 1.0, 0, clear=1)
+        nat.sgd_fuse_begin()
+        try:
+            dx = conv_backward(spec, xn, dzn, dw, need_dx)
+            torch.cuda.synchronize()
+            taken = nat.sgd_fuse_taken()
+        finally:
+            nat.sgd_fuse_register(0, clear=1)
+    finally:
+        nat.conv_pair_mode(3)
+        nat.conv_pair_force(0, 0)
+    if need_dx:
+        assert torch.equal(dx, dx_ref)
+    if path == "pair":  # forced 4-way WGRAD split: one finish group, the update must be taken
+        assert taken == [dw.data_ptr()]
+    assert taken in ([], [dw.data_ptr()])
+    if not taken:  # the finish did not qualify (multi-group / no split): gradient stored
+        assert torch.equal(p, p0) and rel_err(dw, dw_ref) < 1e-6
+        return
+    assert float(dw.abs().max()) == 0.0  # the gradient never reached memory
+    d = dw_ref + wd * p0
+    b_ref = mom * buf0 + d
+    p_ref = p0 - lr * b_ref
+    assert torch.allclose(buf, b_ref, rtol=1e-5, atol=1e-7)
+    assert torch.allclose(p, p_ref, rtol=1e-6, atol=1e-7)
+    # the bf16 forward operand [K][R][S][C] (pad channels untouched = 0)
+    wc = spec.wc.view(K, 3, 3, Cin).float()[..., :Creal]
+    assert torch.equal(wc, p.permute(0, 2, 3, 1).to(torch.bfloat16).float())
