@@ -187,6 +187,20 @@ PYBIND11_MODULE(_native, m) {
     if (rc >= 2) check(rc - 2, "conv_dgrad_tr");
     return rc == 1;
   });
+  // tap-reuse backward-data reading the FORWARD weight copy wc k-major; xf = (z, g, coef, C,
+  // mask): dz computed in the patch load (dz pointer ignored). True when served.
+  m.def("conv_dgrad_tr_wc", [](py::tuple g, uintptr_t dz, uintptr_t wc, uintptr_t dx,
+                               uintptr_t ws, size_t ws_elems, uintptr_t st, py::object xf) {
+    auto c = geom(g);
+    ddp_amd::BnBwdXf xv{};
+    const ddp_amd::BnBwdXf* xp = xf_args(xf, &xv);
+    const int rc = ddp_conv_dgrad_tr_wc(&c, P<void>(dz), P<void>(wc), P<void>(dx), P<float>(ws),
+                                        ws_elems, xp, S(st));
+    if (rc < 0) check(rc, "conv_dgrad_tr_wc");
+    if (rc >= 2) check(rc - 2, "conv_dgrad_tr_wc");
+    return rc == 1;
+  }, py::arg("g"), py::arg("dz"), py::arg("wc"), py::arg("dx"), py::arg("ws"), py::arg("ws_elems"),
+     py::arg("stream"), py::arg("xf") = py::none());
   m.def("conv_tr_would_serve", [](py::tuple g, size_t ws_elems, int in_mode) {
     auto c = geom(g);
     return ddp_conv_tr_would_serve(&c, ws_elems, in_mode) == 1;

@@ -180,6 +180,10 @@ int ddp_conv_tr_would_serve(const ddp_amd::ConvGeom* g, size_t ws_elems, int in_
 // g = the forward geometry; 1 served, 0 not served, >= 2 HIP error (rc - 2)
 int ddp_conv_dgrad_tr(const ddp_amd::ConvGeom* g, const void* dz, const void* wt, void* dx,
                       float* ws, size_t ws_elems, hipStream_t st);
+// the same with the weights read k-major from the FORWARD copy wc = bf16 [K][3][3][C] (no
+// transposed copy) and, with xf, dz computed from (z, g, coef) while the patch loads
+int ddp_conv_dgrad_tr_wc(const ddp_amd::ConvGeom* g, const void* dz, const void* wc, void* dx,
+                         float* ws, size_t ws_elems, const ddp_amd::BnBwdXf* xf, hipStream_t st);
 // tap-reuse policy: mode -1 clear table, 0/1 disable/enable (table entries), 4 enable with the
 // heuristic for untabled shapes, 2 forward / 5 backward-data table entry (M, K, C, H) ->
 // (bm, bn, splits, stages) (bm = 0: use the implicit-GEMM kernel), 3 force the same (sweeps)

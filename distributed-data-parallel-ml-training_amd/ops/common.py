@@ -58,7 +58,7 @@ def load_conv_tuning(n=None, path=None):
         n.conv_tr_set(2, int(e["M"]), int(e["K"]), int(e["C"]), int(e["H"]), int(e["bm"]),
                       int(e["bn"]), int(e["splits"]), int(e.get("stages", 0)))
     # backward-data entries: keyed by the dgrad problem (M, K = forward C, C = forward K, H);
-    # the layers with at least one served entry get a transposed weight copy (ops/layers.py)
+    # (TR_DGRAD_SHAPES: the forward shapes with at least one served entry)
     TR_DGRAD_SHAPES.clear()
     for e in table.get("tr_dgrad_entries", []):
         if int(e["bm"]) > 0:

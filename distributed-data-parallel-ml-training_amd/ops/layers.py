@@ -49,14 +49,10 @@ class ConvBNActSpec:
         self.eps = float(bn.eps) if bn is not None else 1e-5
         dev = conv.weight.device
         self.wc = torch.empty(K, R, S, self.C, dtype=BF16, device=dev)
-        # transposed copy [C][R][S][K] only for the tap-reuse backward-data kernel (conv_tr.hip
-        # ddp_conv_dgrad_tr); the implicit-GEMM dgrad reads Wc k-major through transposing LDS
-        # reads and needs none
+        # transposed copy [C][R][S][K]: none. Both backward-data kernels (implicit GEMM and the
+        # tap-reuse one) read Wc k-major through transposing LDS reads (ds_read_b64_tr_b16);
+        # only probes that time the older transposed-copy kernel set one themselves
         self.wt = None
-        if (DGRAD_TR and R == 3 and S == 3 and conv.stride[0] == 1 and conv.padding[0] == 1
-                and self.C == Cr and Cr % 64 == 0 and K % 64 == 0 and dev.type == "cuda"
-                and (DGRAD_TR == 2 or (K, Cr) in _common.TR_DGRAD_SHAPES)):
-            self.wt = torch.empty(self.C, R, S, K, dtype=BF16, device=dev)
         self._packed_version = None
         conv.weight._ddp_amd_pack = self.pack_desc  # the fused optimizer repacks after its step
         # per-step zeroed accumulators (StepScratch): BN statistics replicas + BN-backward sums
@@ -205,13 +201,12 @@ class GradLink:
 # 3x3 stride-1 forward convolutions through the tap-reuse kernel (conv_tr.hip); =0 restores the
 # implicit-GEMM kernel for every layer (the native side also reads DDP_AMD_CONV_TR)
 CONV_TR = os.environ.get("DDP_AMD_CONV_TR", "1") != "0"
-# backward-data of 3x3 stride-1 layers through the tap-reuse kernel where the measured table
-# says so (needs a transposed bf16 weight copy per eligible layer, repacked by the optimizer);
-# =0 (default) keeps the implicit-GEMM dgrad / backward pair everywhere. Opt-in: the kernel
-# wins per layer at 256 images (profiles/r3_conv_tr_dgrad_sweep.jsonl) but the transposed-copy
-# repack in the fused SGD costs more than it saves end to end (b256 0.8887 vs 0.8857 ms,
-# b32 0.4421 vs 0.4164 ms, same box; profiles/r3_conv_tr_dgrad.md)
-# (2: give every eligible layer the copy, e.g. for sweeps)
+# backward-data of 3x3 stride-1 layers through the tap-reuse kernel (conv_tr.hip, weights read
+# k-major from the forward copy Wc, the BatchNorm-backward dz computed in its patch load) where
+# the measured table (tr_dgrad_entries) says it beats the backward pair, followed by the weight
+# gradient alone. Round 3's version needed a transposed weight copy whose repack in the SGD cost
+# more than the kernel saved (profiles/r3_conv_tr_dgrad.md); this one needs none.
+# DDP_AMD_DGRAD_TR=1 enables it.
 DGRAD_TR = int(os.environ.get("DDP_AMD_DGRAD_TR", "0"))
 # a block's BatchNorm + ReLU (+ 2x2 pool) forward computed by the NEXT block's tap-reuse conv
 # while it loads its input patch (conv_tr.hip fused input; no bn_act_fwd launch); =0 restores the
@@ -257,6 +252,22 @@ def bn_bwd_fuse_pays(H, W, pool=True):
     return H * W <= BN_BWD_FUSE_MAX_HW
 
 
+def dgrad_tr_serves(spec, x, need_dx, link=None):
+    """Does this layer's backward-data go through the tap-reuse kernel (DGRAD_TR)? A plain 3x3
+    stride-1 layer whose shape the measured table assigns to it."""
+    if not (DGRAD_TR and need_dx and link is None and not _common.BWD_SIDE_STREAM
+            and spec.R == 3 and spec.S == 3 and spec.stride == 1 and spec.pad == 1
+            and spec.C == spec.Cr and spec.wc is not None and x.is_cuda):
+        return False
+    N, H, W, _ = x.shape
+    key = (N, H, W)
+    cache = spec.__dict__.setdefault("_tr_dgrad_cache", {})
+    if key not in cache:
+        cache[key] = bool(native().conv_tr_would_serve(spec.geom(N, H, W), workspace(x.device).numel(),
+                                                       -1))
+    return cache[key]
+
+
 def conv_xf_ok(spec, x, need_dx, link=None):
     """Can this layer's backward GEMMs take the BatchNorm-backward apply on their A operand
     (conv_igemm.hip XF)? Not for an accumulating second-branch dgrad (ResNet GradLink) nor for
@@ -288,17 +299,17 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=Non
             raise ValueError("conv_backward: pass either dz or xf")
         if need_dx and ((link is not None and link.buf is not None) or spec.wt is not None):
             raise ValueError("conv_backward: xf cannot serve an accumulating / tap-reuse dgrad")
-    if (xf is None and need_dx and link is None and bna is None and bnf is None
-            and spec.wt is not None and not _common.BWD_SIDE_STREAM
-            and native().conv_tr_would_serve(g, ws.numel(), -1)):
-        # tap-reuse backward-data (conv_tr.hip) + the weight gradient as its own launch
-        native().conv_wgrad(g, ptr(dz), ptr(x), ptr(dweight), ptr(ws), ws.numel(), 0, s)
-        if weight is not None:
-            grad_ready([weight])
+    if bna is None and bnf is None and dgrad_tr_serves(spec, x, need_dx, link):
+        # tap-reuse backward-data (conv_tr.hip, Wc read k-major, dz from xf in the patch load)
+        # FIRST, then the weight gradient alone: its finish may apply the layer's SGD step
         dx = torch.empty_like(x)
-        if not native().conv_dgrad_tr(g, ptr(dz), ptr(spec.wt), ptr(dx), ptr(ws), ws.numel(), s):
-            raise RuntimeError("tap-reuse dgrad refused a shape it reported as served")
-        return dx
+        if native().conv_dgrad_tr_wc(g, ptr(dz), ptr(spec.wc), ptr(dx), ptr(ws), ws.numel(), s,
+                                     xf=xf):
+            native().conv_wgrad(g, ptr(dz), ptr(x), ptr(dweight), ptr(ws), ws.numel(), 0, s,
+                                xf=xf, final=1)
+            if weight is not None:
+                grad_ready([weight])
+            return dx
     if (need_dx and link is None and not _common.BWD_SIDE_STREAM and spec.stride == 1
             and spec.C == spec.Cr):
         # wgrad + dgrad of this layer as one grouped launch (+ one finish launch) when the
@@ -494,7 +505,8 @@ class _ConvBNActFn(torch.autograd.Function):
         if (_common.BN_BWD_FUSE and prev is not None and ctx.prev_z is not None
                 and ctx.needs_input_grad[0] and ctx.in_link is None and spec.stride == 1
                 and not prev.residual and prev.K == spec.C and spec.C == spec.Cr
-                and bn_bwd_fuse_pays(x.shape[1], x.shape[2], prev.pool)):
+                and bn_bwd_fuse_pays(x.shape[1], x.shape[2], prev.pool)
+                and not dgrad_tr_serves(spec, x, True, ctx.in_link)):
             pz = ctx.prev_z
             bnf = (ptr(pz), ptr(prev.coef), ptr(prev.sums), int(prev.pool), int(prev.relu),
                    pz.shape[1], pz.shape[2])
