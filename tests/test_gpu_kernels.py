@@ -689,7 +689,8 @@ def test_conv_bwd_xf(native_ext, case, pair_mode):
     conv, spec, x, xn = _conv_setup(N, Cin, H, H, K, 3, 1, 1, Creal)
     need_dx = not first
     s = stream_handle()
-    zt = bf(F.conv2d(x, conv.weight, conv.bias, 1, 1))  # bf16-valued conv output, NCHW
+    with torch.no_grad():  # bf16-valued conv output, NCHW (a leaf for the BN reference below)
+        zt = bf(F.conv2d(x, conv.weight, conv.bias, 1, 1))
     zn = zt.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
     gamma = torch.rand(K, device=DEV) + 0.5
     beta = torch.randn(K, device=DEV) * 0.1
