@@ -177,8 +177,11 @@ def join_side_streams():
 # reduce kernel stores dy_bn, the finalize writes the per-channel affine form of dz, and the
 # producing conv's backward GEMMs compute dz = A dy_bn + B z + C while staging their A operand —
 # dz is never written and never re-read. Layers the one-launch local BN backward serves keep it.
-# DDP_AMD_BN_BWD_XF=0 restores reduce -> finalize -> apply -> GEMMs on dz.
-BN_BWD_XF = os.environ.get("DDP_AMD_BN_BWD_XF", "1") != "0"
+# Opt-in (DDP_AMD_BN_BWD_XF=1): measured SLOWER end to end — VGG-11 b256 1.181 vs 0.852 ms,
+# b32 0.420 vs 0.402 ms (same box, profiles/r4d_*): the XF GEMMs stage z AND dy_bn (twice the
+# A-operand bytes, 72 KB of LDS -> 2 blocks per CU) and each k-step waits for its stage's DMAs
+# and a barrier before the rewrite, which serialises the ring (the 8x8 pair: 226 vs 46 us).
+BN_BWD_XF = os.environ.get("DDP_AMD_BN_BWD_XF", "0") == "1"
 
 
 # BatchNorm-backward sums of a Conv->BN->ReLU(->pool) block accumulated by the NEXT block's
