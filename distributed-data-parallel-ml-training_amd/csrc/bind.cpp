@@ -201,6 +201,32 @@ PYBIND11_MODULE(_native, m) {
     return rc == 1;
   }, py::arg("g"), py::arg("dz"), py::arg("wc"), py::arg("dx"), py::arg("ws"), py::arg("ws_elems"),
      py::arg("stream"), py::arg("xf") = py::none());
+  // VGG input block with z recomputed (conv_l0.hip): forward = statistics + BN/ReLU/pool
+  // passes into y; backward = BN-backward sums + dz passes (dgamma / dbeta accumulated)
+  m.def("l0_ok", [](py::tuple g) {
+    auto c = geom(g);
+    return ddp_l0_ok(&c) == 1;
+  });
+  m.def("l0_fwd", [](py::tuple g, uintptr_t x, uintptr_t wc, uintptr_t bias, float eps, int relu,
+                     uintptr_t stats, uintptr_t gamma, uintptr_t beta, uintptr_t coef, uintptr_t y,
+                     uintptr_t st) {
+    auto c = geom(g);
+    ddp_amd::L0Io io{};
+    io.x = P<void>(x); io.wc = P<void>(wc); io.bias = P<float>(bias); io.eps = eps; io.relu = relu;
+    io.stats = P<float>(stats); io.gamma = P<float>(gamma); io.beta = P<float>(beta);
+    io.coef = P<float>(coef); io.y = P<void>(y);
+    check(ddp_l0_fwd(&c, &io, S(st)), "l0_fwd");
+  });
+  m.def("l0_bwd", [](py::tuple g, uintptr_t x, uintptr_t wc, uintptr_t bias, float eps, int relu,
+                     uintptr_t coef, uintptr_t dy, uintptr_t sums, uintptr_t dz, uintptr_t dgamma,
+                     uintptr_t dbeta, uintptr_t st) {
+    auto c = geom(g);
+    ddp_amd::L0Io io{};
+    io.x = P<void>(x); io.wc = P<void>(wc); io.bias = P<float>(bias); io.eps = eps; io.relu = relu;
+    io.coef = P<float>(coef); io.dy = P<void>(dy); io.sums = P<float>(sums); io.dz = P<void>(dz);
+    io.dgamma = P<float>(dgamma); io.dbeta = P<float>(dbeta);
+    check(ddp_l0_bwd(&c, &io, S(st)), "l0_bwd");
+  });
   m.def("conv_tr_would_serve", [](py::tuple g, size_t ws_elems, int in_mode) {
     auto c = geom(g);
     return ddp_conv_tr_would_serve(&c, ws_elems, in_mode) == 1;

@@ -128,6 +128,26 @@ struct SgdFuse {
   int nesterov;
 };
 
+// VGG input block (conv_l0.hip): conv 3x3 (8 padded channels -> 64) + train-mode BN + ReLU +
+// 2x2 max-pool with z recomputed instead of stored
+struct L0Io {
+  const void* x;        // [N][H][W][8] bf16
+  const void* wc;       // [64][3][3][8] bf16
+  const float* bias;    // [64] or null
+  float eps;
+  int relu;
+  float* stats;         // [kStatRep][2][64] (zeroed per step)
+  const float* gamma;
+  const float* beta;
+  float* coef;          // [6][64] scale, shift, mean, invstd, k1, k2
+  void* y;              // [N][H/2][W/2][64] bf16 (forward output)
+  const void* dy;       // [N][H/2][W/2][64] bf16 (backward input)
+  float* sums;          // [kStatRep][2][64] (zeroed per step)
+  void* dz;             // [N][H][W][64] bf16 (backward output)
+  float* dgamma;
+  float* dbeta;
+};
+
 struct PackDesc {
   const float* p;          // fp32 master [K][Cr][R][S] (krsc == 0) or [K][R][S][Cr] (krsc == 1)
   unsigned short* wc;      // bf16 [K][R][S][C]   (may be null)
@@ -241,6 +261,9 @@ int ddp_bn_pool3_bwd(const ddp_amd::BnArgs* a, const unsigned char* idx, hipStre
 void ddp_conv_pair_mode(int mode, int items);
 void ddp_sgd_fuse_register(float* dw, const ddp_amd::SgdFuse* f, int clear);
 void ddp_sgd_fuse_begin();
+int ddp_l0_ok(const ddp_amd::ConvGeom* g);
+int ddp_l0_fwd(const ddp_amd::ConvGeom* g, const ddp_amd::L0Io* io, hipStream_t st);
+int ddp_l0_bwd(const ddp_amd::ConvGeom* g, const ddp_amd::L0Io* io, hipStream_t st);
 int ddp_conv_wgrad_final(const ddp_amd::ConvGeom* g, const void* dy, const void* x, float* dw,
                          float* ws, size_t ws_elems, int splits, const ddp_amd::BnBwdXf* xf,
                          hipStream_t st);

@@ -1,0 +1,420 @@
+// VGG input block for gfx950: conv 3x3 / s1 / p1 (3 image channels zero-padded to 8 -> 64) +
+// training-mode BatchNorm + ReLU + 2x2/s2 max-pool, with the pre-BatchNorm activation z
+// RECOMPUTED wherever it is needed instead of stored.
+//
+// Reference parity: the first block of part1/model.py:18-25 (Conv2d(3, 64, 3, padding=1) ->
+// BatchNorm2d(64) -> ReLU -> MaxPool2d(2, 2)); SURVEY.md §2.D row 0.
+//
+// Why: the layer's convolution is 0.9 GFLOP at batch 256 (27 MACs per output), but its output z
+// is the largest activation of the network (N x 32 x 32 x 64 bf16 = 33.5 MB at b256). The
+// unfused chain streams it five times — conv store, BN+pool read, BN-backward reduce read, apply
+// read — for ~66 us of a 0.85 ms step (profiles/r4f_vgg11_b256.md). Recomputing z from the
+// 4.2 MB input costs a few microseconds of MFMA per pass, so here:
+//   l0_stats_kernel  conv -> per-channel sum / sum of squares of the bf16-rounded z (no store)
+//   l0_fwd_kernel    conv -> BN (coefficients folded from the statistics in every block; block 0
+//                    writes the [6][64] table) -> ReLU -> 2x2 max-pool -> pooled y (8.4 MB)
+//   l0_bwd_kernel<0> conv -> the pool window's argmax and ReLU mask -> BN-backward sums S1 / S2
+//   l0_bwd_kernel<1> conv -> dz = scale * (dy_bn - k1 - xhat * k2) stored bf16 for the weight
+//                    gradient GEMM (k1 / k2 folded from S1 / S2; block 0 adds dgamma / dbeta)
+// Every pass runs the same conv code on the same inputs, so z, the window argmax and the ReLU
+// decisions are bit-identical to the forward's; the arithmetic of each step is the one of
+// conv_smallk.hip (conv) and bn_act.hip (finalize, apply, pool rule).
+//
+// Tiling: a wave owns 16 output pixels = 2 image rows x 8 columns (four whole 2x2 pool windows)
+// x 64 channels: the conv is conv_smallk.hip's direct MFMA (weights in registers, lane = one
+// pixel x 4 channels per 16-channel tile), and a pool window's four values sit in lanes
+// {l, l^1, l^8, l^9} of the same 16-lane row — exchanged with DPP (quad_perm, row_ror:8), no LDS.
+#include "common.h"
+#include "api.h"
+
+#include <algorithm>
+
+namespace ddp_amd {
+namespace l0 {
+
+constexpr int kK = 64;    // output channels
+constexpr int kNT = 4;    // 16-channel MFMA column tiles
+constexpr int kNKS = 3;   // k-steps of 4 taps (9 taps padded to 12)
+
+struct Args {
+  const unsigned short* x;   // [N][H][W][8] bf16 (channels 3..7 zero)
+  const unsigned short* wc;  // [64][3][3][8] bf16
+  const float* bias;         // [64] or null
+  int N, H, W, tiles;        // tiles = N * (H / 2) * (W / 8)
+  float eps;
+  int relu;
+  float* stats;              // [kStatRep][2][64] forward sums (zeroed per step)
+  const float* gamma;
+  const float* beta;
+  float* coef;               // [6][64]: scale, shift, mean, invstd, k1, k2
+  unsigned short* y;         // [N][H/2][W/2][64] pooled output
+  const unsigned short* dy;  // [N][H/2][W/2][64] gradient at the pooled output
+  float* sums;               // [kStatRep][2][64] BN-backward sums (zeroed per step)
+  unsigned short* dz;        // [N][H][W][64] gradient at z
+  float* dgamma;             // accumulated (arena)
+  float* dbeta;
+};
+
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bf16x8 as_bf(const uint4& v) { return __builtin_bit_cast(bf16x8, v); }
+
+// lane l of each 16-lane row <- lane l ^ 1 / l ^ 8
+__device__ __forceinline__ float xor1(float v) { return dpp_f<0xB1>(v); }
+__device__ __forceinline__ float xor8(float v) { return dpp_f<0x128>(v); }  // row_ror:8
+
+struct Tile {
+  int n, h, w;  // this lane's pixel
+  int hp, wo;   // its pool window (pooled row / column)
+  int d;        // its position in the window (bn_act.hip order: 0 (0,0), 1 (0,1), 2 (1,0), 3 (1,1))
+};
+
+__device__ __forceinline__ Tile tile_pixel(const Args& a, int t, int rl) {
+  const int wb = a.W / 8, per_img = (a.H / 2) * wb;
+  Tile p;
+  p.n = t / per_img;
+  const int rem = t - p.n * per_img;
+  p.hp = rem / wb;
+  const int cb = rem - p.hp * wb;
+  const int r = rl >> 3, c = rl & 7;
+  p.h = 2 * p.hp + r;
+  p.w = 8 * cb + c;
+  p.wo = 4 * cb + (c >> 1);
+  p.d = 2 * r + (c & 1);
+  return p;
+}
+
+// z of this lane's pixel for channels j*16 + 4g + v (bf16-rounded, + bias): conv_smallk.hip math
+__device__ __forceinline__ void conv_z(const Args& a, const uint4 (&wreg)[kNKS][kNT],
+                                       const float (&bias)[kNT][4], const Tile& p, int g,
+                                       float (&z)[kNT][4]) {
+  uint4 xf[kNKS];
+#pragma unroll
+  for (int t = 0; t < kNKS; ++t) {
+    const int tap = 4 * t + g;
+    const int r = tap / 3, s = tap - r * 3;
+    const int h = p.h + r - 1, w = p.w + s - 1;
+    xf[t] = (tap < 9 && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W)
+                ? *reinterpret_cast<const uint4*>(a.x + (((size_t)p.n * a.H + h) * a.W + w) * 8)
+                : make_uint4(0, 0, 0, 0);
+  }
+  f32x4 acc[kNT];
+#pragma unroll
+  for (int j = 0; j < kNT; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < kNKS; ++t)
+#pragma unroll
+    for (int j = 0; j < kNT; ++j)
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(wreg[t][j]), as_bf(xf[t]), acc[j], 0, 0, 0);
+#pragma unroll
+  for (int j = 0; j < kNT; ++j)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) z[j][v] = bf2f(f2bf(acc[j][v] + bias[j][v]));
+}
+
+__device__ __forceinline__ void load_weights(const Args& a, int g, int rl, uint4 (&wreg)[kNKS][kNT],
+                                             float (&bias)[kNT][4]) {
+#pragma unroll
+  for (int t = 0; t < kNKS; ++t)
+#pragma unroll
+    for (int j = 0; j < kNT; ++j) {
+      const int tap = 4 * t + g;
+      wreg[t][j] = tap < 9 ? *reinterpret_cast<const uint4*>(a.wc + ((size_t)(j * 16 + rl) * 9 + tap) * 8)
+                           : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+  for (int j = 0; j < kNT; ++j)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) bias[j][v] = a.bias ? a.bias[j * 16 + 4 * g + v] : 0.f;
+}
+
+// the four values of this lane's pool window, in window order 0..3: position k is held by the
+// lane whose d differs from this lane's in bits k ^ d (bit 0: lane ^ 1, bit 1: lane ^ 8).
+// Selected with compile-time k (a runtime-indexed array would live in scratch memory).
+__device__ __forceinline__ void window4(float v, int d, float (&q)[4]) {
+  const float x1 = xor1(v), x8 = xor8(v), x9 = xor1(x8);
+  const bool d0 = d & 1, d1 = (d >> 1) & 1;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bool m0 = d0 != (bool)(k & 1), m1 = d1 != (bool)(k & 2);
+    q[k] = m1 ? (m0 ? x9 : x8) : (m0 ? x1 : v);
+  }
+}
+
+// block reduction of per-lane channel sums (lane: channels j*16 + 4g + v) -> one atomic per
+// channel per block into replica blockIdx.x % kStatRep (conv_smallk.hip scheme)
+__device__ __forceinline__ void block_sums(float (&s1)[kNT][4], float (&s2)[kNT][4], float* rep,
+                                           int rl, int g) {
+#pragma unroll
+  for (int j = 0; j < kNT; ++j)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      s1[j][v] = dpp_sum16(s1[j][v]);
+      s2[j][v] = dpp_sum16(s2[j][v]);
+    }
+  __shared__ float red[4][2][kK];
+  const int wib = threadIdx.x >> 6;
+  if (rl == 0) {
+#pragma unroll
+    for (int j = 0; j < kNT; ++j)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        red[wib][0][j * 16 + 4 * g + v] = s1[j][v];
+        red[wib][1][j * 16 + 4 * g + v] = s2[j][v];
+      }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * kK) {
+    const int k = threadIdx.x / kK, c = threadIdx.x - k * kK;
+    atomicAdd(rep + k * kK + c, red[0][k][c] + red[1][k][c] + red[2][k][c] + red[3][k][c]);
+  }
+}
+
+// forward statistics of z (no store)
+__global__ __launch_bounds__(256) void l0_stats_kernel(Args a) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, rl = lane & 15;
+  uint4 wreg[kNKS][kNT];
+  float bias[kNT][4];
+  load_weights(a, g, rl, wreg, bias);
+  float s1[kNT][4] = {}, s2[kNT][4] = {};
+  const int nw = gridDim.x * 4;
+  for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < a.tiles; t += nw) {
+    const Tile p = tile_pixel(a, t, rl);
+    float z[kNT][4];
+    conv_z(a, wreg, bias, p, g, z);
+#pragma unroll
+    for (int j = 0; j < kNT; ++j)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        s1[j][v] += z[j][v];
+        s2[j][v] += z[j][v] * z[j][v];
+      }
+  }
+  block_sums(s1, s2, a.stats + (blockIdx.x % kStatRep) * 2 * kK, rl, g);
+}
+
+// this lane's 16 channels' (scale, shift) from the statistics replicas (bn_act.hip finalize);
+// block 0 also writes the [6][64] table for the backward
+__device__ __forceinline__ void fwd_coeffs(const Args& a, int g, float (&sc)[kNT][4],
+                                           float (&sh)[kNT][4]) {
+  __shared__ float cf[2][kK];
+  if (threadIdx.x < kK) {
+    const int c = threadIdx.x;
+    const float M = (float)a.N * a.H * a.W;
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int r = 0; r < kStatRep; ++r) {
+      s1 += a.stats[r * 2 * kK + c];
+      s2 += a.stats[r * 2 * kK + kK + c];
+    }
+    const float mu = s1 / M;
+    const float var = fmaxf(s2 / M - mu * mu, 0.f);
+    const float is = rsqrtf(var + a.eps);
+    const float s = a.gamma[c] * is, h = a.beta[c] - mu * s;
+    cf[0][c] = s;
+    cf[1][c] = h;
+    if (blockIdx.x == 0) {
+      a.coef[0 * kK + c] = s;
+      a.coef[1 * kK + c] = h;
+      a.coef[2 * kK + c] = mu;
+      a.coef[3 * kK + c] = is;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kNT; ++j)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      sc[j][v] = cf[0][j * 16 + 4 * g + v];
+      sh[j][v] = cf[1][j * 16 + 4 * g + v];
+    }
+}
+
+__global__ __launch_bounds__(256) void l0_fwd_kernel(Args a) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, rl = lane & 15;
+  uint4 wreg[kNKS][kNT];
+  float bias[kNT][4], sc[kNT][4], sh[kNT][4];
+  load_weights(a, g, rl, wreg, bias);
+  fwd_coeffs(a, g, sc, sh);
+  const int Ho = a.H / 2, Wo = a.W / 2;
+  const int nw = gridDim.x * 4;
+  for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < a.tiles; t += nw) {
+    const Tile p = tile_pixel(a, t, rl);
+    float z[kNT][4];
+    conv_z(a, wreg, bias, p, g, z);
+    u16x4 o[kNT];
+#pragma unroll
+    for (int j = 0; j < kNT; ++j)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        float y = z[j][v] * sc[j][v] + sh[j][v];  // (bn_act.hip apply expression)
+        if (a.relu) y = fmaxf(y, 0.f);
+        float q[4];
+        window4(y, p.d, q);
+        float best = -INFINITY;
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+          if (q[d] > best || q[d] != q[d]) best = q[d];  // bn_act.hip's pool rule
+        o[j][v] = f2bf(best);
+      }
+    if (p.d == 0) {
+      unsigned short* dst = a.y + (((size_t)p.n * Ho + p.hp) * Wo + p.wo) * kK + 4 * g;
+#pragma unroll
+      for (int j = 0; j < kNT; ++j) *reinterpret_cast<u16x4*>(dst + j * 16) = o[j];
+    }
+  }
+}
+
+// BN backward through the recomputed z. APPLY = 0: S1 / S2 sums; 1: dz (+ dgamma / dbeta)
+template <int APPLY>
+__global__ __launch_bounds__(256) void l0_bwd_kernel(Args a) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, rl = lane & 15;
+  uint4 wreg[kNKS][kNT];
+  float bias[kNT][4];
+  load_weights(a, g, rl, wreg, bias);
+  __shared__ float cf[6][kK];
+  if (threadIdx.x < kK) {
+    const int c = threadIdx.x;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) cf[r][c] = a.coef[r * kK + c];
+    if (APPLY) {  // finalize of the backward sums (bn_act.hip bn_finalize_bwd_kernel)
+      const float inv_m = 1.f / ((float)a.N * a.H * a.W);
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int r = 0; r < kStatRep; ++r) {
+        s1 += a.sums[r * 2 * kK + c];
+        s2 += a.sums[r * 2 * kK + kK + c];
+      }
+      cf[4][c] = s1 * inv_m;
+      cf[5][c] = s2 * inv_m;
+      if (blockIdx.x == 0) {
+        a.coef[4 * kK + c] = s1 * inv_m;
+        a.coef[5 * kK + c] = s2 * inv_m;
+        if (a.dgamma) a.dgamma[c] += s2;  // one writer per channel
+        if (a.dbeta) a.dbeta[c] += s1;
+      }
+    }
+  }
+  __syncthreads();
+  float sc[kNT][4], sh[kNT][4], mu[kNT][4], is[kNT][4], k1[kNT][4], k2[kNT][4];
+#pragma unroll
+  for (int j = 0; j < kNT; ++j)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int c = j * 16 + 4 * g + v;
+      sc[j][v] = cf[0][c];
+      sh[j][v] = cf[1][c];
+      mu[j][v] = cf[2][c];
+      is[j][v] = cf[3][c];
+      k1[j][v] = APPLY ? cf[4][c] : 0.f;
+      k2[j][v] = APPLY ? cf[5][c] : 0.f;
+    }
+  float s1[kNT][4] = {}, s2[kNT][4] = {};
+  const int Ho = a.H / 2, Wo = a.W / 2;
+  const int nw = gridDim.x * 4;
+  for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < a.tiles; t += nw) {
+    const Tile p = tile_pixel(a, t, rl);
+    // the pooled gradient of this lane's window (the four lanes of a window load the same 8 B)
+    const unsigned short* src = a.dy + (((size_t)p.n * Ho + p.hp) * Wo + p.wo) * kK + 4 * g;
+    u16x4 dv[kNT];
+#pragma unroll
+    for (int j = 0; j < kNT; ++j) dv[j] = *reinterpret_cast<const u16x4*>(src + j * 16);
+    float z[kNT][4];
+    conv_z(a, wreg, bias, p, g, z);
+    u16x4 o[kNT];
+#pragma unroll
+    for (int j = 0; j < kNT; ++j)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float zf = z[j][v];
+        const float y = zf * sc[j][v] + sh[j][v];
+        const float xh = (zf - mu[j][v]) * is[j][v];
+        float q[4];
+        window4(a.relu ? fmaxf(y, 0.f) : y, p.d, q);
+        float best = -INFINITY;
+        int arg = 0;
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+          if (q[d] > best || q[d] != q[d]) { best = q[d]; arg = d; }
+        const float gv = arg == p.d ? bf2f(dv[j][v]) : 0.f;
+        const float dyb = (a.relu && !(y > 0.f)) ? 0.f : gv;
+        if (APPLY) {
+          o[j][v] = f2bf(sc[j][v] * (dyb - k1[j][v] - xh * k2[j][v]));
+        } else {
+          s1[j][v] += dyb;
+          s2[j][v] += dyb * xh;
+        }
+      }
+    if (APPLY) {
+      unsigned short* dst = a.dz + (((size_t)p.n * a.H + p.h) * a.W + p.w) * kK + 4 * g;
+#pragma unroll
+      for (int j = 0; j < kNT; ++j) *reinterpret_cast<u16x4*>(dst + j * 16) = o[j];
+    }
+  }
+  if (!APPLY) block_sums(s1, s2, a.sums + (blockIdx.x % kStatRep) * 2 * kK, rl, g);
+}
+
+// ~8 tiles per wave (conv_smallk.hip's default), at most 2048 blocks
+static unsigned grid_for(int tiles) {
+  const int waves = (tiles + 7) / 8;
+  return (unsigned)std::max(1, std::min(2048, (waves + 3) / 4));
+}
+
+}  // namespace l0
+}  // namespace ddp_amd
+
+using namespace ddp_amd;
+
+static bool l0_shape_ok(const ConvGeom* g) {
+  return g->C == 8 && g->Creal <= 8 && g->K == l0::kK && g->R == 3 && g->S == 3 &&
+         g->stride == 1 && g->pad == 1 && g->P == g->H && g->Q == g->W && g->H % 2 == 0 &&
+         g->W % 8 == 0 && (size_t)g->N * g->H * g->W * l0::kK < (1ull << 31);
+}
+
+extern "C" int ddp_l0_ok(const ConvGeom* g) { return l0_shape_ok(g) ? 1 : 0; }
+
+static l0::Args l0_args(const ConvGeom* g, const L0Io* io) {
+  l0::Args a{};
+  a.x = (const unsigned short*)io->x;
+  a.wc = (const unsigned short*)io->wc;
+  a.bias = io->bias;
+  a.N = g->N; a.H = g->H; a.W = g->W;
+  a.tiles = g->N * (g->H / 2) * (g->W / 8);
+  a.eps = io->eps;
+  a.relu = io->relu;
+  a.stats = io->stats;
+  a.gamma = io->gamma;
+  a.beta = io->beta;
+  a.coef = io->coef;
+  a.y = (unsigned short*)io->y;
+  a.dy = (const unsigned short*)io->dy;
+  a.sums = io->sums;
+  a.dz = (unsigned short*)io->dz;
+  a.dgamma = io->dgamma;
+  a.dbeta = io->dbeta;
+  return a;
+}
+
+// forward: statistics pass + BN / ReLU / pool pass (stats zeroed by the caller); -1 = shape not
+// served
+extern "C" int ddp_l0_fwd(const ConvGeom* g, const L0Io* io, hipStream_t st) {
+  if (!l0_shape_ok(g) || !io->x || !io->wc || !io->stats || !io->gamma || !io->beta ||
+      !io->coef || !io->y)
+    return -1;
+  const l0::Args a = l0_args(g, io);
+  const unsigned nb = l0::grid_for(a.tiles);
+  hipLaunchKernelGGL(l0::l0_stats_kernel, dim3(nb), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(l0::l0_fwd_kernel, dim3(nb), dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+// backward: sums pass + dz pass (sums zeroed by the caller; coef = the forward's table)
+extern "C" int ddp_l0_bwd(const ConvGeom* g, const L0Io* io, hipStream_t st) {
+  if (!l0_shape_ok(g) || !io->x || !io->wc || !io->coef || !io->dy || !io->sums || !io->dz)
+    return -1;
+  const l0::Args a = l0_args(g, io);
+  const unsigned nb = l0::grid_for(a.tiles);
+  hipLaunchKernelGGL(l0::l0_bwd_kernel<0>, dim3(nb), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(l0::l0_bwd_kernel<1>, dim3(nb), dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}

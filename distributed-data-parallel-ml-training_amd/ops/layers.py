@@ -352,6 +352,24 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=Non
     return (dx, bool(done)) if bna is not None else dx
 
 
+# VGG input block (conv 3x3 over the 8-channel padded image -> 64, BN, ReLU, 2x2 pool) through
+# conv_l0.hip: its pre-BN activation z (the network's largest tensor) is recomputed from the
+# input in every pass that needs it instead of being stored and streamed four times.
+# DDP_AMD_L0_FUSE=0 restores conv_smallk + bn_act passes.
+L0_FUSE = os.environ.get("DDP_AMD_L0_FUSE", "1") != "0"
+
+
+def l0_serves(spec, x):
+    N, H, W, C = x.shape
+    if not (L0_FUSE and x.is_cuda and C == 8 and spec.C == 8 and spec.K == 64 and spec.pool
+            and spec.relu and not spec.maxpool3 and not spec.residual):
+        return False
+    cache = spec.__dict__.setdefault("_l0_cache", {})
+    if (N, H, W) not in cache:
+        cache[(N, H, W)] = bool(native().l0_ok(spec.geom(N, H, W)))
+    return cache[(N, H, W)]
+
+
 def _defer_bn(spec, residual, running_mean, N, Ho, Wo):
     """Defer this block's BatchNorm + ReLU (+ pool) forward into the next block's conv: only on
     a plain Conv->BN->ReLU(->pool) chain (no residual, batch statistics) whose next conv the
@@ -405,6 +423,19 @@ class _ConvBNActFn(torch.autograd.Function):
         if bn.track_running_stats and bn.running_mean is not None:
             rm, rv = bn.running_mean, bn.running_var
             use_running = 0 if bn.training else 1
+        ctx.l0 = residual is None and rm is None and fin is None and l0_serves(spec, x)
+        if ctx.l0:
+            # input block: statistics pass + BN/ReLU/pool pass, z never stored (conv_l0.hip)
+            native().l0_fwd(spec.geom(N, H, W), ptr(x), ptr(spec.wc), ptr(bias), spec.eps,
+                            int(spec.relu), ptr(stats), ptr(gamma), ptr(beta), ptr(spec.coef),
+                            ptr(y), stream_handle())
+            spec.fwd_z = None
+            spec.last_deferred = False
+            ctx.pool3_idx = None
+            ctx.spec, ctx.has_res, ctx.in_link, ctx.res_link = spec, False, in_link, res_link
+            ctx.prev_z = None
+            ctx.save_for_backward(x, None, stats, weight, bias, gamma, beta, None)
+            return y
         fused = False
         if residual is None and rm is None and BN_FWD_FUSE:
             # batch-statistics BN without residual (VGG): may run inside the conv's split-K finish
@@ -446,6 +477,22 @@ class _ConvBNActFn(torch.autograd.Function):
     def backward(ctx, dy):
         spec = ctx.spec
         x, z, stats, weight, bias, gamma, beta, residual = ctx.saved_tensors
+        if ctx.l0:
+            # input block: BN-backward sums + dz passes over the recomputed z, then the weight
+            # gradient GEMM on dz (the input itself needs no gradient)
+            N, H, W, _ = x.shape
+            dy = dy.contiguous()
+            gw, gg, gbt = ensure_grad(weight), ensure_grad(gamma), ensure_grad(beta)
+            if bias is not None:
+                ensure_grad(bias)  # analytically zero under batch-statistics BN (bn_act.hip)
+            dz = torch.empty(N, H, W, spec.K, dtype=BF16, device=x.device)
+            native().l0_bwd(spec.geom(N, H, W), ptr(x), ptr(spec.wc), ptr(bias), spec.eps,
+                            int(spec.relu), ptr(spec.coef), ptr(dy), ptr(spec.sums), ptr(dz),
+                            ptr(gg), ptr(gbt), stream_handle())
+            grad_ready([gamma, beta, bias])
+            dx = conv_backward(spec, x, dz, gw, ctx.needs_input_grad[0], ctx.in_link,
+                               weight=weight)
+            return dx, None, None, None, None, None, None, None, None
         N, P, Q, K = z.shape
         sums = spec.sums  # zeroed together with the statistics at the start of the forward
         dres = torch.empty_like(z) if (ctx.has_res and ctx.needs_input_grad[5]) else None

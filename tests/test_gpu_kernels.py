@@ -812,3 +812,51 @@ def test_sgd_in_backward_finish(native_ext, path):
     # the bf16 forward operand [K][R][S][C] (pad channels untouched = 0)
     wc = spec.wc.view(K, 3, 3, Cin).float()[..., :Creal]
     assert torch.equal(wc, p.permute(0, 2, 3, 1).to(torch.bfloat16).float())
+
+
+@pytest.mark.parametrize("N", [4, 32])
+def test_l0_fused_input_block(native_ext, N):
+    """VGG input block with z recomputed (conv_l0.hip): forward y = maxpool(relu(BN(conv(x)))) and
+    backward dz = d loss / d z, dgamma, dbeta against fp32 PyTorch autograd of the same block on
+    the same bf16-valued operands (z rounded to bf16 as the kernels store/recompute it)."""
+    from ddp_amd.ops.common import ptr, stream_handle
+    nat = native_ext
+    K, H = 64, 32
+    conv, spec, x, xn = _conv_setup(N, 8, H, H, K, 3, 1, 1, Creal=3)
+    g = spec.geom(N, H, H)
+    assert nat.l0_ok(g)
+    gamma = torch.rand(K, device=DEV) + 0.5
+    beta = torch.randn(K, device=DEV) * 0.1
+    eps = 1e-5
+    s = stream_handle()
+    stats = torch.zeros(16 * 2 * K, device=DEV)
+    coef = torch.full((6 * K,), float("nan"), device=DEV)
+    y = torch.full((N, H // 2, H // 2, K), float("nan"), device=DEV, dtype=torch.bfloat16)
+    nat.l0_fwd(g, ptr(xn), ptr(spec.wc), ptr(conv.bias), eps, 1, ptr(stats), ptr(gamma),
+               ptr(beta), ptr(coef), ptr(y), s)
+    dy = bf(torch.randn(N, K, H // 2, H // 2, device=DEV))
+    dyn = dy.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    sums = torch.zeros(16 * 2 * K, device=DEV)
+    dz = torch.full((N, H, H, K), float("nan"), device=DEV, dtype=torch.bfloat16)
+    dg = torch.zeros(K, device=DEV)
+    db = torch.zeros(K, device=DEV)
+    nat.l0_bwd(g, ptr(xn), ptr(spec.wc), ptr(conv.bias), eps, 1, ptr(coef), ptr(dyn), ptr(sums),
+               ptr(dz), ptr(dg), ptr(db), s)
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        z = bf(F.conv2d(x, conv.weight, conv.bias, 1, 1))
+    zr = z.clone().requires_grad_(True)
+    gr = gamma.clone().requires_grad_(True)
+    br = beta.clone().requires_grad_(True)
+    ref = F.max_pool2d(F.relu(F.batch_norm(zr, None, None, gr, br, training=True, eps=eps)), 2, 2)
+    ref.backward(dy)
+    assert not torch.isnan(y.float()).any() and not torch.isnan(dz.float()).any()
+    assert rel_err(y.permute(0, 3, 1, 2), ref) < 1e-2
+    assert rel_err(dz.permute(0, 3, 1, 2), zr.grad) < 2e-2
+    assert rel_err(dg, gr.grad) < 1e-2
+    assert rel_err(db, br.grad) < 1e-2
+    # the forward statistics are those of the bf16-rounded z
+    st = stats.view(16, 2 * K).sum(0)
+    zf = z.permute(0, 2, 3, 1).reshape(-1, K)
+    assert torch.allclose(st[:K], zf.sum(0), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(st[K:], (zf * zf).sum(0), rtol=1e-3, atol=1e-2)
