@@ -84,11 +84,27 @@ __device__ __forceinline__ Tile tile_pixel(const Args& a, int t, int rl) {
   return p;
 }
 
-// z of this lane's pixel for channels j*16 + 4g + v (bf16-rounded, + bias): conv_smallk.hip math
-__device__ __forceinline__ void conv_z(const Args& a, const uint4 (&wreg)[kNKS][kNT],
-                                       const float (&bias)[kNT][4], const Tile& p, int g,
-                                       float (&z)[kNT][4]) {
-  uint4 xf[kNKS];
+// LDS weight image [64 rows][13 taps][8 ch] (12 used taps + 1 pad tap per row spreads the 16
+// rows a ds_read_b128 lane group reads over the banks, conv_smallk.hip's stem layout), staged
+// once per block: the per-wave register copy of round-4's first version cost 48 VGPRs and
+// capped the kernel at 2 waves per SIMD
+constexpr int kRow = 13;
+struct Smem {
+  uint4 w[kK * kRow];
+  float cf[7][kK];  // 0 scale, 1 shift, 2 mean, 3 inv-std, 4 / 5 backward sums, 6 bias
+  float red[4][2][kK];
+};
+
+__device__ __forceinline__ void stage_weights(const Args& a, Smem& sm) {
+  for (int i = threadIdx.x; i < kK * 12; i += 256) {
+    const int k = i / 12, tap = i - k * 12;
+    sm.w[k * kRow + tap] = tap < 9 ? *reinterpret_cast<const uint4*>(a.wc + ((size_t)k * 9 + tap) * 8)
+                                   : make_uint4(0, 0, 0, 0);
+  }
+}
+
+// activation fragments of one tile: lane l loads tap 4t + (l >> 4) of its pixel (16 B)
+__device__ __forceinline__ void load_x(const Args& a, const Tile& p, int g, uint4 (&xf)[kNKS]) {
 #pragma unroll
   for (int t = 0; t < kNKS; ++t) {
     const int tap = 4 * t + g;
@@ -98,6 +114,11 @@ __device__ __forceinline__ void conv_z(const Args& a, const uint4 (&wreg)[kNKS][
                 ? *reinterpret_cast<const uint4*>(a.x + (((size_t)p.n * a.H + h) * a.W + w) * 8)
                 : make_uint4(0, 0, 0, 0);
   }
+}
+
+// z of this lane's pixel for channels j*16 + 4g + v (bf16-rounded, + bias): conv_smallk.hip math
+__device__ __forceinline__ void conv_z(const Smem& sm, const uint4 (&xf)[kNKS], int g, int rl,
+                                       float (&z)[kNT][4]) {
   f32x4 acc[kNT];
 #pragma unroll
   for (int j = 0; j < kNT; ++j) acc[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -105,27 +126,16 @@ __device__ __forceinline__ void conv_z(const Args& a, const uint4 (&wreg)[kNKS][
   for (int t = 0; t < kNKS; ++t)
 #pragma unroll
     for (int j = 0; j < kNT; ++j)
-      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(wreg[t][j]), as_bf(xf[t]), acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(sm.w[(j * 16 + rl) * kRow + 4 * t + g]),
+                                                      as_bf(xf[t]), acc[j], 0, 0, 0);
 #pragma unroll
   for (int j = 0; j < kNT; ++j)
 #pragma unroll
-    for (int v = 0; v < 4; ++v) z[j][v] = bf2f(f2bf(acc[j][v] + bias[j][v]));
+    for (int v = 0; v < 4; ++v) z[j][v] = bf2f(f2bf(acc[j][v] + sm.cf[6][j * 16 + 4 * g + v]));
 }
 
-__device__ __forceinline__ void load_weights(const Args& a, int g, int rl, uint4 (&wreg)[kNKS][kNT],
-                                             float (&bias)[kNT][4]) {
-#pragma unroll
-  for (int t = 0; t < kNKS; ++t)
-#pragma unroll
-    for (int j = 0; j < kNT; ++j) {
-      const int tap = 4 * t + g;
-      wreg[t][j] = tap < 9 ? *reinterpret_cast<const uint4*>(a.wc + ((size_t)(j * 16 + rl) * 9 + tap) * 8)
-                           : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-  for (int j = 0; j < kNT; ++j)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) bias[j][v] = a.bias ? a.bias[j * 16 + 4 * g + v] : 0.f;
+__device__ __forceinline__ void stage_bias(const Args& a, Smem& sm) {
+  if (threadIdx.x < kK) sm.cf[6][threadIdx.x] = a.bias ? a.bias[threadIdx.x] : 0.f;
 }
 
 // the four values of this lane's pool window, in window order 0..3: position k is held by the
@@ -144,7 +154,7 @@ __device__ __forceinline__ void window4(float v, int d, float (&q)[4]) {
 // block reduction of per-lane channel sums (lane: channels j*16 + 4g + v) -> one atomic per
 // channel per block into replica blockIdx.x % kStatRep (conv_smallk.hip scheme)
 __device__ __forceinline__ void block_sums(float (&s1)[kNT][4], float (&s2)[kNT][4], float* rep,
-                                           int rl, int g) {
+                                           int rl, int g, Smem& sm) {
 #pragma unroll
   for (int j = 0; j < kNT; ++j)
 #pragma unroll
@@ -152,36 +162,47 @@ __device__ __forceinline__ void block_sums(float (&s1)[kNT][4], float (&s2)[kNT]
       s1[j][v] = dpp_sum16(s1[j][v]);
       s2[j][v] = dpp_sum16(s2[j][v]);
     }
-  __shared__ float red[4][2][kK];
   const int wib = threadIdx.x >> 6;
   if (rl == 0) {
 #pragma unroll
     for (int j = 0; j < kNT; ++j)
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        red[wib][0][j * 16 + 4 * g + v] = s1[j][v];
-        red[wib][1][j * 16 + 4 * g + v] = s2[j][v];
+        sm.red[wib][0][j * 16 + 4 * g + v] = s1[j][v];
+        sm.red[wib][1][j * 16 + 4 * g + v] = s2[j][v];
       }
   }
   __syncthreads();
   if (threadIdx.x < 2 * kK) {
     const int k = threadIdx.x / kK, c = threadIdx.x - k * kK;
-    atomicAdd(rep + k * kK + c, red[0][k][c] + red[1][k][c] + red[2][k][c] + red[3][k][c]);
+    atomicAdd(rep + k * kK + c,
+              sm.red[0][k][c] + sm.red[1][k][c] + sm.red[2][k][c] + sm.red[3][k][c]);
   }
 }
 
+// Work split: a block = 4 waves, a wave walks tiles wave, wave + nw, ... (at most 1024 blocks:
+// every block ends with one atomic per channel into a statistics replica). Latency is hidden by
+// occupancy (waves per SIMD), not by a register prefetch: a second operand set cost ~40 VGPRs.
+#define L0_TILE_LOOP_BEGIN                                                  \
+  const int nw = gridDim.x * 4;                                            \
+  for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < a.tiles; t += nw) { \
+    /* keeps the LDS weight reads inside the loop (hoisted, they are 48 VGPRs) */ \
+    asm volatile("" ::: "memory");                                         \
+    const Tile cur = tile_pixel(a, t, rl);                                 \
+    uint4 xc[kNKS];                                                        \
+    load_x(a, cur, g, xc);
+
 // forward statistics of z (no store)
 __global__ __launch_bounds__(256) void l0_stats_kernel(Args a) {
+  __shared__ Smem sm;
   const int lane = threadIdx.x & 63, g = lane >> 4, rl = lane & 15;
-  uint4 wreg[kNKS][kNT];
-  float bias[kNT][4];
-  load_weights(a, g, rl, wreg, bias);
+  stage_weights(a, sm);
+  stage_bias(a, sm);
+  __syncthreads();
   float s1[kNT][4] = {}, s2[kNT][4] = {};
-  const int nw = gridDim.x * 4;
-  for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < a.tiles; t += nw) {
-    const Tile p = tile_pixel(a, t, rl);
+  L0_TILE_LOOP_BEGIN
     float z[kNT][4];
-    conv_z(a, wreg, bias, p, g, z);
+    conv_z(sm, xc, g, rl, z);
 #pragma unroll
     for (int j = 0; j < kNT; ++j)
 #pragma unroll
@@ -190,15 +211,15 @@ __global__ __launch_bounds__(256) void l0_stats_kernel(Args a) {
         s2[j][v] += z[j][v] * z[j][v];
       }
   }
-  block_sums(s1, s2, a.stats + (blockIdx.x % kStatRep) * 2 * kK, rl, g);
+  block_sums(s1, s2, a.stats + (blockIdx.x % kStatRep) * 2 * kK, rl, g, sm);
 }
 
-// this lane's 16 channels' (scale, shift) from the statistics replicas (bn_act.hip finalize);
-// block 0 also writes the [6][64] table for the backward
-__device__ __forceinline__ void fwd_coeffs(const Args& a, int g, float (&sc)[kNT][4],
-                                           float (&sh)[kNT][4]) {
-  __shared__ float cf[2][kK];
-  if (threadIdx.x < kK) {
+__global__ __launch_bounds__(256) void l0_fwd_kernel(Args a) {
+  __shared__ Smem sm;
+  const int lane = threadIdx.x & 63, g = lane >> 4, rl = lane & 15;
+  stage_weights(a, sm);
+  stage_bias(a, sm);
+  if (threadIdx.x < kK) {  // (scale, shift) from the statistics replicas (bn_act.hip finalize)
     const int c = threadIdx.x;
     const float M = (float)a.N * a.H * a.W;
     float s1 = 0.f, s2 = 0.f;
@@ -210,55 +231,39 @@ __device__ __forceinline__ void fwd_coeffs(const Args& a, int g, float (&sc)[kNT
     const float mu = s1 / M;
     const float var = fmaxf(s2 / M - mu * mu, 0.f);
     const float is = rsqrtf(var + a.eps);
-    const float s = a.gamma[c] * is, h = a.beta[c] - mu * s;
-    cf[0][c] = s;
-    cf[1][c] = h;
-    if (blockIdx.x == 0) {
-      a.coef[0 * kK + c] = s;
-      a.coef[1 * kK + c] = h;
+    const float sc = a.gamma[c] * is, sh = a.beta[c] - mu * sc;
+    sm.cf[0][c] = sc;
+    sm.cf[1][c] = sh;
+    if (blockIdx.x == 0) {  // the table the backward reads
+      a.coef[0 * kK + c] = sc;
+      a.coef[1 * kK + c] = sh;
       a.coef[2 * kK + c] = mu;
       a.coef[3 * kK + c] = is;
     }
   }
   __syncthreads();
-#pragma unroll
-  for (int j = 0; j < kNT; ++j)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      sc[j][v] = cf[0][j * 16 + 4 * g + v];
-      sh[j][v] = cf[1][j * 16 + 4 * g + v];
-    }
-}
-
-__global__ __launch_bounds__(256) void l0_fwd_kernel(Args a) {
-  const int lane = threadIdx.x & 63, g = lane >> 4, rl = lane & 15;
-  uint4 wreg[kNKS][kNT];
-  float bias[kNT][4], sc[kNT][4], sh[kNT][4];
-  load_weights(a, g, rl, wreg, bias);
-  fwd_coeffs(a, g, sc, sh);
   const int Ho = a.H / 2, Wo = a.W / 2;
-  const int nw = gridDim.x * 4;
-  for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < a.tiles; t += nw) {
-    const Tile p = tile_pixel(a, t, rl);
+  L0_TILE_LOOP_BEGIN
     float z[kNT][4];
-    conv_z(a, wreg, bias, p, g, z);
+    conv_z(sm, xc, g, rl, z);
     u16x4 o[kNT];
 #pragma unroll
     for (int j = 0; j < kNT; ++j)
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        float y = z[j][v] * sc[j][v] + sh[j][v];  // (bn_act.hip apply expression)
+        const int c = j * 16 + 4 * g + v;
+        float y = z[j][v] * sm.cf[0][c] + sm.cf[1][c];  // (bn_act.hip apply expression)
         if (a.relu) y = fmaxf(y, 0.f);
         float q[4];
-        window4(y, p.d, q);
+        window4(y, cur.d, q);
         float best = -INFINITY;
 #pragma unroll
         for (int d = 0; d < 4; ++d)
           if (q[d] > best || q[d] != q[d]) best = q[d];  // bn_act.hip's pool rule
         o[j][v] = f2bf(best);
       }
-    if (p.d == 0) {
-      unsigned short* dst = a.y + (((size_t)p.n * Ho + p.hp) * Wo + p.wo) * kK + 4 * g;
+    if (cur.d == 0) {
+      unsigned short* dst = a.y + (((size_t)cur.n * Ho + cur.hp) * Wo + cur.wo) * kK + 4 * g;
 #pragma unroll
       for (int j = 0; j < kNT; ++j) *reinterpret_cast<u16x4*>(dst + j * 16) = o[j];
     }
@@ -268,15 +273,14 @@ __global__ __launch_bounds__(256) void l0_fwd_kernel(Args a) {
 // BN backward through the recomputed z. APPLY = 0: S1 / S2 sums; 1: dz (+ dgamma / dbeta)
 template <int APPLY>
 __global__ __launch_bounds__(256) void l0_bwd_kernel(Args a) {
+  __shared__ Smem sm;
   const int lane = threadIdx.x & 63, g = lane >> 4, rl = lane & 15;
-  uint4 wreg[kNKS][kNT];
-  float bias[kNT][4];
-  load_weights(a, g, rl, wreg, bias);
-  __shared__ float cf[6][kK];
+  stage_weights(a, sm);
+  stage_bias(a, sm);
   if (threadIdx.x < kK) {
     const int c = threadIdx.x;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) cf[r][c] = a.coef[r * kK + c];
+    for (int r = 0; r < 4; ++r) sm.cf[r][c] = a.coef[r * kK + c];
     if (APPLY) {  // finalize of the backward sums (bn_act.hip bn_finalize_bwd_kernel)
       const float inv_m = 1.f / ((float)a.N * a.H * a.W);
       float s1 = 0.f, s2 = 0.f;
@@ -285,8 +289,8 @@ __global__ __launch_bounds__(256) void l0_bwd_kernel(Args a) {
         s1 += a.sums[r * 2 * kK + c];
         s2 += a.sums[r * 2 * kK + kK + c];
       }
-      cf[4][c] = s1 * inv_m;
-      cf[5][c] = s2 * inv_m;
+      sm.cf[4][c] = s1 * inv_m;
+      sm.cf[5][c] = s2 * inv_m;
       if (blockIdx.x == 0) {
         a.coef[4 * kK + c] = s1 * inv_m;
         a.coef[5 * kK + c] = s2 * inv_m;
@@ -296,68 +300,55 @@ __global__ __launch_bounds__(256) void l0_bwd_kernel(Args a) {
     }
   }
   __syncthreads();
-  float sc[kNT][4], sh[kNT][4], mu[kNT][4], is[kNT][4], k1[kNT][4], k2[kNT][4];
-#pragma unroll
-  for (int j = 0; j < kNT; ++j)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int c = j * 16 + 4 * g + v;
-      sc[j][v] = cf[0][c];
-      sh[j][v] = cf[1][c];
-      mu[j][v] = cf[2][c];
-      is[j][v] = cf[3][c];
-      k1[j][v] = APPLY ? cf[4][c] : 0.f;
-      k2[j][v] = APPLY ? cf[5][c] : 0.f;
-    }
   float s1[kNT][4] = {}, s2[kNT][4] = {};
   const int Ho = a.H / 2, Wo = a.W / 2;
-  const int nw = gridDim.x * 4;
-  for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < a.tiles; t += nw) {
-    const Tile p = tile_pixel(a, t, rl);
+  L0_TILE_LOOP_BEGIN
     // the pooled gradient of this lane's window (the four lanes of a window load the same 8 B)
-    const unsigned short* src = a.dy + (((size_t)p.n * Ho + p.hp) * Wo + p.wo) * kK + 4 * g;
+    const unsigned short* src = a.dy + (((size_t)cur.n * Ho + cur.hp) * Wo + cur.wo) * kK + 4 * g;
     u16x4 dv[kNT];
 #pragma unroll
     for (int j = 0; j < kNT; ++j) dv[j] = *reinterpret_cast<const u16x4*>(src + j * 16);
     float z[kNT][4];
-    conv_z(a, wreg, bias, p, g, z);
+    conv_z(sm, xc, g, rl, z);
     u16x4 o[kNT];
 #pragma unroll
     for (int j = 0; j < kNT; ++j)
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
+        const int c = j * 16 + 4 * g + v;
         const float zf = z[j][v];
-        const float y = zf * sc[j][v] + sh[j][v];
-        const float xh = (zf - mu[j][v]) * is[j][v];
+        const float y = zf * sm.cf[0][c] + sm.cf[1][c];
+        const float xh = (zf - sm.cf[2][c]) * sm.cf[3][c];
         float q[4];
-        window4(a.relu ? fmaxf(y, 0.f) : y, p.d, q);
+        window4(a.relu ? fmaxf(y, 0.f) : y, cur.d, q);
         float best = -INFINITY;
         int arg = 0;
 #pragma unroll
         for (int d = 0; d < 4; ++d)
           if (q[d] > best || q[d] != q[d]) { best = q[d]; arg = d; }
-        const float gv = arg == p.d ? bf2f(dv[j][v]) : 0.f;
+        const float gv = arg == cur.d ? bf2f(dv[j][v]) : 0.f;
         const float dyb = (a.relu && !(y > 0.f)) ? 0.f : gv;
         if (APPLY) {
-          o[j][v] = f2bf(sc[j][v] * (dyb - k1[j][v] - xh * k2[j][v]));
+          o[j][v] = f2bf(sm.cf[0][c] * (dyb - sm.cf[4][c] - xh * sm.cf[5][c]));
         } else {
           s1[j][v] += dyb;
           s2[j][v] += dyb * xh;
         }
       }
     if (APPLY) {
-      unsigned short* dst = a.dz + (((size_t)p.n * a.H + p.h) * a.W + p.w) * kK + 4 * g;
+      unsigned short* dst = a.dz + (((size_t)cur.n * a.H + cur.h) * a.W + cur.w) * kK + 4 * g;
 #pragma unroll
       for (int j = 0; j < kNT; ++j) *reinterpret_cast<u16x4*>(dst + j * 16) = o[j];
     }
   }
-  if (!APPLY) block_sums(s1, s2, a.sums + (blockIdx.x % kStatRep) * 2 * kK, rl, g);
+  if (!APPLY) block_sums(s1, s2, a.sums + (blockIdx.x % kStatRep) * 2 * kK, rl, g, sm);
 }
+#undef L0_TILE_LOOP_BEGIN
 
-// ~8 tiles per wave (conv_smallk.hip's default), at most 2048 blocks
+// one tile per wave where the grid allows, at most 1024 blocks (4 per CU; the statistics
+// atomics stay at one per channel per block)
 static unsigned grid_for(int tiles) {
-  const int waves = (tiles + 7) / 8;
-  return (unsigned)std::max(1, std::min(2048, (waves + 3) / 4));
+  return (unsigned)std::max(1, std::min(1024, (tiles + 3) / 4));
 }
 
 }  // namespace l0
