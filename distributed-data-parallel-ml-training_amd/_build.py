@@ -63,7 +63,25 @@ def _compile(cmd, src, obj, hdr_time, verbose):
     return obj, True
 
 
+def _sources():
+    return (sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+            + sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))) + [os.path.join(CSRC, "bind.cpp")])
+
+
+def up_to_date():
+    """The in-tree extension is newer than every source and header. The object cache
+    (build/native) does not travel with a snapshot, so this is what a GPU box checks: an
+    up-to-date extension is loaded as is instead of being rebuilt there."""
+    out = ext_path()
+    if not os.path.exists(out):
+        return False
+    newest = max([_newest_header()] + [os.path.getmtime(s) for s in _sources()])
+    return os.path.getmtime(out) >= newest
+
+
 def build(verbose=True, jobs=None):
+    if not os.path.isdir(BUILD) and up_to_date():
+        return ext_path()
     hipcc = _hipcc()
     os.makedirs(BUILD, exist_ok=True)
     inc = _includes()

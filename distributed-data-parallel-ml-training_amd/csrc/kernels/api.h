@@ -144,6 +144,7 @@ struct L0Io {
   const void* dy;       // [N][H/2][W/2][64] bf16 (backward input)
   float* sums;          // [kStatRep][2][64] (zeroed per step)
   void* dz;             // [N][H][W][64] bf16 (backward output)
+  void* code;           // [N][H/2][W/2][64] uint8: per pooled value, where its gradient goes
   float* dgamma;
   float* dbeta;
 };

@@ -51,6 +51,10 @@ struct Args {
   const unsigned short* dy;  // [N][H/2][W/2][64] gradient at the pooled output
   float* sums;               // [kStatRep][2][64] BN-backward sums (zeroed per step)
   unsigned short* dz;        // [N][H][W][64] gradient at z
+  unsigned* code;            // per pool window and channel: the position (0..3) that takes the
+                             // gradient, 4 = none (ReLU cut), 0xFF = NaN window; lane-major
+                             // [window][g][j][v] bytes, written by the forward, read by both
+                             // backward passes
   float* dgamma;             // accumulated (arena)
   float* dbeta;
 };
@@ -138,17 +142,13 @@ __device__ __forceinline__ void stage_bias(const Args& a, Smem& sm) {
   if (threadIdx.x < kK) sm.cf[6][threadIdx.x] = a.bias ? a.bias[threadIdx.x] : 0.f;
 }
 
-// the four values of this lane's pool window, in window order 0..3: position k is held by the
-// lane whose d differs from this lane's in bits k ^ d (bit 0: lane ^ 1, bit 1: lane ^ 8).
-// Selected with compile-time k (a runtime-indexed array would live in scratch memory).
-__device__ __forceinline__ void window4(float v, int d, float (&q)[4]) {
-  const float x1 = xor1(v), x8 = xor8(v), x9 = xor1(x8);
-  const bool d0 = d & 1, d1 = (d >> 1) & 1;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const bool m0 = d0 != (bool)(k & 1), m1 = d1 != (bool)(k & 2);
-    q[k] = m1 ? (m0 ? x9 : x8) : (m0 ? x1 : v);
-  }
+__device__ __forceinline__ int xor1i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false); }
+__device__ __forceinline__ int xor8i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false); }
+
+// max over the pool window (lanes l, l^1, l^8, l^9), NaN-propagating like bn_act.hip's pool
+__device__ __forceinline__ float window_max(float v) {
+  v = __builtin_elementwise_maximum(v, xor1(v));
+  return __builtin_elementwise_maximum(v, xor8(v));
 }
 
 // block reduction of per-lane channel sums (lane: channels j*16 + 4g + v) -> one atomic per
@@ -180,94 +180,141 @@ __device__ __forceinline__ void block_sums(float (&s1)[kNT][4], float (&s2)[kNT]
   }
 }
 
+// one tile's global operands: the input fragments and (backward) the pooled gradient of the
+// lane's window (the four lanes of a window load the same 8 B)
+struct Ops {
+  uint4 x[kNKS];
+  u16x4 dy[kNT];
+  uint4 code;
+};
+
+__device__ __forceinline__ size_t window_of(const Args& a, const Tile& p) {
+  return ((size_t)p.n * (a.H / 2) + p.hp) * (a.W / 2) + p.wo;
+}
+
+template <bool DY>
+__device__ __forceinline__ void load_ops(const Args& a, const Tile& p, int g, Ops& o) {
+  load_x(a, p, g, o.x);
+  if (DY) {
+    const size_t win = window_of(a, p);
+    const unsigned short* src = a.dy + win * kK + 4 * g;
+#pragma unroll
+    for (int j = 0; j < kNT; ++j) o.dy[j] = *reinterpret_cast<const u16x4*>(src + j * 16);
+    o.code = *reinterpret_cast<const uint4*>(a.code + win * (kK / 4) + g * 4);
+  }
+}
+
 // Work split: a block = 4 waves, a wave walks tiles wave, wave + nw, ... (at most 1024 blocks:
 // every block ends with one atomic per channel into a statistics replica). Latency is hidden by
-// occupancy (waves per SIMD), not by a register prefetch: a second operand set cost ~40 VGPRs.
-#define L0_TILE_LOOP_BEGIN                                                  \
-  const int nw = gridDim.x * 4;                                            \
-  for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < a.tiles; t += nw) { \
-    /* keeps the LDS weight reads inside the loop (hoisted, they are 48 VGPRs) */ \
-    asm volatile("" ::: "memory");                                         \
-    const Tile cur = tile_pixel(a, t, rl);                                 \
-    uint4 xc[kNKS];                                                        \
-    load_x(a, cur, g, xc);
+// occupancy (waves per SIMD): prefetching the next tile's operands into registers measured
+// slower (r4i: bwd 31 vs 28 us at b256, 176 VGPRs -> 2 waves per SIMD).
+template <bool DY, class Setup, class Body>
+__device__ __forceinline__ void tile_loop(const Args& a, int g, int rl, Setup setup, Body body) {
+  const int nw = gridDim.x * 4;
+  setup();
+  __syncthreads();
+  for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < a.tiles; t += nw) {
+    // keeps the LDS weight reads inside the loop (hoisted, they are 48 VGPRs)
+    asm volatile("" ::: "memory");
+    const Tile cur = tile_pixel(a, t, rl);
+    Ops op;
+    load_ops<DY>(a, cur, g, op);
+    body(cur, op);
+  }
+}
 
 // forward statistics of z (no store)
 __global__ __launch_bounds__(256) void l0_stats_kernel(Args a) {
   __shared__ Smem sm;
   const int lane = threadIdx.x & 63, g = lane >> 4, rl = lane & 15;
-  stage_weights(a, sm);
-  stage_bias(a, sm);
-  __syncthreads();
   float s1[kNT][4] = {}, s2[kNT][4] = {};
-  L0_TILE_LOOP_BEGIN
-    float z[kNT][4];
-    conv_z(sm, xc, g, rl, z);
+  tile_loop<false>(
+      a, g, rl,
+      [&] {
+        stage_weights(a, sm);
+        stage_bias(a, sm);
+      },
+      [&](const Tile&, const Ops& op) {
+        float z[kNT][4];
+        conv_z(sm, op.x, g, rl, z);
 #pragma unroll
-    for (int j = 0; j < kNT; ++j)
+        for (int j = 0; j < kNT; ++j)
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        s1[j][v] += z[j][v];
-        s2[j][v] += z[j][v] * z[j][v];
-      }
-  }
+          for (int v = 0; v < 4; ++v) {
+            s1[j][v] += z[j][v];
+            s2[j][v] += z[j][v] * z[j][v];
+          }
+      });
   block_sums(s1, s2, a.stats + (blockIdx.x % kStatRep) * 2 * kK, rl, g, sm);
 }
 
 __global__ __launch_bounds__(256) void l0_fwd_kernel(Args a) {
   __shared__ Smem sm;
   const int lane = threadIdx.x & 63, g = lane >> 4, rl = lane & 15;
-  stage_weights(a, sm);
-  stage_bias(a, sm);
-  if (threadIdx.x < kK) {  // (scale, shift) from the statistics replicas (bn_act.hip finalize)
-    const int c = threadIdx.x;
-    const float M = (float)a.N * a.H * a.W;
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int r = 0; r < kStatRep; ++r) {
-      s1 += a.stats[r * 2 * kK + c];
-      s2 += a.stats[r * 2 * kK + kK + c];
-    }
-    const float mu = s1 / M;
-    const float var = fmaxf(s2 / M - mu * mu, 0.f);
-    const float is = rsqrtf(var + a.eps);
-    const float sc = a.gamma[c] * is, sh = a.beta[c] - mu * sc;
-    sm.cf[0][c] = sc;
-    sm.cf[1][c] = sh;
-    if (blockIdx.x == 0) {  // the table the backward reads
-      a.coef[0 * kK + c] = sc;
-      a.coef[1 * kK + c] = sh;
-      a.coef[2 * kK + c] = mu;
-      a.coef[3 * kK + c] = is;
-    }
-  }
-  __syncthreads();
   const int Ho = a.H / 2, Wo = a.W / 2;
-  L0_TILE_LOOP_BEGIN
-    float z[kNT][4];
-    conv_z(sm, xc, g, rl, z);
-    u16x4 o[kNT];
+  tile_loop<false>(
+      a, g, rl,
+      [&] {
+        stage_weights(a, sm);
+        stage_bias(a, sm);
+        if (threadIdx.x < kK) {  // (scale, shift) from the statistics replicas (bn_act.hip finalize)
+          const int c = threadIdx.x;
+          const float M = (float)a.N * a.H * a.W;
+          float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int j = 0; j < kNT; ++j)
+          for (int r = 0; r < kStatRep; ++r) {
+            s1 += a.stats[r * 2 * kK + c];
+            s2 += a.stats[r * 2 * kK + kK + c];
+          }
+          const float mu = s1 / M;
+          const float var = fmaxf(s2 / M - mu * mu, 0.f);
+          const float is = rsqrtf(var + a.eps);
+          const float sc = a.gamma[c] * is, sh = a.beta[c] - mu * sc;
+          sm.cf[0][c] = sc;
+          sm.cf[1][c] = sh;
+          if (blockIdx.x == 0) {  // the table the backward reads
+            a.coef[0 * kK + c] = sc;
+            a.coef[1 * kK + c] = sh;
+            a.coef[2 * kK + c] = mu;
+            a.coef[3 * kK + c] = is;
+          }
+        }
+      },
+      [&](const Tile& cur, const Ops& op) {
+        float z[kNT][4];
+        conv_z(sm, op.x, g, rl, z);
+        const int bit = 1 << cur.d;
+        u16x4 o[kNT];
+        unsigned cw[kNT];
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int c = j * 16 + 4 * g + v;
-        float y = z[j][v] * sm.cf[0][c] + sm.cf[1][c];  // (bn_act.hip apply expression)
-        if (a.relu) y = fmaxf(y, 0.f);
-        float q[4];
-        window4(y, cur.d, q);
-        float best = -INFINITY;
+        for (int j = 0; j < kNT; ++j) {
+          cw[j] = 0;
 #pragma unroll
-        for (int d = 0; d < 4; ++d)
-          if (q[d] > best || q[d] != q[d]) best = q[d];  // bn_act.hip's pool rule
-        o[j][v] = f2bf(best);
-      }
-    if (cur.d == 0) {
-      unsigned short* dst = a.y + (((size_t)cur.n * Ho + cur.hp) * Wo + cur.wo) * kK + 4 * g;
+          for (int v = 0; v < 4; ++v) {
+            const int c = j * 16 + 4 * g + v;
+            float y = z[j][v] * sm.cf[0][c] + sm.cf[1][c];  // (bn_act.hip apply expression)
+            if (a.relu) y = fmaxf(y, 0.f);
+            const float m = window_max(y);
+            o[j][v] = f2bf(m);
+            // the gradient's destination: the window's first maximum (bn_act.hip's tie rule:
+            // every lane sets bit d when it holds the max, the lowest bit of the OR wins),
+            // none when ReLU zeroed the whole window (its winner had y <= 0)
+            int b = y == m ? bit : 0;
+            b |= xor1i(b);
+            b |= xor8i(b);
+            const unsigned cd = b == 0 ? 0xFFu : (a.relu && !(m > 0.f)) ? 4u : (unsigned)__builtin_ctz(b);
+            cw[j] |= cd << (8 * v);
+          }
+        }
+        if (cur.d == 0) {
+          const size_t win = window_of(a, cur);
+          unsigned short* dst = a.y + win * kK + 4 * g;
 #pragma unroll
-      for (int j = 0; j < kNT; ++j) *reinterpret_cast<u16x4*>(dst + j * 16) = o[j];
-    }
-  }
+          for (int j = 0; j < kNT; ++j) *reinterpret_cast<u16x4*>(dst + j * 16) = o[j];
+          *reinterpret_cast<uint4*>(a.code + win * (kK / 4) + g * 4) =
+              make_uint4(cw[0], cw[1], cw[2], cw[3]);
+        }
+      });
 }
 
 // BN backward through the recomputed z. APPLY = 0: S1 / S2 sums; 1: dz (+ dgamma / dbeta)
@@ -275,80 +322,78 @@ template <int APPLY>
 __global__ __launch_bounds__(256) void l0_bwd_kernel(Args a) {
   __shared__ Smem sm;
   const int lane = threadIdx.x & 63, g = lane >> 4, rl = lane & 15;
-  stage_weights(a, sm);
-  stage_bias(a, sm);
-  if (threadIdx.x < kK) {
-    const int c = threadIdx.x;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) sm.cf[r][c] = a.coef[r * kK + c];
-    if (APPLY) {  // finalize of the backward sums (bn_act.hip bn_finalize_bwd_kernel)
-      const float inv_m = 1.f / ((float)a.N * a.H * a.W);
-      float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int r = 0; r < kStatRep; ++r) {
-        s1 += a.sums[r * 2 * kK + c];
-        s2 += a.sums[r * 2 * kK + kK + c];
-      }
-      sm.cf[4][c] = s1 * inv_m;
-      sm.cf[5][c] = s2 * inv_m;
-      if (blockIdx.x == 0) {
-        a.coef[4 * kK + c] = s1 * inv_m;
-        a.coef[5 * kK + c] = s2 * inv_m;
-        if (a.dgamma) a.dgamma[c] += s2;  // one writer per channel
-        if (a.dbeta) a.dbeta[c] += s1;
-      }
-    }
-  }
-  __syncthreads();
   float s1[kNT][4] = {}, s2[kNT][4] = {};
-  const int Ho = a.H / 2, Wo = a.W / 2;
-  L0_TILE_LOOP_BEGIN
-    // the pooled gradient of this lane's window (the four lanes of a window load the same 8 B)
-    const unsigned short* src = a.dy + (((size_t)cur.n * Ho + cur.hp) * Wo + cur.wo) * kK + 4 * g;
-    u16x4 dv[kNT];
+  tile_loop<true>(
+      a, g, rl,
+      [&] {
+        stage_weights(a, sm);
+        stage_bias(a, sm);
+        if (threadIdx.x < kK) {
+          const int c = threadIdx.x;
+          // LDS rows: 0 scale, 2 invstd, 3 -mean * invstd (xhat = z * [2] + [3]); APPLY:
+          // 4 / 5 with dz = scale * dy_bn + z * [4] + [5], the bn_act.hip apply expression
+          // scale * (dy_bn - k1 - xhat * k2) expanded in z
+          const float sc = a.coef[c], mu = a.coef[2 * kK + c], is = a.coef[3 * kK + c];
+          sm.cf[0][c] = sc;
+          sm.cf[2][c] = is;
+          sm.cf[3][c] = -mu * is;
+          if (APPLY) {  // finalize of the backward sums (bn_act.hip bn_finalize_bwd_kernel)
+            const float inv_m = 1.f / ((float)a.N * a.H * a.W);
+            float t1 = 0.f, t2 = 0.f;
 #pragma unroll
-    for (int j = 0; j < kNT; ++j) dv[j] = *reinterpret_cast<const u16x4*>(src + j * 16);
-    float z[kNT][4];
-    conv_z(sm, xc, g, rl, z);
-    u16x4 o[kNT];
-#pragma unroll
-    for (int j = 0; j < kNT; ++j)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int c = j * 16 + 4 * g + v;
-        const float zf = z[j][v];
-        const float y = zf * sm.cf[0][c] + sm.cf[1][c];
-        const float xh = (zf - sm.cf[2][c]) * sm.cf[3][c];
-        float q[4];
-        window4(a.relu ? fmaxf(y, 0.f) : y, cur.d, q);
-        float best = -INFINITY;
-        int arg = 0;
-#pragma unroll
-        for (int d = 0; d < 4; ++d)
-          if (q[d] > best || q[d] != q[d]) { best = q[d]; arg = d; }
-        const float gv = arg == cur.d ? bf2f(dv[j][v]) : 0.f;
-        const float dyb = (a.relu && !(y > 0.f)) ? 0.f : gv;
-        if (APPLY) {
-          o[j][v] = f2bf(sm.cf[0][c] * (dyb - sm.cf[4][c] - xh * sm.cf[5][c]));
-        } else {
-          s1[j][v] += dyb;
-          s2[j][v] += dyb * xh;
+            for (int r = 0; r < kStatRep; ++r) {
+              t1 += a.sums[r * 2 * kK + c];
+              t2 += a.sums[r * 2 * kK + kK + c];
+            }
+            const float k1 = t1 * inv_m, k2 = t2 * inv_m;
+            sm.cf[4][c] = -sc * k2 * is;
+            sm.cf[5][c] = sc * (k2 * is * mu - k1);
+            if (blockIdx.x == 0) {
+              a.coef[4 * kK + c] = k1;
+              a.coef[5 * kK + c] = k2;
+              if (a.dgamma) a.dgamma[c] += t2;  // one writer per channel
+              if (a.dbeta) a.dbeta[c] += t1;
+            }
+          }
         }
-      }
-    if (APPLY) {
-      unsigned short* dst = a.dz + (((size_t)cur.n * a.H + cur.h) * a.W + cur.w) * kK + 4 * g;
+      },
+      [&](const Tile& cur, const Ops& op) {
+        float z[kNT][4];
+        conv_z(sm, op.x, g, rl, z);
+        const unsigned cw[kNT] = {op.code.x, op.code.y, op.code.z, op.code.w};
+        u16x4 o[kNT];
 #pragma unroll
-      for (int j = 0; j < kNT; ++j) *reinterpret_cast<u16x4*>(dst + j * 16) = o[j];
-    }
-  }
+        for (int j = 0; j < kNT; ++j)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int c = j * 16 + 4 * g + v;
+            const float zf = z[j][v];
+            // the forward's verdict: this lane's pixel takes the pooled gradient
+            const float dyb = ((cw[j] >> (8 * v)) & 0xFFu) == (unsigned)cur.d ? bf2f(op.dy[j][v]) : 0.f;
+            if (APPLY) {
+              o[j][v] = f2bf(sm.cf[0][c] * dyb + (zf * sm.cf[4][c] + sm.cf[5][c]));
+            } else {
+              s1[j][v] += dyb;
+              s2[j][v] += dyb * (zf * sm.cf[2][c] + sm.cf[3][c]);
+            }
+          }
+        if (APPLY) {
+          unsigned short* dst = a.dz + (((size_t)cur.n * a.H + cur.h) * a.W + cur.w) * kK + 4 * g;
+#pragma unroll
+          for (int j = 0; j < kNT; ++j) *reinterpret_cast<u16x4*>(dst + j * 16) = o[j];
+        }
+      });
   if (!APPLY) block_sums(s1, s2, a.sums + (blockIdx.x % kStatRep) * 2 * kK, rl, g, sm);
 }
-#undef L0_TILE_LOOP_BEGIN
 
 // one tile per wave where the grid allows, at most 1024 blocks (4 per CU; the statistics
 // atomics stay at one per channel per block)
 static unsigned grid_for(int tiles) {
-  return (unsigned)std::max(1, std::min(1024, (tiles + 3) / 4));
+  static const int cap = [] {
+    const char* e = std::getenv("DDP_AMD_L0_BLOCKS");
+    return e ? std::max(1, atoi(e)) : 1024;
+  }();
+  return (unsigned)std::max(1, std::min(cap, (tiles + 3) / 4));
 }
 
 }  // namespace l0
@@ -381,6 +426,7 @@ static l0::Args l0_args(const ConvGeom* g, const L0Io* io) {
   a.dy = (const unsigned short*)io->dy;
   a.sums = io->sums;
   a.dz = (unsigned short*)io->dz;
+  a.code = (unsigned*)io->code;
   a.dgamma = io->dgamma;
   a.dbeta = io->dbeta;
   return a;
@@ -390,7 +436,7 @@ static l0::Args l0_args(const ConvGeom* g, const L0Io* io) {
 // served
 extern "C" int ddp_l0_fwd(const ConvGeom* g, const L0Io* io, hipStream_t st) {
   if (!l0_shape_ok(g) || !io->x || !io->wc || !io->stats || !io->gamma || !io->beta ||
-      !io->coef || !io->y)
+      !io->coef || !io->y || !io->code)
     return -1;
   const l0::Args a = l0_args(g, io);
   const unsigned nb = l0::grid_for(a.tiles);
@@ -401,7 +447,8 @@ extern "C" int ddp_l0_fwd(const ConvGeom* g, const L0Io* io, hipStream_t st) {
 
 // backward: sums pass + dz pass (sums zeroed by the caller; coef = the forward's table)
 extern "C" int ddp_l0_bwd(const ConvGeom* g, const L0Io* io, hipStream_t st) {
-  if (!l0_shape_ok(g) || !io->x || !io->wc || !io->coef || !io->dy || !io->sums || !io->dz)
+  if (!l0_shape_ok(g) || !io->x || !io->wc || !io->coef || !io->dy || !io->sums || !io->dz ||
+      !io->code)
     return -1;
   const l0::Args a = l0_args(g, io);
   const unsigned nb = l0::grid_for(a.tiles);

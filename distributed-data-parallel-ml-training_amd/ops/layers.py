@@ -426,9 +426,12 @@ class _ConvBNActFn(torch.autograd.Function):
         ctx.l0 = residual is None and rm is None and fin is None and l0_serves(spec, x)
         if ctx.l0:
             # input block: statistics pass + BN/ReLU/pool pass, z never stored (conv_l0.hip)
+            # code: per pooled value, the window position its gradient goes to (1 B each)
+            code = torch.empty(N, Ho, Wo, spec.K, dtype=torch.uint8, device=x.device)
             native().l0_fwd(spec.geom(N, H, W), ptr(x), ptr(spec.wc), ptr(bias), spec.eps,
                             int(spec.relu), ptr(stats), ptr(gamma), ptr(beta), ptr(spec.coef),
-                            ptr(y), stream_handle())
+                            ptr(y), ptr(code), stream_handle())
+            ctx.l0_code = code
             spec.fwd_z = None
             spec.last_deferred = False
             ctx.pool3_idx = None
@@ -488,7 +491,8 @@ class _ConvBNActFn(torch.autograd.Function):
             dz = torch.empty(N, H, W, spec.K, dtype=BF16, device=x.device)
             native().l0_bwd(spec.geom(N, H, W), ptr(x), ptr(spec.wc), ptr(bias), spec.eps,
                             int(spec.relu), ptr(spec.coef), ptr(dy), ptr(spec.sums), ptr(dz),
-                            ptr(gg), ptr(gbt), stream_handle())
+                            ptr(gg), ptr(gbt), ptr(ctx.l0_code), stream_handle())
+            ctx.l0_code = None
             grad_ready([gamma, beta, bias])
             dx = conv_backward(spec, x, dz, gw, ctx.needs_input_grad[0], ctx.in_link,
                                weight=weight)

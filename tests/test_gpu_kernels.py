@@ -832,8 +832,9 @@ def test_l0_fused_input_block(native_ext, N):
     stats = torch.zeros(16 * 2 * K, device=DEV)
     coef = torch.full((6 * K,), float("nan"), device=DEV)
     y = torch.full((N, H // 2, H // 2, K), float("nan"), device=DEV, dtype=torch.bfloat16)
+    code = torch.full((N, H // 2, H // 2, K), 0xEE, device=DEV, dtype=torch.uint8)
     nat.l0_fwd(g, ptr(xn), ptr(spec.wc), ptr(conv.bias), eps, 1, ptr(stats), ptr(gamma),
-               ptr(beta), ptr(coef), ptr(y), s)
+               ptr(beta), ptr(coef), ptr(y), ptr(code), s)
     dy = bf(torch.randn(N, K, H // 2, H // 2, device=DEV))
     dyn = dy.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
     sums = torch.zeros(16 * 2 * K, device=DEV)
@@ -841,8 +842,13 @@ def test_l0_fused_input_block(native_ext, N):
     dg = torch.zeros(K, device=DEV)
     db = torch.zeros(K, device=DEV)
     nat.l0_bwd(g, ptr(xn), ptr(spec.wc), ptr(conv.bias), eps, 1, ptr(coef), ptr(dyn), ptr(sums),
-               ptr(dz), ptr(dg), ptr(db), s)
+               ptr(dz), ptr(dg), ptr(db), ptr(code), s)
     torch.cuda.synchronize()
+    # every pooled value got a verdict: a window position, or 4 = ReLU zeroed the window; the
+    # bytes are lane-major ([g][j][v] for channel j*16 + 4g + v), 4 exactly where y is 0
+    assert int(code.max()) <= 4
+    code_c = code.view(N, H // 2, H // 2, 4, 4, 4).permute(0, 1, 2, 4, 3, 5).reshape(y.shape)
+    assert torch.equal(code_c == 4, y == 0)
     with torch.no_grad():
         z = bf(F.conv2d(x, conv.weight, conv.bias, 1, 1))
     zr = z.clone().requires_grad_(True)
