@@ -12,18 +12,22 @@
 // 4.2 MB input costs a few microseconds of MFMA per pass, so here:
 //   l0_stats_kernel  conv -> per-channel sum / sum of squares of the bf16-rounded z (no store)
 //   l0_fwd_kernel    conv -> BN (coefficients folded from the statistics in every block; block 0
-//                    writes the [6][64] table) -> ReLU -> 2x2 max-pool -> pooled y (8.4 MB)
-//   l0_bwd_kernel<0> conv -> the pool window's argmax and ReLU mask -> BN-backward sums S1 / S2
+//                    writes the [6][64] table) -> ReLU -> 2x2 max-pool -> pooled y (8.4 MB) and,
+//                    per pooled value, the window position its gradient goes to (1 B, 4.2 MB)
+//   l0_bwd_kernel<0> conv -> BN-backward sums S1 / S2 of the routed gradient
 //   l0_bwd_kernel<1> conv -> dz = scale * (dy_bn - k1 - xhat * k2) stored bf16 for the weight
 //                    gradient GEMM (k1 / k2 folded from S1 / S2; block 0 adds dgamma / dbeta)
-// Every pass runs the same conv code on the same inputs, so z, the window argmax and the ReLU
-// decisions are bit-identical to the forward's; the arithmetic of each step is the one of
-// conv_smallk.hip (conv) and bn_act.hip (finalize, apply, pool rule).
+// Every pass runs the same conv code on the same inputs, so z is bit-identical to the forward's;
+// the arithmetic of each step is the one of conv_smallk.hip (conv) and bn_act.hip (finalize,
+// apply, first-maximum pool rule).
 //
 // Tiling: a wave owns 16 output pixels = 2 image rows x 8 columns (four whole 2x2 pool windows)
-// x 64 channels: the conv is conv_smallk.hip's direct MFMA (weights in registers, lane = one
-// pixel x 4 channels per 16-channel tile), and a pool window's four values sit in lanes
-// {l, l^1, l^8, l^9} of the same 16-lane row — exchanged with DPP (quad_perm, row_ror:8), no LDS.
+// x 64 channels: the conv is conv_smallk.hip's direct MFMA (lane = one pixel x 4 channels per
+// 16-channel tile, weights read from an LDS image staged once per block), and a pool window's
+// four values sit in lanes {l, l^1, l^8, l^9} of the same 16-lane row — max and argmax are
+// exchanged with DPP (quad_perm, row_ror:8), no LDS.
+// Measured (profiles/r4k_vgg11_b256_l0v5.md): 12.0 + 19.1 us forward, 15.3 + 17.3 us backward
+// at b256 against ~66 us of conv + BN passes unfused; step 0.835-0.846 vs 0.855 ms same box.
 #include "common.h"
 #include "api.h"
 
@@ -386,14 +390,12 @@ __global__ __launch_bounds__(256) void l0_bwd_kernel(Args a) {
   if (!APPLY) block_sums(s1, s2, a.sums + (blockIdx.x % kStatRep) * 2 * kK, rl, g, sm);
 }
 
-// one tile per wave where the grid allows, at most 1024 blocks (4 per CU; the statistics
-// atomics stay at one per channel per block)
+// one tile per wave where the grid allows, at most 1024 blocks (4 per CU): every block adds one
+// partial sum per channel into a statistics replica, and memory-side atomics serialise per
+// address (measured r4j, b256: 1024 blocks 15.3 / 17.3 us backward passes, 4096 blocks 35.6 /
+// 26.5 us; 512 / 2048 blocks equal to 1024 within the run-to-run spread)
 static unsigned grid_for(int tiles) {
-  static const int cap = [] {
-    const char* e = std::getenv("DDP_AMD_L0_BLOCKS");
-    return e ? std::max(1, atoi(e)) : 1024;
-  }();
-  return (unsigned)std::max(1, std::min(cap, (tiles + 3) / 4));
+  return (unsigned)std::max(1, std::min(1024, (tiles + 3) / 4));
 }
 
 }  // namespace l0
