@@ -66,18 +66,6 @@ static const ddp_amd::BnBwdFuse* bn_fuse(py::object o, ddp_amd::BnBwdFuse* f) {
   return f;
 }
 
-// (z, g, coef, C[, mask]) -> BnBwdXf (None -> nullptr)
-static const ddp_amd::BnBwdXf* xf_args(py::object o, ddp_amd::BnBwdXf* x) {
-  if (o.is_none()) return nullptr;
-  auto t = o.cast<py::tuple>();
-  x->z = P<void>(t[0].cast<uintptr_t>());
-  x->g = P<void>(t[1].cast<uintptr_t>());
-  x->coef = P<float>(t[2].cast<uintptr_t>());
-  x->C = t[3].cast<int>();
-  x->mask = t.size() > 4 ? t[4].cast<int>() : 0;
-  return x;
-}
-
 // (dz, dgamma, dbeta) -> BnBwdApply (None -> nullptr)
 static const ddp_amd::BnBwdApply* bn_apply(py::object o, ddp_amd::BnBwdApply* out) {
   if (o.is_none()) return nullptr;
@@ -179,28 +167,6 @@ PYBIND11_MODULE(_native, m) {
   }, py::arg("g"), py::arg("x"), py::arg("wc"), py::arg("bias"), py::arg("z"), py::arg("stats"),
      py::arg("ws"), py::arg("ws_elems"), py::arg("st"), py::arg("bn") = py::none(),
      py::arg("fin") = py::none());
-  m.def("conv_dgrad_tr", [](py::tuple g, uintptr_t dz, uintptr_t wt, uintptr_t dx, uintptr_t ws,
-                            size_t ws_elems, uintptr_t st) {
-    auto c = geom(g);
-    const int rc = ddp_conv_dgrad_tr(&c, P<void>(dz), P<void>(wt), P<void>(dx), P<float>(ws),
-                                     ws_elems, S(st));
-    if (rc >= 2) check(rc - 2, "conv_dgrad_tr");
-    return rc == 1;
-  });
-  // tap-reuse backward-data reading the FORWARD weight copy wc k-major; xf = (z, g, coef, C,
-  // mask): dz computed in the patch load (dz pointer ignored). True when served.
-  m.def("conv_dgrad_tr_wc", [](py::tuple g, uintptr_t dz, uintptr_t wc, uintptr_t dx,
-                               uintptr_t ws, size_t ws_elems, uintptr_t st, py::object xf) {
-    auto c = geom(g);
-    ddp_amd::BnBwdXf xv{};
-    const ddp_amd::BnBwdXf* xp = xf_args(xf, &xv);
-    const int rc = ddp_conv_dgrad_tr_wc(&c, P<void>(dz), P<void>(wc), P<void>(dx), P<float>(ws),
-                                        ws_elems, xp, S(st));
-    if (rc < 0) check(rc, "conv_dgrad_tr_wc");
-    if (rc >= 2) check(rc - 2, "conv_dgrad_tr_wc");
-    return rc == 1;
-  }, py::arg("g"), py::arg("dz"), py::arg("wc"), py::arg("dx"), py::arg("ws"), py::arg("ws_elems"),
-     py::arg("stream"), py::arg("xf") = py::none());
   // VGG input block with z recomputed (conv_l0.hip): forward = statistics + BN/ReLU/pool
   // passes into y; backward = BN-backward sums + dz passes (dgamma / dbeta accumulated)
   m.def("l0_ok", [](py::tuple g) {
@@ -293,82 +259,43 @@ PYBIND11_MODULE(_native, m) {
   // block whose BatchNorm-backward sums the dgrad epilogue accumulates (api.h BnBwdFuse)
   // bna: optional (dz, dgamma, dbeta) — complete that block's BN backward in the split-K finish
   // when possible (api.h BnBwdApply); returns True when it did (dx is then NOT written)
-  // xf: optional (z, g, coef, C) — the BatchNorm-backward apply computed on the A operand of
-  // the backward GEMMs (api.h BnBwdXf; dy is then ignored: the operand is dz = A g + B z + C)
-  m.def("conv_xf_ok", [](py::tuple g, int need_dx) {
-    auto c = geom(g);
-    return ddp_conv_xf_ok(&c, need_dx) != 0;
-  });
   m.def("conv_dgrad", [](py::tuple g, uintptr_t dy, uintptr_t wt, uintptr_t dx, uintptr_t ws,
                          size_t ws_elems, int splits, uintptr_t st, int accumulate, py::object bn,
-                         py::object bna, py::object xf) {
+                         py::object bna) {
     auto c = geom(g);
-    ddp_amd::BnBwdXf xv{};
-    const ddp_amd::BnBwdXf* xp = xf_args(xf, &xv);
-    if (xp) {
-      ddp_amd::BnBwdFuse f{};
-      const ddp_amd::BnBwdFuse* fp = bn_fuse(bn, &f);
-      ddp_amd::BnBwdApply ap{};
-      const ddp_amd::BnBwdApply* app = fp ? bn_apply(bna, &ap) : nullptr;
-      int done = 0;
-      if (accumulate) check(-4, "conv_dgrad (xf cannot accumulate)");
-      check(ddp_conv_dgrad_xf(&c, P<void>(wt), P<void>(dx), P<float>(ws), ws_elems, fp, app,
-                              &done, xp, S(st)), "conv_dgrad_xf");
-      return done == 1;
-    }
     if (bn.is_none()) {
       check(ddp_conv_dgrad(&c, P<void>(dy), P<void>(wt), P<void>(dx), P<float>(ws), ws_elems,
                            splits, accumulate, S(st)), "conv_dgrad");
       return false;
     }
-    auto t = bn.cast<py::tuple>();
     ddp_amd::BnBwdFuse f{};
-    f.z = P<unsigned short>(t[0].cast<uintptr_t>());
-    f.coef = P<float>(t[1].cast<uintptr_t>());
-    f.sums = P<float>(t[2].cast<uintptr_t>());
-    f.pool = t[3].cast<int>();
-    f.relu = t[4].cast<int>();
-    f.Hz = t[5].cast<int>();
-    f.Wz = t[6].cast<int>();
+    const ddp_amd::BnBwdFuse* fp = bn_fuse(bn, &f);
     ddp_amd::BnBwdApply ap{};
     const ddp_amd::BnBwdApply* app = bn_apply(bna, &ap);
     int done = 0;
     check(ddp_conv_dgrad_bn(&c, P<void>(dy), P<void>(wt), P<void>(dx), P<float>(ws), ws_elems,
-                            splits, &f, app, &done, S(st)), "conv_dgrad_bn");
+                            splits, fp, app, &done, S(st)), "conv_dgrad_bn");
     return done == 1;
   }, py::arg("g"), py::arg("dy"), py::arg("wt"), py::arg("dx"), py::arg("ws"),
      py::arg("ws_elems"), py::arg("splits"), py::arg("stream"), py::arg("accumulate") = 0,
-     py::arg("bn") = py::none(), py::arg("bna") = py::none(), py::arg("xf") = py::none());
+     py::arg("bn") = py::none(), py::arg("bna") = py::none());
   // one layer's backward: WGRAD (dw += ...) and stride-1 DGRAD (dx = ..., optional BN-backward
   // sums) as one grouped launch when the policy allows (ddp_conv_bwd_pair), else two
   m.def("conv_bwd_pair", [](py::tuple g, uintptr_t dy, uintptr_t wc, uintptr_t dx, uintptr_t x,
                             uintptr_t dw, uintptr_t ws, size_t ws_elems, uintptr_t st,
-                            py::object bn, py::object bna, py::object xf) {
-    ddp_amd::BnBwdXf xv{};
-    const ddp_amd::BnBwdXf* xp = xf_args(xf, &xv);
+                            py::object bn, py::object bna) {
     auto c = geom(g);
     ddp_amd::BnBwdApply ap{};
     const ddp_amd::BnBwdApply* app = bn_apply(bna, &ap);
     int done = 0;
     ddp_amd::BnBwdFuse f{};
-    const ddp_amd::BnBwdFuse* fp = nullptr;
-    if (!bn.is_none()) {
-      auto t = bn.cast<py::tuple>();
-      f.z = P<unsigned short>(t[0].cast<uintptr_t>());
-      f.coef = P<float>(t[1].cast<uintptr_t>());
-      f.sums = P<float>(t[2].cast<uintptr_t>());
-      f.pool = t[3].cast<int>();
-      f.relu = t[4].cast<int>();
-      f.Hz = t[5].cast<int>();
-      f.Wz = t[6].cast<int>();
-      fp = &f;
-    }
+    const ddp_amd::BnBwdFuse* fp = bn_fuse(bn, &f);
     check(ddp_conv_bwd_pair(&c, P<void>(dy), P<void>(wc), P<void>(dx), P<void>(x), P<float>(dw),
-                            P<float>(ws), ws_elems, fp, app, &done, S(st), xp), "conv_bwd_pair");
+                            P<float>(ws), ws_elems, fp, app, &done, S(st)), "conv_bwd_pair");
     return done == 1;
   }, py::arg("g"), py::arg("dy"), py::arg("wc"), py::arg("dx"), py::arg("x"), py::arg("dw"),
      py::arg("ws"), py::arg("ws_elems"), py::arg("stream"), py::arg("bn") = py::none(),
-     py::arg("bna") = py::none(), py::arg("xf") = py::none());
+     py::arg("bna") = py::none());
   // SGD in the backward (world 1): register a conv weight's gradient view with its update
   // (p, momentum buffer, bf16 copy, lr, momentum, wd, grad_scale, nesterov); dw = 0 with
   // clear = 1 switches it off. sgd_fuse_taken: gradient views whose WGRAD finish applied it
@@ -399,18 +326,16 @@ PYBIND11_MODULE(_native, m) {
         py::arg("splits_dg"), py::arg("splits_wg"));
   // final = 1: no DGRAD of this layer follows (its finish may apply a registered SGD step)
   m.def("conv_wgrad", [](py::tuple g, uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws,
-                         size_t ws_elems, int splits, uintptr_t st, py::object xf, int final_) {
+                         size_t ws_elems, int splits, uintptr_t st, int final_) {
     auto c = geom(g);
-    ddp_amd::BnBwdXf xv{};
-    const ddp_amd::BnBwdXf* xp = xf_args(xf, &xv);
     if (final_)
       check(ddp_conv_wgrad_final(&c, P<void>(dy), P<void>(x), P<float>(dw), P<float>(ws),
-                                 ws_elems, splits, xp, S(st)), "conv_wgrad");
+                                 ws_elems, splits, S(st)), "conv_wgrad");
     else
-      check(ddp_conv_wgrad_xf(&c, P<void>(dy), P<void>(x), P<float>(dw), P<float>(ws), ws_elems,
-                              splits, xp, S(st)), "conv_wgrad");
+      check(ddp_conv_wgrad(&c, P<void>(dy), P<void>(x), P<float>(dw), P<float>(ws), ws_elems,
+                           splits, S(st)), "conv_wgrad");
   }, py::arg("g"), py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("ws"), py::arg("ws_elems"),
-     py::arg("splits"), py::arg("stream"), py::arg("xf") = py::none(), py::arg("final") = 0);
+     py::arg("splits"), py::arg("stream"), py::arg("final") = 0);
 
   m.def("bn_act_fwd", [](int N, int H, int W, int C, int pool, int relu, float eps, uintptr_t z,
                          uintptr_t res, uintptr_t stats, uintptr_t gamma, uintptr_t beta,
@@ -467,22 +392,6 @@ PYBIND11_MODULE(_native, m) {
      py::arg("beta"), py::arg("dout"), py::arg("sums"), py::arg("dz"), py::arg("dres"),
      py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("stream"), py::arg("coef"),
      py::arg("sums_ready") = 0);
-  // BatchNorm backward without its apply pass: reduce (+ dy_bn stored to dyb) + finalize into
-  // xcoef; the conv backward then takes xf = (z, dyb, xcoef, C) (bn_act.hip ddp_bn_bwd_xf)
-  m.def("bn_bwd_xf_ok", [](int N, int H, int W, int C, int pool, int res, int sums_ready) {
-    return ddp_bn_bwd_xf_ok(N, H, W, C, pool, res, sums_ready) != 0;
-  });
-  m.def("bn_bwd_xf", [](int N, int H, int W, int C, int pool, int relu, float eps, uintptr_t z,
-                        uintptr_t res, uintptr_t dout, uintptr_t sums, uintptr_t dyb,
-                        uintptr_t xcoef, uintptr_t dgamma, uintptr_t dbeta, uintptr_t coef,
-                        uintptr_t st) {
-    ddp_amd::BnArgs a{};
-    a.N = N; a.H = H; a.W = W; a.C = C; a.pool = pool; a.relu = relu; a.eps = eps;
-    a.z = P<unsigned short>(z); a.res = P<unsigned short>(res); a.dout = P<unsigned short>(dout);
-    a.sums = P<float>(sums); a.dyb = P<unsigned short>(dyb); a.xcoef = P<float>(xcoef);
-    a.dgamma = P<float>(dgamma); a.dbeta = P<float>(dbeta); a.coef = P<float>(coef);
-    check(ddp_bn_bwd_xf(&a, S(st)), "bn_bwd_xf");
-  });
   // ResNet stem: BN + ReLU + MaxPool2d(3, 2, 1) in one pass each way (bn_act.hip bn_pool3_*):
   // (N, H, W) = conv output, out / dout pooled, idx = uint8 window argmax (pooled shape)
   m.def("bn_pool3_fwd", [](int N, int H, int W, int C, int relu, float eps, uintptr_t z,

@@ -46,10 +46,6 @@ struct BnArgs {
                                 // backward reads the table its forward wrote
   int sums_ready;               // backward: sums already accumulated (BnBwdFuse in the next
                                 // layer's dgrad) -> finalize + apply only
-  unsigned short* dyb;          // backward without apply (ddp_bn_bwd_xf): dy_bn, the routed /
-                                // masked gradient at the BN output (z's shape; = d residual)
-  float* xcoef;                 // ... and the [C/8][3|5][8] table of dz = A dy_bn + B z + C
-                                // (+ scale, shift when the consumer masks: dyb == nullptr)
 };
 
 // BatchNorm-backward statistics fused into a conv dgrad: the dgrad output IS the gradient at the
@@ -102,18 +98,6 @@ struct TrFwdIn {
   int relu, pool;
   float* coef;              // [6][C] coefficient table written for its backward
   unsigned short* y;        // materialised conv input [N][H][W][C] (the wgrad operand)
-};
-
-// BatchNorm-backward apply fused into the A-operand staging of the producing conv's backward
-// GEMMs (conv_igemm.hip XF): dz = A[c] * g + B[c] * z + C[c] is computed in LDS; dz never exists.
-struct BnBwdXf {
-  const void* z;        // the conv output the BatchNorm normalised [N][P][Q][C] (bf16)
-  const void* g;        // mask = 0: gradient at the BN output after ReLU mask / pool routing
-                        // (dy_bn); mask = 1 (no pool, no residual): the raw gradient at the
-                        // block output — the consumer applies the ReLU mask itself
-  const float* coef;    // [C/8][3 or 5][8]: A | B | C (| scale | shift) of 8 channels
-  int C;
-  int mask;
 };
 
 // SGD in the backward (conv_igemm.hip wgrad_finish_krsc_body): the optimizer step of one conv
@@ -197,16 +181,8 @@ int ddp_conv_fwd_tr(const ddp_amd::ConvGeom* g, const void* x, const void* wc, c
                     const ddp_amd::BnFwdFuse* bn, int* bn_done, const ddp_amd::TrFwdIn* in,
                     hipStream_t st);
 int ddp_conv_tr_would_serve(const ddp_amd::ConvGeom* g, size_t ws_elems, int in_mode);
-// backward-data of a 3x3/s1/p1 conv through the tap-reuse kernel (wt = bf16 [C][3][3][K]);
-// g = the forward geometry; 1 served, 0 not served, >= 2 HIP error (rc - 2)
-int ddp_conv_dgrad_tr(const ddp_amd::ConvGeom* g, const void* dz, const void* wt, void* dx,
-                      float* ws, size_t ws_elems, hipStream_t st);
-// the same with the weights read k-major from the FORWARD copy wc = bf16 [K][3][3][C] (no
-// transposed copy) and, with xf, dz computed from (z, g, coef) while the patch loads
-int ddp_conv_dgrad_tr_wc(const ddp_amd::ConvGeom* g, const void* dz, const void* wc, void* dx,
-                         float* ws, size_t ws_elems, const ddp_amd::BnBwdXf* xf, hipStream_t st);
 // tap-reuse policy: mode -1 clear table, 0/1 disable/enable (table entries), 4 enable with the
-// heuristic for untabled shapes, 2 forward / 5 backward-data table entry (M, K, C, H) ->
+// heuristic for untabled shapes, 2 table entry (M, K, C, H) ->
 // (bm, bn, splits, stages) (bm = 0: use the implicit-GEMM kernel), 3 force the same (sweeps)
 void ddp_conv_tr_set(int mode, int M, int K, int C, int H, int bm, int bn, int splits, int stages);
 int ddp_conv_tr_geometry(int BM, int N, int H, int W, int* out7);
@@ -224,19 +200,10 @@ int ddp_conv_dgrad(const ddp_amd::ConvGeom* g, const void* dy, const void* wt, v
 int ddp_conv_dgrad_bn(const ddp_amd::ConvGeom* g, const void* dy, const void* wt, void* dx,
                       float* ws, size_t ws_elems, int splits, const ddp_amd::BnBwdFuse* bn,
                       const ddp_amd::BnBwdApply* ba, int* bn_done, hipStream_t st);
-int ddp_conv_xf_ok(const ddp_amd::ConvGeom* g, int need_dx);
-int ddp_conv_dgrad_xf(const ddp_amd::ConvGeom* g, const void* wc, void* dx, float* ws,
-                      size_t ws_elems, const ddp_amd::BnBwdFuse* bn, const ddp_amd::BnBwdApply* ba,
-                      int* bn_done, const ddp_amd::BnBwdXf* xf, hipStream_t st);
-int ddp_conv_wgrad_xf(const ddp_amd::ConvGeom* g, const void* dy, const void* x, float* dw,
-                      float* ws, size_t ws_elems, int splits, const ddp_amd::BnBwdXf* xf,
-                      hipStream_t st);
 int ddp_conv_wgrad(const ddp_amd::ConvGeom* g, const void* dy, const void* x, float* dw,
                    float* ws, size_t ws_elems, int splits, hipStream_t st);
 int ddp_bn_act_fwd(const ddp_amd::BnArgs* a, hipStream_t st);
 int ddp_bn_act_bwd(const ddp_amd::BnArgs* a, hipStream_t st);
-int ddp_bn_bwd_xf_ok(int N, int H, int W, int C, int pool, int res, int sums_ready);
-int ddp_bn_bwd_xf(const ddp_amd::BnArgs* a, hipStream_t st);
 // small layers: the whole BatchNorm backward in one launch, one block per 8 channels
 // (bn_act_bwd_local_kernel); ok = this layer takes that path; set = its loads-per-thread
 // limit (0 = off)
@@ -266,15 +233,14 @@ int ddp_l0_ok(const ddp_amd::ConvGeom* g);
 int ddp_l0_fwd(const ddp_amd::ConvGeom* g, const ddp_amd::L0Io* io, hipStream_t st);
 int ddp_l0_bwd(const ddp_amd::ConvGeom* g, const ddp_amd::L0Io* io, hipStream_t st);
 int ddp_conv_wgrad_final(const ddp_amd::ConvGeom* g, const void* dy, const void* x, float* dw,
-                         float* ws, size_t ws_elems, int splits, const ddp_amd::BnBwdXf* xf,
-                         hipStream_t st);
+                         float* ws, size_t ws_elems, int splits, hipStream_t st);
 int ddp_sgd_fuse_taken(uintptr_t* out, int cap);
 // sweeps (tools/conv_tune.py --pairs): force the paired launch with these split-K factors (0 = off)
 void ddp_conv_pair_force(int splits_dg, int splits_wg);
 int ddp_conv_bwd_pair(const ddp_amd::ConvGeom* g, const void* dy, const void* wc, void* dx,
                       const void* x, float* dw, float* ws, size_t ws_elems,
                       const ddp_amd::BnBwdFuse* bn, const ddp_amd::BnBwdApply* ba, int* bn_done,
-                      hipStream_t st, const ddp_amd::BnBwdXf* xf);
+                      hipStream_t st);
 void ddp_conv_tune_set(int mode, int M, int N, int K, int tile, int splits, int stages);
 void ddp_conv_tune_clear();
 void ddp_conv_force_tile(int tile_plus_one, int stages);

@@ -20,11 +20,6 @@
 // (blocks x channels x replicas below kFoldBytes) the finalize step is FOLDED into the apply
 // kernel instead: every block reduces the replicas it needs into LDS, saving a launch (each
 // dispatch costs ~4-5 us of the captured step).
-// Backward without an apply pass (ddp_bn_bwd_xf): the reduce kernel also stores dy_bn (the
-// routed, masked gradient at the BN output — also the residual branch's gradient), and the
-// finalize writes dz = A * dy_bn + B * z + C per channel (A = scale, B = -scale * invstd * k2,
-// C = scale * (invstd * k2 * mean - k1)) for the conv backward GEMMs, which compute dz while
-// staging their A operand (conv_igemm.hip XF): dz is never written or re-read.
 // Every apply/reduce thread owns 8 contiguous channels (one 16-byte vector) of an output pixel
 // and reads its coefficients straight from the (L2-resident) table: no LDS, no barrier before
 // the streaming loads.
@@ -320,12 +315,6 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
         acc[0][e] += dyb[d][e];
         acc[1][e] += dyb[d][e] * xh[d][e];
       }
-      if (a.dyb) {  // (ddp_bn_bwd_xf) dy_bn for the consumer GEMMs' A-operand transform
-        u16x8 o;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = f2bf(dyb[d][e]);  // exact: a routed / masked bf16 value
-        st8(a.dyb + L.off[it][d], o);
-      }
     }
   }
   // block reduction over the 256/Gb threads sharing each channel group, then one atomic per
@@ -345,39 +334,6 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
       atomicAdd(rep + k * a.C + (cg_base + g) * 8 + e, s);
     }
   }
-}
-
-// (ddp_bn_bwd_xf) k1 / k2 -> the per-channel affine form of the BN-backward apply, for the conv
-// backward GEMMs' A-operand transform: xcoef[c / 8][rows][8] = A | B | C (| scale | shift) with
-// dz = A * dy_bn + B * z + C (the apply kernel's scale * (dy_bn - k1 - xhat * k2) expanded);
-// rows = 5 when the consumer applies the ReLU mask itself (a.dyb == nullptr with ReLU, no pool,
-// no residual: dy_bn = [scale * z + shift > 0] * dout needs nothing stored). dgamma += S2,
-// dbeta += S1 as in bn_finalize_bwd_kernel.
-__global__ __launch_bounds__(256) void bn_finalize_bwd_xf_kernel(BnArgs a) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= a.C) return;
-  const float inv_m = 1.f / ((float)a.N * a.H * a.W);
-  float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-  for (int r = 0; r < kStatRep; ++r) {
-    s1 += a.sums[r * 2 * a.C + c];
-    s2 += a.sums[r * 2 * a.C + a.C + c];
-  }
-  const float k1 = s1 * inv_m, k2 = s2 * inv_m;
-  const float sc = a.coef[kSc * a.C + c], mu = a.coef[kMu * a.C + c], is = a.coef[kIs * a.C + c];
-  a.coef[kK1 * a.C + c] = k1;
-  a.coef[kK2 * a.C + c] = k2;
-  const bool mask = a.dyb == nullptr && a.relu;  // (no ReLU: dy_bn = dout, nothing to mask)
-  float* x = a.xcoef + (c >> 3) * (mask ? 40 : 24) + (c & 7);
-  x[0] = sc;
-  x[8] = -sc * is * k2;
-  x[16] = sc * (is * k2 * mu - k1);
-  if (mask) {
-    x[24] = sc;
-    x[32] = a.coef[kSh * a.C + c];
-  }
-  if (a.dgamma) a.dgamma[c] += s2;
-  if (a.dbeta) a.dbeta[c] += s1;
 }
 
 template <bool POOL, int IPT>
@@ -740,7 +696,7 @@ extern "C" int ddp_bn_act_fwd(const BnArgs* args, hipStream_t st) {
 // Target reduce-grid size (DDP_AMD_BN_BWD_BLOCKS overrides).
 static size_t kBwdBlocks = 1024;
 
-template <bool POOL, int IPT, bool APPLY>
+template <bool POOL, int IPT>
 static void launch_bwd(const BnArgs& a, size_t npix, int Gb, int chunks, hipStream_t st) {
   const unsigned bx = blocks_for(npix, (size_t)(256 / Gb) * IPT);
   if (!a.sums_ready)  // (else: accumulated by the next layer's dgrad epilogue, BnBwdFuse)
@@ -749,12 +705,8 @@ static void launch_bwd(const BnArgs& a, size_t npix, int Gb, int chunks, hipStre
   // replicas the reduce just wrote with memory-side atomics) measured 3-4x slower applies at
   // batch 256 and +50 us per b32 step; the reduce's last-arriving block doing it measured slower
   // than the launch boundary too (profiles/r2_launch_reduction_ab.md, r3_bn_bwd_one_launch.md).
-  if (APPLY) {
-    hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3(blocks_for(a.C, 256)), dim3(256), 0, st, a);
-    hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT>), dim3(bx, chunks), dim3(256), 0, st, a);
-  } else {
-    hipLaunchKernelGGL(bn_finalize_bwd_xf_kernel, dim3(blocks_for(a.C, 256)), dim3(256), 0, st, a);
-  }
+  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3(blocks_for(a.C, 256)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT>), dim3(bx, chunks), dim3(256), 0, st, a);
 }
 
 // One-block-per-channel-group backward (bn_act_bwd_local_kernel): items per thread for npix
@@ -812,8 +764,7 @@ extern "C" int ddp_bn_bwd_local_ok(int N, int H, int W, int C, int pool) {
   return local_cfg(a, &ipt) ? 1 : 0;
 }
 
-// reduce(+finalize, +apply) grid shape shared by ddp_bn_act_bwd and ddp_bn_bwd_xf
-template <bool APPLY>
+// reduce + finalize + apply
 static int launch_reduce_chain(const BnArgs& a, hipStream_t st) {
   static const bool init = [] {
     if (const char* e = std::getenv("DDP_AMD_BN_BWD_BLOCKS")) kBwdBlocks = std::max(1, std::atoi(e));
@@ -837,13 +788,13 @@ static int launch_reduce_chain(const BnArgs& a, hipStream_t st) {
   if (blocks1 > 2 * kBwdBlocks)
     while (ipt < 4 && blocks1 / ipt > kBwdBlocks) ipt *= 2;
   if (a.pool) {
-    if (ipt >= 4) launch_bwd<true, 4, APPLY>(a, npix, Gb, chunks, st);
-    else if (ipt == 2) launch_bwd<true, 2, APPLY>(a, npix, Gb, chunks, st);
-    else launch_bwd<true, 1, APPLY>(a, npix, Gb, chunks, st);
+    if (ipt >= 4) launch_bwd<true, 4>(a, npix, Gb, chunks, st);
+    else if (ipt == 2) launch_bwd<true, 2>(a, npix, Gb, chunks, st);
+    else launch_bwd<true, 1>(a, npix, Gb, chunks, st);
   } else {
-    if (ipt >= 4) launch_bwd<false, 4, APPLY>(a, npix, Gb, chunks, st);
-    else if (ipt == 2) launch_bwd<false, 2, APPLY>(a, npix, Gb, chunks, st);
-    else launch_bwd<false, 1, APPLY>(a, npix, Gb, chunks, st);
+    if (ipt >= 4) launch_bwd<false, 4>(a, npix, Gb, chunks, st);
+    else if (ipt == 2) launch_bwd<false, 2>(a, npix, Gb, chunks, st);
+    else launch_bwd<false, 1>(a, npix, Gb, chunks, st);
   }
   return (int)hipGetLastError();
 }
@@ -852,7 +803,6 @@ static int launch_reduce_chain(const BnArgs& a, hipStream_t st) {
 // zero on entry (per-step scratch, zeroed once per forward).
 extern "C" int ddp_bn_act_bwd(const BnArgs* args, hipStream_t st) {
   BnArgs a = *args;
-  a.dyb = nullptr;
   if (a.C % 8 || a.coef == nullptr || a.sums == nullptr) return -1;
   if (a.pool && a.res) return -1;
   int ipt;
@@ -863,36 +813,8 @@ extern "C" int ddp_bn_act_bwd(const BnArgs* args, hipStream_t st) {
     else launch_local<false>(a, ipt, st);
     return (int)hipGetLastError();
   }
-  return launch_reduce_chain<true>(a, st);
+  return launch_reduce_chain(a, st);
 }
-
-// Is the apply-free backward (ddp_bn_bwd_xf) the one to run for this layer? Not for layers the
-// one-launch local kernel serves (one launch beats reduce + finalize), nor when the sums came
-// from the next layer's dgrad epilogue (sums_ready: no reduce pass to store dy_bn in).
-extern "C" int ddp_bn_bwd_xf_ok(int N, int H, int W, int C, int pool, int res, int sums_ready) {
-  BnArgs a{};
-  a.N = N; a.H = H; a.W = W; a.C = C; a.pool = pool;
-  a.res = res ? reinterpret_cast<const unsigned short*>(16) : nullptr;
-  int ipt;
-  if (C % 8 || (pool && res) || sums_ready || local_cfg(a, &ipt)) return 0;
-  const int G = C / 8, Gb = G < 256 ? G : 256;
-  return ((Gb < 256 && 256 % Gb) || (G > 256 && G % 256)) ? 0 : 1;
-}
-
-// BatchNorm backward WITHOUT the apply pass: reduce (S1 / S2, and dy_bn stored to a.dyb) +
-// finalize into a.xcoef ([C/8][3][8] = A | B | C of dz = A * dy_bn + B * z + C) and dgamma /
-// dbeta. The conv backward GEMMs then take (z, dy_bn, xcoef) as their A operand (BnBwdXf).
-// a.dyb doubles as the residual-branch gradient. Without pool and residual a.dyb may be null:
-// the table then carries scale / shift too and the GEMMs mask the raw dout themselves
-// (BnBwdXf::mask). Requires ddp_bn_bwd_xf_ok.
-extern "C" int ddp_bn_bwd_xf(const BnArgs* args, hipStream_t st) {
-  BnArgs a = *args;
-  if (a.C % 8 || a.coef == nullptr || a.sums == nullptr || a.xcoef == nullptr ||
-      a.sums_ready || (a.pool && a.res) || (a.dyb == nullptr && (a.pool || a.res)))
-    return -1;
-  return launch_reduce_chain<false>(a, st);
-}
-
 
 // ResNet stem BN + ReLU + MaxPool2d(3, 2, 1) (bn_pool3_*): a.H x a.W = conv output, a.out /
 // a.dout = pooled [N][Ho][Wo][C], idx = the forward's window argmax bytes (pooled shape).

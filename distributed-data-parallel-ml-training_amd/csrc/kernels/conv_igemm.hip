@@ -109,25 +109,7 @@ struct ConvArgs {
   // stores of whole tile rows instead of 8-B fragments of 16 rows per instruction
   int epi_stage;
   int nmajor;                // tile order (common.h tile_order_n): 1 = row tiles fastest
-  // DGRAD / WGRAD A-operand transform (XF instantiations): the A operand is the gradient at a
-  // training-mode BatchNorm's input, dz = xA[c] * g + xB[c] * z + xC[c], computed while the tile
-  // sits in LDS — its BN-backward "apply" pass never runs and dz is never stored. ``a`` = z
-  // (the conv output the BN normalised), ``xg`` = g (the gradient at the BN output after the
-  // ReLU mask and pool routing: bn_act.hip reduce kernel's dyb, same [pixel][channel] layout),
-  // ``xcoef`` = [xc / 8][rows][8] fp32 (xA | xB | xC [| scale | shift] of 8 channels).
-  // xmask: g is the RAW gradient at the BN output of a block without pool / residual, and the
-  // ReLU mask is applied here (scale * z + shift > 0; rows = 5) — the BN reduce then stores
-  // nothing; otherwise g = dy_bn, already routed and masked (rows = 3).
-  const unsigned short* xg;
-  const float* xcoef;
-  int xc;
-  int xmask;
 };
-
-// LDS elements (u16) of the XF coefficient table in front of the operand ring (64-aligned)
-__host__ __device__ inline int xf_table_elems(int xc, int xmask) {
-  return (xc * (xmask ? 10 : 6) + 63) / 64 * 64;
-}
 
 // ------------------------------------------------------------------ operand gathers
 // Index math is hoisted: the pixel decomposition of a GEMM row is computed once per kernel
@@ -243,13 +225,10 @@ struct ConvSmem {
 // The GEMM body. ``bid`` / ``nblk`` stand for blockIdx.x / gridDim.x, so a grouped launch
 // (conv_bwd_pair_kernel: the DGRAD and WGRAD GEMMs of one layer in ONE launch) can hand each
 // problem its own block range. ``smem`` = the launching kernel's single LDS array.
-template <int MODE, int BM, int BN, int NST, int BNF = 0, int XF = 0>
-__device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned short* smem_base,
+template <int MODE, int BM, int BN, int NST, int BNF = 0>
+__device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned short* smem,
                                                 const int bid, const int nblk) {
   constexpr int BK = 64;
-  static_assert(!XF || (MODE != MODE_FWD && BM <= 128 && BN <= 128), "XF: DGRAD/WGRAD, BM <= 128");
-  // XF: the coefficient table occupies the front of the LDS array, the ring follows
-  unsigned short* const smem = smem_base + (XF ? xf_table_elems(args.xc, args.xmask) : 0);
   constexpr int WTM = BM / 2, WTN = BN / 2;
   // BNF: 0 none, 1 = the preceding block is pooled (generic epilogue, window-argmax routing),
   // 2 = no pool (lean epilogue, same row offsets as the output). The generic epilogue also
@@ -259,8 +238,7 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
   constexpr int CA = BM * BK / 8 / 256;  // 16-B chunks per thread per tile
   constexpr int CB = BN * BK / 8 / 256;
   constexpr int TILE_A = BM * BK, TILE_B = BN * BK;
-  constexpr int TILE_G = XF ? TILE_A : 0;        // XF: the g operand, staged beside z
-  constexpr int STAGE = TILE_A + TILE_B + TILE_G;
+  constexpr int STAGE = TILE_A + TILE_B;
   static_assert(CA >= 1 && CB >= 1, "tile too small for 256 threads");
   static_assert(NST >= 2 && NST <= 4, "2..4 LDS stages");
 
@@ -314,8 +292,6 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
   const int lcB = !BKM ? lcA : ((tid % (BN / 8)) ^ mc_swz<BN>(tid / (BN / 8)));
   const __amdgpu_buffer_rsrc_t rsA = make_rsrc(args.a, args.a_bytes);
   const __amdgpu_buffer_rsrc_t rsB = make_rsrc(args.b, args.b_bytes);
-  // XF: g has z's layout and size (a_bytes)
-  const __amdgpu_buffer_rsrc_t rsG = make_rsrc(XF ? args.xg : args.a, args.a_bytes);
 
   auto setup = [&](int item) {
     zsplit = item / tiles;
@@ -381,7 +357,6 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
   auto issue = [&](int ks, int buf) {
     unsigned short* As = smem + buf * STAGE;
     unsigned short* Bs = As + TILE_A;
-    unsigned short* Gs = Bs + TILE_B;
     const int k0 = ks * BK;
     if (MODE != MODE_WGRAD) {
       const int W_ = MODE == MODE_FWD ? gg.W : gg.Q;
@@ -396,7 +371,6 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
           else
             ok = (unsigned)(a_h0[i] - kr) < (unsigned)gg.P && (unsigned)(a_w0[i] - ks_) < (unsigned)gg.Q;
           dma_buf(rsA, ok ? a_off[i] + tap : (int)kOOB, As + (wid * 64 + 256 * i) * 8);
-          if (XF) dma_buf(rsG, ok ? a_off[i] + tap : (int)kOOB, Gs + (wid * 64 + 256 * i) * 8);
         }
         int boff;
         if (MODE == MODE_FWD) {
@@ -454,10 +428,8 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
       constexpr int NCB = BN / 8;
       const int ka = 2 * k0 * gg.K;
 #pragma unroll
-      for (int i = 0; i < CA; ++i) {  // dy[m][kout]; m >= Kg lands past the buffer -> zeros
+      for (int i = 0; i < CA; ++i)  // dy[m][kout]; m >= Kg lands past the buffer -> zeros
         dma_buf(rsA, a_off[i] + ka, As + (wid * 64 + 256 * i) * 8);
-        if (XF) dma_buf(rsG, a_off[i] + ka, Gs + (wid * 64 + 256 * i) * 8);
-      }
       // "same" convolution (stride 1, P == H, Q == W): the input pixel of output pixel m at tap
       // (r, s) is m + (r - pad) * W + (s - pad), so the offset is linear in m; only the border
       // test needs (p, q)
@@ -549,76 +521,6 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
           // operands swapped (D^T = B^T A^T): each lane ends up owning ONE output row and FOUR
           // consecutive output columns, so the epilogue stores 8 B (bf16) / 16 B (fp32) per lane
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
-    }
-  };
-
-  // ---------------- XF: BatchNorm-backward apply on the staged A operand ----------------
-  // Each thread rewrites exactly the A chunks its own DMAs filled (z at As, g at Gs, same slot):
-  // dz = xA * g + xB * z + xC for its 8 channels, zero for a padding / out-of-range chunk (its
-  // DMAs read zeros, but dz there is 0, not xC). Called once the stage's DMAs are retired by
-  // vmcnt + a barrier; a barrier after it publishes the rewritten chunks to the other waves.
-  // The coefficient table sits in front of the ring (loaded once per block).
-  auto xform = [&](int ks, int buf) {
-    unsigned short* As = smem + buf * STAGE;
-    const unsigned short* Gs = As + TILE_A + TILE_B;
-    const float* xct = reinterpret_cast<const float*>(smem_base);
-    int c0;
-    bool ok[CA];
-    if (MODE == MODE_DGRAD) {  // fast path only (host: K % 64 == 0, stride 1): uniform tap
-      const int k0 = ks * BK;
-      const int rs = k0 / gg.K;
-      const int kr_ = rs / gg.S, ks2 = rs - kr_ * gg.S;
-      c0 = k0 - rs * gg.K + lcA * 8;
-#pragma unroll
-      for (int i = 0; i < CA; ++i)
-        ok[i] = (unsigned)(a_h0[i] - kr_) < (unsigned)gg.P && (unsigned)(a_w0[i] - ks2) < (unsigned)gg.Q;
-    } else {  // WGRAD: rows = pixels ks*64 + m, columns = output channels (BM <= 128: one kout)
-      constexpr int NCA = BM / 8;
-      c0 = row0 + lcA * 8;
-#pragma unroll
-      for (int i = 0; i < CA; ++i)
-        ok[i] = c0 < args.Mg && ks * BK + (tid + i * 256) / NCA < args.Kg;
-    }
-    const bool xm = args.xmask;  // uniform
-    const float* cp = xct + (c0 >> 3) * (xm ? 40 : 24);
-    float xa[8], xb[8], xc8[8], xs[8], xh[8];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const f32x4 a = *reinterpret_cast<const f32x4*>(cp + 4 * h);
-      const f32x4 b = *reinterpret_cast<const f32x4*>(cp + 8 + 4 * h);
-      const f32x4 d = *reinterpret_cast<const f32x4*>(cp + 16 + 4 * h);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) { xa[4 * h + e] = a[e]; xb[4 * h + e] = b[e]; xc8[4 * h + e] = d[e]; }
-    }
-    if (xm) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const f32x4 a = *reinterpret_cast<const f32x4*>(cp + 24 + 4 * h);
-        const f32x4 b = *reinterpret_cast<const f32x4*>(cp + 32 + 4 * h);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { xs[4 * h + e] = a[e]; xh[4 * h + e] = b[e]; }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < CA; ++i) {
-      unsigned short* slot = As + (tid + 256 * i) * 8;
-      u16x8 o;
-      if (ok[i]) {
-        const u16x8 zv = *reinterpret_cast<const u16x8*>(slot);
-        const u16x8 gv = *reinterpret_cast<const u16x8*>(Gs + (tid + 256 * i) * 8);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float zf = bf2f(zv[e]);
-          float gf = bf2f(gv[e]);
-          // (the forward's ReLU input: bf16 z times the same fp32 scale / shift, bn_act.hip)
-          if (xm && !(zf * xs[e] + xh[e] > 0.f)) gf = 0.f;
-          o[e] = f2bf(fmaf(xa[e], gf, fmaf(xb[e], zf, xc8[e])));
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = 0;
-      }
-      *reinterpret_cast<u16x8*>(slot) = o;
     }
   };
 
@@ -1013,12 +915,7 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
   };
 
   // NST-stage LDS ring: the DMAs of up to NST-1 k-steps are in flight while one is computed.
-  constexpr int DMA = CA + CB + (XF ? CA : 0);  // vector-memory instructions per thread per stage
-  if (XF) {  // the block's coefficient table (before any DMA is in flight)
-    float* xct = reinterpret_cast<float*>(smem_base);
-    for (int i = tid; i < args.xc * (args.xmask ? 5 : 3); i += 256) xct[i] = args.xcoef[i];
-    __syncthreads();
-  }
+  constexpr int DMA = CA + CB;  // vector-memory instructions per thread per stage
   for (int item = bid; item < nitems; item += nblk) {
     setup(item);
 #pragma unroll
@@ -1029,36 +926,17 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
 #pragma unroll
     for (int s = 0; s < NST - 1; ++s)
       if (kb + s < ke) issue(kb + s, s);
-    if (XF) {  // stage kb: retire its DMAs (all but the ones issued after it), barrier, rewrite
-      const int after = min(NST - 2, ke - 1 - kb);
-      if (NST >= 4 && after >= 2) wait_dma_barrier<(NST >= 4 ? 2 : 0) * DMA>();
-      else if (NST >= 3 && after >= 1) wait_dma_barrier<(NST >= 3 ? 1 : 0) * DMA>();
-      else wait_dma_barrier<0>();
-      xform(kb, 0);
-    }
     int stage = 0;
     for (int ks = kb; ks < ke; ++ks) {
       // stages issued after ks and still allowed in flight: min(NST-2, ke-1-ks)
       const int ahead = ke - 1 - ks;
-      if (XF) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the xform's LDS writes
       if (NST >= 4 && ahead >= 2) wait_dma_barrier<(NST >= 4 ? 2 : 0) * DMA>();
       else if (NST >= 3 && ahead >= 1) wait_dma_barrier<(NST >= 3 ? 1 : 0) * DMA>();
       else wait_dma_barrier<0>();
       // every wave finished computing ks-1: its buffer takes k-step ks+NST-1
       if (ks + NST - 1 < ke) issue(ks + NST - 1, stage == 0 ? NST - 1 : stage - 1);
       compute(stage);
-      const int next = stage + 1 == NST ? 0 : stage + 1;
-      if (XF && ks + 1 < ke) {
-        // k-step ks+1: its DMAs were issued before the ones of ks+2.. (at most NST-2 stages,
-        // min(NST-2, ke-ks-2) of them real); retire it, barrier (LDS-DMA data is visible to a
-        // ds_read only after the issuing wave's vmcnt AND a barrier), rewrite the A chunks
-        const int after = ke - 2 - ks;
-        if (NST >= 4 && after >= 2) wait_dma_barrier<(NST >= 4 ? 2 : 0) * DMA>();
-        else if (NST >= 3 && after >= 1) wait_dma_barrier<(NST >= 3 ? 1 : 0) * DMA>();
-        else wait_dma_barrier<0>();
-        xform(ks + 1, next);
-      }
-      stage = next;
+      stage = stage + 1 == NST ? 0 : stage + 1;
     }
     epilogue(row0, col0, zsplit, args.splits > 1);
     // all reads of the ring done before the next item's prologue DMA. Not after the last item:
@@ -1074,21 +952,21 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
 #ifndef DDP_CONV_WAVES_PER_EU
 #define DDP_CONV_WAVES_PER_EU 2
 #endif
-template <int MODE, int BM, int BN, int NST, int BNF = 0, int XF = 0>
+template <int MODE, int BM, int BN, int NST, int BNF = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DDP_CONV_WAVES_PER_EU)))
 void conv_igemm_kernel(ConvArgs args) {
   // dynamic: the launcher sizes the ring to the stages a work item can use (launch_gemm_t)
   extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
-  conv_igemm_body<MODE, BM, BN, NST, BNF, XF>(args, smem, blockIdx.x, gridDim.x);
+  conv_igemm_body<MODE, BM, BN, NST, BNF>(args, smem, blockIdx.x, gridDim.x);
 }
 
 // BNF 2 (no-pool BN-backward sums in the lean epilogue): the extra per-column coefficients push
 // the big tiles past 256 registers (1 wave per SIMD); ask the register allocator for 2 waves.
-template <int MODE, int BM, int BN, int NST, int XF = 0>
+template <int MODE, int BM, int BN, int NST>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 void conv_igemm_bnf2_kernel(ConvArgs args) {
   extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
-  conv_igemm_body<MODE, BM, BN, NST, 2, XF>(args, smem, blockIdx.x, gridDim.x);
+  conv_igemm_body<MODE, BM, BN, NST, 2>(args, smem, blockIdx.x, gridDim.x);
 }
 
 // One layer's backward GEMMs in ONE launch: blocks [0, n_dg) run the DGRAD problem, the rest
@@ -1103,17 +981,6 @@ __global__ __launch_bounds__(256) void conv_bwd_pair_kernel(ConvArgs dg, ConvArg
   else
     conv_igemm_body<MODE_WGRAD, BM, BN, NST, 0>(wg, smem, blockIdx.x - n_dg, gridDim.x - n_dg);
 }
-// The same with the BatchNorm-backward apply on both halves' A operand (XF): both GEMMs read dz
-// of this layer's BN backward, computed in LDS from z and g (dynamic LDS: table + XF ring)
-template <int BM, int BN, int NST, int BNF>
-__global__ __launch_bounds__(256) void conv_bwd_pair_xf_kernel(ConvArgs dg, ConvArgs wg, int n_dg) {
-  extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
-  if ((int)blockIdx.x < n_dg)
-    conv_igemm_body<MODE_DGRAD, BM, BN, NST, BNF, 1>(dg, smem, blockIdx.x, n_dg);
-  else
-    conv_igemm_body<MODE_WGRAD, BM, BN, NST, 0, 1>(wg, smem, blockIdx.x - n_dg, gridDim.x - n_dg);
-}
-
 // Split-K finish for FWD/DGRAD: sum the slabs in split order -> (+bias) bf16 output
 // (+ per-channel stats of the rounded output for FWD).
 // Thread layout: cg_local = tid % Gb (8 channels each), rows strided; stats reduced in
@@ -1896,9 +1763,9 @@ static int stages_for(int BM, int BN) {
   return 3;
 }
 
-template <int MODE, int BM, int BN, int NST, int BNF, int XF = 0>
+template <int MODE, int BM, int BN, int NST, int BNF>
 static void launch_gemm_t(const ConvArgs& a, int items, hipStream_t st) {
-  constexpr int kStageBytes = (BM + BN + (XF ? BM : 0)) * 64 * 2;
+  constexpr int kStageBytes = (BM + BN) * 64 * 2;
   // A work item of k k-steps touches min(NST, k) ring stages (the prologue issues k-steps
   // 0..NST-2, the loop refills the stage freed by the previous k-step only while k-steps
   // remain). Short reductions — the 1x1 convs over 64/128 channels, 1-2 k-steps — thus need a
@@ -1910,16 +1777,15 @@ static void launch_gemm_t(const ConvArgs& a, int items, hipStream_t st) {
   const int stages = std::max(1, std::min(NST, a.ksteps_per_split));
   size_t lds = (size_t)stages * kStageBytes;
   if (a.epi_stage && lds < (size_t)kTileBytes) lds = kTileBytes;
-  if (XF) lds += 2 * (size_t)xf_table_elems(a.xc, a.xmask);  // coefficient table, then the ring
   void (*kern)(ConvArgs);
-  if constexpr (BNF == 2 && MODE == MODE_DGRAD) kern = conv_igemm_bnf2_kernel<MODE, BM, BN, NST, XF>;
-  else kern = conv_igemm_kernel<MODE, BM, BN, NST, BNF, XF>;
+  if constexpr (BNF == 2 && MODE == MODE_DGRAD) kern = conv_igemm_bnf2_kernel<MODE, BM, BN, NST>;
+  else kern = conv_igemm_kernel<MODE, BM, BN, NST, BNF>;
   static bool attr = false;
   if (!attr) {
     // an error here surfaces through the caller's hipGetLastError
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                              XF ? 160 * 1024 : std::max(NST * kStageBytes, kTileBytes));
+                              std::max(NST * kStageBytes, kTileBytes));
     attr = true;
   }
   // persistent grid: at most the resident workgroup slots (queried once per instantiation)
@@ -1937,16 +1803,6 @@ static void launch_gemm_t(const ConvArgs& a, int items, hipStream_t st) {
 
 template <int MODE, int BM, int BN, int NST>
 static void launch_gemm(const ConvArgs& a, int items, hipStream_t st) {
-  if constexpr (MODE != MODE_FWD && BM <= 128 && BN <= 128 && NST <= 3) {
-    if (a.xg) {  // BatchNorm-backward apply on the A operand (xf_ok / launch_cfg checked it)
-      if constexpr (MODE == MODE_DGRAD) {
-        if (a.has_bnf && a.splits <= 1)
-          return a.bnf.pool ? launch_gemm_t<MODE, BM, BN, NST, 1, 1>(a, items, st)
-                            : launch_gemm_t<MODE, BM, BN, NST, 2, 1>(a, items, st);
-      }
-      return launch_gemm_t<MODE, BM, BN, NST, 0, 1>(a, items, st);
-    }
-  }
   if constexpr (MODE == MODE_DGRAD) {
     // the BN-backward sums are reduced in the non-split epilogue: a single split only (split
     // GEMMs reduce them in the finish kernel)
@@ -2181,7 +2037,6 @@ static void launch_cfg(ConvArgs& a, int splits, hipStream_t st, int nst_req = 0)
   constexpr int kMaxStages = kStageBytes * 4 <= 163840 ? 4 : (kStageBytes * 3 <= 163840 ? 3 : 2);
   int nst = nst_req >= 2 && nst_req <= 4 ? nst_req : stages_for(BM, BN);
   nst = std::min(nst, kMaxStages);
-  if (a.xg) nst = std::min(nst, (BM == 128 && BN == 128) ? 2 : 3);  // XF: g doubles the A bytes
   if constexpr (kMaxStages >= 4) {
     if (nst == 4) { launch_gemm<MODE, BM, BN, 4>(a, items, st); goto launched; }
   }
@@ -2259,11 +2114,6 @@ static void plan_mode(ConvArgs& a, size_t ws_elems, int* best_out, int* sp, int*
       sp[best] = spl;
       nst = it->second.stages;
     }
-  }
-  if (a.xg && best > 3) {  // XF kernels exist for the 128/64 tiles only
-    best = 0;
-    for (int i = 1; i < 4; ++i)
-      if (c[i] < c[best]) best = i;
   }
   *best_out = best;
   *nst_out = nst;
@@ -2439,29 +2289,13 @@ extern "C" int ddp_conv_fwd_finish(const ConvGeom* g, float* ws, int splits, con
   return (int)hipGetLastError();
 }
 
-// XF (BatchNorm-backward apply on the A operand) is available for: WGRAD always; DGRAD of a
-// stride-1 conv with K % 64 == 0 (the uniform-tap fast path), not accumulating into dx
-static bool xf_dgrad_ok(const ConvGeom* g) { return g->stride == 1 && g->K % 64 == 0; }
-static void set_xf(ConvArgs& a, const BnBwdXf* xf) {
-  if (!xf) return;
-  a.a = (const unsigned short*)xf->z;
-  a.xg = (const unsigned short*)xf->g;
-  a.xcoef = xf->coef;
-  a.xc = xf->C;
-  a.xmask = xf->mask;
-}
-extern "C" int ddp_conv_xf_ok(const ConvGeom* g, int need_dx) {
-  return (g->K % 8 == 0 && g->C % 8 == 0 && (!need_dx || xf_dgrad_ok(g))) ? 1 : 0;
-}
-
 static int conv_dgrad_impl(const ConvGeom* g, const void* dy, const void* wc, void* dx,
                            float* ws, size_t ws_elems, int splits, int accumulate,
                            const BnBwdFuse* bn, const BnBwdApply* ba, int* bn_done,
-                           hipStream_t st, const BnBwdXf* xf = nullptr) {
+                           hipStream_t st) {
   if (bn_done) *bn_done = 0;
   if (g->C % 8 || g->K % 8) return -1;
   if (bn && (accumulate || g->stride != 1)) return -3;  // fused BN sums: plain stride-1 dgrad only
-  if (xf && (accumulate || !xf_dgrad_ok(g) || xf->C != g->K)) return -4;
   ConvArgs a{};
   a.accumulate = accumulate;
   if (bn) {
@@ -2483,7 +2317,6 @@ static int conv_dgrad_impl(const ConvGeom* g, const void* dy, const void* wc, vo
     return -2;
   a.a_bytes = (int)(2 * dya);
   a.b_bytes = (int)(2 * wb);
-  set_xf(a, xf);
   if (g->stride == 1) {
     a.Mg = g->N * g->H * g->W;
     a.Kg = g->R * g->S * g->K;
@@ -2544,26 +2377,9 @@ extern "C" int ddp_conv_dgrad_bn(const ConvGeom* g, const void* dy, const void* 
   return conv_dgrad_impl(g, dy, wc, dx, ws, ws_elems, splits, 0, bn, ba, bn_done, st);
 }
 
-extern "C" int ddp_conv_wgrad_xf(const ConvGeom* g, const void* dy, const void* x, float* dw,
-                                 float* ws, size_t ws_elems, int splits, const BnBwdXf* xf,
-                                 hipStream_t st);
 extern "C" int ddp_conv_wgrad(const ConvGeom* g, const void* dy, const void* x, float* dw,
                               float* ws, size_t ws_elems, int splits, hipStream_t st) {
-  return ddp_conv_wgrad_xf(g, dy, x, dw, ws, ws_elems, splits, nullptr, st);
-}
-
-extern "C" int ddp_conv_dgrad_xf(const ConvGeom* g, const void* wc, void* dx, float* ws,
-                                 size_t ws_elems, const BnBwdFuse* bn, const BnBwdApply* ba,
-                                 int* bn_done, const BnBwdXf* xf, hipStream_t st) {
-  if (!xf) return -1;
-  return conv_dgrad_impl(g, nullptr, wc, dx, ws, ws_elems, 0, 0, bn, ba, bn_done, st, xf);
-}
-
-extern "C" int ddp_conv_wgrad_xf(const ConvGeom* g, const void* dy, const void* x, float* dw,
-                                 float* ws, size_t ws_elems, int splits, const BnBwdXf* xf,
-                                 hipStream_t st) {
   if (g->C % 8 || g->K % 8) return -1;
-  if (xf && xf->C != g->K) return -4;
   ConvArgs a{};
   a.g = *g;
   a.a = (const unsigned short*)dy;
@@ -2581,7 +2397,6 @@ extern "C" int ddp_conv_wgrad_xf(const ConvGeom* g, const void* dy, const void* 
   a.b_bytes = (int)(2 * xb);
   a.dPQ = make_fastdiv(g->P * g->Q);
   a.dQ = make_fastdiv(g->Q);
-  set_xf(a, xf);
   launch_mode<MODE_WGRAD>(a, ws_elems, st);
   return (int)hipGetLastError();
 }
@@ -2606,16 +2421,15 @@ extern "C" void ddp_conv_pair_mode(int m, int items) {
 extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* wc, void* dx,
                                  const void* x, float* dw, float* ws, size_t ws_elems,
                                  const BnBwdFuse* bn, const BnBwdApply* ba, int* bn_done,
-                                 hipStream_t st, const BnBwdXf* xf) {
+                                 hipStream_t st) {
   if (bn_done) *bn_done = 0;
   if (!bn) ba = nullptr;
-  if (xf && (!xf_dgrad_ok(g) || xf->C != g->K)) return -4;
   auto separate = [&]() -> int {
     // DGRAD first: the WGRAD finish may then apply the layer's SGD step (g_sgd_allow)
-    const int r = conv_dgrad_impl(g, dy, wc, dx, ws, ws_elems, 0, 0, bn, ba, bn_done, st, xf);
+    const int r = conv_dgrad_impl(g, dy, wc, dx, ws, ws_elems, 0, 0, bn, ba, bn_done, st);
     if (r) return r;
     g_sgd_allow = true;
-    const int rw = ddp_conv_wgrad_xf(g, dy, x, dw, ws, ws_elems, 0, xf, st);
+    const int rw = ddp_conv_wgrad(g, dy, x, dw, ws, ws_elems, 0, st);
     g_sgd_allow = false;
     return rw;
   };
@@ -2655,8 +2469,6 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
   w.b_bytes = (int)(2 * xb);
   w.dPQ = make_fastdiv(g->P * g->Q);
   w.dQ = make_fastdiv(g->Q);
-  set_xf(d, xf);
-  set_xf(w, xf);
   // measured pair entry (tools/conv_tune.py --pairs) or forced splits (its sweep) first
   bool tuned = false;
   int sd = 1, sw = 1;
@@ -2699,23 +2511,7 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
   if (dneed + wneed > ws_elems) return separate();
   if (g_pair_mode == 3 && !both64 && itd + itw > g_pair_items) return separate();
   const bool bnf1 = d.has_bnf && d.splits <= 1;
-  if (xf) {
-    static const bool attr = [] {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv_bwd_pair_xf_kernel<64, 64, 3, 0>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv_bwd_pair_xf_kernel<64, 64, 3, 1>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      return true;
-    }();
-    (void)attr;
-    const size_t lds = 2 * (size_t)xf_table_elems(xf->C, xf->mask) + 3 * (size_t)(64 + 64 + 64) * 64 * 2;
-    if (bnf1)
-      hipLaunchKernelGGL((conv_bwd_pair_xf_kernel<64, 64, 3, 1>), dim3(itd + itw), dim3(256), lds,
-                         st, d, w, itd);
-    else
-      hipLaunchKernelGGL((conv_bwd_pair_xf_kernel<64, 64, 3, 0>), dim3(itd + itw), dim3(256), lds,
-                         st, d, w, itd);
-  } else if (bnf1) {
+  if (bnf1) {  } else if (bnf1) {
     hipLaunchKernelGGL((conv_bwd_pair_kernel<64, 64, 3, 1>), dim3(itd + itw), dim3(256), 0, st,
                        d, w, itd);
   } else {
@@ -2756,10 +2552,9 @@ extern "C" void ddp_sgd_fuse_register(float* dw, const SgdFuse* f, int clear) {
 extern "C" void ddp_sgd_fuse_begin() { g_sgd_taken.clear(); }
 // a WGRAD whose layer runs no DGRAD (the input layer): its finish may apply the SGD step
 extern "C" int ddp_conv_wgrad_final(const ConvGeom* g, const void* dy, const void* x, float* dw,
-                                    float* ws, size_t ws_elems, int splits, const BnBwdXf* xf,
-                                    hipStream_t st) {
+                                    float* ws, size_t ws_elems, int splits, hipStream_t st) {
   g_sgd_allow = true;
-  const int r = ddp_conv_wgrad_xf(g, dy, x, dw, ws, ws_elems, splits, xf, st);
+  const int r = ddp_conv_wgrad(g, dy, x, dw, ws, ws_elems, splits, st);
   g_sgd_allow = false;
   return r;
 }

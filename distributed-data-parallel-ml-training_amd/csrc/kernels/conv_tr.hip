@@ -101,8 +101,6 @@ struct Args {
   int nmajor;                // tile order: 0 = column tiles fastest, 1 = row tiles fastest (each
                              // XCD's run of consecutive tiles then shares one weight slice)
   int abuf_elems;            // bf16 elements of one patch buffer (16-B multiple)
-  int flip;                  // weights read at tap 8 - t (backward-data: dx = conv(dz, W
-                             // flipped + transposed), wc = the [C][3][3][K] copy)
   // fused input (template IN = 1: BN + ReLU, IN = 2: BN + ReLU + 2x2/s2 max-pool): the conv
   // input x = [pool](relu(scale * zin + shift)) is computed while the patch is loaded; zin is
   // the preceding block's conv output [N][Hz][Wz][C] (Hz = 2H when pooled), its BatchNorm
@@ -118,34 +116,9 @@ struct Args {
   float* in_coef;            // [6][C]: scale, shift, mean, invstd (written by block 0)
   unsigned short* y_out;     // [N][H][W][C]
   int z_bytes;
-  // IN = 3 (backward-data only): the patch is the gradient at a training-mode BatchNorm's input,
-  // dz = xA[c] * g + xB[c] * z + xC[c], computed while it is loaded (conv_igemm.hip XF): zin = z,
-  // xg = g (same [N][H][W][C] layout), xcoef = [C/8][3 or 5][8] (xmask: g is the raw block
-  // output gradient and the ReLU mask scale * z + shift > 0 is applied here) — the BN-backward
-  // apply pass never runs
-  const unsigned short* xg;
-  const float* xcoef;
-  int xmask;
 };
 
-// KM (backward-data only): the weights are read k-major straight from the FORWARD copy
-// Wc [Kf][3][3][Cf] (k = Kf = this problem's input channels, columns = Cf = its output
-// channels): 16-B chunks of 8 output channels land in a [k][col] tile (conv_igemm.hip's mc_swz
-// layout) read with ds_read_b64_tr_b16 — no transposed weight copy to maintain.
-typedef short v4i16_t __attribute__((ext_vector_type(4)));
-typedef short short8_t __attribute__((ext_vector_type(8)));
-typedef __attribute__((address_space(3))) v4i16_t lds_v4i16_t;
-template <int NCOL>
-__device__ __forceinline__ int km_swz(int m) {
-  if (NCOL >= 128) return (((m & 3) | (((m >> 3) & 1) << 2)) << 1) & (NCOL / 8 - 1);
-  return ((((m >> 1) & 1) | (((m >> 3) & 1) << 1)) << 1);
-}
-template <int NCOL>
-__device__ __forceinline__ int km_off(int m, int col) {
-  return m * NCOL + (((col >> 3) ^ km_swz<NCOL>(m)) << 3) + (col & 7);
-}
-
-template <int BM, int BN, int NST, int NL, int IN, int KM = 0>
+template <int BM, int BN, int NST, int NL, int IN>
 #ifndef DDP_TR_WAVES_PER_EU
 #define DDP_TR_WAVES_PER_EU 1  // (A/B knob: -DDDP_TR_WAVES_PER_EU=3 asks for 3 waves per SIMD)
 #endif
@@ -161,9 +134,8 @@ void conv_tr_fwd_kernel(Args a) {
   unsigned short* abuf = smem;                          // 2 patch buffers
   unsigned short* bring = smem + 2 * aelems;            // NST x BTILE
   float* cf = reinterpret_cast<float*>(bring + NST * BTILE);  // IN: [2][C] scale | shift
-  constexpr int NP = IN == 2 ? 4 : (IN == 3 ? 2 : 1);  // source loads per patch item
+  constexpr int NP = IN == 2 ? 4 : 1;                   // source loads per patch item
   constexpr bool BNIN = IN == 1 || IN == 2;             // BN + ReLU (+ pool) input
-  static_assert(!KM || BN <= 128, "k-major weights: one logical chunk per thread");
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -186,12 +158,6 @@ void conv_tr_fwd_kernel(Args a) {
   const int h0 = (tm % a.bands) * a.rows;  // first output row of the band
 
   const __amdgpu_buffer_rsrc_t rsA = IN ? make_rsrc(a.zin, a.z_bytes) : make_rsrc(a.x, a.x_bytes);
-  const __amdgpu_buffer_rsrc_t rsG = make_rsrc(IN == 3 ? a.xg : a.x, IN == 3 ? a.z_bytes : 16);
-  if (IN == 3) {  // the BN-backward affine table of every input channel into LDS
-    const int n = (C / 8) * (a.xmask ? 40 : 24);
-    for (int i = tid; i < n; i += 256) cf[i] = a.xcoef[i];
-    __syncthreads();
-  }
   if (BNIN) {
     // BatchNorm finalize of the input channels (batch statistics of zin over N*Hz*Wz), as
     // bn_act.hip fold_fwd_coeffs: every block reduces the replicas into LDS; block 0 also
@@ -265,16 +231,10 @@ void conv_tr_fwd_kernel(Args a) {
   auto load_a = [&](int cb) {
     const unsigned coff = (unsigned)(cb * 128);
 #pragma unroll
-    for (int u = 0; u < NL; ++u) {
-      if constexpr (IN == 3) {
-        areg[u][0] = __builtin_amdgcn_raw_buffer_load_b128(rsA, (int)(asrc[u] + coff), 0, 0);
-        areg[u][1] = __builtin_amdgcn_raw_buffer_load_b128(rsG, (int)(asrc[u] + coff), 0, 0);
-      } else {
+    for (int u = 0; u < NL; ++u)
 #pragma unroll
-        for (int d = 0; d < NP; ++d)
-          areg[u][d] = __builtin_amdgcn_raw_buffer_load_b128(rsA, (int)(asrc[u] + coff + pofs[d]), 0, 0);
-      }
-    }
+      for (int d = 0; d < NP; ++d)
+        areg[u][d] = __builtin_amdgcn_raw_buffer_load_b128(rsA, (int)(asrc[u] + coff + pofs[d]), 0, 0);
   };
   auto store_a = [&](int buf, int cb) {
     char* dst = reinterpret_cast<char*>(abuf + buf * aelems);
@@ -287,45 +247,11 @@ void conv_tr_fwd_kernel(Args a) {
         sh[e] = cf[C + c0 + e];
       }
     }
-    float xa[8], xb[8], xc[8];
-    if (IN == 3) {
-      const bool xm = a.xmask;
-      const float* xt = cf + (cb * 8 + (tid & 7)) * (xm ? 40 : 24);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        xa[e] = xt[e];
-        xb[e] = xt[8 + e];
-        xc[e] = xt[16 + e];
-        sc[e] = xm ? xt[24 + e] : 0.f;
-        sh[e] = xm ? xt[32 + e] : 0.f;
-      }
-    }
 #pragma unroll
     for (int u = 0; u < NL; ++u) {
       if (adst[u] < 0) continue;
       v4i v = areg[u][0];
-      if (IN == 3) {
-        if (asrc[u] == kOOB) {
-          v = (v4i){0, 0, 0, 0};  // conv zero padding of dz (not xC)
-        } else {
-          const v4i zq = areg[u][0], gq = areg[u][1];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float o[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              const int ch = 2 * e + h;
-              const unsigned zw = (unsigned)zq[e], gw = (unsigned)gq[e];
-              const float zf = __uint_as_float(h ? (zw & 0xffff0000u) : (zw << 16));
-              float gf = __uint_as_float(h ? (gw & 0xffff0000u) : (gw << 16));
-              // (the forward's ReLU input: bf16 z times the same fp32 scale / shift)
-              if (a.xmask && !(zf * sc[ch] + sh[ch] > 0.f)) gf = 0.f;
-              o[h] = fmaf(xa[ch], gf, fmaf(xb[ch], zf, xc[ch]));
-            }
-            v[e] = (int)((unsigned)f2bf(o[0]) | ((unsigned)f2bf(o[1]) << 16));
-          }
-        }
-      } else if (BNIN) {
+      if (BNIN) {
         if (asrc[u] == kOOB) {
           v = (v4i){0, 0, 0, 0};  // conv zero padding of the post-BN activation
         } else {
@@ -355,25 +281,15 @@ void conv_tr_fwd_kernel(Args a) {
   // ---- B (weights) DMA: row (tid >> 3) + 32 i of the [col][k] tile, logical chunk lcB
   const int lcB = (tid & 7) ^ ((tid >> 4) & 7);
   unsigned boff[CB];
-  if constexpr (KM) {  // chunk tid + 256 i = row m (k), physical chunk tid % (BN/8)
-    constexpr int NCB = BN / 8;
-    const int m = tid / NCB;
-    const int col = col0 + ((tid % NCB) ^ km_swz<BN>(m)) * 8;  // same logical chunk for every i
 #pragma unroll
-    for (int i = 0; i < CB; ++i)
-      boff[i] = col < K ? (unsigned)(2 * ((m + i * (256 / NCB)) * 9 * K + col)) : kOOB;
-  } else {
-#pragma unroll
-    for (int i = 0; i < CB; ++i) {
-      const int col = col0 + (tid >> 3) + 32 * i;
-      boff[i] = col < K ? (unsigned)(2 * (col * 9 * C + lcB * 8)) : kOOB;
-    }
+  for (int i = 0; i < CB; ++i) {
+    const int col = col0 + (tid >> 3) + 32 * i;
+    boff[i] = col < K ? (unsigned)(2 * (col * 9 * C + lcB * 8)) : kOOB;
   }
 
   auto issue_b = [&](int j, int slot) {
     const int cb = cb0 + j / 9, t = j - (j / 9) * 9;
-    const int tw = a.flip ? 8 - t : t;
-    const unsigned k0 = KM ? (unsigned)(2 * ((cb * 64 * 9 + tw) * K)) : (unsigned)(2 * (tw * C + cb * 64));
+    const unsigned k0 = (unsigned)(2 * (t * C + cb * 64));
     unsigned short* dst = bring + slot * BTILE;
 #pragma unroll
     for (int i = 0; i < CB; ++i) dma(rsB, boff[i] + k0, dst + (wid * 64 + 256 * i) * 8);
@@ -395,14 +311,7 @@ void conv_tr_fwd_kernel(Args a) {
   const int kk_a = (plane_base(4, a.plane) - plane_base(0, a.plane)) * 16;  // chunk planes +4
   int fb_off[TN];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    if constexpr (KM) {  // ds_read_b64_tr_b16 rows m0, m0 + 4 (as conv_igemm.hip's k-major B)
-      const int m0 = 8 * (lane >> 4) + ((lane >> 2) & 3);
-      fb_off[j] = km_off<BN>(m0, wn * WTN + j * 16 + 4 * (lane & 3));
-    } else {
-      fb_off[j] = rk_off(wn * WTN + j * 16 + (lane & 15), lane >> 4);
-    }
-  }
+  for (int j = 0; j < TN; ++j) fb_off[j] = rk_off(wn * WTN + j * 16 + (lane & 15), lane >> 4);
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -429,16 +338,7 @@ void conv_tr_fwd_kernel(Args a) {
         if (s != 1 && !ok) fa[i] = (bf16x8){};
       }
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        if constexpr (KM) {
-          const unsigned short* base = Bs + fb_off[j] + kk * BN;
-          const v4i16_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16_t*)base);
-          const v4i16_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16_t*)(base + 4 * BN));
-          fb[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-        } else {
-          fb[j] = *reinterpret_cast<const bf16x8*>(Bs + (fb_off[j] ^ (kk ? 32 : 0)));
-        }
-      }
+      for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(Bs + (fb_off[j] ^ (kk ? 32 : 0)));
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -647,45 +547,40 @@ static Geo geometry(int BM, int N, int H, int W) {
   return g;
 }
 
-// in: 0 plain, 1 / 2 BN + ReLU (+ pool) input ([2][C] table), 3 BN-backward dz ([C/8][5][8])
+// in: 0 plain, 1 / 2 BN + ReLU (+ pool) input ([2][C] table)
 static size_t lds_bytes(const Args& a, int nst, int bn, int in) {
-  const size_t table = in == 3 ? 5 * (size_t)a.C * 4 : (in ? 2 * (size_t)a.C * 4 : 0);
+  const size_t table = in ? 2 * (size_t)a.C * 4 : 0;
   return 2 * (size_t)a.abuf_elems * 2 + (size_t)nst * bn * 64 * 2 + table;
 }
 
-template <int BM, int BN, int NST, int NL, int IN, int KM>
+template <int BM, int BN, int NST, int NL, int IN>
 static void launch_t(const Args& a, int items, hipStream_t st) {
   const size_t lds = lds_bytes(a, NST, BN, IN);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv_tr_fwd_kernel<BM, BN, NST, NL, IN, KM>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv_tr_fwd_kernel<BM, BN, NST, NL, IN>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((conv_tr_fwd_kernel<BM, BN, NST, NL, IN, KM>), dim3(items), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((conv_tr_fwd_kernel<BM, BN, NST, NL, IN>), dim3(items), dim3(256), lds, st, a);
 }
 
-template <int BM, int BN, int NST, int IN, int KM = 0>
+template <int BM, int BN, int NST, int IN>
 static bool launch_nl(const Args& a, int nl, int items, hipStream_t st) {
   if (lds_bytes(a, NST, BN, IN) > 160 * 1024) return false;
   switch (nl) {
-    case 1: launch_t<BM, BN, NST, 1, IN, KM>(a, items, st); return true;
-    case 2: launch_t<BM, BN, NST, 2, IN, KM>(a, items, st); return true;
-    case 3: launch_t<BM, BN, NST, 3, IN, KM>(a, items, st); return true;
-    case 4: launch_t<BM, BN, NST, 4, IN, KM>(a, items, st); return true;
-    case 5: launch_t<BM, BN, NST, 5, IN, KM>(a, items, st); return true;
-    case 6: launch_t<BM, BN, NST, 6, IN, KM>(a, items, st); return true;
+    case 1: launch_t<BM, BN, NST, 1, IN>(a, items, st); return true;
+    case 2: launch_t<BM, BN, NST, 2, IN>(a, items, st); return true;
+    case 3: launch_t<BM, BN, NST, 3, IN>(a, items, st); return true;
+    case 4: launch_t<BM, BN, NST, 4, IN>(a, items, st); return true;
+    case 5: launch_t<BM, BN, NST, 5, IN>(a, items, st); return true;
+    case 6: launch_t<BM, BN, NST, 6, IN>(a, items, st); return true;
     default: return false;
   }
 }
 
 template <int BM, int BN>
-static bool launch_bmbn(int nst, int in, const Args& a, int nl, int items, hipStream_t st,
-                        int km = 0) {
-  if (km) {  // backward-data from the forward weight copy (3 stages; plain or XF patch)
-    if (in == 3) return launch_nl<BM, BN, 3, 3, 1>(a, nl, items, st);
-    return in == 0 && launch_nl<BM, BN, 3, 0, 1>(a, nl, items, st);
-  }
+static bool launch_bmbn(int nst, int in, const Args& a, int nl, int items, hipStream_t st) {
   if (in == 1) return nst == 3 && launch_nl<BM, BN, 3, 1>(a, nl, items, st);
   if (in == 2) return nst == 3 && launch_nl<BM, BN, 3, 2>(a, nl, items, st);
   switch (nst) {
@@ -704,16 +599,15 @@ struct Cfg {
 
 // B ring depth: the table's (3 was fastest for every VGG layer: deeper rings cost occupancy,
 // profiles/r3_conv_tr_sweep.jsonl); the fused-input modes are built with 3 only
-static bool launch_stages(const Cfg& c, int in, const Args& a, int nl, int items, hipStream_t st,
-                          int km = 0) {
-  const int n = (in || km) ? 3 : (c.stages ? c.stages : 3);
-  if (c.bm == 128 && c.bn == 128) return launch_bmbn<128, 128>(n, in, a, nl, items, st, km);
-  if (c.bm == 128 && c.bn == 64) return launch_bmbn<128, 64>(n, in, a, nl, items, st, km);
-  if (c.bm == 64 && c.bn == 128) return launch_bmbn<64, 128>(n, in, a, nl, items, st, km);
-  if (c.bm == 64 && c.bn == 64) return launch_bmbn<64, 64>(n, in, a, nl, items, st, km);
+static bool launch_stages(const Cfg& c, int in, const Args& a, int nl, int items, hipStream_t st) {
+  const int n = in ? 3 : (c.stages ? c.stages : 3);
+  if (c.bm == 128 && c.bn == 128) return launch_bmbn<128, 128>(n, in, a, nl, items, st);
+  if (c.bm == 128 && c.bn == 64) return launch_bmbn<128, 64>(n, in, a, nl, items, st);
+  if (c.bm == 64 && c.bn == 128) return launch_bmbn<64, 128>(n, in, a, nl, items, st);
+  if (c.bm == 64 && c.bn == 64) return launch_bmbn<64, 64>(n, in, a, nl, items, st);
   return false;
 }
-static std::map<std::tuple<int, int, int, int, int>, Cfg> g_tr_tuned;  // (op, M, K, C, H)
+static std::map<std::tuple<int, int, int, int>, Cfg> g_tr_tuned;  // (M, K, C, H)
 static int g_tr_mode = -1;  // -1 unread; 0 off; 1 on (DDP_AMD_CONV_TR)
 static Cfg g_tr_force{0, 0, 0, 0};
 
@@ -744,8 +638,7 @@ extern "C" void ddp_conv_tr_set(int mode, int M, int K, int C, int H, int bm, in
   // mode: -1 clear table, 0/1 enable, 2 add table entry, 3 force (bm, bn, splits) for sweeps
   if (mode == -1) { tr::g_tr_tuned.clear(); return; }
   if (mode == 0 || mode == 1 || mode == 4) { tr::g_tr_mode = mode == 4 ? 2 : mode; return; }
-  if (mode == 2 || mode == 5)  // 2: forward entry, 5: backward-data entry (dgrad GEMM's K, C)
-    { tr::g_tr_tuned[std::make_tuple(mode == 5 ? 1 : 0, M, K, C, H)] = tr::Cfg{bm, bn, splits, stages}; return; }
+  if (mode == 2) { tr::g_tr_tuned[std::make_tuple(M, K, C, H)] = tr::Cfg{bm, bn, splits, stages}; return; }
   if (mode == 3) tr::g_tr_force = tr::Cfg{bm, bn, splits, stages};
 }
 
@@ -758,8 +651,7 @@ struct Plan {
 };
 
 // the launch decision shared by ddp_conv_fwd_tr and ddp_conv_tr_would_serve
-static bool plan(const ConvGeom* g, float* ws, size_t ws_elems, int in_mode, Plan* p,
-                 int op = 0) {
+static bool plan(const ConvGeom* g, float* ws, size_t ws_elems, int in_mode, Plan* p) {
   if (g_tr_mode < 0) {
     // 0 off, 1 (default) table entries only, 2 also the heuristic for untabled shapes
     const char* e = std::getenv("DDP_AMD_CONV_TR");
@@ -774,18 +666,18 @@ static bool plan(const ConvGeom* g, float* ws, size_t ws_elems, int in_mode, Pla
   const size_t xe = M * C * (in_mode == 2 ? 4 : 1), we = (size_t)K * 9 * C;
   if (2 * xe >= kOOB || 2 * we >= kOOB || M * K >= kOOB) return false;
   Cfg c;
-  auto it = g_tr_tuned.find(std::make_tuple(op, (int)M, K, C, H));
+  auto it = g_tr_tuned.find(std::make_tuple((int)M, K, C, H));
   if (g_tr_force.bm) c = g_tr_force;
   else if (it != g_tr_tuned.end()) c = it->second;
-  else if (g_tr_mode == 2 && op == 0) c = heuristic(N, H, W, C, K);
+  else if (g_tr_mode == 2) c = heuristic(N, H, W, C, K);
   else return false;  // default: only the layers the measured table assigns to this kernel
   if (c.bm == 0) return false;  // table entry "use the implicit-GEMM kernel"
   if (K % c.bn || M % c.bm) return false;
   const Geo geo = geometry(c.bm, N, H, W);
   if (!geo.ok || geo.nl < 1 || geo.nl > 6) return false;
-  const int nst = (in_mode || op == 1) ? 3 : (c.stages ? c.stages : 3);
+  const int nst = in_mode ? 3 : (c.stages ? c.stages : 3);
   const size_t lds = 2 * (size_t)geo.abuf * 2 + (size_t)nst * c.bn * 64 * 2 +
-                     (in_mode == 3 ? 5 * (size_t)C * 4 : (in_mode ? 2 * (size_t)C * 4 : 0));
+                     (in_mode ? 2 * (size_t)C * 4 : 0);
   if (lds > 160 * 1024) return false;
   const int ncb = C / 64;
   int splits = std::max(1, std::min(c.splits, ncb));
@@ -864,92 +756,12 @@ extern "C" int ddp_conv_fwd_tr(const ConvGeom* g, const void* x, const void* wc,
   return 1;
 }
 
-// Backward-data of a 3x3 / stride 1 / pad 1 conv through the tap-reuse kernel: dx = conv(dz,
-// flip(W)^T) — the same 3x3 problem with the channel roles swapped (input dz with K channels,
-// output dx with C channels) and the weights read from the transposed copy wt [C][3][3][K] at
-// tap 8 - t. g = the FORWARD geometry. Returns 1 served, 0 not served (use ddp_conv_dgrad /
-// the backward pair), >= 2 HIP error.
-// kmajor = 1: ``w`` is the FORWARD copy Wc [K][3][3][C], read k-major (KM kernels; no
-// transposed copy); 0: ``w`` = the transposed copy wt. ``xf`` (kmajor only): dz is computed
-// while the patch loads from (xf->z, xf->g, xf->coef) — ``dz`` is then ignored (IN = 3).
-static int conv_dgrad_tr_impl(const ConvGeom* g, const void* dz, const void* w, void* dx,
-                              float* ws, size_t ws_elems, int kmajor, const BnBwdXf* xf,
-                              hipStream_t st) {
-  using namespace ddp_amd::tr;
-  ConvGeom t = *g;
-  t.C = g->K;
-  t.K = g->C;
-  t.Creal = g->K;
-  if (g->Creal != g->C) return 0;
-  if (xf && (!kmajor || xf->C != g->K || xf->C % 8)) return -1;
-  const int in = xf ? 3 : 0;
-  Plan pl;
-  if (!plan(&t, ws, ws_elems, in, &pl, 1)) return 0;
-  const Cfg& c = pl.c;
-  const Geo& geo = pl.geo;
-  const size_t M = (size_t)t.N * t.H * t.W;
-  Args a{};
-  a.N = t.N; a.H = t.H; a.W = t.W; a.C = t.C; a.K = t.K;
-  a.x = (const unsigned short*)dz;
-  a.wc = (const unsigned short*)w;
-  a.z = (unsigned short*)dx;
-  a.ws = ws;
-  a.splits = pl.splits;
-  a.cbps = pl.cbps;
-  a.imgs = geo.imgs; a.rows = geo.rows; a.bands = geo.bands;
-  a.imgp = geo.imgp; a.plane = geo.plane; a.zslot = geo.zslot;
-  a.x_bytes = (int)(2 * M * t.C);
-  a.w_bytes = (int)(2 * (size_t)t.K * 9 * t.C);
-  a.abuf_elems = geo.abuf;
-  a.tiles_m = (int)(M / c.bm);
-  a.tiles_n = t.K / c.bn;
-  a.nmajor = tile_order_n();
-  a.flip = 1;
-  if (xf) {
-    a.zin = (const unsigned short*)xf->z;
-    a.xg = (const unsigned short*)xf->g;
-    a.xcoef = xf->coef;
-    a.xmask = xf->mask;
-    a.z_bytes = (int)(2 * M * t.C);
-  }
-  const int items = a.tiles_m * a.tiles_n * pl.splits;
-  if (!launch_stages(c, in, a, geo.nl, items, st, kmajor)) return 0;
-  int e = (int)hipGetLastError();
-  if (e) return 2 + e;
-  if (pl.splits > 1) {
-    e = ddp_conv_fwd_finish(&t, ws, pl.splits, nullptr, dx, nullptr, nullptr, nullptr, st);
-    if (e) return 2 + e;
-  }
-  return 1;
-}
-
-extern "C" int ddp_conv_dgrad_tr(const ConvGeom* g, const void* dz, const void* wt, void* dx,
-                                 float* ws, size_t ws_elems, hipStream_t st) {
-  return conv_dgrad_tr_impl(g, dz, wt, dx, ws, ws_elems, 0, nullptr, st);
-}
-
-// Backward-data through the tap-reuse kernel with the weights read from the forward copy
-// Wc (k-major) and, with ``xf``, the BatchNorm-backward dz computed in the patch load.
-extern "C" int ddp_conv_dgrad_tr_wc(const ConvGeom* g, const void* dz, const void* wc, void* dx,
-                                    float* ws, size_t ws_elems, const BnBwdXf* xf,
-                                    hipStream_t st) {
-  return conv_dgrad_tr_impl(g, dz, wc, dx, ws, ws_elems, 1, xf, st);
-}
-
 // would ddp_conv_fwd_tr serve this problem (with a fused input of mode in_mode: 0 none,
 // 1 BN+ReLU, 2 BN+ReLU+pool)? No launch.
-// (in_mode -1: the backward-data problem of ddp_conv_dgrad_tr for the forward geometry g)
 extern "C" int ddp_conv_tr_would_serve(const ConvGeom* g, size_t ws_elems, int in_mode) {
   ddp_amd::tr::Plan pl;
   float dummy;
-  if (in_mode < 0) {
-    ConvGeom t = *g;
-    t.C = g->K;
-    t.K = g->C;
-    t.Creal = g->K;
-    if (g->Creal != g->C) return 0;
-    return ddp_amd::tr::plan(&t, ws_elems ? &dummy : nullptr, ws_elems, 0, &pl, 1) ? 1 : 0;
-  }
+  if (in_mode < 0) return 0;
   return ddp_amd::tr::plan(g, ws_elems ? &dummy : nullptr, ws_elems, in_mode, &pl) ? 1 : 0;
 }
 

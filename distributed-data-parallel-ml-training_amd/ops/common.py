@@ -33,8 +33,6 @@ def native():
 TUNING_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "conv_tuning.json")
 
 
-# (forward K, forward C) of the 3x3 layers whose backward-data the tap-reuse table serves
-TR_DGRAD_SHAPES = set()
 
 
 def load_conv_tuning(n=None, path=None):
@@ -57,16 +55,7 @@ def load_conv_tuning(n=None, path=None):
     for e in table.get("tr_entries", []):
         n.conv_tr_set(2, int(e["M"]), int(e["K"]), int(e["C"]), int(e["H"]), int(e["bm"]),
                       int(e["bn"]), int(e["splits"]), int(e.get("stages", 0)))
-    # backward-data entries: keyed by the dgrad problem (M, K = forward C, C = forward K, H);
-    # (TR_DGRAD_SHAPES: the forward shapes with at least one served entry)
-    TR_DGRAD_SHAPES.clear()
-    for e in table.get("tr_dgrad_entries", []):
-        if int(e["bm"]) > 0:
-            TR_DGRAD_SHAPES.add((int(e["C"]), int(e["K"])))  # (forward K, forward C)
-        n.conv_tr_set(5, int(e["M"]), int(e["K"]), int(e["C"]), int(e["H"]), int(e["bm"]),
-                      int(e["bn"]), int(e["splits"]), int(e.get("stages", 0)))
-    return (len(table.get("entries", [])) + len(table.get("tr_entries", []))
-            + len(table.get("tr_dgrad_entries", [])))
+    return len(table.get("entries", [])) + len(table.get("tr_entries", []))
 
 
 def weight_krsc(w):
@@ -173,15 +162,11 @@ def join_side_streams():
         st.join()
 
 
-# BatchNorm backward without its apply pass (bn_act.hip ddp_bn_bwd_xf + conv_igemm.hip XF): the
-# reduce kernel stores dy_bn, the finalize writes the per-channel affine form of dz, and the
-# producing conv's backward GEMMs compute dz = A dy_bn + B z + C while staging their A operand —
-# dz is never written and never re-read. Layers the one-launch local BN backward serves keep it.
-# Opt-in (DDP_AMD_BN_BWD_XF=1): measured SLOWER end to end — VGG-11 b256 1.181 vs 0.852 ms,
-# b32 0.420 vs 0.402 ms (same box, profiles/r4d_*): the XF GEMMs stage z AND dy_bn (twice the
-# A-operand bytes, 72 KB of LDS -> 2 blocks per CU) and each k-step waits for its stage's DMAs
-# and a barrier before the rewrite, which serialises the ring (the 8x8 pair: 226 vs 46 us).
-BN_BWD_XF = os.environ.get("DDP_AMD_BN_BWD_XF", "0") == "1"
+# (Round 4 built and removed two more backward variants, both measured slower on every config:
+# the apply-free BatchNorm backward whose dz the conv GEMMs computed while staging their A
+# operand — VGG-11 b256 1.181 vs 0.852 ms, ResNet-50 35.89 vs 26.55 ms: the GEMMs staged z AND
+# dy_bn and serialised their LDS ring on the rewrite — and the tap-reuse backward-data kernel,
+# b256 0.898 vs 0.837 ms; profiles/r4d_ab.md, r4e_notes.md.)
 
 
 # BatchNorm-backward sums of a Conv->BN->ReLU(->pool) block accumulated by the NEXT block's

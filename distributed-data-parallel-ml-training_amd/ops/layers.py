@@ -49,9 +49,8 @@ class ConvBNActSpec:
         self.eps = float(bn.eps) if bn is not None else 1e-5
         dev = conv.weight.device
         self.wc = torch.empty(K, R, S, self.C, dtype=BF16, device=dev)
-        # transposed copy [C][R][S][K]: none. Both backward-data kernels (implicit GEMM and the
-        # tap-reuse one) read Wc k-major through transposing LDS reads (ds_read_b64_tr_b16);
-        # only probes that time the older transposed-copy kernel set one themselves
+        # transposed copy [C][R][S][K]: none. The backward-data GEMM reads Wc k-major through
+        # transposing LDS reads (ds_read_b64_tr_b16); the optimizer's repack keeps the slot
         self.wt = None
         self._packed_version = None
         conv.weight._ddp_amd_pack = self.pack_desc  # the fused optimizer repacks after its step
@@ -64,9 +63,6 @@ class ConvBNActSpec:
         # per-layer BN coefficient table [6][K] (scale, shift, mean, invstd | k1, k2): written
         # by the forward's finalize kernel, read by the backward (one use per step per layer)
         self.coef = torch.empty(6 * K, dtype=F32, device=dev)
-        # apply-free BN backward (BN_BWD_XF): [K/8][3 or 5][8] affine form of dz (+ the ReLU
-        # mask's scale / shift) for the conv GEMMs
-        self.xcoef = torch.empty(5 * K, dtype=F32, device=dev)
         # BnBwdFuse chaining (VGG): ``prev`` is the Conv->BN->ReLU(->pool) block that produces
         # this block's input; this block's dgrad accumulates prev's BatchNorm-backward sums in
         # its epilogue and sets ``prev.sums_ready`` so prev's backward skips its reduce pass
@@ -201,13 +197,6 @@ class GradLink:
 # 3x3 stride-1 forward convolutions through the tap-reuse kernel (conv_tr.hip); =0 restores the
 # implicit-GEMM kernel for every layer (the native side also reads DDP_AMD_CONV_TR)
 CONV_TR = os.environ.get("DDP_AMD_CONV_TR", "1") != "0"
-# backward-data of 3x3 stride-1 layers through the tap-reuse kernel (conv_tr.hip, weights read
-# k-major from the forward copy Wc, the BatchNorm-backward dz computed in its patch load) where
-# the measured table (tr_dgrad_entries) says it beats the backward pair, followed by the weight
-# gradient alone. Round 3's version needed a transposed weight copy whose repack in the SGD cost
-# more than the kernel saved (profiles/r3_conv_tr_dgrad.md); this one needs none.
-# DDP_AMD_DGRAD_TR=1 enables it.
-DGRAD_TR = int(os.environ.get("DDP_AMD_DGRAD_TR", "0"))
 # a block's BatchNorm + ReLU (+ 2x2 pool) forward computed by the NEXT block's tap-reuse conv
 # while it loads its input patch (conv_tr.hip fused input; no bn_act_fwd launch); =0 restores the
 # separate pass
@@ -252,71 +241,25 @@ def bn_bwd_fuse_pays(H, W, pool=True):
     return H * W <= BN_BWD_FUSE_MAX_HW
 
 
-def dgrad_tr_serves(spec, x, need_dx, link=None):
-    """Does this layer's backward-data go through the tap-reuse kernel (DGRAD_TR)? A plain 3x3
-    stride-1 layer whose shape the measured table assigns to it."""
-    if not (DGRAD_TR and need_dx and link is None and not _common.BWD_SIDE_STREAM
-            and spec.R == 3 and spec.S == 3 and spec.stride == 1 and spec.pad == 1
-            and spec.C == spec.Cr and spec.wc is not None and x.is_cuda):
-        return False
-    N, H, W, _ = x.shape
-    key = (N, H, W)
-    cache = spec.__dict__.setdefault("_tr_dgrad_cache", {})
-    if key not in cache:
-        cache[key] = bool(native().conv_tr_would_serve(spec.geom(N, H, W), workspace(x.device).numel(),
-                                                       -1))
-    return cache[key]
-
-
-def conv_xf_ok(spec, x, need_dx, link=None):
-    """Can this layer's backward GEMMs take the BatchNorm-backward apply on their A operand
-    (conv_igemm.hip XF)? Not for an accumulating second-branch dgrad (ResNet GradLink) nor for
-    the opt-in tap-reuse dgrad."""
-    if need_dx and ((link is not None and link.buf is not None) or spec.wt is not None):
-        return False
-    N, H, W, _ = x.shape
-    return bool(native().conv_xf_ok(spec.geom(N, H, W), int(bool(need_dx))))
-
-
-def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=None, bna=None,
-                  xf=None):
+def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=None, bna=None):
     """dW += wgrad(dz, x); returns dx (or None). With ``weight`` (the parameter whose gradient
     is dweight) and the backward side stream enabled, the wgrad runs on the side stream and the
     parameter is announced ready there (common.side_stream); otherwise everything is stream-
     ordered on the current stream and the caller announces the gradient.
     ``bna`` = (dz_prev, dgamma_prev, dbeta_prev) pointers (with ``bnf``): the preceding block's
     whole BatchNorm backward may be completed in the dgrad's split-K finish; the return value is
-    then (dx, done) — when done, dx was NOT written and dz_prev / dgamma / dbeta were.
-    ``xf`` = (z, dy_bn, xcoef, K) pointers: dz is not a tensor — both GEMMs compute it from the
-    BatchNorm's input z and output gradient dy_bn while staging their A operand (``dz`` is then
-    None; conv_xf_ok must have said yes)."""
+    then (dx, done) — when done, dx was NOT written and dz_prev / dgamma / dbeta were."""
     N, H, W, C = x.shape
     g = spec.geom(N, H, W, weight_krsc(dweight))
     s = stream_handle()
     ws = workspace(x.device)
-    if xf is not None:
-        if dz is not None:
-            raise ValueError("conv_backward: pass either dz or xf")
-        if need_dx and ((link is not None and link.buf is not None) or spec.wt is not None):
-            raise ValueError("conv_backward: xf cannot serve an accumulating / tap-reuse dgrad")
-    if bna is None and bnf is None and dgrad_tr_serves(spec, x, need_dx, link):
-        # tap-reuse backward-data (conv_tr.hip, Wc read k-major, dz from xf in the patch load)
-        # FIRST, then the weight gradient alone: its finish may apply the layer's SGD step
-        dx = torch.empty_like(x)
-        if native().conv_dgrad_tr_wc(g, ptr(dz), ptr(spec.wc), ptr(dx), ptr(ws), ws.numel(), s,
-                                     xf=xf):
-            native().conv_wgrad(g, ptr(dz), ptr(x), ptr(dweight), ptr(ws), ws.numel(), 0, s,
-                                xf=xf, final=1)
-            if weight is not None:
-                grad_ready([weight])
-            return dx
     if (need_dx and link is None and not _common.BWD_SIDE_STREAM and spec.stride == 1
             and spec.C == spec.Cr):
         # wgrad + dgrad of this layer as one grouped launch (+ one finish launch) when the
         # kernel policy allows it (conv_igemm.hip ddp_conv_bwd_pair), else the two launches
         dx = torch.empty_like(x)
         done = native().conv_bwd_pair(g, ptr(dz), ptr(spec.wc), ptr(dx), ptr(x), ptr(dweight),
-                                      ptr(ws), ws.numel(), s, bn=bnf, bna=bna, xf=xf)
+                                      ptr(ws), ws.numel(), s, bn=bnf, bna=bna)
         if weight is not None:
             grad_ready([weight])
         return (dx, bool(done)) if bna is not None else dx
@@ -324,11 +267,11 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=Non
         side = side_stream(x.device, x, dz)
         with torch.cuda.stream(side.stream):
             native().conv_wgrad(g, ptr(dz), ptr(x), ptr(dweight), ptr(side.ws), side.ws.numel(), 0,
-                                side.stream.cuda_stream, xf=xf)
+                                side.stream.cuda_stream)
             grad_ready([weight])
     else:
         # final: no dgrad of this layer follows, so its finish may apply a registered SGD step
-        native().conv_wgrad(g, ptr(dz), ptr(x), ptr(dweight), ptr(ws), ws.numel(), 0, s, xf=xf,
+        native().conv_wgrad(g, ptr(dz), ptr(x), ptr(dweight), ptr(ws), ws.numel(), 0, s,
                             final=int(not need_dx))
         if weight is not None:
             grad_ready([weight])
@@ -344,7 +287,7 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=Non
         return link.result()
     dx = torch.empty_like(x)
     done = native().conv_dgrad(g, ptr(dz), ptr(spec.wc), ptr(dx), ptr(ws), ws.numel(), 0, s,
-                               bn=bnf, bna=bna, xf=xf)
+                               bn=bnf, bna=bna)
     if link is not None:
         link.seen += 1
         link.buf = dx
@@ -507,27 +450,7 @@ class _ConvBNActFn(torch.autograd.Function):
         sums_ready, spec.sums_ready = spec.sums_ready, False
         dz_done, spec.dz_fused = spec.dz_fused, None
         spec.fwd_z = None
-        xf = None
-        need_dx = ctx.needs_input_grad[0]
-        if (_common.BN_BWD_XF and dz_done is None and ctx.pool3_idx is None and not sums_ready
-                and native().bn_bwd_xf_ok(N, P, Q, K, int(spec.pool), int(ctx.has_res), 0)
-                and conv_xf_ok(spec, x, need_dx, ctx.in_link)):
-            # apply-free BatchNorm backward: reduce (+ dy_bn) and finalize here, dz computed by
-            # the conv backward GEMMs below from (z, dy_bn) — never stored (conv_igemm.hip XF)
-            dy = dy.contiguous()
-            # pooled / residual blocks: the reduce stores dy_bn (routed, masked; also the
-            # residual gradient); plain blocks: the GEMMs mask the raw dy themselves
-            plain = not spec.pool and not ctx.has_res
-            dyb = None if plain else torch.empty_like(z)
-            native().bn_bwd_xf(N, P, Q, K, int(spec.pool), int(spec.relu), spec.eps, ptr(z),
-                               ptr(residual), ptr(dy), ptr(sums), ptr(dyb), ptr(spec.xcoef),
-                               ptr(gg), ptr(gbt), ptr(spec.coef), stream_handle())
-            xf = (ptr(z), ptr(dy) if plain else ptr(dyb), ptr(spec.xcoef), K,
-                  int(plain and spec.relu))
-            dz = None
-            if dres is not None:
-                dres = dyb  # the residual branch's gradient IS dy_bn
-        elif dz_done is not None:
+        if dz_done is not None:
             # the next block's dgrad finish already ran this block's whole BN backward (dz,
             # dgamma, dbeta; conv_igemm.hip splitk_finish_bnbwd_kernel): dy was never written
             dz, zref = dz_done
@@ -556,8 +479,7 @@ class _ConvBNActFn(torch.autograd.Function):
         if (_common.BN_BWD_FUSE and prev is not None and ctx.prev_z is not None
                 and ctx.needs_input_grad[0] and ctx.in_link is None and spec.stride == 1
                 and not prev.residual and prev.K == spec.C and spec.C == spec.Cr
-                and bn_bwd_fuse_pays(x.shape[1], x.shape[2], prev.pool)
-                and not dgrad_tr_serves(spec, x, True, ctx.in_link)):
+                and bn_bwd_fuse_pays(x.shape[1], x.shape[2], prev.pool)):
             pz = ctx.prev_z
             bnf = (ptr(pz), ptr(prev.coef), ptr(prev.sums), int(prev.pool), int(prev.relu),
                    pz.shape[1], pz.shape[2])
@@ -567,7 +489,7 @@ class _ConvBNActFn(torch.autograd.Function):
                        ptr(ensure_grad(prev.bn.bias)))
         if bna is not None:
             dx, done = conv_backward(spec, x, dz, gw, ctx.needs_input_grad[0], ctx.in_link,
-                                     weight=weight, bnf=bnf, bna=bna, xf=xf)
+                                     weight=weight, bnf=bnf, bna=bna)
             if done:  # prev's backward skips its BN backward; dx was not written
                 prev.dz_fused = (dz_prev, ctx.prev_z)
             else:
@@ -576,7 +498,7 @@ class _ConvBNActFn(torch.autograd.Function):
             if bnf is not None:
                 prev.sums_ready = True
             dx = conv_backward(spec, x, dz, gw, ctx.needs_input_grad[0], ctx.in_link,
-                               weight=weight, bnf=bnf, xf=xf)
+                               weight=weight, bnf=bnf)
         ctx.prev_z = None
         return dx, None, None, None, None, dres, None, None, None
 

@@ -212,85 +212,3 @@ def test_vgg_forward_with_deferred_bn_matches_separate_passes(native_ext):
     a, b = out[True][1], out[False][1]
     cos = float(torch.dot(a, b) / (a.norm() * b.norm()))
     assert cos > 0.99, cos
-
-
-@pytest.mark.parametrize("N,C,H,K,cfg", [(8, 128, 8, 256, (64, 64, 1)), (4, 64, 16, 128, (128, 64, 1)),
-                                         (32, 512, 2, 512, (64, 64, 8)), (16, 256, 4, 512, (64, 128, 2))])
-def test_conv_dgrad_tr_matches_reference(native_ext, N, C, H, K, cfg):
-    """Backward-data through the tap-reuse kernel (flipped taps, transposed bf16 weight copy
-    [C][3][3][K]) against fp32 PyTorch conv2d's input gradient and the implicit-GEMM dgrad."""
-    from ddp_amd.ops.common import ptr, stream_handle, workspace
-    nat = native_ext
-    conv, spec, x, xn = _conv_setup(N, C, H, H, K, 3, 1, 1)
-    spec.wt = torch.empty(C, 3, 3, K, dtype=torch.bfloat16, device=DEV)
-    spec._packed_version = None
-    spec.maybe_pack()
-    dz = bf(torch.randn(N, K, H, H, device=DEV))
-    dzn = dz.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
-    ws = workspace(torch.device(DEV))
-    s = stream_handle()
-    g = spec.geom(N, H, H)
-    dx = torch.full((N, H, H, C), float("nan"), device=DEV, dtype=torch.bfloat16)
-    _force(nat, *cfg)
-    try:
-        assert nat.conv_dgrad_tr(g, ptr(dzn), ptr(spec.wt), ptr(dx), ptr(ws), ws.numel(), s)
-    finally:
-        _force(nat, 0, 0, 0)
-    dx2 = torch.empty_like(dx)
-    nat.conv_dgrad(g, ptr(dzn), ptr(spec.wc), ptr(dx2), ptr(ws), ws.numel(), 0, s)
-    torch.cuda.synchronize()
-    xr = x.clone().requires_grad_(True)
-    F.conv2d(xr, conv.weight, None, 1, 1).backward(dz)
-    ref = xr.grad.permute(0, 2, 3, 1)
-    assert not torch.isnan(dx.float()).any()
-    assert rel_err(dx, ref) < 1e-2
-    assert rel_err(dx, dx2) < 1e-2
-
-
-@pytest.mark.parametrize("xf", [None, "dyb", "mask"])
-@pytest.mark.parametrize("N,C,H,K,cfg", [(8, 128, 8, 256, (64, 64, 1)), (4, 64, 16, 128, (128, 64, 1)),
-                                         (32, 512, 2, 512, (64, 64, 8)), (16, 256, 4, 512, (64, 128, 2)),
-                                         (8, 256, 8, 256, (128, 128, 1))])
-def test_conv_dgrad_tr_wc_matches_reference(native_ext, N, C, H, K, cfg, xf):
-    """Backward-data through the tap-reuse kernel with the weights read k-major from the
-    FORWARD copy Wc (no transposed copy) — plain dz, or dz = xA * g + xB * z + xC computed in
-    the patch load from the BatchNorm's input z and output gradient g (xf "dyb"; "mask": g is
-    the raw block-output gradient and the ReLU mask scale * z + shift > 0 is applied in the
-    load) — against fp32 PyTorch conv2d's input gradient of the same dz."""
-    from ddp_amd.ops.common import ptr, stream_handle, workspace
-    nat = native_ext
-    conv, spec, x, xn = _conv_setup(N, C, H, H, K, 3, 1, 1)
-    ws = workspace(torch.device(DEV))
-    s = stream_handle()
-    g = spec.geom(N, H, H)
-    xf_args, dzn = None, None
-    if xf is None:
-        dz = bf(torch.randn(N, K, H, H, device=DEV))
-        dzn = dz.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
-    else:
-        mask = xf == "mask"
-        z = bf(torch.randn(N, H, H, K, device=DEV))
-        gr = bf(torch.randn(N, H, H, K, device=DEV))
-        rows = 5 if mask else 3
-        coef = torch.randn(rows, K, device=DEV) * 0.5
-        gm = gr
-        if mask:
-            gm = torch.where(z * coef[3] + coef[4] > 0, gr, torch.zeros_like(gr))
-        dz_nhwc = bf(torch.addcmul(torch.addcmul(coef[2], coef[1], z), coef[0], gm))
-        dz = dz_nhwc.permute(0, 3, 1, 2).contiguous()
-        table = coef.view(rows, K // 8, 8).permute(1, 0, 2).contiguous()  # [K/8][rows][8]
-        zb, gb = z.to(torch.bfloat16), gr.to(torch.bfloat16)
-        xf_args = (ptr(zb), ptr(gb), ptr(table), K, int(mask))
-    dx = torch.full((N, H, H, C), float("nan"), device=DEV, dtype=torch.bfloat16)
-    _force(nat, *cfg)
-    try:
-        assert nat.conv_dgrad_tr_wc(g, ptr(dzn), ptr(spec.wc), ptr(dx), ptr(ws), ws.numel(), s,
-                                    xf=xf_args)
-    finally:
-        _force(nat, 0, 0, 0)
-    torch.cuda.synchronize()
-    xr = x.clone().requires_grad_(True)
-    F.conv2d(xr, conv.weight, None, 1, 1).backward(dz)
-    ref = xr.grad.permute(0, 2, 3, 1)
-    assert not torch.isnan(dx.float()).any()
-    assert rel_err(dx, ref) < 1e-2

@@ -178,13 +178,11 @@ def _bn_ref(z, gamma, beta, eps, relu, pool, res=None):
                                             (8, 2048, 2, False, True), (16, 128, 16, True, False),
                                             (32, 256, 8, False, False), (16, 256, 8, False, True),
                                             (32, 64, 8, True, False)])
-@pytest.mark.parametrize("mode", ["split", "local", "xf"])
+@pytest.mark.parametrize("mode", ["split", "local"])
 def test_bn_act_fwd_bwd(native_ext, N, C, H, pool, res, mode):
     """split: reduce -> finalize -> apply launches; local: one block per 8 channels does the
     whole backward in one launch (bn_act_bwd_local_kernel; the shapes cover 1-8 items per
-    thread, pooled, plain and residual); xf: the apply-free backward (bn_act.hip ddp_bn_bwd_xf):
-    reduce + dy_bn + finalize into the [C/8][3][8] affine table the conv GEMMs consume — dz is
-    rebuilt here from (z, dy_bn, table) and must equal the reference's dz."""
+    thread, pooled, plain and residual)."""
     from ddp_amd.ops.common import ptr, stream_handle
     nat = native_ext
     nat.bn_bwd_local_set(64 if mode == "local" else 0)  # local: any shape it can hold
@@ -227,27 +225,10 @@ def _bn_case(nat, N, C, H, pool, res, mode, ptr, stream_handle):
     dg = torch.zeros(C, device=DEV)
     db = torch.zeros(C, device=DEV)
     dbias = torch.zeros(C, device=DEV)
-    if mode == "xf":
-        assert nat.bn_bwd_xf_ok(N, H, H, C, int(pool), int(res), 0)
-        plain = not pool and not res  # the consumer masks the raw dout: nothing stored
-        dyb = None if plain else torch.full_like(zn, float("nan"))
-        xcoef = torch.full((5 * C,), float("nan"), device=DEV)
-        nat.bn_bwd_xf(N, H, H, C, int(pool), 1, 1e-5, ptr(zn), ptr(rn), ptr(doutn), ptr(sums),
-                      ptr(dyb), ptr(xcoef), ptr(dg), ptr(db), ptr(coef), s)
-        torch.cuda.synchronize()
-        rows = 5 if plain else 3
-        t = xcoef[:rows * C].view(C // 8, rows, 8)
-        A, B, Cc = (t[:, k, :].reshape(C) for k in range(3))
-        if plain:  # the GEMMs' mask: scale * z + shift > 0 (rows 3 / 4 of the table)
-            sc, sh = t[:, 3, :].reshape(C), t[:, 4, :].reshape(C)
-            dyb = torch.where(zn.float() * sc + sh > 0, doutn.float(), 0.0)
-        dz = (A * dyb.float() + B * zn.float() + Cc).to(torch.bfloat16)
-        dres = dyb if res else None
-    else:
-        nat.bn_act_bwd(N, H, H, C, int(pool), 1, 1e-5, ptr(zn), ptr(rn), ptr(stats), ptr(gamma),
-                       ptr(beta), ptr(doutn), ptr(sums), ptr(dz), ptr(dres), ptr(dg), ptr(db),
-                       ptr(dbias), s, ptr(coef))
-        torch.cuda.synchronize()
+    nat.bn_act_bwd(N, H, H, C, int(pool), 1, 1e-5, ptr(zn), ptr(rn), ptr(stats), ptr(gamma),
+                   ptr(beta), ptr(doutn), ptr(sums), ptr(dz), ptr(dres), ptr(dg), ptr(db),
+                   ptr(dbias), s, ptr(coef))
+    torch.cuda.synchronize()
     assert rel_err(dz.permute(0, 3, 1, 2), zr.grad) < 2e-2
     assert rel_err(dg, gr.grad) < 1e-2
     assert rel_err(db, br.grad) < 1e-2
@@ -673,16 +654,14 @@ def test_conv_every_tile(native_ext, case, tile):
 @pytest.mark.parametrize("case", [(32, 64, 16, 128, True, False), (8, 128, 8, 256, False, False),
                                   (32, 256, 4, 512, True, False), (4, 64, 32, 64, True, False),
                                   (8, 8, 32, 64, True, True), (4, 64, 14, 128, False, False)])
-def test_conv_bwd_xf(native_ext, case, pair_mode):
-    """Apply-free BatchNorm backward feeding the conv backward GEMMs (conv_igemm.hip XF): the
-    dgrad / wgrad A operand is dz = A dy_bn + B z + C computed in LDS from the BN input z and the
-    routed gradient dy_bn (bn_act.hip ddp_bn_bwd_xf). dx and dW must match fp32 PyTorch through
-    conv -> BN -> ReLU (-> 2x2 pool), and the path with a materialised dz (reduce -> finalize
-    -> apply -> GEMMs), separately launched (pair mode 0) and as the grouped backward pair (3).
-    Covers pooled / unpooled BN, the padded input layer (C = 8: wgrad only) and a 14x14 image
-    (partial tiles). Reference hot path: /root/reference/part1/model.py:18-27."""
+def test_conv_bwd_after_bn(native_ext, case, pair_mode):
+    """The conv backward GEMMs on the dz of a training-mode BatchNorm backward (reduce ->
+    finalize -> apply): dx and dW must match fp32 PyTorch through conv -> BN -> ReLU (-> 2x2
+    pool), separately launched (pair mode 0) and as the grouped backward pair (3). Covers pooled
+    / unpooled BN, the padded input layer (C = 8: wgrad only) and a 14x14 image (partial
+    tiles). Reference hot path: /root/reference/part1/model.py:18-27."""
     from ddp_amd.ops.common import ptr, stream_handle
-    from ddp_amd.ops.layers import conv_backward, conv_xf_ok
+    from ddp_amd.ops.layers import conv_backward
     nat = native_ext
     N, Cin, H, K, pool, first = case
     Creal = 3 if first else Cin
@@ -712,46 +691,23 @@ def test_conv_bwd_xf(native_ext, case, pair_mode):
     F.conv2d(xr, wr, None, 1, 1).backward(zr.grad)
     nat.bn_bwd_local_set(0)
     nat.conv_pair_mode(pair_mode)
-    res = {}
     try:
-        assert nat.bn_bwd_xf_ok(N, H, H, K, int(pool), 0, 0)
-        assert conv_xf_ok(spec, xn, need_dx)
-        for use_xf in (False, True):
-            sums = torch.zeros(16 * 2 * K, device=DEV)
-            dg = torch.zeros(K, device=DEV)
-            db = torch.zeros(K, device=DEV)
-            dw = torch.zeros_like(conv.weight, memory_format=torch.channels_last)
-            if use_xf:
-                # unpooled: the GEMMs apply the ReLU mask to the raw dout (nothing stored)
-                dyb = torch.full_like(zn, float("nan")) if pool else None
-                xcoef = torch.full((5 * K,), float("nan"), device=DEV)
-                nat.bn_bwd_xf(N, H, H, K, int(pool), 1, 1e-5, ptr(zn), 0, ptr(doutn), ptr(sums),
-                              ptr(dyb), ptr(xcoef), ptr(dg), ptr(db), ptr(coef), s)
-                g = dyb if pool else doutn
-                dx = conv_backward(spec, xn, None, dw, need_dx,
-                                   xf=(ptr(zn), ptr(g), ptr(xcoef), K, int(not pool)))
-            else:
-                dz = torch.empty_like(zn)
-                nat.bn_act_bwd(N, H, H, K, int(pool), 1, 1e-5, ptr(zn), 0, ptr(stats), ptr(gamma),
-                               ptr(beta), ptr(doutn), ptr(sums), ptr(dz), 0, ptr(dg), ptr(db), 0,
-                               s, ptr(coef))
-                dx = conv_backward(spec, xn, dz, dw, need_dx)
-            torch.cuda.synchronize()
-            res[use_xf] = (dx, dw, dg, db)
+        sums = torch.zeros(16 * 2 * K, device=DEV)
+        dg = torch.zeros(K, device=DEV)
+        db = torch.zeros(K, device=DEV)
+        dw = torch.zeros_like(conv.weight, memory_format=torch.channels_last)
+        dz = torch.empty_like(zn)
+        nat.bn_act_bwd(N, H, H, K, int(pool), 1, 1e-5, ptr(zn), 0, ptr(stats), ptr(gamma),
+                       ptr(beta), ptr(doutn), ptr(sums), ptr(dz), 0, ptr(dg), ptr(db), 0,
+                       s, ptr(coef))
+        dx = conv_backward(spec, xn, dz, dw, need_dx)
+        torch.cuda.synchronize()
     finally:
         nat.bn_bwd_local_set(8)
         nat.conv_pair_mode(3)
-    for use_xf in (False, True):
-        dx, dw, dg, db = res[use_xf]
-        assert rel_err(dw, wr.grad) < 2e-2, (use_xf, rel_err(dw, wr.grad))
-        if need_dx:
-            assert rel_err(dx.permute(0, 3, 1, 2), xr.grad) < 2e-2, (use_xf,)
-    # XF vs the materialised dz: the same bf16 dz up to fp32 rounding of the affine form
-    assert rel_err(res[True][1], res[False][1]) < 1e-2
+    assert rel_err(dw, wr.grad) < 2e-2, rel_err(dw, wr.grad)
     if need_dx:
-        assert rel_err(res[True][0], res[False][0]) < 1e-2
-    assert torch.allclose(res[True][2], res[False][2], rtol=1e-4, atol=1e-4)
-    assert torch.allclose(res[True][3], res[False][3], rtol=1e-4, atol=1e-4)
+        assert rel_err(dx.permute(0, 3, 1, 2), xr.grad) < 2e-2
 
 
 @pytest.mark.parametrize("path", ["pair", "separate", "layer0"])

@@ -51,68 +51,10 @@ def graph_time(fn, n=20, reps=5):
     return statistics.median(ts)
 
 
-def sweep_dgrad(a, nat, dev, ws, entries):
-    """Backward of each layer: the trained path (backward pair or dgrad + wgrad launches of the
-    implicit-GEMM kernel) vs the weight gradient alone + the tap-reuse backward-data kernel."""
-    import torch
-    from ddp_amd.ops.common import ptr, stream_handle
-    from ddp_amd.ops.layers import ConvBNActSpec, conv_backward
-    for B in a.batch:
-        for C, K, H in LAYERS:
-            conv = torch.nn.Conv2d(C, K, 3, 1, 1).to(dev)
-            conv.weight.data = conv.weight.data.contiguous(memory_format=torch.channels_last)
-            spec = ConvBNActSpec(conv, None)
-            wt = torch.empty(C, 3, 3, K, dtype=torch.bfloat16, device=dev)
-            spec.wt = wt
-            spec.maybe_pack()
-            x = torch.randn(B, H, H, C, device=dev).to(torch.bfloat16)
-            dz = torch.randn(B, H, H, K, device=dev).to(torch.bfloat16)
-            dw = torch.zeros_like(conv.weight)
-            dx = torch.empty_like(x)
-            g = spec.geom(B, H, H, 1)
-            spec.wt = None  # the trained path as shipped
-
-            def trained():
-                conv_backward(spec, x, dz, dw, True)
-
-            def wgrad():
-                nat.conv_wgrad(g, ptr(dz), ptr(x), ptr(dw), ptr(ws), ws.numel(), 0, stream_handle())
-
-            def dg_tr():
-                if not nat.conv_dgrad_tr(g, ptr(dz), ptr(wt), ptr(dx), ptr(ws), ws.numel(),
-                                         stream_handle()):
-                    raise RuntimeError("not served")
-
-            base, tw = graph_time(trained), graph_time(wgrad)
-            best = (base, (0, 0, 0, 0))
-            res = {}
-            for bm, bn, s, n in CANDS:
-                if C % bn or s > K // 64 or n != 3:
-                    continue
-                nat.conv_tr_set(3, 0, 0, 0, 0, bm, bn, s, n)
-                try:
-                    t = graph_time(dg_tr) + tw
-                except RuntimeError:
-                    continue
-                finally:
-                    nat.conv_tr_set(3, 0, 0, 0, 0, 0, 0, 0, 0)
-                res[f"{bm}x{bn}s{s}"] = round(t, 2)
-                if t < best[0] * (1.0 - a.margin):
-                    best = (t, (bm, bn, s, n))
-            ent = {"M": B * H * H, "K": C, "C": K, "H": H, "bm": best[1][0], "bn": best[1][1],
-                   "splits": best[1][2], "stages": best[1][3], "us": round(best[0], 2),
-                   "trained_us": round(base, 2), "wgrad_us": round(tw, 2),
-                   "shape": f"vgg11 N{B} {C}->{K} {H}x{H} backward"}
-            entries.append(ent)
-            print(json.dumps(dict(ent, candidates=res)), flush=True)
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, nargs="+", default=[256, 128, 64, 32])
     ap.add_argument("--write", action="store_true")
-    ap.add_argument("--dgrad", action="store_true",
-                    help="sweep the backward-data kernel instead (tr_dgrad_entries)")
     ap.add_argument("--out", default=None,
                     help="write the merged table here instead of over ops/conv_tuning.json")
     ap.add_argument("--model", default="vgg11", choices=["vgg11", "resnet50"],
@@ -128,17 +70,6 @@ def main():
     dev = torch.device("cuda", 0)
     ws = workspace(dev)
     entries = []
-    if a.dgrad:
-        sweep_dgrad(a, nat, dev, ws, entries)
-        if a.write:
-            path = os.environ.get("DDP_AMD_CONV_TUNING_FILE", TUNING_FILE)
-            with open(path) as f:
-                table = json.load(f)
-            table["tr_dgrad_entries"] = sorted(entries, key=lambda e: (e["H"], e["K"], e["M"]))
-            with open(a.out or path, "w") as f:
-                json.dump(table, f, indent=1)
-            print(f"wrote {len(entries)} backward-data entries to {a.out or path}")
-        return
     for B in a.batch:
         for C, K, H in (RESNET_LAYERS if a.model == "resnet50" else LAYERS):
             conv = torch.nn.Conv2d(C, K, 3, 1, 1).to(dev)
