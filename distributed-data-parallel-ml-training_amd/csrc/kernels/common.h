@@ -84,17 +84,6 @@ __device__ __forceinline__ float wave_max(float v) {
   return fmaxf(fmaxf(lane_f(v, 0), lane_f(v, 16)), fmaxf(lane_f(v, 32), lane_f(v, 48)));
 }
 
-// GEMM tile order of the conv kernels (DDP_AMD_TILE_ORDER=n: row tiles fastest, so the run of
-// consecutive tiles that xcd_remap gives one XCD shares a weight slice in that XCD's L2; default
-// m: column tiles fastest). Host side, read once.
-inline int tile_order_n() {
-  static const int v = [] {
-    const char* e = std::getenv("DDP_AMD_TILE_ORDER");
-    return (e && e[0] == 'n') ? 1 : 0;
-  }();
-  return v;
-}
-
 // Bijective XCD-aware block remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
 // consecutive logical tiles land on the same XCD (shared L2) instead of round-robin.
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {

@@ -98,8 +98,6 @@ struct Args {
   int imgp, plane, zslot;    // patch pitch per image, pixels per chunk plane, zero pixel
   int x_bytes, w_bytes;
   int tiles_m, tiles_n;
-  int nmajor;                // tile order: 0 = column tiles fastest, 1 = row tiles fastest (each
-                             // XCD's run of consecutive tiles then shares one weight slice)
   int abuf_elems;            // bf16 elements of one patch buffer (16-B multiple)
   // fused input (template IN = 1: BN + ReLU, IN = 2: BN + ReLU + 2x2/s2 max-pool): the conv
   // input x = [pool](relu(scale * zin + shift)) is computed while the patch is loaded; zin is
@@ -148,8 +146,8 @@ void conv_tr_fwd_kernel(Args a) {
   const int item = blockIdx.x;
   const int sp = item / tiles;
   const int tile = xcd_remap(item - sp * tiles, tiles);
-  const int tm = a.nmajor ? tile % a.tiles_m : tile / a.tiles_n;
-  const int tn = a.nmajor ? tile / a.tiles_m : tile - tm * a.tiles_n;
+  const int tm = tile / a.tiles_n;  // column tiles fastest (as conv_igemm.hip)
+  const int tn = tile - tm * a.tiles_n;
   const int row0 = tm * BM, col0 = tn * BN;
   const int cb0 = sp * a.cbps, cb1 = min(ncb, cb0 + a.cbps);
   const int nsteps = (cb1 - cb0) * 9;
@@ -733,7 +731,6 @@ extern "C" int ddp_conv_fwd_tr(const ConvGeom* g, const void* x, const void* wc,
   a.abuf_elems = geo.abuf;
   a.tiles_m = (int)(M / c.bm);
   a.tiles_n = K / c.bn;
-  a.nmajor = tile_order_n();
   if (in) {
     a.zin = (const unsigned short*)in->z;
     a.in_stats = in->stats;
