@@ -175,9 +175,10 @@ PYBIND11_MODULE(_native, m) {
   });
   m.def("l0_fwd", [](py::tuple g, uintptr_t x, uintptr_t wc, uintptr_t bias, float eps, int relu,
                      uintptr_t stats, uintptr_t gamma, uintptr_t beta, uintptr_t coef, uintptr_t y,
-                     uintptr_t code, uintptr_t st) {
+                     uintptr_t code, uintptr_t zw, uintptr_t st) {
     auto c = geom(g);
     ddp_amd::L0Io io{};
+    io.zw = P<void>(zw);
     io.x = P<void>(x); io.wc = P<void>(wc); io.bias = P<float>(bias); io.eps = eps; io.relu = relu;
     io.stats = P<float>(stats); io.gamma = P<float>(gamma); io.beta = P<float>(beta);
     io.coef = P<float>(coef); io.y = P<void>(y); io.code = P<void>(code);
@@ -185,12 +186,13 @@ PYBIND11_MODULE(_native, m) {
   });
   m.def("l0_bwd", [](py::tuple g, uintptr_t x, uintptr_t wc, uintptr_t bias, float eps, int relu,
                      uintptr_t coef, uintptr_t dy, uintptr_t sums, uintptr_t dz, uintptr_t dgamma,
-                     uintptr_t dbeta, uintptr_t code, uintptr_t st) {
+                     uintptr_t dbeta, uintptr_t code, uintptr_t zw, uintptr_t st) {
     auto c = geom(g);
     ddp_amd::L0Io io{};
     io.x = P<void>(x); io.wc = P<void>(wc); io.bias = P<float>(bias); io.eps = eps; io.relu = relu;
     io.coef = P<float>(coef); io.dy = P<void>(dy); io.sums = P<float>(sums); io.dz = P<void>(dz);
     io.dgamma = P<float>(dgamma); io.dbeta = P<float>(dbeta); io.code = P<void>(code);
+    io.zw = P<void>(zw);
     check(ddp_l0_bwd(&c, &io, S(st)), "l0_bwd");
   });
   m.def("conv_tr_would_serve", [](py::tuple g, size_t ws_elems, int in_mode) {
@@ -319,6 +321,11 @@ PYBIND11_MODULE(_native, m) {
     }
     v.resize(n);
     return v;
+  });
+  m.def("conv_dense2x2_set", [](int on) { ddp_conv_dense2x2_set(on); });
+  m.def("conv_dense2x2_ok", [](py::tuple g) {
+    auto c = geom(g);
+    return ddp_conv_dense2x2_ok(&c) != 0;
   });
   m.def("conv_pair_mode", [](int mode, int items) { ddp_conv_pair_mode(mode, items); },
         py::arg("mode"), py::arg("items") = 0);

@@ -129,6 +129,7 @@ struct L0Io {
   float* sums;          // [kStatRep][2][64] (zeroed per step)
   void* dz;             // [N][H][W][64] bf16 (backward output)
   void* code;           // [N][H/2][W/2][64] uint8: per pooled value, where its gradient goes
+  void* zw;             // [N][H/2][W/2][64] bf16: z of that pixel (forward -> backward sums)
   float* dgamma;
   float* dbeta;
 };
@@ -242,6 +243,10 @@ int ddp_conv_bwd_pair(const ddp_amd::ConvGeom* g, const void* dy, const void* wc
                       const ddp_amd::BnBwdFuse* bn, const ddp_amd::BnBwdApply* ba, int* bn_done,
                       hipStream_t st);
 void ddp_conv_tune_set(int mode, int M, int N, int K, int tile, int splits, int stages);
+// dense 2x2 form of 3x3 / s1 / p1 convs over 2x2 images (conv_igemm.hip ConvArgs::d2x2): ok =
+// this geometry takes it (FWD and DGRAD), set = switch it on / off (DDP_AMD_DENSE2X2)
+int ddp_conv_dense2x2_ok(const ddp_amd::ConvGeom* g);
+void ddp_conv_dense2x2_set(int on);
 void ddp_conv_tune_clear();
 void ddp_conv_force_tile(int tile_plus_one, int stages);
 int ddp_pack_conv_weights(const ddp_amd::PackDesc* descs, int n, hipStream_t st);

@@ -108,6 +108,16 @@ struct ConvArgs {
   // FWD / DGRAD bf16 output through the LDS-staged epilogue (conv_igemm_body): full 16-B
   // stores of whole tile rows instead of 8-B fragments of 16 rows per instruction
   int epi_stage;
+  // Dense 2x2 form of a 3x3 / s1 / p1 conv over 2x2 images (FWD, DGRAD; host: dense2x2_args):
+  // every output pixel (p, q) sees every input pixel (h, w) through tap (h - p + 1, w - q + 1),
+  // so the conv is ONE GEMM over whole images — FWD: [N] x [(h, w, c) = 4C] x [(p, q, k) = 4K],
+  // DGRAD the transpose — with a block-structured weight W2[(p,q,k)][(h,w,c)] = Wc[k][tap][c]
+  // that is never materialised: the B offsets pick the tap per (column tile, k-step). It skips
+  // the 5 of 9 taps per pixel that hit padding (2.25x fewer MFMAs than the implicit GEMM), and
+  // its NHWC output bytes are the standard ones (the split-K finish runs on the 3x3 view).
+  int d2x2;                  // 1: g is the dense 1x1 view (N, 1, 1, 4C -> 4K), B = Wc [K][9][C]
+  int d2C, d2K;              // the 3x3 conv's C and K
+  int no_finish;             // host: launch the GEMM only (the caller runs the finish)
 };
 
 // ------------------------------------------------------------------ operand gathers
@@ -276,6 +286,7 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
   KInfo xk;              // WGRAD: (r,s,c) of this thread's B' column group
   int xk_same = 0;       // WGRAD "same" conv: byte offset of tap (r,s) channel c relative to m
   int row0 = 0, col0 = 0, zsplit = 0, ks_begin = 0, ks_end = 0, cur_tile = 0;
+  int d2pos = 0;         // dense 2x2: the column tile's output pixel (FWD) / input pixel (DGRAD)
   const bool phase = MODE == MODE_DGRAD && args.phase;
   const int Sdec = phase ? args.St : gg.S;  // taps per kernel row in the reduction index
   const int cdim = MODE == MODE_FWD ? gg.C : gg.K;
@@ -315,11 +326,31 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
                                          : ri.base + (ri.h0 * gg.Q + ri.w0) * gg.K;
         a_off[i] = 2 * (e + (fast ? lcA * 8 : 0));
       }
-      if (MODE == MODE_FWD) {
+      if (MODE == MODE_FWD && args.d2x2) {
+        // dense 2x2: column (p, q, k) reads Wc row k; the tap follows (p, q) and the k-step
+        d2pos = col0 / args.d2K;
+#pragma unroll
+        for (int i = 0; i < CB; ++i) {
+          const int col = col0 + (tid >> 3) + 32 * i;
+          b_off[i] = col < args.Ng ? 2 * ((col - d2pos * args.d2K) * 9 * args.d2C + lcB * 8)
+                                   : (int)kOOB;
+        }
+      } else if (MODE == MODE_FWD) {
 #pragma unroll
         for (int i = 0; i < CB; ++i) {
           const int col = col0 + (tid >> 3) + 32 * i;
           b_off[i] = col < args.Ng ? 2 * (col * args.Kg + lcB * 8) : (int)kOOB;
+        }
+      } else if (args.d2x2) {
+        // dense 2x2 DGRAD: column (h, w, c) = channel c of Wc rows k (the k-step's reduction
+        // rows (p, q, k)), tap from (h, w) and the k-step's (p, q)
+        d2pos = col0 / args.d2C;
+#pragma unroll
+        for (int i = 0; i < CB; ++i) {
+          const int col = col0 + (lcB ^ swz_row_step<BN>(i)) * 8;
+          b_off[i] = col < args.Ng ? 2 * (((tid + i * 256) / (BN / 8)) * 9 * args.d2C + col -
+                                          d2pos * args.d2C)
+                                   : (int)kOOB;
         }
       } else {  // DGRAD: row m of the k-step = output channel kc + m, columns = input channels
 #pragma unroll
@@ -375,7 +406,15 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
           dma_buf(rsA, ok ? a_off[i] + tap : (int)kOOB, As + (wid * 64 + 256 * i) * 8);
         }
         int boff;
-        if (MODE == MODE_FWD) {
+        if (args.d2x2) {
+          // FWD: k-step = input pixel hw, channels c0..; DGRAD: k-step = output pixel pq,
+          // channels k0..; the column tile fixed the other pixel (d2pos)
+          const int pix = MODE == MODE_FWD ? kc / args.d2C : kc / args.d2K;
+          const int ch = kc - pix * (MODE == MODE_FWD ? args.d2C : args.d2K);
+          const int pq = MODE == MODE_FWD ? d2pos : pix, hw = MODE == MODE_FWD ? pix : d2pos;
+          const int tap = ((hw >> 1) - (pq >> 1) + 1) * 3 + ((hw & 1) - (pq & 1) + 1);
+          boff = MODE == MODE_FWD ? 2 * (tap * args.d2C + ch) : 2 * ((ch * 9 + tap) * args.d2C);
+        } else if (MODE == MODE_FWD) {
           boff = 2 * k0;
         } else {  // Wc[kc + m][r][s][c]
           const int rr = phase ? args.r0 + gg.stride * kr : kr, ss = phase ? args.s0 + gg.stride * ks_ : ks_;
@@ -2046,7 +2085,7 @@ static void launch_cfg(ConvArgs& a, int splits, hipStream_t st, int nst_req = 0)
   }
   launch_gemm<MODE, BM, BN, 2>(a, items, st);
 launched:
-  launch_finish<MODE>(a, st);
+  if (!a.no_finish) launch_finish<MODE>(a, st);
 }
 
 // Measured tile / split-K choices per GEMM problem (tools/conv_tune.py sweeps every candidate
@@ -2167,10 +2206,97 @@ extern "C" void ddp_conv_force_tile(int tile_plus_one, int stages) {
   g_force_stages = stages;
 }
 
+// ---- dense 2x2 form of the 3x3 convs over 2x2 images (ConvArgs::d2x2; VGG-11's last two
+// layers): DDP_AMD_DENSE2X2=0 / ddp_conv_dense2x2_set(0) restores the implicit GEMM
+static int g_dense2x2 = -1;
+static bool dense2x2_on() {
+  if (g_dense2x2 < 0) {
+    const char* e = std::getenv("DDP_AMD_DENSE2X2");
+    g_dense2x2 = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_dense2x2 != 0;
+}
+extern "C" void ddp_conv_dense2x2_set(int on) { g_dense2x2 = on ? 1 : 0; }
+extern "C" int ddp_conv_dense2x2_ok(const ConvGeom* g) {
+  return dense2x2_on() && g->R == 3 && g->S == 3 && g->stride == 1 && g->pad == 1 &&
+         g->H == 2 && g->W == 2 && g->P == 2 && g->Q == 2 && g->C % 64 == 0 && g->K % 64 == 0 &&
+         g->Creal == g->C && fits_buffer((size_t)g->K * 9 * g->C) &&
+         fits_buffer((size_t)g->N * 4 * std::max(g->C, g->K));
+}
+// the dense GEMM's operands: A = the NHWC activation of whole 2x2 images (x for FWD, dy for
+// DGRAD) read as [N][4 * channels], B = Wc [K][9][C] through ConvArgs::d2x2 addressing
+static void dense2x2_args(ConvArgs& a, const ConvGeom* g, int mode) {
+  a.g = *g;
+  a.g.H = a.g.W = a.g.P = a.g.Q = 1;
+  a.g.R = a.g.S = 1;
+  a.g.pad = 0;
+  a.g.C = a.g.Creal = 4 * g->C;
+  a.g.K = 4 * g->K;
+  a.Mg = g->N;
+  a.Ng = mode == MODE_FWD ? 4 * g->K : 4 * g->C;
+  a.Kg = mode == MODE_FWD ? 4 * g->C : 4 * g->K;
+  a.d2x2 = 1;
+  a.d2C = g->C;
+  a.d2K = g->K;
+  a.a_bytes = (int)(2 * (size_t)g->N * a.Kg);
+  a.b_bytes = (int)(2 * (size_t)g->K * 9 * g->C);
+}
+// split-K factor of a dense problem that must end in a finish (>= 2; 0 = does not fit ws)
+static int dense2x2_splits(const ConvArgs& a, size_t ws_elems) {
+  const int tiles = ((a.Mg + 63) / 64) * ((a.Ng + 63) / 64), ksteps = a.Kg / 64;
+  int sp = std::max(2, std::min((512 + tiles - 1) / tiles, ksteps / 4));
+  const size_t slab = (size_t)a.Mg * a.Ng;
+  if ((size_t)sp * slab > ws_elems) sp = (int)(ws_elems / slab);
+  return sp >= 2 ? sp : 0;
+}
+// the 3x3 view of a dense problem for its split-K finish: the slab bytes [split][N][4 x ch]
+// are [split][N * 4][ch] (NHWC), so the standard finishes (bias, statistics, BatchNorm) apply
+static ConvArgs finish_view(const ConvArgs& a, const ConvGeom* g, int mode) {
+  if (!a.d2x2) return a;
+  ConvArgs f = a;
+  f.g = *g;
+  f.d2x2 = 0;
+  f.Mg = g->N * g->P * g->Q;
+  f.Ng = mode == MODE_FWD ? g->K : g->C;
+  f.Kg = 9 * (mode == MODE_FWD ? g->C : g->K);
+  return f;
+}
+
+// FWD through the dense 2x2 GEMM + the standard finish; -1 = not served
+static int conv_fwd_dense(const ConvGeom* g, const void* x, const void* wc, const float* bias,
+                          void* y, float* stats, float* ws, size_t ws_elems, const BnFwdFuse* bn,
+                          int* bn_done, hipStream_t st) {
+  if (!ddp_conv_dense2x2_ok(g) || ws == nullptr) return -1;
+  ConvArgs a{};
+  dense2x2_args(a, g, MODE_FWD);
+  a.a = (const unsigned short*)x;
+  a.b = (const unsigned short*)wc;
+  a.out = (unsigned short*)y;
+  a.ws = ws;
+  a.splits = dense2x2_splits(a, ws_elems);
+  if (a.splits < 2) return -1;
+  a.no_finish = 1;
+  launch_mode<MODE_FWD>(a, ws_elems, st);
+  ConvArgs f = finish_view(a, g, MODE_FWD);
+  f.no_finish = 0;
+  f.bias = bias;
+  f.stats = stats;
+  if (bn && f.Mg <= kBnFwdFuseMaxRows) {
+    f.bnfwd = bn;
+    f.bnfwd_done = bn_done;
+  }
+  launch_finish<MODE_FWD>(f, st);
+  return (int)hipGetLastError();
+}
+
 extern "C" int ddp_conv_fwd(const ConvGeom* g, const void* x, const void* wc, const float* bias,
                             void* y, float* stats, float* ws, size_t ws_elems, int splits,
                             hipStream_t st) {
   if (g->C % 8 || g->K % 8) return -1;
+  {
+    const int r = conv_fwd_dense(g, x, wc, bias, y, stats, ws, ws_elems, nullptr, nullptr, st);
+    if (r >= 0) return r;
+  }
   ConvArgs a{};
   a.g = *g;
   a.a = (const unsigned short*)x;
@@ -2237,6 +2363,13 @@ extern "C" int ddp_conv_fwd_bn(const ConvGeom* g, const void* x, const void* wc,
     return !(e && e[0] == '0');
   }();
   if (g->C % 8 || g->K % 8) return -1;
+  int done = 0;
+  {
+    const int r = conv_fwd_dense(g, x, wc, bias, z, stats, ws, ws_elems, enabled ? bn : nullptr,
+                                 &done, st);
+    if (r > 0) return 2 + r;
+    if (r == 0) return done;
+  }
   ConvArgs a{};
   a.g = *g;
   a.a = (const unsigned short*)x;
@@ -2252,7 +2385,6 @@ extern "C" int ddp_conv_fwd_bn(const ConvGeom* g, const void* x, const void* wc,
   if (!fits_buffer(xa) || !fits_buffer(wb) || !fits_buffer((size_t)a.Mg * a.Ng)) return -2;
   a.a_bytes = (int)(2 * xa);
   a.b_bytes = (int)(2 * wb);
-  int done = 0;
   if (enabled && bn && a.Mg <= kBnFwdFuseMaxRows) {
     a.bnfwd = bn;
     a.bnfwd_done = &done;
@@ -2297,6 +2429,33 @@ static int conv_dgrad_impl(const ConvGeom* g, const void* dy, const void* wc, vo
   if (bn_done) *bn_done = 0;
   if (g->C % 8 || g->K % 8) return -1;
   if (bn && (accumulate || g->stride != 1)) return -3;  // fused BN sums: plain stride-1 dgrad only
+  if (!accumulate && ddp_conv_dense2x2_ok(g) && ws != nullptr) {
+    // dense 2x2 GEMM; the preceding block's BatchNorm-backward sums (bn) and the split-K
+    // reduction run in the standard finish of the 3x3 view
+    ConvArgs d{};
+    dense2x2_args(d, g, MODE_DGRAD);
+    d.a = (const unsigned short*)dy;
+    d.b = (const unsigned short*)wc;
+    d.out = (unsigned short*)dx;
+    d.ws = ws;
+    d.splits = bn ? dense2x2_splits(d, ws_elems) : splits;
+    if (!bn || d.splits >= 2) {
+      d.no_finish = 1;
+      launch_mode<MODE_DGRAD>(d, ws_elems, st);
+      if (d.splits > 1) {
+        ConvArgs f = finish_view(d, g, MODE_DGRAD);
+        f.no_finish = 0;
+        if (bn) {
+          f.has_bnf = 1;
+          f.bnf = *bn;
+          f.bnapply = ba;
+          f.bnapply_done = bn_done;
+        }
+        launch_finish<MODE_DGRAD>(f, st);
+      }
+      return (int)hipGetLastError();
+    }
+  }
   ConvArgs a{};
   a.accumulate = accumulate;
   if (bn) {
@@ -2486,6 +2645,12 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
       sw = it->second.stages;
     }
   }
+  // dense 2x2 DGRAD (the WGRAD half stays 3x3 and keeps the measured entry's split, so its
+  // finish still takes the layer's SGD step): the DGRAD split from the cost model
+  if (ddp_conv_dense2x2_ok(g)) {
+    dense2x2_args(d, g, MODE_DGRAD);
+    if (tuned) tile_cost(64, 64, d, ws_elems, &sd);
+  }
   bool both64 = tuned;
   if (!tuned) {
     int spd[kNumTiles], bd, nd, spw[kNumTiles], bw, nw;
@@ -2502,6 +2667,8 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
       sw = spw[3];
     }
   }
+  // a dense DGRAD reduces the BatchNorm-backward sums in the finish of its 3x3 view
+  if (d.d2x2 && d.has_bnf) sd = std::max(sd, 2);
   // the slab workspace is split between the two problems
   const int itd = prepare_cfg<MODE_DGRAD, 64, 64>(d, std::max(1, sd));
   size_t dneed = needs_finish(MODE_DGRAD, d) ? (size_t)d.splits * d.Mg * d.Ng : 0;
@@ -2511,6 +2678,7 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
   const size_t wneed = needs_finish(MODE_WGRAD, w) ? (size_t)w.splits * w.Mg * w.Ng : 0;
   if (dneed + wneed > ws_elems) return separate();
   if (g_pair_mode == 3 && !both64 && itd + itw > g_pair_items) return separate();
+  if (d.d2x2 && d.has_bnf && d.splits < 2) return separate();
   const bool bnf1 = d.has_bnf && d.splits <= 1;
   if (bnf1) {  } else if (bnf1) {
     hipLaunchKernelGGL((conv_bwd_pair_kernel<64, 64, 3, 1>), dim3(itd + itw), dim3(256), 0, st,
@@ -2524,21 +2692,22 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
     Allow() { g_sgd_allow = true; }
     ~Allow() { g_sgd_allow = false; }
   } allow;
-  if (fd && fw && w.g.wkrsc && bnbwd_fusable(d)) {
+  const ConvArgs dv = finish_view(d, g, MODE_DGRAD);  // (d itself unless dense)
+  if (fd && fw && w.g.wkrsc && bnbwd_fusable(dv)) {
     const WgFinishArgs wa = wg_finish_args(w);
-    launch_finish_bnbwd(d, st, &wa);
+    launch_finish_bnbwd(dv, st, &wa);
   } else if (fd && fw && w.g.wkrsc) {
     int bx, ch;
-    dg_finish_grid(d, &bx, &ch);
-    const FinishArgs fa = finish_args(MODE_DGRAD, d);
+    dg_finish_grid(dv, &bx, &ch);
+    const FinishArgs fa = finish_args(MODE_DGRAD, dv);
     const WgFinishArgs wa = wg_finish_args(w);
     const dim3 grid(bx * ch + wa.gx * wa.gy);
-    if (d.has_bnf)
+    if (dv.has_bnf)
       hipLaunchKernelGGL(bwd_pair_finish_kernel<true>, grid, dim3(256), 0, st, fa, bx, ch, wa);
     else
       hipLaunchKernelGGL(bwd_pair_finish_kernel<false>, grid, dim3(256), 0, st, fa, bx, ch, wa);
   } else {
-    launch_finish<MODE_DGRAD>(d, st);
+    launch_finish<MODE_DGRAD>(dv, st);
     launch_finish<MODE_WGRAD>(w, st);
   }
   return (int)hipGetLastError();

@@ -59,6 +59,8 @@ struct Args {
                              // gradient, 4 = none (ReLU cut), 0xFF = NaN window; lane-major
                              // [window][g][j][v] bytes, written by the forward, read by both
                              // backward passes
+  unsigned short* zw;        // [N][H/2][W/2][64] bf16: z of the pixel code points to (forward;
+                             // the backward sums need nothing else of the window)
   float* dgamma;             // accumulated (arena)
   float* dbeta;
 };
@@ -287,8 +289,8 @@ __global__ __launch_bounds__(256) void l0_fwd_kernel(Args a) {
       [&](const Tile& cur, const Ops& op) {
         float z[kNT][4];
         conv_z(sm, op.x, g, rl, z);
-        const int bit = 1 << cur.d;
-        u16x4 o[kNT];
+        const int bit = 1 << cur.d, upto = (2 << cur.d) - 1;
+        u16x4 o[kNT], ow[kNT];
         unsigned cw[kNT];
 #pragma unroll
         for (int j = 0; j < kNT; ++j) {
@@ -308,6 +310,11 @@ __global__ __launch_bounds__(256) void l0_fwd_kernel(Args a) {
             b |= xor8i(b);
             const unsigned cd = b == 0 ? 0xFFu : (a.relu && !(m > 0.f)) ? 4u : (unsigned)__builtin_ctz(b);
             cw[j] |= cd << (8 * v);
+            // the winner's z to every lane of the window (the others add exact zeros)
+            float zs = (b & upto) == bit ? z[j][v] : 0.f;
+            zs += xor1(zs);
+            zs += xor8(zs);
+            ow[j][v] = f2bf(zs);  // (exact: z is bf16-valued)
           }
         }
         if (cur.d == 0) {
@@ -315,10 +322,66 @@ __global__ __launch_bounds__(256) void l0_fwd_kernel(Args a) {
           unsigned short* dst = a.y + win * kK + 4 * g;
 #pragma unroll
           for (int j = 0; j < kNT; ++j) *reinterpret_cast<u16x4*>(dst + j * 16) = o[j];
+          unsigned short* dzw = a.zw + win * kK + 4 * g;
+#pragma unroll
+          for (int j = 0; j < kNT; ++j) *reinterpret_cast<u16x4*>(dzw + j * 16) = ow[j];
           *reinterpret_cast<uint4*>(a.code + win * (kK / 4) + g * 4) =
               make_uint4(cw[0], cw[1], cw[2], cw[3]);
         }
       });
+}
+
+// BatchNorm-backward sums S1 = sum dy_bn, S2 = sum dy_bn * xhat without the conv: dy_bn is the
+// pooled gradient at the pixel the forward's code names (zero elsewhere), and that pixel's z is
+// the recorded zw, so each pooled value contributes dy * [pass] and dy * (zw - mean) * invstd
+// once. A thread owns one window x the 16 channels j*16 + 4g + v of its lane group g (the code
+// bytes' order), walking windows with a grid stride; block reduction through LDS, one atomic
+// per channel per block into replica blockIdx.x % kStatRep.
+__global__ __launch_bounds__(256) void l0_sums_kernel(Args a, int windows) {
+  __shared__ float red[256][33];
+  const int tid = threadIdx.x, g = tid & 3;
+  float mu[kNT][4], is[kNT][4], s1[kNT][4] = {}, s2[kNT][4] = {};
+#pragma unroll
+  for (int j = 0; j < kNT; ++j)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int c = j * 16 + 4 * g + v;
+      mu[j][v] = a.coef[2 * kK + c];
+      is[j][v] = a.coef[3 * kK + c];
+    }
+  for (int w = blockIdx.x * 64 + (tid >> 2); w < windows; w += gridDim.x * 64) {
+    const uint4 cq = *reinterpret_cast<const uint4*>(a.code + (size_t)w * (kK / 4) + g * 4);
+    const unsigned cw[kNT] = {cq.x, cq.y, cq.z, cq.w};
+    u16x4 dv[kNT], zv[kNT];
+#pragma unroll
+    for (int j = 0; j < kNT; ++j) {
+      dv[j] = *reinterpret_cast<const u16x4*>(a.dy + (size_t)w * kK + j * 16 + 4 * g);
+      zv[j] = *reinterpret_cast<const u16x4*>(a.zw + (size_t)w * kK + j * 16 + 4 * g);
+    }
+#pragma unroll
+    for (int j = 0; j < kNT; ++j)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float d = ((cw[j] >> (8 * v)) & 0xFFu) < 4u ? bf2f(dv[j][v]) : 0.f;
+        s1[j][v] += d;
+        s2[j][v] += d * ((bf2f(zv[j][v]) - mu[j][v]) * is[j][v]);
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < kNT; ++j)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      red[tid][j * 4 + v] = s1[j][v];
+      red[tid][16 + j * 4 + v] = s2[j][v];
+    }
+  __syncthreads();
+  if (tid < 2 * kK) {
+    const int k = tid / kK, c = tid - k * kK;
+    const int gg = (c & 15) >> 2, e = k * 16 + (c >> 4) * 4 + (c & 3);
+    float t = 0.f;
+    for (int i = 0; i < 64; ++i) t += red[4 * i + gg][e];
+    atomicAdd(a.sums + (blockIdx.x % kStatRep) * 2 * kK + k * kK + c, t);
+  }
 }
 
 // BN backward through the recomputed z. APPLY = 0: S1 / S2 sums; 1: dz (+ dgamma / dbeta)
@@ -429,6 +492,7 @@ static l0::Args l0_args(const ConvGeom* g, const L0Io* io) {
   a.sums = io->sums;
   a.dz = (unsigned short*)io->dz;
   a.code = (unsigned*)io->code;
+  a.zw = (unsigned short*)io->zw;
   a.dgamma = io->dgamma;
   a.dbeta = io->dbeta;
   return a;
@@ -438,7 +502,7 @@ static l0::Args l0_args(const ConvGeom* g, const L0Io* io) {
 // served
 extern "C" int ddp_l0_fwd(const ConvGeom* g, const L0Io* io, hipStream_t st) {
   if (!l0_shape_ok(g) || !io->x || !io->wc || !io->stats || !io->gamma || !io->beta ||
-      !io->coef || !io->y || !io->code)
+      !io->coef || !io->y || !io->code || !io->zw)
     return -1;
   const l0::Args a = l0_args(g, io);
   const unsigned nb = l0::grid_for(a.tiles);
@@ -450,11 +514,13 @@ extern "C" int ddp_l0_fwd(const ConvGeom* g, const L0Io* io, hipStream_t st) {
 // backward: sums pass + dz pass (sums zeroed by the caller; coef = the forward's table)
 extern "C" int ddp_l0_bwd(const ConvGeom* g, const L0Io* io, hipStream_t st) {
   if (!l0_shape_ok(g) || !io->x || !io->wc || !io->coef || !io->dy || !io->sums || !io->dz ||
-      !io->code)
+      !io->code || !io->zw)
     return -1;
   const l0::Args a = l0_args(g, io);
   const unsigned nb = l0::grid_for(a.tiles);
-  hipLaunchKernelGGL(l0::l0_bwd_kernel<0>, dim3(nb), dim3(256), 0, st, a);
+  const int windows = g->N * (g->H / 2) * (g->W / 2);
+  const unsigned ns = (unsigned)std::max(1, std::min(512, (windows + 127) / 128));
+  hipLaunchKernelGGL(l0::l0_sums_kernel, dim3(ns), dim3(256), 0, st, a, windows);
   hipLaunchKernelGGL(l0::l0_bwd_kernel<1>, dim3(nb), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }

@@ -659,6 +659,9 @@ static bool plan(const ConvGeom* g, float* ws, size_t ws_elems, int in_mode, Pla
   if (g->R != 3 || g->S != 3 || g->stride != 1 || g->pad != 1 || g->P != g->H || g->Q != g->W)
     return false;
   if (g->C % 64 || g->K % 64 || g->Creal != g->C) return false;
+  // 2x2 images go to the dense GEMM form (conv_igemm.hip: 4 of 9 taps per pixel are real),
+  // unless a sweep / test forces this kernel
+  if (!g_tr_force.bm && ddp_conv_dense2x2_ok(g)) return false;
   const int N = g->N, H = g->H, W = g->W, C = g->C, K = g->K;
   const size_t M = (size_t)N * H * W;
   const size_t xe = M * C * (in_mode == 2 ? 4 : 1), we = (size_t)K * 9 * C;

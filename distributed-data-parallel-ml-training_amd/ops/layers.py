@@ -370,11 +370,13 @@ class _ConvBNActFn(torch.autograd.Function):
         if ctx.l0:
             # input block: statistics pass + BN/ReLU/pool pass, z never stored (conv_l0.hip)
             # code: per pooled value, the window position its gradient goes to (1 B each)
+            # and that pixel's z (bf16), so the backward sums need no conv
             code = torch.empty(N, Ho, Wo, spec.K, dtype=torch.uint8, device=x.device)
+            zw = torch.empty(N, Ho, Wo, spec.K, dtype=BF16, device=x.device)
             native().l0_fwd(spec.geom(N, H, W), ptr(x), ptr(spec.wc), ptr(bias), spec.eps,
                             int(spec.relu), ptr(stats), ptr(gamma), ptr(beta), ptr(spec.coef),
-                            ptr(y), ptr(code), stream_handle())
-            ctx.l0_code = code
+                            ptr(y), ptr(code), ptr(zw), stream_handle())
+            ctx.l0_code = (code, zw)
             spec.fwd_z = None
             spec.last_deferred = False
             ctx.pool3_idx = None
@@ -434,7 +436,8 @@ class _ConvBNActFn(torch.autograd.Function):
             dz = torch.empty(N, H, W, spec.K, dtype=BF16, device=x.device)
             native().l0_bwd(spec.geom(N, H, W), ptr(x), ptr(spec.wc), ptr(bias), spec.eps,
                             int(spec.relu), ptr(spec.coef), ptr(dy), ptr(spec.sums), ptr(dz),
-                            ptr(gg), ptr(gbt), ptr(ctx.l0_code), stream_handle())
+                            ptr(gg), ptr(gbt), ptr(ctx.l0_code[0]), ptr(ctx.l0_code[1]),
+                            stream_handle())
             ctx.l0_code = None
             grad_ready([gamma, beta, bias])
             dx = conv_backward(spec, x, dz, gw, ctx.needs_input_grad[0], ctx.in_link,

@@ -651,6 +651,51 @@ def test_conv_every_tile(native_ext, case, tile):
 
 
 @pytest.mark.parametrize("pair_mode", [0, 3])
+@pytest.mark.parametrize("N,C,K", [(32, 512, 512), (256, 512, 512), (64, 128, 256)])
+def test_conv_dense2x2(native_ext, N, C, K, pair_mode):
+    """3x3 / s1 / p1 convs over 2x2 images as ONE dense GEMM per direction (conv_igemm.hip
+    ConvArgs::d2x2: the tap of each (output pixel, input pixel) block read straight from Wc, the
+    split-K finish on the 3x3 view): z, the BatchNorm statistics of the rounded z, dx and dW
+    against fp32 PyTorch, and against the implicit-GEMM path (dense switched off), separately
+    launched (pair mode 0) and as the grouped backward pair (3). VGG-11 layers 6-7
+    (/root/reference/part1/model.py:18-23 at 2x2)."""
+    from ddp_amd.ops.layers import conv_forward, conv_backward
+    nat = native_ext
+    conv, spec, x, xn = _conv_setup(N, C, 2, 2, K, 3, 1, 1)
+    assert nat.conv_dense2x2_ok(spec.geom(N, 2, 2))
+    dz = bf(torch.randn(N, K, 2, 2, device=DEV))
+    dzn = dz.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    out = {}
+    nat.conv_pair_mode(pair_mode)
+    try:
+        for dense in (1, 0):
+            nat.conv_dense2x2_set(dense)
+            stats = torch.zeros(16 * 2 * K, device=DEV)
+            dw = torch.zeros_like(conv.weight, memory_format=torch.channels_last)
+            z = conv_forward(spec, xn, conv.bias, stats)
+            dx = conv_backward(spec, xn, dzn, dw, True)
+            torch.cuda.synchronize()
+            out[dense] = (z.clone(), stats.view(16, 2 * K).sum(0), dx.clone(), dw.clone())
+    finally:
+        nat.conv_dense2x2_set(1)
+        nat.conv_pair_mode(3)
+    ref = F.conv2d(x, conv.weight, conv.bias, 1, 1).permute(0, 2, 3, 1)
+    xr = x.clone().requires_grad_(True)
+    wr = conv.weight.detach().clone().requires_grad_(True)
+    F.conv2d(xr, wr, None, 1, 1).backward(dz)
+    for dense in (1, 0):
+        z, st, dx, dw = out[dense]
+        assert rel_err(z, ref) < 1e-2, (dense, rel_err(z, ref))
+        zf = z.float().reshape(-1, K)
+        assert torch.allclose(st[:K], zf.sum(0), rtol=1e-3, atol=1e-2), dense
+        assert torch.allclose(st[K:], (zf * zf).sum(0), rtol=1e-3, atol=1e-2), dense
+        assert rel_err(dx.permute(0, 3, 1, 2), xr.grad) < 1e-2, dense
+        assert rel_err(dw, wr.grad) < 1e-2, dense
+    assert rel_err(out[1][0], out[0][0]) < 1e-2
+    assert rel_err(out[1][2], out[0][2]) < 1e-2
+
+
+@pytest.mark.parametrize("pair_mode", [0, 3])
 @pytest.mark.parametrize("case", [(32, 64, 16, 128, True, False), (8, 128, 8, 256, False, False),
                                   (32, 256, 4, 512, True, False), (4, 64, 32, 64, True, False),
                                   (8, 8, 32, 64, True, True), (4, 64, 14, 128, False, False)])
@@ -789,8 +834,9 @@ def test_l0_fused_input_block(native_ext, N):
     coef = torch.full((6 * K,), float("nan"), device=DEV)
     y = torch.full((N, H // 2, H // 2, K), float("nan"), device=DEV, dtype=torch.bfloat16)
     code = torch.full((N, H // 2, H // 2, K), 0xEE, device=DEV, dtype=torch.uint8)
+    zw = torch.full((N, H // 2, H // 2, K), float("nan"), device=DEV, dtype=torch.bfloat16)
     nat.l0_fwd(g, ptr(xn), ptr(spec.wc), ptr(conv.bias), eps, 1, ptr(stats), ptr(gamma),
-               ptr(beta), ptr(coef), ptr(y), ptr(code), s)
+               ptr(beta), ptr(coef), ptr(y), ptr(code), ptr(zw), s)
     dy = bf(torch.randn(N, K, H // 2, H // 2, device=DEV))
     dyn = dy.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
     sums = torch.zeros(16 * 2 * K, device=DEV)
@@ -798,13 +844,21 @@ def test_l0_fused_input_block(native_ext, N):
     dg = torch.zeros(K, device=DEV)
     db = torch.zeros(K, device=DEV)
     nat.l0_bwd(g, ptr(xn), ptr(spec.wc), ptr(conv.bias), eps, 1, ptr(coef), ptr(dyn), ptr(sums),
-               ptr(dz), ptr(dg), ptr(db), ptr(code), s)
+               ptr(dz), ptr(dg), ptr(db), ptr(code), ptr(zw), s)
     torch.cuda.synchronize()
     # every pooled value got a verdict: a window position, or 4 = ReLU zeroed the window; the
     # bytes are lane-major ([g][j][v] for channel j*16 + 4g + v), 4 exactly where y is 0
     assert int(code.max()) <= 4
     code_c = code.view(N, H // 2, H // 2, 4, 4, 4).permute(0, 1, 2, 4, 3, 5).reshape(y.shape)
     assert torch.equal(code_c == 4, y == 0)
+    # zw: the z of the pixel the code names (any window position where code is 4: all ReLU-cut)
+    zp = bf(F.conv2d(x, conv.weight, conv.bias, 1, 1)).permute(0, 2, 3, 1)  # [N][H][W][K]
+    win = zp.reshape(N, H // 2, 2, H // 2, 2, K).permute(0, 1, 3, 2, 4, 5).reshape(N, H // 2, H // 2, 4, K)
+    sel = code_c.long().clamp(max=3).unsqueeze(3)
+    zsel = torch.gather(win, 3, sel).squeeze(3)
+    ok = code_c < 4
+    # (the kernel's bf16 z may differ from the reference conv's rounding by one bf16 step)
+    assert torch.allclose(zw.float()[ok], zsel[ok], rtol=8e-3, atol=1e-2)
     with torch.no_grad():
         z = bf(F.conv2d(x, conv.weight, conv.bias, 1, 1))
     zr = z.clone().requires_grad_(True)
