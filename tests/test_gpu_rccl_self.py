@@ -97,7 +97,9 @@ def test_captured_ddp_step_with_live_rccl(native_ext, segmented):
         m.close()
     (e0, e1), g0 = res[False]
     (l0, _), g1 = res[True]
-    tol = min(0.99, _cos(e0, e1) - 0.005)  # two executions differ by float-atomic ordering
+    # two executions differ by float-atomic ordering (BatchNorm statistics move bf16 pool-window
+    # ties and ReLU edges): the compared steps must sit within 3x that run-to-run noise
+    tol = min(0.99, 1.0 - 3.0 * (1.0 - _cos(e0, e1)))
     assert float(e0.norm()) > 0
     for a, b in ((e0, l0), (g0, g1), (e0, g1)):
         assert _cos(a, b) > tol, (_cos(a, b), tol)
@@ -298,13 +300,18 @@ def test_captured_strategy_step_with_live_rccl(native_ext, strategy):
         torch.cuda.synchronize()
         return arena.data - snap[0]
 
-    e_ref = [run(ref_step._body), run(ref_step._body)]
+    e_ref = [run(ref_step._body), run(ref_step._body), run(ref_step._body)]
     e_sync = run(st._body)
     st.warmup(1)
     st.capture()
     assert st.graph is not None
     replays = [run(st.step), run(st.step)]
-    tol = min(0.99, _cos(e_ref[0], e_ref[1]) - 0.005)
+    # run-to-run noise of the reference itself: the BatchNorm statistics are fp32 atomics, and
+    # their summation order moves bf16 pool-window ties / ReLU edges, so two identical eager steps
+    # already differ (measured cos 0.99-0.999, tools/probes/grad_determinism.py); a synced step
+    # must sit within 3x that noise of the reference
+    noise = 1.0 - min(_cos(e_ref[0], e_ref[1]), _cos(e_ref[0], e_ref[2]), _cos(e_ref[1], e_ref[2]))
+    tol = min(0.99, 1.0 - 3.0 * noise)
     assert float(e_ref[0].norm()) > 0
     for d in [e_sync] + replays:
         assert not torch.isnan(d).any()

@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Run the eager VGG-11 training step twice from one snapshot (parameters, momentum, data
+cursor) and report, per parameter tensor, how much the two gradients differ: which layer's
+backward is not run-to-run deterministic, and by how much.
+
+    python tools/probes/grad_determinism.py [--batch 32] [--runs 3]
+
+SGD in the backward is switched off (the gradients stay in the arena)."""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, REPO)
+os.environ["DDP_AMD_SGD_IN_BWD"] = "0"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--runs", type=int, default=3)
+    a = ap.parse_args()
+    import torch
+    from ddp_amd.models import VGG11
+    from ddp_amd.optim import FusedSGD
+    from ddp_amd.data import SyntheticCIFAR10, DeviceLoader
+    from ddp_amd.engine import TrainStep, CrossEntropyLoss
+    torch.manual_seed(13)
+    m = VGG11().cuda()
+    opt = FusedSGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    ld = DeviceLoader(SyntheticCIFAR10(True, n=max(256, a.batch)), a.batch, "cuda")
+    st = TrainStep(m, opt, CrossEntropyLoss(), ld, sync=None)
+    arena = opt.arena
+    snap = (arena.data.clone(), opt.momentum_buffer.clone(), ld.cursor.clone())
+    names = [n for n, _ in m.named_parameters()]
+    params = [p for _, p in m.named_parameters()]
+    grads = []
+    for _ in range(a.runs):
+        arena.data.copy_(snap[0])
+        opt.momentum_buffer.copy_(snap[1])
+        ld.cursor.copy_(snap[2])
+        arena.grad.zero_()
+        for sp in m.fused_plan():
+            sp._packed_version = None
+            sp.maybe_pack()
+        torch.cuda.synchronize()
+        # the step's fused SGD consumes and clears the gradient: capture it right after backward
+        st.optimizer.step_orig = st.optimizer.step
+        saved = {}
+
+        def grab(*args, **kw):
+            saved["g"] = [p.grad.detach().clone() if p.grad is not None else None for p in params]
+            return st.optimizer.step_orig(*args, **kw)
+        st.optimizer.step = grab
+        st._body()
+        torch.cuda.synchronize()
+        st.optimizer.step = st.optimizer.step_orig
+        grads.append(saved["g"])
+    print(f"batch {a.batch}: per-parameter max relative difference between runs (vs run 0)")
+    for i, n in enumerate(names):
+        g0 = grads[0][i]
+        if g0 is None:
+            continue
+        rels = []
+        for r in range(1, a.runs):
+            d = (grads[r][i] - g0).float()
+            rels.append(float(d.norm() / (g0.float().norm() + 1e-30)))
+        print(f"  {n:40s} {tuple(g0.shape)!s:24s} |g| {float(g0.float().norm()):.3e}  "
+              f"rel diff {max(rels):.3e}")
+
+
+if __name__ == "__main__":
+    main()
