@@ -56,6 +56,11 @@ def main():
         torch.cuda.synchronize()
         st.optimizer.step = st.optimizer.step_orig
         grads.append(saved["g"])
+    flat = [torch.cat([g.float().reshape(-1) for g in gr if g is not None]) for gr in grads]
+    for r in range(a.runs):
+        for q in range(r + 1, a.runs):
+            d = float((flat[q] - flat[r]).norm() / flat[r].norm())
+            print(f"runs {r} vs {q}: whole-gradient relative difference {d:.3e}")
     print(f"batch {a.batch}: per-parameter max relative difference between runs (vs run 0)")
     for i, n in enumerate(names):
         g0 = grads[0][i]
