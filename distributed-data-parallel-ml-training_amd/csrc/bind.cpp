@@ -438,6 +438,21 @@ PYBIND11_MODULE(_native, m) {
   }, py::arg("x"), py::arg("W"), py::arg("b"), py::arg("labels"), py::arg("B"), py::arg("F"),
      py::arg("J"), py::arg("logits"), py::arg("dlogits"), py::arg("loss_sum"), py::arg("correct"),
      py::arg("stream"), py::arg("loss_acc") = 0);
+  // the head with the last block's BN + ReLU + 2x2 pool folded in (writes the features y)
+  m.def("bn_pool_linear_ce_fwd", [](uintptr_t z, uintptr_t stats, uintptr_t gamma, uintptr_t beta,
+                                    float eps, int relu, uintptr_t coef, uintptr_t y, uintptr_t W,
+                                    uintptr_t b, uintptr_t labels, int B, int F, int J,
+                                    uintptr_t dlogits, uintptr_t loss_sum, uintptr_t st,
+                                    uintptr_t loss_acc) {
+    ddp_amd::HeadBnIn h{P<unsigned short>(z), P<float>(stats), P<float>(gamma), P<float>(beta),
+                        eps, relu, P<float>(coef), P<unsigned short>(y)};
+    check(ddp_bn_pool_linear_ce_fwd(&h, P<float>(W), P<float>(b), P<long long>(labels), B, F, J,
+                                    P<float>(dlogits), P<float>(loss_sum), nullptr,
+                                    P<float>(loss_acc), S(st)), "bn_pool_linear_ce_fwd");
+  }, py::arg("z"), py::arg("stats"), py::arg("gamma"), py::arg("beta"), py::arg("eps"),
+     py::arg("relu"), py::arg("coef"), py::arg("y"), py::arg("W"), py::arg("b"), py::arg("labels"),
+     py::arg("B"), py::arg("F"), py::arg("J"), py::arg("dlogits"), py::arg("loss_sum"),
+     py::arg("stream"), py::arg("loss_acc") = 0);
   m.def("linear_bwd", [](uintptr_t dlogits, uintptr_t x, uintptr_t W, int B, int F, int J,
                          uintptr_t gscale, uintptr_t dx, uintptr_t dW, uintptr_t db,
                          uintptr_t st) {

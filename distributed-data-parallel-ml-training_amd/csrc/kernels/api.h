@@ -100,6 +100,19 @@ struct TrFwdIn {
   unsigned short* y;        // materialised conv input [N][H][W][C] (the wgrad operand)
 };
 
+// The last Conv->BN->ReLU->2x2-pool block over 2x2 images computed inside the classifier head's
+// forward (linear_ce.hip): x = the pooled features it writes
+struct HeadBnIn {
+  const unsigned short* z;  // [B][2][2][F] the block's conv output (bf16)
+  const float* stats;       // its statistics replicas [kStatRep][2][F]
+  const float* gamma;
+  const float* beta;
+  float eps;
+  int relu;
+  float* coef;              // [6][F]: block 0 writes scale, shift, mean, invstd
+  unsigned short* y;        // [B][F] pooled features (written)
+};
+
 // SGD in the backward (conv_igemm.hip wgrad_finish_krsc_body): the optimizer step of one conv
 // weight, applied by the WGRAD split-K finish that produces its complete gradient
 // (torch.optim.SGD, dampening 0: d = g * grad_scale + wd * p; buf = momentum * buf + d;
@@ -211,6 +224,9 @@ int ddp_bn_act_bwd(const ddp_amd::BnArgs* a, hipStream_t st);
 int ddp_bn_bwd_local_ok(int N, int H, int W, int C, int pool);
 void ddp_bn_bwd_local_set(long long max_loads);
 // mid-size layers: the same in one launch over up to kStatRep blocks per 64 channels that meet at
+int ddp_bn_pool_linear_ce_fwd(const ddp_amd::HeadBnIn* bn, const float* W, const float* b,
+                              const long long* labels, int B, int F, int J, float* dlogits,
+                              float* loss_sum, int* correct, float* loss_acc, hipStream_t st);
 int ddp_linear_ce_fwd(const void* x, const float* W, const float* b, const long long* labels,
                       int B, int F, int J, float* logits, float* dlogits, float* loss_sum,
                       int* correct, float* loss_acc, hipStream_t st);

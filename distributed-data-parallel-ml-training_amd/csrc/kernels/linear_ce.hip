@@ -19,10 +19,43 @@
 namespace ddp_amd {
 
 
+// BN = true: the head input x is the last Conv->BN->ReLU->2x2-pool block's output over 2x2
+// images, computed here from its conv output z (HeadBnIn) instead of by a separate BatchNorm
+// pass: the block's coefficients are folded from its statistics replicas in every block (block
+// 0 writes the [6][F] table its backward reads), each lane applies BN + ReLU to its 8 channels
+// of the four window pixels, max-pools them (bn_act.hip's rule) and stores the bf16 feature,
+// which then feeds the dot products exactly as a loaded x would.
+constexpr int kMaxHeadF = 1024;
+template <bool BN>
 __global__ __launch_bounds__(256) void linear_ce_fwd_kernel(
     const unsigned short* __restrict__ x, const float* __restrict__ W, const float* __restrict__ b,
     const long long* __restrict__ labels, int B, int F, int J, float inv_b, float* logits_out,
-    float* dlogits, float* loss_sum, int* correct, float* loss_acc) {
+    float* dlogits, float* loss_sum, int* correct, float* loss_acc, HeadBnIn bn) {
+  __shared__ float cf[BN ? 2 * kMaxHeadF : 1];
+  if constexpr (BN) {
+    const float M = 4.f * B;
+    for (int c = threadIdx.x; c < F; c += 256) {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int r = 0; r < kStatRep; ++r) {
+        s1 += bn.stats[r * 2 * F + c];
+        s2 += bn.stats[r * 2 * F + F + c];
+      }
+      const float mu = s1 / M;
+      const float var = fmaxf(s2 / M - mu * mu, 0.f);
+      const float is = rsqrtf(var + bn.eps);
+      const float sc = bn.gamma[c] * is, sh = bn.beta[c] - mu * sc;
+      cf[c] = sc;
+      cf[F + c] = sh;
+      if (blockIdx.x == 0) {
+        bn.coef[0 * F + c] = sc;
+        bn.coef[1 * F + c] = sh;
+        bn.coef[2 * F + c] = mu;
+        bn.coef[3 * F + c] = is;
+      }
+    }
+    __syncthreads();
+  }
   const int lane = threadIdx.x & 63;
   const int row_raw = blockIdx.x * 4 + (threadIdx.x >> 6);
   const bool live = row_raw < B;
@@ -31,7 +64,27 @@ __global__ __launch_bounds__(256) void linear_ce_fwd_kernel(
 #pragma unroll
   for (int j = 0; j < kMaxJ; ++j) acc[j] = 0.f;
   for (int f0 = lane * 8; f0 < F; f0 += 64 * 8) {
-    const u16x8 xv = ld8(x + (size_t)row * F + f0);
+    u16x8 xv;
+    if constexpr (BN) {
+      const unsigned short* zp = bn.z + (size_t)row * 4 * F + f0;  // pixels (0,0) (0,1) (1,0) (1,1)
+      u16x8 q[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) q[d] = ld8(zp + d * F);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float best = 0.f;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          float y = bf2f(q[d][e]) * cf[f0 + e] + cf[F + f0 + e];  // (bn_act.hip apply expression)
+          if (bn.relu) y = fmaxf(y, 0.f);
+          if (d == 0 || y > best || y != y) best = y;  // bn_act.hip's pool rule
+        }
+        xv[e] = f2bf(best);
+      }
+      if (live) st8(bn.y + (size_t)row * F + f0, xv);
+    } else {
+      xv = ld8(x + (size_t)row * F + f0);
+    }
     float xf[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) xf[e] = bf2f(xv[e]);
@@ -201,9 +254,23 @@ extern "C" int ddp_linear_ce_fwd(const void* x, const float* W, const float* b,
                                  float* dlogits, float* loss_sum, int* correct, float* loss_acc,
                                  hipStream_t st) {
   if (J > kMaxJ || F % 8) return -1;
-  hipLaunchKernelGGL(linear_ce_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, st,
+  hipLaunchKernelGGL(linear_ce_fwd_kernel<false>, dim3((B + 3) / 4), dim3(256), 0, st,
                      (const unsigned short*)x, W, b, labels, B, F, J, 1.f / (float)B, logits,
-                     dlogits, loss_sum, correct, loss_acc);
+                     dlogits, loss_sum, correct, loss_acc, HeadBnIn{});
+  return (int)hipGetLastError();
+}
+
+// the head with the last block's BatchNorm + ReLU + 2x2 pool folded in (x = bn->y is written)
+extern "C" int ddp_bn_pool_linear_ce_fwd(const HeadBnIn* bn, const float* W, const float* b,
+                                         const long long* labels, int B, int F, int J,
+                                         float* dlogits, float* loss_sum, int* correct,
+                                         float* loss_acc, hipStream_t st) {
+  if (J > kMaxJ || F % 8 || F > kMaxHeadF || !bn || !bn->z || !bn->stats || !bn->gamma ||
+      !bn->beta || !bn->coef || !bn->y)
+    return -1;
+  hipLaunchKernelGGL(linear_ce_fwd_kernel<true>, dim3((B + 3) / 4), dim3(256), 0, st,
+                     (const unsigned short*)bn->y, W, b, labels, B, F, J, 1.f / (float)B,
+                     nullptr, dlogits, loss_sum, correct, loss_acc, *bn);
   return (int)hipGetLastError();
 }
 

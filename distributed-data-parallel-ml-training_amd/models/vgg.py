@@ -166,8 +166,13 @@ class _VGG(nn.Module):
                 acc.add_(loss.detach())
             return loss
         from ..ops.layers import linear_cross_entropy
-        return linear_cross_entropy(self._features_fused(x), self.fc1, labels, acc, transient,
-                                    bn_prev=self.fused_plan()[-1])
+        last = self.fused_plan()[-1]
+        last.defer_to_head = True  # its BN + ReLU + pool may run inside the head's kernel
+        try:
+            h = self._features_fused(x)
+        finally:
+            last.defer_to_head = False
+        return linear_cross_entropy(h, self.fc1, labels, acc, transient, bn_prev=last)
 
 
 def VGG11():

@@ -220,6 +220,9 @@ BN_BWD_APPLY_FUSE = os.environ.get("DDP_AMD_BN_BWD_APPLY_FUSE", "1") != "0"
 HEAD_BN_FUSE = os.environ.get("DDP_AMD_HEAD_BN_FUSE", "1") != "0"
 # ... with the head's dW / db in the same launch (=0: a separate linear_bwd launch)
 HEAD_ONE_LAUNCH = os.environ.get("DDP_AMD_HEAD_ONE_LAUNCH", "1") != "0"
+# ... and its BN + ReLU + 2x2 pool FORWARD folded into the head's forward kernel (linear_ce.hip
+# HeadBnIn: one launch fewer; the training loss path only, VGG's 2x2 last block)
+HEAD_BN_FWD = os.environ.get("DDP_AMD_HEAD_BN_FWD", "1") != "0"
 BN_BWD_FUSE_MAX_HW = int(os.environ.get("DDP_AMD_BN_BWD_FUSE_MAX_HW", "16"))
 # preceding block without a max-pool (ResNet's conv1 -> conv2 -> conv3 chain): one z load per
 # dgrad output element in the epilogue would replace a whole dy + z pass of the reduce kernel,
@@ -395,8 +398,12 @@ class _ConvBNActFn(torch.autograd.Function):
             z = conv_forward(spec, x, bias, stats, fin=fin)
         spec.fwd_z = z
         ctx.pool3_idx = None
+        # the classifier head computes this block's BN + ReLU + pool (set by forward_loss on the
+        # last block; linear_ce.hip HeadBnIn) — or the next conv does (conv_tr fused input)
+        to_head = (HEAD_BN_FWD and getattr(spec, "defer_to_head", False) and residual is None
+                   and rm is None and spec.pool and P == 2 and Q == 2 and spec.relu)
         spec.last_deferred = (not fused and not spec.maxpool3
-                              and _defer_bn(spec, residual, rm, N, Ho, Wo))
+                              and (to_head or _defer_bn(spec, residual, rm, N, Ho, Wo)))
         if spec.maxpool3:
             idx = torch.empty(N, Ho, Wo, spec.K, dtype=torch.uint8, device=x.device)
             native().bn_pool3_fwd(N, P, Q, spec.K, int(spec.relu), spec.eps, ptr(z), ptr(stats),
@@ -406,7 +413,7 @@ class _ConvBNActFn(torch.autograd.Function):
                                   use_running, ptr(spec.coef))
             ctx.pool3_idx = idx
         elif spec.last_deferred:
-            spec.deferred = y  # computed by the next block's conv (conv_tr.hip fused input)
+            spec.deferred = y  # computed by the next block's conv or the head (see to_head)
         elif not fused:
             native().bn_act_fwd(N, P, Q, spec.K, int(spec.pool), int(spec.relu), spec.eps, ptr(z),
                                 ptr(residual), ptr(stats), ptr(gamma), ptr(beta), ptr(y),
@@ -564,8 +571,19 @@ class _LinearCEFn(torch.autograd.Function):
         loss = (step_scratch(x.device).take_transient(1).view(()) if transient
                 else torch.zeros((), dtype=F32, device=x.device))
         dl = torch.empty(B, J, dtype=F32, device=x.device)
-        native().linear_ce_fwd(ptr(x), ptr(weight), ptr(bias), ptr(labels), B, F, J, 0, ptr(dl),
-                               ptr(loss), 0, stream_handle(), loss_acc=ptr(acc))
+        if (bn_prev is not None and bn_prev.deferred is not None
+                and bn_prev.deferred.data_ptr() == x.data_ptr() and ctx.prev_z is not None):
+            # the last block deferred its BN + ReLU + pool here: x is written by this kernel
+            bn_prev.deferred = None
+            bn = bn_prev.bn
+            native().bn_pool_linear_ce_fwd(ptr(ctx.prev_z), ptr(bn_prev.stats), ptr(bn.weight),
+                                           ptr(bn.bias), bn_prev.eps, int(bn_prev.relu),
+                                           ptr(bn_prev.coef), ptr(x), ptr(weight), ptr(bias),
+                                           ptr(labels), B, F, J, ptr(dl), ptr(loss),
+                                           stream_handle(), loss_acc=ptr(acc))
+        else:
+            native().linear_ce_fwd(ptr(x), ptr(weight), ptr(bias), ptr(labels), B, F, J, 0,
+                                   ptr(dl), ptr(loss), 0, stream_handle(), loss_acc=ptr(acc))
         ctx.save_for_backward(x, weight, bias, dl)
         return loss
 
