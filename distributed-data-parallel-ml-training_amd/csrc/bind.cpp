@@ -208,27 +208,9 @@ PYBIND11_MODULE(_native, m) {
     ddp_conv_tr_geometry(BM, N, H, W, o);
     return std::vector<int>(o, o + 7);
   });
-  // classifier-head dx + the preceding block's BN backward; bn = (z, coef, sums, pool, relu, Hz,
-  // Wz), bna = (dz, dgamma, dbeta); True when launched (dx is then not computed)
-  m.def("linear_dx_bn", [](uintptr_t dl, uintptr_t W, int B, int F, int J, uintptr_t g,
-                           py::tuple bn, py::tuple bna, uintptr_t st) {
-    ddp_amd::BnBwdFuse f{};
-    f.z = P<unsigned short>(bn[0].cast<uintptr_t>());
-    f.coef = P<float>(bn[1].cast<uintptr_t>());
-    f.sums = P<float>(bn[2].cast<uintptr_t>());
-    f.pool = bn[3].cast<int>();
-    f.relu = bn[4].cast<int>();
-    f.Hz = bn[5].cast<int>();
-    f.Wz = bn[6].cast<int>();
-    ddp_amd::BnBwdApply ap{};
-    bn_apply(bna, &ap);
-    const int rc = ddp_linear_dx_bn(P<float>(dl), P<float>(W), B, F, J, P<float>(g), &f, &ap, S(st));
-    if (rc < 0) check(rc, "linear_dx_bn");
-    if (rc >= 2) check(rc - 2, "linear_dx_bn");
-    return rc == 1;
-  });
   // the whole head backward (dx fused with the preceding block's BatchNorm backward + dW / db)
-  // in one launch; returns False when not served (nothing launched)
+  // in one launch; bn = (z, coef, sums, pool, relu, Hz, Wz), bna = (dz, dgamma, dbeta); returns
+  // False when not served (nothing launched; dx is then computed by linear_bwd)
   m.def("linear_head_bwd_bn", [](uintptr_t dl, uintptr_t W, uintptr_t x, int B, int F, int J,
                                  uintptr_t g, py::tuple bn, py::tuple bna, uintptr_t dW,
                                  uintptr_t db, uintptr_t st) {

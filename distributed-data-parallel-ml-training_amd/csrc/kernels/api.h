@@ -181,8 +181,6 @@ int ddp_conv_fwd(const ddp_amd::ConvGeom* g, const void* x, const void* wc, cons
 int ddp_conv_fwd_bn(const ddp_amd::ConvGeom* g, const void* x, const void* wc, const float* bias,
                     void* z, float* stats, float* ws, size_t ws_elems, const ddp_amd::BnFwdFuse* bn,
                     hipStream_t st);
-// classifier-head dx fused with the preceding block's whole BN backward (conv_igemm.hip
-// linear_dx_bnbwd_kernel): 1 launched, 0 not served, < 0 invalid, >= 2 HIP error (rc - 2)
 // split-K finish of a forward GEMM computed elsewhere (slabs [splits][M][K] -> z + statistics,
 // or the BatchNorm-fused finish with ``bn``); returns the HIP error code
 int ddp_conv_fwd_finish(const ddp_amd::ConvGeom* g, float* ws, int splits, const float* bias,
@@ -200,8 +198,9 @@ int ddp_conv_tr_would_serve(const ddp_amd::ConvGeom* g, size_t ws_elems, int in_
 // (bm, bn, splits, stages) (bm = 0: use the implicit-GEMM kernel), 3 force the same (sweeps)
 void ddp_conv_tr_set(int mode, int M, int K, int C, int H, int bm, int bn, int splits, int stages);
 int ddp_conv_tr_geometry(int BM, int N, int H, int W, int* out7);
-int ddp_linear_dx_bn(const float* dl, const float* W, int B, int F, int J, const float* gscale,
-                     const ddp_amd::BnBwdFuse* bn, const ddp_amd::BnBwdApply* ba, hipStream_t st);
+// classifier-head dx fused with the preceding block's whole BN backward + dW / db in one launch
+// (conv_igemm.hip linear_head_bwd_kernel): 1 launched, 0 not served, < 0 invalid, >= 2 HIP
+// error (rc - 2)
 int ddp_linear_head_bwd_bn(const float* dl, const float* W, const void* x, int B, int F, int J,
                            const float* gscale, const ddp_amd::BnBwdFuse* bn,
                            const ddp_amd::BnBwdApply* ba, float* dW, float* db, hipStream_t st);

@@ -1392,7 +1392,7 @@ __device__ __forceinline__ void finish_bnbwd_body(const FinishArgs& fa, const Bn
 }
 
 // The BN-backward part of finish_bnbwd_body for dx rows held in v (fp32, rounded to bf16 here
-// like a stored dgrad output): shared with the classifier-head variant (linear_dx_bnbwd_kernel).
+// like a stored dgrad output): used by the classifier-head kernel (linear_head_bwd_kernel).
 template <int RPT, bool POOL>
 __device__ __forceinline__ void bnbwd_from_dx(const BnBwdFuse& bn, const BnBwdApply& ba, int Mg,
                                               int Ng, int H, int W, float (*v)[8],
@@ -1541,14 +1541,6 @@ __device__ __forceinline__ void linear_dx_bnbwd_body(const float* __restrict__ d
     }
   }
   bnbwd_from_dx<RPT, true>(bn, ba, B, F, 1, 1, v, wred, half, lane, c0);
-}
-
-template <int RPT>
-__global__ __launch_bounds__(256) void linear_dx_bnbwd_kernel(const float* __restrict__ dl,
-                                                              const float* __restrict__ Wt, int B,
-                                                              int F, int J, const float* gscale,
-                                                              BnBwdFuse bn, BnBwdApply ba) {
-  linear_dx_bnbwd_body<RPT>(dl, Wt, B, F, J, gscale, bn, ba, blockIdx.x);
 }
 
 // The whole head backward in ONE launch: blocks [0, F/16) run the fused dx + BatchNorm backward
@@ -2318,11 +2310,10 @@ extern "C" int ddp_conv_fwd(const ConvGeom* g, const void* x, const void* wc, co
   return (int)hipGetLastError();
 }
 
-// 1: launched (dx NOT written; dz / dgamma / dbeta of the block before the head written),
-// 0: shape not served (caller runs linear_bwd with dx + that block's BN backward), < 0 invalid,
+// dx fused with the BatchNorm backward AND dW / db in one launch. 1: launched (dx NOT written;
+// dz / dgamma / dbeta of the block before the head written), 0: shape not served (nothing
+// launched; caller runs linear_bwd with dx + that block's BN backward), < 0 invalid,
 // >= 2: HIP error (rc - 2)
-// dx fused with the BatchNorm backward AND dW / db in one launch; same return codes as
-// ddp_linear_dx_bn (0: not served — nothing was launched)
 extern "C" int ddp_linear_head_bwd_bn(const float* dl, const float* W, const void* x, int B,
                                       int F, int J, const float* gscale, const BnBwdFuse* bn,
                                       const BnBwdApply* ba, float* dW, float* db, hipStream_t st) {
@@ -2335,20 +2326,6 @@ extern "C" int ddp_linear_head_bwd_bn(const float* dl, const float* W, const voi
   if (B <= 128) hipLaunchKernelGGL(linear_head_bwd_kernel<1>, grid, dim3(256), 0, st, dl, W, xb, B, F, J, gscale, *bn, *ba, dW, db, ndx, nfx);
   else if (B <= 256) hipLaunchKernelGGL(linear_head_bwd_kernel<2>, grid, dim3(256), 0, st, dl, W, xb, B, F, J, gscale, *bn, *ba, dW, db, ndx, nfx);
   else hipLaunchKernelGGL(linear_head_bwd_kernel<4>, grid, dim3(256), 0, st, dl, W, xb, B, F, J, gscale, *bn, *ba, dW, db, ndx, nfx);
-  const int e = (int)hipGetLastError();
-  return e ? 2 + e : 1;
-}
-
-extern "C" int ddp_linear_dx_bn(const float* dl, const float* W, int B, int F, int J,
-                                const float* gscale, const BnBwdFuse* bn, const BnBwdApply* ba,
-                                hipStream_t st) {
-  if (!bn || !ba || !dl || !W) return -1;
-  if (J < 1 || J > 16 || F % 16 || B < 1 || B > 512 || !bn->pool || bn->Hz != 2 || bn->Wz != 2)
-    return 0;
-  const dim3 grid(F / 16);
-  if (B <= 128) hipLaunchKernelGGL(linear_dx_bnbwd_kernel<1>, grid, dim3(256), 0, st, dl, W, B, F, J, gscale, *bn, *ba);
-  else if (B <= 256) hipLaunchKernelGGL(linear_dx_bnbwd_kernel<2>, grid, dim3(256), 0, st, dl, W, B, F, J, gscale, *bn, *ba);
-  else hipLaunchKernelGGL(linear_dx_bnbwd_kernel<4>, grid, dim3(256), 0, st, dl, W, B, F, J, gscale, *bn, *ba);
   const int e = (int)hipGetLastError();
   return e ? 2 + e : 1;
 }

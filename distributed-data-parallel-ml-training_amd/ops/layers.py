@@ -216,10 +216,9 @@ BN_FWD_FUSE = os.environ.get("DDP_AMD_BN_FWD_FUSE", "1") != "0"
 # the preceding block's whole BatchNorm backward completed in a small dgrad's split-K finish
 # (conv_igemm.hip splitk_finish_bnbwd_kernel; BnBwdFuse chain only)
 BN_BWD_APPLY_FUSE = os.environ.get("DDP_AMD_BN_BWD_APPLY_FUSE", "1") != "0"
-# ... and into the classifier head's dx (linear_dx_bnbwd_kernel; needs BN_BWD_APPLY_FUSE too)
+# ... and into the classifier head's backward: dx + that BN backward + dW / db in one launch
+# (conv_igemm.hip linear_head_bwd_kernel; needs BN_BWD_APPLY_FUSE too)
 HEAD_BN_FUSE = os.environ.get("DDP_AMD_HEAD_BN_FUSE", "1") != "0"
-# ... with the head's dW / db in the same launch (=0: a separate linear_bwd launch)
-HEAD_ONE_LAUNCH = os.environ.get("DDP_AMD_HEAD_ONE_LAUNCH", "1") != "0"
 # ... and its BN + ReLU + 2x2 pool FORWARD folded into the head's forward kernel (linear_ce.hip
 # HeadBnIn: one launch fewer; the training loss path only, VGG's 2x2 last block)
 HEAD_BN_FWD = os.environ.get("DDP_AMD_HEAD_BN_FWD", "1") != "0"
@@ -562,7 +561,7 @@ class _LinearCEFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, labels, acc, transient, bn_prev=None):
         B, F = x.shape
         # the Conv->BN->ReLU->pool block whose output x is: its BN backward may be fused into
-        # the head's dx (conv_igemm.hip linear_dx_bnbwd_kernel)
+        # the head's backward (conv_igemm.hip linear_head_bwd_kernel)
         ctx.bn_prev = bn_prev
         ctx.prev_z = bn_prev.fwd_z if bn_prev is not None else None
         J = weight.shape[0]
@@ -604,16 +603,9 @@ class _LinearCEFn(torch.autograd.Function):
             dz_prev = torch.empty_like(pz)
             bnf = (ptr(pz), ptr(prev.coef), ptr(prev.sums), 1, int(prev.relu), 2, 2)
             bna = (ptr(dz_prev), ptr(ensure_grad(prev.bn.weight)), ptr(ensure_grad(prev.bn.bias)))
-            if HEAD_ONE_LAUNCH:
-                # dx + the block's whole BN backward + dW / db: one launch (linear_head_bwd_kernel)
-                done = native().linear_head_bwd_bn(ptr(dl), ptr(weight), ptr(x), B, F, J, ptr(g),
-                                                   bnf, bna, ptr(gw), ptr(gb), stream_handle())
-            else:
-                done = native().linear_dx_bn(ptr(dl), ptr(weight), B, F, J, ptr(g), bnf, bna,
-                                             stream_handle())
-                if done:
-                    native().linear_bwd(ptr(dl), ptr(x), ptr(weight), B, F, J, ptr(g), 0,
-                                        ptr(gw), ptr(gb), stream_handle())
+            # dx + the block's whole BN backward + dW / db: one launch (linear_head_bwd_kernel)
+            done = native().linear_head_bwd_bn(ptr(dl), ptr(weight), ptr(x), B, F, J, ptr(g),
+                                               bnf, bna, ptr(gw), ptr(gb), stream_handle())
             if done:  # dx never materialised: the block's backward takes dz_prev
                 prev.dz_fused = (dz_prev, pz)
                 grad_ready([weight, bias])

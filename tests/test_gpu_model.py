@@ -288,7 +288,7 @@ def test_bn_fused_into_splitk_finishes_matches_unfused(native_ext):
     """BatchNorm forward fused into the split-K finish of the small forward GEMMs and the
     preceding block's whole BatchNorm backward completed in the small dgrads' finishes
     (ops.layers BN_FWD_FUSE / BN_BWD_APPLY_FUSE, conv_igemm.hip splitk_finish_bnfwd_kernel /
-    splitk_finish_bnbwd_kernel, and the head's linear_dx_bnbwd_kernel) vs the separate finish +
+    splitk_finish_bnbwd_kernel, and the head's linear_head_bwd_kernel) vs the separate finish +
     BN kernels, at the 8-GPU share of the
     reference batch (32 images): same loss, gradients within the run-to-run spread of two
     unfused runs; the fused launches must actually be taken."""
