@@ -2657,7 +2657,7 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
   if (g_pair_mode == 3 && !both64 && itd + itw > g_pair_items) return separate();
   if (d.d2x2 && d.has_bnf && d.splits < 2) return separate();
   const bool bnf1 = d.has_bnf && d.splits <= 1;
-  if (bnf1) {  } else if (bnf1) {
+  if (bnf1) {
     hipLaunchKernelGGL((conv_bwd_pair_kernel<64, 64, 3, 1>), dim3(itd + itw), dim3(256), 0, st,
                        d, w, itd);
   } else {

@@ -222,7 +222,12 @@ HEAD_BN_FUSE = os.environ.get("DDP_AMD_HEAD_BN_FUSE", "1") != "0"
 # ... and its BN + ReLU + 2x2 pool FORWARD folded into the head's forward kernel (linear_ce.hip
 # HeadBnIn: one launch fewer; the training loss path only, VGG's 2x2 last block)
 HEAD_BN_FWD = os.environ.get("DDP_AMD_HEAD_BN_FWD", "1") != "0"
-BN_BWD_FUSE_MAX_HW = int(os.environ.get("DDP_AMD_BN_BWD_FUSE_MAX_HW", "16"))
+# largest dgrad output H*W that takes the fused sums: 16 (4x4 / 2x2) from 128 images per GPU up,
+# 256 (also 16x16 / 8x8) at the strong-scaling shares of at most 64 images (b64 0.4556 vs 0.4594
+# ms, b32 0.3921 vs 0.3952; b128 / b256 unchanged, profiles/r4z3_bn_sums_threshold.md); the
+# environment variable sets one threshold for every batch
+_MAX_HW_ENV = os.environ.get("DDP_AMD_BN_BWD_FUSE_MAX_HW")
+BN_BWD_FUSE_MAX_HW = int(_MAX_HW_ENV) if _MAX_HW_ENV else None
 # preceding block without a max-pool (ResNet's conv1 -> conv2 -> conv3 chain): one z load per
 # dgrad output element in the epilogue would replace a whole dy + z pass of the reduce kernel,
 # but measured on ResNet-50 b256 the BNF epilogue makes the big dgrad GEMMs slower than the pass
@@ -230,17 +235,21 @@ BN_BWD_FUSE_MAX_HW = int(os.environ.get("DDP_AMD_BN_BWD_FUSE_MAX_HW", "16"))
 BN_BWD_FUSE_NOPOOL = os.environ.get("DDP_AMD_BN_BWD_FUSE_NOPOOL", "0") == "1"
 
 
-def bn_bwd_fuse_pays(H, W, pool=True):
+def bn_bwd_fuse_pays(H, W, pool=True, N=None):
     """Fuse the preceding block's BatchNorm-backward sums into this dgrad only when the dgrad
-    output is spatially small (H*W <= 16: VGG's 4x4 / 2x2 layers). Measured (VGG-11 b256 and
-    b32, tools/conv_tune.py and the step profiles): there the fused epilogue costs 2-5 us less
-    than the reduce kernel it replaces; on 16x16 / 8x8 outputs its z gather (4 loads per pooled
-    pixel, exposed after the MFMA loop) costs 10-15 us MORE than the streaming reduce kernel.
+    output is spatially small: H*W <= 16 (VGG's 4x4 / 2x2 layers), or <= 256 at N <= 64 images
+    (BN_BWD_FUSE_MAX_HW). Measured (VGG-11, tools/conv_tune.py and the step profiles): on the
+    small outputs the fused epilogue costs 2-5 us less than the reduce kernel it replaces; on the
+    b128 / b256 16x16 / 8x8 outputs its z gather (4 loads per pooled pixel, exposed after the
+    MFMA loop) costs as much as the streaming reduce pass, at b32 / b64 the launch it saves wins.
     Without a pool (one z load per element): only with DDP_AMD_BN_BWD_FUSE_NOPOOL=1 (measured
-    slower on ResNet-50, profiles/r2_resnet50_b256.md)."""
+    slower on ResNet-50, profiles/r2_resnet50_b256.md, again in round 4: 9443 vs 9573 img/s)."""
     if not pool:
         return BN_BWD_FUSE_NOPOOL
-    return H * W <= BN_BWD_FUSE_MAX_HW
+    lim = BN_BWD_FUSE_MAX_HW
+    if lim is None:
+        lim = 256 if N is not None and N <= 64 else 16
+    return H * W <= lim
 
 
 def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=None, bna=None):
@@ -488,7 +497,7 @@ class _ConvBNActFn(torch.autograd.Function):
         if (_common.BN_BWD_FUSE and prev is not None and ctx.prev_z is not None
                 and ctx.needs_input_grad[0] and ctx.in_link is None and spec.stride == 1
                 and not prev.residual and prev.K == spec.C and spec.C == spec.Cr
-                and bn_bwd_fuse_pays(x.shape[1], x.shape[2], prev.pool)):
+                and bn_bwd_fuse_pays(x.shape[1], x.shape[2], prev.pool, x.shape[0])):
             pz = ctx.prev_z
             bnf = (ptr(pz), ptr(prev.coef), ptr(prev.sums), int(prev.pool), int(prev.relu),
                    pz.shape[1], pz.shape[2])

@@ -245,21 +245,26 @@ def test_backward_side_stream_matches_single_stream(native_ext, model_name):
         assert cos(ga, gb) > min(0.98, base - 0.1), (n, cos(ga, gb), base)
 
 
-def test_bn_backward_fused_sums_match_reduce_kernel(native_ext):
+@pytest.mark.parametrize("batch,max_hw", [(64, 16), (256, 64), (32, 256)])
+def test_bn_backward_fused_sums_match_reduce_kernel(native_ext, batch, max_hw):
     """BatchNorm-backward sums accumulated by the next layer's dgrad epilogue / split-K finish
     (ops.common.BN_BWD_FUSE) give the same gradients as the separate reduce kernel, within the
-    run-to-run noise of two unfused runs."""
+    run-to-run noise of two unfused runs. ``max_hw`` = ops.layers.BN_BWD_FUSE_MAX_HW: 64 / 256
+    also fuse the 8x8 / 16x16 dgrad outputs, where the backward pair runs with the sums in its
+    single-split epilogue (conv_bwd_pair_kernel<..., 1>)."""
     from ddp_amd.models import VGG11
     from ddp_amd.engine import CrossEntropyLoss
     from ddp_amd.optim import FusedSGD
-    from ddp_amd.ops import common
+    from ddp_amd.ops import common, layers
     torch.manual_seed(0)
     a = VGG11().cuda()
     b, c = copy.deepcopy(a), copy.deepcopy(a)
-    x = torch.randn(64, 3, 32, 32, device="cuda")
-    y = torch.randint(0, 10, (64,), device="cuda")
+    x = torch.randn(batch, 3, 32, 32, device="cuda")
+    y = torch.randint(0, 10, (batch,), device="cuda")
     grads = []
     saved = common.BN_BWD_FUSE
+    saved_hw = layers.BN_BWD_FUSE_MAX_HW
+    layers.BN_BWD_FUSE_MAX_HW = max_hw
     try:
         for m, fuse in ((a, True), (b, False), (c, False)):
             common.BN_BWD_FUSE = fuse
@@ -270,6 +275,7 @@ def test_bn_backward_fused_sums_match_reduce_kernel(native_ext):
             grads.append([p.grad.clone() for p in m.parameters()])
     finally:
         common.BN_BWD_FUSE = saved
+        layers.BN_BWD_FUSE_MAX_HW = saved_hw
 
     def cos(u, v):
         return float(torch.dot(u.reshape(-1), v.reshape(-1)) / (u.norm() * v.norm() + 1e-20))

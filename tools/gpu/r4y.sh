@@ -10,3 +10,10 @@ timeout -k 10 200 python bench.py > $O/bench_default.log 2>&1 || { tail -5 $O/be
 tail -1 $O/bench_default.log
 timeout -k 10 300 python bench.py --model resnet50 --steps 8 --warmup 4 --ref-window 0 > $O/resnet.log 2>&1 || { tail -5 $O/resnet.log; exit 1; }
 tail -1 $O/resnet.log | cut -c1-200
+# A/B: the no-pool BN-backward epilogue fusion on ResNet-50, the BN-sums fusion on 8x8 outputs
+timeout -k 10 300 env DDP_AMD_BN_BWD_FUSE_NOPOOL=1 python bench.py --model resnet50 --steps 8 --warmup 4 --ref-window 0 > $O/resnet_nopool.log 2>&1 || { tail -5 $O/resnet_nopool.log; exit 1; }
+echo "nopool: $(tail -1 $O/resnet_nopool.log | cut -c1-120)"
+for B in 32 64; do for hw in 16 64 16 64; do
+  timeout -k 10 200 env DDP_AMD_BN_BWD_FUSE_MAX_HW=$hw python bench.py --global-batch $B --steps 60 --warmup 10 --ref-window 0 > $O/b${B}_hw${hw}.log 2>&1 || { tail -5 $O/b${B}_hw${hw}.log; exit 1; }
+  echo "b$B hw$hw $(tail -1 $O/b${B}_hw${hw}.log | grep -oE '"ms_per_step": [0-9.]+')"
+done; done
