@@ -618,7 +618,8 @@ def test_vgg11_lr01_headline_regime_tracks_fp32_family(native_ext):
       * the spike is the model's: fp32's peak and the fused peak are both above 2 ln 10 or
         both below;
       * while the fp32 family agrees within 2 % (k < k0), fused tracks the emulated oracle within
-        3x its self-noise + 1 %;
+        1 % plus the larger of 3x its self-noise and the family's own spread at that step (the
+        half-ulp weight perturbations alone move the fp32 loss by up to ~1.5 % at step 2);
       * the fused mean loss over steps 10..19 (the bench's timed window after warm-up) lies in
         the family's range widened by 25 %, and the fused final loss is below its peak."""
     import math
@@ -682,7 +683,9 @@ def test_vgg11_lr01_headline_regime_tracks_fp32_family(native_ext):
         k0 += 1
     floor = max([abs(a - b) / abs(b) for a, b in zip(lg[:k0], lg2[:k0])] + [0.0])
     for k in range(k0):
-        assert abs(lg[k] - le[k]) / abs(le[k]) <= 3 * floor + 0.01, (k, lg[k], le[k], floor)
+        fam_k = max(abs(f[k] - lf[k]) / abs(lf[k]) for f in fam)
+        assert abs(lg[k] - le[k]) / abs(le[k]) <= max(3 * floor, fam_k) + 0.01, \
+            (k, lg[k], le[k], floor, fam_k)
     w = slice(10, steps)
     means = [sum(f[w]) / len(f[w]) for f in fam]
     mg = sum(lg[w]) / len(lg[w])

@@ -98,7 +98,7 @@ def main():
             # (ops.layers BnBwdFuse): tune that variant. prev block's z is 2x larger if pooled.
             bn = None
             if (model == "vgg11" and prev_hw is not None and C == Cr
-                    and bn_bwd_fuse_pays(H, W, True, N)):
+                    and bn_bwd_fuse_pays(H, W, prev_hw != H, N)):
                 zh = prev_hw
                 pz = torch.randn(N, zh, zh, C, device=dev).to(torch.bfloat16)
                 pcoef = torch.rand(6 * C, device=dev)
@@ -229,7 +229,7 @@ def tune_pairs(args):
             # (VGG: the preceding block's BN-backward sums ride in the dgrad epilogue; ResNet
             # keeps its separate reduce pass by default, ops/common.py BN_BWD_FUSE_NOPOOL)
             if (model == "vgg11" and prev_hw is not None and C == Cr
-                    and bn_bwd_fuse_pays(H, W, True, N)):
+                    and bn_bwd_fuse_pays(H, W, prev_hw != H, N)):
                 pz = torch.randn(N, prev_hw, prev_hw, C, device=dev).to(torch.bfloat16)
                 pcoef = torch.rand(6 * C, device=dev)
                 psums = torch.zeros(16 * 2 * C, device=dev)
