@@ -66,6 +66,14 @@ def parse():
     p.add_argument("--zero", action="store_true",
                    help="pipelined DDP step with the ZeRO-1 sharded update (reduce-scatter -> "
                         "SGD on 1/N of the parameters -> all-gather, parallel/zero.py)")
+    p.add_argument("--update", default="auto",
+                   help="pipelined DDP step, per gradient bucket: 'allreduce' = fp32 all-reduce + "
+                        "replicated SGD; 'shard16' = fp32 reduce-scatter + SGD on this rank's "
+                        "shard + all-gather of the bf16 operand bytes (parallel/zero.py "
+                        "ShardedBf16Update: 25%% fewer wire bytes, 1/N of the SGD); 'auto' = the "
+                        "cheaper of the two per bucket from the all-reduce / reduce-scatter / "
+                        "all-gather timings of the start-up probe (parallel/cut_plan.py); or one "
+                        "code per bucket, last layers first, e.g. s16,s16,ar")
     p.add_argument("--lr", type=float, default=None,
                    help="SGD learning rate (default: the reference's 0.1 for VGG; 0.01 for "
                         "ResNet-50, whose random-init training on the synthetic data is chaotic "
@@ -201,11 +209,17 @@ def main():
             cuts = cut_plan["cuts"]
             args.segmented = ",".join(str(c) for c in cuts)
             cut_source = cut_plan["source"]
+    update_plan = None
     if segmented:
+        emu_gbps = float(os.environ.get("DDP_AMD_EMULATE_COMM_GBPS", "0"))
+        emu_world = int(os.environ.get("DDP_AMD_EMULATE_WORLD", "8"))
+        update_plan = choose_update(args, model, cuts, world, comm_table, cut_plan,
+                                    emu_world if (world == 1 and emu_gbps > 0) else world)
         step = SegmentedDDPStep(model, opt, criterion, loader, split=cuts,
                                 emulate=int(os.environ.get("DDP_AMD_EMULATE_COMM", "0")),
-                                emulate_gbps=float(os.environ.get("DDP_AMD_EMULATE_COMM_GBPS", "0")),
-                                grad_comm=args.grad_comm, zero=args.zero)
+                                emulate_gbps=emu_gbps, emulate_world=emu_world,
+                                grad_comm=args.grad_comm, zero=args.zero,
+                                update=update_plan["update"])
     elif args.zero:
         raise SystemExit("--zero needs the pipelined DDP step (--segmented with cuts, hipGraph)")
     else:
@@ -274,11 +288,15 @@ def main():
         step.pop_loss()
     consistent = True
     if world > 1:
+        if hasattr(step, "sync_masters"):
+            step.sync_masters()  # sharded updates: owners' fp32 masters to every rank
         consistent = check_replicas(arena, world)
     plan = comm_plan(args, world, step, model, cuts, segmented, comm_table)
     plan["cut_source"] = cut_source if segmented else None
     if cut_plan is not None:
         plan["cut_plan"] = cut_plan
+    if update_plan is not None:
+        plan["update_plan"] = update_plan
     ms = elapsed / args.steps * 1000.0
     value = global_batch * args.steps / elapsed
     out = {
@@ -307,7 +325,11 @@ def main():
                    "comm": (f"segmented@{args.segmented}" if segmented else "overlap-stream" if getattr(getattr(model, "reducer", None), "overlap",
                                                          lambda: False)() else "inline"),
                    "optimizer": f"SGD(lr={lr:g}, momentum=0.9, wd=1e-4) fused" +
-                                (", ZeRO-1 sharded" if args.zero else "")},
+                                (", ZeRO-1 sharded" if args.zero else "") +
+                                (", sharded update + bf16 operand all-gather on buckets "
+                                 + ",".join(str(j) for j, u in enumerate(update_plan["update"])
+                                            if u == "s16")
+                                 if update_plan and "s16" in update_plan["update"] else "")},
         "launcher": os.environ.get("DDP_AMD_LAUNCHER",
                                    "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ
                                    else ("env" if world > 1 else "single-process")),
@@ -368,13 +390,71 @@ def choose_cuts_on_node(model, opt, criterion, loader, args, world, comm_table):
     stage_us = [float(v) for v in t]
     rows, table_src = rows_for(comm_table or load_table(), world, args.grad_comm)
     wire = 0.5 if args.grad_comm == "bf16" else 1.0
-    best, ranked = plan_cuts(stage_us, pbytes, rows, wire_scale=wire)
+    upd = "auto" if (args.update == "auto" and args.grad_comm == "fp32" and not args.zero) else \
+        ("shard16" if args.update == "shard16" else "allreduce")
+    best, ranked = plan_cuts(stage_us, pbytes, rows, wire_scale=wire, update=upd, world=world)
     return {"source": "probe" if comm_table is not None else "table", "comm_table": table_src,
             "cuts": best["cuts"], "stage_us": [round(v, 1) for v in stage_us],
             "stage_param_bytes": pbytes, "bucket_bytes": best["bucket_bytes"],
             "predicted_allreduce_us": [round(v, 1) for v in best["allreduce_us"]],
             "predicted_step_us": round(best["step_us"], 1),
-            "predicted_exposed_us": round(best["exposed_us"], 1), "top5": ranked[:5]}
+            "predicted_exposed_us": round(best["exposed_us"], 1), "update": best["update"],
+            "top5": ranked[:5]}
+
+
+def choose_update(args, model, cuts, world, comm_table, cut_plan, plan_world):
+    """Per-bucket update plan of the pipelined step ("ar" = all-reduce + replicated SGD, "s16" =
+    reduce-scatter + shard SGD + bf16 operand all-gather). --update allreduce / shard16 force one
+    plan for every bucket; auto takes the cut planner's per-bucket choice when it ran, else
+    prices each bucket with parallel/cut_plan.py bucket_costs on the probe's (or the table's)
+    collective timings. The sharded plan needs fp32 gradients, no --zero, and buckets that
+    divide into 4-element multiples per rank (64-aligned buckets: 1, 2, 4, 8 ranks)."""
+    from ddp_amd.parallel.bucket_plan import load_table, rows_for
+    from ddp_amd.parallel.cut_plan import SGD_US_PER_BYTE, bucket_costs
+    inner = model.module
+    arena = model.arena
+    pidx = {id(p): i for i, p in enumerate(arena.params)}
+    first = sorted(pidx[id(inner.first_param_of_stage(c))] for c in cuts)
+    bounds = [len(arena.params)] + first[::-1] + [0]
+    ranges = []
+    for j in range(len(bounds) - 1):
+        i1, i0 = bounds[j], bounds[j + 1]
+        ranges.append((arena.offsets[i0], arena.offsets[i1] if i1 < len(arena.params) else arena.total))
+    nb = len(ranges)
+    if args.update not in ("auto", "allreduce", "shard16"):
+        codes = args.update.split(",")
+        if len(codes) != nb or any(c not in ("ar", "s16") for c in codes):
+            raise SystemExit(f"--update {args.update}: need {nb} codes (ar / s16) for cuts {cuts}")
+        return {"update": codes, "source": "forced per bucket"}
+    even = plan_world >= 1 and all((hi - lo) % plan_world == 0 and ((hi - lo) // plan_world) % 4 == 0
+                                   for lo, hi in ranges)
+    allowed = args.grad_comm == "fp32" and not args.zero and even
+    if args.update == "allreduce" or not allowed or (plan_world <= 1 and args.update == "auto"):
+        why = ("forced" if args.update == "allreduce" else "one rank: nothing to shard"
+               if plan_world <= 1 else "sharded plan not applicable (bf16 wire, --zero or "
+               "uneven shards)")
+        if args.update == "shard16" and not allowed:
+            raise SystemExit("--update shard16 needs --grad-comm fp32, no --zero and buckets "
+                             f"divisible by {plan_world} ranks")
+        return {"update": ["ar"] * nb, "source": why}
+    if args.update == "shard16":
+        return {"update": ["s16"] * nb, "source": "forced"}
+    if cut_plan is not None and cut_plan.get("update") and len(cut_plan["update"]) == nb:
+        return {"update": list(cut_plan["update"]), "source": "cut planner"}
+    emu_gbps = float(os.environ.get("DDP_AMD_EMULATE_COMM_GBPS", "0"))
+    if world == 1 and emu_gbps > 0:  # one-GPU stand-in study: price the stand-in itself
+        from ddp_amd.parallel.cut_plan import stand_in_rows
+        rows, src = stand_in_rows(plan_world, emu_gbps), f"stand-in {emu_gbps:g} GB/s"
+    else:
+        rows, src = rows_for(comm_table or load_table(), max(plan_world, 2), "fp32")
+    sgd = (lambda b: b * SGD_US_PER_BYTE)
+    out, costs = [], []
+    for lo, hi in ranges:
+        (t_ar, u_ar), (t_s, u_s) = bucket_costs(rows, 4 * (hi - lo), 1.0, plan_world, sgd)
+        out.append("s16" if t_s + u_s < t_ar + u_ar else "ar")
+        costs.append({"bytes": 4 * (hi - lo), "ar_us": round(t_ar + u_ar, 1),
+                      "s16_us": round(t_s + u_s, 1)})
+    return {"update": out, "source": f"priced on {src}", "bucket_costs": costs}
 
 
 def native_version():

@@ -453,9 +453,7 @@ PYBIND11_MODULE(_native, m) {
     check(ddp_sgd(P<float>(p), P<float>(g), P<float>(buf), n, lr, momentum, wd, grad_scale,
                   nesterov, S(st)), "sgd");
   });
-  m.def("conv_options", [](int persistent, int stages) {
-    ddp_conv_options(persistent, stages);
-  }, py::arg("persistent") = 0, py::arg("stages") = 2);
+  m.def("conv_options", [](int stages) { ddp_conv_options(stages); }, py::arg("stages") = 2);
   // measured tile/split table (mode 0 fwd, 1 dgrad, 2 wgrad; GEMM dims M, N, K; tile 0..3 =
   // 128x128, 128x64, 64x128, 64x64) and the forced-tile switch used by tools/conv_tune.py
   m.def("conv_tune_set", [](int mode, int M, int N, int K, int tile, int splits, int stages) {
@@ -484,14 +482,41 @@ PYBIND11_MODULE(_native, m) {
   m.def("sgd_pack", [](uintptr_t items, int n_items, uintptr_t descs, uintptr_t p, uintptr_t g,
                        uintptr_t buf, float lr, float momentum, float wd, float grad_scale,
                        int nesterov, uintptr_t st, int zero_grad, uintptr_t counter, int delta,
-                       uintptr_t skip) {
+                       uintptr_t skip, uintptr_t shadow, uintptr_t slot, uintptr_t done,
+                       uintptr_t signal) {
     check(ddp_sgd_pack(P<void>(items), n_items, P<long long>(descs), P<float>(p), P<float>(g),
                        P<float>(buf), lr, momentum, wd, grad_scale, nesterov, zero_grad,
-                       P<int>(counter), delta, P<const unsigned>(skip), S(st)), "sgd_pack");
+                       P<int>(counter), delta, P<const unsigned>(skip), P<unsigned short>(shadow),
+                       P<float>(slot), P<unsigned>(done), P<unsigned>(signal), S(st)),
+          "sgd_pack");
   }, py::arg("items"), py::arg("n_items"), py::arg("descs"), py::arg("p"), py::arg("g"),
      py::arg("buf"), py::arg("lr"), py::arg("momentum"), py::arg("wd"), py::arg("grad_scale"),
      py::arg("nesterov"), py::arg("stream"), py::arg("zero_grad") = 0, py::arg("counter") = 0,
-     py::arg("delta") = 0, py::arg("skip") = 0);
+     py::arg("delta") = 0, py::arg("skip") = 0, py::arg("shadow") = 0, py::arg("slot") = 0,
+     py::arg("done") = 0, py::arg("signal") = 0);
+  // descs: list of (p, wc, wt, K, Cr, C, R, S, krsc) as in pack_conv_weights
+  m.def("shard_tail", [](uintptr_t segs, int n_segs, uintptr_t src, uintptr_t dst,
+                         std::vector<std::tuple<uintptr_t, uintptr_t, uintptr_t, int, int, int,
+                                                int, int, int>> descs,
+                         uintptr_t done, uintptr_t signal, uintptr_t skip, uintptr_t st) {
+    std::vector<ddp_amd::PackDesc> d;
+    for (auto& t : descs) {
+      ddp_amd::PackDesc x;
+      x.p = P<float>(std::get<0>(t));
+      x.wc = P<unsigned short>(std::get<1>(t));
+      x.wt = P<unsigned short>(std::get<2>(t));
+      x.K = std::get<3>(t); x.Cr = std::get<4>(t); x.C = std::get<5>(t);
+      x.R = std::get<6>(t); x.S = std::get<7>(t);
+      x.krsc = std::get<8>(t);
+      d.push_back(x);
+    }
+    check(ddp_shard_tail(P<void>(segs), n_segs, P<float>(src), P<float>(dst), d.data(),
+                         (int)d.size(), P<unsigned>(done), P<unsigned>(signal),
+                         P<const unsigned>(skip), S(st)), "shard_tail");
+  });
+  m.def("seg_copy_f32", [](uintptr_t table, int n, uintptr_t src, uintptr_t dst, uintptr_t st) {
+    check(ddp_seg_copy_f32(P<void>(table), n, P<float>(src), P<float>(dst), S(st)), "seg_copy_f32");
+  });
   m.def("sgd_tile_dims", [](int RS) {
     int tk, tc;
     ddp_sgd_tile_dims(RS, &tk, &tc);
@@ -606,6 +631,10 @@ PYBIND11_MODULE(_native, m) {
       })
       .def("all_gather", [](RcclComm& c, uintptr_t s, uintptr_t r, size_t n, int dt, uintptr_t st) {
         c.all_gather(P<void>(s), P<void>(r), n, dt, S(st));
+      })
+      .def("all_gather2", [](RcclComm& c, uintptr_t s1, uintptr_t r1, size_t n1, int dt1,
+                             uintptr_t s2, uintptr_t r2, size_t n2, int dt2, uintptr_t st) {
+        c.all_gather2(P<void>(s1), P<void>(r1), n1, dt1, P<void>(s2), P<void>(r2), n2, dt2, S(st));
       })
       .def("reduce_scatter", [](RcclComm& c, uintptr_t s, uintptr_t r, size_t n, int dt, int op,
                                 uintptr_t st) { c.reduce_scatter(P<void>(s), P<void>(r), n, dt, op, S(st)); })

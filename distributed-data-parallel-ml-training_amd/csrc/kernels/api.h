@@ -238,7 +238,7 @@ int ddp_sgd(float* p, const float* g, float* buf, size_t n, float lr, float mome
             float grad_scale, int nesterov, hipStream_t st);
 int ddp_conv_fwd_smallk(const ddp_amd::ConvGeom* g, const void* x, const void* wc,
                         const float* bias, void* y, float* stats, hipStream_t st);
-void ddp_conv_options(int persistent, int stages);
+void ddp_conv_options(int stages);
 void ddp_conv_epi_stage_set(int on);
 int ddp_bn_pool3_fwd(const ddp_amd::BnArgs* a, unsigned char* idx, hipStream_t st);
 int ddp_bn_pool3_bwd(const ddp_amd::BnArgs* a, const unsigned char* idx, hipStream_t st);
@@ -267,7 +267,14 @@ void ddp_conv_force_tile(int tile_plus_one, int stages);
 int ddp_pack_conv_weights(const ddp_amd::PackDesc* descs, int n, hipStream_t st);
 int ddp_sgd_pack(const void* items, int n_items, const long long* descs, float* p, float* g,
                  float* buf, float lr, float momentum, float wd, float grad_scale, int nesterov,
-                 int zero_grad, int* counter, int delta, const unsigned* skip, hipStream_t st);
+                 int zero_grad, int* counter, int delta, const unsigned* skip,
+                 unsigned short* shadow, float* slot, unsigned* done, unsigned* signal,
+                 hipStream_t st);
+// tail of a pipelined step with sharded buckets: gathered small-tensor slots -> fp32 arena,
+// re-pack of channel-padded conv operands, then release-increment ``signal`` (optim.hip)
+int ddp_shard_tail(const void* segs, int n_segs, const float* src, float* dst,
+                   const ddp_amd::PackDesc* pack, int n_pack, unsigned* done, unsigned* signal,
+                   const unsigned* skip, hipStream_t st);
 void ddp_sgd_tile_dims(int RS, int* TK, int* TC);
 int ddp_counter_add(int* c, int delta, hipStream_t st);
 int ddp_synth_generate(unsigned char* images, int* labels, int n, int pix_per_img,
@@ -292,5 +299,7 @@ int ddp_flag_signal(unsigned* flag, hipStream_t st);
 int ddp_flag_wait(const unsigned* flag, unsigned* expected, unsigned* err, float timeout_s,
                   hipStream_t st);
 int ddp_pack_bf16(const float* x, size_t n, unsigned short* y, hipStream_t st);
+// segment copy of fp32 runs: table of int4 {src_index, dst_index, count, -}, one block each
+int ddp_seg_copy_f32(const void* table, int n, const float* src, float* dst, hipStream_t st);
 int ddp_unpack_bf16(const unsigned short* y, size_t n, float* x, hipStream_t st);
 }

@@ -6,8 +6,9 @@
 // scale   : x *= s (2B's `param.grad /= world_size`, part2/part2b/main.py:103, when the
 //           backend has no native average).
 // comm_standin : world-1 stand-in for a collective (overlap studies on one GPU): a few blocks
-//           (like RCCL's channels) make one read+write pass over the bucket, then hold their
-//           CUs until the modelled transfer time has elapsed (s_sleep on the constant clock).
+//           (like RCCL's channels) make one read+write pass over the bucket and hold their
+//           CUs until the modelled transfer time has elapsed since the kernel started
+//           (s_sleep on the constant clock).
 // flag_signal / flag_wait : device-side stream edge between the step graph and the comm stream
 //           (engine/step.py SegmentedDDPStep): signal = one agent-scope release increment of a
 //           counter; wait = one wave spins (s_sleep) until the counter reaches the next expected
@@ -39,10 +40,12 @@ __global__ __launch_bounds__(256) void scale_kernel(float* x, size_t n, float s)
 
 __global__ __launch_bounds__(256) void comm_standin_kernel(float* x, size_t n, long long ticks,
                                                            float scale) {
-  // hold the CU for the modelled transfer time, THEN write the bucket (x *= scale): with
-  // scale != 1 a consumer that does not wait for the collective reads the old values (tests)
+  // one read + write pass over the bucket (x *= scale: with scale != 1 a consumer that does not
+  // wait for the collective reads the old values, tests), then hold the CU until the modelled
+  // time has elapsed since the kernel started: the modelled collective time INCLUDES its own
+  // memory traffic, as an RCCL kernel's does (until round 4 the pass ran after the full wait,
+  // adding ~20-30 us per 19 MB bucket on top of the model)
   const long long t0 = wall_clock64();
-  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(4);
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n / 4; i += stride) {
     float4 v = reinterpret_cast<float4*>(x)[i];
@@ -52,6 +55,7 @@ __global__ __launch_bounds__(256) void comm_standin_kernel(float* x, size_t n, l
   }
   if (blockIdx.x == 0)
     for (size_t i = (n / 4) * 4 + threadIdx.x; i < n; i += blockDim.x) x[i] *= scale;
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(4);
 }
 
 __global__ __launch_bounds__(64) void flag_signal_kernel(unsigned* flag) {
@@ -139,9 +143,27 @@ __global__ __launch_bounds__(256) void unpack_bf16_kernel(const unsigned short* 
     x[i] = bf2f(y[i]);
 }
 
+// fp32 segment copy: one block per {src_index, dst_index, count} entry (the sharded update's
+// unpack of the gathered small-tensor slots into the parameter arena)
+__global__ __launch_bounds__(256) void seg_copy_f32_kernel(const int4* __restrict__ table,
+                                                           const float* __restrict__ src,
+                                                           float* __restrict__ dst) {
+  const int4 e = table[blockIdx.x];
+  const float* s = src + (size_t)(unsigned)e.x;
+  float* d = dst + (size_t)(unsigned)e.y;
+  for (int i = threadIdx.x; i < e.z; i += 256) d[i] = s[i];
+}
+
 }  // namespace ddp_amd
 
 using namespace ddp_amd;
+
+extern "C" int ddp_seg_copy_f32(const void* table, int n, const float* src, float* dst,
+                                hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(seg_copy_f32_kernel, dim3(n), dim3(256), 0, st, (const int4*)table, src, dst);
+  return (int)hipGetLastError();
+}
 
 static unsigned blocks_for(size_t n) {
   size_t b = (n + 255) / 256;

@@ -1738,7 +1738,6 @@ static FastDiv make_fastdiv(int d) {
 
 static bool fits_buffer(size_t elems) { return elems * 2 < (size_t)kOOB; }
 
-static int g_persistent = 0;    // grid = resident slots, blocks loop over work items
 static int g_stages = 2;        // LDS ring depth policy (see stages_for)
 constexpr int kNumCUs = 256;
 // LDS-staged FWD / DGRAD epilogue (conv_igemm_body); DDP_AMD_EPI_STAGE=0 restores the direct
@@ -1821,17 +1820,9 @@ static void launch_gemm_t(const ConvArgs& a, int items, hipStream_t st) {
                               std::max(NST * kStageBytes, kTileBytes));
     attr = true;
   }
-  // persistent grid: at most the resident workgroup slots (queried once per instantiation)
-  static int resident = 0;
-  if (resident == 0) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 256, NST * kStageBytes) != hipSuccess ||
-        nb < 1)
-      nb = 1;
-    resident = nb;
-  }
-  const int grid = g_persistent ? std::min(items, kNumCUs * resident) : items;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, a);
+  // one work item (tile x split) per workgroup (a persistent grid sized to the resident slots
+  // was measured no faster and removed in round 5)
+  hipLaunchKernelGGL(kern, dim3(items), dim3(256), lds, st, a);
 }
 
 template <int MODE, int BM, int BN, int NST>
@@ -2171,10 +2162,7 @@ static void launch_mode(ConvArgs& a, size_t ws_elems, hipStream_t st) {
   }
 }
 
-extern "C" void ddp_conv_options(int persistent, int stages) {
-  g_persistent = persistent;
-  g_stages = stages;
-}
+extern "C" void ddp_conv_options(int stages) { g_stages = stages; }
 
 // tile: index into the launch_mode table (0..kNumTiles-1)
 extern "C" void ddp_conv_tune_set(int mode, int M, int N, int K, int tile, int splits, int stages) {

@@ -121,7 +121,38 @@ struct SgdHyper {
   // a gradient bucket timed out — the update is then skipped instead of applying gradients
   // that were never averaged (the host raises on the error at its next check)
   const unsigned* skip;
+  // sharded update with a bf16 operand all-gather (parallel/zero.py ShardedBf16Update): item 3
+  // also stores bf16(new p) into ``shadow`` (the bf16 operand image of the arena, same element
+  // index) and, for the small fp32-wire tensors, the new p into ``slot`` (the all-gather send slot)
+  unsigned short* shadow;
+  float* slot;
+  // optional completion signal (engine/step.py SegmentedDDPStep, last bucket): the last block
+  // to finish (``done`` ticket, reset by it) release-increments ``signal`` — the step's
+  // "every parameter updated" flag without a separate signal launch
+  unsigned* done;
+  unsigned* signal;
 };
+
+// Last-block-done hand-off: every block's writes are fenced, the block that takes the last
+// ticket resets the ticket and release-increments the flag (acquired by flag_wait_kernel).
+__device__ __forceinline__ bool last_block_done(unsigned* done) {
+  __syncthreads();
+  __shared__ unsigned last;
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const unsigned t = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    last = (t == gridDim.x - 1) ? 1u : 0u;
+  }
+  __syncthreads();
+  return last != 0u;
+}
+
+__device__ __forceinline__ void signal_flag(unsigned* done, unsigned* signal) {
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(signal, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 
 __device__ __forceinline__ float sgd1(float p, float g, float& b, const SgdHyper& h) {
   float d = g * h.grad_scale + h.wd * p;
@@ -132,12 +163,23 @@ __device__ __forceinline__ float sgd1(float p, float g, float& b, const SgdHyper
   return p - h.lr * d;
 }
 
+__device__ void sgd_pack_body(const int4* __restrict__ items, const long long* __restrict__ descs,
+                              float* __restrict__ p, float* __restrict__ g,
+                              float* __restrict__ buf, const SgdHyper& h, float* tile);
+
 __global__ __launch_bounds__(256) void sgd_pack_kernel(const int4* __restrict__ items,
                                                        const long long* __restrict__ descs,
                                                        float* __restrict__ p,
                                                        float* __restrict__ g,
                                                        float* __restrict__ buf, SgdHyper h) {
   __shared__ float tile[kTileElems];
+  sgd_pack_body(items, descs, p, g, buf, h, tile);
+  if (h.signal && last_block_done(h.done)) signal_flag(h.done, h.signal);
+}
+
+__device__ void sgd_pack_body(const int4* __restrict__ items, const long long* __restrict__ descs,
+                              float* __restrict__ p, float* __restrict__ g,
+                              float* __restrict__ buf, const SgdHyper& h, float* tile) {
   const int4 it = items[blockIdx.x];
   const int tid = threadIdx.x;
   if (h.counter && blockIdx.x == 0 && tid == 0) atomicAdd(h.counter, h.delta);
@@ -166,6 +208,42 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(const int4* __restrict__ 
         }
       }
     }
+    return;
+  }
+  if (it.x == 3) {
+    // {3, offset, count, slot_offset | -1}: this rank's shard of a sharded bucket — SGD on the
+    // fp32 master + momentum, bf16 operand image of the new values, fp32 send slot of the
+    // small tensors (offset, count and slot_offset multiples of 4: 64-aligned tensors, shards
+    // of n/w with n % 64 == 0 and w | 8)
+    const size_t off = (size_t)(unsigned)it.y;
+    const int cnt = it.z;
+    float* slot = it.w >= 0 && h.slot ? h.slot + it.w : nullptr;
+    for (int i = tid * 4; i < cnt; i += 256 * 4) {
+      float4 pv = *reinterpret_cast<float4*>(p + off + i);
+      const float4 gv = *reinterpret_cast<const float4*>(g + off + i);
+      float4 bv = *reinterpret_cast<float4*>(buf + off + i);
+      pv.x = sgd1(pv.x, gv.x, bv.x, h);
+      pv.y = sgd1(pv.y, gv.y, bv.y, h);
+      pv.z = sgd1(pv.z, gv.z, bv.z, h);
+      pv.w = sgd1(pv.w, gv.w, bv.w, h);
+      *reinterpret_cast<float4*>(p + off + i) = pv;
+      *reinterpret_cast<float4*>(buf + off + i) = bv;
+      if (h.zero_grad) *reinterpret_cast<float4*>(g + off + i) = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (h.shadow) {
+        uint2 pk;
+        pk.x = (unsigned)f2bf(pv.x) | ((unsigned)f2bf(pv.y) << 16);
+        pk.y = (unsigned)f2bf(pv.z) | ((unsigned)f2bf(pv.w) << 16);
+        *reinterpret_cast<uint2*>(h.shadow + off + i) = pk;
+      }
+      if (slot) *reinterpret_cast<float4*>(slot + i) = pv;
+    }
+    return;
+  }
+  if (it.x == 4) {
+    // {4, offset, count, -}: clear gradients outside this rank's shard (count multiple of 4)
+    const size_t off = (size_t)(unsigned)it.y;
+    for (int i = tid * 4; i < it.z; i += 256 * 4)
+      *reinterpret_cast<float4*>(g + off + i) = make_float4(0.f, 0.f, 0.f, 0.f);
     return;
   }
   if (it.x == 2) {
@@ -253,6 +331,54 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(const int4* __restrict__ 
   }
 }
 
+// Tail of a pipelined step with sharded buckets (parallel/zero.py ShardedBf16Update.tail): one
+// block per segment copies gathered small-tensor values (fp32 send slots of every rank) into
+// the fp32 parameter arena; the last block to finish re-packs the bf16 operand copies of the
+// channel-padded conv weights among them (their masters are complete only now) and signals
+// the step's "every parameter updated" flag. Segment entries: int4 {src, dst, count, -}.
+constexpr int kMaxTailPack = 4;
+struct TailArgs {
+  const int4* segs;
+  int n_segs;
+  const float* src;
+  float* dst;
+  PackDesc pack[kMaxTailPack];
+  int n_pack;
+  unsigned* done;
+  unsigned* signal;
+  const unsigned* skip;
+};
+
+__global__ __launch_bounds__(256) void shard_tail_kernel(TailArgs a) {
+  const bool skipped = a.skip && __hip_atomic_load(a.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+  if (!skipped && (int)blockIdx.x < a.n_segs) {
+    const int4 e = a.segs[blockIdx.x];
+    const float* s = a.src + (size_t)(unsigned)e.x;
+    float* d = a.dst + (size_t)(unsigned)e.y;
+    for (int i = threadIdx.x; i < e.z; i += 256) d[i] = s[i];
+  }
+  if (!last_block_done(a.done)) return;
+  __threadfence();  // acquire side: the other blocks' copies are visible to this block
+  if (!skipped) {
+    for (int q = 0; q < a.n_pack; ++q) {
+      const PackDesc& d = a.pack[q];
+      const int rs = d.R * d.S;
+      const int total = d.K * rs * d.C;
+      for (int i = threadIdx.x; i < total; i += 256) {  // Wc [k][r][s][c], zero padded c
+        const int c = i % d.C, t1 = i / d.C;
+        const int sx = t1 % d.S, t2 = t1 / d.S;
+        const int r = t2 % d.R, k = t2 / d.R;
+        const float v = c < d.Cr ? d.p[master_index(d, k, c, r, sx)] : 0.f;
+        d.wc[i] = f2bf(v);
+      }
+    }
+    __syncthreads();
+    __threadfence();
+  }
+  if (a.signal) signal_flag(a.done, a.signal);
+  else if (threadIdx.x == 0) __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ void counter_add_kernel(int* c, int delta) {
   if (threadIdx.x == 0 && blockIdx.x == 0) *c += delta;
 }
@@ -291,11 +417,25 @@ extern "C" int ddp_pack_conv_weights(const PackDesc* descs, int n, hipStream_t s
 extern "C" int ddp_sgd_pack(const void* items, int n_items, const long long* descs, float* p,
                             float* g, float* buf, float lr, float momentum, float wd,
                             float grad_scale, int nesterov, int zero_grad, int* counter,
-                            int delta, const unsigned* skip, hipStream_t st) {
-  SgdHyper h{lr, momentum, wd, grad_scale, nesterov, zero_grad, counter, delta, skip};
+                            int delta, const unsigned* skip, unsigned short* shadow, float* slot,
+                            unsigned* done, unsigned* signal, hipStream_t st) {
+  SgdHyper h{lr, momentum, wd, grad_scale, nesterov, zero_grad, counter, delta, skip, shadow, slot,
+             done, signal};
   if (n_items <= 0) return 0;
   hipLaunchKernelGGL(sgd_pack_kernel, dim3(n_items), dim3(256), 0, st, (const int4*)items, descs,
                      p, g, buf, h);
+  return (int)hipGetLastError();
+}
+
+extern "C" int ddp_shard_tail(const void* segs, int n_segs, const float* src, float* dst,
+                              const PackDesc* pack, int n_pack, unsigned* done, unsigned* signal,
+                              const unsigned* skip, hipStream_t st) {
+  if (n_pack > kMaxTailPack || !done) return -1;
+  TailArgs a{};
+  a.segs = (const int4*)segs; a.n_segs = n_segs; a.src = src; a.dst = dst;
+  for (int i = 0; i < n_pack; ++i) a.pack[i] = pack[i];
+  a.n_pack = n_pack; a.done = done; a.signal = signal; a.skip = skip;
+  hipLaunchKernelGGL(shard_tail_kernel, dim3(n_segs > 0 ? n_segs : 1), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
 

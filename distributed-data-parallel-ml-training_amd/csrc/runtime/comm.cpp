@@ -120,6 +120,20 @@ void RcclComm::all_gather(const void* send, void* recv, size_t count, int dtype,
   NCCL_OK(ncclAllGather(send, recv, count, to_nccl(dtype), comm_, st));
 }
 
+void RcclComm::all_gather2(const void* send1, void* recv1, size_t count1, int dtype1,
+                           const void* send2, void* recv2, size_t count2, int dtype2,
+                           hipStream_t st) {
+  if (comm_ == nullptr) {
+    if (send1 != recv1) KERNEL_OK(ddp_copy_bytes(recv1, send1, count1 * dtype_bytes(dtype1), st));
+    if (send2 != recv2) KERNEL_OK(ddp_copy_bytes(recv2, send2, count2 * dtype_bytes(dtype2), st));
+    return;
+  }
+  NCCL_OK(ncclGroupStart());
+  if (count1) NCCL_OK(ncclAllGather(send1, recv1, count1, to_nccl(dtype1), comm_, st));
+  if (count2) NCCL_OK(ncclAllGather(send2, recv2, count2, to_nccl(dtype2), comm_, st));
+  NCCL_OK(ncclGroupEnd());
+}
+
 void RcclComm::reduce_scatter(const void* send, void* recv, size_t count, int dtype, int op,
                               hipStream_t st) {
   if (comm_ == nullptr) {

@@ -43,6 +43,10 @@ class RcclComm {
   void all_reduce(void* buf, size_t count, int dtype, int op, hipStream_t st);
   void broadcast(void* buf, size_t count, int dtype, int root, hipStream_t st);
   void all_gather(const void* send, void* recv, size_t count, int dtype, hipStream_t st);
+  // two all-gathers in ONE RCCL group (one launch): the sharded update's bf16 operand image and
+  // its small fp32 tensors (parallel/zero.py ShardedBf16Update)
+  void all_gather2(const void* send1, void* recv1, size_t count1, int dtype1, const void* send2,
+                   void* recv2, size_t count2, int dtype2, hipStream_t st);
   void reduce_scatter(const void* send, void* recv, size_t count, int dtype, int op, hipStream_t st);
   // gather: root receives world*count elements (rank-major) into recv; root's own slot copied.
   void gather(const void* send, void* recv, size_t count, int dtype, int root, hipStream_t st);

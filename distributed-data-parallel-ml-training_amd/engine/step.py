@@ -44,6 +44,9 @@ def sgd_in_backward_ok(model):
     collective, and not switched off (DDP_AMD_SGD_IN_BWD=0)."""
     if os.environ.get("DDP_AMD_SGD_IN_BWD", "1") == "0":
         return False
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return False  # gradients of a multi-rank job are reduced before any update
     if int(os.environ.get("DDP_AMD_EMULATE_COMM", "0")) > 0 or \
             float(os.environ.get("DDP_AMD_EMULATE_COMM_GBPS", "0")) > 0:
         return False
@@ -249,8 +252,12 @@ class SegmentedDDPStep(TrainStep):
     WAIT_TIMEOUT_S = 100.0  # a device-side wait that exceeds this records an error and returns
 
     def __init__(self, ddp, optimizer, criterion, loader, split=4, emulate=0, emulate_gbps=0.0,
-                 emulate_scale=1.0, grad_comm="fp32", zero=False, collectives=True):
+                 emulate_scale=1.0, grad_comm="fp32", zero=False, collectives=True,
+                 update="allreduce", emulate_world=8):
         super().__init__(ddp, optimizer, criterion, loader, sync=None, use_graph=True)
+        # every bucket's update runs on the comm stream after its collective: never in the
+        # backward (an emulated or single-rank collective still has to see the gradients)
+        self.opt_in_bwd = False
         inner = getattr(ddp, "module", None)
         if inner is None or not hasattr(inner, "forward_loss_split") or not self.fold_opt:
             raise ValueError("SegmentedDDPStep needs a DDP-wrapped model with forward_loss_split, "
@@ -284,8 +291,11 @@ class SegmentedDDPStep(TrainStep):
         prio = os.environ.get("DDP_AMD_COMM_PRIORITY", "high")
         self.comm_stream = torch.cuda.Stream(priority=-1 if prio == "high" else 0)
         self.comm_a = None
-        # collectives=False: no bucket all-reduce at all (profile_stage_times: per-segment
-        # compute times of a cut-everywhere step on a multi-rank job, state rolled back after)
+        # collectives=False: no collective at all — no bucket all-reduce, no BatchNorm-buffer
+        # broadcast (profile_stage_times: per-segment compute times of a cut-everywhere step on
+        # a multi-rank job, state rolled back after; a rank that fails there cannot leave its
+        # peers blocked inside a captured collective)
+        self.sync_buffers = bool(collectives)
         if collectives and is_live(ddp.comm):
             from ..parallel.comm import RcclCommunicator
             self.comm_a = RcclCommunicator(ddp.comm.rank, ddp.comm.world, ddp.comm.device,
@@ -295,21 +305,49 @@ class SegmentedDDPStep(TrainStep):
             warm = torch.zeros(64, dtype=torch.float32, device=loader.device)
             self.comm_a.all_reduce(warm)
             torch.cuda.synchronize()
-        # ZeRO-1 (parallel/zero.py): reduce-scatter -> SGD on this rank's shard -> all-gather of
-        # the updated parameters, per bucket, instead of all-reduce -> replicated SGD
+        # Per-bucket update plan (parallel/cut_plan.py prices both):
+        #   "ar"  all-reduce(avg) of the bucket's fp32 gradients -> replicated fused SGD
+        #   "s16" reduce-scatter fp32 -> SGD on this rank's shard -> ONE grouped all-gather of the
+        #         bf16 operand image + the small fp32 tensors (parallel/zero.py ShardedBf16Update)
+        # ``update``: "allreduce" (all "ar"), "shard16" (all "s16"), or one code per bucket.
+        # ``zero=True``: the fp32-master ZeRO-1 update of every bucket (ShardedUpdate).
+        if isinstance(update, str):
+            if update not in ("allreduce", "shard16"):
+                raise ValueError("update must be 'allreduce', 'shard16' or a per-bucket list")
+            update = ["s16" if update == "shard16" else "ar"] * len(self.buckets)
+        update = list(update)
+        if len(update) != len(self.buckets) or any(u not in ("ar", "s16") for u in update):
+            raise ValueError(f"per-bucket update plan {update} does not match "
+                             f"{len(self.buckets)} buckets")
+        self.update = update
         self.zero = None
+        self.shard16 = None
         if zero:
             if grad_comm != "fp32":
                 raise ValueError("the sharded (ZeRO-1) update communicates fp32 gradients")
             from ..parallel.zero import ShardedUpdate
             self.zero = ShardedUpdate(arena, optimizer, self.comm_a or ddp.comm,
                                       [((i0, i1), (lo, hi)) for (i0, i1), (lo, hi) in self.buckets])
+        elif "s16" in update:
+            if grad_comm != "fp32":
+                raise ValueError("the sharded bf16-gather update reduces fp32 gradients")
+            from ..parallel.zero import ShardedBf16Update
+            comm = self.comm_a or ddp.comm
+            if hasattr(inner, "fused_plan"):
+                inner.fused_plan()  # the operand copies (bf16 Wc) must exist to be re-pointed
+            emu = None
+            if comm.world == 1 and not is_live(comm) and (self.emulate or self.emulate_gbps > 0):
+                emu = int(emulate_world)  # stand-in: shard as rank 0 of an N-GPU job
+            self.shard16 = ShardedBf16Update(
+                arena, optimizer, comm,
+                [((i0, i1), (lo, hi)) for (i0, i1), (lo, hi) in self.buckets],
+                which=[j for j, u in enumerate(update) if u == "s16"], emulate_world=emu)
         self._stage = None
         if grad_comm == "bf16":
             self._stage = torch.empty(arena.total, dtype=torch.bfloat16, device=loader.device)
         # [0] = S (segment backward done, counts up), [1] = D (step's updates done), [2], [3] =
-        # the waiters' expected counts, [4] = error word. D starts at 1: the first step's forward
-        # has nothing to wait for.
+        # the waiters' expected counts, [4] = error word, [5] = last-block-done ticket of the
+        # launch that signals D. D starts at 1: the first step's forward has nothing to wait for.
         self._flags = torch.zeros(8, dtype=torch.int32, device=loader.device)
         self._flags[1] = 1
         self.graphs = None
@@ -352,7 +390,8 @@ class SegmentedDDPStep(TrainStep):
         main = torch.cuda.current_stream()
         native().flag_wait(self._fp(1), self._fp(3), self._fp(4), self.WAIT_TIMEOUT_S,
                            main.cuda_stream)
-        self.ddp._sync_buffers()  # what DDP.forward would do (no-op without buffers / at world 1)
+        if self.sync_buffers:
+            self.ddp._sync_buffers()  # what DDP.forward would do (no-op without buffers / world 1)
         with self.ddp.no_sync():
             with trace_range("data"):
                 x, y = self.loader.fill(advance=False)
@@ -389,8 +428,43 @@ class SegmentedDDPStep(TrainStep):
         if t0 is not None:
             self.probe.append((j, t0, self._probe_event(cs)))
 
+    def _standin(self, cs):
+        """Timed stand-in for one collective of the sharded update (one GPU): a 32-CU pass
+        lasting its modelled time at the all-reduce algorithm bandwidth ``emulate_gbps``; a
+        reduce-scatter or an all-gather moves half an all-reduce's bytes per input byte."""
+        from ..ops.common import native
+
+        def run(kind, nbytes, ptr, n):
+            if self.emulate_gbps > 0:
+                us = 0.5 * nbytes / (self.emulate_gbps * 1e3)
+                native().comm_standin(ptr, n, 32, us, self.emulate_scale if n else 1.0,
+                                      cs.cuda_stream)
+            else:
+                for _ in range(self.emulate):
+                    if n:
+                        native().scale(ptr, n, 1.0, cs.cuda_stream)
+        return run
+
     def _comm_body(self, j, cs, i0, i1, lo, hi, last):
         from ..ops.common import native
+        if self.shard16 is not None:
+            if self.update[j] == "s16":
+                with trace_range(f"shard16_update_bucket{j}"):
+                    self.shard16.step(j, stream=cs, skip=self._fp(4),
+                                      counter=self.loader.cursor_advance() if last else None,
+                                      standin=self._standin(cs) if self.comm_a is None else None)
+            else:
+                with trace_range(f"sync_bucket{j}"):
+                    self._allreduce(lo, hi, cs, self.comm_a)
+                with trace_range(f"optimizer_bucket{j}"):
+                    self.optimizer.step(zero_grad=True, params=(i0, i1), stream=cs,
+                                        skip=self._fp(4),
+                                        counter=self.loader.cursor_advance() if last else None)
+            if last:  # small-tensor unpack + operand re-pack + signal D, one launch
+                with trace_range("shard16_tail"):
+                    self.shard16.tail(stream=cs, done=self._fp(5), signal=self._fp(1),
+                                      skip=self._fp(4))
+            return
         if self.zero is not None:
             with trace_range(f"zero_update_bucket{j}"):
                 self.zero.step(j, stream=cs, skip=self._fp(4),
@@ -403,10 +477,11 @@ class SegmentedDDPStep(TrainStep):
         with trace_range(f"optimizer_bucket{j}"):
             # a timed-out wait (error word set) skips the update: never apply gradients whose
             # bucket was not averaged
+            # the last bucket's update launch also signals D (last-block-done ticket in
+            # flags[5]): no separate signal launch on the critical comm stream
             self.optimizer.step(zero_grad=True, params=(i0, i1), stream=cs, skip=self._fp(4),
-                                counter=self.loader.cursor_advance() if last else None)
-        if last:
-            native().flag_signal(self._fp(1), cs.cuda_stream)
+                                counter=self.loader.cursor_advance() if last else None,
+                                signal=(self._fp(5), self._fp(1)) if last else None)
 
     def _segments(self):
         return [self._seg_first] + [(lambda j=j: self._seg(j)) for j in range(1, len(self.buckets))]
@@ -455,10 +530,29 @@ class SegmentedDDPStep(TrainStep):
             raise RuntimeError("SegmentedDDPStep: a device-side stream wait timed out "
                                f"(> {self.WAIT_TIMEOUT_S}s); the step's results are invalid")
 
+    def sync_masters(self):
+        """Make every rank's fp32 master weights complete (the sharded update keeps each
+        operand tensor's master only on its shard owner): before check_replicas / state_dict."""
+        if self.shard16 is not None:
+            torch.cuda.current_stream().wait_stream(self.comm_stream)
+            self.shard16.gather_masters()
+            torch.cuda.synchronize()
+
     def validate_distributed(self, arena, world, timeout_s=120.0):
-        ok = super().validate_distributed(arena, world, timeout_s)
+        if world <= 1:
+            return True
+        self.step()
+        if not self.wait(timeout_s):
+            raise RuntimeError(f"captured step did not finish within {timeout_s}s "
+                               "(collective hang inside the hipGraph?)")
         self.check_error()
-        return ok
+        self.sync_masters()
+        from ..parallel.ddp import check_replicas
+        if check_replicas(arena, world):
+            return True
+        self.graph = self.graphs = None
+        self.eager_only = True
+        return False
 
     def pop_loss(self):
         v = super().pop_loss()
@@ -478,6 +572,10 @@ def profile_stage_times(ddp, optimizer, criterion, loader, n_stages, reps=4):
     parallel/cut_plan.plan_cuts."""
     arena = ddp.arena
     snap = (arena.data.clone(), optimizer.momentum_buffer.clone(), loader.cursor.clone())
+    # module buffers too (ResNet's BatchNorm running statistics): the profiling batches must
+    # not leave extra updates behind
+    bufs = [b for b in ddp.module.buffers()]
+    bsnap = [b.clone() for b in bufs]
     st = SegmentedDDPStep(ddp, optimizer, criterion, loader, split=list(range(1, n_stages)),
                           collectives=False)
     try:
@@ -497,6 +595,8 @@ def profile_stage_times(ddp, optimizer, criterion, loader, n_stages, reps=4):
         arena.data.copy_(snap[0])
         optimizer.momentum_buffer.copy_(snap[1])
         loader.cursor.copy_(snap[2])
+        for b, v in zip(bufs, bsnap):
+            b.copy_(v)
         arena.grad.zero_()
         optimizer.repack()
         torch.cuda.synchronize()

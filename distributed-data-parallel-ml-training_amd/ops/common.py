@@ -13,14 +13,11 @@ def native():
     global _NATIVE
     if _NATIVE is None:
         _NATIVE = _load()
-        # DDP_AMD_CONV_PERSISTENT=1: conv grids sized to the resident slots, blocks loop over
-        # tiles (default 0: one tile per workgroup)
         # DDP_AMD_CONV_STAGES: LDS ring depth policy of the conv GEMMs (2 = double buffering)
         # (split-K always goes through fp32 slabs + a deterministic finish: the fp32-atomic
         # variants measured 6-60 % slower steps, profiles/r2_launch_reduction_ab.md, and were
         # removed in round 4)
-        _NATIVE.conv_options(int(os.environ.get("DDP_AMD_CONV_PERSISTENT", "0")),
-                             int(os.environ.get("DDP_AMD_CONV_STAGES", str(CONV_STAGES))))
+        _NATIVE.conv_options(int(os.environ.get("DDP_AMD_CONV_STAGES", str(CONV_STAGES))))
         # DDP_AMD_BWD_PAIR: one layer's wgrad + dgrad as ONE grouped launch — 0 never,
         # 1 when both problems pick the 64x64 tile, 2 always (stride-1 layers), 3 (default)
         # also when the paired launch has <= DDP_AMD_BWD_PAIR_ITEMS (1024) work items
@@ -103,63 +100,6 @@ def workspace(device):
         ws = torch.empty(WORKSPACE_ELEMS, dtype=torch.float32, device=device)
         _WS[key] = ws
     return ws
-
-
-# ---------------------------------------------------------------- backward side stream
-# Weight gradients are off the backward's critical path (only the all-reduce / optimizer consume
-# them), while each layer's data gradient feeds the next layer. The conv backward therefore
-# runs wgrad (+ its split-K finish) on a side stream concurrently with dgrad and the next
-# layer's BatchNorm backward on the main stream: the two kernels fill each other's partial
-# waves (a 576-workgroup wgrad on 512 resident slots leaves most of the chip idle for its
-# second wave). Fork = side waits on main; join = an autograd end-of-backward callback makes
-# main wait on side. Tensors the side stream reads are kept alive until the join, so the
-# caching allocator cannot recycle them under a running wgrad. Captured into the step's
-# hipGraph as a fork/join of two branches. OFF by default (DDP_AMD_BWD_STREAMS=1 enables it):
-# measured on MI355X / ROCm 7, a captured step with cross-stream edges executes on several
-# hardware queues with a completion-signal hop per edge (~5-10 us gaps, inflated dispatches),
-# which cost more than the overlap gained (VGG-11 b256: 1.115 ms vs 1.00 ms single-stream).
-BWD_SIDE_STREAM = os.environ.get("DDP_AMD_BWD_STREAMS", "0") == "1"
-
-
-class _SideStream:
-    def __init__(self, device):
-        self.stream = torch.cuda.Stream(device=device)
-        # own split-K workspace: wgrad on the side stream runs concurrently with main-stream GEMMs
-        self.ws = torch.empty(WORKSPACE_ELEMS, dtype=torch.float32, device=device)
-        self.keep = []
-        self.main = None
-
-    def join(self):
-        if self.main is not None:
-            self.main.wait_stream(self.stream)
-        self.keep.clear()
-        self.main = None
-
-
-_SIDE = {}
-
-
-def side_stream(device, *keep):
-    """Fork the backward side stream off the current stream (first call of a backward pass also
-    queues the join). Returns the _SideStream; ``keep`` tensors stay alive until the join."""
-    key = str(device)
-    st = _SIDE.get(key)
-    if st is None:
-        st = _SideStream(device)
-        _SIDE[key] = st
-    cur = torch.cuda.current_stream(device)
-    if st.main is None:
-        st.main = cur
-        torch.autograd.Variable._execution_engine.queue_callback(st.join)
-    st.stream.wait_stream(cur)
-    st.keep.extend(keep)
-    return st
-
-
-def join_side_streams():
-    """Make the main stream wait on every side stream (outside autograd, e.g. after an error)."""
-    for st in _SIDE.values():
-        st.join()
 
 
 # (Round 4 built and removed two more backward variants, both measured slower on every config:

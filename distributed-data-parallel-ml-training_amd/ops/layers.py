@@ -16,7 +16,7 @@ import os
 import torch
 
 from .common import (native, ptr, stream_handle, check, grad_ready, ensure_grad, workspace,
-                     step_scratch, weight_krsc, side_stream, STAT_REPLICAS)
+                     step_scratch, weight_krsc, STAT_REPLICAS)
 from . import common as _common
 
 BF16 = torch.bfloat16
@@ -86,6 +86,15 @@ class ConvBNActSpec:
         w = self.conv.weight
         return (ptr(w), ptr(self.wc), ptr(self.wt), self.K, self.Cr, self.C,
                 self.R, self.S, weight_krsc(w))
+
+    def rebind_wc(self, flat):
+        """Make the bf16 operand copy a view of ``flat`` (same element order as Wc; the sharded
+        update's shadow arena, parallel/zero.py ShardedBf16Update). The next maybe_pack()
+        rebuilds it from the fp32 master."""
+        if flat.dtype != BF16 or flat.numel() != self.wc.numel():
+            raise ValueError("operand view must be bf16 with the operand copy's element count")
+        self.wc = flat.view(self.wc.shape)
+        self._packed_version = None
 
     def maybe_pack(self):
         w = self.conv.weight
@@ -228,11 +237,6 @@ HEAD_BN_FWD = os.environ.get("DDP_AMD_HEAD_BN_FWD", "1") != "0"
 # environment variable sets one threshold for every batch
 _MAX_HW_ENV = os.environ.get("DDP_AMD_BN_BWD_FUSE_MAX_HW")
 BN_BWD_FUSE_MAX_HW = int(_MAX_HW_ENV) if _MAX_HW_ENV else None
-# preceding block without a max-pool (ResNet's conv1 -> conv2 -> conv3 chain): one z load per
-# dgrad output element in the epilogue would replace a whole dy + z pass of the reduce kernel,
-# but measured on ResNet-50 b256 the BNF epilogue makes the big dgrad GEMMs slower than the pass
-# it saves (30.65 vs 28.23 ms/step, profiles/r2_resnet50_b256.md) -> opt-in (=1)
-BN_BWD_FUSE_NOPOOL = os.environ.get("DDP_AMD_BN_BWD_FUSE_NOPOOL", "0") == "1"
 
 
 def bn_bwd_fuse_pays(H, W, pool=True, N=None):
@@ -242,10 +246,12 @@ def bn_bwd_fuse_pays(H, W, pool=True, N=None):
     small outputs the fused epilogue costs 2-5 us less than the reduce kernel it replaces; on the
     b128 / b256 16x16 / 8x8 outputs its z gather (4 loads per pooled pixel, exposed after the
     MFMA loop) costs as much as the streaming reduce pass, at b32 / b64 the launch it saves wins.
-    Without a pool (one z load per element): only with DDP_AMD_BN_BWD_FUSE_NOPOOL=1 (measured
-    slower on ResNet-50, profiles/r2_resnet50_b256.md, again in round 4: 9443 vs 9573 img/s)."""
+    Never without a pool (ResNet's conv1 -> conv2 -> conv3 chain): one z load per dgrad output
+    element in the epilogue made the big dgrad GEMMs slower than the reduce pass it saves
+    (ResNet-50 b256 30.65 vs 28.23 ms, profiles/r2_resnet50_b256.md; again in round 4: 9443 vs
+    9573 img/s; the opt-in was removed in round 5)."""
     if not pool:
-        return BN_BWD_FUSE_NOPOOL
+        return False
     lim = BN_BWD_FUSE_MAX_HW
     if lim is None:
         lim = 256 if N is not None and N <= 64 else 16
@@ -253,10 +259,11 @@ def bn_bwd_fuse_pays(H, W, pool=True, N=None):
 
 
 def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=None, bna=None):
-    """dW += wgrad(dz, x); returns dx (or None). With ``weight`` (the parameter whose gradient
-    is dweight) and the backward side stream enabled, the wgrad runs on the side stream and the
-    parameter is announced ready there (common.side_stream); otherwise everything is stream-
-    ordered on the current stream and the caller announces the gradient.
+    """dW += wgrad(dz, x); returns dx (or None). Everything is stream-ordered on the current
+    stream; with ``weight`` (the parameter whose gradient is dweight) the gradient is announced
+    ready here, else by the caller. (A backward side stream for the wgrad was measured slower,
+    VGG-11 b256 1.115 vs 1.00 ms: a captured fork/join runs on several hardware queues with a
+    completion-signal hop per edge; removed in round 5.)
     ``bna`` = (dz_prev, dgamma_prev, dbeta_prev) pointers (with ``bnf``): the preceding block's
     whole BatchNorm backward may be completed in the dgrad's split-K finish; the return value is
     then (dx, done) — when done, dx was NOT written and dz_prev / dgamma / dbeta were."""
@@ -264,8 +271,7 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=Non
     g = spec.geom(N, H, W, weight_krsc(dweight))
     s = stream_handle()
     ws = workspace(x.device)
-    if (need_dx and link is None and not _common.BWD_SIDE_STREAM and spec.stride == 1
-            and spec.C == spec.Cr):
+    if need_dx and link is None and spec.stride == 1 and spec.C == spec.Cr:
         # wgrad + dgrad of this layer as one grouped launch (+ one finish launch) when the
         # kernel policy allows it (conv_igemm.hip ddp_conv_bwd_pair), else the two launches
         dx = torch.empty_like(x)
@@ -274,18 +280,11 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=Non
         if weight is not None:
             grad_ready([weight])
         return (dx, bool(done)) if bna is not None else dx
-    if weight is not None and _common.BWD_SIDE_STREAM:
-        side = side_stream(x.device, x, dz)
-        with torch.cuda.stream(side.stream):
-            native().conv_wgrad(g, ptr(dz), ptr(x), ptr(dweight), ptr(side.ws), side.ws.numel(), 0,
-                                side.stream.cuda_stream)
-            grad_ready([weight])
-    else:
-        # final: no dgrad of this layer follows, so its finish may apply a registered SGD step
-        native().conv_wgrad(g, ptr(dz), ptr(x), ptr(dweight), ptr(ws), ws.numel(), 0, s,
-                            final=int(not need_dx))
-        if weight is not None:
-            grad_ready([weight])
+    # final: no dgrad of this layer follows, so its finish may apply a registered SGD step
+    native().conv_wgrad(g, ptr(dz), ptr(x), ptr(dweight), ptr(ws), ws.numel(), 0, s,
+                        final=int(not need_dx))
+    if weight is not None:
+        grad_ready([weight])
     if not need_dx:
         return (None, False) if bna is not None else None
     if spec.C != spec.Cr:

@@ -205,14 +205,15 @@ class FusedSGD(torch.optim.SGD):
 
     @torch.no_grad()
     def step(self, closure=None, zero_grad=False, counter=None, skip=None, params=None,
-             stream=None, fused_taken=False):
+             stream=None, fused_taken=False, signal=None):
         """One fused launch. ``params = (i0, i1)``: only parameters i0 <= i < i1 (arena order);
         ``stream``: launch on this torch stream instead of the current one. ``zero_grad=True`` also clears every gradient after its use (the
         next step then needs no zero_grad fill); ``counter=(int32 device ptr, delta)`` is
         advanced by the same launch (the on-device data cursor of engine/step.py); ``skip`` =
         device pointer of a uint32 error word: the update is skipped when it is non-zero.
         ``fused_taken=True``: skip the parameters whose update the backward already applied
-        (register_in_backward)."""
+        (register_in_backward). ``signal = (ticket ptr, flag ptr)``: the launch's last block to
+        finish release-increments the uint32 flag (zeroed uint32 ticket)."""
         if not self._fused:
             out = super().step(closure)
             if zero_grad:
@@ -227,6 +228,8 @@ class FusedSGD(torch.optim.SGD):
         if n_items == 0:  # every tensor was updated in the backward: only the data cursor
             if counter:
                 native().counter_add(int(counter[0]), int(counter[1]), s)
+            if signal:
+                native().flag_signal(int(signal[1]), s)
             return None
         # one launch: SGD over every tensor + bf16 re-pack of every conv weight
         native().sgd_pack(items.data_ptr(), n_items, descs.data_ptr(), a.data.data_ptr(),
@@ -236,7 +239,9 @@ class FusedSGD(torch.optim.SGD):
                           zero_grad=int(bool(zero_grad)),
                           counter=int(counter[0]) if counter else 0,
                           delta=int(counter[1]) if counter else 0,
-                          skip=int(skip) if skip else 0)
+                          skip=int(skip) if skip else 0,
+                          done=int(signal[0]) if signal else 0,
+                          signal=int(signal[1]) if signal else 0)
         return None
 
     def state_dict(self):

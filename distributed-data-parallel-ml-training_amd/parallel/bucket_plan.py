@@ -129,6 +129,15 @@ def probe_table(comm, world, dtype="fp32", device="cuda", sizes=None, iters=10, 
     if not ok:
         raise RuntimeError("start-up all-reduce probe returned wrong sums (on at least one rank)")
     rows = [{k: r[k] for k in ("bytes", "us", "algbw_GBps", "busbw_GBps")} for r in rows]
+    if dtype == "fp32" and os.environ.get("DDP_AMD_SHARD_PROBE", "1") != "0":
+        # the sharded update's collectives at the same bucket sizes (parallel/cut_plan.py
+        # shard16_us prices it from these columns instead of the half-all-reduce model)
+        from .commbench import shard_sweep
+        sh = {r["bytes"]: r for r in shard_sweep(comm, [r["bytes"] for r in rows], device=device,
+                                                  iters=iters, warmup=warmup)}
+        for r in rows:
+            if r["bytes"] in sh:
+                r["rs_us"], r["ag16_us"] = sh[r["bytes"]]["rs_us"], sh[r["bytes"]]["ag16_us"]
     return {"worlds": {str(world): {"source": "measured at start-up", dtype: rows}}}
 
 
@@ -150,7 +159,8 @@ def merge_rows(path, world, dtype, rows, source="measured"):
     if ent.get("source") == "model":
         ent.clear()  # measured rows replace the model for this world size entirely
     ent["source"] = source
-    ent[dtype] = [{k: r[k] for k in ("bytes", "us", "algbw_GBps", "busbw_GBps") if k in r}
+    ent[dtype] = [{k: r[k] for k in ("bytes", "us", "algbw_GBps", "busbw_GBps", "rs_us",
+                                     "ag16_us") if k in r}
                   for r in rows if r.get("correct", True)]
     tmp = path + ".tmp"
     with open(tmp, "w") as f:

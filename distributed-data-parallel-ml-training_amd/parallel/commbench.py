@@ -60,3 +60,45 @@ def allreduce_sweep(comm, sizes, dtype=torch.float32, device="cpu", iters=20, wa
                      "busbw_GBps": round(algbw * 2 * (n - 1) / n, 3) if n > 1 else None,
                      "correct": ok})
     return rows
+
+
+def shard_sweep(comm, sizes, device="cpu", iters=20, warmup=5):
+    """Per fp32 bucket size S: mean time of a reduce-scatter(avg) of S bytes of fp32 and of an
+    all-gather of S/2 bytes of bf16 (the sharded update's two collectives, parallel/zero.py
+    ShardedBf16Update), max over ranks -> ``{"bytes", "rs_us", "ag16_us"}`` rows (merged into the
+    all-reduce rows by bucket_plan.probe_table; priced by parallel/cut_plan.py shard16_us)."""
+    from .comm import AVG
+    is_cuda = torch.device(device).type == "cuda"
+    n = comm.world
+    rows = []
+
+    def sync():
+        if is_cuda:
+            torch.cuda.synchronize()
+
+    def timed(fn):
+        for _ in range(warmup):
+            fn()
+        sync()
+        if dist.is_initialized() and n > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        sync()
+        dt = (time.perf_counter() - t0) / iters
+        if dist.is_initialized() and n > 1:
+            m = torch.tensor([dt], dtype=torch.float64)
+            dist.all_reduce(m, op=dist.ReduceOp.MAX)
+            dt = float(m.item())
+        return round(dt * 1e6, 2)
+
+    for nbytes in sizes:
+        numel = max(n * 4, nbytes // 4 // (4 * n) * (4 * n))
+        g = torch.ones(numel, dtype=torch.float32, device=device)
+        w = torch.zeros(numel, dtype=torch.bfloat16, device=device)
+        wv = w if is_cuda else w.view(torch.int32)  # Gloo: bf16 pairs as int32 words
+        rs = timed(lambda: comm.reduce_scatter_inplace(g, AVG))
+        ag = timed(lambda: comm.all_gather_inplace(wv))
+        rows.append({"bytes": numel * 4, "rs_us": rs, "ag16_us": ag})
+    return rows

@@ -37,21 +37,63 @@ COMM_OVERHEAD_US = 4.0
 CONTENTION = 0.15
 
 
+# the sharded bf16-gather update issues one more collective launch and one more small kernel
+# (the small-tensor unpack) per bucket than all-reduce + SGD
+SHARD16_EXTRA_US = COMM_OVERHEAD_US
+
+
+def shard16_us(rows, fp32_bytes, world):
+    """Reduce-scatter of ``fp32_bytes`` of gradients + all-gather of the bucket's bf16 operand
+    image (half the bytes). Measured columns of the start-up probe (``rs_us`` / ``ag16_us``,
+    parallel/commbench.py shard_sweep) when present, else the ring model: a reduce-scatter or an
+    all-gather of S input bytes moves half an all-reduce's traffic, t = 0.5 x t_allreduce(S)."""
+    if not rows:
+        return 0.0
+    if all("rs_us" in r and "ag16_us" in r for r in rows):
+        return _interp(rows, fp32_bytes, "rs_us") + _interp(rows, fp32_bytes, "ag16_us")
+    return 0.5 * predict_us(rows, fp32_bytes) + 0.5 * predict_us(rows, fp32_bytes // 2)
+
+
+def _interp(rows, nbytes, key):
+    """Column ``key`` (us) at ``nbytes``: linear in size between rows, proportional beyond."""
+    rs = sorted(rows, key=lambda r: r["bytes"])
+    if nbytes <= rs[0]["bytes"]:
+        return rs[0][key]
+    for a, b in zip(rs, rs[1:]):
+        if nbytes <= b["bytes"]:
+            t = (nbytes - a["bytes"]) / (b["bytes"] - a["bytes"])
+            return a[key] * (1 - t) + b[key] * t
+    return rs[-1][key] * nbytes / rs[-1]["bytes"]
+
+
+def bucket_costs(rows, pb, wire_scale, world, sgd):
+    """(all-reduce plan, sharded plan) of one bucket of ``pb`` fp32 parameter bytes, each as
+    (collective us, update us)."""
+    wire = int(pb * wire_scale)
+    ar = (predict_us(rows, wire) if rows else 0.0, sgd(pb))
+    s16 = (shard16_us(rows, pb, world), sgd(pb) / max(world, 1) + SHARD16_EXTRA_US)
+    return ar, s16
+
+
 def _overlap(a, b, spans):
     return sum(max(0.0, min(b, e) - max(a, s)) for s, e in spans)
 
 
 def schedule(stage_us, param_bytes, cuts, rows, wire_scale=1.0, head_bytes=0,
              seg_overhead_us=SEG_OVERHEAD_US, sgd_us=None, comm_overhead_us=COMM_OVERHEAD_US,
-             contention=CONTENTION):
+             contention=CONTENTION, update="allreduce", world=8):
     """Replay one pipelined step with cuts before the stages in ``cuts``.
 
     stage_us[i]: backward time of fused stage i (stage S-1's entry also carries the forward and
     the classifier head: every candidate's first segment contains it). param_bytes[i]: fp32
     bytes of stage i's parameters (head_bytes: the classifier's, in the first bucket).
     wire_scale: wire bytes per fp32 byte (0.5 for a bf16 wire). sgd_us(bytes) -> update time
-    (default: SGD_US_PER_BYTE). Returns a dict with the step time, the per-bucket wire bytes, the
-    predicted all-reduce time per bucket and the exposed communication time."""
+    (default: SGD_US_PER_BYTE). ``update``: "allreduce" (all-reduce + replicated SGD per
+    bucket), "shard16" (reduce-scatter + 1/world SGD + bf16 operand all-gather,
+    parallel/zero.py ShardedBf16Update; fp32 gradients only) or "auto" (the cheaper of the two
+    per bucket). Returns a dict with the step time, the per-bucket wire bytes, the predicted
+    collective time per bucket, the per-bucket plan ("ar" / "s16") and the exposed
+    communication time."""
     S = len(stage_us)
     cuts = sorted(set(int(c) for c in cuts))
     if any(not 0 < c < S for c in cuts):
@@ -60,8 +102,11 @@ def schedule(stage_us, param_bytes, cuts, rows, wire_scale=1.0, head_bytes=0,
     bounds = [S] + cuts[::-1] + [0]
     t_main = 0.0
     free = 0.0
-    buckets, ar, busy = [], [], []
+    buckets, ar, busy, plan = [], [], [], []
     free_before_last = 0.0
+    if update not in ("allreduce", "shard16", "auto"):
+        raise ValueError("update must be allreduce, shard16 or auto")
+    shard_ok = update != "allreduce" and wire_scale == 1.0 and world > 1
     for j in range(len(bounds) - 1):
         if j == len(bounds) - 2:
             free_before_last = free
@@ -71,17 +116,22 @@ def schedule(stage_us, param_bytes, cuts, rows, wire_scale=1.0, head_bytes=0,
         t_main += seg + contention * _overlap(t_main, t_main + seg, busy)
         pb = sum(param_bytes[lo:hi]) + (head_bytes if j == 0 else 0)
         wire = int(pb * wire_scale)
-        t_ar = predict_us(rows, wire) if rows else 0.0
+        (t_ar, u_ar), (t_s, u_s) = bucket_costs(rows, pb, wire_scale, world, sgd)
+        code = "ar"
+        if shard_ok and (update == "shard16" or t_s + u_s < t_ar + u_ar):
+            code, t_ar, u_ar, wire = "s16", t_s, u_s, int(pb * 1.5)
         start = max(t_main, free) + comm_overhead_us
-        free = start + t_ar + sgd(pb)
+        free = start + t_ar + u_ar
         busy.append((start, start + t_ar))
         buckets.append(wire)
         ar.append(t_ar)
+        plan.append(code)
     end = max(t_main, free)
     # slack: how long before the end of the backward the earlier buckets are all done (a plan
     # that finishes them with margin tolerates a slower collective than the probe measured)
     return {"cuts": cuts, "step_us": end, "backward_us": t_main, "exposed_us": end - t_main,
-            "slack_us": t_main - free_before_last, "bucket_bytes": buckets, "allreduce_us": ar}
+            "slack_us": t_main - free_before_last, "bucket_bytes": buckets, "allreduce_us": ar,
+            "update": plan}
 
 
 def schedule_inline(stage_us, param_bytes, rows, wire_scale=1.0, head_bytes=0, sgd_us=None):
@@ -97,7 +147,7 @@ def schedule_inline(stage_us, param_bytes, rows, wire_scale=1.0, head_bytes=0, s
 
 def plan_cuts(stage_us, param_bytes, rows, wire_scale=1.0, head_bytes=0, max_cuts=3,
               seg_overhead_us=SEG_OVERHEAD_US, sgd_us=None, comm_overhead_us=COMM_OVERHEAD_US,
-              tie_us=1.0, candidates=None, contention=CONTENTION):
+              tie_us=1.0, candidates=None, contention=CONTENTION, update="allreduce", world=8):
     """Best cut set and the predicted schedules of the candidates: (best_schedule, ranked list
     of (step_us, cuts)). Among the sets within ``tie_us`` of the fastest: the fewest cuts, then
     the most slack (the earlier buckets finish furthest ahead of the end of the backward).
@@ -112,7 +162,7 @@ def plan_cuts(stage_us, param_bytes, rows, wire_scale=1.0, head_bytes=0, max_cut
     for c in candidates:
         c = tuple(sorted(c))
         r = schedule(stage_us, param_bytes, c, rows, wire_scale, head_bytes,
-                     seg_overhead_us, sgd_us, comm_overhead_us, contention)
+                     seg_overhead_us, sgd_us, comm_overhead_us, contention, update, world)
         cands.append((r["step_us"], len(c), c, r))
     fastest = min(t for t, _, _, _ in cands)
     near = [x for x in cands if x[0] <= fastest + tie_us]

@@ -337,6 +337,93 @@ def zero_worker(rank, world, port, q, steps):
         raise
 
 
+def shard16_worker(rank, world, port, q, steps):
+    """Replicated update with the GPU's operand semantics (fp32 all-reduce + SGD on the fp32
+    master of every parameter; the forward reads bf16(master) of the conv weights) vs the
+    sharded update with the bf16 operand all-gather (parallel/zero.py ShardedBf16Update): same
+    init and data, cuts before stages 3 and 6 (three buckets)."""
+    try:
+        _init(rank, world, port)
+        import torch.distributed as dist
+        from ddp_amd.models import VGG11
+        from ddp_amd.optim import FusedSGD
+        from ddp_amd.parallel import TorchCommunicator, DistributedDataParallel, check_replicas
+        from ddp_amd.parallel.comm import AVG
+        from ddp_amd.parallel.zero import ShardedBf16Update, arena_buckets, operand_tensors
+        from ddp_amd.engine import CrossEntropyLoss
+        from ddp_amd.data import SyntheticCIFAR10, CPULoader
+        comm = TorchCommunicator()
+        crit = CrossEntropyLoss()
+        loader = CPULoader(SyntheticCIFAR10(True, n=4 * world * steps), 4, num_replicas=world,
+                           rank=rank)
+        batches = [b for _, b in zip(range(steps), loader)]
+        out = {}
+        lr, m, wd = 0.05, 0.9, 1e-4
+        for mode in ("replicated", "shard16"):
+            torch.manual_seed(89395)
+            ddp = DistributedDataParallel(VGG11(), comm, bucket_cap_mb=4.0)
+            opt = FusedSGD(ddp.parameters(), lr=lr, momentum=m, weight_decay=wd)
+            a = ddp.arena
+            pidx = {id(p): i for i, p in enumerate(a.params)}
+            firsts = [pidx[id(ddp.module.layers[i].weight)] for i in (11, 22)]  # stages 3, 6
+            buckets = arena_buckets(a, firsts)
+            op = operand_tensors(a)
+            ends = list(a.offsets[1:]) + [a.total]
+            upd = None
+            if mode == "shard16":
+                upd = ShardedBf16Update(a, opt, comm, buckets)
+                out["shards"] = [upd.shard(j) for j in range(len(buckets))]
+                out["n_operand"] = sum(op)
+                out["wire"] = [upd.wire_bytes(j) for j in range(len(buckets))]
+            else:
+                master, mom = a.data.detach().clone(), torch.zeros_like(a.data)
+
+                def materialize():
+                    with torch.no_grad():
+                        for (o, e), is_op in zip(zip(a.offsets, ends), op):
+                            a.data[o:e] = (master[o:e].to(torch.bfloat16).float() if is_op
+                                           else master[o:e])
+                materialize()
+            for x, y in batches:
+                opt.zero_grad()
+                with ddp.no_sync():
+                    crit(ddp(x), y).backward()
+                if upd is not None:
+                    for j in range(len(buckets)):
+                        upd.step(j)
+                else:
+                    with torch.no_grad():
+                        comm.all_reduce(a.grad, AVG)
+                        d = a.grad.add(master, alpha=wd)
+                        mom.mul_(m).add_(d)
+                        master.add_(mom, alpha=-lr)
+                        a.grad.zero_()
+                    materialize()
+            out[mode + "_operand"] = a.data.detach().clone()
+            if upd is not None:
+                out["grad_zero"] = bool((a.grad == 0).all())
+                out["operands_consistent"] = check_replicas(a, world)
+                upd.gather_masters()
+                out[mode] = upd.master.clone()
+                out["data_is_master"] = bool(torch.equal(a.data, upd.master))
+                out["masters_consistent"] = check_replicas(a, world)
+            else:
+                out[mode] = master.clone()
+        dist.destroy_process_group()
+        q.put((rank, {"replicated": out["replicated"].numpy(), "shard16": out["shard16"].numpy(),
+                      "replicated_operand": out["replicated_operand"].numpy(),
+                      "shard16_operand": out["shard16_operand"].numpy(),
+                      "grad_zero": out["grad_zero"], "shards": out["shards"],
+                      "operands_consistent": out["operands_consistent"],
+                      "masters_consistent": out["masters_consistent"],
+                      "data_is_master": out["data_is_master"], "n_operand": out["n_operand"],
+                      "wire": out["wire"]}))
+    except Exception:
+        import traceback
+        q.put((rank, {"error": traceback.format_exc()}))
+        raise
+
+
 def uid_bootstrap_worker(rank, world, port, q):
     """RcclCommunicator's ncclUniqueId exchange over the c10d TCPStore with a stand-in native
     module (no GPU): rank 0 creates each uid, every rank constructs its communicator from it."""

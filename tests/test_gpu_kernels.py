@@ -67,11 +67,11 @@ def test_conv_fwd_stats(native_ext, case):
     assert torch.allclose(stats[K:], (zf * zf).sum(0), rtol=1e-3, atol=1e-2)
 
 
-@pytest.mark.parametrize("layout", ["kcrs", "krsc", "krsc_persistent"])
+@pytest.mark.parametrize("layout", ["kcrs", "krsc", "krsc_deep"])
 @pytest.mark.parametrize("case", [c for c in CONV_CASES if c[1] != 8])
 def test_conv_dgrad(native_ext, case, layout):
     """dgrad + wgrad; the weight gradient in the standard [K][C][R][S] layout and the GPU arena's
-    [K][R][S][C] layout (also with the persistent grid and the deepest LDS ring)."""
+    [K][R][S][C] layout (also with the deepest LDS ring)."""
     from ddp_amd.ops.layers import conv_backward
     N, Cin, H, W, K, R, stride, pad = case
     conv, spec, x, xn = _conv_setup(N, Cin, H, W, K, R, stride, pad)
@@ -80,15 +80,13 @@ def test_conv_dgrad(native_ext, case, layout):
     dzn = dz.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
     fmt = torch.contiguous_format if layout == "kcrs" else torch.channels_last
     dw = torch.zeros_like(conv.weight, memory_format=fmt)
-    # the persistent grid with the deepest LDS ring
-    native_ext.conv_options(int(layout == "krsc_persistent"),
-                            4 if layout == "krsc_persistent" else (3 if layout == "krsc" else 2))
+    native_ext.conv_options(4 if layout == "krsc_deep" else (3 if layout == "krsc" else 2))
     try:
         dx = conv_backward(spec, xn, dzn, dw, True)
         torch.cuda.synchronize()
     finally:
         from ddp_amd.ops.common import CONV_STAGES
-        native_ext.conv_options(0, CONV_STAGES)
+        native_ext.conv_options(CONV_STAGES)
     xr = x.clone().requires_grad_(True)
     wr = conv.weight.detach().clone().requires_grad_(True)
     out = F.conv2d(xr, wr, None, stride, pad)

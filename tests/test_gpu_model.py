@@ -207,44 +207,6 @@ def test_fused_eval_metrics_match(native_ext):
     assert abs(int(hits) - cb) <= 1  # a near-tie may round differently
 
 
-@pytest.mark.parametrize("model_name", ["vgg11"])
-def test_backward_side_stream_matches_single_stream(native_ext, model_name):
-    """Weight gradients on the backward side stream (ops.common.BWD_SIDE_STREAM) agree with the
-    single-stream backward as closely as two single-stream runs agree with each other (float
-    atomics make repeated runs differ; a random-init net amplifies that in early layers)."""
-    from ddp_amd.models import build
-    from ddp_amd.engine import CrossEntropyLoss
-    from ddp_amd.optim import FusedSGD
-    from ddp_amd.ops import common
-    torch.manual_seed(0)
-    a = build(model_name).cuda()
-    b, c = copy.deepcopy(a), copy.deepcopy(a)
-    size, ncls = (32, 10) if model_name == "vgg11" else (64, 1000)
-    x = torch.randn(16, 3, size, size, device="cuda")
-    y = torch.randint(0, ncls, (16,), device="cuda")
-    grads = []
-    saved = common.BWD_SIDE_STREAM
-    try:
-        for m, side in ((a, True), (b, False), (c, False)):
-            common.BWD_SIDE_STREAM = side
-            opt = FusedSGD(m.parameters(), lr=0.1)
-            opt.zero_grad()
-            CrossEntropyLoss()(m(x), y).backward()
-            torch.cuda.synchronize()
-            grads.append([p.grad.clone() for p in m.parameters()])
-    finally:
-        common.BWD_SIDE_STREAM = saved
-
-    def cos(u, v):
-        return float(torch.dot(u.reshape(-1), v.reshape(-1)) / (u.norm() * v.norm() + 1e-20))
-
-    for (n, _), ga, gb, gc in zip(a.named_parameters(), *grads):
-        if float(gb.norm()) < 1e-6:
-            continue
-        base = cos(gb, gc)
-        assert cos(ga, gb) > min(0.98, base - 0.1), (n, cos(ga, gb), base)
-
-
 @pytest.mark.parametrize("batch,max_hw", [(64, 16), (256, 64), (32, 256)])
 def test_bn_backward_fused_sums_match_reduce_kernel(native_ext, batch, max_hw):
     """BatchNorm-backward sums accumulated by the next layer's dgrad epilogue / split-K finish
@@ -505,6 +467,83 @@ def test_segmented_ddp_step_matches_single_graph(native_ext, split):
     assert abs(float(slow_graph.norm()) / float(slow_eager.norm()) - 1) < 0.02
     for st in (ss, slow):
         st.check_error()
+    m.close()
+
+
+@pytest.mark.parametrize("scale", [1.0, 2.0])
+def test_shard16_emulated_world_updates_rank0_shard(native_ext, scale):
+    """One-GPU stand-in of the 8-GPU sharded update (SegmentedDDPStep(update="shard16") with a
+    timed stand-in collective, parallel/zero.py ShardedBf16Update emulate_world=8): each bucket's
+    SGD touches exactly rank 0's 1/8 shard, that shard's update matches the replicated
+    TrainStep's on the same elements (eager and replayed), the bf16 operand copies of the
+    shard are bf16(new master), and the other 7/8 stay untouched. With a slow stand-in that
+    doubles the gradients (scale 2) the replayed update must see the doubled values: the shard
+    SGD waits for the reduce-scatter."""
+    from ddp_amd.models import VGG11
+    from ddp_amd.engine import CrossEntropyLoss, TrainStep, SegmentedDDPStep
+    from ddp_amd.optim import FusedSGD
+    from ddp_amd.data import SyntheticCIFAR10, DeviceLoader
+    from ddp_amd.parallel import DistributedDataParallel, RcclCommunicator
+    torch.manual_seed(4)
+    m = DistributedDataParallel(VGG11().cuda(), RcclCommunicator(0, 1, 0), bucket_cap_mb=256.0,
+                                first_bucket_cap_mb=256.0)
+    opt = FusedSGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    ld = DeviceLoader(SyntheticCIFAR10(True, n=512), 64, "cuda")
+    crit = CrossEntropyLoss()
+    ts = TrainStep(m, opt, crit, ld)
+    ss = SegmentedDDPStep(m, opt, crit, ld, split=[3, 6], emulate_gbps=171.0 if scale == 1 else 20.0,
+                          emulate_scale=scale, update="shard16", emulate_world=8)
+    ss.WAIT_TIMEOUT_S = 20.0
+    u = ss.shard16
+    assert u is not None and u.emulated and u.world == 8
+    ts.warmup(2)
+    torch.cuda.synchronize()
+    snap = (m.arena.data.clone(), opt.momentum_buffer.clone(), ld.cursor.clone())
+
+    def run(fn):
+        m.arena.data.copy_(snap[0]); opt.momentum_buffer.copy_(snap[1]); ld.cursor.copy_(snap[2])
+        m.arena.grad.zero_()
+        for sp in m.module.fused_plan():
+            sp._packed_version = None
+            sp.maybe_pack()
+        torch.cuda.synchronize()
+        fn()
+        torch.cuda.synchronize()
+        assert int(ld.cursor.item()) == int(snap[2].item()) + 1
+        return m.arena.data - snap[0]
+
+    def cos(a, b):
+        return float(torch.dot(a, b) / (a.norm() * b.norm()))
+
+    ref, ref2 = run(ts._body), run(ts._body)
+    base = cos(ref, ref2)
+    mask = torch.zeros(m.arena.total, dtype=torch.bool, device="cuda")
+    for j in range(len(ss.buckets)):
+        s0, s1 = u.shard(j)
+        mask[s0:s1] = True
+    eager = run(ss._body)
+    ss.warmup(1)
+    ss.capture()
+    graph = run(ss.step)
+    ss.check_error()
+    for d in (eager, graph):
+        assert float(d[~mask].abs().max()) == 0.0  # other ranks' shards untouched
+        if scale == 1.0:
+            assert cos(ref[mask], d[mask]) > min(0.99, base - 0.005)
+            assert abs(float(d[mask].norm()) / float(ref[mask].norm()) - 1) < 0.02
+        else:  # doubled gradients reached the shard SGD
+            assert float(d[mask].norm()) / float(ref[mask].norm()) > 1.3
+    assert cos(eager[mask], graph[mask]) > min(0.99, base - 0.005)
+    # the operand image of rank 0's shard is bf16(new master)
+    for j in range(len(ss.buckets)):
+        s0, s1 = u.shard(j)
+        want = m.arena.data[s0:s1].to(torch.bfloat16)
+        op = torch.zeros(m.arena.total, dtype=torch.bool, device="cuda")
+        for (o, e, is_op) in u._tensors:
+            if is_op:
+                op[o:e] = True
+        sel = op[s0:s1]
+        assert torch.equal(u.data16[s0:s1][sel], want[sel])
     m.close()
 
 

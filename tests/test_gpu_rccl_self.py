@@ -48,7 +48,8 @@ def _restore(m, opt, ld, snap):
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("segmented", [None, "4", "2,5", "4:bf16", "3,6:zero"])
+@pytest.mark.parametrize("segmented", [None, "4", "2,5", "4:bf16", "3,6:zero", "3,6:shard16",
+                                       "3,6:mixed"])
 def test_captured_ddp_step_with_live_rccl(native_ext, segmented):
     """Captured DDP step (inline bucket all-reduce, or the pipelined segmented step: each
     bucket's all-reduce — fp32 or bf16 wire — and optimizer update on the comm stream, on the
@@ -71,10 +72,13 @@ def test_captured_ddp_step_with_live_rccl(native_ext, segmented):
         ld = DeviceLoader(SyntheticCIFAR10(True, n=512), 64, "cuda")
         if segmented:
             cuts, _, opt_ = segmented.partition(":")
+            upd = {"shard16": "shard16", "mixed": ["s16", "s16", "ar"]}.get(opt_, "allreduce")
             st = SegmentedDDPStep(m, opt, CrossEntropyLoss(), ld,
                                   split=[int(v) for v in cuts.split(",")],
                                   grad_comm="bf16" if opt_ == "bf16" else "fp32",
-                                  zero=opt_ == "zero")
+                                  zero=opt_ == "zero", update=upd)
+            if opt_ in ("shard16", "mixed"):
+                assert st.shard16 is not None and not st.shard16.emulated
             st.WAIT_TIMEOUT_S = 20.0
         else:
             st = TrainStep(m, opt, CrossEntropyLoss(), ld)
@@ -99,7 +103,8 @@ def test_captured_ddp_step_with_live_rccl(native_ext, segmented):
     (l0, _), g1 = res[True]
     # two executions differ by float-atomic ordering (BatchNorm statistics move bf16 pool-window
     # ties and ReLU edges): the compared steps must sit within 3x that run-to-run noise
-    tol = min(0.99, 1.0 - 3.0 * (1.0 - _cos(e0, e1)))
+    # (floored: a race that made the noise itself worse must not loosen the check without bound)
+    tol = max(0.97, min(0.99, 1.0 - 3.0 * (1.0 - _cos(e0, e1))))
     assert float(e0.norm()) > 0
     for a, b in ((e0, l0), (g0, g1), (e0, g1)):
         assert _cos(a, b) > tol, (_cos(a, b), tol)

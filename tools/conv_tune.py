@@ -227,7 +227,7 @@ def tune_pairs(args):
         for (N, C, H, W, K, R, stride, pad, Cr) in layers:
             bn = None
             # (VGG: the preceding block's BN-backward sums ride in the dgrad epilogue; ResNet
-            # keeps its separate reduce pass by default, ops/common.py BN_BWD_FUSE_NOPOOL)
+            # keeps its separate reduce pass, ops/layers.py bn_bwd_fuse_pays)
             if (model == "vgg11" and prev_hw is not None and C == Cr
                     and bn_bwd_fuse_pays(H, W, prev_hw != H, N)):
                 pz = torch.randn(N, prev_hw, prev_hw, C, device=dev).to(torch.bfloat16)

@@ -69,9 +69,6 @@ def main():
         native().conv_epi_stage_set(0)
         r["fwd+stats(direct epi)"] = timeit(lambda: conv_forward(spec, x, None, stats))
         native().conv_epi_stage_set(1)
-        native().conv_options(1, 2)
-        r["fwd+stats(persistent)"] = timeit(lambda: conv_forward(spec, x, None, stats))
-        native().conv_options(0, 2)
         # BN backward passes over the conv output (reduce -> finalize -> apply, no residual)
         z = conv_forward(spec, x, None, stats)
         y = torch.empty_like(z)
