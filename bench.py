@@ -366,7 +366,7 @@ def choose_cuts_on_node(model, opt, criterion, loader, args, world, comm_table):
     import torch.distributed as dist
     from ddp_amd.engine.step import profile_stage_times
     from ddp_amd.parallel.bucket_plan import load_table, rows_for
-    from ddp_amd.parallel.cut_plan import plan_cuts
+    from ddp_amd.parallel.cut_plan import plan_cuts, seg_boundary_us
     inner = model.module
     n = inner.n_stages()
     arena = model.arena
@@ -392,7 +392,8 @@ def choose_cuts_on_node(model, opt, criterion, loader, args, world, comm_table):
     wire = 0.5 if args.grad_comm == "bf16" else 1.0
     upd = "auto" if (args.update == "auto" and args.grad_comm == "fp32" and not args.zero) else \
         ("shard16" if args.update == "shard16" else "allreduce")
-    best, ranked = plan_cuts(stage_us, pbytes, rows, wire_scale=wire, update=upd, world=world)
+    best, ranked = plan_cuts(stage_us, pbytes, rows, wire_scale=wire, update=upd, world=world,
+                             seg_overhead_us=seg_boundary_us(loader.batch_size))
     return {"source": "probe" if comm_table is not None else "table", "comm_table": table_src,
             "cuts": best["cuts"], "stage_us": [round(v, 1) for v in stage_us],
             "stage_param_bytes": pbytes, "bucket_bytes": best["bucket_bytes"],

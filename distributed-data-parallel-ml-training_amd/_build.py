@@ -22,7 +22,6 @@ import sysconfig
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
-BUILD = os.path.join(REPO, "build", "native")
 ARCH = os.environ.get("DDP_AMD_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
@@ -40,9 +39,16 @@ def _includes():
             "-I" + sysconfig.get_paths()["include"], "-I" + os.path.join(ROCM, "include")]
 
 
-def ext_path():
+# build variants: name -> (module file stem, object dir, extra defines). "det" is the
+# deterministic-statistics test build (csrc/kernels/api.h kStatRep; loaded by _ext.load() when
+# DDP_AMD_DETERMINISTIC=1).
+VARIANTS = {"release": ("_native", "native", []),
+            "det": ("_native_det", "native_det", ["-DDDP_AMD_DETERMINISTIC"])}
+
+
+def ext_path(variant="release"):
     suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
-    return os.path.join(PKG_DIR, "_native" + suffix)
+    return os.path.join(PKG_DIR, VARIANTS[variant][0] + suffix)
 
 
 def _newest_header():
@@ -68,27 +74,37 @@ def _sources():
             + sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))) + [os.path.join(CSRC, "bind.cpp")])
 
 
-def up_to_date():
+def up_to_date(variant="release"):
     """The in-tree extension is newer than every source and header. The object cache
     (build/native) does not travel with a snapshot, so this is what a GPU box checks: an
     up-to-date extension is loaded as is instead of being rebuilt there."""
-    out = ext_path()
+    out = ext_path(variant)
     if not os.path.exists(out):
         return False
     newest = max([_newest_header()] + [os.path.getmtime(s) for s in _sources()])
     return os.path.getmtime(out) >= newest
 
 
-def build(verbose=True, jobs=None):
-    if not os.path.isdir(BUILD) and up_to_date():
-        return ext_path()
+def build(verbose=True, jobs=None, variants=("release", "det")):
+    """Build every variant (release = the shipped extension, det = the deterministic-
+    statistics test build); returns the release path."""
+    for v in variants:
+        _build_variant(v, verbose, jobs)
+    return ext_path()
+
+
+def _build_variant(variant, verbose=True, jobs=None):
+    stem, objdir, defines = VARIANTS[variant]
+    BUILD = os.path.join(REPO, "build", objdir)
+    if not os.path.isdir(BUILD) and up_to_date(variant):
+        return ext_path(variant)
     hipcc = _hipcc()
     os.makedirs(BUILD, exist_ok=True)
     inc = _includes()
     # DDP_AMD_DEBUG_BUILD=1: -O1 -g and the DDP_DEVICE_CHECK bounds checks (common.h)
     debug = os.environ.get("DDP_AMD_DEBUG_BUILD", "0") == "1"
     common = (["-O1", "-g", "-DDDP_AMD_DEBUG"] if debug else ["-O3"]) + \
-        ["-std=c++17", "-fPIC", "-Wno-unused-result"]
+        ["-std=c++17", "-fPIC", "-Wno-unused-result"] + defines
     hdr_time = _newest_header()
     tasks = []
     for src in sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))):
@@ -110,7 +126,7 @@ def build(verbose=True, jobs=None):
             o, ch = f.result()
             objs.append(o)
             changed |= ch
-    out = ext_path()
+    out = ext_path(variant)
     if changed or not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(o) for o in objs):
         tmp = out + ".tmp"
         cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp,

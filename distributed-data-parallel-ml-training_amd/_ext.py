@@ -16,8 +16,11 @@ _module = None
 
 
 def so_path():
+    """The release build, or the deterministic-statistics test build with
+    DDP_AMD_DETERMINISTIC=1 (_build.py variant "det")."""
     suffix = importlib.machinery.EXTENSION_SUFFIXES[0]
-    return os.path.join(_PKG_DIR, _MODNAME + suffix)
+    name = _MODNAME + ("_det" if os.environ.get("DDP_AMD_DETERMINISTIC", "0") == "1" else "")
+    return os.path.join(_PKG_DIR, name + suffix)
 
 
 def available():

@@ -586,6 +586,10 @@ PYBIND11_MODULE(_native, m) {
     return out;
   });
   m.def("make_unique_id", []() { return py::bytes(RcclComm::make_unique_id()); });
+  // BatchNorm statistics replicas per accumulator (api.h kStatRep) and whether this is the
+  // deterministic-statistics build (_build.py variant "det")
+  m.def("stat_replicas", []() { return ddp_amd::kStatRep; });
+  m.def("deterministic", []() { return ddp_amd::kDeterministic; });
 
   // host-only readiness / launch-order state machine (no GPU needed: CPU tests drive it with
   // the same hook orders as the Python twin, tests/test_bucket_scheduler_cpu.py)

@@ -8,8 +8,19 @@
 namespace ddp_amd {
 
 // BatchNorm statistics are accumulated into kStatRep replicas [rep][2][C] (sum, sum of squares)
-// to spread float-atomic contention over many addresses; consumers sum the replicas.
+// to spread float-atomic contention over many addresses; consumers sum the replicas in replica
+// order. Deterministic-statistics build (_build.py variant "det": -DDDP_AMD_DETERMINISTIC,
+// loaded with DDP_AMD_DETERMINISTIC=1): every block owns a replica of its own (block id <
+// kStatRep), so each address receives exactly one float add onto zero and the consumers' fixed
+// order makes the statistics — and the whole step — bitwise reproducible (test mode; a block id
+// beyond kStatRep poisons replica 0 with NaN so it cannot pass silently).
+#ifdef DDP_AMD_DETERMINISTIC
+constexpr int kStatRep = 4096;
+constexpr bool kDeterministic = true;
+#else
 constexpr int kStatRep = 16;
+constexpr bool kDeterministic = false;
+#endif
 
 struct ConvGeom {
   int N, H, W, C;     // input (NHWC, C % 8 == 0)

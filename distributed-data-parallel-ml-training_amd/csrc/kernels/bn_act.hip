@@ -319,7 +319,7 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
   }
   // block reduction over the 256/Gb threads sharing each channel group, then one atomic per
   // channel per block into this block's replica
-  float* rep = a.sums + (blockIdx.x % kStatRep) * 2 * a.C;
+  float* rep = a.sums + stat_rep(blockIdx.x) * 2 * a.C;
   const int tid = threadIdx.x;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
@@ -331,7 +331,7 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
       const int g = idx / 8, e = idx % 8;
       float s = 0.f;
       for (int r = 0; r < prows; ++r) s += red[e * 256 + r * Gb + g];
-      atomicAdd(rep + k * a.C + (cg_base + g) * 8 + e, s);
+      atomicAdd(rep + k * a.C + (cg_base + g) * 8 + e, stat_val(s, blockIdx.x));
     }
   }
 }
@@ -643,11 +643,12 @@ __global__ __launch_bounds__(256) void bn_pool3_bwd_kernel(BnArgs a, int Ho, int
     }
   }
   __syncthreads();
-  float* rep = a.sums + (blockIdx.x % kStatRep) * 2 * a.C;
+  float* rep = a.sums + stat_rep(blockIdx.x) * 2 * a.C;
   for (int k = threadIdx.x; k < 2 * a.C; k += 256) {
     const int which = k / a.C, c = k - which * a.C;
-    atomicAdd(rep + which * a.C + c, red[0][which][c] + red[1][which][c] + red[2][which][c] +
-                                         red[3][which][c]);
+    atomicAdd(rep + which * a.C + c,
+              stat_val(red[0][which][c] + red[1][which][c] + red[2][which][c] + red[3][which][c],
+                       blockIdx.x));
   }
 }
 

@@ -5,6 +5,8 @@
 #include <stdint.h>
 #include <cstdlib>
 
+#include "api.h"
+
 namespace ddp_amd {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -32,6 +34,25 @@ constexpr int kWave = 64;  // CDNA wavefront width (never 32)
   do {                        \
   } while (0)
 #endif
+
+// Replica of a block's BatchNorm-statistics partial sums (api.h kStatRep) and the value it adds:
+// release builds spread blocks over the replicas; the deterministic build gives each block its
+// own replica and poisons replica 0 with NaN when a grid outgrows kStatRep.
+__device__ __forceinline__ int stat_rep(int b) {
+#ifdef DDP_AMD_DETERMINISTIC
+  return b < kStatRep ? b : 0;
+#else
+  return b % kStatRep;
+#endif
+}
+__device__ __forceinline__ float stat_val(float v, int b) {
+#ifdef DDP_AMD_DETERMINISTIC
+  return b < kStatRep ? v : __builtin_nanf("");
+#else
+  (void)b;
+  return v;
+#endif
+}
 
 // bf16 <-> fp32 bit conversions. round-to-nearest-even; NaN kept NaN.
 __device__ __forceinline__ float bf2f(unsigned short h) {

@@ -674,13 +674,13 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
         }
       }
       __syncthreads();
-      float* st = args.stats + (bid % kStatRep) * 2 * args.Ng;  // spread contention
+      float* st = args.stats + stat_rep(bid) * 2 * args.Ng;  // spread contention
       for (int k = tid; k < 2 * BN; k += 256) {
         const int which = k / BN, cl = k - which * BN;
         if (col0 + cl >= args.Ng) continue;
         const float t = sl[(0 * 2 + which) * BN + cl] + sl[(1 * 2 + which) * BN + cl] +
                         sl[(2 * 2 + which) * BN + cl] + sl[(3 * 2 + which) * BN + cl];
-        atomicAdd(st + which * args.Ng + col0 + cl, t);
+        atomicAdd(st + which * args.Ng + col0 + cl, stat_val(t, bid));
       }
     }
     return;
@@ -785,7 +785,7 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
       __syncthreads();
       if (wm == 0 && rl == 0) {
         float* st = (MODE == MODE_FWD ? args.stats : args.bnf.sums) +
-                    (bid % kStatRep) * 2 * args.Ng;  // spread contention
+                    stat_rep(bid) * 2 * args.Ng;  // spread contention
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int col = cbase + j * 16;
@@ -794,8 +794,8 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
           const float* s1 = sl + ((((2 + wn) * TN + j) * 4 + (lane >> 4)) * 8);
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
-            atomicAdd(st + col + t, s0[t] + s1[t]);
-            atomicAdd(st + args.Ng + col + t, s0[4 + t] + s1[4 + t]);
+            atomicAdd(st + col + t, stat_val(s0[t] + s1[t], bid));
+            atomicAdd(st + args.Ng + col + t, stat_val(s0[4 + t] + s1[4 + t], bid));
           }
         }
       }
@@ -939,7 +939,7 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
     __syncthreads();
     if (wm == 0 && rl == 0) {
       float* st = (MODE == MODE_FWD ? args.stats : args.bnf.sums) +
-                  (bid % kStatRep) * 2 * args.Ng;  // spread contention
+                  stat_rep(bid) * 2 * args.Ng;  // spread contention
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int col = col0 + wn * WTN + j * 16 + cq;
@@ -947,8 +947,8 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
         const float* slot = reinterpret_cast<const float*>(smem) + (((wn * TN + j) * 4 + (lane >> 4)) * 8);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          atomicAdd(st + col + t, stat_s[j][t] + slot[t]);
-          atomicAdd(st + args.Ng + col + t, stat_ss[j][t] + slot[4 + t]);
+          atomicAdd(st + col + t, stat_val(stat_s[j][t] + slot[t], bid));
+          atomicAdd(st + args.Ng + col + t, stat_val(stat_ss[j][t] + slot[4 + t], bid));
         }
       }
     }
@@ -1179,8 +1179,9 @@ __device__ __forceinline__ void splitk_finish_body(const FinishArgs& fa, float* 
     if (by * Gb + c >= G) continue;
     float t = 0.f;
     for (int r = 0; r < prows; ++r) t += red[k][e][r * Gb + c];
-    float* st = stats + ((bx + by) % kStatRep) * 2 * Ng;
-    atomicAdd(st + k * Ng + (by * Gb + c) * 8 + e, t);
+    const int lb = by * gx + bx;  // linear block id (the deterministic build needs it unique)
+    float* st = stats + stat_rep(lb) * 2 * Ng;
+    atomicAdd(st + k * Ng + (by * Gb + c) * 8 + e, stat_val(t, lb));
   }
 }
 
@@ -1567,7 +1568,9 @@ __global__ __launch_bounds__(256) void linear_head_bwd_kernel(const float* __res
 // (reduction order fixed inside a group), transposes (r,s,c) -> (c,r,s) through LDS, and adds
 // into the PyTorch-layout gradient with coalesced stores (one atomic add per group when the
 // splits are divided into several groups).
-constexpr int kWgFinishGroup = 32;
+// slabs per finish block row; several rows combine with float atomics (one row in the
+// deterministic build: a fixed summation order)
+constexpr int kWgFinishGroup = kDeterministic ? (1 << 30) : 32;
 __global__ __launch_bounds__(256) void wgrad_finish_kernel(const float* ws, int splits, int K,
                                                            int R, int S, int C, int Creal,
                                                            float* dw) {
@@ -1611,7 +1614,7 @@ __device__ __forceinline__ float sgd_step1(float p, float g, float& b, const Sgd
 // gradient) the finish applies the optimizer step to the layer's weights instead of storing the
 // gradient: p -= lr * (momentum buffer update of g + wd * p), plus the bf16 forward operand copy
 // — the gradient never reaches memory and the step's separate SGD pass skips this tensor.
-constexpr int kWgFinishGroupKrsc = 16;
+constexpr int kWgFinishGroupKrsc = kDeterministic ? (1 << 30) : 16;
 __device__ __forceinline__ void wgrad_finish_krsc_body(const float* __restrict__ ws, int splits,
                                                        int K, int RS, int C, int Creal,
                                                        float* __restrict__ dw, int bx, int by,

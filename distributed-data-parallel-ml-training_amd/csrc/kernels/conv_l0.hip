@@ -182,7 +182,8 @@ __device__ __forceinline__ void block_sums(float (&s1)[kNT][4], float (&s2)[kNT]
   if (threadIdx.x < 2 * kK) {
     const int k = threadIdx.x / kK, c = threadIdx.x - k * kK;
     atomicAdd(rep + k * kK + c,
-              sm.red[0][k][c] + sm.red[1][k][c] + sm.red[2][k][c] + sm.red[3][k][c]);
+              stat_val(sm.red[0][k][c] + sm.red[1][k][c] + sm.red[2][k][c] + sm.red[3][k][c],
+                       blockIdx.x));
   }
 }
 
@@ -251,7 +252,7 @@ __global__ __launch_bounds__(256) void l0_stats_kernel(Args a) {
             s2[j][v] += z[j][v] * z[j][v];
           }
       });
-  block_sums(s1, s2, a.stats + (blockIdx.x % kStatRep) * 2 * kK, rl, g, sm);
+  block_sums(s1, s2, a.stats + stat_rep(blockIdx.x) * 2 * kK, rl, g, sm);
 }
 
 __global__ __launch_bounds__(256) void l0_fwd_kernel(Args a) {
@@ -380,7 +381,7 @@ __global__ __launch_bounds__(256) void l0_sums_kernel(Args a, int windows) {
     const int gg = (c & 15) >> 2, e = k * 16 + (c >> 4) * 4 + (c & 3);
     float t = 0.f;
     for (int i = 0; i < 64; ++i) t += red[4 * i + gg][e];
-    atomicAdd(a.sums + (blockIdx.x % kStatRep) * 2 * kK + k * kK + c, t);
+    atomicAdd(a.sums + stat_rep(blockIdx.x) * 2 * kK + k * kK + c, stat_val(t, blockIdx.x));
   }
 }
 
@@ -450,7 +451,7 @@ __global__ __launch_bounds__(256) void l0_bwd_kernel(Args a) {
           for (int j = 0; j < kNT; ++j) *reinterpret_cast<u16x4*>(dst + j * 16) = o[j];
         }
       });
-  if (!APPLY) block_sums(s1, s2, a.sums + (blockIdx.x % kStatRep) * 2 * kK, rl, g, sm);
+  if (!APPLY) block_sums(s1, s2, a.sums + stat_rep(blockIdx.x) * 2 * kK, rl, g, sm);
 }
 
 // one tile per wave where the grid allows, at most 1024 blocks (4 per CU): every block adds one

@@ -198,7 +198,7 @@ __global__ __launch_bounds__(256) void conv_smallk_fwd_kernel(SmallKArgs a) {
   if (threadIdx.x < 2 * a.K) {
     const int k = threadIdx.x / a.K, c = threadIdx.x - k * a.K;
     const float t = red[0][k][c] + red[1][k][c] + red[2][k][c] + red[3][k][c];
-    atomicAdd(a.stats + (blockIdx.x % kStatRep) * 2 * a.K + k * a.K + c, t);
+    atomicAdd(a.stats + stat_rep(blockIdx.x) * 2 * a.K + k * a.K + c, stat_val(t, blockIdx.x));
   }
 }
 
@@ -336,7 +336,7 @@ __global__ __launch_bounds__(256) void conv_smallk_lds_kernel(SmallKArgs a) {
     float t = 0.f;
 #pragma unroll
     for (int w = 0; w < 4; ++w) t += red[(w * 2 + k) * 64 + c];
-    atomicAdd(a.stats + (blockIdx.x % kStatRep) * 2 * a.K + k * a.K + c, t);
+    atomicAdd(a.stats + stat_rep(blockIdx.x) * 2 * a.K + k * a.K + c, stat_val(t, blockIdx.x));
   }
 }
 

@@ -443,7 +443,7 @@ void conv_tr_fwd_kernel(Args a) {
   if (!red) return;
   __syncthreads();
   if (wm == 0 && rl == 0) {
-    float* st = a.stats + (blockIdx.x % kStatRep) * 2 * K;
+    float* st = a.stats + stat_rep(blockIdx.x) * 2 * K;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int col = cbase + j * 16;
@@ -452,8 +452,8 @@ void conv_tr_fwd_kernel(Args a) {
       const float* s1 = sl + ((((2 + wn) * TN + j) * 4 + (lane >> 4)) * 8);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        atomicAdd(st + col + q, s0[q] + s1[q]);
-        atomicAdd(st + K + col + q, s0[4 + q] + s1[4 + q]);
+        atomicAdd(st + col + q, stat_val(s0[q] + s1[q], blockIdx.x));
+        atomicAdd(st + K + col + q, stat_val(s0[4 + q] + s1[4 + q], blockIdx.x));
       }
     }
   }

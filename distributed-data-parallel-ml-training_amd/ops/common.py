@@ -120,7 +120,16 @@ BN_BWD_FUSE = os.environ.get("DDP_AMD_BN_BWD_FUSE", "1") != "0"
 # must start at zero each step (BatchNorm statistics replicas, BN-backward sums). The model's
 # forward zeroes the used prefix with ONE fill instead of one memset per layer and direction.
 # Constraint: a forward must be followed by its backward before the next training forward.
-STAT_REPLICAS = 16  # == kStatRep in csrc/kernels/api.h
+_STAT_REPLICAS = None
+
+
+def stat_replicas():
+    """BatchNorm statistics replicas per accumulator (csrc/kernels/api.h kStatRep: 16, or one
+    per block in the deterministic-statistics build)."""
+    global _STAT_REPLICAS
+    if _STAT_REPLICAS is None:
+        _STAT_REPLICAS = int(native().stat_replicas())
+    return _STAT_REPLICAS
 SCRATCH_ELEMS = 8 << 20
 
 

@@ -16,7 +16,7 @@ import os
 import torch
 
 from .common import (native, ptr, stream_handle, check, grad_ready, ensure_grad, workspace,
-                     step_scratch, weight_krsc, STAT_REPLICAS)
+                     step_scratch, weight_krsc, stat_replicas)
 from . import common as _common
 
 BF16 = torch.bfloat16
@@ -57,9 +57,10 @@ class ConvBNActSpec:
         # per-step zeroed accumulators (StepScratch): BN statistics replicas + BN-backward sums
         sc = step_scratch(dev)
         self.scratch = sc
-        self.stats = sc.take(STAT_REPLICAS * 2 * K)[:STAT_REPLICAS * 2 * K]
-        sums = sc.take(STAT_REPLICAS * 2 * K + 64)
-        self.sums = sums[:STAT_REPLICAS * 2 * K]
+        nrep = stat_replicas()
+        self.stats = sc.take(nrep * 2 * K)[:nrep * 2 * K]
+        sums = sc.take(nrep * 2 * K + 64)
+        self.sums = sums[:nrep * 2 * K]
         # per-layer BN coefficient table [6][K] (scale, shift, mean, invstd | k1, k2): written
         # by the forward's finalize kernel, read by the backward (one use per step per layer)
         self.coef = torch.empty(6 * K, dtype=F32, device=dev)
@@ -133,7 +134,7 @@ def _bn_act_fwd_now(spec, z, y):
 
 def conv_forward(spec, x, bias=None, stats=None, bn_fuse=None, fin=None):
     """z = conv(x) + bias (bf16 NHWC); stats[16][2][K] += per-channel sum / sumsq of z
-    (accumulated into STAT_REPLICAS replicas; the consumer sums them).
+    (accumulated into stat_replicas() replicas; the consumer sums them).
 
     ``bn_fuse`` = (gamma, beta, eps, relu, pool, coef, y, P, Q) pointers/values: when the GEMM
     runs split-K and is small (the strong-scaling batches' deep layers), its finish kernel also

@@ -25,21 +25,47 @@ import itertools
 
 from .bucket_plan import predict_us
 
-# measured on one MI355X (profiles/r2_pipelined_ddp.md, "World 1" section): each extra segment
-# boundary (graph launch gap + flag signal + flag wait) costs ~4.5-5 us
-SEG_OVERHEAD_US = 5.0
+# Constants fitted on one MI355X (round 5, profiles/r5d_cut_sweep.md): the stand-in cut sweep
+# (53 configurations: VGG-11 at 32 / 64 / 128 / 256 images per GPU, 4-7 cut sets, all-reduce,
+# sharded and mixed per-bucket plans, 32-CU stand-in collectives at 171 GB/s) against the
+# per-stage times of tools/stage_times.py; with these values every configuration is predicted
+# within 4.5 % (tests/test_cut_plan.py).
+#
+# Cost of one segment boundary (graph launch gap + flag signal / wait + the cross-stage fusions
+# a cut disables: the consumer conv's fused BatchNorm input, the BN-backward sums in the next
+# dgrad). Grows with the per-GPU batch because the disabled fusions move more bytes:
+# us = SEG_BOUNDARY_US + SEG_BOUNDARY_US_PER_IMAGE x batch (stage times measured with a cut
+# before EVERY stage already contain one boundary each).
+SEG_BOUNDARY_US = 14.0
+SEG_BOUNDARY_US_PER_IMAGE = 0.035
+SEG_OVERHEAD_US = SEG_BOUNDARY_US + SEG_BOUNDARY_US_PER_IMAGE * 32
 # fused SGD + bf16 re-pack per fp32 parameter byte (sgd_pack_kernel: 42 us for VGG-11's 36.9 MB)
 SGD_US_PER_BYTE = 42.4 / 36.9e6
-# the comm stream's flag wait + RCCL launch, per bucket
+# the comm stream's flag wait + collective launch, per bucket (fit: 4 us; the pipeline probe,
+# profiles/r5c_probe_*.md, shows 2-4 us beyond the modelled collective + SGD on the big buckets)
 COMM_OVERHEAD_US = 4.0
-# a collective occupies CUs (RCCL channels / the stand-in's 32 workgroups): the backward that runs
-# under it is slowed by about this fraction of the overlap
-CONTENTION = 0.15
+# a collective occupies CUs: the backward that runs under it is slowed by this fraction of the
+# overlap. Measured with the 32-CU stand-in (tools/pipeline_probe.py: -0.03 .. +0.06 over four
+# configurations) and fitted at 0. The stand-in holds its CUs in an s_sleep loop, so a live RCCL
+# kernel (which moves its data through the CUs) may contend more: this is the one factor a
+# one-GPU box cannot measure.
+CONTENTION = 0.0
 
 
-# the sharded bf16-gather update issues one more collective launch and one more small kernel
-# (the small-tensor unpack) per bucket than all-reduce + SGD
-SHARD16_EXTRA_US = COMM_OVERHEAD_US
+def seg_boundary_us(per_gpu_batch):
+    """Segment-boundary cost at this per-GPU batch (see SEG_BOUNDARY_US)."""
+    return SEG_BOUNDARY_US + SEG_BOUNDARY_US_PER_IMAGE * per_gpu_batch
+
+
+# the sharded bf16-gather update issues one more collective and its shard SGD with the slot
+# copies per bucket (fitted 15 us beyond the two modelled collectives + 1/w SGD; the pipeline
+# probe shows 20-25 us including that SGD)
+SHARD16_EXTRA_US = 15.0
+# ... and the step-tail launch after the last bucket (fitted 0: it replaces the signal launch)
+SHARD16_TAIL_US = 0.0
+# the optimizer update on the comm stream is a memory-bound pass: the backward running beside
+# it slows by this fraction of the overlap (fitted 0 on the sweep)
+SGD_CONTENTION = 0.0
 
 
 def shard16_us(rows, fp32_bytes, world):
@@ -81,7 +107,8 @@ def _overlap(a, b, spans):
 
 def schedule(stage_us, param_bytes, cuts, rows, wire_scale=1.0, head_bytes=0,
              seg_overhead_us=SEG_OVERHEAD_US, sgd_us=None, comm_overhead_us=COMM_OVERHEAD_US,
-             contention=CONTENTION, update="allreduce", world=8):
+             contention=CONTENTION, update="allreduce", world=8,
+             shard16_tail_us=None, sgd_contention=None):
     """Replay one pipelined step with cuts before the stages in ``cuts``.
 
     stage_us[i]: backward time of fused stage i (stage S-1's entry also carries the forward and
@@ -99,30 +126,52 @@ def schedule(stage_us, param_bytes, cuts, rows, wire_scale=1.0, head_bytes=0,
     if any(not 0 < c < S for c in cuts):
         raise ValueError(f"cuts must lie in 1..{S - 1}")
     sgd = sgd_us or (lambda b: b * SGD_US_PER_BYTE)
+    if shard16_tail_us is None:
+        shard16_tail_us = SHARD16_TAIL_US
+    if sgd_contention is None:
+        sgd_contention = SGD_CONTENTION
     bounds = [S] + cuts[::-1] + [0]
     t_main = 0.0
     free = 0.0
-    buckets, ar, busy, plan = [], [], [], []
+    buckets, ar, busy, plan, sgd_busy = [], [], [], [], []
     free_before_last = 0.0
+    forced = None
+    if isinstance(update, (list, tuple)):
+        forced, update = list(update), "auto"
+        if len(forced) != len(bounds) - 1:
+            raise ValueError("per-bucket plan does not match the cuts")
     if update not in ("allreduce", "shard16", "auto"):
-        raise ValueError("update must be allreduce, shard16 or auto")
+        raise ValueError("update must be allreduce, shard16, auto or a per-bucket list")
     shard_ok = update != "allreduce" and wire_scale == 1.0 and world > 1
     for j in range(len(bounds) - 1):
         if j == len(bounds) - 2:
             free_before_last = free
         lo, hi = bounds[j + 1], bounds[j]
-        seg = sum(stage_us[lo:hi]) + (seg_overhead_us if j > 0 else 0.0)
+        # stage_us come from a step cut before EVERY stage (profile_stage_times), so each holds
+        # one segment boundary: a segment of several stages saves the boundaries inside it
+        seg = sum(stage_us[lo:hi]) - (hi - lo - 1) * seg_overhead_us
         # (one pass: the buckets launched so far slow this segment by their overlap with it)
-        t_main += seg + contention * _overlap(t_main, t_main + seg, busy)
+        t_main += seg + contention * _overlap(t_main, t_main + seg, busy) + \
+            sgd_contention * _overlap(t_main, t_main + seg, sgd_busy)
         pb = sum(param_bytes[lo:hi]) + (head_bytes if j == 0 else 0)
         wire = int(pb * wire_scale)
         (t_ar, u_ar), (t_s, u_s) = bucket_costs(rows, pb, wire_scale, world, sgd)
+        last = j == len(bounds) - 2
+        if last:  # the sharded plan's step tail (small-tensor unpack + re-pack + signal)
+            u_s += shard16_tail_us
         code = "ar"
-        if shard_ok and (update == "shard16" or t_s + u_s < t_ar + u_ar):
-            code, t_ar, u_ar, wire = "s16", t_s, u_s, int(pb * 1.5)
+        if forced is not None:
+            code = forced[j]
+        elif shard_ok and (update == "shard16" or t_s + u_s < t_ar + u_ar):
+            code = "s16"
+        if code == "s16":
+            t_ar, u_ar, wire = t_s, u_s, int(pb * 1.5)
+        elif last and forced is not None and "s16" in forced:
+            u_ar += shard16_tail_us
         start = max(t_main, free) + comm_overhead_us
         free = start + t_ar + u_ar
         busy.append((start, start + t_ar))
+        sgd_busy.append((start + t_ar, free))
         buckets.append(wire)
         ar.append(t_ar)
         plan.append(code)

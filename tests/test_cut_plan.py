@@ -1,12 +1,14 @@
-"""Cut-point chooser of the pipelined multi-GPU DDP step (parallel/cut_plan.py), CPU only.
+"""Cut-point and update-plan chooser of the pipelined multi-GPU DDP step (parallel/cut_plan.py),
+CPU only, against round-5 measurements on one MI355X (profiles/r5d_cut_sweep.md).
 
-Stage backward times are the measured per-stage sums of the round-3 step profiles
-(profiles/r3h_vgg11_b32.md, profiles/r3h_vgg11_b256.md: every kernel of a stage's backward, the
-last stage also carrying the forward); the collective is the one-GPU timed stand-in of
-profiles/r2_pipelined_ddp.md (bytes / 171 or 300 GB/s algorithm bandwidth). The chooser must
-land on a cut set that the measured cut sweep of that file places at (or within a few % of) the
-best, move the cuts when the bandwidth changes, and fall back to one bucket-free plan shape when
-communication is free. Reference: torch DDP's 25 MB buckets, /root/reference/part3/main.py:174.
+STAGES: per-stage backward times of the round-5 kernels (tools/stage_times.py: a step cut before
+every fused stage, no collective; stage 7 also carries the forward, the classifier head and the
+data step). SWEEP: ms/step of bench.py's pipelined step for every cut set x per-bucket update
+plan ("ar" = all-reduce + replicated SGD, "s16" = reduce-scatter + shard SGD + bf16 operand
+all-gather), one-GPU timed stand-in collectives at 171 GB/s (an 8-GPU all-reduce's algorithm
+bandwidth at ~300 GB/s bus bandwidth), sharded as rank 0 of 8. The model must predict every
+swept configuration within 5 %, and its choice must be (near) the measured best.
+Reference: torch DDP's 25 MB buckets, /root/reference/part3/main.py:174.
 """
 import os
 import sys
@@ -16,76 +18,120 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
-from ddp_amd.parallel.cut_plan import plan_cuts, schedule, stand_in_rows  # noqa: E402
+from ddp_amd.parallel.cut_plan import (plan_cuts, schedule, seg_boundary_us,  # noqa: E402
+                                       stand_in_rows)
 
 # fp32 parameter bytes per VGG-11 fused stage (conv w + b, BN gamma + beta); classifier apart
 PBYTES = [6912 + 768, 294912 + 1536, 1179648 + 3072, 2359296 + 3072, 4718592 + 6144,
           9437184 + 6144, 9437184 + 6144, 9437184 + 6144]
 HEAD = 4 * (5120 + 10)
-# us per stage backward (stage 7 + forward + head), round-3 profiles
-STAGES = {32: [27.6, 36.1, 32.1, 37.3, 26.3, 27.6, 29.0, 24.4 + 163.0],
-          256: [55.8, 81.3, 74.9, 93.3, 77.8, 93.3, 50.7, 52.9 + 245.0]}
-# measured ms/step of the cut sweep (profiles/r2_pipelined_ddp.md), per (batch, GB/s)
+# us per stage backward (stage 7 + forward + head), round-5 kernels (gpurun_out/r5d/stages_b*.json)
+STAGES = {32: [33.6, 38.4, 42.8, 52.3, 40.1, 38.2, 41.1, 182.0],
+          64: [36.9, 44.1, 51.4, 58.2, 49.3, 62.7, 40.0, 207.4],
+          128: [44.5, 66.3, 61.1, 77.4, 67.8, 81.4, 47.0, 242.0],
+          256: [62.6, 99.9, 89.7, 113.0, 96.8, 115.7, 66.3, 337.5]}
+# measured ms/step per (cuts, per-bucket plan), per-GPU batch (stand-in at 171 GB/s)
 SWEEP = {
-    (32, 171): {(4,): .7044, (3, 6): .6382, (2, 5): .678, (2, 4, 6): .65, (3, 5, 7): .6105,
-                (1, 3, 5): .6846, (3, 5): .6749, (4, 6): .6403, (2, 6): .6455},
-    (256, 171): {(4,): .9637, (3, 6): .9632, (2, 5): .9411, (2, 4, 6): .949, (3, 5, 7): .9578,
-                 (1, 3, 5): .9401, (3, 5): .9505, (4, 6): .9693, (2, 6): .9694},
-    (32, 300): {(4,): .6139, (3, 6): .5667, (2, 5): .5868, (2, 4, 6): .5741, (3, 5, 7): .5781,
-                (1, 3, 5): .5968, (3, 5): .5849, (4, 6): .5827, (2, 6): .5975},
+    32: {
+        ((3, 6), 'ar,ar,ar'): 0.4637,
+        ((3, 6), 's16,s16,s16'): 0.4349,
+        ((3, 5, 7), 'ar,ar,ar,ar'): 0.445,
+        ((3, 5, 7), 's16,s16,s16,s16'): 0.4416,
+        ((4,), 'ar,ar'): 0.508,
+        ((4,), 's16,s16'): 0.4628,
+        ((2, 5), 'ar,ar,ar'): 0.4847,
+        ((2, 5), 's16,s16,s16'): 0.4617,
+        ((2, 4, 6), 'ar,ar,ar,ar'): 0.4689,
+        ((2, 4, 6), 's16,s16,s16,s16'): 0.4541,
+        ((4, 6), 'ar,ar,ar'): 0.4671,
+        ((4, 6), 's16,s16,s16'): 0.4361,
+        ((5,), 'ar,ar'): 0.4902,
+        ((5,), 's16,s16'): 0.4466,
+        ((3, 6), 's16,s16,ar'): 0.4171,
+        ((3, 6), 's16,ar,ar'): 0.4343,
+    },
+    64: {
+        ((3, 6), 'ar,ar,ar'): 0.4883,
+        ((3, 6), 's16,s16,s16'): 0.5049,
+        ((3, 5, 7), 'ar,ar,ar,ar'): 0.4941,
+        ((3, 5, 7), 's16,s16,s16,s16'): 0.5194,
+        ((2, 5), 'ar,ar,ar'): 0.5374,
+        ((2, 5), 's16,s16,s16'): 0.5149,
+        ((4,), 'ar,ar'): 0.5629,
+        ((4,), 's16,s16'): 0.5186,
+        ((3, 6), 's16,s16,ar'): 0.4884,
+        ((3, 6), 's16,ar,ar'): 0.4934,
+    },
+    128: {
+        ((3, 6), 'ar,ar,ar'): 0.6249,
+        ((3, 6), 's16,s16,s16'): 0.6407,
+        ((3, 5, 7), 'ar,ar,ar,ar'): 0.6443,
+        ((3, 5, 7), 's16,s16,s16,s16'): 0.6472,
+        ((2, 5), 'ar,ar,ar'): 0.6112,
+        ((2, 5), 's16,s16,s16'): 0.6275,
+        ((4,), 'ar,ar'): 0.6391,
+        ((4,), 's16,s16'): 0.6421,
+        ((3, 6), 's16,s16,ar'): 0.6225,
+        ((3, 6), 's16,ar,ar'): 0.6181,
+    },
+    256: {
+        ((3, 6), 'ar,ar,ar'): 0.8959,
+        ((3, 6), 's16,s16,s16'): 0.8619,
+        ((3, 5, 7), 'ar,ar,ar,ar'): 0.9209,
+        ((3, 5, 7), 's16,s16,s16,s16'): 0.8764,
+        ((4,), 'ar,ar'): 0.8809,
+        ((4,), 's16,s16'): 0.8581,
+        ((2, 5), 'ar,ar,ar'): 0.881,
+        ((2, 5), 's16,s16,s16'): 0.859,
+        ((2, 4, 6), 'ar,ar,ar,ar'): 0.916,
+        ((2, 4, 6), 's16,s16,s16,s16'): 0.8749,
+        ((4, 6), 'ar,ar,ar'): 0.9195,
+        ((4, 6), 's16,s16,s16'): 0.8724,
+        ((5,), 'ar,ar'): 0.934,
+        ((5,), 's16,s16'): 0.8954,
+    },
 }
+ROWS = stand_in_rows(8, 171)
 
 
-@pytest.mark.parametrize("batch,gbps", sorted(SWEEP))
-def test_chooser_lands_near_the_measured_best_cut_set(batch, gbps):
-    meas = SWEEP[(batch, gbps)]
-    best, ranked = plan_cuts(STAGES[batch], PBYTES, stand_in_rows(8, gbps), head_bytes=HEAD,
-                             candidates=list(meas))
-    pick = tuple(best["cuts"])
-    assert meas[pick] <= min(meas.values()) * 1.04, (pick, meas[pick], min(meas.values()))
-    # the round-2 fixed defaults (3,6 up to 128 images per GPU, 2,5 at 256) are in the running
-    default = (3, 6) if batch <= 128 else (2, 5)
-    sched = schedule(STAGES[batch], PBYTES, default, stand_in_rows(8, gbps), head_bytes=HEAD)
-    assert sched["step_us"] <= best["step_us"] * 1.08
+def predict(batch, cuts, plan):
+    return schedule(STAGES[batch], PBYTES, cuts, ROWS, head_bytes=HEAD,
+                    seg_overhead_us=seg_boundary_us(batch), update=plan.split(","),
+                    world=8)["step_us"] / 1000.0
 
 
-def test_measured_best_reproduced_on_the_full_search():
-    # 8-GPU-sized stand-in at 171 GB/s: the sweep's best 3-cut set at 32 images / GPU and the
-    # 2,5 default at 256 (within the model's tie) come out of the unrestricted search too
-    b32, _ = plan_cuts(STAGES[32], PBYTES, stand_in_rows(8, 171), head_bytes=HEAD)
-    assert len(b32["cuts"]) == 3 and b32["cuts"][-2:] == [5, 7]
-    b256, _ = plan_cuts(STAGES[256], PBYTES, stand_in_rows(8, 171), head_bytes=HEAD,
-                        candidates=list(SWEEP[(256, 171)]))
-    assert b256["cuts"] == [2, 5]
+@pytest.mark.parametrize("batch", sorted(SWEEP))
+def test_model_predicts_every_swept_configuration(batch):
+    errs = {k: predict(batch, k[0], k[1]) / v - 1 for k, v in SWEEP[batch].items()}
+    worst = max(errs.items(), key=lambda kv: abs(kv[1]))
+    assert abs(worst[1]) < 0.05, worst
 
 
-def test_cuts_move_with_bandwidth():
-    st = STAGES[32]
-    slow, _ = plan_cuts(st, PBYTES, stand_in_rows(8, 50), head_bytes=HEAD)
-    mid, _ = plan_cuts(st, PBYTES, stand_in_rows(8, 171), head_bytes=HEAD)
-    fast, _ = plan_cuts(st, PBYTES, stand_in_rows(8, 2000), head_bytes=HEAD)
-    # a fast link needs few segment boundaries (each costs a graph gap); a slow one wants the
-    # big 512-channel buckets split off early so their all-reduces start during the backward
-    assert len(fast["cuts"]) < len(mid["cuts"])
-    assert slow["cuts"] != mid["cuts"]
-    assert slow["exposed_us"] > mid["exposed_us"] > fast["exposed_us"] >= 0
-    # bf16 wire = half the bytes: never predicted slower than fp32
-    f32, _ = plan_cuts(st, PBYTES, stand_in_rows(8, 171), head_bytes=HEAD)
-    b16, _ = plan_cuts(st, PBYTES, stand_in_rows(8, 171), head_bytes=HEAD, wire_scale=0.5)
-    assert b16["step_us"] <= f32["step_us"]
-    assert sum(b16["bucket_bytes"]) * 2 == pytest.approx(sum(f32["bucket_bytes"]), rel=1e-6)
+@pytest.mark.parametrize("batch", sorted(SWEEP))
+def test_choice_among_swept_configurations_is_near_the_measured_best(batch):
+    meas = SWEEP[batch]
+    pick = min(meas, key=lambda k: predict(batch, k[0], k[1]))
+    assert meas[pick] <= min(meas.values()) * 1.03, (pick, meas[pick], min(meas.values()))
 
 
-def test_schedule_accounting():
-    st = [10.0, 10.0, 10.0, 100.0]
-    pb = [1000, 1000, 1000, 1000]
-    rows = stand_in_rows(2, 1.0)  # 1 GB/s: 1 us per KB
-    r = schedule(st, pb, [2], rows, seg_overhead_us=0.0, sgd_us=lambda b: 0.0,
-                 comm_overhead_us=0.0, contention=0.0)
-    # segment 0 = stages 2,3 (110 us), its bucket (2000 B = 2 us) runs under segment 1
-    assert r["bucket_bytes"] == [2000, 2000]
-    assert r["backward_us"] == pytest.approx(130.0)
-    assert r["step_us"] == pytest.approx(132.0)  # the last bucket is exposed
-    assert r["exposed_us"] == pytest.approx(2.0)
-    with pytest.raises(ValueError):
-        schedule(st, pb, [0], rows)
+def test_auto_plan_shards_the_big_buckets_and_not_the_last_at_32_images():
+    # 32 images / GPU, cuts 3,6: the measured best plan is s16,s16,ar (0.417 ms vs 0.445 for the
+    # best all-reduce plan); the planner's per-bucket choice must reproduce it
+    best, _ = plan_cuts(STAGES[32], PBYTES, ROWS, head_bytes=HEAD, update="auto", world=8,
+                        seg_overhead_us=seg_boundary_us(32), candidates=[(3, 6)])
+    assert best["update"] == ["s16", "s16", "ar"]
+    assert best["step_us"] < schedule(STAGES[32], PBYTES, (3, 6), ROWS, head_bytes=HEAD,
+                                      seg_overhead_us=seg_boundary_us(32))["step_us"]
+
+
+def test_single_rank_never_shards_and_bf16_wire_never_shards():
+    for kw in ({"world": 1}, {"world": 8, "wire_scale": 0.5}):
+        r = schedule(STAGES[32], PBYTES, (3, 6), ROWS, head_bytes=HEAD, update="auto", **kw)
+        assert r["update"] == ["ar", "ar", "ar"]
+
+
+def test_full_search_prefers_fewer_cuts_within_the_tie():
+    best, ranked = plan_cuts(STAGES[256], PBYTES, ROWS, head_bytes=HEAD, update="auto", world=8,
+                             seg_overhead_us=seg_boundary_us(256))
+    assert 1 <= len(best["cuts"]) <= 3
+    assert ranked[0][0] <= best["step_us"] + 1.0
