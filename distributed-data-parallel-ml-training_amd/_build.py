@@ -56,10 +56,28 @@ def _newest_header():
     return max((os.path.getmtime(h) for h in hs), default=0.0)
 
 
+def _deps(obj):
+    """Headers the object was built from (the compiler's -MMD file), or None if unknown."""
+    d = obj + ".d"
+    if not os.path.exists(d):
+        return None
+    with open(d) as f:
+        text = f.read().replace("\\\n", " ")
+    parts = text.split(":", 1)
+    return [t for t in parts[1].split()] if len(parts) == 2 else None
+
+
 def _compile(cmd, src, obj, hdr_time, verbose):
     if os.path.exists(obj):
         t = os.path.getmtime(obj)
-        if t >= os.path.getmtime(src) and t >= hdr_time:
+        deps = _deps(obj)
+        # a source is rebuilt when it or a header IT includes changed (all headers when the
+        # dependency file is missing)
+        newest = (max([os.path.getmtime(x) for x in deps if os.path.exists(x)] + [0.0])
+                  if deps is not None else hdr_time)
+        if deps is not None and any(not os.path.exists(x) for x in deps):
+            newest = hdr_time
+        if t >= os.path.getmtime(src) and t >= newest:
             return obj, False
     if verbose:
         print("[ddp_amd build]", os.path.relpath(src, PKG_DIR), flush=True)
@@ -109,13 +127,14 @@ def _build_variant(variant, verbose=True, jobs=None):
     tasks = []
     for src in sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))):
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-x", "hip", *common, *inc, "-c", src, "-o", obj]
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-x", "hip", *common, *inc, "-c", src, "-o", obj,
+               "-MMD", "-MF", obj + ".d"]
         tasks.append((cmd, src, obj))
     host_srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))) + [os.path.join(CSRC, "bind.cpp")]
     for src in host_srcs:
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         cmd = [hipcc, "-x", "c++", "-D__HIP_PLATFORM_AMD__", *common, "-fvisibility=hidden", *inc,
-               "-c", src, "-o", obj]
+               "-c", src, "-o", obj, "-MMD", "-MF", obj + ".d"]
         tasks.append((cmd, src, obj))
     jobs = jobs or min(8, os.cpu_count() or 4)
     changed = False

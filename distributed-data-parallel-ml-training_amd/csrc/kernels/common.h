@@ -54,6 +54,20 @@ __device__ __forceinline__ float stat_val(float v, int b) {
 #endif
 }
 
+// One SGD element update (torch.optim.SGD: d = g + wd p; b = m b + d; d = nesterov ? d + m b : b;
+// p -= lr d), with every multiply-add an explicit fma in one fixed order: the optimizer launch
+// (optim.hip) and the SGD in the WGRAD finish (conv_igemm.hip) are separate translation units,
+// and left to -ffp-contract they round differently (1 ulp; tests/test_gpu_deterministic.py).
+__device__ __forceinline__ float sgd_update1(float p, float g, float& b, float lr, float momentum,
+                                             float wd, float grad_scale, int nesterov) {
+  float d = __builtin_fmaf(wd, p, g * grad_scale);
+  if (momentum != 0.f) {
+    b = __builtin_fmaf(momentum, b, d);
+    d = nesterov ? __builtin_fmaf(momentum, b, d) : b;
+  }
+  return __builtin_fmaf(-lr, d, p);
+}
+
 // bf16 <-> fp32 bit conversions. round-to-nearest-even; NaN kept NaN.
 __device__ __forceinline__ float bf2f(unsigned short h) {
   return __uint_as_float(((unsigned int)h) << 16);

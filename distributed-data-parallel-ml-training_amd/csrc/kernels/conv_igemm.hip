@@ -1602,12 +1602,7 @@ __global__ __launch_bounds__(256) void wgrad_finish_kernel(const float* ws, int 
 // this is a vectorised sum of the slabs — no transpose. blockIdx.y = group of kWgFinishGroupKrsc
 // slabs (fixed order inside a group); several groups combine with atomics.
 __device__ __forceinline__ float sgd_step1(float p, float g, float& b, const SgdFuse& h) {
-  float d = g * h.grad_scale + h.wd * p;
-  if (h.momentum != 0.f) {
-    b = h.momentum * b + d;
-    d = h.nesterov ? d + h.momentum * b : b;
-  }
-  return p - h.lr * d;
+  return sgd_update1(p, g, b, h.lr, h.momentum, h.wd, h.grad_scale, h.nesterov);
 }
 
 // With ``sg.p`` (SGD in the backward, api.h SgdFuse; single group only: the sum is the final

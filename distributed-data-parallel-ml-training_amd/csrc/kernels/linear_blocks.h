@@ -10,7 +10,9 @@ constexpr int kMaxJ = 16;
 
 // dW / db: block = 64 feature columns x one 64-row batch chunk (4 row groups of 16 rows);
 // partial sums reduced through LDS, one atomic per (j, f) per block.
-constexpr int kDwRows = 8;  // many small row chunks: latency-bound otherwise
+// many small row chunks (latency-bound otherwise), combined with float atomics; the
+// deterministic build takes every row in one chunk (one add per address onto zero)
+constexpr int kDwRows = kDeterministic ? (1 << 24) : 8;
 __device__ __forceinline__ void linear_dw_block(const float* __restrict__ dlogits,
                                                 const unsigned short* __restrict__ x, int B, int F,
                                                 int J, const float* gscale, float* dW, float* db,

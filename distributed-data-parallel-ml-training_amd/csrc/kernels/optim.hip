@@ -31,24 +31,14 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
     float* bb = &bv.x;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      float d = gg[e] * grad_scale + wd * pp[e];
-      if (momentum != 0.f) {
-        bb[e] = momentum * bb[e] + d;
-        d = nesterov ? d + momentum * bb[e] : bb[e];
-      }
-      pp[e] -= lr * d;
+      pp[e] = sgd_update1(pp[e], gg[e], bb[e], lr, momentum, wd, grad_scale, nesterov);
     }
     reinterpret_cast<float4*>(p)[i] = pv;
     reinterpret_cast<float4*>(buf)[i] = bv;
   }
   // scalar tail
   for (size_t i = n4 * 4 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += stride) {
-    float d = g[i] * grad_scale + wd * p[i];
-    if (momentum != 0.f) {
-      buf[i] = momentum * buf[i] + d;
-      d = nesterov ? d + momentum * buf[i] : buf[i];
-    }
-    p[i] -= lr * d;
+    p[i] = sgd_update1(p[i], g[i], buf[i], lr, momentum, wd, grad_scale, nesterov);
   }
 }
 
@@ -155,12 +145,7 @@ __device__ __forceinline__ void signal_flag(unsigned* done, unsigned* signal) {
 }
 
 __device__ __forceinline__ float sgd1(float p, float g, float& b, const SgdHyper& h) {
-  float d = g * h.grad_scale + h.wd * p;
-  if (h.momentum != 0.f) {
-    b = h.momentum * b + d;
-    d = h.nesterov ? d + h.momentum * b : b;
-  }
-  return p - h.lr * d;
+  return sgd_update1(p, g, b, h.lr, h.momentum, h.wd, h.grad_scale, h.nesterov);
 }
 
 __device__ void sgd_pack_body(const int4* __restrict__ items, const long long* __restrict__ descs,

@@ -547,6 +547,54 @@ def test_shard16_emulated_world_updates_rank0_shard(native_ext, scale):
     m.close()
 
 
+@pytest.mark.parametrize("batch", [32, 256])
+def test_sgd_in_backward_covers_every_parameter_once(native_ext, batch):
+    """SGD in the backward (engine/step.py TrainStep.opt_in_bwd, one GPU): the conv weights whose
+    WGRAD finish took the update are exactly excluded from the step's SGD launch, that launch
+    covers every other parameter, and nothing is in both (a weight updated twice would take a
+    second momentum step; one in neither would never train). Eager and captured. The values are
+    compared bitwise against the separate SGD launch in the deterministic-statistics build
+    (tests/test_gpu_deterministic.py, "sgd_in_bwd_equals_separate")."""
+    from ddp_amd.models import VGG11
+    from ddp_amd.engine import CrossEntropyLoss, TrainStep
+    from ddp_amd.optim import FusedSGD
+    from ddp_amd.data import SyntheticCIFAR10, DeviceLoader
+    torch.manual_seed(5)
+    m = VGG11().cuda()
+    opt = FusedSGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    ld = DeviceLoader(SyntheticCIFAR10(True, n=2 * batch), batch, "cuda", cpad=8)
+    st = TrainStep(m, opt, CrossEntropyLoss(), ld)
+    assert st.opt_in_bwd
+    seen = []
+    orig = opt._work_table
+
+    def spy(prange=None, exclude=frozenset()):
+        r = orig(prange, exclude)
+        seen.append((prange, frozenset(exclude)))
+        return r
+    opt._work_table = spy
+    st._body()
+    st.warmup(1)
+    st.capture()
+    st.step()
+    torch.cuda.synchronize()
+    opt._work_table = orig
+    calls = [(p, e) for p, e in seen if p is None]
+    assert calls, "the step's SGD launch never built its work table"
+    registered = set(opt._bwd_index.values())
+    n = len(opt.arena.params)
+    for _, exclude in calls:
+        assert exclude <= registered, exclude - registered
+        keep = [i for i in range(n) if i not in exclude]
+        items = {i for i in keep if opt._per_param[i]}
+        assert items == set(keep), set(keep) - items  # every kept parameter has work items
+        assert not items & exclude
+        assert items | exclude == set(range(n))
+    # at 256 images every conv weight's WGRAD has a split-K finish that takes the update
+    if batch == 256:
+        assert any(len(e) > 0 for _, e in calls)
+
+
 def _plain_vgg_forward(model, x):
     """The reference forward (/root/reference/part1/model.py:42-46) on ATen, any device, fp32."""
     y = model.layers(x)

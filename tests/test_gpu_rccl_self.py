@@ -316,7 +316,7 @@ def test_captured_strategy_step_with_live_rccl(native_ext, strategy):
     # already differ (measured cos 0.99-0.999, tools/probes/grad_determinism.py); a synced step
     # must sit within 3x that noise of the reference
     noise = 1.0 - min(_cos(e_ref[0], e_ref[1]), _cos(e_ref[0], e_ref[2]), _cos(e_ref[1], e_ref[2]))
-    tol = min(0.99, 1.0 - 3.0 * noise)
+    tol = max(0.97, min(0.99, 1.0 - 3.0 * noise))  # floored: a worse race must not loosen it
     assert float(e_ref[0].norm()) > 0
     for d in [e_sync] + replays:
         assert not torch.isnan(d).any()
@@ -338,7 +338,7 @@ def test_profile_stage_times_rolls_back_and_feeds_cut_plan(native_ext):
     from ddp_amd.engine import CrossEntropyLoss
     from ddp_amd.engine.step import profile_stage_times
     from ddp_amd.parallel import DistributedDataParallel, RcclCommunicator
-    from ddp_amd.parallel.cut_plan import plan_cuts, stand_in_rows
+    from ddp_amd.parallel.cut_plan import plan_cuts, seg_boundary_us, stand_in_rows
     torch.manual_seed(17)
     m = DistributedDataParallel(VGG11().cuda(), RcclCommunicator(0, 1, 0, self_comm=False),
                                 bucket_cap_mb=256.0, first_bucket_cap_mb=256.0)
@@ -356,7 +356,9 @@ def test_profile_stage_times_rolls_back_and_feeds_cut_plan(native_ext):
     assert torch.equal(ld.cursor, snap[2])
     pbytes = [4 * sum(p.numel() for p in (sp.conv.weight, sp.conv.bias, sp.bn.weight, sp.bn.bias))
               for sp in m.module.fused_plan()]
-    best, ranked = plan_cuts(us, pbytes, stand_in_rows(8, 171.0), head_bytes=4 * 5130)
+    best, ranked = plan_cuts(us, pbytes, stand_in_rows(8, 171.0), head_bytes=4 * 5130,
+                             seg_overhead_us=seg_boundary_us(32))
     assert best["cuts"] and all(0 < c < n for c in best["cuts"])
-    assert best["step_us"] >= sum(us)
+    # each profiled stage holds one segment boundary; a plan with fewer cuts saves the rest
+    assert best["step_us"] >= sum(us) - (n - 1 - len(best["cuts"])) * seg_boundary_us(32)
     m.close()
