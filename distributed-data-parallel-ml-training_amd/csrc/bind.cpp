@@ -573,6 +573,22 @@ PYBIND11_MODULE(_native, m) {
   m.def("unpack_bf16", [](uintptr_t y, size_t n, uintptr_t x, uintptr_t st) {
     check(ddp_unpack_bf16(P<unsigned short>(y), n, P<float>(x), S(st)), "unpack_bf16");
   });
+  // raw hipMemsetAsync / hipMemcpyAsync (D2D): tests/test_gpu_graph_memset.py checks the
+  // ordering of captured memset / memcpy graph nodes against kernel nodes (the library itself
+  // uses the copy / fill kernels above inside captured steps)
+  m.def("memset_async", [](uintptr_t p, int value, size_t n, uintptr_t st) {
+    check((int)hipMemsetAsync(P<void>(p), value, n, S(st)), "hipMemsetAsync");
+  });
+  m.def("memcpy_async", [](uintptr_t dst, uintptr_t src, size_t n, uintptr_t st) {
+    check((int)hipMemcpyAsync(P<void>(dst), P<void>(src), n, hipMemcpyDeviceToDevice, S(st)),
+          "hipMemcpyAsync");
+  });
+  m.def("copy_bytes", [](uintptr_t dst, uintptr_t src, size_t n, uintptr_t st) {
+    check(ddp_copy_bytes(P<void>(dst), P<void>(src), n, S(st)), "copy_bytes");
+  });
+  m.def("fill_bytes", [](uintptr_t dst, int value, size_t n, uintptr_t st) {
+    check(ddp_fill_bytes(P<void>(dst), value, n, S(st)), "fill_bytes");
+  });
   m.def("scale", [](uintptr_t x, size_t n, float s, uintptr_t st) {
     check(ddp_scale(P<float>(x), n, s, S(st)), "scale");
   });
