@@ -27,18 +27,39 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tools"))
 
 PEAK_TFLOPS = 2500.0
+# --trace (round 5): each timed phase is bracketed by marker kernels whose GRID SIZE encodes the
+# phase id, so tools/probes/roofline_trace.py can sum the KERNEL durations of a rocprofv3 kernel
+# trace per phase. Host-issued launch loops timed with two events (the default) measure the
+# dispatch floor on small GEMMs (~18 us for every b32 hipBLASLt cell in round 4), not the GEMM.
+TRACE = {"on": False, "phases": [], "marker": None}
 
 
-def timeit(fn, reps=30):
+def _marker(pid):
+    import torch
+    from ddp_amd.ops.common import native
+    if TRACE["marker"] is None:
+        TRACE["marker"] = torch.zeros(4096 * 256 * 16 + 16, dtype=torch.uint8, device="cuda")
+    # fill_bytes launches ceil((n / 16 + 1) / 256) workgroups: n = pid * 4096 + 16 -> pid + 1
+    native().fill_bytes(TRACE["marker"].data_ptr(), 0, pid * 4096 + 16,
+                        torch.cuda.current_stream().cuda_stream)
+
+
+def timeit(fn, reps=30, label=None):
     import torch
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
+    if TRACE["on"]:
+        pid = len(TRACE["phases"]) + 1
+        TRACE["phases"].append({"id": pid, "label": label, "reps": reps})
+        _marker(pid)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
         fn()
     e1.record()
+    if TRACE["on"]:
+        _marker(0)
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) * 1000.0 / reps
 
@@ -47,7 +68,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, nargs="+", default=[256])
     ap.add_argument("--json", default=None)
+    ap.add_argument("--trace", default=None,
+                    help="write the phase list here; run under rocprofv3 --kernel-trace and "
+                         "post-process with tools/probes/roofline_trace.py")
     a = ap.parse_args()
+    TRACE["on"] = bool(a.trace)
     import torch
     import ddp_amd  # noqa: F401
     from ddp_amd.ops.layers import ConvBNActSpec, conv_forward, conv_backward
@@ -63,7 +88,8 @@ def main():
             x = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
             dz = torch.randn(N, H, W, K, device=dev).to(torch.bfloat16)
             dw = torch.zeros_like(conv.weight)
-            stats = torch.zeros(16 * 2 * K, device=dev)
+            from ddp_amd.ops.common import stat_replicas
+            stats = torch.zeros(stat_replicas() * 2 * K, device=dev)
             M = N * H * W
             gf = 2.0 * M * K * 9 * Cr / 1e9
             shapes = {"fwd": (M, K, 9 * Cr), "dgrad": (M, Cr, 9 * K), "wgrad": (K, 9 * Cr, M)}
@@ -71,15 +97,17 @@ def main():
             for name, (m, n, k) in shapes.items():
                 A = torch.randn(m, k, device=dev, dtype=torch.bfloat16)
                 Bm = torch.randn(k, n, device=dev, dtype=torch.bfloat16)
-                mm[name] = timeit(lambda: torch.matmul(A, Bm))
+                mm[name] = timeit(lambda: torch.matmul(A, Bm), label=(B, li, "mm_" + name))
                 del A, Bm
-            ours = {"fwd": timeit(lambda: conv_forward(spec, x, None, stats))}
+            ours = {"fwd": timeit(lambda: conv_forward(spec, x, None, stats), label=(B, li, "ours_fwd"))}
             if li == 0:  # the input layer has no dx
-                ours["wgrad"] = timeit(lambda: conv_backward(spec, x, dz, dw, False))
+                ours["wgrad"] = timeit(lambda: conv_backward(spec, x, dz, dw, False),
+                                       label=(B, li, "ours_bwd"))
                 mm_bwd = mm["wgrad"]
                 bwd_gf = gf
             else:
-                ours["bwd_pair"] = timeit(lambda: conv_backward(spec, x, dz, dw, True))
+                ours["bwd_pair"] = timeit(lambda: conv_backward(spec, x, dz, dw, True),
+                                          label=(B, li, "ours_bwd"))
                 mm_bwd = mm["dgrad"] + mm["wgrad"]
                 bwd_gf = 2 * gf
             ours_bwd = ours.get("bwd_pair", ours.get("wgrad"))
@@ -106,6 +134,9 @@ def main():
     if a.json:
         with open(a.json, "w") as f:
             json.dump(rows, f, indent=1)
+    if a.trace:
+        with open(a.trace, "w") as f:
+            json.dump({"phases": TRACE["phases"], "rows": rows}, f, indent=1)
 
 
 if __name__ == "__main__":
