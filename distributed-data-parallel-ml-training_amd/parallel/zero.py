@@ -285,11 +285,19 @@ class ShardedBf16Update:
         self.opt.repack()
 
     def _device_tables(self, j):
+        items = self.shard_items(j, self.rank)
+        dev = self.arena.data.device
+        return torch.tensor(items, dtype=torch.int32, device=dev), len(items)
+
+    def shard_items(self, j, rank):
+        """Work items of ``rank``'s update launch for bucket j (optim.hip sgd_pack_kernel):
+        {3, offset, count, slot offset | -1} over its shard (SGD + bf16 operand + small-tensor
+        send slot), {4, offset, count, -} clearing the rest of the bucket's gradients."""
         (_, (lo, hi)) = self.buckets[j]
         plan = self._plan[j]
-        s0, s1 = self.shard(j)
+        s0, s1 = self.shard(j, rank)
         items = []
-        mine = {s: k for s, _, k in plan["small"][self.rank]}
+        mine = {s: k for s, _, k in plan["small"][rank]}
         for s, e, op in self._pieces(s0, s1):
             for c0 in range(s, e, 8192):
                 c1 = min(e, c0 + 8192)
@@ -297,13 +305,13 @@ class ShardedBf16Update:
         for a0, a1 in ((lo, s0), (s1, hi)):
             for c0 in range(a0, a1, 65536):
                 items.append([4, c0, min(a1, c0 + 65536) - c0, 0])
-        dev = self.arena.data.device
-        return torch.tensor(items, dtype=torch.int32, device=dev), len(items)
+        return items
 
-    def _tail_table(self):
-        """Unpack segments of every sharded bucket (gathered slot -> fp32 arena; emulated: this
-        rank's own only, the other ranks' slots hold nothing) and the operands to re-pack."""
-        segs, descs = [], []
+    def tail_segments(self):
+        """Copy segments of the step tail (optim.hip shard_tail_kernel): {slot index, arena
+        index, count, -} for every sharded bucket's gathered small-tensor values (emulated: this
+        rank's own only — the other ranks' slots hold nothing)."""
+        segs = []
         ranks = [self.rank] if self.emulated else range(self.world)
         for j in sorted(self.which):
             plan = self._plan[j]
@@ -312,7 +320,13 @@ class ShardedBf16Update:
                 for s, c, k in plan["small"][r]:
                     for c0 in range(0, c, 4096):
                         segs.append([row + k + c0, s + c0, min(4096, c - c0), 0])
-            descs += [self.arena.params[i]._ddp_amd_pack() for i in plan["repack"]]
+        return segs
+
+    def _tail_table(self):
+        """Tail copy segments (device table) and the operands to re-pack."""
+        segs, descs = self.tail_segments(), []
+        for j in sorted(self.which):
+            descs += [self.arena.params[i]._ddp_amd_pack() for i in self._plan[j]["repack"]]
         if len(descs) > 4:
             raise ValueError("more than 4 channel-padded operands to re-pack in the step tail")
         dev = self.arena.data.device

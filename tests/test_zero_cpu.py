@@ -80,3 +80,79 @@ def test_shard16_matches_replicated(world):
         assert len({b - a for a, b in spans}) == 1
     rs, ag = map(sum, zip(*out[0]["wire"]))
     assert 1.5 * rs / 2 <= rs + ag <= 0.76 * 2 * rs  # 6 B vs 8 B per operand parameter
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_shard16_device_tables_simulated(world):
+    """The GPU launch tables of the sharded update (parallel/zero.py shard_items /
+    tail_segments, consumed by optim.hip sgd_pack_kernel items 3 / 4 and shard_tail_kernel) for
+    every rank of a ``world``-rank job, executed by a host model of those kernels and of the
+    grouped all-gather: every arena element of a bucket is updated by exactly one rank (item 3)
+    and cleared by every other (item 4); after the all-gather of the send slots and the tail's
+    copies, every rank's fp32 masters of the small tensors equal their owners' values; the bf16
+    operand image of every element comes from its owner. CPU only (no collectives, no GPU)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from ddp_amd.models import VGG11
+    from ddp_amd.optim.arena import ParamArena
+    from ddp_amd.parallel.zero import ShardedBf16Update, arena_buckets
+
+    class _Comm:
+        def __init__(self, rank):
+            self.rank, self.world = rank, world
+
+    class _Opt:
+        pass
+    torch.manual_seed(0)
+    m = VGG11()
+    arena = ParamArena(list(m.parameters()), krsc=False)
+    pidx = {id(p): i for i, p in enumerate(arena.params)}
+    buckets = arena_buckets(arena, [pidx[id(m.layers[i].weight)] for i in (11, 22)])
+    ups = [ShardedBf16Update(arena, _Opt(), _Comm(r), buckets) for r in range(world)]
+    total = arena.total
+    # "new master" values each owner computes for its shard: a recognisable function of index
+    newval = torch.arange(total, dtype=torch.float32) * 0.5 + 1.0
+    masters = [arena.data.detach().clone() for _ in range(world)]
+    slots = [torch.full_like(ups[0].slots, float("nan")) for _ in range(world)]
+    shadow = [torch.zeros(total, dtype=torch.float32) for _ in range(world)]
+    updated = torch.zeros(total, dtype=torch.int32)
+    for j in range(len(buckets)):
+        (_, (lo, hi)) = buckets[j]
+        plan = ups[0]._plan[j]
+        for r in range(world):
+            row0 = plan["slot_base"] + r * plan["M"]
+            cleared = torch.zeros(total, dtype=torch.bool)
+            for kind, off, cnt, slot in ups[r].shard_items(j, r):
+                assert off % 4 == 0 and cnt % 4 == 0 and lo <= off and off + cnt <= hi
+                if kind == 3:
+                    masters[r][off:off + cnt] = newval[off:off + cnt]
+                    shadow[r][off:off + cnt] = newval[off:off + cnt]
+                    updated[off:off + cnt] += 1
+                    if slot >= 0:
+                        assert slot % 4 == 0 and slot + cnt <= plan["M"]
+                        slots[r][row0 + slot:row0 + slot + cnt] = newval[off:off + cnt]
+                else:
+                    assert kind == 4
+                    cleared[off:off + cnt] = True
+            s0, s1 = ups[r].shard(j, r)
+            assert bool(cleared[lo:s0].all()) and bool(cleared[s1:hi].all())
+            assert not bool(cleared[s0:s1].any())
+        # grouped all-gather: operand image rows and slot rows from their owners
+        for r in range(world):
+            for q in range(world):
+                a, b = ups[q].shard(j, q)
+                shadow[r][a:b] = shadow[q][a:b]
+                rq = plan["slot_base"] + q * plan["M"]
+                slots[r][rq:rq + plan["M"]] = slots[q][rq:rq + plan["M"]]
+    assert bool((updated == 1).all()), "every element updated by exactly one rank"
+    for r in range(world):
+        for src, dst, cnt, _ in ups[r].tail_segments():
+            masters[r][dst:dst + cnt] = slots[r][src:src + cnt]
+    small = torch.ones(total, dtype=torch.bool)
+    for t0, t1, is_op in ups[0]._tensors:
+        if is_op:
+            small[t0:t1] = False
+    for r in range(world):
+        assert torch.equal(masters[r][small], newval[small]), r  # small tensors complete everywhere
+        assert torch.equal(shadow[r], newval)  # operand image complete everywhere
