@@ -555,9 +555,11 @@ PYBIND11_MODULE(_native, m) {
   m.def("mean_ws", [](uintptr_t in, size_t n, int ws, uintptr_t out, uintptr_t st) {
     check(ddp_mean_ws(P<float>(in), n, ws, P<float>(out), S(st)), "mean_ws");
   });
-  m.def("comm_standin", [](uintptr_t x, size_t n, int blocks, float usec, float scale, uintptr_t st) {
-    check(ddp_comm_standin(P<float>(x), n, blocks, usec, scale, S(st)), "comm_standin");
-  });
+  m.def("comm_standin", [](uintptr_t x, size_t n, int blocks, float usec, float scale, uintptr_t st,
+                           int passes) {
+    check(ddp_comm_standin(P<float>(x), n, blocks, usec, scale, passes, S(st)), "comm_standin");
+  }, py::arg("x"), py::arg("n"), py::arg("blocks"), py::arg("usec"), py::arg("scale"),
+     py::arg("stream"), py::arg("passes") = 1);
   m.def("flag_signal", [](uintptr_t flag, uintptr_t st) {
     check(ddp_flag_signal(P<unsigned>(flag), S(st)), "flag_signal");
   });

@@ -305,7 +305,8 @@ int ddp_scale(float* x, size_t n, float s, hipStream_t st);
 // kernel copy / byte fill (graph-capture-safe stand-ins for hipMemcpyAsync / hipMemsetAsync)
 int ddp_copy_bytes(void* dst, const void* src, size_t n, hipStream_t st);
 int ddp_fill_bytes(void* dst, int value, size_t n, hipStream_t st);
-int ddp_comm_standin(float* x, size_t n, int blocks, float usec, float scale, hipStream_t st);
+int ddp_comm_standin(float* x, size_t n, int blocks, float usec, float scale, int passes,
+                     hipStream_t st);
 int ddp_flag_signal(unsigned* flag, hipStream_t st);
 int ddp_flag_wait(const unsigned* flag, unsigned* expected, unsigned* err, float timeout_s,
                   hipStream_t st);

@@ -39,23 +39,30 @@ __global__ __launch_bounds__(256) void scale_kernel(float* x, size_t n, float s)
 }
 
 __global__ __launch_bounds__(256) void comm_standin_kernel(float* x, size_t n, long long ticks,
-                                                           float scale) {
+                                                           float scale, int passes) {
   // one read + write pass over the bucket (x *= scale: with scale != 1 a consumer that does not
   // wait for the collective reads the old values, tests), then hold the CU until the modelled
   // time has elapsed since the kernel started: the modelled collective time INCLUDES its own
   // memory traffic, as an RCCL kernel's does (until round 4 the pass ran after the full wait,
   // adding ~20-30 us per 19 MB bucket on top of the model)
+  // passes > 1 ("busy" stand-in): that many paced read + write passes spread over the modelled
+  // time instead of one pass and a sleep — the memory traffic of a live collective (a ring
+  // all-reduce reads and writes its bucket ~2 (w-1)/w times each way) beside the backward
   const long long t0 = wall_clock64();
   const size_t stride = (size_t)gridDim.x * blockDim.x;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n / 4; i += stride) {
-    float4 v = reinterpret_cast<float4*>(x)[i];
-    v.x *= scale; v.y *= scale; v.z *= scale; v.w *= scale;
-    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));  // keep the store at scale 1
-    reinterpret_cast<float4*>(x)[i] = v;
+  for (int p = 0; p < passes; ++p) {
+    const float sc = p == passes - 1 ? scale : 1.f;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n / 4; i += stride) {
+      float4 v = reinterpret_cast<float4*>(x)[i];
+      v.x *= sc; v.y *= sc; v.z *= sc; v.w *= sc;
+      asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));  // keep the store at scale 1
+      reinterpret_cast<float4*>(x)[i] = v;
+    }
+    if (blockIdx.x == 0)
+      for (size_t i = (n / 4) * 4 + threadIdx.x; i < n; i += blockDim.x) x[i] *= sc;
+    const long long until = t0 + ticks * (p + 1) / passes;
+    while (wall_clock64() - until < 0) __builtin_amdgcn_s_sleep(4);
   }
-  if (blockIdx.x == 0)
-    for (size_t i = (n / 4) * 4 + threadIdx.x; i < n; i += blockDim.x) x[i] *= scale;
-  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(4);
 }
 
 __global__ __launch_bounds__(64) void flag_signal_kernel(unsigned* flag) {
@@ -210,12 +217,12 @@ extern "C" int ddp_scale(float* x, size_t n, float s, hipStream_t st) {
 }
 
 extern "C" int ddp_comm_standin(float* x, size_t n, int blocks, float usec, float scale,
-                                hipStream_t st) {
+                                int passes, hipStream_t st) {
   const int khz = wall_khz();
   if ((uintptr_t)x % 16) return -1;
   const long long ticks = (long long)((double)usec * khz / 1000.0);
   hipLaunchKernelGGL(comm_standin_kernel, dim3(blocks < 1 ? 1 : blocks), dim3(256), 0, st, x, n, ticks,
-                     scale);
+                     scale, passes < 1 ? 1 : passes);
   return (int)hipGetLastError();
 }
 

@@ -390,7 +390,7 @@ void Reducer::launch(int b) {
     // one pass over the bucket, like the reduction kernel of an all-reduce
     if (emulate_gbps_ > 0.0) {
       const float us = (float)(4.0 * bs.count / (emulate_gbps_ * 1e3));
-      if (ddp_comm_standin(buf, bs.count, emulate_blocks_, us, 1.0f, target) != 0)
+      if (ddp_comm_standin(buf, bs.count, emulate_blocks_, us, 1.0f, 1, target) != 0)
         throw std::runtime_error("emulated collective launch failed");
     } else {
       for (int i = 0; i < emulate_passes_; ++i)

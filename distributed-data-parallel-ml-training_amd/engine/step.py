@@ -253,7 +253,7 @@ class SegmentedDDPStep(TrainStep):
 
     def __init__(self, ddp, optimizer, criterion, loader, split=4, emulate=0, emulate_gbps=0.0,
                  emulate_scale=1.0, grad_comm="fp32", zero=False, collectives=True,
-                 update="allreduce", emulate_world=8):
+                 update="allreduce", emulate_world=8, emulate_passes=1):
         super().__init__(ddp, optimizer, criterion, loader, sync=None, use_graph=True)
         # every bucket's update runs on the comm stream after its collective: never in the
         # backward (an emulated or single-rank collective still has to see the gradients)
@@ -266,6 +266,9 @@ class SegmentedDDPStep(TrainStep):
         self.ddp, self.splits, self.emulate = ddp, splits, int(emulate)
         self.split = splits[0] if len(splits) == 1 else splits
         self.emulate_gbps, self.emulate_scale = float(emulate_gbps), float(emulate_scale)
+        # emulate_passes > 1: the stand-in collectives stream their bucket that many times,
+        # paced over the modelled time (a live collective's memory traffic beside the backward)
+        self.emulate_passes = max(1, int(emulate_passes))
         if grad_comm not in ("fp32", "bf16"):
             raise ValueError("grad_comm must be 'fp32' or 'bf16'")
         self.grad_comm = grad_comm
@@ -380,7 +383,7 @@ class SegmentedDDPStep(TrainStep):
                 comm.comm.all_reduce(g.data_ptr() + 4 * lo, n, 0, AVG, cs)
         elif self.emulate_gbps > 0:  # timed 32-CU stand-in (comm_util.hip comm_standin)
             native().comm_standin(g.data_ptr() + 4 * lo, n, 32, 4.0 * n / (self.emulate_gbps * 1e3),
-                                  self.emulate_scale, cs)
+                                  self.emulate_scale, cs, self.emulate_passes)
         else:
             for _ in range(self.emulate):
                 native().scale(g.data_ptr() + 4 * lo, n, 1.0, cs)
@@ -437,8 +440,14 @@ class SegmentedDDPStep(TrainStep):
         def run(kind, nbytes, ptr, n):
             if self.emulate_gbps > 0:
                 us = 0.5 * nbytes / (self.emulate_gbps * 1e3)
-                native().comm_standin(ptr, n, 32, us, self.emulate_scale if n else 1.0,
-                                      cs.cuda_stream)
+                passes = self.emulate_passes
+                if n == 0 and passes > 1:
+                    # busy all-gather: stream the bucket's (already cleared) gradient slice, as
+                    # many bytes as the bf16 all-gather moves (never the operand image itself)
+                    (_, (lo, hi)) = self.buckets[self._standin_bucket]
+                    ptr, n = self.ddp.arena.grad.data_ptr() + 4 * lo, (hi - lo) // 2
+                native().comm_standin(ptr, n, 32, us, self.emulate_scale if kind != "all_gather" else 1.0,
+                                      cs.cuda_stream, max(1, passes // 2))
             else:
                 for _ in range(self.emulate):
                     if n:
@@ -449,6 +458,7 @@ class SegmentedDDPStep(TrainStep):
         from ..ops.common import native
         if self.shard16 is not None:
             if self.update[j] == "s16":
+                self._standin_bucket = j
                 with trace_range(f"shard16_update_bucket{j}"):
                     self.shard16.step(j, stream=cs, skip=self._fp(4),
                                       counter=self.loader.cursor_advance() if last else None,

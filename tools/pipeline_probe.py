@@ -43,7 +43,8 @@ def build(a, gbps, update):
     opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
     st = SegmentedDDPStep(model, opt, CrossEntropyLoss(), loader,
                           split=[int(v) for v in a.cuts.split(",")], emulate_gbps=gbps,
-                          emulate=0, update=update, emulate_world=a.world)
+                          emulate=0, update=update, emulate_world=a.world,
+                          emulate_passes=a.passes)
     st.warmup(2)
     st.capture()
     return st
@@ -96,6 +97,10 @@ def main():
     ap.add_argument("--update", default="shard16", choices=["allreduce", "shard16"])
     ap.add_argument("--gbps", type=float, default=171.0)
     ap.add_argument("--world", type=int, default=8, help="emulated world of the sharded update")
+    ap.add_argument("--passes", type=int, default=1,
+                    help="stand-in passes over the bucket paced over the modelled time (an "
+                         "all-reduce: 2 = a ring's read + write traffic; the sharded plan's two "
+                         "collectives get half each)")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--probe-steps", type=int, default=9)
     a = ap.parse_args()
@@ -134,7 +139,7 @@ def main():
             model_us.append(4 * ne / (a.gbps * 1e3))
     comm_us = [(y - x) * 1e3 for x, y in s["comm_ms"]]
     print(f"VGG-11 b{a.batch}, cuts {a.cuts}, update {a.update}, stand-in {a.gbps} GB/s "
-          f"(emulated world {a.world})\n")
+          f"(emulated world {a.world}, {a.passes} pass(es) over each bucket)\n")
     print("| run | wall ms/step | host enqueue ms/step |")
     print("|---|---|---|")
     for tag in ("standin", "nocomm"):
@@ -153,7 +158,8 @@ def main():
           f"comm-stream overhead beyond the modelled collective per bucket: "
           f"{', '.join(f'{v:.1f}' for v in over)} us")
     res.update(contention=round(contention, 4), comm_overhead_us=[round(v, 1) for v in over],
-               batch=a.batch, cuts=a.cuts, update=a.update, gbps=a.gbps, world=a.world)
+               batch=a.batch, cuts=a.cuts, update=a.update, gbps=a.gbps, world=a.world,
+               passes=a.passes)
     print(json.dumps(res))
 
 
