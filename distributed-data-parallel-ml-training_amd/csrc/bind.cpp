@@ -329,9 +329,11 @@ PYBIND11_MODULE(_native, m) {
   m.def("bn_act_fwd", [](int N, int H, int W, int C, int pool, int relu, float eps, uintptr_t z,
                          uintptr_t res, uintptr_t stats, uintptr_t gamma, uintptr_t beta,
                          uintptr_t out, uintptr_t st, uintptr_t running_mean,
-                         uintptr_t running_var, float momentum, int use_running, uintptr_t coef) {
+                         uintptr_t running_var, float momentum, int use_running, uintptr_t coef,
+                         uintptr_t mask) {
     ddp_amd::BnArgs a{};
     a.coef = P<float>(coef);
+    a.mask = P<unsigned char>(mask);
     a.N = N; a.H = H; a.W = W; a.C = C; a.pool = pool; a.relu = relu; a.eps = eps;
     a.z = P<unsigned short>(z); a.res = P<unsigned short>(res); a.stats = P<float>(stats);
     a.gamma = P<float>(gamma); a.beta = P<float>(beta); a.out = P<unsigned short>(out);
@@ -342,7 +344,7 @@ PYBIND11_MODULE(_native, m) {
      py::arg("eps"), py::arg("z"), py::arg("res"), py::arg("stats"), py::arg("gamma"),
      py::arg("beta"), py::arg("out"), py::arg("stream"), py::arg("running_mean") = 0,
      py::arg("running_var") = 0, py::arg("momentum") = 0.1f, py::arg("use_running") = 0,
-     py::arg("coef") = 0);
+     py::arg("coef") = 0, py::arg("mask") = 0);
   m.def("maxpool_fwd", [](uintptr_t x, int N, int H, int W, int C, int KH, int KW, int stride,
                           int pad, int Ho, int Wo, uintptr_t y, uintptr_t idx, uintptr_t st) {
     check(ddp_maxpool_fwd(P<void>(x), N, H, W, C, KH, KW, stride, pad, Ho, Wo, P<void>(y),
@@ -366,10 +368,11 @@ PYBIND11_MODULE(_native, m) {
                          uintptr_t res, uintptr_t stats, uintptr_t gamma, uintptr_t beta,
                          uintptr_t dout, uintptr_t sums, uintptr_t dz, uintptr_t dres,
                          uintptr_t dgamma, uintptr_t dbeta, uintptr_t dbias, uintptr_t st,
-                         uintptr_t coef, int sums_ready) {
+                         uintptr_t coef, int sums_ready, uintptr_t mask) {
     ddp_amd::BnArgs a{};
     a.coef = P<float>(coef);
     a.sums_ready = sums_ready;
+    a.mask = P<unsigned char>(mask);
     a.N = N; a.H = H; a.W = W; a.C = C; a.pool = pool; a.relu = relu; a.eps = eps;
     a.z = P<unsigned short>(z); a.res = P<unsigned short>(res); a.stats = P<float>(stats);
     a.gamma = P<float>(gamma); a.beta = P<float>(beta); a.dout = P<unsigned short>(dout);
@@ -380,7 +383,7 @@ PYBIND11_MODULE(_native, m) {
      py::arg("eps"), py::arg("z"), py::arg("res"), py::arg("stats"), py::arg("gamma"),
      py::arg("beta"), py::arg("dout"), py::arg("sums"), py::arg("dz"), py::arg("dres"),
      py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("stream"), py::arg("coef"),
-     py::arg("sums_ready") = 0);
+     py::arg("sums_ready") = 0, py::arg("mask") = 0);
   // ResNet stem: BN + ReLU + MaxPool2d(3, 2, 1) in one pass each way (bn_act.hip bn_pool3_*):
   // (N, H, W) = conv output, out / dout pooled, idx = uint8 window argmax (pooled shape)
   m.def("bn_pool3_fwd", [](int N, int H, int W, int C, int relu, float eps, uintptr_t z,

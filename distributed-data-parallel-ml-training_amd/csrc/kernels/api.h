@@ -57,6 +57,10 @@ struct BnArgs {
                                 // backward reads the table its forward wrote
   int sums_ready;               // backward: sums already accumulated (BnBwdFuse in the next
                                 // layer's dgrad) -> finalize + apply only
+  unsigned char* mask;          // residual blocks (res, ReLU, no pool): [N*H*W][C/8] bytes, bit e
+                                // of a channel group = its pre-ReLU value was > 0. Forward writes
+                                // it; the backward reads it INSTEAD of the residual (1/16 of the
+                                // bytes) — the residual only ever served the ReLU mask there
 };
 
 // BatchNorm-backward statistics fused into a conv dgrad: the dgrad output IS the gradient at the

@@ -187,12 +187,14 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnArgs a) {
     float best[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) best[e] = -INFINITY;
+    unsigned mb = 0;
 #pragma unroll
     for (int d = 0; d < NP; ++d) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         float y = bf2f(zv[it][d][e]) * sc[it][e] + sh[it][e];
         if (!POOL && a.res) y += bf2f(rv[it][POOL ? 0 : d][e]);
+        if (!POOL) mb |= (y > 0.f ? 1u : 0u) << e;  // the backward's ReLU rule (NaN -> 0)
         if (a.relu) y = fmaxf(y, 0.f);
         if (!POOL || y > best[e] || y != y) best[e] = y;
       }
@@ -201,6 +203,7 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnArgs a) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = f2bf(best[e]);
     st8(a.out + pix * a.C + cg * 8, o);
+    if (!POOL && a.mask) a.mask[t] = (unsigned char)mb;  // t = pixel * G + cg
   }
 }
 
@@ -213,6 +216,7 @@ struct BwdItems {
   u16x8 dv[IPT];
   u16x8 zv[IPT][NP];
   u16x8 rv[IPT][POOL ? 1 : NP];  // residual: only without pooling (host rejects pool + res)
+  unsigned mb[IPT];              // ReLU mask byte (BnArgs::mask) in place of the residual
   size_t off[IPT][NP];
   bool ok[IPT];
 };
@@ -226,6 +230,7 @@ __device__ __forceinline__ void bwd_load(const BnArgs& a, BwdItems<POOL, IPT>& L
     const size_t p = p0 + it * pstride;
     L.ok[it] = p < npix;
     const size_t pp = L.ok[it] ? p : 0;
+    L.mb[it] = 0;
     const int wo = (int)(pp % Wo);
     const int ho = (int)((pp / Wo) % Ho);
     const int n = (int)(pp / ((size_t)Wo * Ho));
@@ -236,7 +241,8 @@ __device__ __forceinline__ void bwd_load(const BnArgs& a, BwdItems<POOL, IPT>& L
       const size_t off = (((size_t)n * a.H + h) * a.W + w) * a.C + cg * 8;
       L.off[it][d] = off;
       L.zv[it][d] = ld8(a.z + off);
-      if (!POOL && a.res) L.rv[it][POOL ? 0 : d] = ld8(a.res + off);
+      if (!POOL && a.mask) L.mb[it] = a.mask[off / 8];
+      else if (!POOL && a.res) L.rv[it][POOL ? 0 : d] = ld8(a.res + off);
     }
   }
 }
@@ -244,9 +250,9 @@ __device__ __forceinline__ void bwd_load(const BnArgs& a, BwdItems<POOL, IPT>& L
 // dy_bn (gradient at the BN output, after ReLU mask and pool routing) and xhat for one item
 template <bool POOL>
 __device__ __forceinline__ void bwd_compute(const BnArgs& a, const u16x8& dv, const u16x8* zv,
-                                            const u16x8* rv, const float* sc, const float* sh,
-                                            const float* mu, const float* is, float (*xh)[8],
-                                            float (*dyb)[8]) {
+                                            const u16x8* rv, unsigned mb, const float* sc,
+                                            const float* sh, const float* mu, const float* is,
+                                            float (*xh)[8], float (*dyb)[8]) {
   constexpr int NP = POOL ? 4 : 1;
   float best[8], yv[NP][8];
   int arg[8];
@@ -258,7 +264,7 @@ __device__ __forceinline__ void bwd_compute(const BnArgs& a, const u16x8& dv, co
     for (int e = 0; e < 8; ++e) {
       const float zf = bf2f(zv[d][e]);
       float y = zf * sc[e] + sh[e];
-      if (!POOL && a.res) y += bf2f(rv[POOL ? 0 : d][e]);
+      if (!POOL && a.res && !a.mask) y += bf2f(rv[POOL ? 0 : d][e]);
       xh[d][e] = (zf - mu[e]) * is[e];
       yv[d][e] = y;
       if (POOL) {
@@ -272,7 +278,9 @@ __device__ __forceinline__ void bwd_compute(const BnArgs& a, const u16x8& dv, co
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const float g = (!POOL || arg[e] == d) ? bf2f(dv[e]) : 0.f;
-      dyb[d][e] = (a.relu && !(yv[d][e] > 0.f)) ? 0.f : g;
+      // with the forward's mask byte: the same verdict (bit e = y > 0), residual never read
+      const bool pos = (!POOL && a.mask) ? ((mb >> e) & 1u) != 0 : yv[d][e] > 0.f;
+      dyb[d][e] = (a.relu && !pos) ? 0.f : g;
     }
 }
 
@@ -307,7 +315,7 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
   for (int it = 0; it < IPT; ++it) {
     if (!L.ok[it]) continue;
     float xh[NP][8], dyb[NP][8];
-    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], sc, sh, mu, is, xh, dyb);
+    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], L.mb[it], sc, sh, mu, is, xh, dyb);
 #pragma unroll
     for (int d = 0; d < NP; ++d) {
 #pragma unroll
@@ -361,7 +369,7 @@ __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(BnArgs a) {
   for (int it = 0; it < IPT; ++it) {
     if (!L.ok[it]) continue;
     float xh[NP][8], dyb[NP][8];
-    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], sc, sh, mu, is, xh, dyb);
+    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], L.mb[it], sc, sh, mu, is, xh, dyb);
 #pragma unroll
     for (int d = 0; d < NP; ++d) {
       u16x8 o, r;
@@ -407,7 +415,7 @@ __global__ __launch_bounds__(NT) void bn_act_bwd_local_kernel(BnArgs a) {
   for (int it = 0; it < IPT; ++it) {
     if (!L.ok[it]) continue;
     float xh[NP][8], dyb[NP][8];
-    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], sc, sh, mu, is, xh, dyb);
+    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], L.mb[it], sc, sh, mu, is, xh, dyb);
 #pragma unroll
     for (int d = 0; d < NP; ++d)
 #pragma unroll
@@ -447,7 +455,7 @@ __global__ __launch_bounds__(NT) void bn_act_bwd_local_kernel(BnArgs a) {
   for (int it = 0; it < IPT; ++it) {
     if (!L.ok[it]) continue;
     float xh[NP][8], dyb[NP][8];
-    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], sc, sh, mu, is, xh, dyb);
+    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], L.mb[it], sc, sh, mu, is, xh, dyb);
 #pragma unroll
     for (int d = 0; d < NP; ++d) {
       u16x8 o, r;
@@ -679,7 +687,7 @@ static void launch_fwd(const BnArgs& a, size_t items, hipStream_t st) {
 extern "C" int ddp_bn_act_fwd(const BnArgs* args, hipStream_t st) {
   BnArgs a = *args;
   if (a.C % 8 || a.coef == nullptr) return -1;
-  if (a.pool && a.res) return -1;  // residual add is only fused without pooling
+  if (a.pool && (a.res || a.mask)) return -1;  // residual add / mask only without pooling
   const int Ho = a.pool ? a.H / 2 : a.H, Wo = a.pool ? a.W / 2 : a.W;
   const size_t items = (size_t)a.N * Ho * Wo * (a.C / 8);
   // 1 item per thread for small layers; 2 (pooled) / 4 (plain) when there are enough to keep
@@ -805,7 +813,7 @@ static int launch_reduce_chain(const BnArgs& a, hipStream_t st) {
 extern "C" int ddp_bn_act_bwd(const BnArgs* args, hipStream_t st) {
   BnArgs a = *args;
   if (a.C % 8 || a.coef == nullptr || a.sums == nullptr) return -1;
-  if (a.pool && a.res) return -1;
+  if (a.pool && (a.res || a.mask)) return -1;
   int ipt;
   if (local_cfg(a, &ipt)) {
     // small layer: the whole backward in one launch (any sums the next layer's dgrad

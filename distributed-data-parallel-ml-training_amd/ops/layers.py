@@ -232,6 +232,10 @@ HEAD_BN_FUSE = os.environ.get("DDP_AMD_HEAD_BN_FUSE", "1") != "0"
 # ... and its BN + ReLU + 2x2 pool FORWARD folded into the head's forward kernel (linear_ce.hip
 # HeadBnIn: one launch fewer; the training loss path only, VGG's 2x2 last block)
 HEAD_BN_FWD = os.environ.get("DDP_AMD_HEAD_BN_FWD", "1") != "0"
+# residual blocks (BN + residual + ReLU, no pool; ResNet's bn3): the forward stores the ReLU
+# mask as one bit per element and the backward reads it instead of the residual tensor, which it
+# only ever needed for that mask (bn_act.hip BnArgs::mask; 1/16 of the bytes, twice per layer)
+BN_RELU_MASK = os.environ.get("DDP_AMD_BN_RELU_MASK", "1") != "0"
 # largest dgrad output H*W that takes the fused sums: 16 (4x4 / 2x2) from 128 images per GPU up,
 # 256 (also 16x16 / 8x8) at the strong-scaling shares of at most 64 images (b64 0.4556 vs 0.4594
 # ms, b32 0.3921 vs 0.3952; b128 / b256 unchanged, profiles/r4z3_bn_sums_threshold.md); the
@@ -423,11 +427,16 @@ class _ConvBNActFn(torch.autograd.Function):
         elif spec.last_deferred:
             spec.deferred = y  # computed by the next block's conv or the head (see to_head)
         elif not fused:
+            mask = None
+            if (BN_RELU_MASK and residual is not None and spec.relu and not spec.pool
+                    and any(ctx.needs_input_grad) and spec.K % 8 == 0):
+                mask = torch.empty(N, P, Q, spec.K // 8, dtype=torch.uint8, device=x.device)
+            ctx.relu_mask = mask
             native().bn_act_fwd(N, P, Q, spec.K, int(spec.pool), int(spec.relu), spec.eps, ptr(z),
                                 ptr(residual), ptr(stats), ptr(gamma), ptr(beta), ptr(y),
                                 stream_handle(), ptr(rm), ptr(rv),
                                 float(bn.momentum if bn.momentum is not None else 0.1),
-                                use_running, ptr(spec.coef))
+                                use_running, ptr(spec.coef), mask=ptr(mask))
         ctx.spec = spec
         ctx.has_res = residual is not None
         ctx.in_link, ctx.res_link = in_link, res_link
@@ -485,10 +494,13 @@ class _ConvBNActFn(torch.autograd.Function):
         else:
             dy = dy.contiguous()
             dz = torch.empty_like(z)
+            mask = getattr(ctx, "relu_mask", None)
+            ctx.relu_mask = None
             native().bn_act_bwd(N, P, Q, K, int(spec.pool), int(spec.relu), spec.eps, ptr(z),
-                                ptr(residual), ptr(stats), ptr(gamma), ptr(beta), ptr(dy),
-                                ptr(sums), ptr(dz), ptr(dres), ptr(gg), ptr(gbt), ptr(gb),
-                                stream_handle(), ptr(spec.coef), sums_ready=int(sums_ready))
+                                0 if mask is not None else ptr(residual), ptr(stats), ptr(gamma),
+                                ptr(beta), ptr(dy), ptr(sums), ptr(dz), ptr(dres), ptr(gg),
+                                ptr(gbt), ptr(gb), stream_handle(), ptr(spec.coef),
+                                sums_ready=int(sums_ready), mask=ptr(mask))
         grad_ready([gamma, beta, bias])
         if ctx.res_link is not None and dres is not None:
             dres = ctx.res_link.offer(dres)

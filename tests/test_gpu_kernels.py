@@ -176,17 +176,21 @@ def _bn_ref(z, gamma, beta, eps, relu, pool, res=None):
                                             (8, 2048, 2, False, True), (16, 128, 16, True, False),
                                             (32, 256, 8, False, False), (16, 256, 8, False, True),
                                             (32, 64, 8, True, False)])
-@pytest.mark.parametrize("mode", ["split", "local"])
+@pytest.mark.parametrize("mode", ["split", "local", "mask", "mask-local"])
 def test_bn_act_fwd_bwd(native_ext, N, C, H, pool, res, mode):
     """split: reduce -> finalize -> apply launches; local: one block per 8 channels does the
     whole backward in one launch (bn_act_bwd_local_kernel; the shapes cover 1-8 items per
-    thread, pooled, plain and residual)."""
+    thread, pooled, plain and residual). mask: residual blocks whose forward stores the ReLU
+    mask bits (BnArgs::mask) and whose backward reads them instead of the residual — must be
+    BITWISE equal to the residual-reading backward."""
     from ddp_amd.ops.common import ptr, stream_handle
     nat = native_ext
-    nat.bn_bwd_local_set(64 if mode == "local" else 0)  # local: any shape it can hold
+    if mode.startswith("mask") and not res:
+        pytest.skip("the ReLU mask serves residual blocks only")
+    nat.bn_bwd_local_set(64 if mode.endswith("local") else 0)  # local: any shape it can hold
     try:
         _bn_case(nat, N, C, H, pool, res, mode, ptr, stream_handle)
-        if mode == "local":
+        if mode.endswith("local"):
             assert nat.bn_bwd_local_ok(N, H, H, C, int(pool))
     finally:
         nat.bn_bwd_local_set(8)  # the shipped limit (bn_act.hip kLocalMaxLoads)
@@ -206,8 +210,10 @@ def _bn_case(nat, N, C, H, pool, res, mode, ptr, stream_handle):
     out = torch.empty(N, Ho, Ho, C, device=DEV, dtype=torch.bfloat16)
     s = stream_handle()
     coef = torch.empty(6 * C, device=DEV)
+    use_mask = mode.startswith("mask")
+    mask = torch.full((N, H, H, C // 8), 0xA5, dtype=torch.uint8, device=DEV) if use_mask else None
     nat.bn_act_fwd(N, H, H, C, int(pool), 1, 1e-5, ptr(zn), ptr(rn), ptr(stats), ptr(gamma),
-                   ptr(beta), ptr(out), s, coef=ptr(coef))
+                   ptr(beta), ptr(out), s, coef=ptr(coef), mask=ptr(mask))
     zr = z.clone().requires_grad_(True)
     gr = gamma.clone().requires_grad_(True)
     br = beta.clone().requires_grad_(True)
@@ -227,6 +233,27 @@ def _bn_case(nat, N, C, H, pool, res, mode, ptr, stream_handle):
                    ptr(beta), ptr(doutn), ptr(sums), ptr(dz), ptr(dres), ptr(dg), ptr(db),
                    ptr(dbias), s, ptr(coef))
     torch.cuda.synchronize()
+    if use_mask:
+        # the mask bits are exactly the pre-ReLU sign test of the forward
+        y_pre = (zn.float() * coef[:C] + coef[C:2 * C] + rn.float())
+        bits = (y_pre > 0).reshape(N, H, H, C // 8, 8).to(torch.int32)
+        want = (bits << torch.arange(8, device=DEV, dtype=torch.int32)).sum(-1)
+        assert torch.equal(mask.to(torch.int32), want)
+        # the mask-reading backward (residual pointer null) is bitwise the residual-reading one
+        sums_m = torch.zeros_like(sums)
+        dz_m, dres_m = torch.empty_like(zn), torch.empty_like(zn)
+        dg_m, db_m = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        nat.bn_act_bwd(N, H, H, C, int(pool), 1, 1e-5, ptr(zn), 0, ptr(stats), ptr(gamma),
+                       ptr(beta), ptr(doutn), ptr(sums_m), ptr(dz_m), ptr(dres_m), ptr(dg_m),
+                       ptr(db_m), 0, s, ptr(coef), mask=ptr(mask))
+        torch.cuda.synchronize()
+        assert torch.equal(dres_m, dres)
+        if mode.endswith("local"):  # in-block sums: no atomics, the whole backward is bitwise
+            assert torch.equal(dz_m, dz)
+        else:  # replica sums through float atomics: equal up to their summation order
+            assert rel_err(dz_m.float(), dz.float()) < 1e-3
+        assert torch.allclose(dg_m, dg, rtol=1e-5, atol=1e-5)
+        assert torch.allclose(db_m, db, rtol=1e-5, atol=1e-5)
     assert rel_err(dz.permute(0, 3, 1, 2), zr.grad) < 2e-2
     assert rel_err(dg, gr.grad) < 1e-2
     assert rel_err(db, br.grad) < 1e-2
