@@ -245,8 +245,14 @@ PYBIND11_MODULE(_native, m) {
   // when possible (api.h BnBwdApply); returns True when it did (dx is then NOT written)
   m.def("conv_dgrad", [](py::tuple g, uintptr_t dy, uintptr_t wt, uintptr_t dx, uintptr_t ws,
                          size_t ws_elems, int splits, uintptr_t st, int accumulate, py::object bn,
-                         py::object bna) {
+                         py::object bna, uintptr_t acc_dy, uintptr_t acc_mask) {
     auto c = geom(g);
+    if (acc_mask) {  // accumulate onto a deferred first branch (acc_dy through the ReLU bits)
+      check(ddp_conv_dgrad_acc(&c, P<void>(dy), P<void>(wt), P<void>(dx), P<float>(ws), ws_elems,
+                               splits, P<void>(acc_dy), P<unsigned char>(acc_mask), S(st)),
+            "conv_dgrad_acc");
+      return false;
+    }
     if (bn.is_none()) {
       check(ddp_conv_dgrad(&c, P<void>(dy), P<void>(wt), P<void>(dx), P<float>(ws), ws_elems,
                            splits, accumulate, S(st)), "conv_dgrad");
@@ -262,7 +268,8 @@ PYBIND11_MODULE(_native, m) {
     return done == 1;
   }, py::arg("g"), py::arg("dy"), py::arg("wt"), py::arg("dx"), py::arg("ws"),
      py::arg("ws_elems"), py::arg("splits"), py::arg("stream"), py::arg("accumulate") = 0,
-     py::arg("bn") = py::none(), py::arg("bna") = py::none());
+     py::arg("bn") = py::none(), py::arg("bna") = py::none(), py::arg("acc_dy") = 0,
+     py::arg("acc_mask") = 0);
   // one layer's backward: WGRAD (dw += ...) and stride-1 DGRAD (dx = ..., optional BN-backward
   // sums) as one grouped launch when the policy allows (ddp_conv_bwd_pair), else two
   m.def("conv_bwd_pair", [](py::tuple g, uintptr_t dy, uintptr_t wc, uintptr_t dx, uintptr_t x,

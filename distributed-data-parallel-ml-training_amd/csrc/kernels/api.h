@@ -223,6 +223,11 @@ int ddp_linear_head_bwd_bn(const float* dl, const float* W, const void* x, int B
 void ddp_conv_bn_fuse_rows(int rows);
 int ddp_conv_dgrad(const ddp_amd::ConvGeom* g, const void* dy, const void* wt, void* dx,
                    float* ws, size_t ws_elems, int splits, int accumulate, hipStream_t st);
+// dx = result + (first gradient branch never stored: acc_dy through the ReLU mask bits acc_mask,
+// bn_act.hip BnArgs::mask); stride 1 only; dx is written, not read
+int ddp_conv_dgrad_acc(const ddp_amd::ConvGeom* g, const void* dy, const void* wt, void* dx,
+                       float* ws, size_t ws_elems, int splits, const void* acc_dy,
+                       const unsigned char* acc_mask, hipStream_t st);
 // ba (optional): also run the preceding block's whole BN backward in the finish when the dgrad
 // is split-K and small (*bn_done = 1: dz / dgamma / dbeta written, dx NOT written)
 int ddp_conv_dgrad_bn(const ddp_amd::ConvGeom* g, const void* dy, const void* wt, void* dx,

@@ -118,7 +118,34 @@ struct ConvArgs {
   int d2x2;                  // 1: g is the dense 1x1 view (N, 1, 1, 4C -> 4K), B = Wc [K][9][C]
   int d2C, d2K;              // the 3x3 conv's C and K
   int no_finish;             // host: launch the GEMM only (the caller runs the finish)
+  // accumulate with a DEFERRED first branch (ResNet identity blocks): the branch's gradient
+  // was never stored; it is acc_dy (the block output's gradient) through acc_mask (the
+  // residual BatchNorm's ReLU bits, bn_act.hip BnArgs::mask; bit e of byte i = channel 8i + e
+  // of the flat [rows][Ng] tensor) — dx = bf16(result + (bit ? acc_dy : 0)), dx never read
+  const unsigned short* acc_dy;
+  const unsigned char* acc_mask;
 };
+
+// the accumulating DGRAD's first-branch value of 4 / 8 consecutive channels starting at flat
+// element e (stored dx, or the deferred masked gradient): bf16 values as stored
+__device__ __forceinline__ uint2 acc_old4(const unsigned short* dx, const unsigned short* acc_dy,
+                                          const unsigned char* acc_mask, size_t e) {
+  if (!acc_mask) return *reinterpret_cast<const uint2*>(dx + e);
+  uint2 v = *reinterpret_cast<const uint2*>(acc_dy + e);
+  const unsigned mb = (unsigned)acc_mask[e >> 3] >> (e & 4);
+  v.x &= ((mb & 1u) ? 0xFFFFu : 0u) | ((mb & 2u) ? 0xFFFF0000u : 0u);
+  v.y &= ((mb & 4u) ? 0xFFFFu : 0u) | ((mb & 8u) ? 0xFFFF0000u : 0u);
+  return v;
+}
+__device__ __forceinline__ u16x8 acc_old8(const unsigned short* dx, const unsigned short* acc_dy,
+                                          const unsigned char* acc_mask, size_t e) {
+  if (!acc_mask) return ld8(dx + e);
+  u16x8 v = ld8(acc_dy + e);
+  const unsigned mb = acc_mask[e >> 3];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = ((mb >> i) & 1u) ? v[i] : (unsigned short)0;
+  return v;
+}
 
 // ------------------------------------------------------------------ operand gathers
 // Index math is hoisted: the pixel decomposition of a GEMM row is computed once per kernel
@@ -636,7 +663,7 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
         unsigned short* dst = args.out + orow * args.Ng + col;
         u16x8 o;
         if (MODE == MODE_DGRAD && args.accumulate) {  // dx += (second gradient branch)
-          const u16x8 old = ld8(dst);
+          const u16x8 old = acc_old8(args.out, args.acc_dy, args.acc_mask, orow * args.Ng + col);
 #pragma unroll
           for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e] + bf2f(old[e]));
         } else {
@@ -860,7 +887,7 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
         }
         if (MODE == MODE_DGRAD && args.accumulate) {  // dx += (second gradient branch)
           uint2* dst = reinterpret_cast<uint2*>(args.out + orow * args.Ng + col);
-          const uint2 old = *dst;
+          const uint2 old = acc_old4(args.out, args.acc_dy, args.acc_mask, orow * args.Ng + col);
           pk.x = (unsigned)f2bf(v[0] + bf2f((unsigned short)(old.x & 0xffff))) |
                  ((unsigned)f2bf(v[1] + bf2f((unsigned short)(old.x >> 16))) << 16);
           pk.y = (unsigned)f2bf(v[2] + bf2f((unsigned short)(old.y & 0xffff))) |
@@ -1075,6 +1102,8 @@ struct FinishArgs {  // split-K finish of a FWD / DGRAD GEMM (one launch or one 
   int accumulate;
   BnBwdFuse bnf;
   int H, W;
+  const unsigned short* acc_dy;  // ConvArgs::acc_dy / acc_mask (deferred first branch)
+  const unsigned char* acc_mask;
 };
 
 // body of splitk_finish_kernel: (bx, by) / gx stand for blockIdx.(x, y) / gridDim.x;
@@ -1124,7 +1153,7 @@ __device__ __forceinline__ void splitk_finish_body(const FinishArgs& fa, float* 
     sum_slabs8(ws + (size_t)row * Ng + cg * 8, slab, 0, splits, v);
     unsigned short* dst = out + map_row(rmap, row) * Ng + cg * 8;
     if (accumulate) {
-      const u16x8 old = ld8(dst);
+      const u16x8 old = acc_old8(out, fa.acc_dy, fa.acc_mask, map_row(rmap, row) * Ng + cg * 8);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += bf2f(old[e]);
     }
@@ -1893,7 +1922,7 @@ static FinishArgs finish_args(int mode, const ConvArgs& a) {
   if (a.phase) rm = RowMap{a.g.stride, a.Hp, a.Wp, a.g.H, a.g.W, a.pa, a.pb};
   const bool fwd = mode == MODE_FWD;
   return FinishArgs{a.ws, a.splits, a.out, fwd ? a.bias : nullptr, fwd ? a.stats : nullptr,
-                    a.Mg, a.Ng, rm, a.accumulate, a.bnf, a.g.H, a.g.W};
+                    a.Mg, a.Ng, rm, a.accumulate, a.bnf, a.g.H, a.g.W, a.acc_dy, a.acc_mask};
 }
 
 // ---- SGD in the backward (world 1, engine/step.py TrainStep): registered weights whose WGRAD
@@ -2388,10 +2417,13 @@ extern "C" int ddp_conv_fwd_finish(const ConvGeom* g, float* ws, int splits, con
 static int conv_dgrad_impl(const ConvGeom* g, const void* dy, const void* wc, void* dx,
                            float* ws, size_t ws_elems, int splits, int accumulate,
                            const BnBwdFuse* bn, const BnBwdApply* ba, int* bn_done,
-                           hipStream_t st) {
+                           hipStream_t st, const void* acc_dy = nullptr,
+                           const unsigned char* acc_mask = nullptr) {
   if (bn_done) *bn_done = 0;
   if (g->C % 8 || g->K % 8) return -1;
   if (bn && (accumulate || g->stride != 1)) return -3;  // fused BN sums: plain stride-1 dgrad only
+  // deferred first branch: every dx element must be written by this call (stride 1)
+  if (acc_mask && (!accumulate || !acc_dy || g->stride != 1)) return -3;
   if (!accumulate && ddp_conv_dense2x2_ok(g) && ws != nullptr) {
     // dense 2x2 GEMM; the preceding block's BatchNorm-backward sums (bn) and the split-K
     // reduction run in the standard finish of the 3x3 view
@@ -2421,6 +2453,8 @@ static int conv_dgrad_impl(const ConvGeom* g, const void* dy, const void* wc, vo
   }
   ConvArgs a{};
   a.accumulate = accumulate;
+  a.acc_dy = (const unsigned short*)acc_dy;
+  a.acc_mask = acc_mask;
   if (bn) {
     a.has_bnf = 1;
     a.bnf = *bn;
@@ -2492,6 +2526,13 @@ extern "C" int ddp_conv_dgrad(const ConvGeom* g, const void* dy, const void* wc,
                               hipStream_t st) {
   return conv_dgrad_impl(g, dy, wc, dx, ws, ws_elems, splits, accumulate, nullptr, nullptr,
                          nullptr, st);
+}
+
+extern "C" int ddp_conv_dgrad_acc(const ConvGeom* g, const void* dy, const void* wc, void* dx,
+                                  float* ws, size_t ws_elems, int splits, const void* acc_dy,
+                                  const unsigned char* acc_mask, hipStream_t st) {
+  return conv_dgrad_impl(g, dy, wc, dx, ws, ws_elems, splits, 1, nullptr, nullptr, nullptr, st,
+                         acc_dy, acc_mask);
 }
 
 extern "C" int ddp_conv_dgrad_bn(const ConvGeom* g, const void* dy, const void* wc, void* dx,

@@ -187,6 +187,16 @@ class GradLink:
         self.expected = consumers
         self.seen = 0
         self.buf = None
+        self.deferred = None  # (dy, relu_mask): a residual gradient that was never stored
+
+    def defer(self, dy, mask):
+        """The residual BatchNorm's gradient dres = dy through its ReLU mask, NOT stored: the
+        other consumer's accumulating dgrad computes it from (dy, mask) in its epilogue
+        (conv_igemm.hip ConvArgs::acc_dy / acc_mask) — one activation-sized write and read
+        fewer per identity block."""
+        self.seen += 1
+        self.deferred = (dy, mask)
+        return None
 
     def offer(self, t):
         """A consumer whose gradient is already a tensor (the BN residual gradient)."""
@@ -236,6 +246,9 @@ HEAD_BN_FWD = os.environ.get("DDP_AMD_HEAD_BN_FWD", "1") != "0"
 # mask as one bit per element and the backward reads it instead of the residual tensor, which it
 # only ever needed for that mask (bn_act.hip BnArgs::mask; 1/16 of the bytes, twice per layer)
 BN_RELU_MASK = os.environ.get("DDP_AMD_BN_RELU_MASK", "1") != "0"
+# ... and an identity block's residual gradient (dy through that mask) is not stored at all: the
+# branch's first 1x1 conv rebuilds it in its accumulating dgrad epilogue (GradLink.defer)
+RES_DEFER = os.environ.get("DDP_AMD_RES_DEFER", "1") != "0"
 # largest dgrad output H*W that takes the fused sums: 16 (4x4 / 2x2) from 128 images per GPU up,
 # 256 (also 16x16 / 8x8) at the strong-scaling shares of at most 64 images (b64 0.4556 vs 0.4594
 # ms, b32 0.3921 vs 0.3952; b128 / b256 unchanged, profiles/r4z3_bn_sums_threshold.md); the
@@ -261,6 +274,15 @@ def bn_bwd_fuse_pays(H, W, pool=True, N=None):
     if lim is None:
         lim = 256 if N is not None and N <= 64 else 16
     return H * W <= lim
+
+
+def _masked(dy, mask):
+    """dy through ReLU mask bits ([..., C/8] bytes, bit e = channel 8i + e): the stored form of a
+    deferred residual gradient (fallback of GradLink.defer)."""
+    bits = (mask.unsqueeze(-1).to(torch.int32) >> torch.arange(8, device=mask.device,
+                                                               dtype=torch.int32)) & 1
+    return torch.where(bits.reshape(dy.shape).bool(), dy, torch.zeros((), dtype=dy.dtype,
+                                                                      device=dy.device))
 
 
 def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=None, bna=None):
@@ -294,6 +316,20 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=Non
         return (None, False) if bna is not None else None
     if spec.C != spec.Cr:
         raise RuntimeError("dgrad requested for a channel-padded input layer")
+    if link is not None and link.deferred is not None and spec.stride == 1:
+        # second branch onto a deferred first branch: dx = dgrad + dy * mask (dx only written)
+        acc_dy, acc_mask = link.deferred
+        link.deferred = None
+        dx = torch.empty_like(x)
+        native().conv_dgrad(g, ptr(dz), ptr(spec.wc), ptr(dx), ptr(ws), ws.numel(), 0, s,
+                            accumulate=1, acc_dy=ptr(acc_dy), acc_mask=ptr(acc_mask))
+        link.seen += 1
+        link.buf = dx
+        return link.result()
+    if link is not None and link.deferred is not None:  # (not hit: identity blocks are stride 1)
+        acc_dy, acc_mask = link.deferred
+        link.deferred = None
+        link.buf = _masked(acc_dy, acc_mask)
     if link is not None and link.buf is not None:
         # second branch: accumulate into the first branch's gradient from the GEMM epilogue
         native().conv_dgrad(g, ptr(dz), ptr(spec.wc), ptr(link.buf), ptr(ws), ws.numel(), 0, s,
@@ -469,7 +505,15 @@ class _ConvBNActFn(torch.autograd.Function):
             return dx, None, None, None, None, None, None, None, None
         N, P, Q, K = z.shape
         sums = spec.sums  # zeroed together with the statistics at the start of the forward
-        dres = torch.empty_like(z) if (ctx.has_res and ctx.needs_input_grad[5]) else None
+        mask = getattr(ctx, "relu_mask", None)
+        ctx.relu_mask = None
+        # identity block: the residual gradient goes to the branch's first conv, whose
+        # accumulating dgrad can rebuild it from (dy, mask) — never store it (RES_DEFER)
+        defer = (RES_DEFER and mask is not None and ctx.res_link is not None
+                 and ctx.needs_input_grad[5] and ctx.res_link.seen == 0
+                 and ctx.res_link.buf is None)
+        dres = torch.empty_like(z) if (ctx.has_res and ctx.needs_input_grad[5]
+                                       and not defer) else None
         gw = ensure_grad(weight)
         gb = ensure_grad(bias) if bias is not None else None
         gg = ensure_grad(gamma)
@@ -494,15 +538,15 @@ class _ConvBNActFn(torch.autograd.Function):
         else:
             dy = dy.contiguous()
             dz = torch.empty_like(z)
-            mask = getattr(ctx, "relu_mask", None)
-            ctx.relu_mask = None
             native().bn_act_bwd(N, P, Q, K, int(spec.pool), int(spec.relu), spec.eps, ptr(z),
                                 0 if mask is not None else ptr(residual), ptr(stats), ptr(gamma),
                                 ptr(beta), ptr(dy), ptr(sums), ptr(dz), ptr(dres), ptr(gg),
                                 ptr(gbt), ptr(gb), stream_handle(), ptr(spec.coef),
                                 sums_ready=int(sums_ready), mask=ptr(mask))
         grad_ready([gamma, beta, bias])
-        if ctx.res_link is not None and dres is not None:
+        if defer:
+            dres = ctx.res_link.defer(dy, mask)
+        elif ctx.res_link is not None and dres is not None:
             dres = ctx.res_link.offer(dres)
         bnf = bna = None
         prev = spec.prev

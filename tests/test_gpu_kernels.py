@@ -534,6 +534,51 @@ def test_conv_splitk_finish_bn_fwd(native_ext, N, C, H, K, pool):
     assert rel_err(y.permute(0, 3, 1, 2), ref) < 1e-2
 
 
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("splits", [1, 3])
+@pytest.mark.parametrize("staged", [0, 1])
+@pytest.mark.parametrize("case", [(4, 64, 14, 14, 256, 1, 1, 0), (4, 256, 14, 14, 64, 1, 1, 0),
+                                  (2, 64, 12, 12, 64, 3, 1, 1)])
+def test_conv_dgrad_deferred_branch(native_ext, case, staged, splits, tile):
+    """Accumulating dgrad onto a DEFERRED first branch (ResNet identity blocks, GradLink.defer):
+    dx = dgrad + (bit ? acc_dy : 0) with the ReLU mask bits of the residual BatchNorm — every
+    epilogue (direct fragment stores, LDS-staged rows, split-K finish) must give exactly what
+    the classic accumulate gives on the stored masked gradient."""
+    from ddp_amd.ops.common import ptr, stream_handle, workspace
+    from ddp_amd.ops.layers import _masked
+    N, Cin, H, W, K, R, stride, pad = case
+    conv, spec, x, xn = _conv_setup(N, Cin, H, W, K, R, stride, pad)
+    ws = workspace(xn.device)
+    g = spec.geom(N, H, W)
+    P, Q = g[9], g[10]
+    dzn = bf(torch.randn(N, K, P, Q, device=DEV)).permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    acc_dy = bf(torch.randn(N, H, W, Cin, device=DEV)).to(torch.bfloat16)
+    mask = torch.randint(0, 256, (N, H, W, Cin // 8), dtype=torch.uint8, device=DEV)
+    stored = _masked(acc_dy, mask)
+    assert torch.equal(stored.float() != 0, ((mask.unsqueeze(-1).long() >> torch.arange(
+        8, device=DEV)) & 1).reshape(acc_dy.shape).bool() & (acc_dy.float() != 0))
+    native_ext.conv_force_tile(tile, 0)
+    native_ext.conv_epi_stage_set(staged)
+    try:
+        dxa = stored.clone()
+        native_ext.conv_dgrad(g, ptr(dzn), ptr(spec.wc), ptr(dxa), ptr(ws), ws.numel(), splits,
+                              stream_handle(), accumulate=1)
+        dxd = torch.full_like(xn, float("nan"))  # written, never read
+        native_ext.conv_dgrad(g, ptr(dzn), ptr(spec.wc), ptr(dxd), ptr(ws), ws.numel(), splits,
+                              stream_handle(), accumulate=1, acc_dy=ptr(acc_dy),
+                              acc_mask=ptr(mask))
+        torch.cuda.synchronize()
+    finally:
+        native_ext.conv_force_tile(0, 0)
+        native_ext.conv_epi_stage_set(1)
+    assert torch.equal(dxd, dxa)
+    xr = x.clone().requires_grad_(True)
+    F.conv2d(xr, conv.weight.detach(), None, stride, pad).backward(
+        dzn.float().permute(0, 3, 1, 2))
+    ref = xr.grad.permute(0, 2, 3, 1) + stored.float()
+    assert rel_err(dxd, ref) < 1e-2
+
+
 @pytest.mark.parametrize("tile", [1, 2, 3, 5])  # the tiles the tuned table uses (not 64x64)
 @pytest.mark.parametrize("case", [(4, 64, 28, 28, 256, 1, 1, 0), (4, 256, 28, 28, 64, 1, 1, 0),
                                   (3, 64, 21, 21, 128, 1, 2, 0), (2, 64, 14, 14, 128, 3, 1, 1)])
