@@ -300,9 +300,6 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
   const int cgl = threadIdx.x % Gb;
   const int prow = threadIdx.x / Gb, prows = 256 / Gb;
   const int c0 = (cg_base + cgl) * 8;
-  BwdItems<POOL, IPT> L;
-  bwd_load<POOL, IPT>(a, L, (size_t)blockIdx.x * prows * IPT + prow, prows, npix, cg_base + cgl,
-                      Ho, Wo);
   float sc[8], sh[8], mu[8], is[8];
   ld8f(a.coef + kSc * a.C + c0, sc);
   ld8f(a.coef + kSh * a.C + c0, sh);
@@ -311,17 +308,25 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
   float acc[2][8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { acc[0][e] = 0.f; acc[1][e] = 0.f; }
+  // grid-stride over the item blocks (nbx of them): a capped grid adds its partial sums once
+  // per block instead of once per 256 x IPT items (launch_bwd's reduce grid)
+  const size_t per_blk = (size_t)prows * IPT;
+  const size_t nbx = (npix + per_blk - 1) / per_blk;
+  for (size_t bb = blockIdx.x; bb < nbx; bb += gridDim.x) {
+    BwdItems<POOL, IPT> L;
+    bwd_load<POOL, IPT>(a, L, bb * per_blk + prow, prows, npix, cg_base + cgl, Ho, Wo);
 #pragma unroll
-  for (int it = 0; it < IPT; ++it) {
-    if (!L.ok[it]) continue;
-    float xh[NP][8], dyb[NP][8];
-    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], L.mb[it], sc, sh, mu, is, xh, dyb);
+    for (int it = 0; it < IPT; ++it) {
+      if (!L.ok[it]) continue;
+      float xh[NP][8], dyb[NP][8];
+      bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], L.mb[it], sc, sh, mu, is, xh, dyb);
 #pragma unroll
-    for (int d = 0; d < NP; ++d) {
+      for (int d = 0; d < NP; ++d) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        acc[0][e] += dyb[d][e];
-        acc[1][e] += dyb[d][e] * xh[d][e];
+        for (int e = 0; e < 8; ++e) {
+          acc[0][e] += dyb[d][e];
+          acc[1][e] += dyb[d][e] * xh[d][e];
+        }
       }
     }
   }
@@ -705,11 +710,25 @@ extern "C" int ddp_bn_act_fwd(const BnArgs* args, hipStream_t st) {
 // Target reduce-grid size (DDP_AMD_BN_BWD_BLOCKS overrides).
 static size_t kBwdBlocks = 1024;
 
+// Reduce-grid cap (DDP_AMD_BN_REDUCE_GRID, 0 = uncapped): the reduce walks its item blocks
+// with a grid stride, so every block adds ONE partial sum per channel. Uncapped, ResNet-50's
+// 56x56x256 layers ran 25088 blocks = 51 MB of memory-side float atomics per layer (~40 us at
+// the ~1.3 TB/s atomic rate, MI355X_MICROARCH.md "Global float atomics").
+static unsigned kReduceGrid = 2048;
+
 template <bool POOL, int IPT>
 static void launch_bwd(const BnArgs& a, size_t npix, int Gb, int chunks, hipStream_t st) {
+  static const bool init = [] {
+    if (const char* e = std::getenv("DDP_AMD_BN_REDUCE_GRID")) kReduceGrid = (unsigned)std::max(0, std::atoi(e));
+    return true;
+  }();
+  (void)init;
   const unsigned bx = blocks_for(npix, (size_t)(256 / Gb) * IPT);
+  // (the deterministic build keeps one replica per block: block ids stay below kStatRep)
+  unsigned rx = kReduceGrid ? std::min(bx, std::max(1u, kReduceGrid / (unsigned)chunks)) : bx;
+  if (kDeterministic) rx = std::min(rx, std::max(1u, (unsigned)kStatRep / (unsigned)chunks));
   if (!a.sums_ready)  // (else: accumulated by the next layer's dgrad epilogue, BnBwdFuse)
-    hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<POOL, IPT>), dim3(bx, chunks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<POOL, IPT>), dim3(rx, chunks), dim3(256), 0, st, a);
   // The finalize stays its own launch: folding it into the apply (every block re-reducing the 16
   // replicas the reduce just wrote with memory-side atomics) measured 3-4x slower applies at
   // batch 256 and +50 us per b32 step; the reduce's last-arriving block doing it measured slower
