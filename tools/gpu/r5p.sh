@@ -1,9 +1,9 @@
 #!/bin/bash
-# round 5: ResNet-50 b256 with the r5o table entries (stem WGRAD split-K 512, accumulate DGRAD
+# round 5: ResNet-50 b256 with the r5o / r5q table (stem WGRAD split-K 512, accumulate DGRAD 128x64, ResNet re-tune
 # 128x64) vs the table before them, interleaved
 cd "$GRAFT_REPO_ROOT" || exit 2
-O=gpurun_out/r5p; mkdir -p $O
-# (OLD: the table of commit 9272947, copied to tools/gpu/conv_tuning_before_r5o.json for the run)
+O=gpurun_out/${TAG:-r5p}; mkdir -p $O
+# (OLD: the table of the commit before, copied to tools/gpu/conv_tuning_before_r5o.json for the run)
 OLD=$GRAFT_REPO_ROOT/tools/gpu/conv_tuning_before_r5o.json
 for i in 1 2; do
   for m in old new; do
