@@ -593,6 +593,48 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
   };
 
   // ---------------- epilogue ----------------
+  // FWD statistics of the LDS-staged epilogue, accumulated ACROSS the work items of one column
+  // tile (a thread keeps its 8 channels for every item with the same col0) and added to the
+  // replicas once per run of such items: with a capped grid (launch_gemm_t, kFwdStatGrid) a
+  // block adds one partial sum per channel instead of one per tile — ResNet-50's 64->256 56x56
+  // convs otherwise add 12544 x 2 KB = 26 MB of memory-side float atomics each.
+  constexpr int SCPR = BN / 8;  // the staged epilogue's 16-B chunks per tile row
+  float run_s[8], run_ss[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { run_s[e] = 0.f; run_ss[e] = 0.f; }
+  int run_col = -1;  // column tile the running sums belong to (uniform), -1: none
+  auto flush_stats = [&](const int c0) {
+    // lanes l, l + CPR, ... of a wave share the chunk column: butterfly over them, then the four
+    // waves meet in LDS (after every wave is done with the operand ring / the staged tile)
+#pragma unroll
+    for (int m = SCPR; m < 64; m *= 2)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        run_s[e] += __shfl_xor(run_s[e], m);
+        run_ss[e] += __shfl_xor(run_ss[e], m);
+      }
+    __syncthreads();
+    float* sl = reinterpret_cast<float*>(smem);  // [wave][2][BN]
+    if (lane < SCPR) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sl[(wid * 2 + 0) * BN + lane * 8 + e] = run_s[e];
+        sl[(wid * 2 + 1) * BN + lane * 8 + e] = run_ss[e];
+      }
+    }
+    __syncthreads();
+    float* st = args.stats + stat_rep(bid) * 2 * args.Ng;  // spread contention
+    for (int k = tid; k < 2 * BN; k += 256) {
+      const int which = k / BN, cl = k - which * BN;
+      if (c0 + cl >= args.Ng) continue;
+      const float t = sl[(0 * 2 + which) * BN + cl] + sl[(1 * 2 + which) * BN + cl] +
+                      sl[(2 * 2 + which) * BN + cl] + sl[(3 * 2 + which) * BN + cl];
+      atomicAdd(st + which * args.Ng + c0 + cl, stat_val(t, bid));
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { run_s[e] = 0.f; run_ss[e] = 0.f; }
+  };
+
   // acc[i][j][v] = D[row0 + wm*WTM + i*16 + (lane&15)][col0 + wn*WTN + j*16 + 4*(lane>>4) + v]
   // Ng % 8 == 0 for every mode (C, K multiples of 8), so a lane's 4 columns are all valid or not.
   auto epilogue = [&](const int row0, const int col0, const int zs, const bool split) {
@@ -627,9 +669,10 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
     const bool cok = col < args.Ng;
     float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (MODE == MODE_FWD && args.bias && cok) ld8f_conv(args.bias + col, bv);
-    float s[8], ss[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { s[e] = 0.f; ss[e] = 0.f; }
+    if (MODE == MODE_FWD && red && run_col != col0) {  // a new column tile: settle the last one
+      if (run_col >= 0) flush_stats(run_col);
+      run_col = col0;
+    }
 #pragma unroll 1
     for (int h = 0; h < 2; ++h) {
       __syncthreads();                     // ring idle (last MFMA reads / previous half stored)
@@ -675,42 +718,13 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             const float rv = bf2f(o[e]);
-            s[e] += rv;
-            ss[e] += rv * rv;
+            run_s[e] += rv;
+            run_ss[e] += rv * rv;
           }
         }
       }
     }
-    if (MODE == MODE_FWD && red) {
-      // lanes l, l + CPR, ... of a wave share the chunk column: butterfly over them, then the
-      // four waves meet in LDS (after every wave is done reading the staged tile)
-#pragma unroll
-      for (int m = CPR; m < 64; m *= 2)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          s[e] += __shfl_xor(s[e], m);
-          ss[e] += __shfl_xor(ss[e], m);
-        }
-      __syncthreads();
-      float* sl = reinterpret_cast<float*>(smem);  // [wave][2][BN]
-      if (lane < CPR) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          sl[(wid * 2 + 0) * BN + lane * 8 + e] = s[e];
-          sl[(wid * 2 + 1) * BN + lane * 8 + e] = ss[e];
-        }
-      }
-      __syncthreads();
-      float* st = args.stats + stat_rep(bid) * 2 * args.Ng;  // spread contention
-      for (int k = tid; k < 2 * BN; k += 256) {
-        const int which = k / BN, cl = k - which * BN;
-        if (col0 + cl >= args.Ng) continue;
-        const float t = sl[(0 * 2 + which) * BN + cl] + sl[(1 * 2 + which) * BN + cl] +
-                        sl[(2 * 2 + which) * BN + cl] + sl[(3 * 2 + which) * BN + cl];
-        atomicAdd(st + which * args.Ng + col0 + cl, stat_val(t, bid));
-      }
-    }
-    return;
+    return;  // (the running statistics are added by the next column tile or after the last item)
   }
   // the LDS operand ring is reused for the statistics hand-off: every wave must be done with it
   if (red) __syncthreads();
@@ -1012,6 +1026,7 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
     // the workgroup slot (and its registers) for a full memory round trip after the last MFMA
     if (item + nblk < nitems) wait_dma_barrier<0>();
   }
+  if (MODE == MODE_FWD && run_col >= 0) flush_stats(run_col);  // (uniform: run_col is)
 }
 
 // 2 waves per SIMD (<= 256 VGPR + AGPR per lane): left to itself the compiler gives the big
@@ -1822,6 +1837,16 @@ static int stages_for(int BM, int BN) {
   return 3;
 }
 
+// DDP_AMD_FWD_STAT_GRID: grid cap of the statistics-reducing FWD GEMMs (0 = one block per item)
+static int fwd_stat_grid() {
+  static const int v = [] {
+    const char* e = std::getenv("DDP_AMD_FWD_STAT_GRID");
+    const int g = e ? std::max(0, std::atoi(e)) : 2048;
+    return (kDeterministic ? std::min(g, kStatRep) : g) / 8 * 8;
+  }();
+  return v;
+}
+
 template <int MODE, int BM, int BN, int NST, int BNF>
 static void launch_gemm_t(const ConvArgs& a, int items, hipStream_t st) {
   constexpr int kStageBytes = (BM + BN) * 64 * 2;
@@ -1848,8 +1873,15 @@ static void launch_gemm_t(const ConvArgs& a, int items, hipStream_t st) {
     attr = true;
   }
   // one work item (tile x split) per workgroup (a persistent grid sized to the resident slots
-  // was measured no faster and removed in round 5)
-  hipLaunchKernelGGL(kern, dim3(items), dim3(256), lds, st, a);
+  // was measured no faster and removed in round 5) — except FWD GEMMs whose LDS-staged
+  // epilogue reduces the BatchNorm statistics: a grid of kFwdStatGrid blocks (a multiple of 8,
+  // so item % 8 keeps naming the block's XCD for xcd_remap) walks the items and adds each
+  // column tile's partial sums once per block (the running sums of conv_igemm_body)
+  int grid = items;
+  if (MODE == MODE_FWD && a.stats && a.splits <= 1 && a.epi_stage && !(BM == 64 && BN == 64) &&
+      fwd_stat_grid() > 0 && items > fwd_stat_grid())
+    grid = fwd_stat_grid();
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, a);
 }
 
 template <int MODE, int BM, int BN, int NST>
