@@ -21,9 +21,15 @@ def test_tuning_table_well_formed():
             assert e["tile"] in (0, 1) and 1 <= e["splits"] <= 16 and 1 <= e["stages"] <= 128
         else:
             assert 0 <= e["tile"] <= 7
-            assert 1 <= e["splits"] <= 64
+            # split-K slabs (splits x M x N fp32) must fit the 32 Mi-element workspace
+            # (ops/common.py WORKSPACE_ELEMS); the stem WGRAD's 512-way split is the largest
+            assert 1 <= e["splits"] <= 1024
+            assert e["splits"] == 1 or e["splits"] * e["M"] * e["N"] <= 32 << 20
         assert min(e["M"], e["N"], e["K"]) > 0
-        assert e["us"] <= e["auto_us"] + 1e-6
+        if "auto_us" in e:  # (hand-added entries from a dedicated sweep carry a "note" instead)
+            assert e["us"] <= e["auto_us"] + 1e-6
+        else:
+            assert "note" in e
         keys.add((e["mode"], e["M"], e["N"], e["K"]))
     assert len(keys) == len({(e["mode"], e["M"], e["N"], e["K"]) for e in t["entries"]})
     # the flagship VGG-11 b256 problems are covered (e.g. layers.18 fwd: M=256*4*4, N=512)
