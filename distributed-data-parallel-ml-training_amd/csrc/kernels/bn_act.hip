@@ -133,16 +133,21 @@ __device__ __forceinline__ void fold_fwd_coeffs(const BnArgs& a, float* l_sc, fl
 }
 
 // ------------------------------- forward apply -------------------------------
-// One thread = IPT items (output pixels) x 8 channels; every load is issued up front.
+// One thread = IPT items (output pixels) x 8 channels; every load is issued up front. A grid
+// smaller than the item blocks walks them with a grid stride (the capped FOLD launch: the
+// replica reduction of fold_fwd_coeffs is paid once per block, not once per 256 x IPT items).
 template <bool POOL, int IPT, bool FOLD>
 __global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnArgs a) {
   constexpr int NP = POOL ? 4 : 1;
   const int G = a.C / 8;
   const int Ho = POOL ? a.H / 2 : a.H, Wo = POOL ? a.W / 2 : a.W;
   const size_t total = (size_t)a.N * Ho * Wo * G;
+  const size_t nbt = (total + 256 * IPT - 1) / (256 * IPT);
+  bool folded = false;
+  for (size_t blk = blockIdx.x; blk < nbt; blk += gridDim.x) {
   u16x8 zv[IPT][NP], rv[IPT][POOL ? 1 : NP];
   float sc[IPT][8], sh[IPT][8];
-  const size_t t0 = (size_t)blockIdx.x * 256 * IPT + threadIdx.x;
+  const size_t t0 = blk * 256 * IPT + threadIdx.x;
 #pragma unroll
   for (int it = 0; it < IPT; ++it) {
     const size_t t = t0 + it * 256;
@@ -166,7 +171,10 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnArgs a) {
   }
   if (FOLD) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    fold_fwd_coeffs(a, lds, lds + a.C);
+    if (!folded) {  // (uniform: the first walked item block of every block)
+      fold_fwd_coeffs(a, lds, lds + a.C);
+      folded = true;
+    }
 #pragma unroll
     for (int it = 0; it < IPT; ++it) {
       const size_t t = t0 + it * 256;
@@ -204,6 +212,7 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnArgs a) {
     for (int e = 0; e < 8; ++e) o[e] = f2bf(best[e]);
     st8(a.out + pix * a.C + cg * 8, o);
     if (!POOL && a.mask) a.mask[t] = (unsigned char)mb;  // t = pixel * G + cg
+  }
   }
 }
 
@@ -349,7 +358,13 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
   }
 }
 
-template <bool POOL, int IPT>
+// FOLD: the backward finalize folded into the apply (no bn_finalize_bwd launch): the block's
+// 256 threads load the 16 replicas of its channel chunk's S1 / S2 with coalesced 16-B loads (16
+// per thread at 256 channels), reduce them in registers in replica order — the finalize's own
+// order, so k1 / k2 are bit-identical to the separate launch — and hand k1 / k2 over in LDS;
+// blocks x == 0 also add dgamma / dbeta and write the table's k1 / k2 rows. The launcher folds
+// only while the grid's replica re-reads stay small (kFoldBwdBytes).
+template <bool POOL, int IPT, bool FOLD = false>
 __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(BnArgs a) {
   constexpr int NP = POOL ? 4 : 1;
   const int G = a.C / 8;
@@ -360,32 +375,74 @@ __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(BnArgs a) {
   const int cgl = threadIdx.x % Gb;
   const int prow = threadIdx.x / Gb, prows = 256 / Gb;
   const int c0 = (cg_base + cgl) * 8;
+  // a capped FOLD grid walks the item blocks with a grid stride (one replica fold per block)
+  const size_t per_blk = (size_t)prows * IPT;
+  const size_t nbx = (npix + per_blk - 1) / per_blk;
   BwdItems<POOL, IPT> L;
-  bwd_load<POOL, IPT>(a, L, (size_t)blockIdx.x * prows * IPT + prow, prows, npix, cg_base + cgl,
+  bwd_load<POOL, IPT>(a, L, (size_t)blockIdx.x * per_blk + prow, prows, npix, cg_base + cgl,
                       Ho, Wo);
   float sc[8], sh[8], mu[8], is[8], k1[8], k2[8];
   ld8f(a.coef + kSc * a.C + c0, sc);
   ld8f(a.coef + kSh * a.C + c0, sh);
   ld8f(a.coef + kMu * a.C + c0, mu);
   ld8f(a.coef + kIs * a.C + c0, is);
-  ld8f(a.coef + kK1 * a.C + c0, k1);
-  ld8f(a.coef + kK2 * a.C + c0, k2);
+  if (FOLD) {
+    __shared__ __attribute__((aligned(16))) float kk[2][2048];  // k1 | k2 of the chunk
+    const int nch = Gb * 8;                 // channels of this block's chunk (<= 2048)
+    const float inv_m = 1.f / ((float)a.N * a.H * a.W);
+    // 4 consecutive values (one float4) per thread and pass: [which][channel] of the chunk
+    for (int q = threadIdx.x * 4; q < 2 * nch; q += 1024) {
+      const int which = q / nch, cl = q - which * nch;
+      const float* src = a.sums + which * a.C + cg_base * 8 + cl;
+      float4 t = *reinterpret_cast<const float4*>(src);
 #pragma unroll
-  for (int it = 0; it < IPT; ++it) {
-    if (!L.ok[it]) continue;
-    float xh[NP][8], dyb[NP][8];
-    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], L.mb[it], sc, sh, mu, is, xh, dyb);
-#pragma unroll
-    for (int d = 0; d < NP; ++d) {
-      u16x8 o, r;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        o[e] = f2bf(sc[e] * (dyb[d][e] - k1[e] - xh[d][e] * k2[e]));  // sc = gamma * invstd
-        r[e] = f2bf(dyb[d][e]);
+      for (int r = 1; r < kStatRep; ++r) {
+        const float4 v = *reinterpret_cast<const float4*>(src + (size_t)r * 2 * a.C);
+        t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
       }
-      st8(a.dz + L.off[it][d], o);
-      if (a.dres) st8(a.dres + L.off[it][d], r);
+      const float tv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        kk[which][cl + e] = tv[e] * inv_m;
+        if (blockIdx.x == 0) {
+          const int c = cg_base * 8 + cl + e;
+          a.coef[(which ? kK2 : kK1) * a.C + c] = tv[e] * inv_m;
+          float* dst = which ? a.dgamma : a.dbeta;  // S2 -> dgamma, S1 -> dbeta
+          if (dst) dst[c] += tv[e];
+        }
+      }
     }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      k1[e] = kk[0][cgl * 8 + e];
+      k2[e] = kk[1][cgl * 8 + e];
+    }
+  } else {
+    ld8f(a.coef + kK1 * a.C + c0, k1);
+    ld8f(a.coef + kK2 * a.C + c0, k2);
+  }
+  for (size_t bb = blockIdx.x;;) {
+#pragma unroll
+    for (int it = 0; it < IPT; ++it) {
+      if (!L.ok[it]) continue;
+      float xh[NP][8], dyb[NP][8];
+      bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], L.mb[it], sc, sh, mu, is, xh, dyb);
+#pragma unroll
+      for (int d = 0; d < NP; ++d) {
+        u16x8 o, r;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          o[e] = f2bf(sc[e] * (dyb[d][e] - k1[e] - xh[d][e] * k2[e]));  // sc = gamma * invstd
+          r[e] = f2bf(dyb[d][e]);
+        }
+        st8(a.dz + L.off[it][d], o);
+        if (a.dres) st8(a.dres + L.off[it][d], r);
+      }
+    }
+    bb += gridDim.x;
+    if (!FOLD || bb >= nbx) break;
+    bwd_load<POOL, IPT>(a, L, bb * per_blk + prow, prows, npix, cg_base + cgl, Ho, Wo);
   }
 }
 
@@ -677,11 +734,30 @@ static unsigned blocks_for(size_t items, size_t per_block) {
 // Folding the finalize into the apply kernel costs every block a replica reduction of its
 // channels; worth it (one launch fewer) while that re-read traffic stays small.
 constexpr size_t kFoldBytes = 24u << 20;
+// Big layers: the FOLD kernels on a capped grid (DDP_AMD_BN_FOLD_FWD_GRID blocks walking the
+// item blocks, forward and backward apply) while that grid's replica re-reads stay within
+// kFoldGridBytes. Off by default: at 2048 blocks ResNet-50 b256 ran 26.26 vs 25.68 ms with the
+// separate finalize launches (profiles/r5v_bn_fold.md) — the 25088-block streaming applies
+// lose more to the capped grid than the finalize launch costs.
+constexpr size_t kFoldGridBytes = 64u << 20;
+static unsigned fold_fwd_grid() {
+  static const unsigned v = [] {
+    const char* e = std::getenv("DDP_AMD_BN_FOLD_FWD_GRID");
+    return (unsigned)(e ? std::max(0, std::atoi(e)) : 0);
+  }();
+  return v;
+}
+
 template <bool POOL, int IPT>
 static void launch_fwd(const BnArgs& a, size_t items, hipStream_t st) {
   const unsigned nb = blocks_for(items, 256 * IPT);
-  if ((size_t)nb * a.C * 2 * kStatRep * sizeof(float) <= kFoldBytes) {
+  const size_t per_block = (size_t)a.C * 2 * kStatRep * sizeof(float);
+  const unsigned cap = std::min(nb, fold_fwd_grid());
+  if ((size_t)nb * per_block <= kFoldBytes) {
     hipLaunchKernelGGL((bn_act_fwd_kernel<POOL, IPT, true>), dim3(nb), dim3(256),
+                       2 * a.C * sizeof(float), st, a);
+  } else if (!kDeterministic && cap >= 1024 && (size_t)cap * per_block <= kFoldGridBytes) {
+    hipLaunchKernelGGL((bn_act_fwd_kernel<POOL, IPT, true>), dim3(cap), dim3(256),
                        2 * a.C * sizeof(float), st, a);
   } else {
     hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3(blocks_for(a.C, 256)), dim3(256), 0, st, a);
@@ -710,6 +786,16 @@ extern "C" int ddp_bn_act_fwd(const BnArgs* args, hipStream_t st) {
 // Target reduce-grid size (DDP_AMD_BN_BWD_BLOCKS overrides).
 static size_t kBwdBlocks = 1024;
 
+// Largest grid-wide replica re-read of a folded backward apply (DDP_AMD_BN_FOLD_BWD_MB, default
+// 32 MB; 0 = always the separate finalize launch)
+static size_t fold_bwd_bytes() {
+  static const size_t v = [] {
+    const char* e = std::getenv("DDP_AMD_BN_FOLD_BWD_MB");
+    return (size_t)(e ? std::max(0, std::atoi(e)) : 32) << 20;
+  }();
+  return v;
+}
+
 // Reduce-grid cap (DDP_AMD_BN_REDUCE_GRID, 0 = uncapped): the reduce walks its item blocks
 // with a grid stride, so every block adds ONE partial sum per channel. Uncapped, ResNet-50's
 // 56x56x256 layers ran 25088 blocks = 51 MB of memory-side float atomics per layer (~40 us at
@@ -733,6 +819,23 @@ static void launch_bwd(const BnArgs& a, size_t npix, int Gb, int chunks, hipStre
   // replicas the reduce just wrote with memory-side atomics) measured 3-4x slower applies at
   // batch 256 and +50 us per b32 step; the reduce's last-arriving block doing it measured slower
   // than the launch boundary too (profiles/r2_launch_reduction_ab.md, r3_bn_bwd_one_launch.md).
+  // finalize folded into the apply while the grid's replica re-reads stay small (every block
+  // reads 16 x 2 x its chunk's channels; L2-served after the first XCD miss)
+  // — or, for bigger grids, on a capped grid that walks the item blocks (kFoldGrid blocks in all)
+  const size_t per_block = (size_t)kStatRep * 2 * (size_t)Gb * 8 * sizeof(float);
+  const size_t fold_bytes = (size_t)bx * chunks * per_block;
+  if (!kDeterministic && fold_bwd_bytes() > 0 && fold_bytes <= fold_bwd_bytes()) {
+    hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT, true>), dim3(bx, chunks), dim3(256), 0,
+                       st, a);
+    return;
+  }
+  const unsigned cx = std::min(bx, fold_fwd_grid() / (unsigned)chunks);
+  if (!kDeterministic && fold_bwd_bytes() > 0 && cx * chunks >= 1024 &&
+      (size_t)cx * chunks * per_block <= kFoldGridBytes) {
+    hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT, true>), dim3(cx, chunks), dim3(256), 0,
+                       st, a);
+    return;
+  }
   hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3(blocks_for(a.C, 256)), dim3(256), 0, st, a);
   hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT>), dim3(bx, chunks), dim3(256), 0, st, a);
 }

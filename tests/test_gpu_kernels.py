@@ -196,6 +196,15 @@ def test_bn_act_fwd_bwd(native_ext, N, C, H, pool, res, mode):
         nat.bn_bwd_local_set(8)  # the shipped limit (bn_act.hip kLocalMaxLoads)
 
 
+@pytest.mark.parametrize("N,C,H,pool,res", [(128, 256, 28, False, True), (128, 128, 56, True, False)])
+def test_bn_act_big_grid_fold(native_ext, N, C, H, pool, res):
+    """Layers big enough for the capped-grid FOLD launches (bn_act.hip: the forward apply and the
+    backward apply walk their item blocks with a grid stride and fold the finalize once per
+    block) against the fp32 PyTorch reference."""
+    from ddp_amd.ops.common import ptr, stream_handle
+    _bn_case(native_ext, N, C, H, pool, res, "split", ptr, stream_handle)
+
+
 def _bn_case(nat, N, C, H, pool, res, mode, ptr, stream_handle):
     z = bf(torch.randn(N, C, H, H, device=DEV) * 2 + 0.5)
     r = bf(torch.randn(N, C, H, H, device=DEV)) if res else None
