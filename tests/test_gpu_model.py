@@ -568,9 +568,9 @@ def test_sgd_in_backward_covers_every_parameter_once(native_ext, batch):
     seen = []
     orig = opt._work_table
 
-    def spy(prange=None, exclude=frozenset()):
-        r = orig(prange, exclude)
-        seen.append((prange, frozenset(exclude)))
+    def spy(prange=None, exclude=frozenset(), pack_only=frozenset()):
+        r = orig(prange, exclude, pack_only)
+        seen.append((prange, frozenset(exclude), frozenset(pack_only)))
         return r
     opt._work_table = spy
     st._body()
@@ -579,20 +579,27 @@ def test_sgd_in_backward_covers_every_parameter_once(native_ext, batch):
     st.step()
     torch.cuda.synchronize()
     opt._work_table = orig
-    calls = [(p, e) for p, e in seen if p is None]
+    calls = [(p, e, po) for p, e, po in seen if p is None]
     assert calls, "the step's SGD launch never built its work table"
     registered = set(opt._bwd_index.values())
     n = len(opt.arena.params)
-    for _, exclude in calls:
+    for _, exclude, pack_only in calls:
         assert exclude <= registered, exclude - registered
+        # masters updated in a pair's WGRAD epilogue: excluded from the SGD, re-packed only
+        assert pack_only <= exclude
         keep = [i for i in range(n) if i not in exclude]
         items = {i for i in keep if opt._per_param[i]}
         assert items == set(keep), set(keep) - items  # every kept parameter has work items
         assert not items & exclude
         assert items | exclude == set(range(n))
-    # at 256 images every conv weight's WGRAD has a split-K finish that takes the update
+        assert all(opt._per_param[i] and all(it[0] == 2 for it in opt._per_param[i])
+                   for i in pack_only)
+    # at 256 images every conv weight's WGRAD has a split-K finish that takes the update; at 32
+    # the backward pairs' unsplit WGRAD halves update the masters
     if batch == 256:
-        assert any(len(e) > 0 for _, e in calls)
+        assert any(len(e) > 0 for _, e, _ in calls)
+    if batch == 32:
+        assert any(len(po) > 0 for _, _, po in calls)
 
 
 def _plain_vgg_forward(model, x):
@@ -667,6 +674,7 @@ def test_vgg11_b256_trajectory_matches_bf16_emulated_oracle(native_ext):
 
     lg, dg = run_fused()
     lg2, dg2 = run_fused()  # same build, same data: the summation-order noise floor
+    lg3, _ = run_fused()    # (a third run: one pair under-samples the floor; r5y2 flake)
     le, de = run_aten(_emulated_vgg_forward)
     lf, df = run_aten(_plain_vgg_forward)
 
@@ -681,9 +689,11 @@ def test_vgg11_b256_trajectory_matches_bf16_emulated_oracle(native_ext):
     print("emu    :", [round(v, 4) for v in le])
     print("fp32   :", [round(v, 4) for v in lf])
     print("update cosine vs self %.4f emu %.4f fp32 %.4f" % (cos(dg, dg2), cos(dg, de), cos(dg, df)))
-    floor = max(r_self)
+    # noise floor: the largest distance between any two runs of the same build
+    floor = max(max(abs(a - b) / abs(b) for a, b in zip(u, v))
+                for u, v in ((lg, lg2), (lg, lg3), (lg2, lg3)))
     for k in range(steps):
-        assert r_emu[k] <= 3.0 * floor + 0.005, (k, r_emu, r_self)
+        assert r_emu[k] <= 3.0 * floor + 0.005, (k, r_emu, r_self, floor)
     assert max(r_f32) < 0.05, r_f32  # bf16 vs fp32 storage: a few % at most
     assert lg[-1] < lg[0] and le[-1] < le[0]
     assert cos(dg, de) >= 0.95 and cos(dg, de) >= cos(dg, dg2) - 0.03
