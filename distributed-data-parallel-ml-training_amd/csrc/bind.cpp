@@ -311,6 +311,16 @@ PYBIND11_MODULE(_native, m) {
     v.resize(n);
     return v;
   });
+  m.def("sgd_fuse_taken_master", []() {
+    std::vector<uintptr_t> v(256);
+    int n = ddp_sgd_fuse_taken_master(v.data(), (int)v.size());
+    if (n > (int)v.size()) {
+      v.resize(n);
+      n = ddp_sgd_fuse_taken_master(v.data(), n);
+    }
+    v.resize(n);
+    return v;
+  });
   m.def("conv_dense2x2_set", [](int on) { ddp_conv_dense2x2_set(on); });
   m.def("conv_dense2x2_ok", [](py::tuple g) {
     auto c = geom(g);

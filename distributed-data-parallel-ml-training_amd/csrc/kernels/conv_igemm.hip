@@ -124,6 +124,12 @@ struct ConvArgs {
   // of the flat [rows][Ng] tensor) — dx = bf16(result + (bit ? acc_dy : 0)), dx never read
   const unsigned short* acc_dy;
   const unsigned char* acc_mask;
+  // WGRAD without split-K (its epilogue owns complete gradient elements) inside the backward
+  // pair launch, SGD in the backward (TrainStep, one GPU): the epilogue applies the update to
+  // the fp32 master + momentum instead of storing the gradient (sgd.p != nullptr). The bf16
+  // operand copy is NOT written here — the pair's DGRAD half is still reading it — but by the
+  // step's SGD launch (pack-only items, optim.hip item 5).
+  SgdFuse sgd;
 };
 
 // the accumulating DGRAD's first-branch value of 4 / 8 consecutive channels starting at flat
@@ -870,7 +876,18 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
       if (!cok || row >= args.Mg) continue;
       const f32x4 v = acc[i][j];
       if (MODE == MODE_WGRAD && !split) {
-        if (g.wkrsc && g.Creal == g.C) {
+        if (g.wkrsc && g.Creal == g.C && args.sgd.p) {  // master-only SGD (see ConvArgs::sgd)
+          const size_t e = ((size_t)row * g.R * g.S + wrs) * g.C + wc;
+          float4 pv = *reinterpret_cast<const float4*>(args.sgd.p + e);
+          float4 bv = *reinterpret_cast<const float4*>(args.sgd.buf + e);
+          const SgdFuse& h = args.sgd;
+          pv.x = sgd_update1(pv.x, v[0], bv.x, h.lr, h.momentum, h.wd, h.grad_scale, h.nesterov);
+          pv.y = sgd_update1(pv.y, v[1], bv.y, h.lr, h.momentum, h.wd, h.grad_scale, h.nesterov);
+          pv.z = sgd_update1(pv.z, v[2], bv.z, h.lr, h.momentum, h.wd, h.grad_scale, h.nesterov);
+          pv.w = sgd_update1(pv.w, v[3], bv.w, h.lr, h.momentum, h.wd, h.grad_scale, h.nesterov);
+          *reinterpret_cast<float4*>(args.sgd.p + e) = pv;
+          *reinterpret_cast<float4*>(args.sgd.buf + e) = bv;
+        } else if (g.wkrsc && g.Creal == g.C) {
           float* d = args.dw + ((size_t)row * g.R * g.S + wrs) * g.C + wc;
           float4 o = *reinterpret_cast<float4*>(d);
           o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
@@ -1965,6 +1982,21 @@ static FinishArgs finish_args(int mode, const ConvArgs& a) {
 // a layer without a DGRAD (g_sgd_allow is raised around exactly those finishes).
 static std::map<const float*, SgdFuse> g_sgd_reg;  // gradient view -> its fused update
 static std::set<const float*> g_sgd_taken;
+static std::set<const float*> g_sgd_master;  // master updated in a pair's WGRAD epilogue: the
+                                             // step's SGD launch re-packs the operand only
+// the pair launch's unsplit WGRAD half (ConvArgs::sgd): any registered weight qualifies, the
+// fp32 master is read by nothing else in the backward
+static SgdFuse sgd_fuse_master(const float* dw) {
+  static const bool on = [] {  // DDP_AMD_SGD_PAIR_MASTER=0: the step's SGD launch does it all
+    const char* e = std::getenv("DDP_AMD_SGD_PAIR_MASTER");
+    return !(e && e[0] == '0');
+  }();
+  if (!on || g_sgd_reg.empty()) return SgdFuse{};
+  auto it = g_sgd_reg.find(dw);
+  if (it == g_sgd_reg.end()) return SgdFuse{};
+  g_sgd_master.insert(dw);
+  return it->second;
+}
 static bool g_sgd_allow = false;
 static SgdFuse sgd_fuse_for(const float* dw, int groups) {
   if (!g_sgd_allow || groups != 1 || g_sgd_reg.empty()) return SgdFuse{};
@@ -2715,6 +2747,8 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
   if (dneed + wneed > ws_elems) return separate();
   if (g_pair_mode == 3 && !both64 && itd + itw > g_pair_items) return separate();
   if (d.d2x2 && d.has_bnf && d.splits < 2) return separate();
+  // unsplit WGRAD half: SGD on the master in its epilogue (no finish would take it)
+  if (!needs_finish(MODE_WGRAD, w) && w.g.wkrsc && w.g.Creal == w.g.C) w.sgd = sgd_fuse_master(dw);
   const bool bnf1 = d.has_bnf && d.splits <= 1;
   if (bnf1) {
     hipLaunchKernelGGL((conv_bwd_pair_kernel<64, 64, 3, 1>), dim3(itd + itw), dim3(256), 0, st,
@@ -2755,7 +2789,18 @@ extern "C" void ddp_sgd_fuse_register(float* dw, const SgdFuse* f, int clear) {
   if (clear) g_sgd_reg.clear();
   if (dw && f) g_sgd_reg[dw] = *f;
 }
-extern "C" void ddp_sgd_fuse_begin() { g_sgd_taken.clear(); }
+extern "C" void ddp_sgd_fuse_begin() {
+  g_sgd_taken.clear();
+  g_sgd_master.clear();
+}
+extern "C" int ddp_sgd_fuse_taken_master(uintptr_t* out, int cap) {
+  int n = 0;
+  for (const float* p : g_sgd_master) {
+    if (n < cap) out[n] = reinterpret_cast<uintptr_t>(p);
+    ++n;
+  }
+  return n;
+}
 // a WGRAD whose layer runs no DGRAD (the input layer): its finish may apply the SGD step
 extern "C" int ddp_conv_wgrad_final(const ConvGeom* g, const void* dy, const void* x, float* dw,
                                     float* ws, size_t ws_elems, int splits, hipStream_t st) {

@@ -231,6 +231,22 @@ __device__ void sgd_pack_body(const int4* __restrict__ items, const long long* _
       *reinterpret_cast<float4*>(g + off + i) = make_float4(0.f, 0.f, 0.f, 0.f);
     return;
   }
+  if (it.x == 5) {
+    // {5, offset in the tensor, count, desc}: operand re-pack only — the fp32 master was already
+    // updated by the backward (conv_igemm.hip ConvArgs::sgd); bf16(p) into the operand copy
+    // (same index order as item 2; count multiple of 4)
+    const long long* d = descs + 12 * it.w;
+    const size_t base = (size_t)d[0] + (unsigned)it.y;
+    unsigned short* wc = reinterpret_cast<unsigned short*>(d[6]) + (unsigned)it.y;
+    for (int i = tid * 4; i < it.z; i += 256 * 4) {
+      const float4 pv = *reinterpret_cast<const float4*>(p + base + i);
+      uint2 pk;
+      pk.x = (unsigned)f2bf(pv.x) | ((unsigned)f2bf(pv.y) << 16);
+      pk.y = (unsigned)f2bf(pv.z) | ((unsigned)f2bf(pv.w) << 16);
+      *reinterpret_cast<uint2*>(wc + i) = pk;
+    }
+    return;
+  }
   if (it.x == 2) {
     // conv weight whose bf16 operand copy has the master's own index order ([K][R][S][C] with
     // C == Cr, or 1x1): elementwise update + bf16 store, no LDS staging

@@ -79,12 +79,20 @@ class FusedSGD(torch.optim.SGD):
         idx = getattr(self, "_bwd_index", {})
         return frozenset(idx[d] for d in native().sgd_fuse_taken() if d in idx)
 
-    def _work_table(self, prange=None, exclude=frozenset()):
+    def _master_in_backward(self):
+        """Parameter indices whose fp32 master (and momentum) a backward pair's unsplit WGRAD
+        epilogue updated: the step's launch re-packs only their bf16 operand copy."""
+        from ..ops.common import native
+        idx = getattr(self, "_bwd_index", {})
+        return frozenset(idx[d] for d in native().sgd_fuse_taken_master() if d in idx)
+
+    def _work_table(self, prange=None, exclude=frozenset(), pack_only=frozenset()):
         """Device work-item table of the fused SGD + re-pack kernel (rebuilt when the set of
         packed conv weights changes, e.g. after the model's fused plan is first built).
         ``prange = (i0, i1)`` restricts it to parameters i0 <= i < i1 (one DDP bucket: the
         pipelined step updates each bucket as soon as its all-reduce is done); ``exclude`` =
-        parameter indices updated elsewhere (SGD in the backward)."""
+        parameter indices updated elsewhere (SGD in the backward); ``pack_only`` (a subset of
+        ``exclude``) = those whose bf16 operand copy is still to be re-packed here (item 5)."""
         from ..ops.common import native
         a = self.arena
         key = tuple(self._packs())
@@ -121,18 +129,23 @@ class FusedSGD(torch.optim.SGD):
             dev = a.data.device
             self._descs = torch.tensor(descs if descs else [[0] * 12], dtype=torch.int64, device=dev)
         rng = tuple(prange) if prange is not None else (0, len(a.params))
-        t = self._tables.get((rng, exclude))
+        t = self._tables.get((rng, exclude, pack_only))
         if t is None:
             keep = [i for i in range(*rng) if i not in exclude]
+            packs = [i for i in range(*rng) if i in pack_only]
+            for i in packs:
+                if not self._per_param[i] or any(it[0] != 2 for it in self._per_param[i]):
+                    raise RuntimeError(f"parameter {i}: no elementwise re-pack layout")
             # conv re-pack items first (the heavier tiles start early), then elementwise items
             sel = [it for i in keep for it in self._per_param[i] if it[0] != 0] + \
+                  [[5] + it[1:] for i in packs for it in self._per_param[i]] + \
                   [it for i in keep for it in self._per_param[i] if it[0] == 0]
             if not sel and not exclude:
                 raise ValueError(f"no parameters in range {rng}")
             items = (torch.tensor(sel, dtype=torch.int32, device=a.data.device) if sel
                      else None)
             t = (items, len(sel))
-            self._tables[(rng, exclude)] = t
+            self._tables[(rng, exclude, pack_only)] = t
         return t[0], t[1], self._descs
 
     def _elem_table(self, lo, hi):
@@ -223,8 +236,11 @@ class FusedSGD(torch.optim.SGD):
         g = self.param_groups[0]
         s = stream.cuda_stream if stream is not None else stream_handle()
         a = self.arena
-        exclude = self._fused_in_backward() if fused_taken else frozenset()
-        items, n_items, descs = self._work_table(params, exclude)
+        exclude = pack_only = frozenset()
+        if fused_taken:
+            pack_only = self._master_in_backward()
+            exclude = self._fused_in_backward() | pack_only
+        items, n_items, descs = self._work_table(params, exclude, pack_only)
         if n_items == 0:  # every tensor was updated in the backward: only the data cursor
             if counter:
                 native().counter_add(int(counter[0]), int(counter[1]), s)
