@@ -63,6 +63,7 @@ static const ddp_amd::BnBwdFuse* bn_fuse(py::object o, ddp_amd::BnBwdFuse* f) {
   f->relu = t[4].cast<int>();
   f->Hz = t[5].cast<int>();
   f->Wz = t[6].cast<int>();
+  f->code = t.size() > 7 ? P<unsigned>(t[7].cast<uintptr_t>()) : nullptr;
   return f;
 }
 
@@ -186,15 +187,19 @@ PYBIND11_MODULE(_native, m) {
   });
   m.def("l0_bwd", [](py::tuple g, uintptr_t x, uintptr_t wc, uintptr_t bias, float eps, int relu,
                      uintptr_t coef, uintptr_t dy, uintptr_t sums, uintptr_t dz, uintptr_t dgamma,
-                     uintptr_t dbeta, uintptr_t code, uintptr_t zw, uintptr_t st) {
+                     uintptr_t dbeta, uintptr_t code, uintptr_t zw, uintptr_t st, int sums_ready) {
     auto c = geom(g);
     ddp_amd::L0Io io{};
     io.x = P<void>(x); io.wc = P<void>(wc); io.bias = P<float>(bias); io.eps = eps; io.relu = relu;
     io.coef = P<float>(coef); io.dy = P<void>(dy); io.sums = P<float>(sums); io.dz = P<void>(dz);
     io.dgamma = P<float>(dgamma); io.dbeta = P<float>(dbeta); io.code = P<void>(code);
     io.zw = P<void>(zw);
+    io.sums_ready = sums_ready;
     check(ddp_l0_bwd(&c, &io, S(st)), "l0_bwd");
-  });
+  }, py::arg("g"), py::arg("x"), py::arg("wc"), py::arg("bias"), py::arg("eps"), py::arg("relu"),
+     py::arg("coef"), py::arg("dy"), py::arg("sums"), py::arg("dz"), py::arg("dgamma"),
+     py::arg("dbeta"), py::arg("code"), py::arg("zw"), py::arg("stream"),
+     py::arg("sums_ready") = 0);
   m.def("conv_tr_would_serve", [](py::tuple g, size_t ws_elems, int in_mode) {
     auto c = geom(g);
     return ddp_conv_tr_would_serve(&c, ws_elems, in_mode) == 1;
@@ -283,7 +288,9 @@ PYBIND11_MODULE(_native, m) {
     const ddp_amd::BnBwdFuse* fp = bn_fuse(bn, &f);
     check(ddp_conv_bwd_pair(&c, P<void>(dy), P<void>(wc), P<void>(dx), P<void>(x), P<float>(dw),
                             P<float>(ws), ws_elems, fp, app, &done, S(st)), "conv_bwd_pair");
-    return done == 1;
+    // 1: the preceding block's whole BN backward ran in the finish (bna); 2: the input block's
+    // BN-backward sums were taken in the finish (bn with code); 0: neither
+    return done;
   }, py::arg("g"), py::arg("dy"), py::arg("wc"), py::arg("dx"), py::arg("x"), py::arg("dw"),
      py::arg("ws"), py::arg("ws_elems"), py::arg("stream"), py::arg("bn") = py::none(),
      py::arg("bna") = py::none());

@@ -74,6 +74,10 @@ struct BnBwdFuse {
   float* sums;              // its backward sums [kStatRep][2][C] (zeroed per forward)
   int pool, relu;           // 2x2/s2 max-pool between z and the dgrad output; ReLU
   int Hz, Wz;               // z spatial dims (2x the dgrad output's when pooled)
+  // VGG input block (conv_l0.hip, z never stored): ``code`` = the forward's per-window gradient
+  // destinations (lane-major bytes, conv_l0.hip Args::code) and ``z`` = its zw (the winner's z,
+  // POOLED shape): the sums are l0_sums_kernel's, taken in the dgrad's split-K finish only
+  const unsigned* code;
 };
 
 // The COMPLETE BatchNorm backward of that preceding block fused into a small dgrad's split-K
@@ -160,6 +164,8 @@ struct L0Io {
   void* zw;             // [N][H/2][W/2][64] bf16: z of that pixel (forward -> backward sums)
   float* dgamma;
   float* dbeta;
+  int sums_ready;       // backward: ``sums`` already accumulated (the next block's dgrad finish,
+                        // BnBwdFuse::code) -> the dz pass only
 };
 
 struct PackDesc {

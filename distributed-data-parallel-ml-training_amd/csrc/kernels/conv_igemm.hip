@@ -1200,7 +1200,23 @@ __device__ __forceinline__ void splitk_finish_body(const FinishArgs& fa, float* 
       }
     }
     st8(dst, o);
-    if (has_bnf) {  // same recomputation as the GEMM epilogue / bn_act.hip bwd_compute
+    if (has_bnf && bnf.code) {
+      // VGG input block: row = its pooled window; the gradient goes to the position the forward
+      // recorded (code < 4: conv_l0.hip, 4 = ReLU cut, 0xFF = NaN window) and that pixel's z is
+      // the recorded zw — l0_sums_kernel's sums S1 = sum dy, S2 = sum dy * xhat, here
+      // Code bytes of channel c: window * 64 + ((c % 16) / 4) * 16 + (c / 16) * 4 + c % 4
+      const int c0 = cg * 8;
+      const unsigned* cw = bnf.code + (size_t)row * 16 + ((c0 & 15) >> 2) * 4 + (c0 >> 4);
+      const unsigned w0 = cw[0], w1 = cw[4];  // channels c0..c0+3 | c0+4..c0+7
+      const u16x8 zz = ld8(bnf.z + (size_t)row * Ng + c0);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const unsigned code = ((e < 4 ? w0 : w1) >> (8 * (e & 3))) & 0xFFu;
+        const float d = code < 4u ? bf2f(o[e]) : 0.f;
+        s[e] += d;
+        ss[e] += d * ((bf2f(zz[e]) - fmu[e]) * fis[e]);
+      }
+    } else if (has_bnf) {  // same recomputation as the GEMM epilogue / bn_act.hip bwd_compute
       const int hw = H * W;
       const int n = row / hw, rem = row - n * hw;
       const int h = rem / W, w = rem - h * W;
@@ -2485,6 +2501,7 @@ static int conv_dgrad_impl(const ConvGeom* g, const void* dy, const void* wc, vo
                            const unsigned char* acc_mask = nullptr) {
   if (bn_done) *bn_done = 0;
   if (g->C % 8 || g->K % 8) return -1;
+  if (bn && bn->code) return -3;  // the input block's sums: the pair launch's finish only
   if (bn && (accumulate || g->stride != 1)) return -3;  // fused BN sums: plain stride-1 dgrad only
   // deferred first branch: every dx element must be written by this call (stride 1)
   if (acc_mask && (!accumulate || !acc_dy || g->stride != 1)) return -3;
@@ -2654,7 +2671,10 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
   if (!bn) ba = nullptr;
   auto separate = [&]() -> int {
     // DGRAD first: the WGRAD finish may then apply the layer's SGD step (g_sgd_allow)
-    const int r = conv_dgrad_impl(g, dy, wc, dx, ws, ws_elems, 0, 0, bn, ba, bn_done, st);
+    // (the input block's sums, bn->code, are taken in the pair's finish only)
+    const BnBwdFuse* bsep = bn && bn->code ? nullptr : bn;
+    const int r = conv_dgrad_impl(g, dy, wc, dx, ws, ws_elems, 0, 0, bsep, bsep ? ba : nullptr,
+                                  bn_done, st);
     if (r) return r;
     g_sgd_allow = true;
     const int rw = ddp_conv_wgrad(g, dy, x, dw, ws, ws_elems, 0, st);
@@ -2747,9 +2767,16 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
   if (dneed + wneed > ws_elems) return separate();
   if (g_pair_mode == 3 && !both64 && itd + itw > g_pair_items) return separate();
   if (d.d2x2 && d.has_bnf && d.splits < 2) return separate();
+  // the input block's sums (bn->code) exist only in the split-K finish: without one, or if the
+  // pair would fuse the BN backward into that finish, drop them (the caller runs l0_sums)
+  if (bn && bn->code && (!needs_finish(MODE_DGRAD, d) || ba || d.d2x2)) {
+    d.has_bnf = 0;
+    bn = nullptr;
+  }
   // unsplit WGRAD half: SGD on the master in its epilogue (no finish would take it)
   if (!needs_finish(MODE_WGRAD, w) && w.g.wkrsc && w.g.Creal == w.g.C) w.sgd = sgd_fuse_master(dw);
   const bool bnf1 = d.has_bnf && d.splits <= 1;
+  const bool l0_sums = d.has_bnf && d.bnf.code != nullptr;  // (a finish exists: checked above)
   if (bnf1) {
     hipLaunchKernelGGL((conv_bwd_pair_kernel<64, 64, 3, 1>), dim3(itd + itw), dim3(256), 0, st,
                        d, w, itd);
@@ -2780,6 +2807,7 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
     launch_finish<MODE_DGRAD>(dv, st);
     launch_finish<MODE_WGRAD>(w, st);
   }
+  if (l0_sums && bn_done) *bn_done = 2;
   return (int)hipGetLastError();
 }
 

@@ -521,7 +521,8 @@ extern "C" int ddp_l0_bwd(const ConvGeom* g, const L0Io* io, hipStream_t st) {
   const unsigned nb = l0::grid_for(a.tiles);
   const int windows = g->N * (g->H / 2) * (g->W / 2);
   const unsigned ns = (unsigned)std::max(1, std::min(512, (windows + 127) / 128));
-  hipLaunchKernelGGL(l0::l0_sums_kernel, dim3(ns), dim3(256), 0, st, a, windows);
+  if (!io->sums_ready)  // (else taken by the next block's dgrad finish, BnBwdFuse::code)
+    hipLaunchKernelGGL(l0::l0_sums_kernel, dim3(ns), dim3(256), 0, st, a, windows);
   hipLaunchKernelGGL(l0::l0_bwd_kernel<1>, dim3(nb), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }

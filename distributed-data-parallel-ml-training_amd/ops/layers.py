@@ -306,14 +306,16 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=Non
                                       ptr(ws), ws.numel(), s, bn=bnf, bna=bna)
         if weight is not None:
             grad_ready([weight])
-        return (dx, bool(done)) if bna is not None else dx
+        if bnf is not None and len(bnf) > 7:  # input block's sums: 2 = taken in the finish
+            return dx, int(done) == 2
+        return (dx, int(done) == 1) if bna is not None else dx
     # final: no dgrad of this layer follows, so its finish may apply a registered SGD step
     native().conv_wgrad(g, ptr(dz), ptr(x), ptr(dweight), ptr(ws), ws.numel(), 0, s,
                         final=int(not need_dx))
     if weight is not None:
         grad_ready([weight])
     if not need_dx:
-        return (None, False) if bna is not None else None
+        return (None, False) if (bna is not None or (bnf is not None and len(bnf) > 7)) else None
     if spec.C != spec.Cr:
         raise RuntimeError("dgrad requested for a channel-padded input layer")
     if link is not None and link.deferred is not None and spec.stride == 1:
@@ -337,12 +339,15 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=Non
         link.seen += 1
         return link.result()
     dx = torch.empty_like(x)
+    l0_mode = bnf is not None and len(bnf) > 7  # (input block's sums: pair launch only)
     done = native().conv_dgrad(g, ptr(dz), ptr(spec.wc), ptr(dx), ptr(ws), ws.numel(), 0, s,
-                               bn=bnf, bna=bna)
+                               bn=None if l0_mode else bnf, bna=bna)
     if link is not None:
         link.seen += 1
         link.buf = dx
         return link.result()
+    if l0_mode:
+        return dx, False
     return (dx, bool(done)) if bna is not None else dx
 
 
@@ -351,6 +356,9 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=Non
 # input in every pass that needs it instead of being stored and streamed four times.
 # DDP_AMD_L0_FUSE=0 restores conv_smallk + bn_act passes.
 L0_FUSE = os.environ.get("DDP_AMD_L0_FUSE", "1") != "0"
+# ... and its BN-backward sums taken in the next block's dgrad split-K finish when that dgrad has
+# one (conv_igemm.hip BnBwdFuse::code; else l0_sums_kernel). =0: always the separate pass
+L0_SUMS_IN_FINISH = os.environ.get("DDP_AMD_L0_SUMS_IN_FINISH", "1") != "0"
 
 
 def l0_serves(spec, x):
@@ -428,6 +436,8 @@ class _ConvBNActFn(torch.autograd.Function):
                             int(spec.relu), ptr(stats), ptr(gamma), ptr(beta), ptr(spec.coef),
                             ptr(y), ptr(code), ptr(zw), stream_handle())
             ctx.l0_code = (code, zw)
+            spec.l0_code = (code, zw)  # (the next block's dgrad finish may take the sums)
+            spec.l0_sums_ready = False
             spec.fwd_z = None
             spec.last_deferred = False
             ctx.pool3_idx = None
@@ -494,11 +504,13 @@ class _ConvBNActFn(torch.autograd.Function):
             if bias is not None:
                 ensure_grad(bias)  # analytically zero under batch-statistics BN (bn_act.hip)
             dz = torch.empty(N, H, W, spec.K, dtype=BF16, device=x.device)
+            ready, spec.l0_sums_ready = getattr(spec, "l0_sums_ready", False), False
             native().l0_bwd(spec.geom(N, H, W), ptr(x), ptr(spec.wc), ptr(bias), spec.eps,
                             int(spec.relu), ptr(spec.coef), ptr(dy), ptr(spec.sums), ptr(dz),
                             ptr(gg), ptr(gbt), ptr(ctx.l0_code[0]), ptr(ctx.l0_code[1]),
-                            stream_handle())
+                            stream_handle(), sums_ready=int(ready))
             ctx.l0_code = None
+            spec.l0_code = None
             grad_ready([gamma, beta, bias])
             dx = conv_backward(spec, x, dz, gw, ctx.needs_input_grad[0], ctx.in_link,
                                weight=weight)
@@ -561,7 +573,18 @@ class _ConvBNActFn(torch.autograd.Function):
                 dz_prev = torch.empty_like(pz)
                 bna = (ptr(dz_prev), ptr(ensure_grad(prev.bn.weight)),
                        ptr(ensure_grad(prev.bn.bias)))
-        if bna is not None:
+        l0c = getattr(prev, "l0_code", None) if prev is not None else None
+        if (bnf is None and L0_SUMS_IN_FINISH and l0c is not None and ctx.needs_input_grad[0]
+                and ctx.in_link is None and spec.stride == 1 and prev.K == spec.C
+                and spec.C == spec.Cr and x.shape[1] * 2 == prev._out_p):
+            # the input block's BN-backward sums in this dgrad's split-K finish (conv_l0.hip's
+            # recorded window codes + winner z): its backward skips l0_sums_kernel
+            code, zw = l0c
+            bl0 = (ptr(zw), ptr(prev.coef), ptr(prev.sums), 1, int(prev.relu), x.shape[1],
+                   x.shape[2], ptr(code))
+            dx, taken = conv_backward(spec, x, dz, gw, True, None, weight=weight, bnf=bl0)
+            prev.l0_sums_ready = bool(taken)
+        elif bna is not None:
             dx, done = conv_backward(spec, x, dz, gw, ctx.needs_input_grad[0], ctx.in_link,
                                      weight=weight, bnf=bnf, bna=bna)
             if done:  # prev's backward skips its BN backward; dx was not written

@@ -207,6 +207,54 @@ def test_fused_eval_metrics_match(native_ext):
     assert abs(int(hits) - cb) <= 1  # a near-tie may round differently
 
 
+@pytest.mark.parametrize("batch", [32, 64])
+def test_l0_sums_in_finish_match_separate_pass(native_ext, batch):
+    """The VGG input block's BN-backward sums taken in the next block's dgrad split-K finish
+    (ops.layers.L0_SUMS_IN_FINISH, conv_igemm.hip BnBwdFuse::code) give the gradients of the
+    separate l0_sums pass, within the run-to-run noise of two separate-pass runs; and at 32
+    images the finish path is actually taken (the input block then skips l0_sums)."""
+    from ddp_amd.models import VGG11
+    from ddp_amd.engine import CrossEntropyLoss
+    from ddp_amd.optim import FusedSGD
+    from ddp_amd.ops import layers
+    torch.manual_seed(1)
+    a = VGG11().cuda()
+    b, c = copy.deepcopy(a), copy.deepcopy(a)
+    x = torch.randn(batch, 3, 32, 32, device="cuda")
+    y = torch.randint(0, 10, (batch,), device="cuda")
+    grads, taken = [], []
+    saved = layers.L0_SUMS_IN_FINISH
+    orig = native_ext.l0_bwd
+
+    def spy(*args, **kw):
+        taken.append(int(kw.get("sums_ready", 0)))
+        return orig(*args, **kw)
+    try:
+        for m, on in ((a, True), (b, False), (c, False)):
+            layers.L0_SUMS_IN_FINISH = on
+            native_ext.l0_bwd = spy
+            opt = FusedSGD(m.parameters(), lr=0.1)
+            opt.zero_grad()
+            CrossEntropyLoss()(m(x), y).backward()
+            torch.cuda.synchronize()
+            grads.append([p.grad.clone() for p in m.parameters()])
+    finally:
+        layers.L0_SUMS_IN_FINISH = saved
+        native_ext.l0_bwd = orig
+    assert taken[1:] == [0, 0]
+    if batch == 32:
+        assert taken[0] == 1, "the conv1 pair's dgrad finish should take the input block's sums"
+
+    def cos(u, v):
+        return float(torch.dot(u.reshape(-1), v.reshape(-1)) / (u.norm() * v.norm() + 1e-20))
+
+    for (n, _), ga, gb, gc in zip(a.named_parameters(), *grads):
+        if float(gb.norm()) < 1e-6:
+            continue
+        base = cos(gb, gc)
+        assert cos(ga, gb) > min(0.98, base - 0.05), (n, cos(ga, gb), base)
+
+
 @pytest.mark.parametrize("batch,max_hw", [(64, 16), (256, 64), (32, 256)])
 def test_bn_backward_fused_sums_match_reduce_kernel(native_ext, batch, max_hw):
     """BatchNorm-backward sums accumulated by the next layer's dgrad epilogue / split-K finish
