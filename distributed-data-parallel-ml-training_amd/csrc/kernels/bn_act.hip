@@ -136,13 +136,15 @@ __device__ __forceinline__ void fold_fwd_coeffs(const BnArgs& a, float* l_sc, fl
 // One thread = IPT items (output pixels) x 8 channels; every load is issued up front. A grid
 // smaller than the item blocks walks them with a grid stride (the capped FOLD launch: the
 // replica reduction of fold_fwd_coeffs is paid once per block, not once per 256 x IPT items).
-template <bool POOL, int IPT, bool FOLD>
+// GS: grid-stride launch (a capped FOLD grid); MASK: also store the ReLU mask bits (residual
+// blocks, BnArgs::mask). Both are template switches so the common launches keep their code.
+template <bool POOL, int IPT, bool FOLD, bool GS = false, bool MASK = false>
 __global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnArgs a) {
   constexpr int NP = POOL ? 4 : 1;
   const int G = a.C / 8;
   const int Ho = POOL ? a.H / 2 : a.H, Wo = POOL ? a.W / 2 : a.W;
   const size_t total = (size_t)a.N * Ho * Wo * G;
-  const size_t nbt = (total + 256 * IPT - 1) / (256 * IPT);
+  const size_t nbt = GS ? (total + 256 * IPT - 1) / (256 * IPT) : (size_t)blockIdx.x + 1;
   bool folded = false;
   for (size_t blk = blockIdx.x; blk < nbt; blk += gridDim.x) {
   u16x8 zv[IPT][NP], rv[IPT][POOL ? 1 : NP];
@@ -202,7 +204,7 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnArgs a) {
       for (int e = 0; e < 8; ++e) {
         float y = bf2f(zv[it][d][e]) * sc[it][e] + sh[it][e];
         if (!POOL && a.res) y += bf2f(rv[it][POOL ? 0 : d][e]);
-        if (!POOL) mb |= (y > 0.f ? 1u : 0u) << e;  // the backward's ReLU rule (NaN -> 0)
+        if (MASK) mb |= (y > 0.f ? 1u : 0u) << e;  // the backward's ReLU rule (NaN -> 0)
         if (a.relu) y = fmaxf(y, 0.f);
         if (!POOL || y > best[e] || y != y) best[e] = y;
       }
@@ -211,7 +213,7 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnArgs a) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = f2bf(best[e]);
     st8(a.out + pix * a.C + cg * 8, o);
-    if (!POOL && a.mask) a.mask[t] = (unsigned char)mb;  // t = pixel * G + cg
+    if (MASK) a.mask[t] = (unsigned char)mb;  // t = pixel * G + cg
   }
   }
 }
@@ -230,7 +232,7 @@ struct BwdItems {
   bool ok[IPT];
 };
 
-template <bool POOL, int IPT>
+template <bool POOL, int IPT, bool MASK = false>
 __device__ __forceinline__ void bwd_load(const BnArgs& a, BwdItems<POOL, IPT>& L, size_t p0,
                                          size_t pstride, size_t npix, int cg, int Ho, int Wo) {
   constexpr int NP = POOL ? 4 : 1;
@@ -250,14 +252,14 @@ __device__ __forceinline__ void bwd_load(const BnArgs& a, BwdItems<POOL, IPT>& L
       const size_t off = (((size_t)n * a.H + h) * a.W + w) * a.C + cg * 8;
       L.off[it][d] = off;
       L.zv[it][d] = ld8(a.z + off);
-      if (!POOL && a.mask) L.mb[it] = a.mask[off / 8];
+      if (MASK) L.mb[it] = a.mask[off / 8];
       else if (!POOL && a.res) L.rv[it][POOL ? 0 : d] = ld8(a.res + off);
     }
   }
 }
 
 // dy_bn (gradient at the BN output, after ReLU mask and pool routing) and xhat for one item
-template <bool POOL>
+template <bool POOL, bool MASK = false>
 __device__ __forceinline__ void bwd_compute(const BnArgs& a, const u16x8& dv, const u16x8* zv,
                                             const u16x8* rv, unsigned mb, const float* sc,
                                             const float* sh, const float* mu, const float* is,
@@ -273,7 +275,7 @@ __device__ __forceinline__ void bwd_compute(const BnArgs& a, const u16x8& dv, co
     for (int e = 0; e < 8; ++e) {
       const float zf = bf2f(zv[d][e]);
       float y = zf * sc[e] + sh[e];
-      if (!POOL && a.res && !a.mask) y += bf2f(rv[POOL ? 0 : d][e]);
+      if (!POOL && !MASK && a.res) y += bf2f(rv[POOL ? 0 : d][e]);
       xh[d][e] = (zf - mu[e]) * is[e];
       yv[d][e] = y;
       if (POOL) {
@@ -288,7 +290,7 @@ __device__ __forceinline__ void bwd_compute(const BnArgs& a, const u16x8& dv, co
     for (int e = 0; e < 8; ++e) {
       const float g = (!POOL || arg[e] == d) ? bf2f(dv[e]) : 0.f;
       // with the forward's mask byte: the same verdict (bit e = y > 0), residual never read
-      const bool pos = (!POOL && a.mask) ? ((mb >> e) & 1u) != 0 : yv[d][e] > 0.f;
+      const bool pos = MASK ? ((mb >> e) & 1u) != 0 : yv[d][e] > 0.f;
       dyb[d][e] = (a.relu && !pos) ? 0.f : g;
     }
 }
@@ -296,7 +298,8 @@ __device__ __forceinline__ void bwd_compute(const BnArgs& a, const u16x8& dv, co
 // Grid: x = blocks of (256/Gb) x IPT items, y = channel chunks of (at most) 256 groups.
 // Partial sums go to kStatRep replicas of [2][C] (replica = blockIdx.x % kStatRep): the number
 // of atomic adders per address drops 16x (memory-side atomics serialise per address).
-template <bool POOL, int IPT>
+// STRIDE: the capped grid walks the item blocks (launch_bwd); else one item block per block
+template <bool POOL, int IPT, bool MASK = false, bool STRIDE = false>
 __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
   constexpr int NP = POOL ? 4 : 1;
   __shared__ float red[8 * 256];
@@ -320,15 +323,15 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
   // grid-stride over the item blocks (nbx of them): a capped grid adds its partial sums once
   // per block instead of once per 256 x IPT items (launch_bwd's reduce grid)
   const size_t per_blk = (size_t)prows * IPT;
-  const size_t nbx = (npix + per_blk - 1) / per_blk;
+  const size_t nbx = STRIDE ? (npix + per_blk - 1) / per_blk : (size_t)blockIdx.x + 1;
   for (size_t bb = blockIdx.x; bb < nbx; bb += gridDim.x) {
     BwdItems<POOL, IPT> L;
-    bwd_load<POOL, IPT>(a, L, bb * per_blk + prow, prows, npix, cg_base + cgl, Ho, Wo);
+    bwd_load<POOL, IPT, MASK>(a, L, bb * per_blk + prow, prows, npix, cg_base + cgl, Ho, Wo);
 #pragma unroll
     for (int it = 0; it < IPT; ++it) {
       if (!L.ok[it]) continue;
       float xh[NP][8], dyb[NP][8];
-      bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], L.mb[it], sc, sh, mu, is, xh, dyb);
+      bwd_compute<POOL, MASK>(a, L.dv[it], L.zv[it], L.rv[it], L.mb[it], sc, sh, mu, is, xh, dyb);
 #pragma unroll
       for (int d = 0; d < NP; ++d) {
 #pragma unroll
@@ -364,7 +367,7 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
 // order, so k1 / k2 are bit-identical to the separate launch — and hand k1 / k2 over in LDS;
 // blocks x == 0 also add dgamma / dbeta and write the table's k1 / k2 rows. The launcher folds
 // only while the grid's replica re-reads stay small (kFoldBwdBytes).
-template <bool POOL, int IPT, bool FOLD = false>
+template <bool POOL, int IPT, bool FOLD = false, bool MASK = false, bool STRIDE = false>
 __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(BnArgs a) {
   constexpr int NP = POOL ? 4 : 1;
   const int G = a.C / 8;
@@ -379,7 +382,7 @@ __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(BnArgs a) {
   const size_t per_blk = (size_t)prows * IPT;
   const size_t nbx = (npix + per_blk - 1) / per_blk;
   BwdItems<POOL, IPT> L;
-  bwd_load<POOL, IPT>(a, L, (size_t)blockIdx.x * per_blk + prow, prows, npix, cg_base + cgl,
+  bwd_load<POOL, IPT, MASK>(a, L, (size_t)blockIdx.x * per_blk + prow, prows, npix, cg_base + cgl,
                       Ho, Wo);
   float sc[8], sh[8], mu[8], is[8], k1[8], k2[8];
   ld8f(a.coef + kSc * a.C + c0, sc);
@@ -427,7 +430,7 @@ __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(BnArgs a) {
     for (int it = 0; it < IPT; ++it) {
       if (!L.ok[it]) continue;
       float xh[NP][8], dyb[NP][8];
-      bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], L.mb[it], sc, sh, mu, is, xh, dyb);
+      bwd_compute<POOL, MASK>(a, L.dv[it], L.zv[it], L.rv[it], L.mb[it], sc, sh, mu, is, xh, dyb);
 #pragma unroll
       for (int d = 0; d < NP; ++d) {
         u16x8 o, r;
@@ -441,8 +444,8 @@ __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(BnArgs a) {
       }
     }
     bb += gridDim.x;
-    if (!FOLD || bb >= nbx) break;
-    bwd_load<POOL, IPT>(a, L, bb * per_blk + prow, prows, npix, cg_base + cgl, Ho, Wo);
+    if (!STRIDE || bb >= nbx) break;
+    bwd_load<POOL, IPT, MASK>(a, L, bb * per_blk + prow, prows, npix, cg_base + cgl, Ho, Wo);
   }
 }
 
@@ -453,7 +456,7 @@ __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(BnArgs a) {
 // applies from the same registers: the whole BatchNorm backward is ONE launch instead of three
 // dependent ones (reduce, finalize, apply ~ 4.5 us each in the captured b32 step), and dy / z are
 // read once instead of twice.
-template <bool POOL, int IPT, int NT>
+template <bool POOL, int IPT, int NT, bool MASK = false>
 __global__ __launch_bounds__(NT) void bn_act_bwd_local_kernel(BnArgs a) {
   constexpr int NP = POOL ? 4 : 1;
   constexpr int NW = NT / kWave;
@@ -464,7 +467,7 @@ __global__ __launch_bounds__(NT) void bn_act_bwd_local_kernel(BnArgs a) {
   const int Ho = POOL ? a.H / 2 : a.H, Wo = POOL ? a.W / 2 : a.W;
   const size_t npix = (size_t)a.N * Ho * Wo;
   BwdItems<POOL, IPT> L;
-  bwd_load<POOL, IPT>(a, L, threadIdx.x, NT, npix, cg, Ho, Wo);
+  bwd_load<POOL, IPT, MASK>(a, L, threadIdx.x, NT, npix, cg, Ho, Wo);
   float sc[8], sh[8], mu[8], is[8];
   ld8f(a.coef + kSc * a.C + c0, sc);
   ld8f(a.coef + kSh * a.C + c0, sh);
@@ -477,7 +480,7 @@ __global__ __launch_bounds__(NT) void bn_act_bwd_local_kernel(BnArgs a) {
   for (int it = 0; it < IPT; ++it) {
     if (!L.ok[it]) continue;
     float xh[NP][8], dyb[NP][8];
-    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], L.mb[it], sc, sh, mu, is, xh, dyb);
+    bwd_compute<POOL, MASK>(a, L.dv[it], L.zv[it], L.rv[it], L.mb[it], sc, sh, mu, is, xh, dyb);
 #pragma unroll
     for (int d = 0; d < NP; ++d)
 #pragma unroll
@@ -517,7 +520,7 @@ __global__ __launch_bounds__(NT) void bn_act_bwd_local_kernel(BnArgs a) {
   for (int it = 0; it < IPT; ++it) {
     if (!L.ok[it]) continue;
     float xh[NP][8], dyb[NP][8];
-    bwd_compute<POOL>(a, L.dv[it], L.zv[it], L.rv[it], L.mb[it], sc, sh, mu, is, xh, dyb);
+    bwd_compute<POOL, MASK>(a, L.dv[it], L.zv[it], L.rv[it], L.mb[it], sc, sh, mu, is, xh, dyb);
 #pragma unroll
     for (int d = 0; d < NP; ++d) {
       u16x8 o, r;
@@ -748,21 +751,30 @@ static unsigned fold_fwd_grid() {
   return v;
 }
 
-template <bool POOL, int IPT>
-static void launch_fwd(const BnArgs& a, size_t items, hipStream_t st) {
+template <bool POOL, int IPT, bool MASK>
+static void launch_fwd_m(const BnArgs& a, size_t items, hipStream_t st) {
   const unsigned nb = blocks_for(items, 256 * IPT);
   const size_t per_block = (size_t)a.C * 2 * kStatRep * sizeof(float);
   const unsigned cap = std::min(nb, fold_fwd_grid());
   if ((size_t)nb * per_block <= kFoldBytes) {
-    hipLaunchKernelGGL((bn_act_fwd_kernel<POOL, IPT, true>), dim3(nb), dim3(256),
+    hipLaunchKernelGGL((bn_act_fwd_kernel<POOL, IPT, true, false, MASK>), dim3(nb), dim3(256),
                        2 * a.C * sizeof(float), st, a);
   } else if (!kDeterministic && cap >= 1024 && (size_t)cap * per_block <= kFoldGridBytes) {
-    hipLaunchKernelGGL((bn_act_fwd_kernel<POOL, IPT, true>), dim3(cap), dim3(256),
+    hipLaunchKernelGGL((bn_act_fwd_kernel<POOL, IPT, true, true, MASK>), dim3(cap), dim3(256),
                        2 * a.C * sizeof(float), st, a);
   } else {
     hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3(blocks_for(a.C, 256)), dim3(256), 0, st, a);
-    hipLaunchKernelGGL((bn_act_fwd_kernel<POOL, IPT, false>), dim3(nb), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((bn_act_fwd_kernel<POOL, IPT, false, false, MASK>), dim3(nb), dim3(256), 0,
+                       st, a);
   }
+}
+
+template <bool POOL, int IPT>
+static void launch_fwd(const BnArgs& a, size_t items, hipStream_t st) {
+  if constexpr (!POOL) {
+    if (a.mask) return launch_fwd_m<POOL, IPT, true>(a, items, st);
+  }
+  launch_fwd_m<POOL, IPT, false>(a, items, st);
 }
 
 extern "C" int ddp_bn_act_fwd(const BnArgs* args, hipStream_t st) {
@@ -802,8 +814,8 @@ static size_t fold_bwd_bytes() {
 // the ~1.3 TB/s atomic rate, MI355X_MICROARCH.md "Global float atomics").
 static unsigned kReduceGrid = 2048;
 
-template <bool POOL, int IPT>
-static void launch_bwd(const BnArgs& a, size_t npix, int Gb, int chunks, hipStream_t st) {
+template <bool POOL, int IPT, bool MASK>
+static void launch_bwd_m(const BnArgs& a, size_t npix, int Gb, int chunks, hipStream_t st) {
   static const bool init = [] {
     if (const char* e = std::getenv("DDP_AMD_BN_REDUCE_GRID")) kReduceGrid = (unsigned)std::max(0, std::atoi(e));
     return true;
@@ -813,8 +825,14 @@ static void launch_bwd(const BnArgs& a, size_t npix, int Gb, int chunks, hipStre
   // (the deterministic build keeps one replica per block: block ids stay below kStatRep)
   unsigned rx = kReduceGrid ? std::min(bx, std::max(1u, kReduceGrid / (unsigned)chunks)) : bx;
   if (kDeterministic) rx = std::min(rx, std::max(1u, (unsigned)kStatRep / (unsigned)chunks));
-  if (!a.sums_ready)  // (else: accumulated by the next layer's dgrad epilogue, BnBwdFuse)
-    hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<POOL, IPT>), dim3(rx, chunks), dim3(256), 0, st, a);
+  if (!a.sums_ready) {  // (else: accumulated by the next layer's dgrad epilogue, BnBwdFuse)
+    if (rx < bx)
+      hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<POOL, IPT, MASK, true>), dim3(rx, chunks),
+                         dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<POOL, IPT, MASK, false>), dim3(bx, chunks),
+                         dim3(256), 0, st, a);
+  }
   // The finalize stays its own launch: folding it into the apply (every block re-reducing the 16
   // replicas the reduce just wrote with memory-side atomics) measured 3-4x slower applies at
   // batch 256 and +50 us per b32 step; the reduce's last-arriving block doing it measured slower
@@ -825,19 +843,28 @@ static void launch_bwd(const BnArgs& a, size_t npix, int Gb, int chunks, hipStre
   const size_t per_block = (size_t)kStatRep * 2 * (size_t)Gb * 8 * sizeof(float);
   const size_t fold_bytes = (size_t)bx * chunks * per_block;
   if (!kDeterministic && fold_bwd_bytes() > 0 && fold_bytes <= fold_bwd_bytes()) {
-    hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT, true>), dim3(bx, chunks), dim3(256), 0,
-                       st, a);
+    hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT, true, MASK, false>), dim3(bx, chunks),
+                       dim3(256), 0, st, a);
     return;
   }
   const unsigned cx = std::min(bx, fold_fwd_grid() / (unsigned)chunks);
   if (!kDeterministic && fold_bwd_bytes() > 0 && cx * chunks >= 1024 &&
       (size_t)cx * chunks * per_block <= kFoldGridBytes) {
-    hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT, true>), dim3(cx, chunks), dim3(256), 0,
-                       st, a);
+    hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT, true, MASK, true>), dim3(cx, chunks),
+                       dim3(256), 0, st, a);
     return;
   }
   hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3(blocks_for(a.C, 256)), dim3(256), 0, st, a);
-  hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT>), dim3(bx, chunks), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((bn_act_bwd_apply_kernel<POOL, IPT, false, MASK, false>), dim3(bx, chunks),
+                     dim3(256), 0, st, a);
+}
+
+template <bool POOL, int IPT>
+static void launch_bwd(const BnArgs& a, size_t npix, int Gb, int chunks, hipStream_t st) {
+  if constexpr (!POOL) {
+    if (a.mask) return launch_bwd_m<POOL, IPT, true>(a, npix, Gb, chunks, st);
+  }
+  launch_bwd_m<POOL, IPT, false>(a, npix, Gb, chunks, st);
 }
 
 // One-block-per-channel-group backward (bn_act_bwd_local_kernel): items per thread for npix
@@ -871,13 +898,21 @@ static bool local_cfg(const BnArgs& a, int* ipt) {
   return false;
 }
 
+template <bool POOL, bool MASK>
+static void launch_local_m(const BnArgs& a, int ipt, hipStream_t st) {
+  const dim3 grid(a.C / 8), block(kLocalThreads);
+  if (ipt == 1) hipLaunchKernelGGL((bn_act_bwd_local_kernel<POOL, 1, kLocalThreads, MASK>), grid, block, 0, st, a);
+  else if (ipt == 2) hipLaunchKernelGGL((bn_act_bwd_local_kernel<POOL, 2, kLocalThreads, MASK>), grid, block, 0, st, a);
+  else if (ipt == 4) hipLaunchKernelGGL((bn_act_bwd_local_kernel<POOL, 4, kLocalThreads, MASK>), grid, block, 0, st, a);
+  else if constexpr (!POOL) hipLaunchKernelGGL((bn_act_bwd_local_kernel<POOL, 8, kLocalThreads, MASK>), grid, block, 0, st, a);
+}
+
 template <bool POOL>
 static void launch_local(const BnArgs& a, int ipt, hipStream_t st) {
-  const dim3 grid(a.C / 8), block(kLocalThreads);
-  if (ipt == 1) hipLaunchKernelGGL((bn_act_bwd_local_kernel<POOL, 1, kLocalThreads>), grid, block, 0, st, a);
-  else if (ipt == 2) hipLaunchKernelGGL((bn_act_bwd_local_kernel<POOL, 2, kLocalThreads>), grid, block, 0, st, a);
-  else if (ipt == 4) hipLaunchKernelGGL((bn_act_bwd_local_kernel<POOL, 4, kLocalThreads>), grid, block, 0, st, a);
-  else if constexpr (!POOL) hipLaunchKernelGGL((bn_act_bwd_local_kernel<POOL, 8, kLocalThreads>), grid, block, 0, st, a);
+  if constexpr (!POOL) {
+    if (a.mask) return launch_local_m<POOL, true>(a, ipt, st);
+  }
+  launch_local_m<POOL, false>(a, ipt, st);
 }
 
 // tests / sweeps: the loads-per-thread limit of the one-launch backward (0 = off)

@@ -267,7 +267,7 @@ struct ConvSmem {
 // The GEMM body. ``bid`` / ``nblk`` stand for blockIdx.x / gridDim.x, so a grouped launch
 // (conv_bwd_pair_kernel: the DGRAD and WGRAD GEMMs of one layer in ONE launch) can hand each
 // problem its own block range. ``smem`` = the launching kernel's single LDS array.
-template <int MODE, int BM, int BN, int NST, int BNF = 0>
+template <int MODE, int BM, int BN, int NST, int BNF = 0, bool XSTAT = false>
 __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned short* smem,
                                                 const int bid, const int nblk) {
   constexpr int BK = 64;
@@ -604,28 +604,30 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
   // replicas once per run of such items: with a capped grid (launch_gemm_t, kFwdStatGrid) a
   // block adds one partial sum per channel instead of one per tile — ResNet-50's 64->256 56x56
   // convs otherwise add 12544 x 2 KB = 26 MB of memory-side float atomics each.
+  // (XSTAT only: the kernel instantiation of the capped-grid launches, launch_gemm_t — the
+  // one-item-per-block launches keep per-item sums and no live running registers)
   constexpr int SCPR = BN / 8;  // the staged epilogue's 16-B chunks per tile row
-  float run_s[8], run_ss[8];
+  float run_s[XSTAT ? 8 : 1], run_ss[XSTAT ? 8 : 1];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) { run_s[e] = 0.f; run_ss[e] = 0.f; }
+  for (int e = 0; e < (XSTAT ? 8 : 1); ++e) { run_s[e] = 0.f; run_ss[e] = 0.f; }
   int run_col = -1;  // column tile the running sums belong to (uniform), -1: none
-  auto flush_stats = [&](const int c0) {
+  auto flush_stats = [&](const int c0, float (&fs)[8], float (&fss)[8]) {
     // lanes l, l + CPR, ... of a wave share the chunk column: butterfly over them, then the four
     // waves meet in LDS (after every wave is done with the operand ring / the staged tile)
 #pragma unroll
     for (int m = SCPR; m < 64; m *= 2)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        run_s[e] += __shfl_xor(run_s[e], m);
-        run_ss[e] += __shfl_xor(run_ss[e], m);
+        fs[e] += __shfl_xor(fs[e], m);
+        fss[e] += __shfl_xor(fss[e], m);
       }
     __syncthreads();
     float* sl = reinterpret_cast<float*>(smem);  // [wave][2][BN]
     if (lane < SCPR) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        sl[(wid * 2 + 0) * BN + lane * 8 + e] = run_s[e];
-        sl[(wid * 2 + 1) * BN + lane * 8 + e] = run_ss[e];
+        sl[(wid * 2 + 0) * BN + lane * 8 + e] = fs[e];
+        sl[(wid * 2 + 1) * BN + lane * 8 + e] = fss[e];
       }
     }
     __syncthreads();
@@ -638,7 +640,7 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
       atomicAdd(st + which * args.Ng + c0 + cl, stat_val(t, bid));
     }
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { run_s[e] = 0.f; run_ss[e] = 0.f; }
+    for (int e = 0; e < 8; ++e) { fs[e] = 0.f; fss[e] = 0.f; }
   };
 
   // acc[i][j][v] = D[row0 + wm*WTM + i*16 + (lane&15)][col0 + wn*WTN + j*16 + 4*(lane>>4) + v]
@@ -675,9 +677,15 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
     const bool cok = col < args.Ng;
     float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (MODE == MODE_FWD && args.bias && cok) ld8f_conv(args.bias + col, bv);
-    if (MODE == MODE_FWD && red && run_col != col0) {  // a new column tile: settle the last one
-      if (run_col >= 0) flush_stats(run_col);
-      run_col = col0;
+    float s[8], ss[8];  // this item's sums (XSTAT: the running sums instead)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { s[e] = 0.f; ss[e] = 0.f; }
+    if constexpr (XSTAT) {
+      if (MODE == MODE_FWD && red && run_col != col0) {  // a new column tile: settle the last one
+        if (run_col >= 0) flush_stats(run_col, *reinterpret_cast<float(*)[8]>(run_s),
+                                      *reinterpret_cast<float(*)[8]>(run_ss));
+        run_col = col0;
+      }
     }
 #pragma unroll 1
     for (int h = 0; h < 2; ++h) {
@@ -724,13 +732,20 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             const float rv = bf2f(o[e]);
-            run_s[e] += rv;
-            run_ss[e] += rv * rv;
+            if constexpr (XSTAT) {
+              run_s[e] += rv;
+              run_ss[e] += rv * rv;
+            } else {
+              s[e] += rv;
+              ss[e] += rv * rv;
+            }
           }
         }
       }
     }
-    return;  // (the running statistics are added by the next column tile or after the last item)
+    // (XSTAT: the running sums are added by the next column tile or after the last item)
+    if (!XSTAT && MODE == MODE_FWD && red) flush_stats(col0, s, ss);
+    return;
   }
   // the LDS operand ring is reused for the statistics hand-off: every wave must be done with it
   if (red) __syncthreads();
@@ -1043,7 +1058,11 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
     // the workgroup slot (and its registers) for a full memory round trip after the last MFMA
     if (item + nblk < nitems) wait_dma_barrier<0>();
   }
-  if (MODE == MODE_FWD && run_col >= 0) flush_stats(run_col);  // (uniform: run_col is)
+  if constexpr (XSTAT) {
+    if (MODE == MODE_FWD && run_col >= 0)  // (uniform: run_col is)
+      flush_stats(run_col, *reinterpret_cast<float(*)[8]>(run_s),
+                  *reinterpret_cast<float(*)[8]>(run_ss));
+  }
 }
 
 // 2 waves per SIMD (<= 256 VGPR + AGPR per lane): left to itself the compiler gives the big
@@ -1052,12 +1071,12 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
 #ifndef DDP_CONV_WAVES_PER_EU
 #define DDP_CONV_WAVES_PER_EU 2
 #endif
-template <int MODE, int BM, int BN, int NST, int BNF = 0>
+template <int MODE, int BM, int BN, int NST, int BNF = 0, bool XSTAT = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DDP_CONV_WAVES_PER_EU)))
 void conv_igemm_kernel(ConvArgs args) {
   // dynamic: the launcher sizes the ring to the stages a work item can use (launch_gemm_t)
   extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
-  conv_igemm_body<MODE, BM, BN, NST, BNF>(args, smem, blockIdx.x, gridDim.x);
+  conv_igemm_body<MODE, BM, BN, NST, BNF, XSTAT>(args, smem, blockIdx.x, gridDim.x);
 }
 
 // BNF 2 (no-pool BN-backward sums in the lean epilogue): the extra per-column coefficients push
@@ -1894,26 +1913,31 @@ static void launch_gemm_t(const ConvArgs& a, int items, hipStream_t st) {
   const int stages = std::max(1, std::min(NST, a.ksteps_per_split));
   size_t lds = (size_t)stages * kStageBytes;
   if (a.epi_stage && lds < (size_t)kTileBytes) lds = kTileBytes;
+  // FWD GEMMs with statistics over many items: a capped grid whose blocks walk the items and
+  // keep running statistics (the XSTAT instantiation, conv_igemm_body)
+  int grid = items;
+  if (MODE == MODE_FWD && a.stats && a.splits <= 1 && a.epi_stage && !(BM == 64 && BN == 64) &&
+      fwd_stat_grid() > 0 && items > fwd_stat_grid())
+    grid = fwd_stat_grid();
   void (*kern)(ConvArgs);
   if constexpr (BNF == 2 && MODE == MODE_DGRAD) kern = conv_igemm_bnf2_kernel<MODE, BM, BN, NST>;
+  else if constexpr (MODE == MODE_FWD && BNF == 0 && !(BM == 64 && BN == 64))
+    kern = grid < items ? conv_igemm_kernel<MODE, BM, BN, NST, 0, true>
+                        : conv_igemm_kernel<MODE, BM, BN, NST, 0, false>;
   else kern = conv_igemm_kernel<MODE, BM, BN, NST, BNF>;
-  static bool attr = false;
-  if (!attr) {
+  static bool attr[2] = {false, false};
+  if (!attr[grid < items]) {
     // an error here surfaces through the caller's hipGetLastError
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize,
                               std::max(NST * kStageBytes, kTileBytes));
-    attr = true;
+    attr[grid < items] = true;
   }
   // one work item (tile x split) per workgroup (a persistent grid sized to the resident slots
   // was measured no faster and removed in round 5) — except FWD GEMMs whose LDS-staged
   // epilogue reduces the BatchNorm statistics: a grid of kFwdStatGrid blocks (a multiple of 8,
   // so item % 8 keeps naming the block's XCD for xcd_remap) walks the items and adds each
   // column tile's partial sums once per block (the running sums of conv_igemm_body)
-  int grid = items;
-  if (MODE == MODE_FWD && a.stats && a.splits <= 1 && a.epi_stage && !(BM == 64 && BN == 64) &&
-      fwd_stat_grid() > 0 && items > fwd_stat_grid())
-    grid = fwd_stat_grid();
   hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, a);
 }
 
