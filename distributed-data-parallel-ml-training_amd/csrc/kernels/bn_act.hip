@@ -173,7 +173,7 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnArgs a) {
   }
   if (FOLD) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    if (!folded) {  // (uniform: the first walked item block of every block)
+    if (!GS || !folded) {  // (uniform: the first walked item block of every block)
       fold_fwd_coeffs(a, lds, lds + a.C);
       folded = true;
     }
@@ -215,6 +215,7 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnArgs a) {
     st8(a.out + pix * a.C + cg * 8, o);
     if (MASK) a.mask[t] = (unsigned char)mb;  // t = pixel * G + cg
   }
+  if (!GS) break;  // (one item block per block)
   }
 }
 
@@ -312,6 +313,14 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
   const int cgl = threadIdx.x % Gb;
   const int prow = threadIdx.x / Gb, prows = 256 / Gb;
   const int c0 = (cg_base + cgl) * 8;
+  // grid-stride over the item blocks (nbx of them): a capped grid adds its partial sums once
+  // per block instead of once per 256 x IPT items (launch_bwd's reduce grid). The items of the
+  // first block are loaded before the coefficients (the one-block-per-item launch's order).
+  const size_t per_blk = (size_t)prows * IPT;
+  const size_t nbx = STRIDE ? (npix + per_blk - 1) / per_blk : (size_t)blockIdx.x + 1;
+  BwdItems<POOL, IPT> L;
+  bwd_load<POOL, IPT, MASK>(a, L, (size_t)blockIdx.x * per_blk + prow, prows, npix,
+                            cg_base + cgl, Ho, Wo);
   float sc[8], sh[8], mu[8], is[8];
   ld8f(a.coef + kSc * a.C + c0, sc);
   ld8f(a.coef + kSh * a.C + c0, sh);
@@ -320,13 +329,7 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
   float acc[2][8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { acc[0][e] = 0.f; acc[1][e] = 0.f; }
-  // grid-stride over the item blocks (nbx of them): a capped grid adds its partial sums once
-  // per block instead of once per 256 x IPT items (launch_bwd's reduce grid)
-  const size_t per_blk = (size_t)prows * IPT;
-  const size_t nbx = STRIDE ? (npix + per_blk - 1) / per_blk : (size_t)blockIdx.x + 1;
-  for (size_t bb = blockIdx.x; bb < nbx; bb += gridDim.x) {
-    BwdItems<POOL, IPT> L;
-    bwd_load<POOL, IPT, MASK>(a, L, bb * per_blk + prow, prows, npix, cg_base + cgl, Ho, Wo);
+  for (size_t bb = blockIdx.x;;) {
 #pragma unroll
     for (int it = 0; it < IPT; ++it) {
       if (!L.ok[it]) continue;
@@ -341,6 +344,9 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
         }
       }
     }
+    bb += gridDim.x;
+    if (!STRIDE || bb >= nbx) break;
+    bwd_load<POOL, IPT, MASK>(a, L, bb * per_blk + prow, prows, npix, cg_base + cgl, Ho, Wo);
   }
   // block reduction over the 256/Gb threads sharing each channel group, then one atomic per
   // channel per block into this block's replica
