@@ -267,7 +267,9 @@ struct ConvSmem {
 // The GEMM body. ``bid`` / ``nblk`` stand for blockIdx.x / gridDim.x, so a grouped launch
 // (conv_bwd_pair_kernel: the DGRAD and WGRAD GEMMs of one layer in ONE launch) can hand each
 // problem its own block range. ``smem`` = the launching kernel's single LDS array.
-template <int MODE, int BM, int BN, int NST, int BNF = 0, bool XSTAT = false>
+// SGDM (WGRAD, backward pair only): the unsplit epilogue applies SGD to the master
+// (ConvArgs::sgd) — a template switch so the other WGRAD launches keep their code
+template <int MODE, int BM, int BN, int NST, int BNF = 0, bool XSTAT = false, bool SGDM = false>
 __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned short* smem,
                                                 const int bid, const int nblk) {
   constexpr int BK = 64;
@@ -891,7 +893,7 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
       if (!cok || row >= args.Mg) continue;
       const f32x4 v = acc[i][j];
       if (MODE == MODE_WGRAD && !split) {
-        if (g.wkrsc && g.Creal == g.C && args.sgd.p) {  // master-only SGD (see ConvArgs::sgd)
+        if (SGDM && g.wkrsc && g.Creal == g.C && args.sgd.p) {  // master-only SGD (ConvArgs::sgd)
           const size_t e = ((size_t)row * g.R * g.S + wrs) * g.C + wc;
           float4 pv = *reinterpret_cast<const float4*>(args.sgd.p + e);
           float4 bv = *reinterpret_cast<const float4*>(args.sgd.buf + e);
@@ -1092,13 +1094,14 @@ void conv_igemm_bnf2_kernel(ConvArgs args) {
 // the WGRAD problem (independent outputs, both read dy). At the strong-scaling batches each of
 // them alone leaves most of the 256 CUs idle and pays its own latency floor; side by side they
 // fill each other's idle slots and cost one dispatch. Same tile config for both (one LDS array).
-template <int BM, int BN, int NST, int BNF>
+template <int BM, int BN, int NST, int BNF, bool SGDM = false>
 __global__ __launch_bounds__(256) void conv_bwd_pair_kernel(ConvArgs dg, ConvArgs wg, int n_dg) {
   __shared__ __attribute__((aligned(16))) unsigned short smem[ConvSmem<BM, BN, NST>::elems];
   if ((int)blockIdx.x < n_dg)
     conv_igemm_body<MODE_DGRAD, BM, BN, NST, BNF>(dg, smem, blockIdx.x, n_dg);
   else
-    conv_igemm_body<MODE_WGRAD, BM, BN, NST, 0>(wg, smem, blockIdx.x - n_dg, gridDim.x - n_dg);
+    conv_igemm_body<MODE_WGRAD, BM, BN, NST, 0, false, SGDM>(wg, smem, blockIdx.x - n_dg,
+                                                           gridDim.x - n_dg);
 }
 // Split-K finish for FWD/DGRAD: sum the slabs in split order -> (+bias) bf16 output
 // (+ per-channel stats of the rounded output for FWD).
@@ -2801,9 +2804,16 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
   if (!needs_finish(MODE_WGRAD, w) && w.g.wkrsc && w.g.Creal == w.g.C) w.sgd = sgd_fuse_master(dw);
   const bool bnf1 = d.has_bnf && d.splits <= 1;
   const bool l0_sums = d.has_bnf && d.bnf.code != nullptr;  // (a finish exists: checked above)
-  if (bnf1) {
+  const bool sgdm = w.sgd.p != nullptr;
+  if (bnf1 && sgdm) {
+    hipLaunchKernelGGL((conv_bwd_pair_kernel<64, 64, 3, 1, true>), dim3(itd + itw), dim3(256), 0,
+                       st, d, w, itd);
+  } else if (bnf1) {
     hipLaunchKernelGGL((conv_bwd_pair_kernel<64, 64, 3, 1>), dim3(itd + itw), dim3(256), 0, st,
                        d, w, itd);
+  } else if (sgdm) {
+    hipLaunchKernelGGL((conv_bwd_pair_kernel<64, 64, 3, 0, true>), dim3(itd + itw), dim3(256), 0,
+                       st, d, w, itd);
   } else {
     hipLaunchKernelGGL((conv_bwd_pair_kernel<64, 64, 3, 0>), dim3(itd + itw), dim3(256), 0, st,
                        d, w, itd);
