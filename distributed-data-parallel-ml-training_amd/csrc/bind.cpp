@@ -354,7 +354,9 @@ PYBIND11_MODULE(_native, m) {
                          uintptr_t res, uintptr_t stats, uintptr_t gamma, uintptr_t beta,
                          uintptr_t out, uintptr_t st, uintptr_t running_mean,
                          uintptr_t running_var, float momentum, int use_running, uintptr_t coef,
-                         uintptr_t mask) {
+                         uintptr_t mask, uintptr_t rstats, uintptr_t rgamma, uintptr_t rbeta,
+                         uintptr_t rcoef, uintptr_t rrunning_mean, uintptr_t rrunning_var,
+                         float reps, float rmomentum) {
     ddp_amd::BnArgs a{};
     a.coef = P<float>(coef);
     a.mask = P<unsigned char>(mask);
@@ -363,12 +365,24 @@ PYBIND11_MODULE(_native, m) {
     a.gamma = P<float>(gamma); a.beta = P<float>(beta); a.out = P<unsigned short>(out);
     a.running_mean = P<float>(running_mean); a.running_var = P<float>(running_var);
     a.momentum = momentum; a.use_running = use_running;
+    if (rcoef) {  // res = the projection shortcut's pre-BN output, r = its BatchNorm
+      ddp_amd::BnArgs r{};
+      r.C = C; r.eps = reps; r.momentum = rmomentum;
+      r.stats = P<float>(rstats); r.gamma = P<float>(rgamma); r.beta = P<float>(rbeta);
+      r.coef = P<float>(rcoef);
+      r.running_mean = P<float>(rrunning_mean); r.running_var = P<float>(rrunning_var);
+      a.rcoef = r.coef;
+      check(ddp_bn_act_fwd_res(&a, &r, S(st)), "bn_act_fwd (shortcut BN)");
+      return;
+    }
     check(ddp_bn_act_fwd(&a, S(st)), "bn_act_fwd");
   }, py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("pool"), py::arg("relu"),
      py::arg("eps"), py::arg("z"), py::arg("res"), py::arg("stats"), py::arg("gamma"),
      py::arg("beta"), py::arg("out"), py::arg("stream"), py::arg("running_mean") = 0,
      py::arg("running_var") = 0, py::arg("momentum") = 0.1f, py::arg("use_running") = 0,
-     py::arg("coef") = 0, py::arg("mask") = 0);
+     py::arg("coef") = 0, py::arg("mask") = 0, py::arg("rstats") = 0, py::arg("rgamma") = 0,
+     py::arg("rbeta") = 0, py::arg("rcoef") = 0, py::arg("rrunning_mean") = 0,
+     py::arg("rrunning_var") = 0, py::arg("reps") = 1e-5f, py::arg("rmomentum") = 0.1f);
   m.def("maxpool_fwd", [](uintptr_t x, int N, int H, int W, int C, int KH, int KW, int stride,
                           int pad, int Ho, int Wo, uintptr_t y, uintptr_t idx, uintptr_t st) {
     check(ddp_maxpool_fwd(P<void>(x), N, H, W, C, KH, KW, stride, pad, Ho, Wo, P<void>(y),
@@ -392,7 +406,8 @@ PYBIND11_MODULE(_native, m) {
                          uintptr_t res, uintptr_t stats, uintptr_t gamma, uintptr_t beta,
                          uintptr_t dout, uintptr_t sums, uintptr_t dz, uintptr_t dres,
                          uintptr_t dgamma, uintptr_t dbeta, uintptr_t dbias, uintptr_t st,
-                         uintptr_t coef, int sums_ready, uintptr_t mask) {
+                         uintptr_t coef, int sums_ready, uintptr_t mask, uintptr_t rcoef,
+                         uintptr_t rsums, uintptr_t rdz, uintptr_t rdgamma, uintptr_t rdbeta) {
     ddp_amd::BnArgs a{};
     a.coef = P<float>(coef);
     a.sums_ready = sums_ready;
@@ -402,12 +417,19 @@ PYBIND11_MODULE(_native, m) {
     a.gamma = P<float>(gamma); a.beta = P<float>(beta); a.dout = P<unsigned short>(dout);
     a.sums = P<float>(sums); a.dz = P<unsigned short>(dz); a.dres = P<unsigned short>(dres);
     a.dgamma = P<float>(dgamma); a.dbeta = P<float>(dbeta); a.dbias = P<float>(dbias);
+    if (rcoef) {  // res = the projection shortcut's pre-BN output: its dz goes to rdz
+      a.rcoef = P<float>(rcoef); a.rsums = P<float>(rsums); a.rdz = P<unsigned short>(rdz);
+      a.rdgamma = P<float>(rdgamma); a.rdbeta = P<float>(rdbeta);
+      check(ddp_bn_act_bwd_res(&a, S(st)), "bn_act_bwd (shortcut BN)");
+      return;
+    }
     check(ddp_bn_act_bwd(&a, S(st)), "bn_act_bwd");
   }, py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("pool"), py::arg("relu"),
      py::arg("eps"), py::arg("z"), py::arg("res"), py::arg("stats"), py::arg("gamma"),
      py::arg("beta"), py::arg("dout"), py::arg("sums"), py::arg("dz"), py::arg("dres"),
      py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("stream"), py::arg("coef"),
-     py::arg("sums_ready") = 0, py::arg("mask") = 0);
+     py::arg("sums_ready") = 0, py::arg("mask") = 0, py::arg("rcoef") = 0, py::arg("rsums") = 0,
+     py::arg("rdz") = 0, py::arg("rdgamma") = 0, py::arg("rdbeta") = 0);
   // ResNet stem: BN + ReLU + MaxPool2d(3, 2, 1) in one pass each way (bn_act.hip bn_pool3_*):
   // (N, H, W) = conv output, out / dout pooled, idx = uint8 window argmax (pooled shape)
   m.def("bn_pool3_fwd", [](int N, int H, int W, int C, int relu, float eps, uintptr_t z,

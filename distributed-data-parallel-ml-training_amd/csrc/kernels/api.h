@@ -61,6 +61,14 @@ struct BnArgs {
                                 // of a channel group = its pre-ReLU value was > 0. Forward writes
                                 // it; the backward reads it INSTEAD of the residual (1/16 of the
                                 // bytes) — the residual only ever served the ReLU mask there
+  // Projection shortcut folded in (ResNet's downsample Conv -> BN, no ReLU): res is the
+  // shortcut conv's PRE-BatchNorm output and these name its BatchNorm, so the shortcut's BN
+  // output is never stored and its backward rides in this block's passes (ddp_bn_act_*_res)
+  float* rcoef;                 // its coef table [6][C]
+  float* rsums;                 // backward: its S2 row ([kStatRep][2][C]; S1 is this BN's own)
+  unsigned short* rdz;          // backward: grad wrt the shortcut conv output
+  float* rdgamma;               // its grad arena slices (accumulated)
+  float* rdbeta;
 };
 
 // BatchNorm-backward statistics fused into a conv dgrad: the dgrad output IS the gradient at the
@@ -243,6 +251,11 @@ int ddp_conv_wgrad(const ddp_amd::ConvGeom* g, const void* dy, const void* x, fl
                    float* ws, size_t ws_elems, int splits, hipStream_t st);
 int ddp_bn_act_fwd(const ddp_amd::BnArgs* a, hipStream_t st);
 int ddp_bn_act_bwd(const ddp_amd::BnArgs* a, hipStream_t st);
+// residual block with the projection shortcut's BatchNorm folded in (BnArgs::rcoef ..): forward
+// y = relu(bn(z) + bn_r(res)), r = the shortcut BN (its stats / gamma / beta / running buffers /
+// coef; the rest of r is ignored); backward writes dz and rdz from one reduce + finalize + apply
+int ddp_bn_act_fwd_res(const ddp_amd::BnArgs* a, const ddp_amd::BnArgs* r, hipStream_t st);
+int ddp_bn_act_bwd_res(const ddp_amd::BnArgs* a, hipStream_t st);
 // small layers: the whole BatchNorm backward in one launch, one block per 8 channels
 // (bn_act_bwd_local_kernel); ok = this layer takes that path; set = its loads-per-thread
 // limit (0 = off)

@@ -46,9 +46,7 @@ __device__ __forceinline__ void ld8f(const float* p, float* v) {
 }
 
 // ------------------------------- finalize kernels -------------------------------
-__global__ __launch_bounds__(256) void bn_finalize_fwd_kernel(BnArgs a) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= a.C) return;
+__device__ __forceinline__ void finalize_fwd_ch(const BnArgs& a, int c) {
   float mu, is;
   if (a.use_running) {  // eval mode of track_running_stats=True BatchNorm
     mu = a.running_mean[c];
@@ -77,6 +75,18 @@ __global__ __launch_bounds__(256) void bn_finalize_fwd_kernel(BnArgs a) {
   a.coef[kIs * a.C + c] = is;
 }
 
+__global__ __launch_bounds__(256) void bn_finalize_fwd_kernel(BnArgs a) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < a.C) finalize_fwd_ch(a, c);
+}
+
+// residual block + projection shortcut: both tables in one launch (y = 0: the block's own BN,
+// y = 1: the shortcut's)
+__global__ __launch_bounds__(256) void bn_finalize_fwd2_kernel(BnArgs a, BnArgs r) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < a.C) finalize_fwd_ch(blockIdx.y ? r : a, c);
+}
+
 __global__ __launch_bounds__(256) void bn_finalize_bwd_kernel(BnArgs a) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= a.C) return;
@@ -91,6 +101,30 @@ __global__ __launch_bounds__(256) void bn_finalize_bwd_kernel(BnArgs a) {
   a.coef[kK2 * a.C + c] = s2 * inv_m;
   if (a.dgamma) a.dgamma[c] += s2;  // one writer per channel: plain accumulate into the arena
   if (a.dbeta) a.dbeta[c] += s1;
+}
+
+// ... with the projection shortcut's BN: both BatchNorms see the same gradient dy_bn (the block
+// output's gradient through the ReLU mask), so they share S1; the shortcut's S2 (sum dy_bn *
+// its xhat) is the third sum of the reduce, in its own replicas' S2 row
+__global__ __launch_bounds__(256) void bn_finalize_bwd_res_kernel(BnArgs a) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= a.C) return;
+  const float inv_m = 1.f / ((float)a.N * a.H * a.W);
+  float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+  for (int r = 0; r < kStatRep; ++r) {
+    s1 += a.sums[r * 2 * a.C + c];
+    s2 += a.sums[r * 2 * a.C + a.C + c];
+    s3 += a.rsums[r * 2 * a.C + a.C + c];
+  }
+  a.coef[kK1 * a.C + c] = s1 * inv_m;
+  a.coef[kK2 * a.C + c] = s2 * inv_m;
+  a.rcoef[kK1 * a.C + c] = s1 * inv_m;
+  a.rcoef[kK2 * a.C + c] = s3 * inv_m;
+  if (a.dgamma) a.dgamma[c] += s2;
+  if (a.dbeta) a.dbeta[c] += s1;
+  if (a.rdgamma) a.rdgamma[c] += s3;
+  if (a.rdbeta) a.rdbeta[c] += s1;
 }
 
 // Replica reduction + coefficients of ALL channels into LDS (sc | sh), done by every block of a
@@ -138,7 +172,9 @@ __device__ __forceinline__ void fold_fwd_coeffs(const BnArgs& a, float* l_sc, fl
 // replica reduction of fold_fwd_coeffs is paid once per block, not once per 256 x IPT items).
 // GS: grid-stride launch (a capped FOLD grid); MASK: also store the ReLU mask bits (residual
 // blocks, BnArgs::mask). Both are template switches so the common launches keep their code.
-template <bool POOL, int IPT, bool FOLD, bool GS = false, bool MASK = false>
+// RBN: res is the projection shortcut's pre-BN output, normalised here with BnArgs::rcoef (the
+// host guarantees 256 % (C / 8) == 0, so a thread's items share one channel group)
+template <bool POOL, int IPT, bool FOLD, bool GS = false, bool MASK = false, bool RBN = false>
 __global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnArgs a) {
   constexpr int NP = POOL ? 4 : 1;
   const int G = a.C / 8;
@@ -150,6 +186,12 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnArgs a) {
   u16x8 zv[IPT][NP], rv[IPT][POOL ? 1 : NP];
   float sc[IPT][8], sh[IPT][8];
   const size_t t0 = blk * 256 * IPT + threadIdx.x;
+  float rsc[8], rsh[8];
+  if (RBN) {
+    const int cg = (int)((t0 < total ? t0 : 0) % G);
+    ld8f(a.rcoef + kSc * a.C + cg * 8, rsc);
+    ld8f(a.rcoef + kSh * a.C + cg * 8, rsh);
+  }
 #pragma unroll
   for (int it = 0; it < IPT; ++it) {
     const size_t t = t0 + it * 256;
@@ -203,7 +245,8 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(BnArgs a) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         float y = bf2f(zv[it][d][e]) * sc[it][e] + sh[it][e];
-        if (!POOL && a.res) y += bf2f(rv[it][POOL ? 0 : d][e]);
+        if (RBN) y += bf2f(rv[it][POOL ? 0 : d][e]) * rsc[e] + rsh[e];
+        else if (!POOL && a.res) y += bf2f(rv[it][POOL ? 0 : d][e]);
         if (MASK) mb |= (y > 0.f ? 1u : 0u) << e;  // the backward's ReLU rule (NaN -> 0)
         if (a.relu) y = fmaxf(y, 0.f);
         if (!POOL || y > best[e] || y != y) best[e] = y;
@@ -233,7 +276,7 @@ struct BwdItems {
   bool ok[IPT];
 };
 
-template <bool POOL, int IPT, bool MASK = false>
+template <bool POOL, int IPT, bool MASK = false, bool RBN = false>
 __device__ __forceinline__ void bwd_load(const BnArgs& a, BwdItems<POOL, IPT>& L, size_t p0,
                                          size_t pstride, size_t npix, int cg, int Ho, int Wo) {
   constexpr int NP = POOL ? 4 : 1;
@@ -254,7 +297,8 @@ __device__ __forceinline__ void bwd_load(const BnArgs& a, BwdItems<POOL, IPT>& L
       L.off[it][d] = off;
       L.zv[it][d] = ld8(a.z + off);
       if (MASK) L.mb[it] = a.mask[off / 8];
-      else if (!POOL && a.res) L.rv[it][POOL ? 0 : d] = ld8(a.res + off);
+      // (RBN: the shortcut's pre-BN z, for its xhat)
+      if (RBN || (!MASK && !POOL && a.res)) L.rv[it][POOL ? 0 : d] = ld8(a.res + off);
     }
   }
 }
@@ -299,9 +343,12 @@ __device__ __forceinline__ void bwd_compute(const BnArgs& a, const u16x8& dv, co
 // Grid: x = blocks of (256/Gb) x IPT items, y = channel chunks of (at most) 256 groups.
 // Partial sums go to kStatRep replicas of [2][C] (replica = blockIdx.x % kStatRep): the number
 // of atomic adders per address drops 16x (memory-side atomics serialise per address).
-// STRIDE: the capped grid walks the item blocks (launch_bwd); else one item block per block
-template <bool POOL, int IPT, bool MASK = false, bool STRIDE = false>
+// STRIDE: the capped grid walks the item blocks (launch_bwd); else one item block per block.
+// RBN (projection shortcut folded in): a third sum, S2 of the shortcut's BN (sum dy_bn * its
+// xhat), into BnArgs::rsums' S2 row (S1 is shared: both BNs see the same dy_bn)
+template <bool POOL, int IPT, bool MASK = false, bool STRIDE = false, bool RBN = false>
 __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
+  constexpr int NS = RBN ? 3 : 2;
   constexpr int NP = POOL ? 4 : 1;
   __shared__ float red[8 * 256];
   DDP_DEVICE_CHECK(a.C % 8 == 0 && (!POOL || (a.H % 2 == 0 && a.W % 2 == 0)));
@@ -319,16 +366,22 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
   const size_t per_blk = (size_t)prows * IPT;
   const size_t nbx = STRIDE ? (npix + per_blk - 1) / per_blk : (size_t)blockIdx.x + 1;
   BwdItems<POOL, IPT> L;
-  bwd_load<POOL, IPT, MASK>(a, L, (size_t)blockIdx.x * per_blk + prow, prows, npix,
-                            cg_base + cgl, Ho, Wo);
-  float sc[8], sh[8], mu[8], is[8];
+  bwd_load<POOL, IPT, MASK, RBN>(a, L, (size_t)blockIdx.x * per_blk + prow, prows, npix,
+                                 cg_base + cgl, Ho, Wo);
+  float sc[8], sh[8], mu[8], is[8], rmu[8], ris[8];
   ld8f(a.coef + kSc * a.C + c0, sc);
   ld8f(a.coef + kSh * a.C + c0, sh);
   ld8f(a.coef + kMu * a.C + c0, mu);
   ld8f(a.coef + kIs * a.C + c0, is);
-  float acc[2][8];
+  if (RBN) {
+    ld8f(a.rcoef + kMu * a.C + c0, rmu);
+    ld8f(a.rcoef + kIs * a.C + c0, ris);
+  }
+  float acc[NS][8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) { acc[0][e] = 0.f; acc[1][e] = 0.f; }
+  for (int k = 0; k < NS; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[k][e] = 0.f;
   for (size_t bb = blockIdx.x;;) {
 #pragma unroll
     for (int it = 0; it < IPT; ++it) {
@@ -341,28 +394,31 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
         for (int e = 0; e < 8; ++e) {
           acc[0][e] += dyb[d][e];
           acc[1][e] += dyb[d][e] * xh[d][e];
+          if (RBN) acc[NS - 1][e] += dyb[d][e] * ((bf2f(L.rv[it][0][e]) - rmu[e]) * ris[e]);
         }
       }
     }
     bb += gridDim.x;
     if (!STRIDE || bb >= nbx) break;
-    bwd_load<POOL, IPT, MASK>(a, L, bb * per_blk + prow, prows, npix, cg_base + cgl, Ho, Wo);
+    bwd_load<POOL, IPT, MASK, RBN>(a, L, bb * per_blk + prow, prows, npix, cg_base + cgl, Ho, Wo);
   }
   // block reduction over the 256/Gb threads sharing each channel group, then one atomic per
   // channel per block into this block's replica
   float* rep = a.sums + stat_rep(blockIdx.x) * 2 * a.C;
   const int tid = threadIdx.x;
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < NS; ++k) {
     if (k) __syncthreads();
 #pragma unroll
     for (int e = 0; e < 8; ++e) red[e * 256 + tid] = acc[k][e];
     __syncthreads();
+    // (k == 2: the shortcut's S2 row)
+    float* dst = k < 2 ? rep + k * a.C : a.rsums + stat_rep(blockIdx.x) * 2 * a.C + a.C;
     for (int idx = tid; idx < Gb * 8; idx += 256) {
       const int g = idx / 8, e = idx % 8;
       float s = 0.f;
       for (int r = 0; r < prows; ++r) s += red[e * 256 + r * Gb + g];
-      atomicAdd(rep + k * a.C + (cg_base + g) * 8 + e, stat_val(s, blockIdx.x));
+      atomicAdd(dst + (cg_base + g) * 8 + e, stat_val(s, blockIdx.x));
     }
   }
 }
@@ -373,7 +429,9 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
 // order, so k1 / k2 are bit-identical to the separate launch — and hand k1 / k2 over in LDS;
 // blocks x == 0 also add dgamma / dbeta and write the table's k1 / k2 rows. The launcher folds
 // only while the grid's replica re-reads stay small (kFoldBwdBytes).
-template <bool POOL, int IPT, bool FOLD = false, bool MASK = false, bool STRIDE = false>
+// RBN: also the projection shortcut's dz (BnArgs::rdz) from the same dy_bn and its own table.
+template <bool POOL, int IPT, bool FOLD = false, bool MASK = false, bool STRIDE = false,
+          bool RBN = false>
 __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(BnArgs a) {
   constexpr int NP = POOL ? 4 : 1;
   const int G = a.C / 8;
@@ -388,9 +446,15 @@ __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(BnArgs a) {
   const size_t per_blk = (size_t)prows * IPT;
   const size_t nbx = (npix + per_blk - 1) / per_blk;
   BwdItems<POOL, IPT> L;
-  bwd_load<POOL, IPT, MASK>(a, L, (size_t)blockIdx.x * per_blk + prow, prows, npix, cg_base + cgl,
-                      Ho, Wo);
-  float sc[8], sh[8], mu[8], is[8], k1[8], k2[8];
+  bwd_load<POOL, IPT, MASK, RBN>(a, L, (size_t)blockIdx.x * per_blk + prow, prows, npix,
+                                 cg_base + cgl, Ho, Wo);
+  float sc[8], sh[8], mu[8], is[8], k1[8], k2[8], rsc[8], rmu[8], ris[8], rk2[8];
+  if (RBN) {
+    ld8f(a.rcoef + kSc * a.C + c0, rsc);
+    ld8f(a.rcoef + kMu * a.C + c0, rmu);
+    ld8f(a.rcoef + kIs * a.C + c0, ris);
+    ld8f(a.rcoef + kK2 * a.C + c0, rk2);
+  }
   ld8f(a.coef + kSc * a.C + c0, sc);
   ld8f(a.coef + kSh * a.C + c0, sh);
   ld8f(a.coef + kMu * a.C + c0, mu);
@@ -443,15 +507,21 @@ __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(BnArgs a) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           o[e] = f2bf(sc[e] * (dyb[d][e] - k1[e] - xh[d][e] * k2[e]));  // sc = gamma * invstd
-          r[e] = f2bf(dyb[d][e]);
+          if (RBN) {  // the shortcut's BN backward: same dy_bn and k1, its xhat / k2 / scale
+            const float xr = (bf2f(L.rv[it][0][e]) - rmu[e]) * ris[e];
+            r[e] = f2bf(rsc[e] * (dyb[d][e] - k1[e] - xr * rk2[e]));
+          } else {
+            r[e] = f2bf(dyb[d][e]);
+          }
         }
         st8(a.dz + L.off[it][d], o);
-        if (a.dres) st8(a.dres + L.off[it][d], r);
+        if (RBN) st8(a.rdz + L.off[it][d], r);
+        else if (a.dres) st8(a.dres + L.off[it][d], r);
       }
     }
     bb += gridDim.x;
     if (!STRIDE || bb >= nbx) break;
-    bwd_load<POOL, IPT, MASK>(a, L, bb * per_blk + prow, prows, npix, cg_base + cgl, Ho, Wo);
+    bwd_load<POOL, IPT, MASK, RBN>(a, L, bb * per_blk + prow, prows, npix, cg_base + cgl, Ho, Wo);
   }
 }
 
@@ -783,8 +853,40 @@ static void launch_fwd(const BnArgs& a, size_t items, hipStream_t st) {
   launch_fwd_m<POOL, IPT, false>(a, items, st);
 }
 
+// residual block + projection shortcut BN (ddp_bn_act_fwd_res): both finalizes in one launch,
+// then the apply normalising both inputs (never folded: a shortcut block's layers are big)
+template <int IPT>
+static void launch_fwd_res(const BnArgs& a, const BnArgs& r, size_t items, hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_fwd2_kernel, dim3(blocks_for(a.C, 256), 2), dim3(256), 0, st, a, r);
+  const unsigned nb = blocks_for(items, 256 * IPT);
+  if (a.mask)
+    hipLaunchKernelGGL((bn_act_fwd_kernel<false, IPT, false, false, true, true>), dim3(nb),
+                       dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((bn_act_fwd_kernel<false, IPT, false, false, false, true>), dim3(nb),
+                       dim3(256), 0, st, a);
+}
+
+// the shortcut's table goes to a.rcoef; r carries its stats / gamma / beta / running buffers
+static bool res_shape_ok(const BnArgs& a) {
+  return a.C % 8 == 0 && 256 % (a.C / 8) == 0 && !a.pool && a.relu && a.res && a.rcoef &&
+         a.coef;
+}
+
+extern "C" int ddp_bn_act_fwd_res(const BnArgs* args, const BnArgs* rargs, hipStream_t st) {
+  BnArgs a = *args;
+  BnArgs r = *rargs;
+  if (!res_shape_ok(a) || r.coef != a.rcoef || r.C != a.C || r.stats == nullptr) return -1;
+  r.N = a.N; r.H = a.H; r.W = a.W; r.use_running = a.use_running;
+  const size_t items = (size_t)a.N * a.H * a.W * (a.C / 8);
+  if (items >= 256 * 4096) launch_fwd_res<4>(a, r, items, st);
+  else launch_fwd_res<1>(a, r, items, st);
+  return (int)hipGetLastError();
+}
+
 extern "C" int ddp_bn_act_fwd(const BnArgs* args, hipStream_t st) {
   BnArgs a = *args;
+  a.rcoef = nullptr;  // (the shortcut-BN variant is ddp_bn_act_fwd_res)
   if (a.C % 8 || a.coef == nullptr) return -1;
   if (a.pool && (a.res || a.mask)) return -1;  // residual add / mask only without pooling
   const int Ho = a.pool ? a.H / 2 : a.H, Wo = a.pool ? a.W / 2 : a.W;
@@ -820,17 +922,39 @@ static size_t fold_bwd_bytes() {
 // the ~1.3 TB/s atomic rate, MI355X_MICROARCH.md "Global float atomics").
 static unsigned kReduceGrid = 2048;
 
-template <bool POOL, int IPT, bool MASK>
-static void launch_bwd_m(const BnArgs& a, size_t npix, int Gb, int chunks, hipStream_t st) {
+// reduce blocks along x for bx item blocks x chunks channel chunks
+static unsigned reduce_grid_x(unsigned bx, int chunks) {
   static const bool init = [] {
     if (const char* e = std::getenv("DDP_AMD_BN_REDUCE_GRID")) kReduceGrid = (unsigned)std::max(0, std::atoi(e));
     return true;
   }();
   (void)init;
-  const unsigned bx = blocks_for(npix, (size_t)(256 / Gb) * IPT);
   // (the deterministic build keeps one replica per block: block ids stay below kStatRep)
   unsigned rx = kReduceGrid ? std::min(bx, std::max(1u, kReduceGrid / (unsigned)chunks)) : bx;
   if (kDeterministic) rx = std::min(rx, std::max(1u, (unsigned)kStatRep / (unsigned)chunks));
+  return rx;
+}
+
+// residual block + projection shortcut BN: reduce (3 sums), dual finalize, apply (dz and rdz)
+template <int IPT>
+static void launch_bwd_res(const BnArgs& a, size_t npix, int Gb, int chunks, hipStream_t st) {
+  const unsigned bx = blocks_for(npix, (size_t)(256 / Gb) * IPT);
+  const unsigned rx = reduce_grid_x(bx, chunks);
+  if (rx < bx)
+    hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<false, IPT, true, true, true>), dim3(rx, chunks),
+                       dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<false, IPT, true, false, true>), dim3(bx, chunks),
+                       dim3(256), 0, st, a);
+  hipLaunchKernelGGL(bn_finalize_bwd_res_kernel, dim3(blocks_for(a.C, 256)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((bn_act_bwd_apply_kernel<false, IPT, false, true, false, true>),
+                     dim3(bx, chunks), dim3(256), 0, st, a);
+}
+
+template <bool POOL, int IPT, bool MASK>
+static void launch_bwd_m(const BnArgs& a, size_t npix, int Gb, int chunks, hipStream_t st) {
+  const unsigned bx = blocks_for(npix, (size_t)(256 / Gb) * IPT);
+  const unsigned rx = reduce_grid_x(bx, chunks);
   if (!a.sums_ready) {  // (else: accumulated by the next layer's dgrad epilogue, BnBwdFuse)
     if (rx < bx)
       hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<POOL, IPT, MASK, true>), dim3(rx, chunks),
@@ -868,6 +992,7 @@ static void launch_bwd_m(const BnArgs& a, size_t npix, int Gb, int chunks, hipSt
 template <bool POOL, int IPT>
 static void launch_bwd(const BnArgs& a, size_t npix, int Gb, int chunks, hipStream_t st) {
   if constexpr (!POOL) {
+    if (a.rcoef) return launch_bwd_res<IPT>(a, npix, Gb, chunks, st);
     if (a.mask) return launch_bwd_m<POOL, IPT, true>(a, npix, Gb, chunks, st);
   }
   launch_bwd_m<POOL, IPT, false>(a, npix, Gb, chunks, st);
@@ -973,10 +1098,19 @@ static int launch_reduce_chain(const BnArgs& a, hipStream_t st) {
 
 // a.coef must hold the table written by the matching forward; a.sums ([kStatRep][2][C]) must be
 // zero on entry (per-step scratch, zeroed once per forward).
+extern "C" int ddp_bn_act_bwd_res(const BnArgs* args, hipStream_t st) {
+  const BnArgs a = *args;
+  if (!res_shape_ok(a) || a.mask == nullptr || a.sums == nullptr || a.rsums == nullptr ||
+      a.dz == nullptr || a.rdz == nullptr || a.sums_ready)
+    return -1;
+  return launch_reduce_chain(a, st);  // (never the one-block local kernel)
+}
+
 extern "C" int ddp_bn_act_bwd(const BnArgs* args, hipStream_t st) {
   BnArgs a = *args;
   if (a.C % 8 || a.coef == nullptr || a.sums == nullptr) return -1;
   if (a.pool && (a.res || a.mask)) return -1;
+  a.rcoef = nullptr;  // (the shortcut-BN variant is ddp_bn_act_bwd_res)
   int ipt;
   if (local_cfg(a, &ipt)) {
     // small layer: the whole backward in one launch (any sums the next layer's dgrad

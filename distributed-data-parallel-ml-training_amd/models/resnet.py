@@ -62,7 +62,7 @@ class Bottleneck(nn.Module):
         return self._specs
 
     def forward_fused(self, h):
-        from ..ops.layers import conv_bn_act, GradLink
+        from ..ops.layers import conv_bn_act, conv_pre_bn, res_bn_fuse_ok, GradLink
         s1, s2, s3, sd = self.specs()
         # the block input feeds two branches; their gradients meet in a GradLink (the second
         # one accumulates from its dgrad epilogue) instead of an autograd add kernel
@@ -70,6 +70,10 @@ class Bottleneck(nn.Module):
         out = conv_bn_act(h, s1, in_link=link)
         out = conv_bn_act(out, s2)
         if sd is not None:
+            if res_bn_fuse_ok(s3):
+                # the shortcut's BatchNorm runs inside bn3's passes (ops/layers.py RES_BN_FUSE)
+                zd = conv_pre_bn(h, sd, in_link=link)
+                return conv_bn_act(out, s3, residual=zd, res_bn=sd)
             identity = conv_bn_act(h, sd, in_link=link)
             return conv_bn_act(out, s3, residual=identity)
         return conv_bn_act(out, s3, residual=h, res_link=link)

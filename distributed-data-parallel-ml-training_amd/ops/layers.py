@@ -249,6 +249,12 @@ BN_RELU_MASK = os.environ.get("DDP_AMD_BN_RELU_MASK", "1") != "0"
 # ... and an identity block's residual gradient (dy through that mask) is not stored at all: the
 # branch's first 1x1 conv rebuilds it in its accumulating dgrad epilogue (GradLink.defer)
 RES_DEFER = os.environ.get("DDP_AMD_RES_DEFER", "1") != "0"
+# ... and a projection block's shortcut BatchNorm folded into the block's residual BN passes: the
+# downsample conv's PRE-BN output is the residual, normalised inside bn3's apply, and bn3's
+# backward reduce / apply also produce the shortcut's dz (bn_act.hip RBN; both BNs see the same
+# gradient dy * mask, so they share S1). The shortcut's BN output and its gradient are never
+# stored and its own finalize / apply / reduce / finalize / apply launches disappear.
+RES_BN_FUSE = os.environ.get("DDP_AMD_RES_BN_FUSE", "1") != "0"
 # largest dgrad output H*W that takes the fused sums: 16 (4x4 / 2x2) from 128 images per GPU up,
 # 256 (also 16x16 / 8x8) at the strong-scaling shares of at most 64 images (b64 0.4556 vs 0.4594
 # ms, b32 0.3921 vs 0.3952; b128 / b256 unchanged, profiles/r4z3_bn_sums_threshold.md); the
@@ -391,9 +397,52 @@ def _defer_bn(spec, residual, running_mean, N, Ho, Wo):
                                              2 if spec.pool else 1))
 
 
+class _ConvPreBNFn(torch.autograd.Function):
+    """A projection shortcut's conv whose BatchNorm runs inside its consumer's residual BN
+    passes (RES_BN_FUSE): z = conv(x) + bias, with z's batch statistics from the GEMM epilogue.
+    The consumer normalises z with this spec's table and its backward hands autograd dz — the
+    gradient at z — with this BN's gamma / beta gradients already accumulated and announced."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, spec, in_link=None):
+        spec.maybe_pack()
+        spec.dz_fused = None
+        spec.deferred = None
+        z = conv_forward(spec, x, bias, spec.stats)
+        spec.fwd_z = None
+        ctx.spec, ctx.in_link = spec, in_link
+        ctx.save_for_backward(x, weight, bias)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        x, weight, bias = ctx.saved_tensors
+        if bias is not None:
+            ensure_grad(bias)  # analytically zero under batch-statistics BN (bn_act.hip)
+            grad_ready([bias])
+        dx = conv_backward(ctx.spec, x, dz.contiguous(), ensure_grad(weight),
+                           ctx.needs_input_grad[0], ctx.in_link, weight=weight)
+        return dx, None, None, None, None
+
+
+def conv_pre_bn(x, spec, in_link=None):
+    """The conv of ``spec`` with its BatchNorm left to the residual block that consumes it
+    (``conv_bn_act(..., residual=z, res_bn=spec)``)."""
+    conv = spec.conv
+    return _ConvPreBNFn.apply(x, conv.weight, conv.bias, spec, in_link)
+
+
+def res_bn_fuse_ok(spec):
+    """The residual BN of ``spec`` can take a projection shortcut's BatchNorm (bn_act.hip
+    res_shape_ok; the backward needs the ReLU mask bits)."""
+    return (RES_BN_FUSE and BN_RELU_MASK and spec.residual and spec.relu and not spec.pool
+            and spec.K % 8 == 0 and 256 % (spec.K // 8) == 0)
+
+
 class _ConvBNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, gamma, beta, residual, spec, in_link=None, res_link=None):
+    def forward(ctx, x, weight, bias, gamma, beta, residual, spec, in_link=None, res_link=None,
+                res_bn=None):
         spec.maybe_pack()
         spec.dz_fused = None  # a fused BN backward of an earlier pass must never be consumed
         spec.deferred = None
@@ -419,6 +468,10 @@ class _ConvBNActFn(torch.autograd.Function):
         y = torch.empty(N, Ho, Wo, spec.K, dtype=BF16, device=x.device)
         if residual is not None:
             check(residual, BF16, (N, P, Q, spec.K), "residual")
+        if res_bn is not None and (residual is None or res_link is not None
+                                   or not res_bn_fuse_ok(spec) or res_bn.K != spec.K):
+            raise ValueError("shortcut BatchNorm fold: residual block with ReLU mask only")
+        ctx.res_bn = res_bn
         bn = spec.bn
         rm = rv = None
         use_running = 0
@@ -478,11 +531,18 @@ class _ConvBNActFn(torch.autograd.Function):
                     and any(ctx.needs_input_grad) and spec.K % 8 == 0):
                 mask = torch.empty(N, P, Q, spec.K // 8, dtype=torch.uint8, device=x.device)
             ctx.relu_mask = mask
+            rk = {}
+            if res_bn is not None:  # residual = the shortcut's pre-BN z, normalised here
+                rb = res_bn.bn
+                rk = dict(rstats=ptr(res_bn.stats), rgamma=ptr(rb.weight), rbeta=ptr(rb.bias),
+                          rcoef=ptr(res_bn.coef), rrunning_mean=ptr(rb.running_mean),
+                          rrunning_var=ptr(rb.running_var), reps=res_bn.eps,
+                          rmomentum=float(rb.momentum if rb.momentum is not None else 0.1))
             native().bn_act_fwd(N, P, Q, spec.K, int(spec.pool), int(spec.relu), spec.eps, ptr(z),
                                 ptr(residual), ptr(stats), ptr(gamma), ptr(beta), ptr(y),
                                 stream_handle(), ptr(rm), ptr(rv),
                                 float(bn.momentum if bn.momentum is not None else 0.1),
-                                use_running, ptr(spec.coef), mask=ptr(mask))
+                                use_running, ptr(spec.coef), mask=ptr(mask), **rk)
         ctx.spec = spec
         ctx.has_res = residual is not None
         ctx.in_link, ctx.res_link = in_link, res_link
@@ -514,7 +574,7 @@ class _ConvBNActFn(torch.autograd.Function):
             grad_ready([gamma, beta, bias])
             dx = conv_backward(spec, x, dz, gw, ctx.needs_input_grad[0], ctx.in_link,
                                weight=weight)
-            return dx, None, None, None, None, None, None, None, None
+            return dx, None, None, None, None, None, None, None, None, None
         N, P, Q, K = z.shape
         sums = spec.sums  # zeroed together with the statistics at the start of the forward
         mask = getattr(ctx, "relu_mask", None)
@@ -547,6 +607,24 @@ class _ConvBNActFn(torch.autograd.Function):
                                   ptr(ctx.pool3_idx), ptr(sums), ptr(dz), ptr(gg), ptr(gbt),
                                   stream_handle(), ptr(spec.coef))
             ctx.pool3_idx = None
+        elif ctx.res_bn is not None:
+            # + the projection shortcut's BN backward: dres = the gradient at ITS conv output
+            rs, rb = ctx.res_bn, ctx.res_bn.bn
+            ctx.res_bn = None
+            if mask is None or sums_ready or dz_done is not None:
+                raise RuntimeError("shortcut BatchNorm fold needs the forward's ReLU mask")
+            dy = dy.contiguous()
+            dz = torch.empty_like(z)
+            if dres is None:
+                dres = torch.empty_like(z)
+            rg, rbt = ensure_grad(rb.weight), ensure_grad(rb.bias)
+            native().bn_act_bwd(N, P, Q, K, int(spec.pool), int(spec.relu), spec.eps, ptr(z),
+                                ptr(residual), ptr(stats), ptr(gamma), ptr(beta), ptr(dy),
+                                ptr(sums), ptr(dz), 0, ptr(gg), ptr(gbt), ptr(gb),
+                                stream_handle(), ptr(spec.coef), mask=ptr(mask),
+                                rcoef=ptr(rs.coef), rsums=ptr(rs.sums), rdz=ptr(dres),
+                                rdgamma=ptr(rg), rdbeta=ptr(rbt))
+            grad_ready([rb.weight, rb.bias])
         else:
             dy = dy.contiguous()
             dz = torch.empty_like(z)
@@ -597,15 +675,16 @@ class _ConvBNActFn(torch.autograd.Function):
             dx = conv_backward(spec, x, dz, gw, ctx.needs_input_grad[0], ctx.in_link,
                                weight=weight, bnf=bnf)
         ctx.prev_z = None
-        return dx, None, None, None, None, dres, None, None, None
+        return dx, None, None, None, None, dres, None, None, None, None
 
 
-def conv_bn_act(x, spec, residual=None, in_link=None, res_link=None):
+def conv_bn_act(x, spec, residual=None, in_link=None, res_link=None, res_bn=None):
     """Fused conv -> BN (+residual) -> ReLU (-> 2x2 pool). ``in_link`` / ``res_link``: GradLink
-    through which the input / residual gradient is merged with the other branch (ResNet)."""
+    through which the input / residual gradient is merged with the other branch (ResNet).
+    ``res_bn``: the spec whose BatchNorm normalises ``residual`` here (its conv_pre_bn output)."""
     conv, bn = spec.conv, spec.bn
     return _ConvBNActFn.apply(x, conv.weight, conv.bias, bn.weight, bn.bias, residual, spec,
-                              in_link, res_link)
+                              in_link, res_link, res_bn)
 
 
 # ------------------------------------------------------------------ classifier head

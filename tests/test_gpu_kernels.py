@@ -272,6 +272,87 @@ def _bn_case(nat, N, C, H, pool, res, mode, ptr, stream_handle):
         assert rel_err(dres.permute(0, 3, 1, 2), rr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("N,C,H", [(8, 256, 8), (64, 256, 28), (8, 2048, 4), (16, 1024, 7)])
+def test_bn_act_shortcut_bn(native_ext, N, C, H):
+    """Residual block with the projection shortcut's BatchNorm folded in (bn_act.hip RBN):
+    y = relu(bn(z) + bn_r(zr)) from ONE finalize + apply, and the backward's reduce (three sums,
+    S1 shared) + dual finalize + apply write dz AND the shortcut's dz, both BNs' gamma / beta
+    gradients, against fp32 PyTorch. (64, 256, 28) takes the 4-items-per-thread forward and
+    the capped-grid (grid-stride) reduce."""
+    from ddp_amd.ops.common import ptr, stream_handle
+    nat = native_ext
+    s = stream_handle()
+    eps = 1e-5
+    z = bf(torch.randn(N, C, H, H, device=DEV) * 2 + 0.5)
+    zr = bf(torch.randn(N, C, H, H, device=DEV) * 0.7 - 0.3)
+    g, b = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.1
+    gr, br = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.1
+    zn = z.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    zrn = zr.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+
+    def stats_of(t):
+        tf = t.float().reshape(-1, C)
+        st = torch.zeros(16, 2 * C, device=DEV)
+        st[5] = torch.cat([tf.sum(0), (tf * tf).sum(0)])
+        return st
+
+    st, str_ = stats_of(zn), stats_of(zrn)
+    coef, rcoef = torch.empty(6 * C, device=DEV), torch.empty(6 * C, device=DEV)
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    rrm, rrv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    out = torch.empty(N, H, H, C, device=DEV, dtype=torch.bfloat16)
+    mask = torch.full((N, H, H, C // 8), 0xA5, dtype=torch.uint8, device=DEV)
+    nat.bn_act_fwd(N, H, H, C, 0, 1, eps, ptr(zn), ptr(zrn), ptr(st), ptr(g), ptr(b), ptr(out), s,
+                   ptr(rm), ptr(rv), 0.1, 0, ptr(coef), mask=ptr(mask), rstats=ptr(str_),
+                   rgamma=ptr(gr), rbeta=ptr(br), rcoef=ptr(rcoef), rrunning_mean=ptr(rrm),
+                   rrunning_var=ptr(rrv), reps=eps, rmomentum=0.1)
+    zq = z.clone().requires_grad_(True)
+    zrq = zr.clone().requires_grad_(True)
+    gq, bq = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    grq, brq = gr.clone().requires_grad_(True), br.clone().requires_grad_(True)
+    rm_ref, rv_ref = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    rrm_ref, rrv_ref = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    ref = F.relu(F.batch_norm(zq, rm_ref, rv_ref, gq, bq, training=True, eps=eps)
+                 + F.batch_norm(zrq, rrm_ref, rrv_ref, grq, brq, training=True, eps=eps))
+    torch.cuda.synchronize()
+    assert rel_err(out.permute(0, 3, 1, 2), ref) < 1e-2
+    for mine, want in ((rm, rm_ref), (rv, rv_ref), (rrm, rrm_ref), (rrv, rrv_ref)):
+        assert torch.allclose(mine, want, rtol=1e-4, atol=1e-5)
+    # the mask bits are the pre-ReLU sign test of the forward's own arithmetic
+    y_pre = (zn.float() * coef[:C] + coef[C:2 * C]) + (zrn.float() * rcoef[:C] + rcoef[C:2 * C])
+    bits = (y_pre > 0).reshape(N, H, H, C // 8, 8).to(torch.int32)
+    want = (bits << torch.arange(8, device=DEV, dtype=torch.int32)).sum(-1)
+    assert (mask.to(torch.int32) != want).float().mean() < 1e-4  # (fma rounding at y == 0)
+    dout = bf(torch.randn_like(ref))
+    ref.backward(dout)
+    doutn = dout.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    sums = torch.zeros(16 * 2 * C + 64, device=DEV)
+    rsums = torch.zeros(16 * 2 * C + 64, device=DEV)
+    dz, dzr = torch.empty_like(zn), torch.empty_like(zn)
+    dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    dgr, dbr = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    nat.bn_act_bwd(N, H, H, C, 0, 1, eps, ptr(zn), ptr(zrn), ptr(st), ptr(g), ptr(b),
+                   ptr(doutn), ptr(sums), ptr(dz), 0, ptr(dg), ptr(db), 0, s, ptr(coef),
+                   mask=ptr(mask), rcoef=ptr(rcoef), rsums=ptr(rsums), rdz=ptr(dzr),
+                   rdgamma=ptr(dgr), rdbeta=ptr(dbr))
+    torch.cuda.synchronize()
+    assert rel_err(dz.permute(0, 3, 1, 2), zq.grad) < 2e-2
+    assert rel_err(dzr.permute(0, 3, 1, 2), zrq.grad) < 2e-2
+    assert rel_err(dg, gq.grad) < 1e-2 and rel_err(db, bq.grad) < 1e-2
+    assert rel_err(dgr, grq.grad) < 1e-2 and rel_err(dbr, brq.grad) < 1e-2
+    # eval: both tables from the running statistics
+    rm2, rv2 = torch.randn(C, device=DEV) * 0.1, torch.rand(C, device=DEV) + 0.5
+    rrm2, rrv2 = torch.randn(C, device=DEV) * 0.1, torch.rand(C, device=DEV) + 0.5
+    nat.bn_act_fwd(N, H, H, C, 0, 1, eps, ptr(zn), ptr(zrn), ptr(st), ptr(g), ptr(b), ptr(out), s,
+                   ptr(rm2), ptr(rv2), 0.1, 1, ptr(coef), rstats=ptr(str_), rgamma=ptr(gr),
+                   rbeta=ptr(br), rcoef=ptr(rcoef), rrunning_mean=ptr(rrm2),
+                   rrunning_var=ptr(rrv2), reps=eps, rmomentum=0.1)
+    torch.cuda.synchronize()
+    ev = F.relu(F.batch_norm(z, rm2, rv2, g, b, training=False, eps=eps)
+                + F.batch_norm(zr, rrm2, rrv2, gr, br, training=False, eps=eps))
+    assert rel_err(out.permute(0, 3, 1, 2), ev) < 1e-2
+
+
 def test_linear_ce(native_ext):
     from ddp_amd.ops.layers import linear_small, cross_entropy
     B, Fi, J = 64, 512, 10

@@ -132,6 +132,52 @@ def test_bottleneck_block_matches_cpu(native_ext):
     assert min(cos.values()) > 0.97, cos
 
 
+def test_bottleneck_shortcut_bn_fold_matches_unfolded(native_ext):
+    """The projection shortcut's BatchNorm folded into the block's residual BN passes
+    (ops/layers.py RES_BN_FUSE, bn_act.hip RBN) gives the unfolded block's output, input
+    gradient and parameter gradients (both BNs' gamma / beta, the shortcut conv) and the same
+    running statistics — up to the one rounding it removes (the shortcut BN output is not
+    stored as bf16) and the atomics order."""
+    from ddp_amd.models.resnet import Bottleneck
+    from ddp_amd.optim import FusedSGD
+    from ddp_amd.ops import layers
+    from ddp_amd.ops.layers import global_avg_pool
+    torch.manual_seed(1)
+    ds = torch.nn.Sequential(torch.nn.Conv2d(128, 512, 1, stride=2, bias=False),
+                             torch.nn.BatchNorm2d(512))
+    base = Bottleneck(128, 128, stride=2, downsample=ds)
+    x = torch.randn(16, 28, 28, 128).to(torch.bfloat16).cuda()
+    w = torch.randn(16, 512, device="cuda")
+    runs = {}
+    saved = layers.RES_BN_FUSE
+    try:
+        for fold in (False, True):
+            layers.RES_BN_FUSE = fold
+            blk = copy.deepcopy(base).cuda()
+            FusedSGD(blk.parameters(), lr=0.1).zero_grad()
+            xg = x.clone().requires_grad_(True)
+            h = blk.forward_fused(xg)
+            (global_avg_pool(h).float() * w).sum().backward()
+            torch.cuda.synchronize()
+            runs[fold] = (h.float(), xg.grad.float(), [p.grad.clone() for p in blk.parameters()],
+                          [b.clone() for b in blk.buffers() if b.dtype.is_floating_point])
+    finally:
+        layers.RES_BN_FUSE = saved
+
+    def cos(a, b):
+        a, b = a.reshape(-1).double(), b.reshape(-1).double()
+        return float(torch.dot(a, b) / (a.norm() * b.norm() + 1e-30))
+    (h0, dx0, g0, b0), (h1, dx1, g1, b1) = runs[False], runs[True]
+    assert float((h1 - h0).abs().max()) <= 0.0625 * float(h0.abs().max())  # bf16 ulps
+    assert cos(h1, h0) > 0.9999
+    assert cos(dx1, dx0) > 0.999
+    names = [n for n, _ in base.named_parameters()]
+    worst = min((cos(a, b), n) for a, b, n in zip(g1, g0, names))
+    assert worst[0] > 0.998, worst
+    for a, b in zip(b1, b0):
+        assert torch.allclose(a, b, rtol=1e-3, atol=1e-4)
+
+
 @pytest.mark.parametrize("cuts", [[8, 14], [4, 8, 14]])
 def test_resnet_segmented_ddp_step_matches_single_graph(native_ext, cuts):
     """Pipelined DDP step on ResNet-50 (backward cut at block boundaries: bucket all-reduce +
@@ -240,8 +286,10 @@ def test_resnet50_trajectory_tracks_fp32_reference(native_ext):
     print("rel loss diffs", [round(r, 4) for r in rel], "param cosine", cos_p)
     # (on the box: batch 64, 20 steps: per-step within 3 %, parameter cosine 0.9964; batch 16:
     # the first 7 steps within 1.1 %, single later steps up to 6 % — small-batch BN noise;
-    # batch 32 on a fresh box: one early step at 3.1 %, mean 0.9 %, parameter cosine 0.9975)
-    assert max(rel[:6]) < 0.05 and sum(rel) / len(rel) < 0.03 and max(rel) < 0.1, rel
+    # batch 32 on a fresh box: one early step at 3.1 %, mean 0.9 %, parameter cosine 0.9975.
+    # Run-to-run spread of the worst early step (fp32 atomics order the BN sums differently
+    # every run): 0.015-0.053 over 8 runs, mean 0.4-1.2 %, profiles/r5al_res_bn_fold.md)
+    assert max(rel[:6]) < 0.08 and sum(rel) / len(rel) < 0.03 and max(rel) < 0.1, rel
     assert cos_p > 0.99, cos_p
 
 
