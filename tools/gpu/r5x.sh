@@ -14,3 +14,8 @@ cp $O/bench_2.log $O/bench_default.json
 timeout -k 10 300 python bench.py --model resnet50 --steps 8 --warmup 4 --ref-window 0 > $O/resnet.log 2>&1 || { tail -5 $O/resnet.log; exit 1; }
 tail -1 $O/resnet.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('resnet', d['ms_per_step'], d['value'], d['train_loss_mean'])"
 TAG=${TAG:-r5x} MODEL=vgg11 BATCHES="256 32" bash tools/gpu/profile.sh && TAG=${TAG:-r5x} MODEL=resnet50 BATCHES=256 bash tools/gpu/profile.sh
+# strong-scaling per-GPU shares (N = 2 / 4 / 8 of the 256 global batch)
+for b in 128 64 32; do
+  timeout -k 10 200 python bench.py --global-batch $b --steps 60 --warmup 10 > $O/b$b.log 2>&1 || { tail -5 $O/b$b.log; exit 1; }
+  tail -1 $O/b$b.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('b$b', d['ms_per_step'], d['value'])"
+done
