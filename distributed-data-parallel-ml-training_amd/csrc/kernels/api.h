@@ -69,6 +69,7 @@ struct BnArgs {
   unsigned short* rdz;          // backward: grad wrt the shortcut conv output
   float* rdgamma;               // its grad arena slices (accumulated)
   float* rdbeta;
+  int red_gb;                   // backward reduce launch: channel groups per block (0 = min(C/8, 256))
 };
 
 // BatchNorm-backward statistics fused into a conv dgrad: the dgrad output IS the gradient at the

@@ -353,7 +353,7 @@ __global__ __launch_bounds__(256) void bn_act_bwd_reduce_kernel(BnArgs a) {
   __shared__ float red[8 * 256];
   DDP_DEVICE_CHECK(a.C % 8 == 0 && (!POOL || (a.H % 2 == 0 && a.W % 2 == 0)));
   const int G = a.C / 8;
-  const int Gb = G < 256 ? G : 256;
+  const int Gb = a.red_gb ? a.red_gb : (G < 256 ? G : 256);  // (reduce_split)
   const int Ho = POOL ? a.H / 2 : a.H, Wo = POOL ? a.W / 2 : a.W;
   const size_t npix = (size_t)a.N * Ho * Wo;
   const int cg_base = blockIdx.y * Gb;
@@ -922,6 +922,28 @@ static size_t fold_bwd_bytes() {
 // the ~1.3 TB/s atomic rate, MI355X_MICROARCH.md "Global float atomics").
 static unsigned kReduceGrid = 2048;
 
+// Channel groups per reduce block (DDP_AMD_BN_REDUCE_GB, default 32 = 256 channels): every
+// block adds one partial sum per channel of its chunk, so a block spanning all of a wide
+// layer's channels (the apply's layout: 2048 channels x 1 pixel row) made the capped grid
+// issue 2048 x 2 x C memory-side atomics — 33 MB at C = 2048, more time than the layer's
+// loads (ResNet-50 layer4: reduce 51 us vs apply 27 us over the same tensors). Narrower chunks
+// reduce 256 / Gb pixel rows in LDS first.
+static int kReduceGb = 32;
+static void reduce_split(const BnArgs& a, int Gb, int chunks, int* rGb, int* rchunks) {
+  static const bool init = [] {
+    if (const char* e = std::getenv("DDP_AMD_BN_REDUCE_GB")) kReduceGb = std::max(0, std::atoi(e));
+    return true;
+  }();
+  (void)init;
+  const int G = a.C / 8;
+  *rGb = Gb;
+  *rchunks = chunks;
+  if (kReduceGb > 0 && Gb > kReduceGb && 256 % kReduceGb == 0 && G % kReduceGb == 0) {
+    *rGb = kReduceGb;
+    *rchunks = G / kReduceGb;
+  }
+}
+
 // reduce blocks along x for bx item blocks x chunks channel chunks
 static unsigned reduce_grid_x(unsigned bx, int chunks) {
   static const bool init = [] {
@@ -939,13 +961,18 @@ static unsigned reduce_grid_x(unsigned bx, int chunks) {
 template <int IPT>
 static void launch_bwd_res(const BnArgs& a, size_t npix, int Gb, int chunks, hipStream_t st) {
   const unsigned bx = blocks_for(npix, (size_t)(256 / Gb) * IPT);
-  const unsigned rx = reduce_grid_x(bx, chunks);
-  if (rx < bx)
-    hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<false, IPT, true, true, true>), dim3(rx, chunks),
-                       dim3(256), 0, st, a);
+  BnArgs ra = a;
+  int rGb, rch;
+  reduce_split(a, Gb, chunks, &rGb, &rch);
+  ra.red_gb = rGb;
+  const unsigned rbx = blocks_for(npix, (size_t)(256 / rGb) * IPT);
+  const unsigned rx = reduce_grid_x(rbx, rch);
+  if (rx < rbx)
+    hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<false, IPT, true, true, true>), dim3(rx, rch),
+                       dim3(256), 0, st, ra);
   else
-    hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<false, IPT, true, false, true>), dim3(bx, chunks),
-                       dim3(256), 0, st, a);
+    hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<false, IPT, true, false, true>), dim3(rbx, rch),
+                       dim3(256), 0, st, ra);
   hipLaunchKernelGGL(bn_finalize_bwd_res_kernel, dim3(blocks_for(a.C, 256)), dim3(256), 0, st, a);
   hipLaunchKernelGGL((bn_act_bwd_apply_kernel<false, IPT, false, true, false, true>),
                      dim3(bx, chunks), dim3(256), 0, st, a);
@@ -954,14 +981,19 @@ static void launch_bwd_res(const BnArgs& a, size_t npix, int Gb, int chunks, hip
 template <bool POOL, int IPT, bool MASK>
 static void launch_bwd_m(const BnArgs& a, size_t npix, int Gb, int chunks, hipStream_t st) {
   const unsigned bx = blocks_for(npix, (size_t)(256 / Gb) * IPT);
-  const unsigned rx = reduce_grid_x(bx, chunks);
   if (!a.sums_ready) {  // (else: accumulated by the next layer's dgrad epilogue, BnBwdFuse)
-    if (rx < bx)
-      hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<POOL, IPT, MASK, true>), dim3(rx, chunks),
-                         dim3(256), 0, st, a);
+    BnArgs ra = a;
+    int rGb, rch;
+    reduce_split(a, Gb, chunks, &rGb, &rch);
+    ra.red_gb = rGb;
+    const unsigned rbx = blocks_for(npix, (size_t)(256 / rGb) * IPT);
+    const unsigned rx = reduce_grid_x(rbx, rch);
+    if (rx < rbx)
+      hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<POOL, IPT, MASK, true>), dim3(rx, rch),
+                         dim3(256), 0, st, ra);
     else
-      hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<POOL, IPT, MASK, false>), dim3(bx, chunks),
-                         dim3(256), 0, st, a);
+      hipLaunchKernelGGL((bn_act_bwd_reduce_kernel<POOL, IPT, MASK, false>), dim3(rbx, rch),
+                         dim3(256), 0, st, ra);
   }
   // The finalize stays its own launch: folding it into the apply (every block re-reducing the 16
   // replicas the reduce just wrote with memory-side atomics) measured 3-4x slower applies at
