@@ -32,6 +32,7 @@ CONV_CASES = [
     (2, 64, 14, 14, 128, 1, 2, 0),   # 1x1 stride 2
     (2, 8, 32, 32, 64, 7, 2, 3),     # 7x7 stem-like
     (3, 8, 40, 40, 64, 7, 2, 3),     # stem, partial last pixel-tile group
+    (128, 8, 224, 224, 64, 7, 2, 3),  # stem: full grid, waves walk several pixel-tile groups
 ]
 
 
