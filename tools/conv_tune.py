@@ -49,6 +49,8 @@ def main():
     ap.add_argument("--quick", action="store_true", help="VGG-11 b256 only")
     ap.add_argument("--sets", default="all", choices=["all", "vgg", "resnet256"])
     ap.add_argument("--merge", default=None, help="existing table to extend (entries kept)")
+    ap.add_argument("--modes", default="fwd,dgrad,wgrad",
+                    help="GEMM kinds to tune (e.g. 'fwd': re-tune the forward entries only)")
     ap.add_argument("--pairs", action="store_true",
                     help="tune the backward pair launch (DGRAD+WGRAD split-K factors, or separate "
                          "launches) of the stride-1 layers instead (--pair-sets)")
@@ -134,6 +136,8 @@ def main():
             label = f"{model} N{N} {Cr}->{K} {H}x{W} k{R} s{stride}"
             for mode, gemms, fn in probs:
                 key = (mode, tuple(gemms))
+                if ["fwd", "dgrad", "wgrad"][mode] not in args.modes.split(","):
+                    continue
                 if key in seen:
                     continue
                 seen.add(key)

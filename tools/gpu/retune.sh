@@ -7,7 +7,7 @@ OUT=gpurun_out/tune
 mkdir -p $OUT
 TABLE=distributed-data-parallel-ml-training_amd/ops/conv_tuning.json
 cp $TABLE $OUT/old.json
-timeout -k 10 ${TUNE_S:-900} python -u tools/conv_tune.py --sets ${SETS:-resnet256} --reps ${REPS:-20} \
+timeout -k 10 ${TUNE_S:-900} python -u tools/conv_tune.py --sets ${SETS:-resnet256} --modes ${MODES:-fwd,dgrad,wgrad} --reps ${REPS:-20} \
     --merge $OUT/old.json --out $OUT/new.json > $OUT/tune.log 2>&1 || { tail -20 $OUT/tune.log; exit 1; }
 tail -3 $OUT/tune.log
 for P in 1 2; do
