@@ -40,6 +40,8 @@ def resnet_layers(B):
         inp = width * 4
         if blocks > 1:  # a representative non-first block
             out.append((B, inp, h_out, h_out, width, 1, 1, 0, inp))
+            if stride != 1:  # its 3x3 runs at stride 1 (the first block's is strided)
+                out.append((B, width, h_out, h_out, width, 3, 1, 1, width))
     return out
 
 
