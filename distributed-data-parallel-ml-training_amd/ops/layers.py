@@ -188,6 +188,7 @@ class GradLink:
         self.seen = 0
         self.buf = None
         self.deferred = None  # (dy, relu_mask): a residual gradient that was never stored
+        self.deferred_dgrad = None  # (geom, dz, wc): a strided shortcut's dgrad, run last
 
     def defer(self, dy, mask):
         """The residual BatchNorm's gradient dres = dy through its ReLU mask, NOT stored: the
@@ -255,6 +256,11 @@ RES_DEFER = os.environ.get("DDP_AMD_RES_DEFER", "1") != "0"
 # gradient dy * mask, so they share S1). The shortcut's BN output and its gradient are never
 # stored and its own finalize / apply / reduce / finalize / apply launches disappear.
 RES_BN_FUSE = os.environ.get("DDP_AMD_RES_BN_FUSE", "1") != "0"
+# ... and a strided shortcut conv whose backward reaches the block input first leaves its dgrad
+# to the other branch: that one writes dx, then the shortcut's phase dgrad ACCUMULATES into the
+# 1/stride^2 of dx it reaches — no zero fill of dx's untouched phases and no read-back of the
+# whole dx by an accumulating second branch (GradLink.deferred_dgrad)
+DS_DGRAD_DEFER = os.environ.get("DDP_AMD_DS_DGRAD_DEFER", "1") != "0"
 # largest dgrad output H*W that takes the fused sums: 16 (4x4 / 2x2) from 128 images per GPU up,
 # 256 (also 16x16 / 8x8) at the strong-scaling shares of at most 64 images (b64 0.4556 vs 0.4594
 # ms, b32 0.3921 vs 0.3952; b128 / b256 unchanged, profiles/r4z3_bn_sums_threshold.md); the
@@ -324,6 +330,13 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=Non
         return (None, False) if (bna is not None or (bnf is not None and len(bnf) > 7)) else None
     if spec.C != spec.Cr:
         raise RuntimeError("dgrad requested for a channel-padded input layer")
+    if (DS_DGRAD_DEFER and link is not None and spec.stride > 1 and link.buf is None
+            and link.deferred is None and link.deferred_dgrad is None
+            and link.seen + 1 < link.expected):
+        # strided first branch: its dgrad runs after the other branch wrote dx (accumulating)
+        link.deferred_dgrad = (g, dz, spec.wc)
+        link.seen += 1
+        return None
     if link is not None and link.deferred is not None and spec.stride == 1:
         # second branch onto a deferred first branch: dx = dgrad + dy * mask (dx only written)
         acc_dy, acc_mask = link.deferred
@@ -348,6 +361,11 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=Non
     l0_mode = bnf is not None and len(bnf) > 7  # (input block's sums: pair launch only)
     done = native().conv_dgrad(g, ptr(dz), ptr(spec.wc), ptr(dx), ptr(ws), ws.numel(), 0, s,
                                bn=None if l0_mode else bnf, bna=bna)
+    if link is not None and link.deferred_dgrad is not None:
+        gd, dzd, wcd = link.deferred_dgrad
+        link.deferred_dgrad = None
+        native().conv_dgrad(gd, ptr(dzd), ptr(wcd), ptr(dx), ptr(ws), ws.numel(), 0, s,
+                            accumulate=1)
     if link is not None:
         link.seen += 1
         link.buf = dx

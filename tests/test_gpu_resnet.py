@@ -149,33 +149,39 @@ def test_bottleneck_shortcut_bn_fold_matches_unfolded(native_ext):
     x = torch.randn(16, 28, 28, 128).to(torch.bfloat16).cuda()
     w = torch.randn(16, 512, device="cuda")
     runs = {}
-    saved = layers.RES_BN_FUSE
+    saved = (layers.RES_BN_FUSE, layers.DS_DGRAD_DEFER)
     try:
-        for fold in (False, True):
-            layers.RES_BN_FUSE = fold
+        # (fold, defer): the shortcut's strided dgrad deferred behind the other branch's
+        # (GradLink.deferred_dgrad) or run first with the zero fill — the unfolded, undeferred
+        # block is the reference for both
+        for fold, defer in ((False, False), (True, True), (True, False)):
+            layers.RES_BN_FUSE, layers.DS_DGRAD_DEFER = fold, defer
             blk = copy.deepcopy(base).cuda()
             FusedSGD(blk.parameters(), lr=0.1).zero_grad()
             xg = x.clone().requires_grad_(True)
             h = blk.forward_fused(xg)
             (global_avg_pool(h).float() * w).sum().backward()
             torch.cuda.synchronize()
-            runs[fold] = (h.float(), xg.grad.float(), [p.grad.clone() for p in blk.parameters()],
-                          [b.clone() for b in blk.buffers() if b.dtype.is_floating_point])
+            runs[(fold, defer)] = (h.float(), xg.grad.float(),
+                                   [p.grad.clone() for p in blk.parameters()],
+                                   [b.clone() for b in blk.buffers() if b.dtype.is_floating_point])
     finally:
-        layers.RES_BN_FUSE = saved
+        layers.RES_BN_FUSE, layers.DS_DGRAD_DEFER = saved
 
     def cos(a, b):
         a, b = a.reshape(-1).double(), b.reshape(-1).double()
         return float(torch.dot(a, b) / (a.norm() * b.norm() + 1e-30))
-    (h0, dx0, g0, b0), (h1, dx1, g1, b1) = runs[False], runs[True]
-    assert float((h1 - h0).abs().max()) <= 0.0625 * float(h0.abs().max())  # bf16 ulps
-    assert cos(h1, h0) > 0.9999
-    assert cos(dx1, dx0) > 0.999
+    h0, dx0, g0, b0 = runs[(False, False)]
     names = [n for n, _ in base.named_parameters()]
-    worst = min((cos(a, b), n) for a, b, n in zip(g1, g0, names))
-    assert worst[0] > 0.998, worst
-    for a, b in zip(b1, b0):
-        assert torch.allclose(a, b, rtol=1e-3, atol=1e-4)
+    for key in ((True, True), (True, False)):
+        h1, dx1, g1, b1 = runs[key]
+        assert float((h1 - h0).abs().max()) <= 0.0625 * float(h0.abs().max())  # bf16 ulps
+        assert cos(h1, h0) > 0.9999
+        assert cos(dx1, dx0) > 0.999, key
+        worst = min((cos(a, b), n) for a, b, n in zip(g1, g0, names))
+        assert worst[0] > 0.998, (key, worst)
+        for a, b in zip(b1, b0):
+            assert torch.allclose(a, b, rtol=1e-3, atol=1e-4)
 
 
 @pytest.mark.parametrize("cuts", [[8, 14], [4, 8, 14]])
