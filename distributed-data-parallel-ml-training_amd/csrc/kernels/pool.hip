@@ -103,24 +103,47 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const unsigned short* 
   }
 }
 
-// Global average pool: thread per (n, 8 channels).
+// Global average pool: a block = 64 (n, 8-channel) items x 4 waves, wave w summing pixels
+// w, w + 4, ... (4 loads in flight per thread), the 4 partial sums meet in LDS. (One thread per
+// item walking all 49 pixels serially ran ResNet-50's 51 MB input in 26 us on 256 blocks.)
 __global__ __launch_bounds__(256) void avgpool_fwd_kernel(const unsigned short* __restrict__ x,
                                                           int N, int HW, int C,
                                                           unsigned short* __restrict__ y) {
+  __shared__ float red[3][64][9];
   const int G = C / 8;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= N * G) return;
-  const int n = t / G, cg = t % G;
+  const int it = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int wv = threadIdx.x >> 6;
+  const bool ok = it < N * G;
+  const int n = ok ? it / G : 0, cg = ok ? it % G : 0;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int p = 0; p < HW; ++p) {
-    const u16x8 v = ld8(x + ((size_t)n * HW + p) * C + cg * 8);
+  const unsigned short* base = x + (size_t)n * HW * C + cg * 8;
+  int p = wv;
+  for (; p + 12 < HW; p += 16) {
+    u16x8 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = ld8(base + (size_t)(p + 4 * u) * C);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += bf2f(v[u][e]);
+  }
+  for (; p < HW; p += 4) {
+    const u16x8 v = ld8(base + (size_t)p * C);
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[e] += bf2f(v[e]);
   }
+  if (wv) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[wv - 1][threadIdx.x & 63][e] = acc[e];
+  }
+  __syncthreads();
+  if (wv || !ok) return;
   u16x8 o;
   const float inv = 1.f / (float)HW;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) o[e] = f2bf(acc[e] * inv);
+  for (int e = 0; e < 8; ++e)
+    o[e] = f2bf((acc[e] + red[0][threadIdx.x][e] + red[1][threadIdx.x][e] +
+                 red[2][threadIdx.x][e]) * inv);
   st8(y + (size_t)n * C + cg * 8, o);
 }
 
@@ -143,14 +166,33 @@ __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const unsigned short* 
   }
 }
 
-// db[j] += sum_b dl[b][j]  (bias gradient of a GEMM-based Linear; bf16 dlogits)
+// db[j] += sum_b dl[b][j]  (bias gradient of a GEMM-based Linear; bf16 dlogits). A block = 16
+// columns x 16 row groups (row group r sums rows r, r + 16, ..., 4 loads in flight), partials
+// meet in LDS. (One thread per column walking all B rows serially took 62 us for ResNet-50's
+// 256 x 1000 logits on 4 blocks.)
 __global__ __launch_bounds__(256) void colsum_kernel(const unsigned short* __restrict__ dl, int B,
                                                      int J, float* __restrict__ db) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= J) return;
+  __shared__ float red[16][17];
+  const int cl = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  const int j = blockIdx.x * 16 + cl;
   float s = 0.f;
-  for (int b = 0; b < B; ++b) s += bf2f(dl[(size_t)b * J + j]);
-  db[j] += s;
+  if (j < J) {
+    int b = rg;
+    for (; b + 48 < B; b += 64) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = bf2f(dl[(size_t)(b + 16 * u) * J + j]);
+      s += (v[0] + v[1]) + (v[2] + v[3]);
+    }
+    for (; b < B; b += 16) s += bf2f(dl[(size_t)b * J + j]);
+  }
+  red[rg][cl] = s;
+  __syncthreads();
+  if (rg || j >= J) return;
+  float t = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) t += red[r][cl];
+  db[j] += t;
 }
 
 }  // namespace ddp_amd
@@ -186,7 +228,7 @@ extern "C" int ddp_maxpool_bwd(const void* dy, const void* idx, int N, int H, in
 
 extern "C" int ddp_avgpool_fwd(const void* x, int N, int HW, int C, void* y, hipStream_t st) {
   if (C % 8) return -1;
-  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3((N * (C / 8) + 255) / 256), dim3(256), 0, st,
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3((N * (C / 8) + 63) / 64), dim3(256), 0, st,
                      (const unsigned short*)x, N, HW, C, (unsigned short*)y);
   return (int)hipGetLastError();
 }
@@ -199,7 +241,7 @@ extern "C" int ddp_avgpool_bwd(const void* dy, int N, int HW, int C, void* dx, h
 }
 
 extern "C" int ddp_colsum(const void* dl, int B, int J, float* db, hipStream_t st) {
-  hipLaunchKernelGGL(colsum_kernel, dim3((J + 255) / 256), dim3(256), 0, st,
+  hipLaunchKernelGGL(colsum_kernel, dim3((J + 15) / 16), dim3(256), 0, st,
                      (const unsigned short*)dl, B, J, db);
   return (int)hipGetLastError();
 }

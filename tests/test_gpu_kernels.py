@@ -511,6 +511,22 @@ def test_maxpool3x3s2_and_avgpool(native_ext):
     a = global_avg_pool(xn.detach().requires_grad_(True))
     ar = x.mean((2, 3))
     assert rel_err(a, ar) < 1e-2
+    # ResNet head shape (7x7, 2048 channels) and an odd one: 4 waves split the pixels
+    for (n, c, hw) in ((8, 2048, 7), (3, 24, 5)):
+        x2 = bf(torch.randn(n, c, hw, hw, device=DEV))
+        a2 = global_avg_pool(x2.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16))
+        assert rel_err(a2, x2.mean((2, 3))) < 1e-2
+
+
+@pytest.mark.parametrize("B,J", [(256, 1000), (37, 10), (64, 17)])
+def test_colsum_bias_grad(native_ext, B, J):
+    """Bias gradient of the GEMM Linear: db += column sums of bf16 dlogits (pool.hip colsum)."""
+    from ddp_amd.ops.common import ptr, stream_handle
+    dl = bf(torch.randn(B, J, device=DEV)).to(torch.bfloat16)
+    db = torch.full((J,), 0.5, device=DEV)
+    native_ext.colsum(ptr(dl), B, J, ptr(db), stream_handle())
+    torch.cuda.synchronize()
+    assert torch.allclose(db, 0.5 + dl.float().sum(0), rtol=1e-5, atol=1e-4)
 
 
 def test_fused_sgd_zero_grad_and_counter(native_ext):
