@@ -32,6 +32,7 @@
 #include "api.h"
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 namespace ddp_amd {
@@ -1163,13 +1164,29 @@ static bool pool3_shape_ok(const BnArgs& a, int* Ho, int* Wo) {
   return (size_t)a.N * a.H * a.W * a.C < (1ull << 31);
 }
 
+// grid caps of the stem passes (DDP_AMD_POOL3_GRIDS="fwd,reduce,apply"). Kernel-trace sweep on
+// ResNet-50 b256 (profiles/r5az_pool3_grids.md): 16384 / 2048 / 4096 take 498 us for the three
+// passes against 524 us at the previous 8192 / 4096 / 16384
+static void pool3_grids(unsigned* g) {
+  static unsigned v[3] = {16384, 2048, 4096};
+  static const bool init = [] {
+    if (const char* e = std::getenv("DDP_AMD_POOL3_GRIDS"))
+      std::sscanf(e, "%u,%u,%u", &v[0], &v[1], &v[2]);
+    return true;
+  }();
+  (void)init;
+  g[0] = std::max(1u, v[0]); g[1] = std::max(1u, v[1]); g[2] = std::max(1u, v[2]);
+}
+
 extern "C" int ddp_bn_pool3_fwd(const BnArgs* args, unsigned char* idx, hipStream_t st) {
   const BnArgs a = *args;
   int Ho, Wo;
   if (!pool3_shape_ok(a, &Ho, &Wo) || idx == nullptr) return -1;
+  unsigned caps[3];
+  pool3_grids(caps);
   hipLaunchKernelGGL(bn_finalize_fwd_kernel, dim3(blocks_for(a.C, 256)), dim3(256), 0, st, a);
   const size_t items = (size_t)a.N * Ho * Wo * (a.C / 8);
-  const unsigned nb = (unsigned)std::min<size_t>(blocks_for(items, 256), 8192);
+  const unsigned nb = (unsigned)std::min<size_t>(blocks_for(items, 256), caps[0]);
   hipLaunchKernelGGL(bn_pool3_fwd_kernel, dim3(nb), dim3(256), 0, st, a, Ho, Wo, idx);
   return (int)hipGetLastError();
 }
@@ -1182,9 +1199,11 @@ extern "C" int ddp_bn_pool3_bwd(const BnArgs* args, const unsigned char* idx, hi
     return -1;
   const size_t nq = (size_t)a.N * Ho * Wo;  // 2x2 pre-pool quads
   const size_t per = 256 / (a.C / 8);
+  unsigned caps[3];
+  pool3_grids(caps);
   // reduce: ~4 quad iterations per thread (fewer replica atomics); apply: one pass
-  const unsigned nr = (unsigned)std::max<size_t>(1, std::min<size_t>(blocks_for(nq, per * 4), 4096));
-  const unsigned na = (unsigned)std::min<size_t>(blocks_for(nq, per), 16384);
+  const unsigned nr = (unsigned)std::max<size_t>(1, std::min<size_t>(blocks_for(nq, per * 4), caps[1]));
+  const unsigned na = (unsigned)std::min<size_t>(blocks_for(nq, per), caps[2]);
   hipLaunchKernelGGL((bn_pool3_bwd_kernel<false>), dim3(nr), dim3(256), 0, st, a, Ho, Wo, idx);
   hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3(blocks_for(a.C, 256)), dim3(256), 0, st, a);
   hipLaunchKernelGGL((bn_pool3_bwd_kernel<true>), dim3(na), dim3(256), 0, st, a, Ho, Wo, idx);
