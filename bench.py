@@ -81,25 +81,45 @@ def parse():
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--train-size", type=int, default=None)
     p.add_argument("--json-out", default=None)
-    p.add_argument("--launch-timeout", type=float, default=3600.0,
-                   help="self-launch (--gpus N > 1 without torchrun): kill every rank and fail "
-                        "after this many seconds")
+    p.add_argument("--attempt-timeout", type=float, default=480.0,
+                   help="N > 1: kill an attempt's ranks after this many seconds and fall back "
+                        "(utils/ladder.py)")
+    p.add_argument("--no-fallback", action="store_true",
+                   help="N > 1: run the given plan once, without the fallback ladder "
+                        "(utils/ladder.py: planned -> inline captured DDP -> eager DDP)")
+    p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                   help="cpu: the same protocol on ATen + Gloo (fp32, eager; the multi-rank "
+                        "launch / fallback / JSON plumbing without a GPU)")
     return p.parse_args()
 
 
 def launch_or_check(args):
-    """``--gpus N`` without an outer launcher spawns N ranks of this script (one process per
-    GPU, ddp_amd/utils/launch.py) and returns the parent's exit code; under a launcher it checks
-    that WORLD_SIZE matches --gpus. Returns None when this process is a rank that should run."""
-    from ddp_amd.utils.launch import self_launch, under_launcher
+    """``--gpus N`` (N > 1) runs the ranks as attempts of the fallback ladder (utils/ladder.py):
+    without an outer launcher this process spawns the N ranks of each attempt itself; as one
+    rank of an outer launcher (torchrun) it supervises its own rank's child of each attempt.
+    Either way it makes no GPU call and returns the exit code. Returns None when this process is
+    a rank that should run (N = 1, an attempt's child, or --no-fallback under a launcher)."""
+    from ddp_amd.utils import ladder
+    from ddp_amd.utils.launch import self_launch, under_launcher, visible_devices
+    attempts = ladder.default_attempts(args.strategy)
     if not under_launcher():
-        if args.gpus > 1:
-            return self_launch(__file__, sys.argv[1:], args.gpus, timeout_s=args.launch_timeout)
-        return None
+        if args.gpus <= 1:
+            return None
+        if args.device == "cuda" and visible_devices() < args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} but only {visible_devices()} GPU(s) visible: "
+                             f"refusing to run {args.gpus} ranks on fewer devices")
+        if args.no_fallback:
+            return self_launch(__file__, sys.argv[1:], args.gpus, timeout_s=args.attempt_timeout,
+                               require_devices=False)
+        return ladder.run_self(__file__, sys.argv[1:], args.gpus, attempts,
+                               timeout_s=args.attempt_timeout)
     world = int(os.environ["WORLD_SIZE"])
     if world != args.gpus:
         raise SystemExit(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report "
                          f"a {world}-rank run as {args.gpus} GPUs")
+    if world > 1 and not args.no_fallback and os.environ.get(ladder.CHILD_ENV) != "1":
+        return ladder.run_under_launcher(__file__, sys.argv[1:], attempts,
+                                         timeout_s=args.attempt_timeout)
     return None
 
 
@@ -108,6 +128,12 @@ def main():
     rc = launch_or_check(args)
     if rc is not None:
         sys.exit(rc)
+    if args.device == "cpu":
+        sys.exit(run_cpu(args))
+    sys.exit(run_gpu(args))
+
+
+def run_gpu(args):
     import torch
     import torch.distributed as dist
     import ddp_amd
@@ -118,7 +144,7 @@ def main():
     from ddp_amd.optim import FusedSGD
     from ddp_amd.parallel import (DistributedDataParallel, RcclCommunicator, STRATEGIES,
                                   check_replicas)
-    from ddp_amd.utils import Watchdog, seed_everything
+    from ddp_amd.utils import Watchdog, fault_point, ladder, seed_everything
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -131,6 +157,9 @@ def main():
     device = torch.device("cuda", local_rank)
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)  # control plane (TCPStore)
+    # failure tests: "bench" fires in every fallback attempt, "bench<k>" in attempt k only
+    fault_point(rank, "bench")
+    fault_point(rank, "bench" + os.environ.get(ladder.ATTEMPT_ENV, "0"))
     comm = RcclCommunicator(rank, world, local_rank)
     # proof of the rank count: what RCCL itself reports for the data-plane communicator
     rccl_ranks = comm.comm.count()
@@ -354,6 +383,115 @@ def main():
         watchdog.stop()
     if world > 1:
         dist.destroy_process_group()
+    # a result whose replicas diverged is not reported as a success (the ladder falls back)
+    return 0 if consistent else ladder.RC_REPLICAS
+
+
+def run_cpu(args):
+    """The benchmark protocol on the CPU (ATen kernels, Gloo, fp32, eager steps): warm-up, K
+    timed steps between barriers, max over ranks, rank 0's JSON line. Exercises the multi-rank
+    launch, the fallback ladder and the JSON contract without a GPU (tests/test_bench_cpu.py);
+    its numbers are CPU numbers (``"device": "cpu"``)."""
+    import torch
+    import torch.distributed as dist
+    import ddp_amd
+    from ddp_amd.data import SyntheticCIFAR10
+    from ddp_amd.data.loader import CPULoader
+    from ddp_amd.engine import CrossEntropyLoss
+    from ddp_amd.models import build
+    from ddp_amd.optim import FusedSGD
+    from ddp_amd.parallel import (DistributedDataParallel, STRATEGIES, TorchCommunicator,
+                                  check_replicas)
+    from ddp_amd.utils import Watchdog, fault_point, ladder, seed_everything
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    torch.set_num_threads(int(os.environ.get("DDP_AMD_CPU_THREADS", "1")))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    fault_point(rank, "bench")
+    fault_point(rank, "bench" + os.environ.get(ladder.ATTEMPT_ENV, "0"))
+    watchdog = None
+    wd_s = float(os.environ.get("DDP_AMD_WATCHDOG_S", "300"))
+    if world > 1 and wd_s > 0:
+        watchdog = Watchdog(timeout_s=wd_s, poll_s=min(1.0, wd_s / 4)).start()
+    seed_everything(ddp_amd.SEED)
+    B = args.per_gpu_batch or int((args.global_batch or 256) / world)
+    scaling = "weak" if args.per_gpu_batch else "strong"
+    loader = CPULoader(SyntheticCIFAR10(True, n=args.train_size), B, world, rank)
+    model = build(args.model)
+    comm = TorchCommunicator() if world > 1 else None
+    sync = None
+    if comm is not None and args.strategy == "ddp":
+        model = DistributedDataParallel(model, comm, bucket_cap_mb=25, first_bucket_cap_mb=1)
+    elif comm is not None:
+        fn = STRATEGIES[args.strategy]
+        sync = lambda m: fn(m, comm)  # noqa: E731
+    lr = args.lr if args.lr is not None else 0.1
+    opt = FusedSGD(model.parameters(), lr=lr, momentum=0.9, weight_decay=1e-4)
+    crit = CrossEntropyLoss()
+    batches = iter(())
+    loss_sum = [0.0]
+
+    def step():
+        nonlocal batches
+        try:
+            x, y = next(batches)
+        except StopIteration:
+            batches = iter(loader)
+            x, y = next(batches)
+        opt.zero_grad()
+        loss = crit(model(x), y)
+        loss.backward()
+        if sync is not None:
+            sync(model)
+        opt.step()
+        loss_sum[0] += float(loss.item())
+        if watchdog is not None:
+            watchdog.beat()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    loss_sum[0] = 0.0
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    arena = model.arena if hasattr(model, "arena") else opt.arena
+    consistent = check_replicas(arena, world)
+    ms = elapsed / max(args.steps, 1) * 1000.0
+    value = B * world * args.steps / elapsed
+    out = {
+        "metric": "images/sec (whole node) VGG-11 CIFAR-10", "value": round(value, 2),
+        "unit": "images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": scaling,
+        "vs_baseline": round(value / BASELINE_IMG_S, 2), "dtype": "fp32", "device": "cpu",
+        "data": "synthetic (CIFAR-10-shaped 3x32x32, 10 classes; random-init weights)",
+        "config": {"model": args.model, "global_batch": B * world, "per_gpu_batch": B,
+                   "seq_len": None, "parallelism": f"dp{world}", "strategy": args.strategy,
+                   "hipgraph": False, "comm": "gloo"},
+        "launcher": os.environ.get("DDP_AMD_LAUNCHER", "torchrun" if "TORCHELASTIC_RUN_ID"
+                                   in os.environ else ("env" if world > 1 else "single-process")),
+        "train_loss_mean": round(loss_sum[0] / max(args.steps, 1), 4),
+        "replicas_consistent": consistent,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if watchdog is not None:
+        watchdog.stop()
+    if world > 1:
+        dist.destroy_process_group()
+    return 0 if consistent else ladder.RC_REPLICAS
 
 
 def choose_cuts_on_node(model, opt, criterion, loader, args, world, comm_table):
@@ -390,7 +528,10 @@ def choose_cuts_on_node(model, opt, criterion, loader, args, world, comm_table):
     stage_us = [float(v) for v in t]
     rows, table_src = rows_for(comm_table or load_table(), world, args.grad_comm)
     wire = 0.5 if args.grad_comm == "bf16" else 1.0
-    upd = "auto" if (args.update == "auto" and args.grad_comm == "fp32" and not args.zero) else \
+    # 'auto' may pick the sharded update for a bucket only when THIS node's reduce-scatter and
+    # all-gather were measured by the start-up probe (never from the model table alone)
+    upd = "auto" if (args.update == "auto" and args.grad_comm == "fp32" and not args.zero
+                     and shard_columns_measured(comm_table, world)) else \
         ("shard16" if args.update == "shard16" else "allreduce")
     best, ranked = plan_cuts(stage_us, pbytes, rows, wire_scale=wire, update=upd, world=world,
                              seg_overhead_us=seg_boundary_us(loader.batch_size))
@@ -430,10 +571,14 @@ def choose_update(args, model, cuts, world, comm_table, cut_plan, plan_world):
     even = plan_world >= 1 and all((hi - lo) % plan_world == 0 and ((hi - lo) // plan_world) % 4 == 0
                                    for lo, hi in ranges)
     allowed = args.grad_comm == "fp32" and not args.zero and even
-    if args.update == "allreduce" or not allowed or (plan_world <= 1 and args.update == "auto"):
+    emu_gbps = float(os.environ.get("DDP_AMD_EMULATE_COMM_GBPS", "0"))
+    measured = shard_columns_measured(comm_table, world) or (world == 1 and emu_gbps > 0)
+    if args.update == "allreduce" or not allowed or (plan_world <= 1 and args.update == "auto") \
+            or (args.update == "auto" and not measured):
         why = ("forced" if args.update == "allreduce" else "one rank: nothing to shard"
                if plan_world <= 1 else "sharded plan not applicable (bf16 wire, --zero or "
-               "uneven shards)")
+               "uneven shards)" if not allowed else "no measured reduce-scatter / all-gather "
+               "curve on this node: all-reduce")
         if args.update == "shard16" and not allowed:
             raise SystemExit("--update shard16 needs --grad-comm fp32, no --zero and buckets "
                              f"divisible by {plan_world} ranks")
@@ -442,7 +587,6 @@ def choose_update(args, model, cuts, world, comm_table, cut_plan, plan_world):
         return {"update": ["s16"] * nb, "source": "forced"}
     if cut_plan is not None and cut_plan.get("update") and len(cut_plan["update"]) == nb:
         return {"update": list(cut_plan["update"]), "source": "cut planner"}
-    emu_gbps = float(os.environ.get("DDP_AMD_EMULATE_COMM_GBPS", "0"))
     if world == 1 and emu_gbps > 0:  # one-GPU stand-in study: price the stand-in itself
         from ddp_amd.parallel.cut_plan import stand_in_rows
         rows, src = stand_in_rows(plan_world, emu_gbps), f"stand-in {emu_gbps:g} GB/s"
@@ -456,6 +600,17 @@ def choose_update(args, model, cuts, world, comm_table, cut_plan, plan_world):
         costs.append({"bytes": 4 * (hi - lo), "ar_us": round(t_ar + u_ar, 1),
                       "s16_us": round(t_s + u_s, 1)})
     return {"update": out, "source": f"priced on {src}", "bucket_costs": costs}
+
+
+def shard_columns_measured(comm_table, world):
+    """True when the start-up probe measured this node's reduce-scatter and bf16 all-gather
+    times (parallel/bucket_plan.py probe_table): the only basis on which --update auto may
+    choose the sharded update."""
+    if not comm_table:
+        return False
+    from ddp_amd.parallel.bucket_plan import rows_for
+    rows, _ = rows_for(comm_table, world, "fp32")
+    return bool(rows) and all("rs_us" in r and "ag16_us" in r for r in rows)
 
 
 def native_version():

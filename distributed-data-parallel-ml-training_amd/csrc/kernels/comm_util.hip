@@ -40,11 +40,12 @@ __global__ __launch_bounds__(256) void scale_kernel(float* x, size_t n, float s)
 
 __global__ __launch_bounds__(256) void comm_standin_kernel(float* x, size_t n, long long ticks,
                                                            float scale, int passes) {
-  // one read + write pass over the bucket (x *= scale: with scale != 1 a consumer that does not
-  // wait for the collective reads the old values, tests), then hold the CU until the modelled
-  // time has elapsed since the kernel started: the modelled collective time INCLUDES its own
-  // memory traffic, as an RCCL kernel's does (until round 4 the pass ran after the full wait,
-  // adding ~20-30 us per 19 MB bucket on top of the model)
+  // one read + write pass over the bucket, then hold the CU until the modelled time has
+  // elapsed since the kernel started: the modelled collective time INCLUDES its own memory
+  // traffic, as an RCCL kernel's does (until round 4 the pass ran after the full wait, adding
+  // ~20-30 us per 19 MB bucket on top of the model).
+  // scale != 1 (tests): the scaling pass is the LAST thing the kernel does, after the whole
+  // modelled time — a consumer that does not wait for the collective reads the old values.
   // passes > 1 ("busy" stand-in): that many paced read + write passes spread over the modelled
   // time instead of one pass and a sleep — the memory traffic of a live collective (a ring
   // all-reduce reads and writes its bucket ~2 (w-1)/w times each way) beside the backward
@@ -52,6 +53,10 @@ __global__ __launch_bounds__(256) void comm_standin_kernel(float* x, size_t n, l
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (int p = 0; p < passes; ++p) {
     const float sc = p == passes - 1 ? scale : 1.f;
+    const long long until = t0 + ticks * (p + 1) / passes;
+    const bool late = sc != 1.f;  // write late: wait first
+    if (late)
+      while (wall_clock64() - until < 0) __builtin_amdgcn_s_sleep(4);
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n / 4; i += stride) {
       float4 v = reinterpret_cast<float4*>(x)[i];
       v.x *= sc; v.y *= sc; v.z *= sc; v.w *= sc;
@@ -60,8 +65,8 @@ __global__ __launch_bounds__(256) void comm_standin_kernel(float* x, size_t n, l
     }
     if (blockIdx.x == 0)
       for (size_t i = (n / 4) * 4 + threadIdx.x; i < n; i += blockDim.x) x[i] *= sc;
-    const long long until = t0 + ticks * (p + 1) / passes;
-    while (wall_clock64() - until < 0) __builtin_amdgcn_s_sleep(4);
+    if (!late)
+      while (wall_clock64() - until < 0) __builtin_amdgcn_s_sleep(4);
   }
 }
 

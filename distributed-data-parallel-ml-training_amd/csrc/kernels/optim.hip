@@ -125,6 +125,17 @@ struct SgdHyper {
 
 // Last-block-done hand-off: every block's writes are fenced, the block that takes the last
 // ticket resets the ticket and release-increments the flag (acquired by flag_wait_kernel).
+// The step's error word (SegmentedDDPStep: a device-side wait timed out), read ONCE per block:
+// every thread of the block takes the same branch, so no thread can leave while others still
+// wait at a barrier of a tile item or of last_block_done (the word may flip during the launch).
+__device__ __forceinline__ bool block_skip(const unsigned* skip) {
+  if (!skip) return false;  // (a kernel argument: uniform)
+  __shared__ unsigned s_skip;
+  if (threadIdx.x == 0) s_skip = __hip_atomic_load(skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  return s_skip != 0u;
+}
+
 __device__ __forceinline__ bool last_block_done(unsigned* done) {
   __syncthreads();
   __shared__ unsigned last;
@@ -168,7 +179,7 @@ __device__ void sgd_pack_body(const int4* __restrict__ items, const long long* _
   const int4 it = items[blockIdx.x];
   const int tid = threadIdx.x;
   if (h.counter && blockIdx.x == 0 && tid == 0) atomicAdd(h.counter, h.delta);
-  if (h.skip && __hip_atomic_load(h.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return;
+  if (block_skip(h.skip)) return;
   if (it.x == 0) {
     const size_t off = (size_t)(unsigned)it.y;
     const int cnt = it.z;
@@ -351,7 +362,7 @@ struct TailArgs {
 };
 
 __global__ __launch_bounds__(256) void shard_tail_kernel(TailArgs a) {
-  const bool skipped = a.skip && __hip_atomic_load(a.skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+  const bool skipped = block_skip(a.skip);
   if (!skipped && (int)blockIdx.x < a.n_segs) {
     const int4 e = a.segs[blockIdx.x];
     const float* s = a.src + (size_t)(unsigned)e.x;

@@ -359,6 +359,17 @@ class SegmentedDDPStep(TrainStep):
         # events recorded on the comm stream around each bucket's collective + update
         self.probe = None
 
+    def tail_step(self, x, y):
+        """The epoch's partial last batch as one eager step. With a sharded update the masters
+        and momentum are authoritative only on their shard owners and the replicated update of
+        TrainStep.tail_step would diverge the replicas: refused (train full batches only, or
+        use the all-reduce plan)."""
+        if self.shard16 is not None or self.zero is not None:
+            raise RuntimeError("SegmentedDDPStep: a partial batch needs the all-reduce update "
+                               "(the sharded update keeps masters / momentum on shard owners)")
+        torch.cuda.current_stream().wait_stream(self.comm_stream)
+        super().tail_step(x, y)
+
     def _probe_event(self, stream):
         ev = torch.cuda.Event(enable_timing=True)
         ev.record(stream)

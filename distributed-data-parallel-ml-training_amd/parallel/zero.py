@@ -384,16 +384,19 @@ class ShardedBf16Update:
 
     @torch.no_grad()
     def gather_masters(self, stream=None):
-        """All-gather the fp32 masters of every sharded bucket (check_replicas, state_dict):
-        afterwards every rank holds the owners' values everywhere. On the CPU the model's
-        parameters then hold the fp32 masters too (until the next step re-materialises the
-        operands)."""
+        """All-gather the fp32 masters AND the momentum buffers of every sharded bucket
+        (check_replicas, optimizer / checkpoint state_dict, an eager step after the replays):
+        a rank updates both only on its own shard, so afterwards every rank holds the owners'
+        values everywhere. On the CPU the model's parameters then hold the fp32 masters too
+        (until the next step re-materialises the operands)."""
         if self.emulated:
             return
         for j in sorted(self.which):
             (_, (lo, hi)) = self.buckets[j]
             buf = self.arena.data if self.cuda else self.master
+            mom = self.opt.momentum_buffer if self.cuda else self.momentum
             self.comm.all_gather_inplace(buf[lo:hi], stream=stream)
+            self.comm.all_gather_inplace(mom[lo:hi], stream=stream)
         if not self.cuda:
             self.arena.data.copy_(self.master)
 
@@ -413,13 +416,18 @@ class ShardedBf16Update:
         s0, s1 = self.shard(j)
         a, g = self.arena, self.opt.param_groups[0]
         lr, m, wd = float(g["lr"]), float(g["momentum"]), float(g["weight_decay"])
+        nesterov, gs = bool(g["nesterov"]), float(self.opt._grad_scale_factor)
         self.comm.reduce_scatter_inplace(a.grad[lo:hi], AVG)
-        # torch.optim.SGD's per-element math (momentum buffer = d on the first step == m*0 + d)
+        # the GPU launch's per-element math (common.h sgd_update1 = torch.optim.SGD's, momentum
+        # buffer = d on the first step == m*0 + d): d = g*scale + wd*p; b = m*b + d;
+        # d = nesterov ? d + m*b : b; p -= lr*d
         p, gr, buf = self.master[s0:s1], a.grad[s0:s1], self.momentum[s0:s1]
-        d = gr.add(p, alpha=wd) if wd != 0 else gr.clone()
+        d = gr * gs if gs != 1.0 else gr.clone()
+        if wd != 0:
+            d.add_(p, alpha=wd)
         if m != 0:
             buf.mul_(m).add_(d)
-            d = buf
+            d = d.add(buf, alpha=m) if nesterov else buf
         p.add_(d, alpha=-lr)
         self.data16[s0:s1] = p.to(torch.bfloat16)
         row = self.slots[plan["slot_base"] + self.rank * plan["M"]:

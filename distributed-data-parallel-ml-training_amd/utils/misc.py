@@ -99,13 +99,14 @@ def load_checkpoint(path, model, optimizer=None, map_location="cpu"):
 
 def fault_point(rank, batch_idx):
     """Fault injection for the failure-detection tests:
-    ``DDP_AMD_FAULT_INJECT=<rank>:<batch>[:exit|hang]`` makes that rank die (``os._exit(17)``)
-    or stop making progress (sleep forever) when it reaches that batch of the epoch."""
+    ``DDP_AMD_FAULT_INJECT=<rank>:<point>[:exit|hang]`` makes that rank die (``os._exit(17)``)
+    or stop making progress (sleep forever) when it reaches that point: a batch index of the
+    epoch, or a named point (``bench<k>``: bench.py start-up in fallback attempt k)."""
     spec = os.environ.get("DDP_AMD_FAULT_INJECT")
     if not spec:
         return
     parts = spec.split(":")
-    if int(parts[0]) != int(rank) or int(parts[1]) != int(batch_idx):
+    if int(parts[0]) != int(rank) or parts[1] != str(batch_idx):
         return
     mode = parts[2] if len(parts) > 2 else "exit"
     print(f"[ddp_amd] fault injected on rank {rank} at batch {batch_idx}: {mode}",

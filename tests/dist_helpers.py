@@ -405,14 +405,18 @@ def shard16_worker(rank, world, port, q, steps):
                 out["operands_consistent"] = check_replicas(a, world)
                 upd.gather_masters()
                 out[mode] = upd.master.clone()
+                out[mode + "_momentum"] = upd.momentum.clone()  # gathered from the owners
                 out["data_is_master"] = bool(torch.equal(a.data, upd.master))
                 out["masters_consistent"] = check_replicas(a, world)
             else:
                 out[mode] = master.clone()
+                out[mode + "_momentum"] = mom.clone()
         dist.destroy_process_group()
         q.put((rank, {"replicated": out["replicated"].numpy(), "shard16": out["shard16"].numpy(),
                       "replicated_operand": out["replicated_operand"].numpy(),
                       "shard16_operand": out["shard16_operand"].numpy(),
+                      "replicated_momentum": out["replicated_momentum"].numpy(),
+                      "shard16_momentum": out["shard16_momentum"].numpy(),
                       "grad_zero": out["grad_zero"], "shards": out["shards"],
                       "operands_consistent": out["operands_consistent"],
                       "masters_consistent": out["masters_consistent"],

@@ -92,3 +92,17 @@ def test_sharding_only_where_every_bucket_divides(world):
             bench.choose_update(_args("shard16"), m, [3, 6], world, None, None, world)
     else:
         assert "s16" in plan["update"]
+
+
+def test_auto_never_shards_without_measured_shard_columns():
+    """--update auto may choose s16 only from THIS node's measured reduce-scatter / all-gather
+    times (advisor round 5): the model table or a probe without those columns -> all-reduce."""
+    m = _Model()
+    t = _table(8, 1.0)
+    for r in t["worlds"]["8"]["fp32"]:
+        del r["rs_us"], r["ag16_us"]
+    plan = bench.choose_update(_args(), m, [3, 6], 8, t, None, 8)
+    assert plan["update"] == ["ar"] * 3 and "measured" in plan["source"]
+    assert bench.choose_update(_args(), m, [3, 6], 8, None, None, 8)["update"] == ["ar"] * 3
+    assert not bench.shard_columns_measured(None, 8)
+    assert bench.shard_columns_measured(_table(8, 1.0), 8)
