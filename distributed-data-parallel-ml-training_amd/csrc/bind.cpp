@@ -335,8 +335,8 @@ PYBIND11_MODULE(_native, m) {
   });
   m.def("conv_pair_mode", [](int mode, int items) { ddp_conv_pair_mode(mode, items); },
         py::arg("mode"), py::arg("items") = 0);
-  m.def("conv_pair_force", [](int sd, int sw) { ddp_conv_pair_force(sd, sw); },
-        py::arg("splits_dg"), py::arg("splits_wg"));
+  m.def("conv_pair_force", [](int sd, int sw, int tile) { ddp_conv_pair_force(sd, sw, tile); },
+        py::arg("splits_dg"), py::arg("splits_wg"), py::arg("tile") = 0);
   // final = 1: no DGRAD of this layer follows (its finish may apply a registered SGD step)
   m.def("conv_wgrad", [](py::tuple g, uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws,
                          size_t ws_elems, int splits, uintptr_t st, int final_) {

@@ -294,7 +294,7 @@ int ddp_sgd_fuse_taken(uintptr_t* out, int cap);
 // gradient views whose MASTER a pair's unsplit WGRAD epilogue updated (operand re-pack pending)
 int ddp_sgd_fuse_taken_master(uintptr_t* out, int cap);
 // sweeps (tools/conv_tune.py --pairs): force the paired launch with these split-K factors (0 = off)
-void ddp_conv_pair_force(int splits_dg, int splits_wg);
+void ddp_conv_pair_force(int splits_dg, int splits_wg, int tile);
 int ddp_conv_bwd_pair(const ddp_amd::ConvGeom* g, const void* dy, const void* wc, void* dx,
                       const void* x, float* dw, float* ws, size_t ws_elems,
                       const ddp_amd::BnBwdFuse* bn, const ddp_amd::BnBwdApply* ba, int* bn_done,

@@ -320,6 +320,17 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
   int kr = 0, ks_ = 0, kc = 0;  // slow path: (r, s, c) of this thread's chunk; fast path: uniform
   KInfo xk;              // WGRAD: (r,s,c) of this thread's B' column group
   int xk_same = 0;       // WGRAD "same" conv: byte offset of tap (r,s) channel c relative to m
+  // WGRAD "same" conv (stride 1, P == H, Q == W): the B' gather walks the reduction rows m of
+  // each chunk 64 at a time, so its pixel (p, q) = ((m mod PQ) / Q, m mod Q) is carried from
+  // k-step to k-step with adds and one conditional wrap each (no per-k-step divides or
+  // multiplies: those made this gather VALU-bound, ~30 integer ops incl. 4-5 quarter-rate
+  // multiplies per 16-B chunk). b_off[i] = byte offset of the chunk's (m, tap, c) in x.
+  int wp[CB], wq[CB];
+  int w_rr = 0, w_ss = 0, w_lim = 0;  // tap offsets r - pad, s - pad; b_off bound (m < Kg)
+  const bool wsame = MODE == MODE_WGRAD && gg.stride == 1 && gg.P == gg.H && gg.Q == gg.W;
+  const int w_dq = wsame ? BK % gg.Q : 0;                 // q advance per k-step
+  const int w_dp = wsame ? (BK / gg.Q) % gg.P : 0;        // p advance per k-step (mod P)
+  const int w_dm = wsame ? 2 * BK * gg.C : 0;             // byte advance per k-step
   int row0 = 0, col0 = 0, zsplit = 0, ks_begin = 0, ks_end = 0, cur_tile = 0;
   int d2pos = 0;         // dense 2x2: the column tile's output pixel (FWD) / input pixel (DGRAD)
   const bool phase = MODE == MODE_DGRAD && args.phase;
@@ -417,7 +428,22 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
       xk.s = rs - xk.r * gg.S;
       xk.ok = j < args.Ng;
       if (!xk.ok) xk.r = -(1 << 20);  // every border test fails -> zeros
-      xk_same = 2 * (((xk.r - gg.pad) * gg.W + (xk.s - gg.pad)) * gg.C + xk.c);
+      xk_same = xk.ok ? 2 * (((xk.r - gg.pad) * gg.W + (xk.s - gg.pad)) * gg.C + xk.c) : 0;
+      if (wsame) {
+        constexpr int NCB = BN / 8;
+        const int pq = gg.P * gg.Q;
+        w_rr = xk.r - gg.pad;
+        w_ss = xk.s - gg.pad;
+        w_lim = args.Kg * (2 * gg.C) + xk_same;
+#pragma unroll
+        for (int i = 0; i < CB; ++i) {
+          const int m = ks_begin * BK + (tid + i * 256) / NCB;
+          const int rem = m % pq;
+          wp[i] = rem / gg.Q;
+          wq[i] = rem - wp[i] * gg.Q;
+          b_off[i] = m * (2 * gg.C) + xk_same;
+        }
+      }
     }
   };
 
@@ -508,17 +534,22 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
         dma_buf(rsA, a_off[i] + ka, As + (wid * 64 + 256 * i) * 8);
       // "same" convolution (stride 1, P == H, Q == W): the input pixel of output pixel m at tap
       // (r, s) is m + (r - pad) * W + (s - pad), so the offset is linear in m; only the border
-      // test needs (p, q)
-      if (gg.stride == 1 && gg.P == gg.H && gg.Q == gg.W) {
+      // test needs (p, q), carried from the previous k-step (wp / wq, set up per item)
+      if (wsame) {
 #pragma unroll
         for (int i = 0; i < CB; ++i) {  // x gather at pixel m for columns (r, s, c..c+7)
-          const int m = k0 + (tid + i * 256) / NCB;
-          const int rem = m - fast_div(m, args.dPQ) * (gg.P * gg.Q);
-          const int p = fast_div(rem, args.dQ);
-          const int q = rem - p * gg.Q;
-          const bool ok = m < args.Kg && (unsigned)(p - gg.pad + xk.r) < (unsigned)gg.H &&
-                          (unsigned)(q - gg.pad + xk.s) < (unsigned)gg.W;
-          dma_buf(rsB, ok ? m * (2 * gg.C) + xk_same : (int)kOOB, Bs + (wid * 64 + 256 * i) * 8);
+          const bool ok = b_off[i] < w_lim && (unsigned)(wp[i] + w_rr) < (unsigned)gg.H &&
+                          (unsigned)(wq[i] + w_ss) < (unsigned)gg.W;
+          dma_buf(rsB, ok ? b_off[i] : (int)kOOB, Bs + (wid * 64 + 256 * i) * 8);
+          // m += 64 for the next k-step (k-steps are issued in order)
+          b_off[i] += w_dm;
+          int q = wq[i] + w_dq;
+          const int cq = q >= gg.Q ? 1 : 0;
+          q -= cq ? gg.Q : 0;
+          int pp = wp[i] + w_dp + cq;
+          pp -= pp >= gg.P ? gg.P : 0;
+          wq[i] = q;
+          wp[i] = pp;
         }
       } else {
 #pragma unroll
@@ -552,52 +583,51 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
                        : mc_off<BN>(m0, wn * WTN + j * 16 + 4 * p);
   }
 
-  auto compute = [&](int buf) {
+  // fragments of one 32-deep half of a k-step (kk = 0 / 32) from LDS buffer ``buf``
+  auto load_frags = [&](int buf, int kk, bf16x8 (&fa)[TM], bf16x8 (&fb)[TN]) {
     const unsigned short* As = smem + buf * STAGE;
     const unsigned short* Bs = As + TILE_A;
-#pragma unroll
-    for (int kk = 0; kk < BK; kk += 32) {
-      bf16x8 fa[TM], fb[TN];
-      // [row][k] tiles: logical chunk kk/8 + (lane>>4); the XOR swizzle is linear in the chunk
-      // index, so the kk = 32 read is the kk = 0 address with chunk bit 2 flipped.
-      // [k][col] tiles: ds_read_b64_tr_b16 — lane 4q+p of each 16-lane group supplies row q,
-      // columns 4p..4p+3; lane i receives column i of the 4 rows; two reads = 8 k-values.
-      if (MODE != MODE_WGRAD) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-          fa[i] = *reinterpret_cast<const bf16x8*>(As + (fa_off[i] ^ (kk ? 32 : 0)));
-      } else {
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const unsigned short* base = As + fa_off[i] + kk * BM;
-          v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)base);
-          v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + 4 * BM));
-          const short8_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-          fa[i] = __builtin_bit_cast(bf16x8, v);
-        }
-      }
-      if (!BKM) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          fb[j] = *reinterpret_cast<const bf16x8*>(Bs + (fb_off[j] ^ (kk ? 32 : 0)));
-      } else {
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const unsigned short* base = Bs + fb_off[j] + kk * BN;
-          v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)base);
-          v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + 4 * BN));
-          const short8_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-          fb[j] = __builtin_bit_cast(bf16x8, v);
-        }
-      }
+    // [row][k] tiles: logical chunk kk/8 + (lane>>4); the XOR swizzle is linear in the chunk
+    // index, so the kk = 32 read is the kk = 0 address with chunk bit 2 flipped.
+    // [k][col] tiles: ds_read_b64_tr_b16 — lane 4q+p of each 16-lane group supplies row q,
+    // columns 4p..4p+3; lane i receives column i of the 4 rows; two reads = 8 k-values.
+    if (MODE != MODE_WGRAD) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
+        fa[i] = *reinterpret_cast<const bf16x8*>(As + (fa_off[i] ^ (kk ? 32 : 0)));
+    } else {
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          // operands swapped (D^T = B^T A^T): each lane ends up owning ONE output row and FOUR
-          // consecutive output columns, so the epilogue stores 8 B (bf16) / 16 B (fp32) per lane
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < TM; ++i) {
+        const unsigned short* base = As + fa_off[i] + kk * BM;
+        v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)base);
+        v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + 4 * BM));
+        const short8_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        fa[i] = __builtin_bit_cast(bf16x8, v);
+      }
     }
+    if (!BKM) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        fb[j] = *reinterpret_cast<const bf16x8*>(Bs + (fb_off[j] ^ (kk ? 32 : 0)));
+    } else {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const unsigned short* base = Bs + fb_off[j] + kk * BN;
+        v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)base);
+        v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + 4 * BN));
+        const short8_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        fb[j] = __builtin_bit_cast(bf16x8, v);
+      }
+    }
+  };
+  auto mma = [&](const bf16x8 (&fa)[TM], const bf16x8 (&fb)[TN]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        // operands swapped (D^T = B^T A^T): each lane ends up owning ONE output row and FOUR
+        // consecutive output columns, so the epilogue stores 8 B (bf16) / 16 B (fp32) per lane
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
   };
 
   // ---------------- epilogue ----------------
@@ -1049,9 +1079,15 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
       if (NST >= 4 && ahead >= 2) wait_dma_barrier<(NST >= 4 ? 2 : 0) * DMA>();
       else if (NST >= 3 && ahead >= 1) wait_dma_barrier<(NST >= 3 ? 1 : 0) * DMA>();
       else wait_dma_barrier<0>();
+      // the first half's fragment reads go out before the next DMA is issued, so their LDS
+      // latency hides behind the gather's address math instead of stalling the MFMAs after it
+      bf16x8 fa0[TM], fb0[TN], fa1[TM], fb1[TN];
+      load_frags(stage, 0, fa0, fb0);
       // every wave finished computing ks-1: its buffer takes k-step ks+NST-1
       if (ks + NST - 1 < ke) issue(ks + NST - 1, stage == 0 ? NST - 1 : stage - 1);
-      compute(stage);
+      load_frags(stage, 32, fa1, fb1);
+      mma(fa0, fb0);
+      mma(fa1, fb1);
       stage = stage + 1 == NST ? 0 : stage + 1;
     }
     epilogue(row0, col0, zsplit, args.splits > 1);
@@ -2300,8 +2336,10 @@ extern "C" void ddp_conv_options(int stages) { g_stages = stages; }
 
 // tile: index into the launch_mode table (0..kNumTiles-1)
 extern "C" void ddp_conv_tune_set(int mode, int M, int N, int K, int tile, int splits, int stages) {
-  if (mode == 3) {  // backward pair: tile = pair on/off, splits / stages = DGRAD / WGRAD splits
-    g_pair_tuned[TuneKey{MODE_DGRAD, M, N, K}] = {tile ? 1 : 0, std::max(1, splits), std::max(1, stages)};
+  if (mode == 3) {  // backward pair: tile = 0 separate / pair tile 1..4 (kPairTiles), splits /
+                    // stages = DGRAD / WGRAD splits
+    g_pair_tuned[TuneKey{MODE_DGRAD, M, N, K}] = {tile >= 0 && tile < 5 ? tile : 1,
+                                                  std::max(1, splits), std::max(1, stages)};
     return;
   }
   if (tile < 0 || tile >= kNumTiles) return;
@@ -2311,9 +2349,11 @@ extern "C" void ddp_conv_tune_clear() {
   g_tuned.clear();
   g_pair_tuned.clear();
 }
-extern "C" void ddp_conv_pair_force(int splits_dg, int splits_wg) {
+static int g_pair_force_tile_req = 0;  // sweeps: 1..4 forces the pair tile
+extern "C" void ddp_conv_pair_force(int splits_dg, int splits_wg, int tile) {
   g_pair_force_dg = splits_dg;
   g_pair_force_wg = splits_wg;
+  g_pair_force_tile_req = tile;
 }
 extern "C" void ddp_conv_force_tile(int tile_plus_one, int stages) {
   g_force_tile = tile_plus_one;
@@ -2690,6 +2730,43 @@ extern "C" void ddp_conv_pair_mode(int m, int items) {
   if (items > 0) g_pair_items = items;
 }
 
+// Tile of a pair launch (both halves share it: one LDS array). Measured pair-table entries
+// (tools/conv_tune.py --pairs) carry it in their ``tile`` field: 0 = separate launches,
+// 1 = 64x64 (3 LDS stages, 3 blocks per CU), 2 = 128x128 (2 stages, 2 per CU), 3 = 64x128 and
+// 4 = 128x64 (3 stages, 2 per CU). The big tiles halve the L2 -> LDS bytes per MFMA of the
+// 64x64 tile, which at b256 needs ~2x the L2 read rate its MFMAs could consume.
+constexpr int kPairTiles = 5;
+template <int BM, int BN, int NST, bool BNF1, bool SGDM>
+static void pair_kernel_launch(const ConvArgs& d, const ConvArgs& w, int itd, int itw,
+                               hipStream_t st) {
+  hipLaunchKernelGGL((conv_bwd_pair_kernel<BM, BN, NST, BNF1 ? 1 : 0, SGDM>), dim3(itd + itw),
+                     dim3(256), 0, st, d, w, itd);
+}
+template <int BM, int BN, int NST>
+static void pair_launch_t(ConvArgs& d, ConvArgs& w, int sd, int sw, float* ws, size_t ws_elems,
+                          int* itd_out, int* itw_out, bool* ok_out, const float* dw,
+                          bool launch, hipStream_t st) {
+  // the slab workspace is split between the two problems
+  const int itd = prepare_cfg<MODE_DGRAD, BM, BN>(d, std::max(1, sd));
+  size_t dneed = needs_finish(MODE_DGRAD, d) ? (size_t)d.splits * d.Mg * d.Ng : 0;
+  dneed = (dneed + 63) / 64 * 64;
+  w.ws = ws + dneed;
+  const int itw = prepare_cfg<MODE_WGRAD, BM, BN>(w, std::max(1, sw));
+  const size_t wneed = needs_finish(MODE_WGRAD, w) ? (size_t)w.splits * w.Mg * w.Ng : 0;
+  *itd_out = itd;
+  *itw_out = itw;
+  *ok_out = dneed + wneed <= ws_elems;
+  if (!launch || !*ok_out) return;
+  // unsplit WGRAD half: SGD on the master in its epilogue (no finish would take it)
+  if (!needs_finish(MODE_WGRAD, w) && w.g.wkrsc && w.g.Creal == w.g.C) w.sgd = sgd_fuse_master(dw);
+  const bool bnf1 = d.has_bnf && d.splits <= 1;
+  const bool sgdm = w.sgd.p != nullptr;
+  if (bnf1 && sgdm) pair_kernel_launch<BM, BN, NST, true, true>(d, w, itd, itw, st);
+  else if (bnf1) pair_kernel_launch<BM, BN, NST, true, false>(d, w, itd, itw, st);
+  else if (sgdm) pair_kernel_launch<BM, BN, NST, false, true>(d, w, itd, itw, st);
+  else pair_kernel_launch<BM, BN, NST, false, false>(d, w, itd, itw, st);
+}
+
 extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* wc, void* dx,
                                  const void* x, float* dw, float* ws, size_t ws_elems,
                                  const BnBwdFuse* bn, const BnBwdApply* ba, int* bn_done,
@@ -2746,7 +2823,7 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
   w.dQ = make_fastdiv(g->Q);
   // measured pair entry (tools/conv_tune.py --pairs) or forced splits (its sweep) first
   bool tuned = false;
-  int sd = 1, sw = 1;
+  int sd = 1, sw = 1, pt = 1;
   if (g_pair_force_dg > 0 && g_pair_force_wg > 0) {
     tuned = true;
     sd = g_pair_force_dg;
@@ -2756,6 +2833,7 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
     if (it != g_pair_tuned.end()) {
       if (!it->second.tile) return separate();
       tuned = true;
+      pt = it->second.tile < kPairTiles ? it->second.tile : 1;
       sd = it->second.splits;
       sw = it->second.stages;
     }
@@ -2784,40 +2862,33 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
   }
   // a dense DGRAD reduces the BatchNorm-backward sums in the finish of its 3x3 view
   if (d.d2x2 && d.has_bnf) sd = std::max(sd, 2);
-  // the slab workspace is split between the two problems
-  const int itd = prepare_cfg<MODE_DGRAD, 64, 64>(d, std::max(1, sd));
-  size_t dneed = needs_finish(MODE_DGRAD, d) ? (size_t)d.splits * d.Mg * d.Ng : 0;
-  dneed = (dneed + 63) / 64 * 64;
-  w.ws = ws + dneed;
-  const int itw = prepare_cfg<MODE_WGRAD, 64, 64>(w, std::max(1, sw));
-  const size_t wneed = needs_finish(MODE_WGRAD, w) ? (size_t)w.splits * w.Mg * w.Ng : 0;
-  if (dneed + wneed > ws_elems) return separate();
+  // the pair's tile: the measured entry's, a forced one (sweeps), else 64x64; the dense 2x2
+  // DGRAD keeps 64x64 (its column tiles pick the weight tap per input pixel)
+  if (g_pair_force_tile_req >= 1 && g_pair_force_tile_req < kPairTiles) pt = g_pair_force_tile_req;
+  if (d.d2x2) pt = 1;
+  // the input block's sums (bn->code) exist only in the split-K finish: without one, or if the
+  // pair would fuse the BN backward into that finish, drop them (the caller runs l0_sums).
+  // (decided on the prepared DGRAD: a dry run of the tile's prepare step)
+  int itd = 0, itw = 0;
+  bool fits = false;
+  auto prep = [&](bool launch) {
+    switch (pt) {
+      case 2: pair_launch_t<128, 128, 2>(d, w, sd, sw, ws, ws_elems, &itd, &itw, &fits, dw, launch, st); break;
+      case 3: pair_launch_t<64, 128, 3>(d, w, sd, sw, ws, ws_elems, &itd, &itw, &fits, dw, launch, st); break;
+      case 4: pair_launch_t<128, 64, 3>(d, w, sd, sw, ws, ws_elems, &itd, &itw, &fits, dw, launch, st); break;
+      default: pair_launch_t<64, 64, 3>(d, w, sd, sw, ws, ws_elems, &itd, &itw, &fits, dw, launch, st); break;
+    }
+  };
+  prep(false);
+  if (!fits) return separate();
   if (g_pair_mode == 3 && !both64 && itd + itw > g_pair_items) return separate();
   if (d.d2x2 && d.has_bnf && d.splits < 2) return separate();
-  // the input block's sums (bn->code) exist only in the split-K finish: without one, or if the
-  // pair would fuse the BN backward into that finish, drop them (the caller runs l0_sums)
   if (bn && bn->code && (!needs_finish(MODE_DGRAD, d) || ba || d.d2x2)) {
     d.has_bnf = 0;
     bn = nullptr;
   }
-  // unsplit WGRAD half: SGD on the master in its epilogue (no finish would take it)
-  if (!needs_finish(MODE_WGRAD, w) && w.g.wkrsc && w.g.Creal == w.g.C) w.sgd = sgd_fuse_master(dw);
-  const bool bnf1 = d.has_bnf && d.splits <= 1;
   const bool l0_sums = d.has_bnf && d.bnf.code != nullptr;  // (a finish exists: checked above)
-  const bool sgdm = w.sgd.p != nullptr;
-  if (bnf1 && sgdm) {
-    hipLaunchKernelGGL((conv_bwd_pair_kernel<64, 64, 3, 1, true>), dim3(itd + itw), dim3(256), 0,
-                       st, d, w, itd);
-  } else if (bnf1) {
-    hipLaunchKernelGGL((conv_bwd_pair_kernel<64, 64, 3, 1>), dim3(itd + itw), dim3(256), 0, st,
-                       d, w, itd);
-  } else if (sgdm) {
-    hipLaunchKernelGGL((conv_bwd_pair_kernel<64, 64, 3, 0, true>), dim3(itd + itw), dim3(256), 0,
-                       st, d, w, itd);
-  } else {
-    hipLaunchKernelGGL((conv_bwd_pair_kernel<64, 64, 3, 0>), dim3(itd + itw), dim3(256), 0, st,
-                       d, w, itd);
-  }
+  prep(true);
   const bool fd = needs_finish(MODE_DGRAD, d), fw = needs_finish(MODE_WGRAD, w);
   struct Allow {  // the finishes below run after both GEMMs of the pair
     Allow() { g_sgd_allow = true; }

@@ -124,23 +124,26 @@ def test_conv_bwd_pair(native_ext, case, mode):
     assert rel_err(dw, wr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("tile", [1, 2, 3, 4])
 @pytest.mark.parametrize("sd,sw", [(1, 1), (1, 8), (3, 4), (6, 1), (4, 24)])
-@pytest.mark.parametrize("case", [(32, 512, 2, 2, 512, 3, 1, 1), (32, 64, 16, 16, 128, 3, 1, 1)])
-def test_conv_bwd_pair_forced_splits(native_ext, case, sd, sw):
-    """The measured pair entries (table mode 3, tools/conv_tune.py --pairs) fix the DGRAD / WGRAD
-    split-K factors of the grouped launch: every (sd, sw) the sweep may pick matches fp32."""
+@pytest.mark.parametrize("case", [(32, 512, 2, 2, 512, 3, 1, 1), (32, 64, 16, 16, 128, 3, 1, 1),
+                                  (32, 256, 4, 4, 512, 3, 1, 1), (16, 128, 8, 8, 256, 3, 1, 1)])
+def test_conv_bwd_pair_forced_splits(native_ext, case, sd, sw, tile):
+    """The measured pair entries (table mode 3, tools/conv_tune.py --pairs) fix the pair tile
+    (1 = 64x64, 2 = 128x128, 3 = 64x128, 4 = 128x64) and the DGRAD / WGRAD split-K factors of the
+    grouped launch: every (tile, sd, sw) the sweep may pick matches fp32."""
     from ddp_amd.ops.layers import conv_backward
     N, Cin, H, W, K, R, stride, pad = case
     conv, spec, x, xn = _conv_setup(N, Cin, H, W, K, R, stride, pad)
     dz = bf(torch.randn(N, K, H, W, device=DEV))
     dzn = dz.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
     dw = torch.zeros_like(conv.weight, memory_format=torch.channels_last)
-    native_ext.conv_pair_force(sd, sw)
+    native_ext.conv_pair_force(sd, sw, tile)
     try:
         dx = conv_backward(spec, xn, dzn, dw, True)
         torch.cuda.synchronize()
     finally:
-        native_ext.conv_pair_force(0, 0)
+        native_ext.conv_pair_force(0, 0, 0)
     xr = x.clone().requires_grad_(True)
     wr = conv.weight.detach().clone().requires_grad_(True)
     F.conv2d(xr, wr, None, stride, pad).backward(dz)

@@ -54,6 +54,9 @@ def main():
     ap.add_argument("--pairs", action="store_true",
                     help="tune the backward pair launch (DGRAD+WGRAD split-K factors, or separate "
                          "launches) of the stride-1 layers instead (--pair-sets)")
+    ap.add_argument("--pair-tiles", default="1,2,3,4",
+                    type=lambda v: [int(t) for t in v.split(",")],
+                    help="pair tiles to sweep (1 = 64x64, 2 = 128x128, 3 = 64x128, 4 = 128x64)")
     ap.add_argument("--pair-sets", default="vgg11:32,64,128,256",
                     help="model:batches[;model:batches], e.g. 'resnet50:256'")
     args = ap.parse_args()
@@ -258,27 +261,34 @@ def tune_pairs(args):
                                 ws.numel(), st, bn=bn)
             Md, Nd, Kd = N * H * W, C, R * R * K
             Mw, Nw, Kw = K, R * R * C, N * H * W
-            n.conv_pair_force(0, 0)
+            n.conv_pair_force(0, 0, 0)
             n.conv_pair_mode(0, 0)
             sep = timeit(call)
             n.conv_pair_mode(pair_mode, 0)
             pol = timeit(call)
             best = (sep, 0, 1, 1)
             kd, kw = (Kd + 63) // 64, (Kw + 63) // 64
-            for sd in (1, 2, 3, 4, 6, 8, 12, 16):
-                if sd > 1 and kd // sd < 2:
-                    continue
-                for sw in (1, 2, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128):
-                    if sw > 1 and kw // sw < 2:
+            # pair tiles (conv_igemm.hip kPairTiles): 1 = 64x64, 2 = 128x128, 3 = 64x128,
+            # 4 = 128x64; a tile with fewer than ~64 work items before split-K is not tried
+            tiles = [t for t, (bm, bn) in {1: (64, 64), 2: (128, 128), 3: (64, 128),
+                                           4: (128, 64)}.items()
+                     if t in args.pair_tiles and
+                     -(-Md // bm) * -(-Nd // bn) + -(-Mw // bm) * -(-Nw // bn) >= 64]
+            for tile in tiles:
+                for sd in (1, 2, 3, 4, 6, 8, 12, 16):
+                    if sd > 1 and kd // sd < 2:
                         continue
-                    need = (sd * Md * Nd if sd > 1 else 0) + (sw * Mw * Nw if sw > 1 else 0) + 64
-                    if need > ws.numel():
-                        continue
-                    n.conv_pair_force(sd, sw)
-                    us = timeit(call)
-                    if us < best[0] * 0.99:
-                        best = (us, 1, sd, sw)
-            n.conv_pair_force(0, 0)
+                    for sw in (1, 2, 4, 6, 8, 12, 16, 24, 32, 48, 64, 96, 128):
+                        if sw > 1 and kw // sw < 2:
+                            continue
+                        need = (sd * Md * Nd if sd > 1 else 0) + (sw * Mw * Nw if sw > 1 else 0) + 64
+                        if need > ws.numel():
+                            continue
+                        n.conv_pair_force(sd, sw, tile)
+                        us = timeit(call)
+                        if us < best[0] * 0.99:
+                            best = (us, tile, sd, sw)
+            n.conv_pair_force(0, 0, 0)
             us, on, sd, sw = best
             ref = min(sep, pol)
             if pol <= us:  # the policy's own choice is (within noise) the best: no entry
@@ -287,7 +297,8 @@ def tune_pairs(args):
             saved += ref - us
             label = f"{model} N{N} {Cr}->{K} {H}x{W} k{R}"
             print(f"{label:32s} separate {sep:6.1f}  policy {pol:6.1f}  -> "
-                  f"{'pair' if on else 'separate'} dg {sd:2d} wg {sw:3d} {us:6.1f} us", flush=True)
+                  f"{f'pair tile {on}' if on else 'separate'} dg {sd:2d} wg {sw:3d} {us:6.1f} us",
+                  flush=True)
             entries.append({"mode": 3, "M": Md, "N": Nd, "K": Kd, "tile": on, "splits": sd,
                             "stages": sw, "us": round(us, 2), "auto_us": round(pol, 2),
                             "shape": label + " bwd pair"})
