@@ -117,7 +117,7 @@ def launch_or_check(args):
     if world != args.gpus:
         raise SystemExit(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report "
                          f"a {world}-rank run as {args.gpus} GPUs")
-    if world > 1 and not args.no_fallback and os.environ.get(ladder.CHILD_ENV) != "1":
+    if world > 1 and not args.no_fallback and ladder.CHILD_ENV not in os.environ:
         return ladder.run_under_launcher(__file__, sys.argv[1:], attempts,
                                          timeout_s=args.attempt_timeout)
     return None
@@ -406,7 +406,7 @@ def run_cpu(args):
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    torch.set_num_threads(int(os.environ.get("DDP_AMD_CPU_THREADS", "1")))
+    torch.set_num_threads(1)  # one core per rank (the CPU tests run several ranks)
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
     fault_point(rank, "bench")

@@ -234,7 +234,7 @@ int ddp_conv_tr_geometry(int BM, int N, int H, int W, int* out7);
 int ddp_linear_head_bwd_bn(const float* dl, const float* W, const void* x, int B, int F, int J,
                            const float* gscale, const ddp_amd::BnBwdFuse* bn,
                            const ddp_amd::BnBwdApply* ba, float* dW, float* db, hipStream_t st);
-// row limit of the BN-fused split-K finishes (default 128 or DDP_AMD_BN_FUSE_MAX_ROWS)
+// row limit of the BN-fused split-K finishes (default 128)
 void ddp_conv_bn_fuse_rows(int rows);
 int ddp_conv_dgrad(const ddp_amd::ConvGeom* g, const void* dy, const void* wt, void* dx,
                    float* ws, size_t ws_elems, int splits, int accumulate, hipStream_t st);
@@ -301,7 +301,7 @@ int ddp_conv_bwd_pair(const ddp_amd::ConvGeom* g, const void* dy, const void* wc
                       hipStream_t st);
 void ddp_conv_tune_set(int mode, int M, int N, int K, int tile, int splits, int stages);
 // dense 2x2 form of 3x3 / s1 / p1 convs over 2x2 images (conv_igemm.hip ConvArgs::d2x2): ok =
-// this geometry takes it (FWD and DGRAD), set = switch it on / off (DDP_AMD_DENSE2X2)
+// this geometry takes it (FWD and DGRAD), set = switch it on / off (tests)
 int ddp_conv_dense2x2_ok(const ddp_amd::ConvGeom* g);
 void ddp_conv_dense2x2_set(int on);
 void ddp_conv_tune_clear();

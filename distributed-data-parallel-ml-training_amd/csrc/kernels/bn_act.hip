@@ -814,19 +814,13 @@ static unsigned blocks_for(size_t items, size_t per_block) {
 // Folding the finalize into the apply kernel costs every block a replica reduction of its
 // channels; worth it (one launch fewer) while that re-read traffic stays small.
 constexpr size_t kFoldBytes = 24u << 20;
-// Big layers: the FOLD kernels on a capped grid (DDP_AMD_BN_FOLD_FWD_GRID blocks walking the
+// Big layers: the FOLD kernels on a capped grid (fold_fwd_grid() blocks walking the
 // item blocks, forward and backward apply) while that grid's replica re-reads stay within
 // kFoldGridBytes. Off by default: at 2048 blocks ResNet-50 b256 ran 26.26 vs 25.68 ms with the
 // separate finalize launches (profiles/r5v_bn_fold.md) — the 25088-block streaming applies
 // lose more to the capped grid than the finalize launch costs.
 constexpr size_t kFoldGridBytes = 64u << 20;
-static unsigned fold_fwd_grid() {
-  static const unsigned v = [] {
-    const char* e = std::getenv("DDP_AMD_BN_FOLD_FWD_GRID");
-    return (unsigned)(e ? std::max(0, std::atoi(e)) : 0);
-  }();
-  return v;
-}
+static unsigned fold_fwd_grid() { return 0u; }
 
 template <bool POOL, int IPT, bool MASK>
 static void launch_fwd_m(const BnArgs& a, size_t items, hipStream_t st) {
@@ -904,26 +898,20 @@ extern "C" int ddp_bn_act_fwd(const BnArgs* args, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// Target reduce-grid size (DDP_AMD_BN_BWD_BLOCKS overrides).
+// Target reduce-grid size (measured).
 static size_t kBwdBlocks = 1024;
 
-// Largest grid-wide replica re-read of a folded backward apply (DDP_AMD_BN_FOLD_BWD_MB, default
+// Largest grid-wide replica re-read of a folded backward apply (default
 // 32 MB; 0 = always the separate finalize launch)
-static size_t fold_bwd_bytes() {
-  static const size_t v = [] {
-    const char* e = std::getenv("DDP_AMD_BN_FOLD_BWD_MB");
-    return (size_t)(e ? std::max(0, std::atoi(e)) : 32) << 20;
-  }();
-  return v;
-}
+static size_t fold_bwd_bytes() { return (size_t)32 << 20; }
 
-// Reduce-grid cap (DDP_AMD_BN_REDUCE_GRID, 0 = uncapped): the reduce walks its item blocks
+// Reduce-grid cap (kReduceGrid, 0 = uncapped): the reduce walks its item blocks
 // with a grid stride, so every block adds ONE partial sum per channel. Uncapped, ResNet-50's
 // 56x56x256 layers ran 25088 blocks = 51 MB of memory-side float atomics per layer (~40 us at
 // the ~1.3 TB/s atomic rate, MI355X_MICROARCH.md "Global float atomics").
 static unsigned kReduceGrid = 2048;
 
-// Channel groups per reduce block (DDP_AMD_BN_REDUCE_GB, default 32 = 256 channels): every
+// Channel groups per reduce block (kReduceGb, 32 = 256 channels): every
 // block adds one partial sum per channel of its chunk, so a block spanning all of a wide
 // layer's channels (the apply's layout: 2048 channels x 1 pixel row) made the capped grid
 // issue 2048 x 2 x C memory-side atomics — 33 MB at C = 2048, more time than the layer's
@@ -931,11 +919,6 @@ static unsigned kReduceGrid = 2048;
 // reduce 256 / Gb pixel rows in LDS first.
 static int kReduceGb = 32;
 static void reduce_split(const BnArgs& a, int Gb, int chunks, int* rGb, int* rchunks) {
-  static const bool init = [] {
-    if (const char* e = std::getenv("DDP_AMD_BN_REDUCE_GB")) kReduceGb = std::max(0, std::atoi(e));
-    return true;
-  }();
-  (void)init;
   const int G = a.C / 8;
   *rGb = Gb;
   *rchunks = chunks;
@@ -947,11 +930,6 @@ static void reduce_split(const BnArgs& a, int Gb, int chunks, int* rGb, int* rch
 
 // reduce blocks along x for bx item blocks x chunks channel chunks
 static unsigned reduce_grid_x(unsigned bx, int chunks) {
-  static const bool init = [] {
-    if (const char* e = std::getenv("DDP_AMD_BN_REDUCE_GRID")) kReduceGrid = (unsigned)std::max(0, std::atoi(e));
-    return true;
-  }();
-  (void)init;
   // (the deterministic build keeps one replica per block: block ids stay below kStatRep)
   unsigned rx = kReduceGrid ? std::min(bx, std::max(1u, kReduceGrid / (unsigned)chunks)) : bx;
   if (kDeterministic) rx = std::min(rx, std::max(1u, (unsigned)kStatRep / (unsigned)chunks));
@@ -1036,18 +1014,13 @@ static void launch_bwd(const BnArgs& a, size_t npix, int Gb, int chunks, hipStre
 // column alone — every 16-byte load is its own cache line — so its time grows with the loads
 // per thread (measured, b64 step: 2 loads 5.1 us, 5 loads 9.6, 8 loads 9.5, 16-20 loads 22 us,
 // against 12-19 us for reduce + finalize + apply): served while ipt x (dy + z [+ res] vectors)
-// <= kLocalMaxLoads (DDP_AMD_BN_BWD_LOCAL_LOADS; 0 = never). Step A/B of the limit (0/5/8/10):
+// <= kLocalMaxLoads (0 = never; bn_bwd_local_set). Step A/B of the limit (0/5/8/10):
 // 8 is best at b32..b128 (b32 0.416 -> 0.405 ms, b64 -1.2 %, b128 -0.9 %), neutral at b256.
 // (1024-thread blocks for the next-bigger layers and a clustered grid-synchronised variant were
 // measured slower and removed in round 4: profiles/r3_conv_occupancy.md, r3_bn_bwd_one_launch.md)
 static int kLocalMaxLoads = 8;
 constexpr int kLocalThreads = 256;
 static bool local_cfg(const BnArgs& a, int* ipt) {
-  static const bool init = [] {
-    if (const char* e = std::getenv("DDP_AMD_BN_BWD_LOCAL_LOADS")) kLocalMaxLoads = std::max(0, std::atoi(e));
-    return true;
-  }();
-  (void)init;
   if (a.C % 8 || (a.pool && a.res)) return false;
   const int Ho = a.pool ? a.H / 2 : a.H, Wo = a.pool ? a.W / 2 : a.W;
   const size_t npix = (size_t)a.N * Ho * Wo;
@@ -1096,11 +1069,6 @@ extern "C" int ddp_bn_bwd_local_ok(int N, int H, int W, int C, int pool) {
 
 // reduce + finalize + apply
 static int launch_reduce_chain(const BnArgs& a, hipStream_t st) {
-  static const bool init = [] {
-    if (const char* e = std::getenv("DDP_AMD_BN_BWD_BLOCKS")) kBwdBlocks = std::max(1, std::atoi(e));
-    return true;
-  }();
-  (void)init;
   const int G = a.C / 8;
   const int Gb = G < 256 ? G : 256;
   if ((Gb < 256 && 256 % Gb) || (G > 256 && G % 256)) return -1;  // channel groups must tile 256 threads
@@ -1164,17 +1132,11 @@ static bool pool3_shape_ok(const BnArgs& a, int* Ho, int* Wo) {
   return (size_t)a.N * a.H * a.W * a.C < (1ull << 31);
 }
 
-// grid caps of the stem passes (DDP_AMD_POOL3_GRIDS="fwd,reduce,apply"). Kernel-trace sweep on
+// grid caps of the stem passes (fwd, reduce, apply). Kernel-trace sweep on
 // ResNet-50 b256 (profiles/r5az_pool3_grids.md): 16384 / 2048 / 4096 take 498 us for the three
 // passes against 524 us at the previous 8192 / 4096 / 16384
 static void pool3_grids(unsigned* g) {
-  static unsigned v[3] = {16384, 2048, 4096};
-  static const bool init = [] {
-    if (const char* e = std::getenv("DDP_AMD_POOL3_GRIDS"))
-      std::sscanf(e, "%u,%u,%u", &v[0], &v[1], &v[2]);
-    return true;
-  }();
-  (void)init;
+  static const unsigned v[3] = {16384, 2048, 4096};
   g[0] = std::max(1u, v[0]); g[1] = std::max(1u, v[1]); g[2] = std::max(1u, v[2]);
 }
 

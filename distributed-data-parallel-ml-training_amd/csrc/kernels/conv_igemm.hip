@@ -1873,16 +1873,10 @@ static bool fits_buffer(size_t elems) { return elems * 2 < (size_t)kOOB; }
 
 static int g_stages = 2;        // LDS ring depth policy (see stages_for)
 constexpr int kNumCUs = 256;
-// LDS-staged FWD / DGRAD epilogue (conv_igemm_body); DDP_AMD_EPI_STAGE=0 restores the direct
+// LDS-staged FWD / DGRAD epilogue (conv_igemm_body); ddp_conv_epi_stage_set(0) restores the direct
 // fragment stores
-static int g_epi_stage = -1;
-static bool epi_stage_enabled() {
-  if (g_epi_stage < 0) {
-    const char* e = std::getenv("DDP_AMD_EPI_STAGE");
-    g_epi_stage = e ? std::atoi(e) : 1;
-  }
-  return g_epi_stage != 0;
-}
+static int g_epi_stage = 1;  // ddp_conv_epi_stage_set (tests: the direct-store oracle)
+static bool epi_stage_enabled() { return g_epi_stage != 0; }
 extern "C" void ddp_conv_epi_stage_set(int on) { g_epi_stage = on ? 1 : 0; }
 
 // Split-K factor for a tile config: aim for >= 2 workgroups per CU, keep >= 4 k-steps per
@@ -1919,7 +1913,7 @@ static double tile_cost(int BM, int BN, const ConvArgs& a, size_t ws_elems, int*
   return t_mfma + t_split;
 }
 
-// LDS ring depth per tile shape (DDP_AMD_CONV_STAGES selects the policy; 2 = double buffer).
+// LDS ring depth per tile shape (ddp_conv_options selects the policy; 2 = double buffer).
 // Bytes per stage: (BM + BN) x 64 x 2 — 32 KB at 128x128, 24 KB at 128x64, 16 KB at 64x64.
 static int stages_for(int BM, int BN) {
   if (g_stages <= 2) return 2;
@@ -1928,14 +1922,10 @@ static int stages_for(int BM, int BN) {
   return 3;
 }
 
-// DDP_AMD_FWD_STAT_GRID: grid cap of the statistics-reducing FWD GEMMs (0 = one block per item)
+// grid cap of the statistics-reducing FWD GEMMs (measured: profiles/r5u_fwd_stat_grid.md)
 static int fwd_stat_grid() {
-  static const int v = [] {
-    const char* e = std::getenv("DDP_AMD_FWD_STAT_GRID");
-    const int g = e ? std::max(0, std::atoi(e)) : 2048;
-    return (kDeterministic ? std::min(g, kStatRep) : g) / 8 * 8;
-  }();
-  return v;
+  constexpr int g = 2048;
+  return (kDeterministic ? std::min(g, kStatRep) : g) / 8 * 8;
 }
 
 template <int MODE, int BM, int BN, int NST, int BNF>
@@ -2024,13 +2014,8 @@ static bool needs_finish(int mode, const ConvArgs& a) {
 // row per thread: the latency-bound finishes of the strong-scaling batches), else 2 (enough
 // workgroups in flight for a bandwidth-bound pass). Measured, same session (gpurun_out/finish,
 // profiles/r2_finish_batched.md): VGG-11 b32 0.4849 -> 0.4705 (2 rows) -> 0.4596 ms (1 row);
-// b256 0.9018 -> 0.8984 (2 rows) vs 0.908 ms (1 row everywhere). DDP_AMD_FINISH_RPT forces.
+// b256 0.9018 -> 0.8984 (2 rows) vs 0.908 ms (1 row everywhere).
 static int finish_rows_per_thread(int Mg, int rows_per_block) {
-  static const int forced = [] {
-    const char* e = std::getenv("DDP_AMD_FINISH_RPT");
-    return e ? std::max(1, std::min(8, std::atoi(e))) : 0;
-  }();
-  if (forced) return forced;
   return (Mg + rows_per_block - 1) / rows_per_block <= 128 ? 1 : 2;
 }
 
@@ -2066,11 +2051,7 @@ static std::set<const float*> g_sgd_master;  // master updated in a pair's WGRAD
 // the pair launch's unsplit WGRAD half (ConvArgs::sgd): any registered weight qualifies, the
 // fp32 master is read by nothing else in the backward
 static SgdFuse sgd_fuse_master(const float* dw) {
-  static const bool on = [] {  // DDP_AMD_SGD_PAIR_MASTER=0: the step's SGD launch does it all
-    const char* e = std::getenv("DDP_AMD_SGD_PAIR_MASTER");
-    return !(e && e[0] == '0');
-  }();
-  if (!on || g_sgd_reg.empty()) return SgdFuse{};
+  if (g_sgd_reg.empty()) return SgdFuse{};
   auto it = g_sgd_reg.find(dw);
   if (it == g_sgd_reg.end()) return SgdFuse{};
   g_sgd_master.insert(dw);
@@ -2096,28 +2077,16 @@ static WgFinishArgs wg_finish_args(const ConvArgs& a) {
 // DGRAD split-K finish with the preceding block's complete BatchNorm backward (small stride-1
 // problems). With ``wa`` (a WGRAD finish of the same backward pair) both run in ONE launch.
 // false = not applicable (plain finish with the BnBwdFuse sums).
-// Row limit of both fused finishes (DDP_AMD_BN_FUSE_MAX_ROWS): one block owns 16 channels of
+// Row limit of both fused finishes (ddp_conv_bn_fuse_rows): one block owns 16 channels of
 // every row, so a bigger GEMM gives each thread several rows of serial, poorly coalesced slab
 // reads on only Ng/16 blocks. Measured on the VGG-11 b32 step (profiles/r2_bn_fused_finish.md):
 // at 128 rows (2x2 layers) the fused forward finish takes 6.4 us vs 5.1 + 4.4-5.3 us for finish
 // + BN apply, the fused backward 11.8 us vs 17 us for finish + finalize + apply; at 512 rows
 // (4x4 layers) 10-13 us (forward, no gain) and 29 us (backward, vs 16 us).
-static int g_bn_fuse_rows = -1;  // -1: not read yet (env, default 128); ddp_conv_bn_fuse_rows
-static int bn_fuse_max_rows() {
-  if (g_bn_fuse_rows < 0) {
-    const char* e = std::getenv("DDP_AMD_BN_FUSE_MAX_ROWS");
-    g_bn_fuse_rows = e ? std::max(0, std::atoi(e)) : 128;
-  }
-  return g_bn_fuse_rows;
-}
-// the backward variant's own limit (DDP_AMD_BN_BWD_FUSE_MAX_ROWS, default: the common one)
-static int bn_bwd_fuse_max_rows() {
-  static const int v = [] {
-    const char* e = std::getenv("DDP_AMD_BN_BWD_FUSE_MAX_ROWS");
-    return e ? std::max(0, std::atoi(e)) : -1;
-  }();
-  return v >= 0 ? v : bn_fuse_max_rows();
-}
+static int g_bn_fuse_rows = 128;  // ddp_conv_bn_fuse_rows (tests)
+static int bn_fuse_max_rows() { return g_bn_fuse_rows; }
+// the backward variant's limit: the common one
+static int bn_bwd_fuse_max_rows() { return bn_fuse_max_rows(); }
 
 static bool bnbwd_fusable(const ConvArgs& a) {
   return a.has_bnf && a.bnapply && a.splits > 1 && !a.phase && !a.accumulate &&
@@ -2361,15 +2330,9 @@ extern "C" void ddp_conv_force_tile(int tile_plus_one, int stages) {
 }
 
 // ---- dense 2x2 form of the 3x3 convs over 2x2 images (ConvArgs::d2x2; VGG-11's last two
-// layers): DDP_AMD_DENSE2X2=0 / ddp_conv_dense2x2_set(0) restores the implicit GEMM
-static int g_dense2x2 = -1;
-static bool dense2x2_on() {
-  if (g_dense2x2 < 0) {
-    const char* e = std::getenv("DDP_AMD_DENSE2X2");
-    g_dense2x2 = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_dense2x2 != 0;
-}
+// layers): ddp_conv_dense2x2_set(0) restores the implicit GEMM
+static int g_dense2x2 = 1;  // ddp_conv_dense2x2_set (tests: the implicit-GEMM oracle)
+static bool dense2x2_on() { return g_dense2x2 != 0; }
 extern "C" void ddp_conv_dense2x2_set(int on) { g_dense2x2 = on ? 1 : 0; }
 extern "C" int ddp_conv_dense2x2_ok(const ConvGeom* g) {
   return dense2x2_on() && g->R == 3 && g->S == 3 && g->stride == 1 && g->pad == 1 &&
@@ -2497,10 +2460,7 @@ extern "C" void ddp_conv_bn_fuse_rows(int rows) { g_bn_fuse_rows = std::max(0, r
 extern "C" int ddp_conv_fwd_bn(const ConvGeom* g, const void* x, const void* wc, const float* bias,
                                void* z, float* stats, float* ws, size_t ws_elems,
                                const BnFwdFuse* bn, hipStream_t st) {
-  static const bool enabled = [] {
-    const char* e = std::getenv("DDP_AMD_BN_FWD_FUSE");
-    return !(e && e[0] == '0');
-  }();
+  constexpr bool enabled = true;  // (ops/layers.py BN_FWD_FUSE switches the caller)
   if (g->C % 8 || g->K % 8) return -1;
   int done = 0;
   {
@@ -2549,11 +2509,7 @@ extern "C" int ddp_conv_fwd_finish(const ConvGeom* g, float* ws, int splits, con
   a.Ng = g->K;
   a.Kg = g->R * g->S * g->C;
   a.splits = splits;
-  static const bool bn_enabled = [] {
-    const char* e = std::getenv("DDP_AMD_BN_FWD_FUSE");
-    return !(e && e[0] == '0');
-  }();
-  if (bn && bn_enabled && a.Mg <= kBnFwdFuseMaxRows) {
+  if (bn && a.Mg <= kBnFwdFuseMaxRows) {
     a.bnfwd = bn;
     a.bnfwd_done = bn_done;
   }
@@ -2717,7 +2673,7 @@ extern "C" int ddp_conv_wgrad(const ConvGeom* g, const void* dy, const void* x, 
 // DGRAD + WGRAD of one stride-1 layer in ONE launch (conv_bwd_pair_kernel) and their split-K
 // finishes in one more (bwd_pair_finish_kernel): two dispatches instead of up to four, and the
 // two latency-bound GEMMs of a small batch share the chip instead of running back to back.
-// Policy (DDP_AMD_BWD_PAIR via ddp_conv_pair_mode): 0 never; 1 when the measured / modelled
+// Policy (ddp_conv_pair_mode, ops/common.py BWD_PAIR_MODE): 0 never; 1 when the measured / modelled
 // choice is the 64x64 tile for both problems; 2 always (both forced to 64x64); 3 (default) when
 // both pick 64x64, or when the paired 64x64 launch has at most g_pair_items work items (about
 // one wave of 4 blocks per CU: the small problems of the strong-scaling batches, where pairing

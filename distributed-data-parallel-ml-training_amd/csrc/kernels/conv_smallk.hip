@@ -369,7 +369,6 @@ using namespace ddp_amd;
 extern "C" int ddp_conv_fwd_smallk(const ConvGeom* g, const void* x, const void* wc,
                                    const float* bias, void* y, float* stats, hipStream_t st) {
   if (g->C != 8 || g->K % 16 || g->K > 64) return -1;
-  if (const char* e = std::getenv("DDP_AMD_SMALLK_TPW")) kSmallkTilesPerWave = std::max(1, std::atoi(e));
   const int taps = g->R * g->S;
   const int nks = (taps + 3) / 4;
   SmallKArgs a;

@@ -606,7 +606,7 @@ static bool launch_stages(const Cfg& c, int in, const Args& a, int nl, int items
   return false;
 }
 static std::map<std::tuple<int, int, int, int>, Cfg> g_tr_tuned;  // (M, K, C, H)
-static int g_tr_mode = -1;  // -1 unread; 0 off; 1 on (DDP_AMD_CONV_TR)
+static int g_tr_mode = 1;  // 0 off, 1 table entries only, 2 also the heuristic (ddp_conv_tr_mode)
 static Cfg g_tr_force{0, 0, 0, 0};
 
 static Cfg heuristic(int N, int H, int W, int C, int K) {
@@ -650,11 +650,6 @@ struct Plan {
 
 // the launch decision shared by ddp_conv_fwd_tr and ddp_conv_tr_would_serve
 static bool plan(const ConvGeom* g, float* ws, size_t ws_elems, int in_mode, Plan* p) {
-  if (g_tr_mode < 0) {
-    // 0 off, 1 (default) table entries only, 2 also the heuristic for untabled shapes
-    const char* e = std::getenv("DDP_AMD_CONV_TR");
-    g_tr_mode = e ? std::max(0, std::min(2, std::atoi(e))) : 1;
-  }
   if (!g_tr_mode) return false;
   if (g->R != 3 || g->S != 3 || g->stride != 1 || g->pad != 1 || g->P != g->H || g->Q != g->W)
     return false;

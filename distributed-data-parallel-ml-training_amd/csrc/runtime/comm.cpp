@@ -288,14 +288,14 @@ Reducer::Reducer(RcclComm* comm, float* arena, std::vector<size_t> offsets,
   done_stream_.assign(nb, nullptr);
   for (size_t b = 0; b < nb; ++b)
     HIP_OK(hipEventCreateWithFlags(&done_ev_[b], hipEventDisableTiming));
-  // comm stream at the highest stream priority (DDP_AMD_COMM_PRIORITY=normal reverts): HIP
-  // keeps high-priority streams on their own hardware queues, so the collectives cannot end up
-  // behind the backward on a queue shared round-robin with the compute stream
+  // comm stream at the highest stream priority: HIP keeps high-priority streams on their own
+  // hardware queues, so the collectives cannot end up behind the backward on a queue shared
+  // round-robin with the compute stream (normal priority: 0 us of overlap measured,
+  // profiles/r2_pipelined_ddp.md)
   int lo = 0, hi = 0;
   HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-  const char* pe = std::getenv("DDP_AMD_COMM_PRIORITY");
-  const bool high = !(pe && std::string(pe) == "normal");
-  HIP_OK(hipStreamCreateWithPriority(&comm_stream_, hipStreamNonBlocking, high ? hi : lo));
+  (void)lo;
+  HIP_OK(hipStreamCreateWithPriority(&comm_stream_, hipStreamNonBlocking, hi));
   prepare();
 }
 

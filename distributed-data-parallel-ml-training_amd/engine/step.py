@@ -285,14 +285,13 @@ class SegmentedDDPStep(TrainStep):
             self.buckets.append(((i0, i1), (lo, hi)))
         self.cut = self.buckets[0][1][0]  # start of the last layers' bucket (tests)
         self.total = arena.total
-        # The comm stream comes from HIP's HIGH-priority hardware-queue pool (env
-        # DDP_AMD_COMM_PRIORITY=normal reverts): normal-priority streams share GPU_MAX_HW_QUEUES
-        # (4) queues round-robin, and with live RCCL communicators (which create streams of
-        # their own) the comm stream landed on the main stream's queue — every bucket then ran
-        # strictly between the segment graphs, 0 us hidden; high priority: 76 of 120 us hidden
-        # (tools/overlap_probe.py, profiles/r2_pipelined_ddp.md).
-        prio = os.environ.get("DDP_AMD_COMM_PRIORITY", "high")
-        self.comm_stream = torch.cuda.Stream(priority=-1 if prio == "high" else 0)
+        # The comm stream comes from HIP's HIGH-priority hardware-queue pool: normal-priority
+        # streams share GPU_MAX_HW_QUEUES (4) queues round-robin, and with live RCCL
+        # communicators (which create streams of their own) the comm stream landed on the main
+        # stream's queue — every bucket then ran strictly between the segment graphs, 0 us
+        # hidden; high priority: 76 of 120 us hidden (tools/overlap_probe.py,
+        # profiles/r2_pipelined_ddp.md).
+        self.comm_stream = torch.cuda.Stream(priority=-1)
         self.comm_a = None
         # collectives=False: no collective at all — no bucket all-reduce, no BatchNorm-buffer
         # broadcast (profile_stage_times: per-segment compute times of a cut-everywhere step on

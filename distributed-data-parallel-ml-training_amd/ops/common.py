@@ -6,23 +6,21 @@ import torch
 from .._ext import load as _load
 
 _NATIVE = None
-CONV_STAGES = 2  # default LDS ring depth policy (env DDP_AMD_CONV_STAGES overrides)
+CONV_STAGES = 2  # LDS ring depth policy of untabulated conv GEMMs (2 = double buffering)
+# backward-pair policy (conv_igemm.hip ddp_conv_pair_mode): 3 = pair when the measured pair
+# table says so, or both problems pick the 64x64 tile, or the paired launch has <= 1024 items
+BWD_PAIR_MODE, BWD_PAIR_ITEMS = 3, 1024
 
 
 def native():
     global _NATIVE
     if _NATIVE is None:
         _NATIVE = _load()
-        # DDP_AMD_CONV_STAGES: LDS ring depth policy of the conv GEMMs (2 = double buffering)
         # (split-K always goes through fp32 slabs + a deterministic finish: the fp32-atomic
         # variants measured 6-60 % slower steps, profiles/r2_launch_reduction_ab.md, and were
         # removed in round 4)
-        _NATIVE.conv_options(int(os.environ.get("DDP_AMD_CONV_STAGES", str(CONV_STAGES))))
-        # DDP_AMD_BWD_PAIR: one layer's wgrad + dgrad as ONE grouped launch — 0 never,
-        # 1 when both problems pick the 64x64 tile, 2 always (stride-1 layers), 3 (default)
-        # also when the paired launch has <= DDP_AMD_BWD_PAIR_ITEMS (1024) work items
-        _NATIVE.conv_pair_mode(int(os.environ.get("DDP_AMD_BWD_PAIR", "3")),
-                               int(os.environ.get("DDP_AMD_BWD_PAIR_ITEMS", "1024")))
+        _NATIVE.conv_options(CONV_STAGES)
+        _NATIVE.conv_pair_mode(BWD_PAIR_MODE, BWD_PAIR_ITEMS)
         load_conv_tuning(_NATIVE)
     return _NATIVE
 
@@ -111,8 +109,8 @@ def workspace(device):
 
 # BatchNorm-backward sums of a Conv->BN->ReLU(->pool) block accumulated by the NEXT block's
 # dgrad epilogue (BnBwdFuse, conv_igemm.hip): the block's backward skips its reduce pass.
-# DDP_AMD_BN_BWD_FUSE=0 restores the separate reduce kernel.
-BN_BWD_FUSE = os.environ.get("DDP_AMD_BN_BWD_FUSE", "1") != "0"
+# False: the separate reduce kernel (the tests' oracle).
+BN_BWD_FUSE = True
 
 
 # ---------------------------------------------------------------- per-step accumulator scratch

@@ -11,7 +11,6 @@ reducer can launch bucket all-reduces while the rest of the backward is still ru
 Reference parity: part1/model.py:11-27 (the Sequential it fuses) and SURVEY.md §2.D kernel list.
 Activations between blocks are NHWC bf16; the first conv's input is zero-padded 3 -> 8 channels.
 """
-import os
 
 import torch
 
@@ -215,58 +214,60 @@ class GradLink:
         return out
 
 
-# 3x3 stride-1 forward convolutions through the tap-reuse kernel (conv_tr.hip); =0 restores the
-# implicit-GEMM kernel for every layer (the native side also reads DDP_AMD_CONV_TR)
-CONV_TR = os.environ.get("DDP_AMD_CONV_TR", "1") != "0"
+# Design switches of the fused paths. Each was measured against the unfused path it replaces
+# (profiles cited below) and won on every measured configuration; the unfused paths stay as the
+# oracles the GPU tests compare the fused ones against (tests flip these module constants), not
+# as run-time options.
+#
+# 3x3 stride-1 forward convolutions through the tap-reuse kernel (conv_tr.hip); False: the
+# implicit-GEMM kernel for every layer
+CONV_TR = True
 # a block's BatchNorm + ReLU (+ 2x2 pool) forward computed by the NEXT block's tap-reuse conv
 # while it loads its input patch (conv_tr.hip fused input; no bn_act_fwd launch); =0 restores the
 # separate pass
-# (1 = every eligible block, 2 (default) = only blocks without a max-pool: a pooled block's
-# consumer loads four pre-pool values per input pixel, measured -1 % at 32 images per GPU but
-# +3 % at 256 (profiles/r3_fused_bn_input.md); DDP_AMD_FUSE_BN_IN_MAX_ROWS: only while the
-# consumer GEMM has at most this many rows)
-FUSE_BN_IN = int(os.environ.get("DDP_AMD_FUSE_BN_IN", "2"))
-FUSE_BN_IN_MAX_ROWS = int(os.environ.get("DDP_AMD_FUSE_BN_IN_MAX_ROWS", str(1 << 30)))
+# (1 = every eligible block, 2 = only blocks without a max-pool: a pooled block's consumer loads
+# four pre-pool values per input pixel, measured -1 % at 32 images per GPU but +3 % at 256
+# (profiles/r3_fused_bn_input.md))
+FUSE_BN_IN = 2
 # mode 2 still fuses pooled blocks up to this many images per GPU: at 32 (the 8-GPU share) the
 # launch it removes outweighs the 4x patch bytes (b32 0.4132 vs 0.4178 ms; at 64 it loses,
 # 0.4933 vs 0.4870; profiles/r3_fused_bn_input.md)
-FUSE_BN_IN_POOL_MAX_BATCH = int(os.environ.get("DDP_AMD_FUSE_BN_IN_POOL_MAX_BATCH", "32"))
+FUSE_BN_IN_POOL_MAX_BATCH = 32
 # BatchNorm forward fused into the split-K finish of small conv GEMMs (conv_igemm.hip
-# splitk_finish_bnfwd_kernel; the native side also honours DDP_AMD_BN_FWD_FUSE=0)
-BN_FWD_FUSE = os.environ.get("DDP_AMD_BN_FWD_FUSE", "1") != "0"
+# splitk_finish_bnfwd_kernel)
+BN_FWD_FUSE = True
 # the preceding block's whole BatchNorm backward completed in a small dgrad's split-K finish
 # (conv_igemm.hip splitk_finish_bnbwd_kernel; BnBwdFuse chain only)
-BN_BWD_APPLY_FUSE = os.environ.get("DDP_AMD_BN_BWD_APPLY_FUSE", "1") != "0"
+BN_BWD_APPLY_FUSE = True
 # ... and into the classifier head's backward: dx + that BN backward + dW / db in one launch
 # (conv_igemm.hip linear_head_bwd_kernel; needs BN_BWD_APPLY_FUSE too)
-HEAD_BN_FUSE = os.environ.get("DDP_AMD_HEAD_BN_FUSE", "1") != "0"
+HEAD_BN_FUSE = True
 # ... and its BN + ReLU + 2x2 pool FORWARD folded into the head's forward kernel (linear_ce.hip
 # HeadBnIn: one launch fewer; the training loss path only, VGG's 2x2 last block)
-HEAD_BN_FWD = os.environ.get("DDP_AMD_HEAD_BN_FWD", "1") != "0"
+HEAD_BN_FWD = True
 # residual blocks (BN + residual + ReLU, no pool; ResNet's bn3): the forward stores the ReLU
 # mask as one bit per element and the backward reads it instead of the residual tensor, which it
 # only ever needed for that mask (bn_act.hip BnArgs::mask; 1/16 of the bytes, twice per layer)
-BN_RELU_MASK = os.environ.get("DDP_AMD_BN_RELU_MASK", "1") != "0"
+BN_RELU_MASK = True
 # ... and an identity block's residual gradient (dy through that mask) is not stored at all: the
 # branch's first 1x1 conv rebuilds it in its accumulating dgrad epilogue (GradLink.defer)
-RES_DEFER = os.environ.get("DDP_AMD_RES_DEFER", "1") != "0"
+RES_DEFER = True
 # ... and a projection block's shortcut BatchNorm folded into the block's residual BN passes: the
 # downsample conv's PRE-BN output is the residual, normalised inside bn3's apply, and bn3's
 # backward reduce / apply also produce the shortcut's dz (bn_act.hip RBN; both BNs see the same
 # gradient dy * mask, so they share S1). The shortcut's BN output and its gradient are never
 # stored and its own finalize / apply / reduce / finalize / apply launches disappear.
-RES_BN_FUSE = os.environ.get("DDP_AMD_RES_BN_FUSE", "1") != "0"
+RES_BN_FUSE = True
 # ... and a strided shortcut conv whose backward reaches the block input first leaves its dgrad
 # to the other branch: that one writes dx, then the shortcut's phase dgrad ACCUMULATES into the
 # 1/stride^2 of dx it reaches — no zero fill of dx's untouched phases and no read-back of the
 # whole dx by an accumulating second branch (GradLink.deferred_dgrad)
-DS_DGRAD_DEFER = os.environ.get("DDP_AMD_DS_DGRAD_DEFER", "1") != "0"
+DS_DGRAD_DEFER = True
 # largest dgrad output H*W that takes the fused sums: 16 (4x4 / 2x2) from 128 images per GPU up,
 # 256 (also 16x16 / 8x8) at the strong-scaling shares of at most 64 images (b64 0.4556 vs 0.4594
-# ms, b32 0.3921 vs 0.3952; b128 / b256 unchanged, profiles/r4z3_bn_sums_threshold.md); the
-# environment variable sets one threshold for every batch
-_MAX_HW_ENV = os.environ.get("DDP_AMD_BN_BWD_FUSE_MAX_HW")
-BN_BWD_FUSE_MAX_HW = int(_MAX_HW_ENV) if _MAX_HW_ENV else None
+# ms, b32 0.3921 vs 0.3952; b128 / b256 unchanged, profiles/r4z3_bn_sums_threshold.md); a
+# number here sets one threshold for every batch (tests)
+BN_BWD_FUSE_MAX_HW = None
 
 
 def bn_bwd_fuse_pays(H, W, pool=True, N=None):
@@ -378,11 +379,11 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=Non
 # VGG input block (conv 3x3 over the 8-channel padded image -> 64, BN, ReLU, 2x2 pool) through
 # conv_l0.hip: its pre-BN activation z (the network's largest tensor) is recomputed from the
 # input in every pass that needs it instead of being stored and streamed four times.
-# DDP_AMD_L0_FUSE=0 restores conv_smallk + bn_act passes.
-L0_FUSE = os.environ.get("DDP_AMD_L0_FUSE", "1") != "0"
+# False: conv_smallk + bn_act passes.
+L0_FUSE = True
 # ... and its BN-backward sums taken in the next block's dgrad split-K finish when that dgrad has
-# one (conv_igemm.hip BnBwdFuse::code; else l0_sums_kernel). =0: always the separate pass
-L0_SUMS_IN_FINISH = os.environ.get("DDP_AMD_L0_SUMS_IN_FINISH", "1") != "0"
+# one (conv_igemm.hip BnBwdFuse::code; else l0_sums_kernel). False: always the separate pass
+L0_SUMS_IN_FINISH = True
 
 
 def l0_serves(spec, x):
@@ -405,8 +406,7 @@ def _defer_bn(spec, residual, running_mean, N, Ho, Wo):
             or running_mean is not None or nxt.C != spec.K or nxt.Cr != nxt.C
             or nxt.R != 3 or nxt.stride != 1 or nxt.pad != 1):
         return False
-    if ((FUSE_BN_IN == 2 and spec.pool and N > FUSE_BN_IN_POOL_MAX_BATCH)
-            or N * Ho * Wo > FUSE_BN_IN_MAX_ROWS):
+    if FUSE_BN_IN == 2 and spec.pool and N > FUSE_BN_IN_POOL_MAX_BATCH:
         return False
     if spec.pool and (Ho * 2 != spec._out_p or Wo * 2 != spec._out_q):
         return False

@@ -40,8 +40,8 @@ import time
 
 from .launch import _SignalGuard, _child_setup, _kill_all, check_no_gpu_init, free_port, rank_env
 
-CHILD_ENV = "DDP_AMD_LADDER_CHILD"    # set in every attempt's ranks (they run, not supervise)
-ATTEMPT_ENV = "DDP_AMD_LADDER_ATTEMPT"  # the attempt index, for fault injection and the JSON
+# set in every attempt's ranks (they run, not supervise): the attempt index (fault injection)
+ATTEMPT_ENV = CHILD_ENV = "DDP_AMD_LADDER_ATTEMPT"
 # exit codes of a rank that ran to the end but whose result must not be reported
 RC_REPLICAS = 5    # replicas not bit-identical after the timed steps
 RC_WATCHDOG = 3    # utils/misc.py Watchdog
@@ -115,7 +115,6 @@ def _spawn(cmd, env, capture_json):
 def _child_env(base, attempt_index, extra):
     env = dict(base)
     env.update(extra)
-    env[CHILD_ENV] = "1"
     env[ATTEMPT_ENV] = str(attempt_index)
     # a hung collective must end the attempt well inside the supervisor's time limit
     env.setdefault("DDP_AMD_WATCHDOG_S", "120")

@@ -25,7 +25,7 @@ SMALL = ["--device", "cpu", "--global-batch", "8", "--steps", "2", "--warmup", "
 def _env(**extra):
     env = dict(os.environ, OMP_NUM_THREADS="1", DDP_AMD_WATCHDOG_S="10", **extra)
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT",
-              "DDP_AMD_LADDER_CHILD", "DDP_AMD_LADDER_ATTEMPT", "DDP_AMD_FAULT_INJECT"):
+              "DDP_AMD_LADDER_ATTEMPT", "DDP_AMD_FAULT_INJECT"):
         env.pop(k, None)
     env.update(extra)
     return env

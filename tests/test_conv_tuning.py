@@ -17,8 +17,8 @@ def test_tuning_table_well_formed():
     keys = set()
     for e in t["entries"]:
         assert e["mode"] in (0, 1, 2, 3)
-        if e["mode"] == 3:  # backward pair: tile = pair on/off, splits / stages = DGRAD / WGRAD
-            assert e["tile"] in (0, 1) and 1 <= e["splits"] <= 16 and 1 <= e["stages"] <= 128
+        if e["mode"] == 3:  # backward pair: tile = 0 separate / pair tile 1..4, splits / stages = DGRAD / WGRAD
+            assert e["tile"] in (0, 1, 2, 3, 4) and 1 <= e["splits"] <= 16 and 1 <= e["stages"] <= 128
         else:
             assert 0 <= e["tile"] <= 7
             # split-K slabs (splits x M x N fp32) must fit the 32 Mi-element workspace

@@ -93,7 +93,7 @@ def test_conv_tr_splitk_bn_fused_finish(native_ext, N, C, H, K, pool):
                             (ptr(gamma), ptr(beta), 1e-5, 1, int(pool), ptr(coef), ptr(y), H, H))
     finally:
         _force(nat, 0, 0, 0)
-        nat.conv_bn_fuse_rows(int(os.environ.get("DDP_AMD_BN_FUSE_MAX_ROWS", "128")))
+        nat.conv_bn_fuse_rows(128)
     torch.cuda.synchronize()
     assert r == 2, "the split-K GEMM must take the BatchNorm-fused finish"
     zr = F.conv2d(x, conv.weight, conv.bias, 1, 1)

@@ -629,7 +629,7 @@ def test_conv_splitk_finish_bn_fwd(native_ext, N, C, H, K, pool):
     finally:
         from ddp_amd.ops.common import load_conv_tuning
         load_conv_tuning(nat)  # back to the shipped table
-        nat.conv_bn_fuse_rows(int(os.environ.get("DDP_AMD_BN_FUSE_MAX_ROWS", "128")))
+        nat.conv_bn_fuse_rows(128)
     assert fused, "the split-K GEMM must take the fused BatchNorm finish"
     y2 = torch.empty_like(y)
     coef2 = torch.zeros_like(coef)

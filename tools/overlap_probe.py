@@ -50,7 +50,7 @@ def main():
     T = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
     summary = {"mode": a.mode, "batch": a.batch, "live_rccl": bool(comm.live),
                "GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES"),
-               "comm_priority": os.environ.get("DDP_AMD_COMM_PRIORITY", "high")}
+               "comm_priority": "high"}
     if a.mode == "eager":
         st = TrainStep(m, opt, crit, ld, use_graph=False)
         st.step()
