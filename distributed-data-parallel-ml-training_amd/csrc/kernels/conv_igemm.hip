@@ -2816,8 +2816,12 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
       sw = spw[3];
     }
   }
-  // a dense DGRAD reduces the BatchNorm-backward sums in the finish of its 3x3 view
+  // a dense DGRAD reduces the BatchNorm-backward sums in the finish of its 3x3 view; the input
+  // block's sums (bn->code) are taken only in a split-K finish: a split DGRAD costs the pair
+  // ~0.5 us where the standalone l0_sums launch it replaces costs 3-6 us (the pair table is
+  // measured on the GEMMs alone, tools/conv_tune.py --pairs)
   if (d.d2x2 && d.has_bnf) sd = std::max(sd, 2);
+  if (bn && bn->code && !ba && !d.d2x2) sd = std::max(sd, 2);
   // the pair's tile: the measured entry's, a forced one (sweeps), else 64x64; the dense 2x2
   // DGRAD keeps 64x64 (its column tiles pick the weight tap per input pixel)
   if (g_pair_force_tile_req >= 1 && g_pair_force_tile_req < kPairTiles) pt = g_pair_force_tile_req;
