@@ -2215,11 +2215,14 @@ launched:
 // in the table fall back to the cost model. g_force_tile (sweeps only) overrides both.
 struct TuneKey {
   int mode, M, N, K;
+  int hw = 0;  // pair entries: the layer's H*W (different convs share GEMM dims: VGG-11's
+               // b256 2x2 and b64 4x4 512->512 DGRADs are both 1024 x 512 x 4608); 0 = any
   bool operator<(const TuneKey& o) const {
     if (mode != o.mode) return mode < o.mode;
     if (M != o.M) return M < o.M;
     if (N != o.N) return N < o.N;
-    return K < o.K;
+    if (K != o.K) return K < o.K;
+    return hw < o.hw;
   }
 };
 struct TuneVal {
@@ -2307,12 +2310,17 @@ extern "C" void ddp_conv_options(int stages) { g_stages = stages; }
 extern "C" void ddp_conv_tune_set(int mode, int M, int N, int K, int tile, int splits, int stages) {
   if (mode == 3) {  // backward pair: tile = 0 separate / pair tile 1..4 (kPairTiles), splits /
                     // stages = DGRAD / WGRAD splits
-    g_pair_tuned[TuneKey{MODE_DGRAD, M, N, K}] = {tile >= 0 && tile < 5 ? tile : 1,
+    g_pair_tuned[TuneKey{MODE_DGRAD, M, N, K}] = {tile >= 0 && tile < 6 ? tile : 1,
                                                   std::max(1, splits), std::max(1, stages)};
     return;
   }
   if (tile < 0 || tile >= kNumTiles) return;
   g_tuned[TuneKey{mode, M, N, K}] = {tile, std::max(1, splits), stages};
+}
+// backward-pair entry for the layer with H*W = hw (tile 0 = separate launches, 1..5 pair tiles)
+extern "C" void ddp_conv_pair_tune_set(int M, int N, int K, int hw, int tile, int sd, int sw) {
+  g_pair_tuned[TuneKey{MODE_DGRAD, M, N, K, hw}] = {tile >= 0 && tile < 6 ? tile : 1,
+                                                    std::max(1, sd), std::max(1, sw)};
 }
 extern "C" void ddp_conv_tune_clear() {
   g_tuned.clear();
@@ -2691,7 +2699,8 @@ extern "C" void ddp_conv_pair_mode(int m, int items) {
 // 1 = 64x64 (3 LDS stages, 3 blocks per CU), 2 = 128x128 (2 stages, 2 per CU), 3 = 64x128 and
 // 4 = 128x64 (3 stages, 2 per CU). The big tiles halve the L2 -> LDS bytes per MFMA of the
 // 64x64 tile, which at b256 needs ~2x the L2 read rate its MFMAs could consume.
-constexpr int kPairTiles = 5;
+// 5 = 128x128 with 3 stages (96 KB: one block per CU, two k-steps of prefetch)
+constexpr int kPairTiles = 6;
 template <int BM, int BN, int NST, bool BNF1, bool SGDM>
 static void pair_kernel_launch(const ConvArgs& d, const ConvArgs& w, int itd, int itw,
                                hipStream_t st) {
@@ -2785,7 +2794,8 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
     sd = g_pair_force_dg;
     sw = g_pair_force_wg;
   } else if (g_force_tile == 0 && g_pair_mode == 3) {
-    auto it = g_pair_tuned.find(TuneKey{MODE_DGRAD, d.Mg, d.Ng, d.Kg});
+    auto it = g_pair_tuned.find(TuneKey{MODE_DGRAD, d.Mg, d.Ng, d.Kg, g->H * g->W});
+    if (it == g_pair_tuned.end()) it = g_pair_tuned.find(TuneKey{MODE_DGRAD, d.Mg, d.Ng, d.Kg, 0});
     if (it != g_pair_tuned.end()) {
       if (!it->second.tile) return separate();
       tuned = true;
@@ -2834,6 +2844,7 @@ extern "C" int ddp_conv_bwd_pair(const ConvGeom* g, const void* dy, const void* 
   auto prep = [&](bool launch) {
     switch (pt) {
       case 2: pair_launch_t<128, 128, 2>(d, w, sd, sw, ws, ws_elems, &itd, &itw, &fits, dw, launch, st); break;
+      case 5: pair_launch_t<128, 128, 3>(d, w, sd, sw, ws, ws_elems, &itd, &itw, &fits, dw, launch, st); break;
       case 3: pair_launch_t<64, 128, 3>(d, w, sd, sw, ws, ws_elems, &itd, &itw, &fits, dw, launch, st); break;
       case 4: pair_launch_t<128, 64, 3>(d, w, sd, sw, ws, ws_elems, &itd, &itw, &fits, dw, launch, st); break;
       default: pair_launch_t<64, 64, 3>(d, w, sd, sw, ws, ws_elems, &itd, &itw, &fits, dw, launch, st); break;

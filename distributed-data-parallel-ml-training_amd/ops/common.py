@@ -36,12 +36,17 @@ def load_conv_tuning(n=None, path=None):
     import json
     n = n or native()
     n.conv_tune_clear()
-    path = path or os.environ.get("DDP_AMD_CONV_TUNING_FILE", TUNING_FILE)
+    # (an empty DDP_AMD_CONV_TUNING_FILE means the shipped table, not "no table")
+    path = path or os.environ.get("DDP_AMD_CONV_TUNING_FILE") or TUNING_FILE
     if os.environ.get("DDP_AMD_CONV_TUNING", "1") == "0" or not os.path.exists(path):
         return 0
     with open(path) as f:
         table = json.load(f)
     for e in table.get("entries", []):
+        if int(e["mode"]) == 3 and "H" in e:  # backward pair of the layer with H x H outputs
+            n.conv_pair_tune_set(int(e["M"]), int(e["N"]), int(e["K"]), int(e["H"]) ** 2,
+                                 int(e["tile"]), int(e["splits"]), int(e.get("stages", 1)))
+            continue
         n.conv_tune_set(int(e["mode"]), int(e["M"]), int(e["N"]), int(e["K"]), int(e["tile"]),
                         int(e["splits"]), int(e.get("stages", 0)))
     # tap-reuse 3x3 forward (conv_tr.hip, tools/conv_tune_tr.py): (M, K, C, H) -> (bm, bn,

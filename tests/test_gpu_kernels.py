@@ -124,7 +124,7 @@ def test_conv_bwd_pair(native_ext, case, mode):
     assert rel_err(dw, wr.grad) < 1e-2
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 4])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5])
 @pytest.mark.parametrize("sd,sw", [(1, 1), (1, 8), (3, 4), (6, 1), (4, 24)])
 @pytest.mark.parametrize("case", [(32, 512, 2, 2, 512, 3, 1, 1), (32, 64, 16, 16, 128, 3, 1, 1),
                                   (32, 256, 4, 4, 512, 3, 1, 1), (16, 128, 8, 8, 256, 3, 1, 1)])
