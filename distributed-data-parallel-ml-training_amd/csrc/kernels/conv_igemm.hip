@@ -130,6 +130,14 @@ struct ConvArgs {
   // operand copy is NOT written here — the pair's DGRAD half is still reading it — but by the
   // step's SGD launch (pack-only items, optim.hip item 5).
   SgdFuse sgd;
+  // WGRAD, pixel-major reduction (host: wgrad_pixmajor_ok): the reduction rows m are walked as
+  // (pixel pq, 64 images) k-steps instead of 64 consecutive pixels. A column tile covers one tap
+  // (C % BN == 0), so whether the tap reaches inside the image is uniform over a k-step, and the
+  // k-steps whose pixel it pushes into the zero padding are skipped: 31 % of them on a 4x4
+  // layer, 56 % on 2x2, 16 % on 8x8 (VGG-11). Every surviving row is in range, so the gathers need
+  // no border test and take the k-step's position as a scalar offset (soffset) — no per-chunk
+  // vector work at all. Needs N % 64 == 0 and P*Q <= 64 (the valid-pixel set is a 64-bit mask).
+  int pixmajor;
 };
 
 // the accumulating DGRAD's first-branch value of 4 / 8 consecutive channels starting at flat
@@ -246,6 +254,12 @@ __device__ __forceinline__ void dma_buf(__amdgpu_buffer_rsrc_t rs, int byte_off,
   // buffer_load_dwordx4 ... lds: LDS destination = wave-uniform base (M0) + lane * 16
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lds_wave_base, 16, byte_off, 0, 0, 0);
 }
+// ... with a wave-uniform part of the offset in soffset (an SGPR: no vector add per chunk)
+__device__ __forceinline__ void dma_buf_s(__amdgpu_buffer_rsrc_t rs, int byte_off, int soff,
+                                          unsigned short* lds_wave_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)lds_wave_base, 16, byte_off,
+                                           __builtin_amdgcn_readfirstlane(soff), 0, 0);
+}
 
 // LDS-DMA completion + workgroup barrier without the vmcnt(0) that __syncthreads implies:
 // waits until at most N of this wave's vector-memory ops are outstanding (the DMAs of the
@@ -331,6 +345,11 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
   const int w_dq = wsame ? BK % gg.Q : 0;                 // q advance per k-step
   const int w_dp = wsame ? (BK / gg.Q) % gg.P : 0;        // p advance per k-step (mod P)
   const int w_dm = wsame ? 2 * BK * gg.C : 0;             // byte advance per k-step
+  // pixel-major WGRAD (ConvArgs::pixmajor): the k-step's (image block n0, pixel pq) and the
+  // tile's tap (pm_r, pm_s), all uniform; pm_mask = the pixels the tap keeps inside the image
+  const bool pm = MODE == MODE_WGRAD && args.pixmajor;
+  unsigned long long pm_mask = 0;
+  int pm_pq = 0, pm_n0 = 0, pm_r = 0, pm_s = 0;
   int row0 = 0, col0 = 0, zsplit = 0, ks_begin = 0, ks_end = 0, cur_tile = 0;
   int d2pos = 0;         // dense 2x2: the column tile's output pixel (FWD) / input pixel (DGRAD)
   const bool phase = MODE == MODE_DGRAD && args.phase;
@@ -427,9 +446,44 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
       xk.r = rs / gg.S;
       xk.s = rs - xk.r * gg.S;
       xk.ok = j < args.Ng;
+      if (pm) {
+        // one tap per column tile: its valid pixels, this split's share of the valid k-steps
+        const int t = col0 / gg.C;
+        pm_r = t / gg.S;
+        pm_s = t - pm_r * gg.S;
+        const int PQ = gg.P * gg.Q, nb = gg.N / BK;
+        unsigned long long m = 0;
+        for (int pq = 0; pq < PQ; ++pq) {
+          const int pp = pq / gg.Q, qq = pq - pp * gg.Q;
+          if ((unsigned)(pp + pm_r - gg.pad) < (unsigned)gg.H &&
+              (unsigned)(qq + pm_s - gg.pad) < (unsigned)gg.W)
+            m |= 1ull << pq;
+        }
+        pm_mask = m;
+        const int V = __builtin_popcountll(m) * nb;
+        const int per = (V + args.splits - 1) / args.splits;
+        ks_begin = min(V, zsplit * per);
+        ks_end = min(V, ks_begin + per);
+        // the first k-step's pixel: the (ks_begin / nb)-th valid one
+        int jv = ks_begin / nb;
+        unsigned long long mm = m;
+        for (; jv > 0 && mm; --jv) mm &= mm - 1;
+        pm_pq = mm ? __builtin_ctzll(mm) : 0;
+        pm_n0 = (ks_begin - (ks_begin / nb) * nb) * BK;
+        constexpr int NCA = BM / 8;
+        constexpr int NCB = BN / 8;
+#pragma unroll
+        for (int i = 0; i < CA; ++i) {  // dy[(n0 + row) * PQ + pq][kout]
+          const int kout = row0 + (lcA ^ swz_row_step<BM>(i)) * 8;
+          a_off[i] = kout < args.Mg ? 2 * (((tid + i * 256) / NCA) * PQ * gg.K + kout) : (int)kOOB;
+        }
+#pragma unroll
+        for (int i = 0; i < CB; ++i)    // x[n0 + row][p + r - pad][q + s - pad][c]
+          b_off[i] = 2 * (((tid + i * 256) / NCB) * gg.H * gg.W * gg.C + (j - t * gg.C));
+      }
       if (!xk.ok) xk.r = -(1 << 20);  // every border test fails -> zeros
       xk_same = xk.ok ? 2 * (((xk.r - gg.pad) * gg.W + (xk.s - gg.pad)) * gg.C + xk.c) : 0;
-      if (wsame) {
+      if (wsame && !pm) {
         constexpr int NCB = BN / 8;
         const int pq = gg.P * gg.Q;
         w_rr = xk.r - gg.pad;
@@ -528,6 +582,23 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
       }
     } else {
       constexpr int NCB = BN / 8;
+      if (pm) {  // (k-steps are issued in order: advance (n0, pq) after each)
+        const int PQ = gg.P * gg.Q;
+        const int pp = pm_pq / gg.Q, qq = pm_pq - pp * gg.Q;
+        const int sa = 2 * ((pm_n0 * PQ + pm_pq) * gg.K);
+        const int sb = 2 * ((pm_n0 * gg.H + pp + pm_r - gg.pad) * gg.W + qq + pm_s - gg.pad) * gg.C;
+#pragma unroll
+        for (int i = 0; i < CA; ++i) dma_buf_s(rsA, a_off[i], sa, As + (wid * 64 + 256 * i) * 8);
+#pragma unroll
+        for (int i = 0; i < CB; ++i) dma_buf_s(rsB, b_off[i], sb, Bs + (wid * 64 + 256 * i) * 8);
+        pm_n0 += BK;
+        if (pm_n0 == gg.N) {
+          pm_n0 = 0;
+          const unsigned long long rest = pm_mask & ~((2ull << pm_pq) - 1ull);
+          pm_pq = rest ? __builtin_ctzll(rest) : pm_pq;
+        }
+        return;
+      }
       const int ka = 2 * k0 * gg.K;
 #pragma unroll
       for (int i = 0; i < CA; ++i)  // dy[m][kout]; m >= Kg lands past the buffer -> zeros
@@ -1982,6 +2053,18 @@ static void launch_gemm(const ConvArgs& a, int items, hipStream_t st) {
   launch_gemm_t<MODE, BM, BN, NST, 0>(a, items, st);
 }
 
+// pixel-major WGRAD (ConvArgs::pixmajor) for this tile: stride-1 "same" conv, 64-image blocks,
+// at most 64 output pixels per image, one tap per column tile. ddp_conv_wgrad_pm_set(0) keeps
+// the pixel-order reduction (tests compare the two).
+static int g_wgrad_pm = 1;
+extern "C" void ddp_conv_wgrad_pm_set(int on) { g_wgrad_pm = on ? 1 : 0; }
+static bool wgrad_pixmajor_ok(const ConvArgs& a, int BN) {
+  const ConvGeom& g = a.g;
+  return g_wgrad_pm && g.stride == 1 && g.P == g.H && g.Q == g.W && g.N % 64 == 0 &&
+         g.P * g.Q <= 64 && g.C % BN == 0 && g.Creal == g.C && a.Ng == g.R * g.S * g.C &&
+         a.Kg == g.N * g.P * g.Q;
+}
+
 // Normalise the split count (no empty split); returns the number of work items (tiles x splits).
 template <int MODE, int BM, int BN>
 static int prepare_cfg(ConvArgs& a, int splits) {
@@ -1993,6 +2076,7 @@ static int prepare_cfg(ConvArgs& a, int splits) {
   a.splits = splits;
   a.ksteps_per_split = per;
   a.epi_stage = MODE != MODE_WGRAD && epi_stage_enabled();
+  a.pixmajor = MODE == MODE_WGRAD && wgrad_pixmajor_ok(a, BN);
   if (MODE == MODE_DGRAD) {
     const int hh = a.phase ? a.Hp : a.g.H, ww = a.phase ? a.Wp : a.g.W;
     a.dPQ = make_fastdiv(std::max(1, hh * ww));

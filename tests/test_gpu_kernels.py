@@ -151,6 +151,41 @@ def test_conv_bwd_pair_forced_splits(native_ext, case, sd, sw, tile):
     assert rel_err(dw, wr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("pm", [1, 0])
+@pytest.mark.parametrize("tile,sd,sw", [(0, 1, 1), (1, 1, 1), (1, 2, 4), (2, 3, 2), (2, 1, 6),
+                                        (3, 2, 3), (4, 1, 8), (5, 1, 4)])
+@pytest.mark.parametrize("case", [(64, 512, 2, 2, 512), (64, 256, 4, 4, 512), (128, 512, 4, 4, 512),
+                                  (64, 256, 8, 8, 256), (128, 128, 8, 8, 256)])
+def test_conv_wgrad_pixel_major(native_ext, case, tile, sd, sw, pm):
+    """Pixel-major WGRAD reduction (conv_igemm.hip ConvArgs::pixmajor: (pixel, 64 images)
+    k-steps, the taps' padding k-steps skipped, scalar-offset gathers) on the 2x2 / 4x4 / 8x8
+    layers at 64 / 128 images, as the pair's WGRAD half (tile 1..5, forced splits) and as the
+    separate launch (tile 0), against fp32 PyTorch — and pm = 0 (pixel order) the same."""
+    from ddp_amd.ops.layers import conv_backward
+    N, Cin, H, W, K = case
+    conv, spec, x, xn = _conv_setup(N, Cin, H, W, K, 3, 1, 1)
+    dz = bf(torch.randn(N, K, H, W, device=DEV))
+    dzn = dz.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    dw = torch.zeros_like(conv.weight, memory_format=torch.channels_last)
+    native_ext.conv_wgrad_pm_set(pm)
+    if tile == 0:
+        native_ext.conv_pair_mode(0)
+    else:
+        native_ext.conv_pair_force(sd, sw, tile)
+    try:
+        dx = conv_backward(spec, xn, dzn, dw, True)
+        torch.cuda.synchronize()
+    finally:
+        native_ext.conv_wgrad_pm_set(1)
+        native_ext.conv_pair_force(0, 0, 0)
+        native_ext.conv_pair_mode(3)
+    xr = x.clone().requires_grad_(True)
+    wr = conv.weight.detach().clone().requires_grad_(True)
+    F.conv2d(xr, wr, None, 1, 1).backward(dz)
+    assert rel_err(dx.permute(0, 3, 1, 2), xr.grad) < 1e-2
+    assert rel_err(dw, wr.grad) < 1e-2
+
+
 @pytest.mark.parametrize("fmt", [torch.contiguous_format, torch.channels_last])
 def test_conv_wgrad_padded_layer0(native_ext, fmt):
     from ddp_amd.ops.layers import conv_backward
