@@ -137,6 +137,11 @@ struct ConvArgs {
   // layer, 56 % on 2x2, 16 % on 8x8 (VGG-11). Every surviving row is in range, so the gathers need
   // no border test and take the k-step's position as a scalar offset (soffset) — no per-chunk
   // vector work at all. Needs N % 64 == 0 and P*Q <= 64 (the valid-pixel set is a 64-bit mask).
+  // FWD / DGRAD (host: rows_pixmajor_ok): the GEMM rows are ordered (pixel, image) and a row
+  // tile holds one pixel of BM images, so the taps that reach into the padding are uniform over
+  // the tile and their k-steps are skipped (31 % of them on a 4x4 layer, 16 % on 8x8); the A
+  // gather is a scalar offset per k-step. The epilogues (and split-K slabs) store to the NHWC
+  // rows, so every finish kernel is unchanged. Needs N % BM == 0 and P*Q <= 64.
   int pixmajor;
 };
 
@@ -348,6 +353,11 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
   // pixel-major WGRAD (ConvArgs::pixmajor): the k-step's (image block n0, pixel pq) and the
   // tile's tap (pm_r, pm_s), all uniform; pm_mask = the pixels the tap keeps inside the image
   const bool pm = MODE == MODE_WGRAD && args.pixmajor;
+  // pixel-major FWD / DGRAD rows: the item's pixel, first image and first row; the pixel's
+  // valid taps and the k-step's tap
+  const bool pmr = MODE != MODE_WGRAD && args.pixmajor;
+  int pmr_pq = 0, pmr_n0 = 0, pmr_row0 = 0, pmr_t = 0;
+  unsigned pmr_mask = 0;
   unsigned long long pm_mask = 0;
   int pm_pq = 0, pm_n0 = 0, pm_r = 0, pm_s = 0;
   int row0 = 0, col0 = 0, zsplit = 0, ks_begin = 0, ks_end = 0, cur_tile = 0;
@@ -382,14 +392,24 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
     ks_begin = zsplit * args.ksteps_per_split;
     ks_end = min(ksteps, ks_begin + args.ksteps_per_split);
     if (MODE != MODE_WGRAD) {
+      if (pmr) {
+        // row (pq, n): the tile's pixel and images; per chunk only the row's image stride
+        pmr_pq = row0 / gg.N;
+        pmr_n0 = row0 - pmr_pq * gg.N;
+        pmr_row0 = row0;
+        const int img = MODE == MODE_FWD ? gg.H * gg.W * gg.C : gg.P * gg.Q * gg.K;
 #pragma unroll
-      for (int i = 0; i < CA; ++i) {
-        const RowInfo ri = row_info<MODE>(args, row0 + (tid >> 3) + 32 * i);
-        a_h0[i] = ri.h0;
-        a_w0[i] = ri.w0;
-        const int e = (MODE == MODE_FWD) ? ri.base + (ri.h0 * gg.W + ri.w0) * gg.C
-                                         : ri.base + (ri.h0 * gg.Q + ri.w0) * gg.K;
-        a_off[i] = 2 * (e + (fast ? lcA * 8 : 0));
+        for (int i = 0; i < CA; ++i) a_off[i] = 2 * (((tid >> 3) + 32 * i) * img + lcA * 8);
+      } else {
+#pragma unroll
+        for (int i = 0; i < CA; ++i) {
+          const RowInfo ri = row_info<MODE>(args, row0 + (tid >> 3) + 32 * i);
+          a_h0[i] = ri.h0;
+          a_w0[i] = ri.w0;
+          const int e = (MODE == MODE_FWD) ? ri.base + (ri.h0 * gg.W + ri.w0) * gg.C
+                                           : ri.base + (ri.h0 * gg.Q + ri.w0) * gg.K;
+          a_off[i] = 2 * (e + (fast ? lcA * 8 : 0));
+        }
       }
       if (MODE == MODE_FWD && args.d2x2) {
         // dense 2x2: column (p, q, k) reads Wc row k; the tap follows (p, q) and the k-step
@@ -427,12 +447,38 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
                                    : (int)kOOB;
         }
       }
-      // decomposition of the first reduction index (fast: of the k-step; slow: of the chunk)
-      const int kk = ks_begin * BK + (fast ? 0 : lcA * 8);
-      const int rs = kk / cdim;
-      kc = kk - rs * cdim;
-      kr = rs / Sdec;
-      ks_ = rs - kr * Sdec;
+      if (pmr) {
+        // the taps that keep the tile's pixel inside the image; this split's share of their
+        // k-steps; the first one's tap and channel block
+        const int pp = pmr_pq / gg.Q, qq = pmr_pq - pp * gg.Q, kb = cdim / BK;
+        unsigned m = 0;
+        for (int r = 0; r < gg.R; ++r)
+          for (int s2 = 0; s2 < gg.S; ++s2) {
+            const bool ok = MODE == MODE_FWD
+                ? (unsigned)(pp + r - gg.pad) < (unsigned)gg.H && (unsigned)(qq + s2 - gg.pad) < (unsigned)gg.W
+                : (unsigned)(pp - r + gg.pad) < (unsigned)gg.P && (unsigned)(qq - s2 + gg.pad) < (unsigned)gg.Q;
+            if (ok) m |= 1u << (r * gg.S + s2);
+          }
+        pmr_mask = m;
+        const int V = __builtin_popcount(m) * kb;
+        const int per = (V + args.splits - 1) / args.splits;
+        ks_begin = min(V, zsplit * per);
+        ks_end = min(V, ks_begin + per);
+        int jv = ks_begin / kb;
+        unsigned mm = m;
+        for (; jv > 0 && mm; --jv) mm &= mm - 1;
+        pmr_t = mm ? __builtin_ctz(mm) : 0;
+        kc = (ks_begin - (ks_begin / kb) * kb) * BK;
+        kr = pmr_t / gg.S;
+        ks_ = pmr_t - kr * gg.S;
+      } else {
+        // decomposition of the first reduction index (fast: of the k-step; slow: of the chunk)
+        const int kk = ks_begin * BK + (fast ? 0 : lcA * 8);
+        const int rs = kk / cdim;
+        kc = kk - rs * cdim;
+        kr = rs / Sdec;
+        ks_ = rs - kr * Sdec;
+      }
     } else {
       constexpr int NCA = BM / 8;
 #pragma unroll
@@ -506,7 +552,27 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
     unsigned short* As = smem + buf * STAGE;
     unsigned short* Bs = As + TILE_A;
     const int k0 = ks * BK;
-    if (MODE != MODE_WGRAD) {
+    if (MODE != MODE_WGRAD && pmr) {
+      const int pp = pmr_pq / gg.Q, qq = pmr_pq - pp * gg.Q;
+      const int hh = MODE == MODE_FWD ? pp + kr - gg.pad : pp - kr + gg.pad;
+      const int ww = MODE == MODE_FWD ? qq + ks_ - gg.pad : qq - ks_ + gg.pad;
+      const int sa = MODE == MODE_FWD ? 2 * (((pmr_n0 * gg.H + hh) * gg.W + ww) * cdim + kc)
+                                      : 2 * (((pmr_n0 * gg.P + hh) * gg.Q + ww) * cdim + kc);
+#pragma unroll
+      for (int i = 0; i < CA; ++i) dma_buf_s(rsA, a_off[i], sa, As + (wid * 64 + 256 * i) * 8);
+      const int boff = MODE == MODE_FWD ? 2 * (pmr_t * cdim + kc)
+                                        : 2 * ((kc * gg.R * gg.S + kr * gg.S + ks_) * gg.C);
+#pragma unroll
+      for (int i = 0; i < CB; ++i) dma_buf(rsB, b_off[i] + boff, Bs + (wid * 64 + 256 * i) * 8);
+      kc += BK;
+      if (kc == cdim) {  // next valid tap
+        kc = 0;
+        const unsigned rest = pmr_mask & ~((2u << pmr_t) - 1u);
+        pmr_t = rest ? __builtin_ctz(rest) : pmr_t;
+        kr = pmr_t / gg.S;
+        ks_ = pmr_t - kr * gg.S;
+      }
+    } else if (MODE != MODE_WGRAD) {
       const int W_ = MODE == MODE_FWD ? gg.W : gg.Q;
       if (fast) {
         // uniform tap (kr, ks_) and channel block kc: the per-chunk work is one bounds test
@@ -819,6 +885,8 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
           const int n = fast_div(row, args.dPQ), rem = row - n * hw;
           const int pi = fast_div(rem, args.dQ), pj = rem - pi * args.Wp;
           orow = ((size_t)n * g.H + args.pa + g.stride * pi) * g.W + args.pb + g.stride * pj;
+        } else if (pmr) {  // (pixel, image) row -> NHWC row
+          orow = (size_t)(pmr_n0 + row - pmr_row0) * (g.P * g.Q) + pmr_pq;
         }
         unsigned short* dst = args.out + orow * args.Ng + col;
         u16x8 o;
@@ -878,6 +946,8 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
         const int n = fast_div(row, args.dPQ), rem = row - n * hw;
         const int pi = fast_div(rem, args.dQ), pj = rem - pi * args.Wp;
         orow = (n * g.H + args.pa + g.stride * pi) * g.W + args.pb + g.stride * pj;
+      } else if (pmr) {  // (pixel, image) row -> NHWC row
+        orow = (pmr_n0 + row - pmr_row0) * (g.P * g.Q) + pmr_pq;
       }
       ro[i] = row < args.Mg ? orow * args.Ng + cbase : -1;
     }
@@ -1020,7 +1090,9 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
           }
         }
       } else if (split) {
-        *reinterpret_cast<float4*>(slab + (size_t)row * args.Ng + col) = (float4){v[0], v[1], v[2], v[3]};
+        // (pixel-major rows: the slab takes the NHWC row, so every finish kernel is unchanged)
+        const size_t srow = pmr ? (size_t)(pmr_n0 + row - pmr_row0) * (g.P * g.Q) + pmr_pq : (size_t)row;
+        *reinterpret_cast<float4*>(slab + srow * args.Ng + col) = (float4){v[0], v[1], v[2], v[3]};
       } else {
         const unsigned short h0 = f2bf(v[0] + bias.x), h1 = f2bf(v[1] + bias.y);
         const unsigned short h2 = f2bf(v[2] + bias.z), h3 = f2bf(v[3] + bias.w);
@@ -1033,6 +1105,8 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
           const int n = fast_div(row, args.dPQ), rem = row - n * hw;
           const int i = fast_div(rem, args.dQ), j = rem - i * args.Wp;
           orow = ((size_t)n * gg.H + args.pa + gg.stride * i) * gg.W + args.pb + gg.stride * j;
+        } else if (pmr) {  // (pixel, image) row -> NHWC row
+          orow = (size_t)(pmr_n0 + row - pmr_row0) * (gg.P * gg.Q) + pmr_pq;
         }
         if (MODE == MODE_DGRAD && args.accumulate) {  // dx += (second gradient branch)
           uint2* dst = reinterpret_cast<uint2*>(args.out + orow * args.Ng + col);
@@ -2056,8 +2130,18 @@ static void launch_gemm(const ConvArgs& a, int items, hipStream_t st) {
 // pixel-major WGRAD (ConvArgs::pixmajor) for this tile: stride-1 "same" conv, 64-image blocks,
 // at most 64 output pixels per image, one tap per column tile. ddp_conv_wgrad_pm_set(0) keeps
 // the pixel-order reduction (tests compare the two).
-static int g_wgrad_pm = 1;
+static int g_wgrad_pm = 1, g_rows_pm = 1;
 extern "C" void ddp_conv_wgrad_pm_set(int on) { g_wgrad_pm = on ? 1 : 0; }
+extern "C" void ddp_conv_rows_pm_set(int on) { g_rows_pm = on ? 1 : 0; }
+// pixel-major FWD / DGRAD rows (ConvArgs::pixmajor) for a BM-row tile
+template <int MODE>
+static bool rows_pixmajor_ok(const ConvArgs& a, int BM) {
+  const ConvGeom& g = a.g;
+  const int cdim = MODE == MODE_FWD ? g.C : g.K;
+  return g_rows_pm && !a.d2x2 && !a.phase && !a.accumulate && g.stride == 1 && g.P == g.H &&
+         g.Q == g.W && cdim % 64 == 0 && g.N % BM == 0 && g.P * g.Q <= 64 && g.R * g.S <= 32 &&
+         g.Creal == g.C && a.Mg == g.N * g.P * g.Q;
+}
 static bool wgrad_pixmajor_ok(const ConvArgs& a, int BN) {
   const ConvGeom& g = a.g;
   return g_wgrad_pm && g.stride == 1 && g.P == g.H && g.Q == g.W && g.N % 64 == 0 &&
@@ -2076,7 +2160,7 @@ static int prepare_cfg(ConvArgs& a, int splits) {
   a.splits = splits;
   a.ksteps_per_split = per;
   a.epi_stage = MODE != MODE_WGRAD && epi_stage_enabled();
-  a.pixmajor = MODE == MODE_WGRAD && wgrad_pixmajor_ok(a, BN);
+  a.pixmajor = MODE == MODE_WGRAD ? wgrad_pixmajor_ok(a, BN) : rows_pixmajor_ok<MODE>(a, BM);
   if (MODE == MODE_DGRAD) {
     const int hh = a.phase ? a.Hp : a.g.H, ww = a.phase ? a.Wp : a.g.W;
     a.dPQ = make_fastdiv(std::max(1, hh * ww));

@@ -186,6 +186,50 @@ def test_conv_wgrad_pixel_major(native_ext, case, tile, sd, sw, pm):
     assert rel_err(dw, wr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("rows_pm", [1, 0])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("splits", [0, 3])
+@pytest.mark.parametrize("case", [(128, 256, 4, 4, 512), (256, 128, 8, 8, 256),
+                                  (128, 512, 2, 2, 512), (64, 512, 4, 4, 256)])
+def test_conv_rows_pixel_major(native_ext, case, splits, tile, rows_pm):
+    """Pixel-major FWD / DGRAD rows (conv_igemm.hip ConvArgs::pixmajor: a row tile = one pixel of
+    BM images, the padding taps' k-steps skipped, NHWC epilogue / slab rows) on every forced tile
+    (pixel-major only where BM divides the batch), unsplit and split 3 ways (slabs + finish),
+    the BN statistics of the rounded z included — against fp32 PyTorch; rows_pm = 0 the same."""
+    from ddp_amd.ops.common import ptr, stream_handle, workspace
+    N, Cin, H, W, K = case
+    conv, spec, x, xn = _conv_setup(N, Cin, H, W, K, 3, 1, 1)
+    ws = workspace(xn.device)
+    g = spec.geom(N, H, W)
+    z = torch.empty(N, H, W, K, dtype=torch.bfloat16, device=DEV)
+    stats = torch.zeros(16 * 2 * K, device=DEV)
+    dz = bf(torch.randn(N, K, H, W, device=DEV))
+    dzn = dz.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16)
+    dx = torch.empty_like(xn)
+    native_ext.conv_rows_pm_set(rows_pm)
+    native_ext.conv_force_tile(tile + 1, 0)
+    native_ext.conv_dense2x2_set(0)  # (2x2: the implicit GEMM, so the rows path is exercised)
+    try:
+        native_ext.conv_fwd(g, ptr(xn), ptr(spec.wc), ptr(conv.bias), ptr(z), ptr(stats), ptr(ws),
+                            ws.numel(), splits, stream_handle())
+        native_ext.conv_dgrad(g, ptr(dzn), ptr(spec.wc), ptr(dx), ptr(ws), ws.numel(), splits,
+                              stream_handle())
+        torch.cuda.synchronize()
+    finally:
+        native_ext.conv_rows_pm_set(1)
+        native_ext.conv_force_tile(0, 0)
+        native_ext.conv_dense2x2_set(1)
+    ref = F.conv2d(x, conv.weight, conv.bias, 1, 1).permute(0, 2, 3, 1)
+    assert rel_err(z, ref) < 1e-2
+    zf = z.float().reshape(-1, K)
+    st = stats.view(16, 2 * K).sum(0)
+    assert torch.allclose(st[:K], zf.sum(0), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(st[K:], (zf * zf).sum(0), rtol=1e-3, atol=1e-2)
+    xr = x.clone().requires_grad_(True)
+    F.conv2d(xr, conv.weight.detach(), None, 1, 1).backward(dz)
+    assert rel_err(dx.permute(0, 3, 1, 2), xr.grad) < 1e-2
+
+
 @pytest.mark.parametrize("fmt", [torch.contiguous_format, torch.channels_last])
 def test_conv_wgrad_padded_layer0(native_ext, fmt):
     from ddp_amd.ops.layers import conv_backward

@@ -54,9 +54,10 @@ def main():
     ap.add_argument("--pairs", action="store_true",
                     help="tune the backward pair launch (DGRAD+WGRAD split-K factors, or separate "
                          "launches) of the stride-1 layers instead (--pair-sets)")
-    ap.add_argument("--pair-tiles", default="1,2,3,4",
+    ap.add_argument("--pair-tiles", default="1,2,3,4,5",
                     type=lambda v: [int(t) for t in v.split(",")],
-                    help="pair tiles to sweep (1 = 64x64, 2 = 128x128, 3 = 64x128, 4 = 128x64)")
+                    help="pair tiles to sweep (1 = 64x64, 2 = 128x128, 3 = 64x128, 4 = 128x64, "
+                         "5 = 128x128 with 3 LDS stages)")
     ap.add_argument("--pair-sets", default="vgg11:32,64,128,256",
                     help="model:batches[;model:batches], e.g. 'resnet50:256'")
     args = ap.parse_args()
@@ -271,7 +272,7 @@ def tune_pairs(args):
             # pair tiles (conv_igemm.hip kPairTiles): 1 = 64x64, 2 = 128x128, 3 = 64x128,
             # 4 = 128x64; a tile with fewer than ~64 work items before split-K is not tried
             tiles = [t for t, (bm, bn) in {1: (64, 64), 2: (128, 128), 3: (64, 128),
-                                           4: (128, 64)}.items()
+                                           4: (128, 64), 5: (128, 128)}.items()
                      if t in args.pair_tiles and
                      -(-Md // bm) * -(-Nd // bn) + -(-Mw // bm) * -(-Nw // bn) >= 64]
             for tile in tiles:
