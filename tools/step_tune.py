@@ -24,7 +24,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tools"))
 
-TILES = {0: None, 1: (64, 64), 2: (128, 128), 3: (64, 128), 4: (128, 64)}
+TILES = {0: None, 1: (64, 64), 2: (128, 128), 3: (64, 128), 4: (128, 64), 5: (128, 128)}
 
 
 def main():
