@@ -136,12 +136,15 @@ struct ConvArgs {
   // k-steps whose pixel it pushes into the zero padding are skipped: 31 % of them on a 4x4
   // layer, 56 % on 2x2, 16 % on 8x8 (VGG-11). Every surviving row is in range, so the gathers need
   // no border test and take the k-step's position as a scalar offset (soffset) — no per-chunk
-  // vector work at all. Needs N % 64 == 0 and P*Q <= 64 (the valid-pixel set is a 64-bit mask).
+  // vector work at all. Needs N % 64 == 0; a tap's valid pixels form a rectangle, walked
+  // row-major (ddp_conv_wgrad_pm_set: 1 = images of <= 64 pixels, 2 = any size).
   // FWD / DGRAD (host: rows_pixmajor_ok): the GEMM rows are ordered (pixel, image) and a row
   // tile holds one pixel of BM images, so the taps that reach into the padding are uniform over
   // the tile and their k-steps are skipped (31 % of them on a 4x4 layer, 16 % on 8x8); the A
   // gather is a scalar offset per k-step. The epilogues (and split-K slabs) store to the NHWC
-  // rows, so every finish kernel is unchanged. Needs N % BM == 0 and P*Q <= 64.
+  // rows, so every finish kernel is unchanged. Needs N % BM == 0 and R*S <= 32 (the valid taps
+  // are a 32-bit mask); ddp_conv_rows_pm_set picks the images (<= 64 pixels or any, all convs
+  // or R*S > 1 only).
   int pixmajor;
 };
 
@@ -351,15 +354,15 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
   const int w_dp = wsame ? (BK / gg.Q) % gg.P : 0;        // p advance per k-step (mod P)
   const int w_dm = wsame ? 2 * BK * gg.C : 0;             // byte advance per k-step
   // pixel-major WGRAD (ConvArgs::pixmajor): the k-step's (image block n0, pixel pq) and the
-  // tile's tap (pm_r, pm_s), all uniform; pm_mask = the pixels the tap keeps inside the image
+  // tile's tap (pm_r, pm_s), all uniform; the pixels the tap keeps inside the image are the
+  // rectangle [p_lo, p_hi) x [pm_qlo, pm_qhi), walked row-major from (pm_p, pm_q)
   const bool pm = MODE == MODE_WGRAD && args.pixmajor;
   // pixel-major FWD / DGRAD rows: the item's pixel, first image and first row; the pixel's
   // valid taps and the k-step's tap
   const bool pmr = MODE != MODE_WGRAD && args.pixmajor;
   int pmr_pq = 0, pmr_n0 = 0, pmr_row0 = 0, pmr_t = 0;
   unsigned pmr_mask = 0;
-  unsigned long long pm_mask = 0;
-  int pm_pq = 0, pm_n0 = 0, pm_r = 0, pm_s = 0;
+  int pm_p = 0, pm_q = 0, pm_qlo = 0, pm_qhi = 0, pm_n0 = 0, pm_r = 0, pm_s = 0;
   int row0 = 0, col0 = 0, zsplit = 0, ks_begin = 0, ks_end = 0, cur_tile = 0;
   int d2pos = 0;         // dense 2x2: the column tile's output pixel (FWD) / input pixel (DGRAD)
   const bool phase = MODE == MODE_DGRAD && args.phase;
@@ -497,25 +500,21 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
         const int t = col0 / gg.C;
         pm_r = t / gg.S;
         pm_s = t - pm_r * gg.S;
+        // the pixels (p, q) with (p + r - pad, q + s - pad) inside the image: a rectangle
         const int PQ = gg.P * gg.Q, nb = gg.N / BK;
-        unsigned long long m = 0;
-        for (int pq = 0; pq < PQ; ++pq) {
-          const int pp = pq / gg.Q, qq = pq - pp * gg.Q;
-          if ((unsigned)(pp + pm_r - gg.pad) < (unsigned)gg.H &&
-              (unsigned)(qq + pm_s - gg.pad) < (unsigned)gg.W)
-            m |= 1ull << pq;
-        }
-        pm_mask = m;
-        const int V = __builtin_popcountll(m) * nb;
+        const int p_lo = max(0, gg.pad - pm_r), p_hi = min(gg.P, gg.H + gg.pad - pm_r);
+        pm_qlo = max(0, gg.pad - pm_s);
+        pm_qhi = min(gg.Q, gg.W + gg.pad - pm_s);
+        const int nq = max(0, pm_qhi - pm_qlo);
+        const int V = max(0, p_hi - p_lo) * nq * nb;
         const int per = (V + args.splits - 1) / args.splits;
         ks_begin = min(V, zsplit * per);
         ks_end = min(V, ks_begin + per);
-        // the first k-step's pixel: the (ks_begin / nb)-th valid one
-        int jv = ks_begin / nb;
-        unsigned long long mm = m;
-        for (; jv > 0 && mm; --jv) mm &= mm - 1;
-        pm_pq = mm ? __builtin_ctzll(mm) : 0;
-        pm_n0 = (ks_begin - (ks_begin / nb) * nb) * BK;
+        // the first k-step's pixel: the (ks_begin / nb)-th of the rectangle, row-major
+        const int jv = ks_begin / nb;
+        pm_p = p_lo + (nq ? jv / nq : 0);
+        pm_q = pm_qlo + (nq ? jv - (jv / nq) * nq : 0);
+        pm_n0 = (ks_begin - jv * nb) * BK;
         constexpr int NCA = BM / 8;
         constexpr int NCB = BN / 8;
 #pragma unroll
@@ -650,9 +649,8 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
       constexpr int NCB = BN / 8;
       if (pm) {  // (k-steps are issued in order: advance (n0, pq) after each)
         const int PQ = gg.P * gg.Q;
-        const int pp = pm_pq / gg.Q, qq = pm_pq - pp * gg.Q;
-        const int sa = 2 * ((pm_n0 * PQ + pm_pq) * gg.K);
-        const int sb = 2 * ((pm_n0 * gg.H + pp + pm_r - gg.pad) * gg.W + qq + pm_s - gg.pad) * gg.C;
+        const int sa = 2 * ((pm_n0 * PQ + pm_p * gg.Q + pm_q) * gg.K);
+        const int sb = 2 * ((pm_n0 * gg.H + pm_p + pm_r - gg.pad) * gg.W + pm_q + pm_s - gg.pad) * gg.C;
 #pragma unroll
         for (int i = 0; i < CA; ++i) dma_buf_s(rsA, a_off[i], sa, As + (wid * 64 + 256 * i) * 8);
 #pragma unroll
@@ -660,8 +658,10 @@ __device__ __forceinline__ void conv_igemm_body(const ConvArgs& args, unsigned s
         pm_n0 += BK;
         if (pm_n0 == gg.N) {
           pm_n0 = 0;
-          const unsigned long long rest = pm_mask & ~((2ull << pm_pq) - 1ull);
-          pm_pq = rest ? __builtin_ctzll(rest) : pm_pq;
+          if (++pm_q == pm_qhi) {
+            pm_q = pm_qlo;
+            ++pm_p;
+          }
         }
         return;
       }
@@ -2131,21 +2131,25 @@ static void launch_gemm(const ConvArgs& a, int items, hipStream_t st) {
 // at most 64 output pixels per image, one tap per column tile. ddp_conv_wgrad_pm_set(0) keeps
 // the pixel-order reduction (tests compare the two).
 static int g_wgrad_pm = 1, g_rows_pm = 1;
-extern "C" void ddp_conv_wgrad_pm_set(int on) { g_wgrad_pm = on ? 1 : 0; }
-extern "C" void ddp_conv_rows_pm_set(int on) { g_rows_pm = on ? 1 : 0; }
+// WGRAD: 0 off, 1 the <= 64-pixel images, 2 any image size
+extern "C" void ddp_conv_wgrad_pm_set(int mode) { g_wgrad_pm = std::max(0, std::min(2, mode)); }
+// rows: 0 off, 1 the <= 64-pixel images, 2 any image size, 3 / 4 = 1 / 2 for R*S > 1 only
+extern "C" void ddp_conv_rows_pm_set(int mode) { g_rows_pm = std::max(0, std::min(4, mode)); }
 // pixel-major FWD / DGRAD rows (ConvArgs::pixmajor) for a BM-row tile
 template <int MODE>
 static bool rows_pixmajor_ok(const ConvArgs& a, int BM) {
   const ConvGeom& g = a.g;
   const int cdim = MODE == MODE_FWD ? g.C : g.K;
+  const bool any_pq = g_rows_pm == 2 || g_rows_pm == 4;
+  if (g_rows_pm >= 3 && g.R * g.S == 1) return false;
   return g_rows_pm && !a.d2x2 && !a.phase && !a.accumulate && g.stride == 1 && g.P == g.H &&
-         g.Q == g.W && cdim % 64 == 0 && g.N % BM == 0 && g.P * g.Q <= 64 && g.R * g.S <= 32 &&
-         g.Creal == g.C && a.Mg == g.N * g.P * g.Q;
+         g.Q == g.W && cdim % 64 == 0 && g.N % BM == 0 && (any_pq || g.P * g.Q <= 64) &&
+         g.R * g.S <= 32 && g.Creal == g.C && a.Mg == g.N * g.P * g.Q;
 }
 static bool wgrad_pixmajor_ok(const ConvArgs& a, int BN) {
   const ConvGeom& g = a.g;
   return g_wgrad_pm && g.stride == 1 && g.P == g.H && g.Q == g.W && g.N % 64 == 0 &&
-         g.P * g.Q <= 64 && g.C % BN == 0 && g.Creal == g.C && a.Ng == g.R * g.S * g.C &&
+         (g_wgrad_pm == 2 || g.P * g.Q <= 64) && g.C % BN == 0 && g.Creal == g.C && a.Ng == g.R * g.S * g.C &&
          a.Kg == g.N * g.P * g.Q;
 }
 

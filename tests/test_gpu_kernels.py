@@ -151,16 +151,18 @@ def test_conv_bwd_pair_forced_splits(native_ext, case, sd, sw, tile):
     assert rel_err(dw, wr.grad) < 1e-2
 
 
-@pytest.mark.parametrize("pm", [1, 0])
+@pytest.mark.parametrize("pm", [1, 2, 0])
 @pytest.mark.parametrize("tile,sd,sw", [(0, 1, 1), (1, 1, 1), (1, 2, 4), (2, 3, 2), (2, 1, 6),
                                         (3, 2, 3), (4, 1, 8), (5, 1, 4)])
 @pytest.mark.parametrize("case", [(64, 512, 2, 2, 512), (64, 256, 4, 4, 512), (128, 512, 4, 4, 512),
-                                  (64, 256, 8, 8, 256), (128, 128, 8, 8, 256)])
+                                  (64, 256, 8, 8, 256), (128, 128, 8, 8, 256), (64, 64, 16, 16, 128),
+                                  (64, 64, 14, 14, 64)])
 def test_conv_wgrad_pixel_major(native_ext, case, tile, sd, sw, pm):
     """Pixel-major WGRAD reduction (conv_igemm.hip ConvArgs::pixmajor: (pixel, 64 images)
     k-steps, the taps' padding k-steps skipped, scalar-offset gathers) on the 2x2 / 4x4 / 8x8
     layers at 64 / 128 images, as the pair's WGRAD half (tile 1..5, forced splits) and as the
-    separate launch (tile 0), against fp32 PyTorch — and pm = 0 (pixel order) the same."""
+    separate launch (tile 0), against fp32 PyTorch — pm = 2 also on the 16x16 / 14x14 images
+    (the tap's valid pixels walked as a rectangle), pm = 0 (pixel order) the same."""
     from ddp_amd.ops.layers import conv_backward
     N, Cin, H, W, K = case
     conv, spec, x, xn = _conv_setup(N, Cin, H, W, K, 3, 1, 1)
@@ -186,16 +188,18 @@ def test_conv_wgrad_pixel_major(native_ext, case, tile, sd, sw, pm):
     assert rel_err(dw, wr.grad) < 1e-2
 
 
-@pytest.mark.parametrize("rows_pm", [1, 0])
+@pytest.mark.parametrize("rows_pm", [1, 2, 0])
 @pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("splits", [0, 3])
 @pytest.mark.parametrize("case", [(128, 256, 4, 4, 512), (256, 128, 8, 8, 256),
-                                  (128, 512, 2, 2, 512), (64, 512, 4, 4, 256)])
+                                  (128, 512, 2, 2, 512), (64, 512, 4, 4, 256),
+                                  (64, 64, 16, 16, 128), (64, 64, 14, 14, 64)])
 def test_conv_rows_pixel_major(native_ext, case, splits, tile, rows_pm):
     """Pixel-major FWD / DGRAD rows (conv_igemm.hip ConvArgs::pixmajor: a row tile = one pixel of
     BM images, the padding taps' k-steps skipped, NHWC epilogue / slab rows) on every forced tile
     (pixel-major only where BM divides the batch), unsplit and split 3 ways (slabs + finish),
-    the BN statistics of the rounded z included — against fp32 PyTorch; rows_pm = 0 the same."""
+    the BN statistics of the rounded z included — against fp32 PyTorch; rows_pm = 2 also takes
+    the images above 64 pixels (16x16, 14x14), rows_pm = 0 none."""
     from ddp_amd.ops.common import ptr, stream_handle, workspace
     N, Cin, H, W, K = case
     conv, spec, x, xn = _conv_setup(N, Cin, H, W, K, 3, 1, 1)

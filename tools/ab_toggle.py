@@ -29,7 +29,7 @@ def main():
     a = ap.parse_args()
     import torch
     import ddp_amd
-    from ddp_amd.data import DeviceLoader, SyntheticCIFAR10
+    from ddp_amd.data import DeviceLoader, SyntheticCIFAR10, SyntheticImageNet
     from ddp_amd.engine import CrossEntropyLoss, TrainStep
     from ddp_amd.models import build
     from ddp_amd.optim import FusedSGD
@@ -39,7 +39,8 @@ def main():
     dev = torch.device("cuda", 0)
     for B in [int(b) for b in a.batches.split(",")]:
         torch.manual_seed(ddp_amd.SEED)
-        loader = DeviceLoader(SyntheticCIFAR10(True), B, dev, 1, 0, train=True, cpad=8)
+        ds = SyntheticImageNet(True, n=4 * B) if a.model == "resnet50" else SyntheticCIFAR10(True)
+        loader = DeviceLoader(ds, B, dev, 1, 0, train=True, cpad=8)
         model = build(a.model).to(dev)
         opt = FusedSGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
         crit = CrossEntropyLoss()
