@@ -303,6 +303,8 @@ void ddp_conv_tune_set(int mode, int M, int N, int K, int tile, int splits, int 
 void ddp_conv_pair_tune_set(int M, int N, int K, int hw, int tile, int sd, int sw);
 void ddp_conv_wgrad_pm_set(int on);
 void ddp_conv_rows_pm_set(int on);
+// tap-reuse forward: split-K combined inside the launch (1) or slabs + a finish launch (0, default)
+void ddp_conv_tr_inlaunch_set(int on);
 // dense 2x2 form of 3x3 / s1 / p1 convs over 2x2 images (conv_igemm.hip ConvArgs::d2x2): ok =
 // this geometry takes it (FWD and DGRAD), set = switch it on / off (tests)
 int ddp_conv_dense2x2_ok(const ddp_amd::ConvGeom* g);

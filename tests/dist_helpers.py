@@ -454,6 +454,7 @@ def uid_bootstrap_worker(rank, world, port, q):
         b = cm.RcclCommunicator(rank, world, 0, key="ddp_amd/rccl_uid_overlap")
         c = cm.RcclCommunicator(rank, world, 0)
         out = {"uids": [x.comm.uid.hex() for x in (a, b, c)], "live": a.live and c.live}
+        dist.barrier()  # rank 0 hosts the store: nobody leaves while a peer may still read it
         dist.destroy_process_group()
         q.put((rank, out))
     except Exception:
