@@ -305,6 +305,9 @@ void ddp_conv_wgrad_pm_set(int on);
 void ddp_conv_rows_pm_set(int on);
 // tap-reuse forward: split-K combined inside the launch (1) or slabs + a finish launch (0, default)
 void ddp_conv_tr_inlaunch_set(int on);
+// BatchNorm backward: fold the finalize into the apply while the grid's replica re-reads stay
+// within this many MB (default 32)
+void ddp_bn_fold_bwd_mb(int mb);
 // dense 2x2 form of 3x3 / s1 / p1 convs over 2x2 images (conv_igemm.hip ConvArgs::d2x2): ok =
 // this geometry takes it (FWD and DGRAD), set = switch it on / off (tests)
 int ddp_conv_dense2x2_ok(const ddp_amd::ConvGeom* g);

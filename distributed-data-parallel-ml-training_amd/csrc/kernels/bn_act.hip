@@ -902,8 +902,10 @@ extern "C" int ddp_bn_act_fwd(const BnArgs* args, hipStream_t st) {
 static size_t kBwdBlocks = 1024;
 
 // Largest grid-wide replica re-read of a folded backward apply (default
-// 32 MB; 0 = always the separate finalize launch)
-static size_t fold_bwd_bytes() { return (size_t)32 << 20; }
+// 32 MB; 0 = always the separate finalize launch; ddp_bn_fold_bwd_mb for A/B studies)
+static size_t g_fold_bwd_mb = 32;
+static size_t fold_bwd_bytes() { return g_fold_bwd_mb << 20; }
+extern "C" void ddp_bn_fold_bwd_mb(int mb) { g_fold_bwd_mb = (size_t)(mb < 0 ? 0 : mb); }
 
 // Reduce-grid cap (kReduceGrid, 0 = uncapped): the reduce walks its item blocks
 // with a grid stride, so every block adds ONE partial sum per channel. Uncapped, ResNet-50's
