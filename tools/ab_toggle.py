@@ -2,6 +2,7 @@
 """In-process A/B of a native kernel switch on the captured VGG-11 training step (one MI355X).
 
     python tools/ab_toggle.py --setter conv_wgrad_pm_set --values 1,0 --batches 256,128,64,32
+    python tools/ab_toggle.py --const ddp_amd.ops.layers:FUSE_BN_IN_POOL_MAX_BATCH --values 32,64
 
 For each batch: one model / optimizer / loader; for every trial and every value, the switch is
 set (``native().<setter>(value)``), a fresh TrainStep is captured (the launch configuration is
@@ -20,7 +21,9 @@ sys.path.insert(0, REPO)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--setter", required=True)
+    ap.add_argument("--setter", default=None, help="native setter, e.g. conv_rows_pm_set")
+    ap.add_argument("--const", default=None,
+                    help="module constant instead, e.g. ddp_amd.ops.layers:FUSE_BN_IN_POOL_MAX_BATCH")
     ap.add_argument("--values", default="1,0")
     ap.add_argument("--batches", default="256,32")
     ap.add_argument("--model", default="vgg11")
@@ -34,7 +37,14 @@ def main():
     from ddp_amd.models import build
     from ddp_amd.optim import FusedSGD
     n = ddp_amd.native()
-    setter = getattr(n, a.setter)
+    if a.const:
+        import importlib
+        mod_name, attr = a.const.split(":")
+        mod = importlib.import_module(mod_name)
+        setter = lambda v: setattr(mod, attr, v)  # noqa: E731
+        a.setter = a.const
+    else:
+        setter = getattr(n, a.setter)
     values = [int(v) for v in a.values.split(",")]
     dev = torch.device("cuda", 0)
     for B in [int(b) for b in a.batches.split(",")]:
