@@ -263,20 +263,21 @@ RES_BN_FUSE = True
 # 1/stride^2 of dx it reaches — no zero fill of dx's untouched phases and no read-back of the
 # whole dx by an accumulating second branch (GradLink.deferred_dgrad)
 DS_DGRAD_DEFER = True
-# largest dgrad output H*W that takes the fused sums: 16 (4x4 / 2x2) from 128 images per GPU up,
-# 256 (also 16x16 / 8x8) at the strong-scaling shares of at most 64 images (b64 0.4556 vs 0.4594
-# ms, b32 0.3921 vs 0.3952; b128 / b256 unchanged, profiles/r4z3_bn_sums_threshold.md); a
-# number here sets one threshold for every batch (tests)
+# largest dgrad output H*W that takes the fused sums: 16 (4x4 / 2x2) at 256 images per GPU,
+# 256 (also 16x16 / 8x8) at the strong-scaling shares of at most 128 images (b64 0.4556 vs
+# 0.4594 ms, b32 0.3921 vs 0.3952, profiles/r4z3_bn_sums_threshold.md; b128 0.5320 vs 0.5353 on
+# the round-6 kernels, every one of 5 in-step trials lower, b256 0.7541 vs 0.7281,
+# profiles/r6ae_ab_constants.jsonl); a number here sets one threshold for every batch (tests)
 BN_BWD_FUSE_MAX_HW = None
 
 
 def bn_bwd_fuse_pays(H, W, pool=True, N=None):
     """Fuse the preceding block's BatchNorm-backward sums into this dgrad only when the dgrad
-    output is spatially small: H*W <= 16 (VGG's 4x4 / 2x2 layers), or <= 256 at N <= 64 images
+    output is spatially small: H*W <= 16 (VGG's 4x4 / 2x2 layers), or <= 256 at N <= 128 images
     (BN_BWD_FUSE_MAX_HW). Measured (VGG-11, tools/conv_tune.py and the step profiles): on the
     small outputs the fused epilogue costs 2-5 us less than the reduce kernel it replaces; on the
-    b128 / b256 16x16 / 8x8 outputs its z gather (4 loads per pooled pixel, exposed after the
-    MFMA loop) costs as much as the streaming reduce pass, at b32 / b64 the launch it saves wins.
+    b256 16x16 / 8x8 outputs its z gather (4 loads per pooled pixel, exposed after the MFMA
+    loop) costs more than the streaming reduce pass, at b32..b128 the launch it saves wins.
     Never without a pool (ResNet's conv1 -> conv2 -> conv3 chain): one z load per dgrad output
     element in the epilogue made the big dgrad GEMMs slower than the reduce pass it saves
     (ResNet-50 b256 30.65 vs 28.23 ms, profiles/r2_resnet50_b256.md; again in round 4: 9443 vs
@@ -285,7 +286,7 @@ def bn_bwd_fuse_pays(H, W, pool=True, N=None):
         return False
     lim = BN_BWD_FUSE_MAX_HW
     if lim is None:
-        lim = 256 if N is not None and N <= 64 else 16
+        lim = 256 if N is not None and N <= 128 else 16
     return H * W <= lim
 
 
