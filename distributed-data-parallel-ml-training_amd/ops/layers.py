@@ -383,8 +383,11 @@ def conv_backward(spec, x, dz, dweight, need_dx, link=None, weight=None, bnf=Non
 # False: conv_smallk + bn_act passes.
 L0_FUSE = True
 # ... and its BN-backward sums taken in the next block's dgrad split-K finish when that dgrad has
-# one (conv_igemm.hip BnBwdFuse::code; else l0_sums_kernel). False: always the separate pass
+# one (conv_igemm.hip BnBwdFuse::code; else l0_sums_kernel). False: always the separate pass.
+# Up to L0_SUMS_IN_FINISH_MAX_BATCH images per GPU: at b64 0.4312 vs 0.4336 ms, at b128 the
+# separate pass wins (0.5290 vs 0.5333; in-step A/B, every trial: profiles/r6af_ab_constants.jsonl)
 L0_SUMS_IN_FINISH = True
+L0_SUMS_IN_FINISH_MAX_BATCH = 64
 
 
 def l0_serves(spec, x):
@@ -672,6 +675,7 @@ class _ConvBNActFn(torch.autograd.Function):
                        ptr(ensure_grad(prev.bn.bias)))
         l0c = getattr(prev, "l0_code", None) if prev is not None else None
         if (bnf is None and L0_SUMS_IN_FINISH and l0c is not None and ctx.needs_input_grad[0]
+                and x.shape[0] <= L0_SUMS_IN_FINISH_MAX_BATCH
                 and ctx.in_link is None and spec.stride == 1 and prev.K == spec.C
                 and spec.C == spec.Cr and x.shape[1] * 2 == prev._out_p):
             # the input block's BN-backward sums in this dgrad's split-K finish (conv_l0.hip's
