@@ -308,6 +308,9 @@ void ddp_conv_tr_inlaunch_set(int on);
 // BatchNorm backward: fold the finalize into the apply while the grid's replica re-reads stay
 // within this many MB (default 32)
 void ddp_bn_fold_bwd_mb(int mb);
+// big BatchNorm layers: finalize folded into the apply on a capped grid of this many blocks
+// (0, default: separate finalize launch)
+void ddp_bn_fold_grid(int blocks);
 // dense 2x2 form of 3x3 / s1 / p1 convs over 2x2 images (conv_igemm.hip ConvArgs::d2x2): ok =
 // this geometry takes it (FWD and DGRAD), set = switch it on / off (tests)
 int ddp_conv_dense2x2_ok(const ddp_amd::ConvGeom* g);

@@ -820,7 +820,9 @@ constexpr size_t kFoldBytes = 24u << 20;
 // separate finalize launches (profiles/r5v_bn_fold.md) — the 25088-block streaming applies
 // lose more to the capped grid than the finalize launch costs.
 constexpr size_t kFoldGridBytes = 64u << 20;
-static unsigned fold_fwd_grid() { return 0u; }
+static unsigned g_fold_grid = 0;  // ddp_bn_fold_grid (A/B studies)
+static unsigned fold_fwd_grid() { return g_fold_grid; }
+extern "C" void ddp_bn_fold_grid(int blocks) { g_fold_grid = blocks > 0 ? (unsigned)blocks : 0u; }
 
 template <bool POOL, int IPT, bool MASK>
 static void launch_fwd_m(const BnArgs& a, size_t items, hipStream_t st) {
