@@ -10,7 +10,9 @@ import sys
 
 def main(prefix, title="rocprofv3 kernel summary"):
     stats = list(csv.DictReader(open(prefix + "_kernel_stats.csv")))
-    trace = list(csv.DictReader(open(prefix + "_kernel_trace.csv")))
+    # (rocprofv3 writes the rows in completion / buffer order, not launch order)
+    trace = sorted(csv.DictReader(open(prefix + "_kernel_trace.csv")),
+                   key=lambda r: int(r["Start_Timestamp"]))
     print(f"# {title}\n")
     print("## Top kernels (whole run)\n")
     print("| kernel | calls | total ms | avg us | % |")
