@@ -512,7 +512,6 @@ PYBIND11_MODULE(_native, m) {
   m.def("conv_tune_clear", []() { ddp_conv_tune_clear(); });
   m.def("conv_wgrad_pm_set", [](int on) { ddp_conv_wgrad_pm_set(on); });
   m.def("conv_rows_pm_set", [](int on) { ddp_conv_rows_pm_set(on); });
-  m.def("conv_tr_inlaunch_set", [](int on) { ddp_conv_tr_inlaunch_set(on); });
   m.def("bn_fold_bwd_mb", [](int mb) { ddp_bn_fold_bwd_mb(mb); });
   m.def("bn_fold_grid", [](int blocks) { ddp_bn_fold_grid(blocks); });
   m.def("conv_pair_tune_set", [](int M, int N, int K, int hw, int tile, int sd, int sw) {

@@ -303,8 +303,6 @@ void ddp_conv_tune_set(int mode, int M, int N, int K, int tile, int splits, int 
 void ddp_conv_pair_tune_set(int M, int N, int K, int hw, int tile, int sd, int sw);
 void ddp_conv_wgrad_pm_set(int on);
 void ddp_conv_rows_pm_set(int on);
-// tap-reuse forward: split-K combined inside the launch (1) or slabs + a finish launch (0, default)
-void ddp_conv_tr_inlaunch_set(int on);
 // BatchNorm backward: fold the finalize into the apply while the grid's replica re-reads stay
 // within this many MB (default 32)
 void ddp_bn_fold_bwd_mb(int mb);

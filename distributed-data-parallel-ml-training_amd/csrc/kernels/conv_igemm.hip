@@ -2676,14 +2676,6 @@ extern "C" int ddp_conv_fwd_bn(const ConvGeom* g, const void* x, const void* wc,
 // Split-K finish of a FWD GEMM computed elsewhere (conv_tr.hip's tap-reuse kernel): slabs
 // [splits][N*P*Q][K] -> bias + bf16 z + statistics, or with ``bn`` (small problems) the
 // BatchNorm-fused finish (*bn_done = 1). Returns the HIP error code.
-// would ddp_conv_fwd_finish run the BatchNorm forward of bn in the finish (launch_finish_bnfwd)?
-extern "C" int ddp_conv_fwd_finish_fuses_bn(const ConvGeom* g, const BnFwdFuse* bn) {
-  if (!bn) return 0;
-  const int Mg = g->N * g->P * g->Q;
-  return Mg <= kBnFwdFuseMaxRows && Mg <= bn_fuse_max_rows() && g->K % 16 == 0 &&
-         bn->P * bn->Q > 0 && Mg % (bn->P * bn->Q) == 0 && (!bn->pool || (bn->P % 2 == 0 && bn->Q % 2 == 0));
-}
-
 extern "C" int ddp_conv_fwd_finish(const ConvGeom* g, float* ws, int splits, const float* bias,
                                    void* z, float* stats, const BnFwdFuse* bn, int* bn_done,
                                    hipStream_t st) {

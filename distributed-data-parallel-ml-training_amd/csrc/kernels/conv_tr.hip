@@ -114,29 +114,7 @@ struct Args {
   float* in_coef;            // [6][C]: scale, shift, mean, invstd (written by block 0)
   unsigned short* y_out;     // [N][H][W][C]
   int z_bytes;
-  // in-launch split-K reduction (null: slabs + a finish launch): per-tile arrival tickets,
-  // zero between launches (the reducing block resets its tile's)
-  unsigned* tickets;
-  int ws_bytes;
 };
-
-// In-launch split-K combine (cdna_hip_programming.md §4 "In-launch split-K reduction", the
-// Guideline 16 R1 form): every split block stores its fp32 slab tile WRITE-THROUGH (sc1 16-B
-// buffer stores: no release fence), every wave drains its stores, one lane takes the tile's
-// ticket with a relaxed agent-scope add, and the block that draws the last ticket reads every
-// slab of the tile with sc1 loads (L1 bypassed, any XCD placement) in split order — the same
-// fixed order as the finish kernel, so the sum does not depend on which block arrives last.
-constexpr int kTickets = 1 << 16;
-__device__ unsigned g_tickets[kTickets];  // zero at code-object load; reset by each reducer
-constexpr int kSc1 = 16;                  // buffer instruction cache-policy bit: sc1
-typedef unsigned v4u32 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ void store_sc1(__amdgpu_buffer_rsrc_t rs, int byte_off, const f32x4& v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, v), rs, byte_off, 0, kSc1);
-}
-__device__ __forceinline__ f32x4 load_sc1(__amdgpu_buffer_rsrc_t rs, int byte_off) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, kSc1));
-}
 
 template <int BM, int BN, int NST, int NL, int IN>
 #ifndef DDP_TR_WAVES_PER_EU
@@ -405,58 +383,21 @@ void conv_tr_fwd_kernel(Args a) {
   // ---- epilogue: acc[i][j][v] = D[row0 + wm*WTM + i*16 + (lane&15)][col0 + wn*WTN + j*16 + 4*(lane>>4) + v]
   const int rl = lane & 15, cq = 4 * (lane >> 4);
   const int cbase = col0 + wn * WTN + cq;
-  int srep = blockIdx.x;  // statistics replica: the block id of the tile's split 0 (in-launch)
   if (a.splits > 1) {
-    if (a.tickets == nullptr) {
-      float* slab = a.ws + (size_t)sp * M * K;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = row0 + wm * WTM + i * 16 + rl;
-        if (row >= M) continue;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int col = cbase + j * 16;
-          if (col >= K) continue;
-          const f32x4 v = acc[i][j];
-          *reinterpret_cast<float4*>(slab + (size_t)row * K + col) = (float4){v[0], v[1], v[2], v[3]};
-        }
-      }
-      return;
-    }
-    // in-launch combine (M % BM == 0 and K % BN == 0 here: every fragment is in range)
-    const __amdgpu_buffer_rsrc_t rsW = make_rsrc(a.ws, a.ws_bytes);
-    const int slab_bytes = M * K * 4;
+    float* slab = a.ws + (size_t)sp * M * K;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int row = row0 + wm * WTM + i * 16 + rl;
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        store_sc1(rsW, sp * slab_bytes + (row * K + cbase + j * 16) * 4, acc[i][j]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
-    __syncthreads();
-    unsigned* flag = reinterpret_cast<unsigned*>(smem);  // (operand space: the k-loop is over)
-    if (tid == 0) {
-      const unsigned old = __hip_atomic_fetch_add(a.tickets + tile, 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned last = old == (unsigned)(a.splits - 1) ? 1u : 0u;
-      if (last) __hip_atomic_store(a.tickets + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      flag[0] = last;
-    }
-    __syncthreads();
-    if (flag[0] == 0u) return;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int row = row0 + wm * WTM + i * 16 + rl;
+      if (row >= M) continue;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int off = (row * K + cbase + j * 16) * 4;
-        f32x4 v = load_sc1(rsW, off);
-        for (int z = 1; z < a.splits; ++z) v += load_sc1(rsW, z * slab_bytes + off);
-        acc[i][j] = v;
+        const int col = cbase + j * 16;
+        if (col >= K) continue;
+        const f32x4 v = acc[i][j];
+        *reinterpret_cast<float4*>(slab + (size_t)row * K + col) = (float4){v[0], v[1], v[2], v[3]};
       }
     }
-    srep = blockIdx.x - sp * tiles;
+    return;
   }
   const bool red = a.stats != nullptr;
   float* sl = reinterpret_cast<float*>(smem);
@@ -502,7 +443,7 @@ void conv_tr_fwd_kernel(Args a) {
   if (!red) return;
   __syncthreads();
   if (wm == 0 && rl == 0) {
-    float* st = a.stats + stat_rep(srep) * 2 * K;
+    float* st = a.stats + stat_rep(blockIdx.x) * 2 * K;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int col = cbase + j * 16;
@@ -511,8 +452,8 @@ void conv_tr_fwd_kernel(Args a) {
       const float* s1 = sl + ((((2 + wn) * TN + j) * 4 + (lane >> 4)) * 8);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        atomicAdd(st + col + q, stat_val(s0[q] + s1[q], srep));
-        atomicAdd(st + K + col + q, stat_val(s0[4 + q] + s1[4 + q], srep));
+        atomicAdd(st + col + q, stat_val(s0[q] + s1[q], blockIdx.x));
+        atomicAdd(st + K + col + q, stat_val(s0[4 + q] + s1[4 + q], blockIdx.x));
       }
     }
   }
@@ -665,19 +606,6 @@ static bool launch_stages(const Cfg& c, int in, const Args& a, int nl, int items
   return false;
 }
 static std::map<std::tuple<int, int, int, int>, Cfg> g_tr_tuned;  // (M, K, C, H)
-// split-K combined in the launch (ddp_conv_tr_inlaunch_set). Off: measured in the captured
-// VGG-11 step against slabs + finish launch, b32 0.3766 vs 0.3741 ms, b64 / b128 equal, b256
-// within noise (profiles/r6x_ab_tr_inlaunch.jsonl) — every split block waits for its
-// write-through slab stores before its ticket, and the reducer's serial sc1 reads of 3-4 slabs
-// cost as much as the finish launch they replace on these 64x64 tiles.
-static int g_tr_inlaunch = 0;
-static unsigned* tickets_ptr() {
-  static unsigned* p = [] {
-    void* q = nullptr;
-    return hipGetSymbolAddress(&q, HIP_SYMBOL(g_tickets)) == hipSuccess ? (unsigned*)q : nullptr;
-  }();
-  return p;
-}
 static int g_tr_mode = 1;  // 0 off, 1 table entries only, 2 also the heuristic (ddp_conv_tr_mode)
 static Cfg g_tr_force{0, 0, 0, 0};
 
@@ -702,9 +630,6 @@ using namespace ddp_amd;
 extern "C" int ddp_conv_fwd_finish(const ConvGeom* g, float* ws, int splits, const float* bias,
                                    void* z, float* stats, const BnFwdFuse* bn, int* bn_done,
                                    hipStream_t st);
-
-extern "C" int ddp_conv_fwd_finish_fuses_bn(const ConvGeom* g, const BnFwdFuse* bn);
-extern "C" void ddp_conv_tr_inlaunch_set(int on) { tr::g_tr_inlaunch = on ? 1 : 0; }
 
 extern "C" void ddp_conv_tr_set(int mode, int M, int K, int C, int H, int bm, int bn, int splits,
                                 int stages) {
@@ -816,20 +741,10 @@ extern "C" int ddp_conv_fwd_tr(const ConvGeom* g, const void* x, const void* wc,
     a.z_bytes = (int)(2 * M * C * (in->pool ? 4 : 1));
   }
   const int items = a.tiles_m * a.tiles_n * pl.splits;
-  // split-K combined inside the launch unless the finish would also run this block's BatchNorm
-  // forward (the small GEMMs' fused finish needs every row of a channel)
-  const size_t ws_bytes = (size_t)pl.splits * M * K * 4;
-  const bool inl = pl.splits > 1 && g_tr_inlaunch && a.tiles_m * a.tiles_n <= kTickets &&
-                   ws_bytes < (1ull << 31) && !(bn && ddp_conv_fwd_finish_fuses_bn(g, bn)) &&
-                   tickets_ptr() != nullptr;
-  if (inl) {
-    a.tickets = tickets_ptr();
-    a.ws_bytes = (int)ws_bytes;
-  }
   if (!launch_stages(c, in_mode, a, geo.nl, items, st)) return 0;
   int e = (int)hipGetLastError();
   if (e) return 2 + e;
-  if (pl.splits > 1 && !inl) {
+  if (pl.splits > 1) {
     e = ddp_conv_fwd_finish(g, ws, pl.splits, bias, z, stats, bn, bn_done, st);
     if (e) return 2 + e;
   }

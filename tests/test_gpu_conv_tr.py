@@ -35,13 +35,8 @@ def _force(nat, bm, bn, splits, stages=0):
     nat.conv_tr_set(3, 0, 0, 0, 0, bm, bn, splits, stages)
 
 
-@pytest.mark.parametrize("inl", [1, 0])
 @pytest.mark.parametrize("case", TR_CASES)
-def test_conv_tr_fwd_matches_reference(native_ext, case, inl):
-    """inl = 1: split-K combined inside the launch (sc1 slabs + per-tile tickets; the last split
-    block reduces), run three times back to back — each reducer resets its ticket, and a reducer
-    whose CU read the same slab lines in the previous launch must not see stale bytes: every run
-    gives the same z, bit for bit. inl = 0: slabs + the finish launch."""
+def test_conv_tr_fwd_matches_reference(native_ext, case):
     from ddp_amd.ops.common import ptr, stream_handle, workspace
     nat = native_ext
     N, C, H, K, BM, BN, splits, stages = case
@@ -52,22 +47,12 @@ def test_conv_tr_fwd_matches_reference(native_ext, case, inl):
     z = torch.full((N, H, H, K), float("nan"), device=DEV, dtype=torch.bfloat16)
     stats = torch.zeros(16 * 2 * K, device=DEV)
     _force(nat, BM, BN, splits, stages)
-    nat.conv_tr_inlaunch_set(inl)
-    runs = []
     try:
-        for rep in range(3):
-            z.fill_(float("nan"))
-            if rep:
-                ws.normal_()  # other values in the slab lines between launches
-            stats.zero_()
-            r = nat.conv_fwd_tr(g, ptr(xn), ptr(spec.wc), ptr(conv.bias), ptr(z), ptr(stats),
-                                ptr(ws), ws.numel(), s)
-            assert r == 1, "the forced tap-reuse configuration must be served"
-            runs.append(z.clone())
+        r = nat.conv_fwd_tr(g, ptr(xn), ptr(spec.wc), ptr(conv.bias), ptr(z), ptr(stats),
+                            ptr(ws), ws.numel(), s)
     finally:
         _force(nat, 0, 0, 0)
-        nat.conv_tr_inlaunch_set(0)
-    assert torch.equal(runs[0], runs[1]) and torch.equal(runs[0], runs[2])
+    assert r == 1, "the forced tap-reuse configuration must be served"
     z2 = torch.empty_like(z)
     stats2 = torch.zeros_like(stats)
     nat.conv_fwd(g, ptr(xn), ptr(spec.wc), ptr(conv.bias), ptr(z2), ptr(stats2), ptr(ws),
